@@ -1,0 +1,95 @@
+"""ctypes binding of libauctiongym_hip.so (the C-ABI declared in include/auctiongym.h).
+
+The library is the product path: there is no CPU fallback. If it is missing, or no GPU
+is visible when a context is created, the calls raise -- they never route to the oracle.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libauctiongym_hip.so")
+
+AG_OK, AG_ERR_INVALID, AG_ERR_UNSUPPORTED, AG_ERR_HIP, AG_ERR_STATE = 0, -1, -2, -3, -4
+FIRST_PRICE, SECOND_PRICE = 0, 1
+ALLOCATOR_ORACLE = 0
+BIDDER_TRUTHFUL = 0
+
+COUNTERS = ("net", "gross", "allocation_regret", "estimation_regret", "overbid_regret",
+            "underbid_regret", "ctr_sqerr", "ctr_bias_sum", "best_ev_sum", "n_logs", "n_won",
+            "paid")
+NUM_COUNTERS = len(COUNTERS)
+FX_FRAC_BITS, FX_LIMB_BITS, FX_LIMBS = 36, 42, 3
+
+# Every symbol include/auctiongym.h declares (tests check the .so exports all of them).
+EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_load_catalog", "ag_allocate",
+           "ag_simulate", "ag_generate", "ag_counters_to_double", "ag_sigmoid", "ag_exp",
+           "ag_last_error", "ag_abi_version")
+
+
+class AgShape(ctypes.Structure):
+    _fields_ = [("num_agents", ctypes.c_int32), ("num_participants", ctypes.c_int32),
+                ("num_items", ctypes.c_int32), ("embedding_size", ctypes.c_int32),
+                ("obs_embedding_size", ctypes.c_int32), ("mechanism", ctypes.c_int32),
+                ("num_slots", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("embedding_var", ctypes.c_double)]
+
+
+class AgBatchIn(ctypes.Structure):
+    _fields_ = [("ctx", ctypes.c_void_p), ("part", ctypes.c_void_p), ("u", ctypes.c_void_p)]
+
+
+class AgBatchOut(ctypes.Structure):
+    _fields_ = [("winner", ctypes.c_void_p), ("price", ctypes.c_void_p),
+                ("second_price", ctypes.c_void_p), ("outcome", ctypes.c_void_p),
+                ("item", ctypes.c_void_p), ("bid", ctypes.c_void_p), ("est_ctr", ctypes.c_void_p),
+                ("true_ctr", ctypes.c_void_p), ("best_ev", ctypes.c_void_p)]
+
+
+class AgError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load the HIP library (raises if it was not built: run `make -C auction-gym_amd`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise AgError(f"{LIB_PATH} is missing: build it with `make -C auction-gym_amd` "
+                      "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
+    sig = {
+        "ag_create": (ctypes.c_int, [i32, ctypes.POINTER(AgShape), ctypes.POINTER(vp)]),
+        "ag_destroy": (ctypes.c_int, [vp]),
+        "ag_set_agent_kinds": (ctypes.c_int, [vp, vp, vp]),
+        "ag_load_catalog": (ctypes.c_int, [vp, vp, vp]),
+        "ag_allocate": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, vp]),
+        "ag_simulate": (ctypes.c_int, [vp, i64, ctypes.POINTER(AgBatchIn),
+                                       ctypes.POINTER(AgBatchOut), vp, vp]),
+        "ag_generate": (ctypes.c_int, [vp, u64, u64, i64, vp, vp, vp, vp]),
+        "ag_counters_to_double": (ctypes.c_int, [vp, i64, vp]),
+        "ag_sigmoid": (ctypes.c_int, [vp, vp, i64, vp]),
+        "ag_exp": (ctypes.c_int, [vp, vp, i64, vp]),
+        "ag_last_error": (ctypes.c_char_p, []),
+        "ag_abi_version": (i32, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc, what=""):
+    if rc != AG_OK:
+        msg = load().ag_last_error().decode(errors="replace")
+        if rc == AG_ERR_INVALID:
+            raise ValueError(msg)
+        if rc == AG_ERR_UNSUPPORTED:
+            raise NotImplementedError(msg)
+        raise AgError(f"{what}: {msg} (status {rc})")

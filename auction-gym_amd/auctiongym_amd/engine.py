@@ -1,0 +1,156 @@
+"""Device-resident batched engine: one ag_ctx per auction population, SoA buffers in HBM.
+
+This is the MI355X-native core the reference-shaped classes (Auction, Agent, ...) sit on.
+Torch is used only for device memory and the current HIP stream; all arithmetic runs in
+the HIP kernels of libauctiongym_hip.so (auction-gym_amd/csrc/ag_kernels.hip).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import AgBatchIn, AgBatchOut, AgShape, check
+
+COUNTERS = _lib.COUNTERS
+NUM_COUNTERS = _lib.NUM_COUNTERS
+FX_LIMBS = _lib.FX_LIMBS
+
+_OUT_FIELDS = ("winner", "price", "second_price", "outcome", "item", "bid", "est_ctr",
+               "true_ctr", "best_ev")
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError("auctiongym_amd needs a ROCm GPU (MI355X); none is visible. "
+                           "There is no CPU fallback.")
+
+
+class AuctionEngine:
+    """Batched Auction.simulate_opportunity for N agents, P participants, K items, E dims."""
+
+    def __init__(self, num_agents, num_participants, num_items, embedding_size,
+                 obs_embedding_size, mechanism, embedding_var=1.0, device=None):
+        require_gpu()
+        self.L = _lib.load()
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self.N, self.P, self.K = int(num_agents), int(num_participants), int(num_items)
+        self.E, self.OE = int(embedding_size), int(obs_embedding_size)
+        self.D = self.E + 1
+        self.mechanism = int(mechanism)
+        self.embedding_var = float(embedding_var)
+        shape = AgShape(self.N, self.P, self.K, self.E, self.OE, self.mechanism, 1, 0,
+                        self.embedding_var)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(self.L.ag_create(self.device.index, ctypes.byref(shape), ctypes.byref(h)),
+                  "ag_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.L.ag_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- setup
+    def set_agent_kinds(self, allocator_kinds, bidder_kinds):
+        a = np.ascontiguousarray(allocator_kinds, np.int32)
+        b = np.ascontiguousarray(bidder_kinds, np.int32)
+        assert a.shape == (self.N,) and b.shape == (self.N,)
+        check(self.L.ag_set_agent_kinds(self._h, a.ctypes.data, b.ctypes.data), "ag_set_agent_kinds")
+
+    def load_catalog(self, items, values):
+        items = np.ascontiguousarray(items, np.float64)
+        values = np.ascontiguousarray(values, np.float64)
+        if items.shape != (self.N, self.K, self.D) or values.shape != (self.N, self.K):
+            raise ValueError(f"catalogue shapes {items.shape}/{values.shape} != "
+                             f"({self.N},{self.K},{self.D})/({self.N},{self.K})")
+        check(self.L.ag_load_catalog(self._h, items.ctypes.data, values.ctypes.data),
+              "ag_load_catalog")
+
+    # ---------------------------------------------------------------- buffers
+    def alloc_inputs(self, B):
+        d = self.device
+        return {"ctx": torch.empty((self.E, B), dtype=torch.float64, device=d),
+                "part": torch.empty((self.P, B), dtype=torch.int32, device=d),
+                "u": torch.empty((B,), dtype=torch.float64, device=d)}
+
+    def alloc_outputs(self, B, fields=_OUT_FIELDS):
+        d, P = self.device, self.P
+        spec = {"winner": ((B,), torch.int32), "price": ((B,), torch.float64),
+                "second_price": ((B,), torch.float64), "outcome": ((B,), torch.uint8),
+                "item": ((P, B), torch.int32), "bid": ((P, B), torch.float64),
+                "est_ctr": ((P, B), torch.float64), "true_ctr": ((P, B), torch.float64),
+                "best_ev": ((P, B), torch.float64)}
+        return {k: torch.empty(spec[k][0], dtype=spec[k][1], device=d) for k in fields}
+
+    def new_counters(self):
+        return torch.zeros((self.N, NUM_COUNTERS, FX_LIMBS), dtype=torch.int64, device=self.device)
+
+    # ---------------------------------------------------------------- hot calls
+    def simulate(self, inputs, outputs, counters=None):
+        B = inputs["u"].shape[0]
+        for k, t in inputs.items():
+            if not t.is_contiguous() or t.device != self.device:
+                raise ValueError(f"input {k} must be a contiguous tensor on {self.device}")
+        if inputs["ctx"].shape != (self.E, B) or inputs["part"].shape != (self.P, B):
+            raise ValueError("inputs must be SoA: ctx [E][B], part [P][B], u [B]")
+        bi = AgBatchIn(_ptr(inputs["ctx"]).value, _ptr(inputs["part"]).value, _ptr(inputs["u"]).value)
+        bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
+        check(self.L.ag_simulate(self._h, B, ctypes.byref(bi), ctypes.byref(bo),
+                                 _ptr(counters), _stream()), "ag_simulate")
+
+    def generate(self, seed, first_auction, inputs):
+        B = inputs["u"].shape[0]
+        check(self.L.ag_generate(self._h, int(seed), int(first_auction), B, _ptr(inputs["ctx"]),
+                                 _ptr(inputs["part"]), _ptr(inputs["u"]), _stream()), "ag_generate")
+
+    def allocate(self, bids):
+        """Batched allocate: bids [P][B] (device, float64) -> winner, price, second_price."""
+        if bids.dim() != 2 or bids.shape[0] != self.P or bids.dtype != torch.float64:
+            raise ValueError("bids must be a float64 [P][B] tensor")
+        bids = bids.contiguous()
+        B = bids.shape[1]
+        w = torch.empty(B, dtype=torch.int32, device=self.device)
+        p = torch.empty(B, dtype=torch.float64, device=self.device)
+        s = torch.empty(B, dtype=torch.float64, device=self.device)
+        check(self.L.ag_allocate(self._h, _ptr(bids), B, _ptr(w), _ptr(p), _ptr(s), _stream()),
+              "ag_allocate")
+        return w, p, s
+
+    # ---------------------------------------------------------------- counters
+    @staticmethod
+    def counters_to_numpy(counters):
+        """Exact fixed-point limbs [N][C][3] (tensor or array) -> float64 [N][C]."""
+        fx = counters.detach().cpu().numpy() if torch.is_tensor(counters) else np.asarray(counters)
+        fx = np.ascontiguousarray(fx, np.int64)
+        n = fx.size // FX_LIMBS
+        out = np.empty(n, np.float64)
+        check(_lib.load().ag_counters_to_double(fx.ctypes.data, n, out.ctypes.data),
+              "ag_counters_to_double")
+        return out.reshape(fx.shape[:-1])
+
+
+def device_exp(x, sigmoid=False):
+    """The kernels' exp (or sigmoid) on a float64 device tensor (known-answer hook)."""
+    require_gpu()
+    L = _lib.load()
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    f = L.ag_sigmoid if sigmoid else L.ag_exp
+    check(f(_ptr(x), _ptr(y), x.numel(), _stream()), "ag_exp")
+    return y

@@ -1,0 +1,103 @@
+// ag_exp.h -- FP64 exp with bit-identical results to the glibc 2.35 x86-64 FMA build of
+// exp(), and the reference sigmoid built on it.
+//
+// Why: the reference's bids are `value * sigmoid(items @ ctx)` (src/Models.py:10-12,
+// src/Bidder.py:34-35) and second-price charges ARE bids, so bit-exact charges need an
+// exp whose every result equals the one the reference used. The pinned numba 0.55.1
+// (requirements.txt:7) lowers np.exp in the jitted sigmoid to the libm call, i.e. glibc.
+//
+// Algorithm (glibc's table-driven exp; restated, not copied): x = k*ln2/128 + r,
+// exp(x) = 2^(k/128) * exp(r), 2^(k/128) from a 128-entry table (ag_exp_table.h, built by
+// tools/gen_exp_table.py), exp(r) - 1 by a degree-5 polynomial, with the FMAs placed
+// where the FMA build of glibc contracts them. The host test
+// (tests/test_exp_restatement.py) compares this exact source, compiled for the CPU,
+// against the host libm on 4e7 inputs over the full double range; the GPU test compares
+// the device build against the same libm.
+//
+// Compile with -ffp-contract=off: every FMA below is explicit.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#if defined(__HIPCC__)
+#define AG_HD __host__ __device__ __forceinline__
+#else
+#define AG_HD static inline
+#include <math.h>
+#endif
+
+namespace agexp {
+
+constexpr double kInvLn2N = 0x1.71547652b82fep0 * 128.0;
+constexpr double kNegLn2HiN = -0x1.62e42fefa0000p-8;
+constexpr double kNegLn2LoN = -0x1.cf79abc9e3b3ap-47;
+constexpr double kShift = 0x1.8p52;
+constexpr double kC2 = 0x1.ffffffffffdbdp-2;
+constexpr double kC3 = 0x1.555555555543cp-3;
+constexpr double kC4 = 0x1.55555cf172b91p-5;
+constexpr double kC5 = 0x1.1111167a4d017p-7;
+
+AG_HD uint64_t asu64(double x) {
+  uint64_t u;
+  memcpy(&u, &x, 8);
+  return u;
+}
+AG_HD double asf64(uint64_t u) {
+  double x;
+  memcpy(&x, &u, 8);
+  return x;
+}
+
+// |x| >= 512 (or the rare k range where the table scale would over/underflow).
+AG_HD double exp_special(double tmp, uint64_t sbits, uint64_t ki) {
+  if ((ki & 0x80000000ull) == 0) {
+    sbits -= 1009ull << 52;  // k > 0: scale down, multiply back
+    double scale = asf64(sbits);
+    return 0x1p1009 * fma(scale, tmp, scale);
+  }
+  sbits += 1022ull << 52;  // k < 0: careful rounding into the subnormal range
+  double scale = asf64(sbits);
+  double y = scale + scale * tmp;
+  if (y < 1.0) {
+    double lo = (scale - y) + scale * tmp;  // not contracted in the glibc build
+    double hi = 1.0 + y;
+    lo = 1.0 - hi + y + lo;
+    y = (hi + lo) - 1.0;
+    if (y == 0.0) y = 0.0;
+  }
+  return 0x1p-1022 * y;
+}
+
+// `tab` points at the 256-entry table (LDS copy on the device, ag_exp_tab on the host).
+AG_HD double exp(double x, const uint64_t *tab) {
+  uint64_t ux = asu64(x);
+  uint32_t abstop = (uint32_t)(ux >> 52) & 0x7ff;
+  if (abstop - 0x3c9u >= 0x408u - 0x3c9u) {           // |x| < 2^-54 or |x| >= 512
+    if (abstop - 0x3c9u >= 0x80000000u) return 1.0 + x; // tiny
+    if (abstop >= 0x409u) {                            // |x| >= 1024, inf, nan
+      if (ux == 0xfff0000000000000ull) return 0.0;
+      if (abstop >= 0x7ffu) return 1.0 + x;
+      return (ux >> 63) ? 0.0 : asf64(0x7ff0000000000000ull);
+    }
+    abstop = 0;  // large |x|: exp_special below
+  }
+  double z = kInvLn2N * x;
+  double kd = z + kShift;
+  uint64_t ki = asu64(kd);
+  kd -= kShift;
+  double r = fma(kd, kNegLn2LoN, fma(kd, kNegLn2HiN, x));
+  uint64_t idx = 2 * (ki & 127);
+  uint64_t top = ki << 45;
+  double tail = asf64(tab[idx]);
+  uint64_t sbits = tab[idx + 1] + top;
+  double r2 = r * r;
+  double tmp = fma(r2 * r2, fma(r, kC5, kC4), fma(r2, fma(r, kC3, kC2), tail + r));
+  if (abstop == 0) return exp_special(tmp, sbits, ki);
+  double scale = asf64(sbits);
+  return fma(scale, tmp, scale);
+}
+
+// src/Models.py:10-12  sigmoid(x) = 1.0 / (1.0 + np.exp(-x))  (IEEE division).
+AG_HD double sigmoid(double z, const uint64_t *tab) { return 1.0 / (1.0 + exp(-z, tab)); }
+
+}  // namespace agexp

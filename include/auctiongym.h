@@ -1,0 +1,165 @@
+/*
+ * auctiongym.h -- C-ABI of the MI355X-native AuctionGym hot path (libauctiongym_hip.so).
+ *
+ * The drop-in boundary for
+ *     Auction.simulate_opportunity -> Agent.bid -> {First,Second}Price.allocate -> Agent.charge
+ * of the reference (soopark0221/auction-gym, src/). The reference is pure Python and has
+ * no FFI; each entry point below names the reference interface it replaces, and
+ * INTEGRATION.md shows the ctypes stub a maintainer would add on the reference side.
+ *
+ * Conventions
+ *  - Every call returns AG_OK (0) or a negative ag_status; ag_last_error() describes it.
+ *  - Plain pointers and sizes only. "dev" pointers are device (HBM) pointers on the ctx's
+ *    device (hipMalloc or a torch tensor's data_ptr); "host" pointers are host memory.
+ *  - Batched arrays are structure-of-arrays: a per-(auction, slot) array is [P][B]
+ *    (slot-major, auction index fastest) so lane i of a wave touches auction i: coalesced.
+ *  - Hot calls (ag_allocate, ag_simulate, ag_generate) allocate nothing, never
+ *    synchronise and are stream-ordered on `stream` (a hipStream_t, NULL = default):
+ *    they may be captured into a hipGraph.
+ *  - One ag_ctx per process and device; a ctx is not thread-safe.
+ */
+#ifndef AUCTIONGYM_H
+#define AUCTIONGYM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AG_ABI_VERSION 1
+
+typedef enum ag_status {
+  AG_OK = 0,
+  AG_ERR_INVALID = -1,     /* bad argument (reference: ValueError, e.g. rng.choice with P > N) */
+  AG_ERR_UNSUPPORTED = -2, /* shape / plugin kind this build does not implement */
+  AG_ERR_HIP = -3,         /* HIP runtime error */
+  AG_ERR_STATE = -4        /* call order (e.g. simulate before ag_load_catalog) */
+} ag_status;
+
+/* Allocation mechanisms: src/AuctionAllocation.py:11-23 (FirstPrice), :26-34 (SecondPrice). */
+typedef enum ag_mechanism { AG_FIRST_PRICE = 0, AG_SECOND_PRICE = 1 } ag_mechanism;
+
+/* Allocator plugins (src/BidderAllocation.py). */
+typedef enum ag_allocator_kind {
+  AG_ALLOCATOR_ORACLE = 0 /* OracleAllocator, src/BidderAllocation.py:71-82 */
+} ag_allocator_kind;
+
+/* Bidder plugins (src/Bidder.py). */
+typedef enum ag_bidder_kind {
+  AG_BIDDER_TRUTHFUL = 0 /* TruthfulBidder, src/Bidder.py:28-35 */
+} ag_bidder_kind;
+
+/* Per-agent counters produced by ag_simulate: the quantities src/main.py:131-147 reads
+ * from Agent (src/Agent.py:70-118) after each iteration, as sums over the agent's logs. */
+typedef enum ag_counter {
+  AG_C_NET = 0,          /* Agent.net_utility        += value*outcome - price (won)   */
+  AG_C_GROSS,            /* Agent.gross_utility      += value*outcome (won)           */
+  AG_C_ALLOC_REGRET,     /* get_allocation_regret:  best_ev - true_ctr*value          */
+  AG_C_EST_REGRET,       /* get_estimation_regret:  est_ctr*value - true_ctr*value    */
+  AG_C_OVERBID,          /* get_overbid_regret:     (price - second_price)*won        */
+  AG_C_UNDERBID,         /* get_underbid_regret:    (price-bid)*!won*(price<true*val) */
+  AG_C_CTR_SQERR,        /* get_CTR_RMSE numerator: (true_ctr - est_ctr)^2            */
+  AG_C_CTR_BIAS,         /* get_CTR_bias numerator: est_ctr/true_ctr over won logs    */
+  AG_C_BEST_EV,          /* mean best expected value numerator (src/main.py:147)      */
+  AG_C_N_LOGS,           /* number of log records (participations)                   */
+  AG_C_N_WON,            /* number of won log records                                 */
+  AG_C_PAID,             /* sum of prices charged (revenue = sum over agents)         */
+  AG_NUM_COUNTERS
+} ag_counter;
+
+/* Counters are accumulated EXACTLY as fixed-point sums: every per-record term is rounded
+ * to a multiple of 2^-AG_FX_FRAC_BITS and the sum is held in AG_FX_LIMBS int64 limbs of
+ * AG_FX_LIMB_BITS bits (value = sum_j limb_j * 2^(j*AG_FX_LIMB_BITS - AG_FX_FRAC_BITS)),
+ * so results are independent of grid size, block order, batch split and GPU count.
+ * Limb arrays can be summed across GPUs with an int64 all-reduce and then normalised. */
+#define AG_FX_FRAC_BITS 36
+#define AG_FX_LIMB_BITS 42
+#define AG_FX_LIMBS 3
+
+typedef struct ag_shape {
+  int32_t num_agents;         /* N: len(auction.agents)                                  */
+  int32_t num_participants;   /* P: num_participants_per_round (src/Auction.py:42)       */
+  int32_t num_items;          /* K: num_items per agent (one value for all agents)       */
+  int32_t embedding_size;     /* E: true context dims; D = E + 1 with the intercept      */
+  int32_t obs_embedding_size; /* OE: observable dims (src/Auction.py:36)                 */
+  int32_t mechanism;          /* ag_mechanism                                            */
+  int32_t num_slots;          /* must be 1 (max_slots is hard-coded, src/main.py:37)     */
+  int32_t reserved;
+  double embedding_var;       /* context ~ N(0, embedding_var) (src/Auction.py:33)       */
+} ag_shape;
+
+typedef struct ag_ctx ag_ctx;
+
+/* Replay inputs of B auctions (dev). The reference draws these from its numpy Generator
+ * in the order src/Auction.py:33 (normal), :42 (choice), :65 (binomial's next_double). */
+typedef struct ag_batch_in {
+  const double *ctx;   /* [E][B] true context without the intercept                      */
+  const int32_t *part; /* [P][B] participating agent index per slot, P distinct of N     */
+  const double *u;     /* [B]    uniform in [0,1) consumed by binomial(1, CTR[winner])   */
+} ag_batch_in;
+
+/* Outputs of B auctions (dev). Any pointer may be NULL to skip that array. */
+typedef struct ag_batch_out {
+  int32_t *winner;       /* [B] winning slot (argsort(-bids)[0]; ties -> lowest slot)    */
+  double *price;         /* [B] price charged (NaN when P == 1: nobody charged)          */
+  double *second_price;  /* [B] second highest bid (NaN when P == 1)                     */
+  uint8_t *outcome;      /* [B] click of the winner, binomial(1, true CTR)               */
+  int32_t *item;         /* [P][B] item chosen by the participant (Agent.select_item)    */
+  double *bid;           /* [P][B] bid submitted                                        */
+  double *est_ctr;       /* [P][B] estimated CTR of the chosen item                     */
+  double *true_ctr;      /* [P][B] true CTR of the chosen item (src/Auction.py:52-53)    */
+  double *best_ev;       /* [P][B] max_k true_CTR_k * value_k                           */
+} ag_batch_out;
+
+/* Create a context on `device` for one auction population (src/main.py:98-109
+ * instantiate_auction). Validates the shape; allocates device workspace once. */
+int ag_create(int32_t device, const ag_shape *shape, ag_ctx **out);
+int ag_destroy(ag_ctx *ctx);
+
+/* Per-agent plugin kinds, host [N] (src/main.py:77-95 instantiate_agents: the eval of
+ * allocator/bidder class names). Default: all OracleAllocator + TruthfulBidder. */
+int ag_set_agent_kinds(ag_ctx *ctx, const int32_t *allocator_kind, const int32_t *bidder_kind);
+
+/* Item catalogue, host: item_emb [N][K][E+1] (embeddings with the intercept column,
+ * src/main.py:60-72) and item_val [N][K]; replaces OracleAllocator.update_item_embeddings
+ * (src/BidderAllocation.py:78-79) and Auction.agent2items / agents2item_values. */
+int ag_load_catalog(ag_ctx *ctx, const double *item_emb, const double *item_val);
+
+/* Batched AllocationMechanism.allocate(bids, num_slots=1) (src/AuctionAllocation.py:7-8,
+ * 19-22, 32-34) over B auctions: bids dev [P][B] -> winner/price/second_price dev [B].
+ * FirstPrice: price = highest bid; SecondPrice: price = second highest. P == 1: FirstPrice
+ * price = the bid, SecondPrice price = NaN, second_price = NaN (empty arrays). */
+int ag_allocate(ag_ctx *ctx, const double *bids, int64_t B, int32_t *winner, double *price,
+                double *second_price, void *stream);
+
+/* B rounds of Auction.simulate_opportunity (src/Auction.py:28-74) in replay mode.
+ * counters_fx: dev int64 [N][AG_NUM_COUNTERS][AG_FX_LIMBS], ACCUMULATED (zero it at the
+ * start of an iteration, like Agent.clear_utility); may be NULL. */
+int ag_simulate(ag_ctx *ctx, int64_t B, const ag_batch_in *in, ag_batch_out *out,
+                int64_t *counters_fx, void *stream);
+
+/* Synthetic replay inputs for auctions [first_auction, first_auction + B) (dev, SoA):
+ * Philox4x32-10 keyed by seed and the GLOBAL auction index, so a sharded batch is
+ * bit-identical to the unsharded one. ctx ~ N(0, embedding_var) (Box-Muller), part =
+ * P distinct of N (Floyd), u ~ U[0,1) with 53 bits. */
+int ag_generate(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B, double *ctx_out,
+                int32_t *part_out, double *u_out, void *stream);
+
+/* Exact counters (host int64 [n][AG_FX_LIMBS], e.g. copied back or all-reduced)
+ * -> doubles (host [n]), correctly rounded from the exact fixed-point sum. */
+int ag_counters_to_double(const int64_t *counters_fx, int64_t n, double *out);
+
+/* Known-answer hooks for the numerics the kernels restate (dev arrays of n):
+ * src/Models.py:10-12 sigmoid with glibc-2.35-identical exp, and that exp alone. */
+int ag_sigmoid(const double *z, double *out, int64_t n, void *stream);
+int ag_exp(const double *x, double *out, int64_t n, void *stream);
+
+/* Thread-local description of the last error. */
+const char *ag_last_error(void);
+int32_t ag_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AUCTIONGYM_H */

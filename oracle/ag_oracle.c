@@ -1,0 +1,315 @@
+/*
+ * ag_oracle.c -- TEST INFRASTRUCTURE ONLY: CPU restatement of the reference hot path.
+ *
+ * This is the checker the HIP kernels are compared against (tests/, smoke(), and the
+ * cpu_baseline leg of bench.py). It is pinned against the golden vectors captured
+ * from the reference itself (tests/golden/, tests/test_oracle_golden.py).
+ *
+ * Compiled with -ffp-contract=off: every fused multiply-add below is an explicit fma()
+ * because the reference's BLAS fuses exactly there (SURVEY §8 a5').
+ */
+#include "ag_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* src/Models.py:10-12: 1.0 / (1.0 + np.exp(-x)); exp is libm's (pinned numba 0.55.1
+ * lowers np.exp to the libm call; requirements.txt:7). */
+double ora_sigmoid(double z) { return 1.0 / (1.0 + exp(-z)); }
+
+/* src/BidderAllocation.py:81-82 `self.item_embeddings @ context` and
+ * src/Auction.py:52 `true_context @ items.T`: numpy -> OpenBLAS dgemv_t. Its kernel
+ * takes the rows in blocks of four, one FMA accumulator per lane, then reduces the
+ * lanes as (l0 + l2) + (l1 + l3); the 1-3 leftover rows are added by scalar C code
+ * that the compiler contracted into FMAs. Verified bit-exact against numpy here for
+ * D <= 7 at any K >= 2 and for every D when K % 4 == 0 (the shipped D = 6, K = 12
+ * included); other shapes: parity unpinned (different OpenBLAS column kernels). */
+double ora_dot(const double *a, const double *x, int32_t D) {
+  int32_t m3 = D & 3, m1 = D - m3;
+  double y = 0.0;
+  if (m1 > 0) {
+    double l0 = 0.0, l1 = 0.0, l2 = 0.0, l3 = 0.0;
+    for (int32_t i = 0; i < m1; i += 4) {
+      l0 = fma(a[i + 0], x[i + 0], l0);
+      l1 = fma(a[i + 1], x[i + 1], l1);
+      l2 = fma(a[i + 2], x[i + 2], l2);
+      l3 = fma(a[i + 3], x[i + 3], l3);
+    }
+    y = (l0 + l2) + (l1 + l3);
+  }
+  const double *at = a + m1, *xt = x + m1;
+  if (m3 == 1)
+    y = fma(at[0], xt[0], y);
+  else if (m3 == 2)
+    y = y + fma(at[0], xt[0], at[1] * xt[1]);
+  else if (m3 == 3)
+    y = y + fma(at[2], xt[2], fma(at[0], xt[0], at[1] * xt[1]));
+  return y;
+}
+
+/* src/Auction.py:65 rng.binomial(1, p) with numpy's inversion sampler for n = 1:
+ * p <= 0.5: X = [U > exp(log(1 - p))];  p > 0.5: X = 1 - [U > exp(log(p))]
+ * (numpy random_binomial / random_binomial_inversion; p == 0 draws nothing). */
+int32_t ora_bernoulli(double p, double u) {
+  if (p == 0.0) return 0;
+  if (p <= 0.5) {
+    double qn = exp(log(1.0 - p));
+    return u > qn ? 1 : 0;
+  }
+  double q = 1.0 - p;
+  double qn = exp(log(1.0 - q));
+  return u > qn ? 0 : 1;
+}
+
+/* src/AuctionAllocation.py:19-23 (FirstPrice) and :32-34 (SecondPrice) for num_slots = 1:
+ * winner = argsort(-bids)[0]; sorted = -sort(-bids); FP: price = sorted[0],
+ * second = sorted[1]; SP: price = second = sorted[1]. Ties: lowest slot (numpy <= 1.22
+ * insertion sort; SURVEY §8 a13'). Absent prices (P == 1) are NaN. */
+static void top2(const double *b, int32_t P, int32_t *w, double *v1, double *v2) {
+  int32_t wi = 0;
+  double m1 = b[0], m2 = -INFINITY;
+  for (int32_t s = 1; s < P; ++s) {
+    double x = b[s];
+    if (x > m1) {
+      m2 = m1;
+      m1 = x;
+      wi = s;
+    } else if (x > m2) {
+      m2 = x;
+    }
+  }
+  *w = wi;
+  *v1 = m1;
+  *v2 = m2;
+}
+
+void ora_allocate(int32_t mech, const double *bids, int64_t B, int32_t P, int32_t *winner,
+                  double *price, double *second_price) {
+  for (int64_t r = 0; r < B; ++r) {
+    int32_t w;
+    double m1, m2;
+    top2(bids + r * P, P, &w, &m1, &m2);
+    winner[r] = w;
+    if (P < 2) {
+      price[r] = (mech == ORA_FIRST_PRICE) ? m1 : NAN;
+      second_price[r] = NAN;
+    } else {
+      price[r] = (mech == ORA_FIRST_PRICE) ? m1 : m2;
+      second_price[r] = m2;
+    }
+  }
+}
+
+/* Per-record term -> fixed point: round(x * 2^36) to nearest-even (include/auctiongym.h
+ * AG_FX_*); terms with |x| >= 2^26 (or non-finite) are dropped, as on the device. */
+int64_t ora_to_fx(double x) {
+  if (!(fabs(x) < 0x1p26)) return 0;
+  return (int64_t)nearbyint(x * 0x1p36);
+}
+
+static void add_limbs(int64_t *L, __int128 v) {
+  __int128 t = ((__int128)L[2] << 84) + ((__int128)L[1] << 42) + (__int128)L[0] + v;
+  const int64_t mask = ((int64_t)1 << 42) - 1;
+  L[0] = (int64_t)(t & mask);
+  t >>= 42;
+  L[1] = (int64_t)(t & mask);
+  t >>= 42;
+  L[2] = (int64_t)t;
+}
+
+/* Agent.select_item (src/Agent.py:29-42) for an OracleAllocator agent: CTR for every
+ * item, first argmax of CTR * value; the true CTR (src/Auction.py:52) is the same bits
+ * because Oracle agents see the true context. Returns best item; *best_ev = max. */
+static int32_t oracle_select(const double *items, const double *vals, int32_t K, int32_t D,
+                             const double *x, double *ctr_best, double *best_ev) {
+  int32_t best = 0;
+  double best_s = 0.0, best_c = 0.0;
+  for (int32_t k = 0; k < K; ++k) {
+    double c = ora_sigmoid(ora_dot(items + (int64_t)k * D, x, D));
+    double s = c * vals[k];
+    if (k == 0 || s > best_s) {
+      best = k;
+      best_s = s;
+      best_c = c;
+    }
+  }
+  *ctr_best = best_c;
+  *best_ev = best_s;
+  return best;
+}
+
+static void simulate_range(const ora_shape *sh, const double *items, const double *values,
+                           int64_t r0, int64_t r1, const double *ctx, const int32_t *part,
+                           const double *u, int32_t *winner, double *price, double *second_price,
+                           uint8_t *outcome, int32_t *item, double *value, double *bid,
+                           double *est_ctr, double *true_ctr, double *best_ev, double *cnt,
+                           __int128 *fx) {
+  const int32_t N = sh->N, P = sh->P, K = sh->K, E = sh->E, D = E + 1;
+  double x[64];
+  double bids[256];
+  for (int64_t r = r0; r < r1; ++r) {
+    /* src/Auction.py:33 true context = [draws, 1.0] */
+    for (int32_t e = 0; e < E; ++e) x[e] = ctx[r * E + e];
+    x[E] = 1.0;
+    /* src/Auction.py:44-54 per participant, in slot order */
+    for (int32_t s = 0; s < P; ++s) {
+      int32_t a = part[r * P + s];
+      double c, bev;
+      int32_t it = oracle_select(items + (int64_t)a * K * D, values + (int64_t)a * K, K, D, x,
+                                 &c, &bev);
+      double v = values[(int64_t)a * K + it];
+      double b = v * c; /* TruthfulBidder.bid, src/Bidder.py:34-35 */
+      int64_t o = r * P + s;
+      item[o] = it;
+      value[o] = v;
+      bid[o] = b;
+      est_ctr[o] = c;
+      true_ctr[o] = c;
+      best_ev[o] = bev;
+      bids[s] = b;
+    }
+    int32_t w;
+    double m1, m2;
+    top2(bids, P, &w, &m1, &m2);
+    double pr, sp;
+    int charged = P >= 2; /* P == 1: empty price arrays -> nobody charged (Auction.py:68) */
+    if (sh->mech == ORA_FIRST_PRICE) {
+      pr = m1;
+      sp = m2;
+    } else {
+      pr = m2;
+      sp = m2;
+    }
+    winner[r] = w;
+    price[r] = charged ? pr : NAN;
+    second_price[r] = charged ? sp : NAN;
+    int32_t oc = ora_bernoulli(true_ctr[r * P + w], u[r]);
+    outcome[r] = (uint8_t)oc;
+    /* Agent.charge / set_price (src/Agent.py:70-77) and the metric getters
+     * (src/Agent.py:96-118) per log record. */
+    for (int32_t s = 0; s < P; ++s) {
+      int64_t o = r * P + s;
+      int32_t a = part[o];
+      int won = charged && s == w;
+      double lp = charged ? pr : 0.0;  /* logged price */
+      double lsp = won ? sp : 0.0;     /* logged second price */
+      double tv = true_ctr[o] * value[o];
+      double t[ORA_NUM_COUNTERS];
+      memset(t, 0, sizeof t);
+      if (won) {
+        double last_value = value[o] * (double)oc;
+        t[ORA_C_NET] = last_value - pr;
+        t[ORA_C_GROSS] = last_value;
+        t[ORA_C_N_WON] = 1.0;
+        t[ORA_C_PAID] = pr;
+        t[ORA_C_CTR_BIAS] = est_ctr[o] / true_ctr[o];
+      }
+      t[ORA_C_ALLOC_REGRET] = best_ev[o] - tv;
+      t[ORA_C_EST_REGRET] = est_ctr[o] * value[o] - tv;
+      t[ORA_C_OVERBID] = (lp - lsp) * (double)won;
+      t[ORA_C_UNDERBID] = (lp - bid[o]) * (double)(!won) * (double)(lp < tv);
+      double d = true_ctr[o] - est_ctr[o];
+      t[ORA_C_CTR_SQERR] = d * d;
+      t[ORA_C_BEST_EV] = best_ev[o];
+      t[ORA_C_N_LOGS] = 1.0;
+      double *C = cnt + (int64_t)a * ORA_NUM_COUNTERS;
+      for (int c = 0; c < ORA_NUM_COUNTERS; ++c) C[c] += t[c];
+      if (fx) {
+        __int128 *F = fx + (int64_t)a * ORA_NUM_COUNTERS;
+        for (int c = 0; c < ORA_NUM_COUNTERS; ++c) F[c] += ora_to_fx(t[c]);
+      }
+    }
+  }
+  (void)N;
+}
+
+void ora_simulate(const ora_shape *s, const double *items, const double *values, int64_t B,
+                  const double *ctx, const int32_t *part, const double *u, int32_t *winner,
+                  double *price, double *second_price, uint8_t *outcome, int32_t *item,
+                  double *value, double *bid, double *est_ctr, double *true_ctr, double *best_ev,
+                  double *counters, int64_t *counters_fx, int32_t nthreads) {
+  const int64_t NC = (int64_t)s->N * ORA_NUM_COUNTERS;
+  if (nthreads < 1) nthreads = 1;
+  double *part_cnt = (double *)calloc((size_t)nthreads * NC, sizeof(double));
+  __int128 *part_fx = (__int128 *)calloc((size_t)nthreads * NC, sizeof(__int128));
+#pragma omp parallel num_threads(nthreads)
+  {
+#ifdef _OPENMP
+    int t = omp_get_thread_num(), nt = omp_get_num_threads();
+#else
+    int t = 0, nt = 1;
+#endif
+    int64_t r0 = B * t / nt, r1 = B * (t + 1) / nt;
+    simulate_range(s, items, values, r0, r1, ctx, part, u, winner, price, second_price, outcome,
+                   item, value, bid, est_ctr, true_ctr, best_ev, part_cnt + (int64_t)t * NC,
+                   part_fx + (int64_t)t * NC);
+  }
+  for (int t = 0; t < nthreads; ++t)
+    for (int64_t i = 0; i < NC; ++i) {
+      counters[i] += part_cnt[(int64_t)t * NC + i];
+      if (counters_fx) add_limbs(counters_fx + i * 3, part_fx[(int64_t)t * NC + i]);
+    }
+  free(part_cnt);
+  free(part_fx);
+}
+
+/* ---- synthetic batch generator (integer part), restating ag_generate ---- */
+
+void ora_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+  uint32_t k0 = key[0], k1 = key[1];
+  for (int i = 0; i < 10; ++i) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    uint32_t n1 = (uint32_t)p1;
+    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    uint32_t n3 = (uint32_t)p0;
+    c0 = n0;
+    c1 = n1;
+    c2 = n2;
+    c3 = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  out[0] = c0;
+  out[1] = c1;
+  out[2] = c2;
+  out[3] = c3;
+}
+
+static void block(uint64_t seed, uint64_t idx, uint32_t blk, uint32_t stream, uint32_t out[4]) {
+  uint32_t ctr[4] = {(uint32_t)idx, (uint32_t)(idx >> 32), blk, stream};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  ora_philox4x32_10(ctr, key, out);
+}
+
+double ora_gen_uniform(uint64_t seed, uint64_t idx) {
+  uint32_t w[4];
+  block(seed, idx, 0, 0, w);
+  uint64_t v = ((uint64_t)w[0] << 32) | w[1];
+  return (double)(v >> 11) * 0x1p-53;
+}
+
+/* Floyd's sampling of P distinct agents out of N; slot order = insertion order.
+ * Step j (j = N-P .. N-1) draws t = floor(word * (j+1) / 2^32) from stream 1. */
+void ora_gen_participants(uint64_t seed, uint64_t idx, int32_t N, int32_t P, int32_t *part_out) {
+  uint32_t w[4];
+  int32_t n = 0;
+  for (int32_t j = N - P; j < N; ++j) {
+    int32_t step = j - (N - P);
+    if ((step & 3) == 0) block(seed, idx, (uint32_t)(step >> 2), 1, w);
+    uint32_t t = (uint32_t)(((uint64_t)w[step & 3] * (uint64_t)(j + 1)) >> 32);
+    int32_t pick = (int32_t)t;
+    for (int32_t q = 0; q < n; ++q)
+      if (part_out[q] == pick) {
+        pick = j;
+        break;
+      }
+    part_out[n++] = pick;
+  }
+}

@@ -1,0 +1,133 @@
+"""ctypes binding of the CPU restatement (oracle/ag_oracle.c) -- TEST INFRASTRUCTURE ONLY.
+
+The oracle is the checker: only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg import this module. The product path (auction-gym_amd/) never does.
+
+Arrays follow the fixtures' row-major layout: per-round [B], per-(round, slot) [B][P].
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "libag_oracle.so")
+
+FIRST_PRICE, SECOND_PRICE = 0, 1
+COUNTERS = ("net", "gross", "allocation_regret", "estimation_regret", "overbid_regret",
+            "underbid_regret", "ctr_sqerr", "ctr_bias_sum", "best_ev_sum", "n_logs", "n_won",
+            "paid")
+NUM_COUNTERS = len(COUNTERS)
+
+_lib = None
+
+
+class _Shape(ctypes.Structure):
+    _fields_ = [("N", ctypes.c_int32), ("P", ctypes.c_int32), ("K", ctypes.c_int32),
+                ("E", ctypes.c_int32), ("mech", ctypes.c_int32)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = ctypes.CDLL(_SO)
+        d, i32, i64, u64 = ctypes.c_double, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
+        vp = ctypes.c_void_p
+        L.ora_sigmoid.restype = d
+        L.ora_sigmoid.argtypes = [d]
+        L.ora_dot.restype = d
+        L.ora_dot.argtypes = [vp, vp, i32]
+        L.ora_bernoulli.restype = i32
+        L.ora_bernoulli.argtypes = [d, d]
+        L.ora_allocate.restype = None
+        L.ora_allocate.argtypes = [i32, vp, i64, i32, vp, vp, vp]
+        L.ora_simulate.restype = None
+        L.ora_simulate.argtypes = [ctypes.POINTER(_Shape), vp, vp, i64, vp, vp, vp] + [vp] * 12 + [i32]
+        L.ora_to_fx.restype = i64
+        L.ora_to_fx.argtypes = [d]
+        L.ora_gen_uniform.restype = d
+        L.ora_gen_uniform.argtypes = [u64, u64]
+        L.ora_gen_participants.restype = None
+        L.ora_gen_participants.argtypes = [u64, u64, i32, i32, vp]
+        L.ora_philox4x32_10.restype = None
+        L.ora_philox4x32_10.argtypes = [vp, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def sigmoid(z):
+    L = lib()
+    return np.array([L.ora_sigmoid(float(v)) for v in np.ravel(z)]).reshape(np.shape(z))
+
+
+def allocate(mech, bids):
+    bids = np.ascontiguousarray(bids, np.float64)
+    B, P = bids.shape
+    w = np.empty(B, np.int32)
+    pr = np.empty(B)
+    sp = np.empty(B)
+    lib().ora_allocate(int(mech), _p(bids), B, P, _p(w), _p(pr), _p(sp))
+    return w, pr, sp
+
+
+def simulate(mech, items, values, ctx, part, u, nthreads=1):
+    """Replay B rounds of Oracle+Truthful agents; returns dict of outputs + counters [N][C]."""
+    items = np.ascontiguousarray(items, np.float64)
+    values = np.ascontiguousarray(values, np.float64)
+    ctx = np.ascontiguousarray(ctx, np.float64)
+    part = np.ascontiguousarray(part, np.int32)
+    u = np.ascontiguousarray(u, np.float64)
+    N, K, D = items.shape
+    B, P = part.shape
+    E = ctx.shape[1]
+    assert D == E + 1 and values.shape == (N, K) and u.shape == (B,)
+    sh = _Shape(N, P, K, E, int(mech))
+    out = dict(winner=np.empty(B, np.int32), price=np.empty(B), second_price=np.empty(B),
+               outcome=np.empty(B, np.uint8), item=np.empty((B, P), np.int32),
+               value=np.empty((B, P)), bid=np.empty((B, P)), est_ctr=np.empty((B, P)),
+               true_ctr=np.empty((B, P)), best_ev=np.empty((B, P)),
+               counters=np.zeros((N, NUM_COUNTERS)),
+               counters_fx=np.zeros((N, NUM_COUNTERS, 3), np.int64))
+    lib().ora_simulate(ctypes.byref(sh), _p(items), _p(values), B, _p(ctx), _p(part), _p(u),
+                       _p(out["winner"]), _p(out["price"]), _p(out["second_price"]),
+                       _p(out["outcome"]), _p(out["item"]), _p(out["value"]), _p(out["bid"]),
+                       _p(out["est_ctr"]), _p(out["true_ctr"]), _p(out["best_ev"]),
+                       _p(out["counters"]), _p(out["counters_fx"]), int(nthreads))
+    return out
+
+
+def fx_limbs_to_int(limbs):
+    """[..., 3] normalised limbs -> Python ints (exact), units of 2^-36."""
+    limbs = np.asarray(limbs)
+    flat = limbs.reshape(-1, 3)
+    vals = [int(a) + (int(b) << 42) + (int(c) << 84) for a, b, c in flat]
+    return np.array(vals, dtype=object).reshape(limbs.shape[:-1])
+
+
+def gen_uniform(seed, idx):
+    return lib().ora_gen_uniform(seed, idx)
+
+
+def gen_participants(seed, idx, N, P):
+    out = np.empty(P, np.int32)
+    lib().ora_gen_participants(seed, idx, N, P, _p(out))
+    return out
+
+
+def philox(ctr, key):
+    c = np.ascontiguousarray(ctr, np.uint32)
+    k = np.ascontiguousarray(key, np.uint32)
+    o = np.empty(4, np.uint32)
+    lib().ora_philox4x32_10(_p(c), _p(k), _p(o))
+    return o

@@ -1,0 +1,323 @@
+#!/usr/bin/env python3 -B
+"""Golden-vector generator (TEST INFRASTRUCTURE; runs only in the dev container).
+
+Imports the reference AuctionGym (`/root/reference/src`, read-only) with harness-only
+shims and records what its hot path computes on fixed seeds, so that the oracle
+(`oracle/`) and the HIP path can be pinned against the reference's own outputs.
+Nothing from the reference is copied: the outputs written here are data
+(inputs + expected outputs) in `tests/golden/*.npz` / `*.json`.
+
+Shims (nothing under /root/reference is modified; run with `python3 -B`):
+  * numba is absent -> `numba.jit` stub. Default "numba-faithful": the sigmoid
+    of `src/Models.py:10-12` evaluated with libm `exp` per element (what the
+    pinned numba 0.55.1, requirements.txt:7, compiles to). This is the exp the
+    oracle and the HIP kernels restate.
+  * seaborn is absent -> empty module (plots only, src/main.py:7).
+  * matplotlib -> Agg backend.
+
+Draw-order replay: alongside the reference rng we advance a CLONE of the same
+PCG64 Generator in the order this repo's replay inputs assume
+(src/Auction.py:30 integers(1,2) -> no draw when max_slots == 1;
+ :33 normal(0, var, E); :42 choice(N, P, replace=False); per-participant
+ bidder draws (none for TruthfulBidder); :65 binomial(1, p) -> one next_double)
+and assert after every round that the clone's state equals the reference's.
+That pins SURVEY §8 a2/a3 on every recorded round.
+
+Usage:  python3 -B tests/golden/make_golden.py [--full]
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+
+REF_SRC = "/root/reference/src"
+REF_CFG = "/root/reference/config"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def install_shims():
+    nb = types.ModuleType("numba")
+    # libm exp called per element through ctypes (math.exp would raise on overflow,
+    # C exp returns inf, as the numba-compiled loop does).
+    import ctypes
+    _libm = ctypes.CDLL("libm.so.6")
+    _libm.exp.restype = ctypes.c_double
+    _libm.exp.argtypes = [ctypes.c_double]
+    _e = np.frompyfunc(_libm.exp, 1, 1)
+
+    def jit(*a, **k):
+        def deco(f):
+            def sigmoid(x):
+                x = np.asarray(x, np.float64)
+                return 1.0 / (1.0 + _e(-x).astype(np.float64))
+            return sigmoid
+        return deco
+
+    nb.jit = jit
+    sys.modules["numba"] = nb
+    sys.modules["seaborn"] = types.ModuleType("seaborn")
+    import matplotlib
+    matplotlib.use("Agg")
+    import torch
+    torch.manual_seed(0)
+
+    class _RP(torch.optim.lr_scheduler.ReduceLROnPlateau):
+        def __init__(self, *a, verbose=None, **k):
+            super().__init__(*a, **k)
+
+    torch.optim.lr_scheduler.ReduceLROnPlateau = _RP
+    sys.path.insert(0, REF_SRC)
+
+
+def write_cfg(cfg):
+    fd, path = tempfile.mkstemp(suffix=".json")
+    with os.fdopen(fd, "w") as f:
+        json.dump(cfg, f)
+    return path
+
+
+def load_cfg(name, **over):
+    with open(os.path.join(REF_CFG, name)) as f:
+        cfg = json.load(f)
+    cfg.update(over)
+    return cfg
+
+
+def oracle_truthful_cfg(n_agents, n_items, P, allocation, seed, E=5, OE=4, var=1.0):
+    return {
+        "random_seed": seed, "num_runs": 1, "num_iter": 1, "rounds_per_iter": 0,
+        "num_participants_per_round": P, "embedding_size": E, "embedding_var": var,
+        "obs_embedding_size": OE, "allocation": allocation,
+        "agents": [{"name": "Truthful Oracle", "num_copies": n_agents, "num_items": n_items,
+                    "allocator": {"type": "OracleAllocator", "kwargs": {}},
+                    "bidder": {"type": "TruthfulBidder", "kwargs": {}}}],
+        "output_dir": "/tmp/ag_golden_unused/",
+    }
+
+
+def capture(cfg, rounds):
+    """Run `rounds` reference rounds (one iteration) and record replay inputs + outputs."""
+    import main as M
+    path = write_cfg(cfg)
+    (rng, config, agent_configs, agents2items, agents2item_values, num_runs, max_slots,
+     E, var, OE) = M.parse_config(path)
+    os.unlink(path)
+    agents = M.instantiate_agents(rng, agent_configs, agents2item_values, agents2items)
+    auction, _, _, _ = M.instantiate_auction(rng, config, agents2items, agents2item_values,
+                                             agents, max_slots, E, var, OE)
+    N = len(agents)
+    P = config["num_participants_per_round"]
+    names = [a.name for a in agents]
+    items = np.stack([agents2items[n] for n in names])          # [N][K][D]
+    values = np.stack([agents2item_values[n] for n in names])   # [N][K]
+
+    clone = np.random.Generator(np.random.PCG64())
+    clone.bit_generator.state = rng.bit_generator.state
+
+    alloc_log = []
+    orig = auction.allocation.allocate
+
+    def wrapped(bids, num_slots):
+        w, p, s = orig(bids, num_slots)
+        alloc_log.append((np.array(bids, np.float64), np.array(w), np.array(p), np.array(s)))
+        return w, p, s
+
+    auction.allocation.allocate = wrapped
+
+    ctx = np.zeros((rounds, E))
+    part = np.zeros((rounds, P), np.int32)
+    u = np.zeros(rounds)
+    rec = {k: np.zeros((rounds, P)) for k in
+           ("bid", "est_ctr", "true_ctr", "best_ev", "value", "price", "second_price")}
+    item = np.zeros((rounds, P), np.int32)
+    won = np.zeros((rounds, P), np.int8)
+    outcome_slot = np.zeros((rounds, P), np.int8)
+    winner = np.full(rounds, -1, np.int32)
+    price = np.full(rounds, np.nan)
+    second = np.full(rounds, np.nan)
+    outcome = np.zeros(rounds, np.int8)
+
+    for r in range(rounds):
+        # replay order (see module docstring)
+        c = clone.normal(0, var, size=E)
+        pa = clone.choice(N, P, replace=False)
+        uu = clone.random()
+        auction.simulate_opportunity()
+        assert clone.bit_generator.state == rng.bit_generator.state, f"draw order diverged at round {r}"
+        ctx[r] = c
+        part[r] = pa
+        u[r] = uu
+        for s, a in enumerate(pa):
+            lg = agents[a].logs[-1]
+            rec["bid"][r, s] = lg.bid
+            rec["est_ctr"][r, s] = lg.estimated_CTR
+            rec["true_ctr"][r, s] = lg.true_CTR
+            rec["best_ev"][r, s] = lg.best_expected_value
+            rec["value"][r, s] = lg.value
+            rec["price"][r, s] = lg.price
+            rec["second_price"][r, s] = lg.second_price
+            item[r, s] = lg.item
+            won[r, s] = bool(lg.won)
+            outcome_slot[r, s] = bool(lg.outcome)
+        bids, w, p, s2 = alloc_log[-1]
+        assert np.array_equal(bids, rec["bid"][r])
+        winner[r] = w[0]
+        if len(p):
+            price[r] = p[0]
+        if len(s2):
+            second[r] = s2[0]
+        if len(p):
+            outcome[r] = outcome_slot[r, w[0]]
+
+    agg = {
+        "net_utility": [a.net_utility for a in agents],
+        "gross_utility": [a.gross_utility for a in agents],
+        "revenue": auction.revenue,
+        "allocation_regret": [float(a.get_allocation_regret()) for a in agents],
+        "estimation_regret": [float(a.get_estimation_regret()) for a in agents],
+        "overbid_regret": [float(a.get_overbid_regret()) for a in agents],
+        "underbid_regret": [float(a.get_underbid_regret()) for a in agents],
+        "ctr_rmse": [float(a.get_CTR_RMSE()) for a in agents],
+        "ctr_bias": [float(a.get_CTR_bias()) if any(o.won for o in a.logs) else float("nan")
+                     for a in agents],
+        "mean_best_ev": [float(np.mean([o.best_expected_value for o in a.logs]))
+                         if a.logs else float("nan") for a in agents],
+        "n_logs": [len(a.logs) for a in agents],
+    }
+    arrays = dict(items=items, values=values, ctx=ctx, part=part, u=u, item=item, won=won,
+                  winner=winner, price=price, second_price=second, outcome=outcome,
+                  **{"slot_" + k: v for k, v in rec.items()})
+    meta = dict(N=N, P=P, K=items.shape[1], E=E, OE=OE, var=var, rounds=rounds,
+                allocation=config["allocation"], seed=config["random_seed"],
+                rng_state_after_setup=None)
+    return arrays, agg, meta
+
+
+def save_capture(name, arrays, agg, meta):
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **arrays)
+    with open(os.path.join(OUT, name + ".json"), "w") as f:
+        json.dump({"meta": meta, "aggregates": agg}, f, indent=1)
+    print("wrote", name, {k: v.shape for k, v in arrays.items()})
+
+
+def alloc_kats():
+    """Reference FirstPrice/SecondPrice.allocate on random and tied bid rows."""
+    import AuctionAllocation as AA
+    g = np.random.default_rng(1234)
+    out = {}
+    for P in (1, 2, 3, 4, 8, 32, 64, 100):
+        rows = [g.lognormal(0.1, 0.2, P) * g.random(P) for _ in range(48)]
+        # ties: all-equal, all-zero, tie at top, tie at second, duplicates of zeros
+        rows.append(np.zeros(P))
+        rows.append(np.full(P, 0.25))
+        b = g.random(P); b[P // 2] = b.max(); rows.append(b)
+        b = g.random(P); b[-1] = b.max(); rows.append(b)
+        b = g.random(P) * (g.random(P) < 0.5); rows.append(b)
+        if P >= 2:
+            b = g.random(P); srt = np.sort(b); b[b == srt[-2]] = 0.0; b[0] = srt[-1] if P > 1 else b[0]
+            rows.append(b)
+        bids = np.stack(rows)
+        for mech in ("FirstPrice", "SecondPrice"):
+            m = getattr(AA, mech)()
+            W, PR, SP = [], [], []
+            for row in bids:
+                w, p, s = m.allocate(row.copy(), 1)
+                W.append(int(w[0]))
+                PR.append(float(p[0]) if len(p) else np.nan)
+                SP.append(float(s[0]) if len(s) else np.nan)
+            out[f"{mech}_P{P}_winner"] = np.array(W, np.int32)
+            out[f"{mech}_P{P}_price"] = np.array(PR)
+            out[f"{mech}_P{P}_second_price"] = np.array(SP)
+        out[f"P{P}_bids"] = bids
+    np.savez_compressed(os.path.join(OUT, "alloc_kat.npz"), **out)
+    print("wrote alloc_kat", len(out))
+
+
+def sigmoid_kats():
+    """Reference sigmoid (numba-faithful shim) on OracleAllocator-shaped dots."""
+    import Models
+    g = np.random.default_rng(7)
+    z = np.concatenate([g.normal(0, 4, 20000), g.uniform(-745, 710, 2000),
+                        np.array([0.0, -0.0, 1e-300, -1e-300, 36.0, -36.0, 709.0, -709.0, -745.0, 40.0])])
+    np.savez_compressed(os.path.join(OUT, "sigmoid_kat.npz"), z=z, sigmoid=Models.sigmoid(z))
+    print("wrote sigmoid_kat")
+
+
+def full_run_aggregates(cfg_name, runs=None, iters=None, rounds=None):
+    """SP_Oracle as shipped: per-iteration revenue / net / gross / regrets (src/main.py:113-155 loop)."""
+    import main as M
+    cfg = load_cfg(cfg_name)
+    if runs is not None:
+        cfg["num_runs"] = runs
+    if iters is not None:
+        cfg["num_iter"] = iters
+    if rounds is not None:
+        cfg["rounds_per_iter"] = rounds
+    path = write_cfg(cfg)
+    (rng, config, agent_configs, agents2items, agents2item_values, num_runs, max_slots,
+     E, var, OE) = M.parse_config(path)
+    os.unlink(path)
+    res = []
+    for run in range(num_runs):
+        agents = M.instantiate_agents(rng, agent_configs, agents2item_values, agents2items)
+        auction, num_iter, rpi, _ = M.instantiate_auction(rng, config, agents2items, agents2item_values,
+                                                          agents, max_slots, E, var, OE)
+        for i in range(num_iter):
+            for _ in range(rpi):
+                auction.simulate_opportunity()
+            row = {"run": run, "iter": i, "revenue": auction.revenue,
+                   "net": [a.net_utility for a in agents], "gross": [a.gross_utility for a in agents],
+                   "allocation_regret": [float(a.get_allocation_regret()) for a in agents],
+                   "estimation_regret": [float(a.get_estimation_regret()) for a in agents],
+                   "overbid_regret": [float(a.get_overbid_regret()) for a in agents],
+                   "underbid_regret": [float(a.get_underbid_regret()) for a in agents],
+                   "ctr_rmse": [float(a.get_CTR_RMSE()) for a in agents],
+                   "mean_best_ev": [float(np.mean([o.best_expected_value for o in a.logs])) for a in agents]}
+            res.append(row)
+            for a in agents:
+                a.update(iteration=i)
+                a.clear_utility()
+                a.clear_logs()
+            auction.clear_revenue()
+            print(cfg_name, run, i, row["revenue"], flush=True)
+    return {"config": cfg, "iterations": res}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--full", action="store_true", help="also run SP_Oracle as shipped (3x20x10k rounds, ~1 min)")
+    args = ap.parse_args()
+    install_shims()
+
+    sigmoid_kats()
+    alloc_kats()
+
+    # 1. SP_Oracle.json exactly as shipped (seed 0, N=6, P=2, K=12, E=5): first 4096 rounds of run 0.
+    a, g, m = capture(load_cfg("SP_Oracle.json"), 4096)
+    save_capture("sp_oracle_r4096", a, g, m)
+    # 2. FirstPrice, 8 truthful Oracle agents, P=3 (FP charges, 3-way allocation).
+    a, g, m = capture(oracle_truthful_cfg(8, 12, 3, "FirstPrice", seed=11), 2048)
+    save_capture("fp_oracle_n8_p3", a, g, m)
+    # 3. SecondPrice, 32 agents, P=8 (wider auctions, the Mixed-population width).
+    a, g, m = capture(oracle_truthful_cfg(32, 12, 8, "SecondPrice", seed=12), 2048)
+    save_capture("sp_oracle_n32_p8", a, g, m)
+    # 4. P=1 edge: prices empty -> nobody charged, no revenue, U still drawn (src/Auction.py:65-74).
+    a, g, m = capture(oracle_truthful_cfg(4, 12, 1, "SecondPrice", seed=13), 256)
+    save_capture("sp_oracle_n4_p1", a, g, m)
+    # 5. Non-default catalogue shape: K=5 items, E=5.
+    a, g, m = capture(oracle_truthful_cfg(5, 5, 2, "FirstPrice", seed=14), 1024)
+    save_capture("fp_oracle_n5_k5", a, g, m)
+
+    if args.full:
+        agg = full_run_aggregates("SP_Oracle.json")
+        with open(os.path.join(OUT, "sp_oracle_full_run.json"), "w") as f:
+            json.dump(agg, f)
+        print("wrote sp_oracle_full_run.json")
+
+
+if __name__ == "__main__":
+    main()

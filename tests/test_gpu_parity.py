@@ -1,0 +1,274 @@
+"""HIP path vs the oracle and the golden vectors (needs an MI355X; `-m gpu`).
+
+Everything goes through the C-ABI (libauctiongym_hip.so) via auctiongym_amd.engine.
+Bar: bit-exact for items, bids, CTRs, winners, prices, outcomes and the fixed-point
+counters; 1e-9 relative for the float counters against the reference aggregates
+(north star: 1e-5).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import CAPTURES, GOLDEN, load_capture, mech_code
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(meta, gpu):
+    from auctiongym_amd.engine import AuctionEngine
+    return AuctionEngine(meta["N"], meta["P"], meta["K"], meta["E"], meta["OE"], mech_code(meta),
+                         meta["var"])
+
+
+def _run(eng, ctx, part, u):
+    """ctx [B][E], part [B][P], u [B] host -> outputs as host arrays in [B]/[B][P] layout."""
+    import torch
+    d = eng.device
+    inp = {"ctx": torch.from_numpy(np.ascontiguousarray(ctx.T)).to(d),
+           "part": torch.from_numpy(np.ascontiguousarray(part.T.astype(np.int32))).to(d),
+           "u": torch.from_numpy(np.ascontiguousarray(u)).to(d)}
+    out = eng.alloc_outputs(len(u))
+    cnt = eng.new_counters()
+    eng.simulate(inp, out, cnt)
+    torch.cuda.synchronize()
+    o = {k: v.cpu().numpy() for k, v in out.items()}
+    for k in ("item", "bid", "est_ctr", "true_ctr", "best_ev"):
+        o[k] = np.ascontiguousarray(o[k].T)
+    o["counters_fx"] = cnt.cpu().numpy()
+    return o
+
+
+def test_device_sigmoid_kat(gpu):
+    import torch
+    from auctiongym_amd.engine import device_exp
+    kat = np.load(os.path.join(GOLDEN, "sigmoid_kat.npz"))
+    z = torch.from_numpy(kat["z"]).to(gpu)
+    assert np.array_equal(device_exp(z, sigmoid=True).cpu().numpy(), kat["sigmoid"])
+
+
+def _libm_exp(x):
+    import ctypes
+    libm = ctypes.CDLL("libm.so.6")
+    libm.exp.restype = ctypes.c_double
+    libm.exp.argtypes = [ctypes.c_double]
+    return np.array([libm.exp(float(v)) for v in x])
+
+
+def test_device_exp_matches_glibc_exactly(gpu):
+    import torch
+    from auctiongym_amd.engine import device_exp
+    g = np.random.default_rng(6)
+    x = np.concatenate([g.uniform(-40, 40, 200000), g.uniform(-745.2, 709.8, 100000),
+                        np.array([0.0, -0.0, 1e-300, -1e-310, 709.78, -708.4, -745.13, 0.5, -0.5])])
+    y = device_exp(torch.from_numpy(x).to(gpu)).cpu().numpy()
+    ref = _libm_exp(x)
+    bad = np.flatnonzero(y.view(np.int64) != ref.view(np.int64))
+    assert bad.size == 0, (x[bad[:5]], y[bad[:5]], ref[bad[:5]])
+
+
+def test_allocate_kat(gpu, oracle):
+    import torch
+    from auctiongym_amd.engine import AuctionEngine
+    kat = np.load(os.path.join(GOLDEN, "alloc_kat.npz"))
+    for P in (1, 2, 3, 4, 8, 32, 64, 100):
+        bids = kat[f"P{P}_bids"]
+        for mech_name, mech in (("FirstPrice", 0), ("SecondPrice", 1)):
+            eng = AuctionEngine(P, P, 1, 1, 0, mech)
+            w, pr, sp = eng.allocate(torch.from_numpy(np.ascontiguousarray(bids.T)).to(gpu))
+            w, pr, sp = w.cpu().numpy(), pr.cpu().numpy(), sp.cpu().numpy()
+            ow, opr, osp = oracle.allocate(mech, bids)
+            assert np.array_equal(w, ow), (P, mech_name)
+            np.testing.assert_array_equal(pr, opr)
+            np.testing.assert_array_equal(sp, osp)
+            np.testing.assert_array_equal(pr, kat[f"{mech_name}_P{P}_price"])
+            np.testing.assert_array_equal(sp, kat[f"{mech_name}_P{P}_second_price"])
+            eng.close()
+
+
+def test_allocate_ragged_and_large(gpu, oracle):
+    import torch
+    from auctiongym_amd.engine import AuctionEngine
+    g = np.random.default_rng(3)
+    for P, B in ((2, 1), (2, 255), (3, 70001), (8, 1 << 20), (33, 5000), (200, 777)):
+        bids = g.random((B, P)) * (g.random((B, P)) < 0.7)
+        for mech in (0, 1):
+            eng = AuctionEngine(P, P, 1, 1, 0, mech)
+            w, pr, sp = eng.allocate(torch.from_numpy(np.ascontiguousarray(bids.T)).to(gpu))
+            ow, opr, osp = oracle.allocate(mech, bids)
+            assert np.array_equal(w.cpu().numpy(), ow)
+            np.testing.assert_array_equal(pr.cpu().numpy(), opr)
+            np.testing.assert_array_equal(sp.cpu().numpy(), osp)
+            eng.close()
+
+
+@pytest.mark.parametrize("name", CAPTURES)
+def test_simulate_replay_matches_reference(gpu, oracle, name):
+    d, meta, agg = load_capture(name)
+    eng = _engine(meta, gpu)
+    eng.load_catalog(d["items"], d["values"])
+    o = _run(eng, d["ctx"], d["part"], d["u"])
+    for mine, ref in (("item", "item"), ("bid", "slot_bid"), ("est_ctr", "slot_est_ctr"),
+                      ("true_ctr", "slot_true_ctr"), ("best_ev", "slot_best_ev")):
+        assert np.array_equal(o[mine], d[ref]), mine
+    assert np.array_equal(o["winner"], d["winner"])
+    if meta["P"] >= 2:
+        assert np.array_equal(o["price"], d["price"])
+        assert np.array_equal(o["second_price"], d["second_price"])
+        assert np.array_equal(o["outcome"], d["outcome"])
+    else:
+        assert np.isnan(o["price"]).all()
+    # exact fixed-point counters == the oracle's, bit for bit
+    orc = oracle.simulate(mech_code(meta), d["items"], d["values"], d["ctx"], d["part"], d["u"])
+    assert np.array_equal(o["counters_fx"], orc["counters_fx"])
+    from auctiongym_amd.engine import AuctionEngine
+    cnt = AuctionEngine.counters_to_numpy(o["counters_fx"])
+    C = {n: i for i, n in enumerate(oracle.COUNTERS)}
+    rt = dict(rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(cnt[:, C["net"]], agg["net_utility"], **rt)
+    np.testing.assert_allclose(cnt[:, C["gross"]], agg["gross_utility"], **rt)
+    np.testing.assert_allclose(cnt[:, C["paid"]].sum(), agg["revenue"], **rt)
+    np.testing.assert_allclose(cnt[:, C["underbid_regret"]], agg["underbid_regret"], **rt)
+    np.testing.assert_allclose(cnt[:, C["overbid_regret"]], agg["overbid_regret"], **rt)
+    eng.close()
+
+
+def test_generator_matches_oracle(gpu, oracle):
+    from auctiongym_amd.engine import AuctionEngine
+    eng = AuctionEngine(32, 8, 12, 5, 4, 1, 1.0)
+    inp = eng.alloc_inputs(100003)
+    eng.generate(1234, 5_000_000_000, inp)
+    part = inp["part"].cpu().numpy()
+    u = inp["u"].cpu().numpy()
+    ctx = inp["ctx"].cpu().numpy()
+    for i in list(range(0, 100003, 997)) + [100002]:
+        idx = 5_000_000_000 + i
+        assert u[i] == oracle.gen_uniform(1234, idx)
+        assert np.array_equal(part[:, i], oracle.gen_participants(1234, idx, 32, 8))
+    assert abs(ctx.mean()) < 0.01 and abs(ctx.std() - 1.0) < 0.01
+    assert (np.sort(part, axis=0)[1:] != np.sort(part, axis=0)[:-1]).all()
+    eng.close()
+
+
+def test_full_size_synthetic_batch_bit_exact(gpu, oracle):
+    """The bench workload shape (SP_Oracle: N=6, P=2, K=12, E=5) at 4M auctions, Philox
+    inputs generated on the GPU, every output compared with the oracle on the same inputs."""
+    import torch
+    from auctiongym_amd.engine import AuctionEngine
+    import auctiongym_amd.main as M
+    with open(os.path.join(GOLDEN, "sp_oracle_full_run.json")) as f:
+        cfg = json.load(f)["config"]
+    B = 1 << 22
+    g = np.random.default_rng(0)
+    items = np.concatenate([g.normal(0, 1, (6, 12, 5)), -3.0 - g.random((6, 12, 1))], axis=2)
+    values = g.lognormal(0.1, 0.2, (6, 12))
+    eng = AuctionEngine(6, 2, 12, 5, 4, 1, cfg["embedding_var"])
+    eng.load_catalog(items, values)
+    inp = eng.alloc_inputs(B)
+    eng.generate(0, 0, inp)
+    out = eng.alloc_outputs(B)
+    cnt = eng.new_counters()
+    eng.simulate(inp, out, cnt)
+    torch.cuda.synchronize()
+    ctx = np.ascontiguousarray(inp["ctx"].cpu().numpy().T)
+    part = np.ascontiguousarray(inp["part"].cpu().numpy().T)
+    u = inp["u"].cpu().numpy()
+    orc = oracle.simulate(1, items, values, ctx, part, u, nthreads=16)
+    assert np.array_equal(out["winner"].cpu().numpy(), orc["winner"])
+    assert np.array_equal(out["price"].cpu().numpy(), orc["price"])
+    assert np.array_equal(out["bid"].cpu().numpy().T, orc["bid"])
+    assert np.array_equal(out["item"].cpu().numpy().T, orc["item"])
+    assert np.array_equal(out["best_ev"].cpu().numpy().T, orc["best_ev"])
+    assert np.array_equal(out["outcome"].cpu().numpy(), orc["outcome"])
+    assert np.array_equal(cnt.cpu().numpy(), orc["counters_fx"])
+    # batch split invariance: two halves accumulate to the same exact counters
+    cnt2 = eng.new_counters()
+    for lo, hi in ((0, B // 3), (B // 3, B)):
+        sub_in = {"ctx": inp["ctx"][:, lo:hi].contiguous(), "part": inp["part"][:, lo:hi].contiguous(),
+                  "u": inp["u"][lo:hi].contiguous()}
+        eng.simulate(sub_in, eng.alloc_outputs(hi - lo, ("winner",)), cnt2)
+    assert torch.equal(cnt, cnt2)
+    eng.close()
+
+
+def test_driver_sp_oracle_matches_reference_full_run(gpu, tmp_path):
+    """auctiongym_amd.main on SP_Oracle.json as shipped (3 x 20 x 10k rounds) vs the
+    reference's per-iteration revenue / net / gross (SURVEY §4 known answers)."""
+    import auctiongym_amd.main as M
+    with open(os.path.join(GOLDEN, "sp_oracle_full_run.json")) as f:
+        ref = json.load(f)
+    cfg = dict(ref["config"], output_dir=str(tmp_path / "out"))
+    p = tmp_path / "SP_Oracle.json"
+    p.write_text(json.dumps(cfg))
+    run2stats, run2rev = M.main([str(p), "--quiet"])
+    rows = iter(ref["iterations"])
+    total = 0.0
+    for run in range(cfg["num_runs"]):
+        stats = run2stats[run]
+        names = list(stats["net_utility"].keys())
+        for it in range(cfg["num_iter"]):
+            row = next(rows)
+            np.testing.assert_allclose(run2rev[run][it], row["revenue"], rtol=1e-12)
+            np.testing.assert_allclose([stats["net_utility"][n][it] for n in names], row["net"], rtol=1e-11)
+            np.testing.assert_allclose([stats["gross_utility"][n][it] for n in names], row["gross"],
+                                       rtol=1e-11)
+            np.testing.assert_allclose([stats["best_expected_value"][n][it] for n in names],
+                                       row["mean_best_ev"], rtol=1e-11)
+            assert all(stats["allocation_regret"][n][it] == 0.0 for n in names)
+            total += run2rev[run][it]
+    np.testing.assert_allclose(total, 247455.77552418958, rtol=1e-12)
+    assert (tmp_path / "out").is_dir()
+
+
+def test_notebook_call_pattern(gpu, tmp_path):
+    """The reference notebooks' loop: simulate_opportunity() per round, then read
+    net/gross/revenue, update, clear (src/*.ipynb cell 4)."""
+    import auctiongym_amd.main as M
+    d, meta, agg = load_capture("sp_oracle_r4096")
+    with open(os.path.join(GOLDEN, "sp_oracle_full_run.json")) as f:
+        cfg = json.load(f)["config"]
+    p = tmp_path / "c.json"
+    p.write_text(json.dumps(cfg))
+    rng, config, agent_configs, a2i, a2v, _, max_slots, E, var, OE = M.parse_config(str(p))
+    agents = M.instantiate_agents(rng, agent_configs, a2v, a2i)
+    auction, _, _, _ = M.instantiate_auction(rng, config, a2i, a2v, agents, max_slots, E, var, OE)
+    for _ in range(4096):
+        auction.simulate_opportunity()
+    np.testing.assert_allclose([a.net_utility for a in agents], agg["net_utility"], rtol=1e-11)
+    np.testing.assert_allclose(auction.revenue, agg["revenue"], rtol=1e-12)
+    logs = agents[0].logs
+    assert len(logs) == agg["n_logs"][0]
+    for a in agents:
+        a.update(iteration=0)
+        a.clear_utility()
+        a.clear_logs()
+    auction.clear_revenue()
+    assert auction.revenue == 0.0 and agents[0].net_utility == 0.0 and agents[0].logs == []
+
+
+def test_errors_are_loud(gpu):
+    from auctiongym_amd.engine import AuctionEngine
+    with pytest.raises(ValueError):
+        AuctionEngine(3, 4, 12, 5, 4, 1)  # P > N: rng.choice raises ValueError too
+    eng = AuctionEngine(4, 2, 12, 5, 4, 1)
+    inp = eng.alloc_inputs(8)
+    with pytest.raises(RuntimeError):
+        eng.simulate(inp, eng.alloc_outputs(8))  # catalogue not loaded
+    with pytest.raises(NotImplementedError):
+        eng.set_agent_kinds([1, 0, 0, 0], [0, 0, 0, 0])
+    eng.close()
+
+
+def test_empty_batch(gpu):
+    import torch
+    from auctiongym_amd.engine import AuctionEngine
+    eng = AuctionEngine(4, 2, 12, 5, 4, 0)
+    g = np.random.default_rng(1)
+    eng.load_catalog(g.normal(size=(4, 12, 6)), g.random((4, 12)))
+    cnt = eng.new_counters()
+    eng.simulate(eng.alloc_inputs(0), eng.alloc_outputs(0), cnt)
+    assert int(cnt.abs().sum()) == 0
+    w, p, s = eng.allocate(torch.empty((2, 0), dtype=torch.float64, device=gpu))
+    assert w.numel() == 0
+    eng.close()

@@ -1,0 +1,130 @@
+"""Host-side logic and the C-ABI library, without a GPU."""
+import ctypes
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT, load_capture
+
+LIB = os.path.join(ROOT, "auction-gym_amd", "auctiongym_amd", "libauctiongym_hip.so")
+HDR = os.path.join(ROOT, "include", "auctiongym.h")
+
+
+def _declared_symbols():
+    import re
+    txt = open(HDR).read()
+    return sorted(set(re.findall(r"^(?:int|int32_t|const char\s*\*)\s*(ag_\w+)\(", txt, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from auctiongym_amd import _lib
+    assert os.path.exists(LIB), "build with `make -C auction-gym_amd`"
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    declared = _declared_symbols()
+    assert declared and set(declared) <= exported, set(declared) - exported
+    assert set(declared) == set(_lib.EXPORTS)
+
+
+def test_library_loads_without_gpu_and_reports_abi():
+    from auctiongym_amd import _lib
+    L = _lib.load()
+    assert L.ag_abi_version() == 1
+
+
+def test_counters_to_double_host_helper():
+    from auctiongym_amd import _lib
+    L = _lib.load()
+    vals = [0, 1, -1, (1 << 36) * 3, -((1 << 90) + 12345), (1 << 100) + 7]
+    limbs = []
+    for v in vals:
+        m = (1 << 42) - 1
+        limbs.append([v & m, (v >> 42) & m, v >> 84])
+    fx = np.array(limbs, np.int64)
+    out = np.empty(len(vals))
+    assert L.ag_counters_to_double(fx.ctypes.data, len(vals), out.ctypes.data) == 0
+    np.testing.assert_array_equal(out, [float(v) * 2.0 ** -36 for v in vals])
+
+
+def test_ctx_creation_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from auctiongym_amd.engine import AuctionEngine
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        AuctionEngine(6, 2, 12, 5, 4, 1)
+
+
+def _sp_config(tmp_path):
+    with open(os.path.join(GOLDEN, "sp_oracle_full_run.json")) as f:
+        cfg = json.load(f)["config"]
+    p = tmp_path / "SP_Oracle.json"
+    p.write_text(json.dumps(cfg))
+    return str(p)
+
+
+def test_parse_config_reproduces_reference_catalogue(tmp_path):
+    import auctiongym_amd.main as M
+    d, meta, _ = load_capture("sp_oracle_r4096")
+    rng, config, agent_configs, a2i, a2v, num_runs, max_slots, E, var, OE = M.parse_config(
+        _sp_config(tmp_path))
+    names = [c["name"] for c in agent_configs]
+    assert names == [f"Truthful Oracle {i}" for i in range(1, 7)]
+    assert np.array_equal(np.stack([a2i[n] for n in names]), d["items"])
+    assert np.array_equal(np.stack([a2v[n] for n in names]), d["values"])
+    assert (num_runs, max_slots, E, var, OE) == (3, 1, 5, 1.0, 4)
+
+
+def test_replay_draws_reproduce_reference_inputs(tmp_path):
+    import auctiongym_amd.main as M
+    from auctiongym_amd.replay import draw_rounds
+    d, meta, _ = load_capture("sp_oracle_r4096")
+    rng, config, agent_configs, *_ = M.parse_config(_sp_config(tmp_path))
+    ctx, part, u = draw_rounds(rng, 4096, meta["N"], meta["P"], meta["E"], meta["var"])
+    assert np.array_equal(ctx.T, d["ctx"]) and np.array_equal(part.T, d["part"])
+    assert np.array_equal(u, d["u"])
+
+
+def test_plugin_factory_semantics(tmp_path):
+    import auctiongym_amd.main as M
+    from auctiongym_amd.Bidder import TruthfulBidder, ValueLearningBidder
+    rng = np.random.default_rng(0)
+    b = M.make_plugin("ValueLearningBidder", rng,
+                      {"gamma_sigma": 0.02, "init_gamma": 1.0, "inference": '"policy"'})
+    assert isinstance(b, ValueLearningBidder) and b.kwargs["inference"] == "policy"
+    assert isinstance(M.make_plugin("TruthfulBidder", rng, {}), TruthfulBidder)
+    with pytest.raises(ValueError):
+        M.make_plugin("os.system", rng, {})
+    mech = M.make_plugin("SecondPrice", rng, {}, pass_rng=False)
+    assert mech.code == 1
+
+
+def test_unbuilt_plugins_are_refused_not_faked(tmp_path):
+    """Learned bidders parse but the GPU path refuses them (no silent CPU path)."""
+    import auctiongym_amd.main as M
+    from auctiongym_amd.Auction import Auction
+    from auctiongym_amd.AuctionAllocation import FirstPrice
+    cfg = {"random_seed": 0, "num_runs": 1, "num_iter": 1, "rounds_per_iter": 10,
+           "num_participants_per_round": 2, "embedding_size": 5, "embedding_var": 1.0,
+           "obs_embedding_size": 4, "allocation": "FirstPrice", "output_dir": str(tmp_path),
+           "agents": [{"name": "DR", "num_copies": 3, "num_items": 12,
+                       "allocator": {"type": "PyTorchLogisticRegressionAllocator",
+                                     "kwargs": {"embedding_size": 4, "num_items": 12}},
+                       "bidder": {"type": "DoublyRobustBidder",
+                                  "kwargs": {"gamma_sigma": 0.02, "init_gamma": 1.0}}}]}
+    p = tmp_path / "c.json"
+    p.write_text(json.dumps(cfg))
+    rng, config, ac, a2i, a2v, _, ms, E, var, OE = M.parse_config(str(p))
+    agents = M.instantiate_agents(rng, ac, a2v, a2i)
+    with pytest.raises(NotImplementedError):
+        Auction(rng, FirstPrice(), agents, a2i, a2v, ms, E, var, OE, 2)
+
+
+def test_graft_entry_build_is_idempotent():
+    import __graft_entry__ as G
+    G.build()
+    assert os.path.exists(LIB)
