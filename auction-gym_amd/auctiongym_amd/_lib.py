@@ -13,6 +13,8 @@ AG_OK, AG_ERR_INVALID, AG_ERR_UNSUPPORTED, AG_ERR_HIP, AG_ERR_STATE = 0, -1, -2,
 FIRST_PRICE, SECOND_PRICE = 0, 1
 ALLOCATOR_ORACLE = 0
 BIDDER_TRUTHFUL = 0
+OPT_ITEM_SEARCH = 0
+ITEM_SEARCH_AUTO, ITEM_SEARCH_EXACT = 0, 1
 
 COUNTERS = ("net", "gross", "allocation_regret", "estimation_regret", "overbid_regret",
             "underbid_regret", "ctr_sqerr", "ctr_bias_sum", "best_ev_sum", "n_logs", "n_won",
@@ -21,7 +23,8 @@ NUM_COUNTERS = len(COUNTERS)
 FX_FRAC_BITS, FX_LIMB_BITS, FX_LIMBS = 36, 42, 3
 
 # Every symbol include/auctiongym.h declares (tests check the .so exports all of them).
-EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_load_catalog", "ag_allocate",
+EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_option", "ag_load_catalog",
+           "ag_allocate",
            "ag_simulate", "ag_generate", "ag_counters_to_double", "ag_sigmoid", "ag_exp",
            "ag_last_error", "ag_abi_version")
 
@@ -67,6 +70,7 @@ def load():
         "ag_destroy": (ctypes.c_int, [vp]),
         "ag_set_agent_kinds": (ctypes.c_int, [vp, vp, vp]),
         "ag_load_catalog": (ctypes.c_int, [vp, vp, vp]),
+        "ag_set_option": (ctypes.c_int, [vp, i32, i64]),
         "ag_allocate": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, vp]),
         "ag_simulate": (ctypes.c_int, [vp, i64, ctypes.POINTER(AgBatchIn),
                                        ctypes.POINTER(AgBatchOut), vp, vp]),

@@ -73,6 +73,12 @@ class AuctionEngine:
         assert a.shape == (self.N,) and b.shape == (self.N,)
         check(self.L.ag_set_agent_kinds(self._h, a.ctypes.data, b.ctypes.data), "ag_set_agent_kinds")
 
+    def set_item_search(self, exact):
+        """exact=True: score every item in FP64 (the reference loop); False (default): f32
+        screen + exact re-score of the near-best items -- identical results."""
+        mode = _lib.ITEM_SEARCH_EXACT if exact else _lib.ITEM_SEARCH_AUTO
+        check(self.L.ag_set_option(self._h, _lib.OPT_ITEM_SEARCH, mode), "ag_set_option")
+
     def load_catalog(self, items, values):
         items = np.ascontiguousarray(items, np.float64)
         values = np.ascontiguousarray(values, np.float64)

@@ -114,13 +114,48 @@ __device__ __forceinline__ unsigned long long to_fx(double x) {
   return (unsigned long long)(long long)rint(x * kFxScale);
 }
 
+// LDS carve of k_simulate (all pieces 16-B aligned; offsets in bytes).
+struct LdsLayout {
+  int32_t tab, items, values, items_f, values_f, amax, cnt, total;
+  int32_t items_stride;    // doubles between agents (odd: spreads agents over banks)
+  int32_t values_stride;   // doubles
+  int32_t items_f_stride;  // floats between agents ([K][8] rows + 4: 16-B slots spread)
+  int32_t values_f_stride; // floats
+};
+
+__host__ inline int32_t align16(int64_t b) { return (int32_t)((b + 15) & ~(int64_t)15); }
+
+__host__ inline LdsLayout make_layout(int N, int K, int D, int replicas, bool counters) {
+  LdsLayout L;
+  L.items_stride = (K * D) | 1;
+  L.values_stride = K | 1;
+  L.items_f_stride = K * 8 + 4;
+  L.values_f_stride = K + 1;
+  int64_t b = 0;
+  L.tab = 0;
+  b += 256 * 8;
+  L.items = align16(b);
+  b = L.items + (int64_t)N * L.items_stride * 8;
+  L.values = align16(b);
+  b = L.values + (int64_t)N * L.values_stride * 8;
+  L.items_f = align16(b);
+  b = L.items_f + (int64_t)N * L.items_f_stride * 4;
+  L.values_f = align16(b);
+  b = L.values_f + (int64_t)N * L.values_f_stride * 4;
+  L.amax = align16(b);
+  b = L.amax + (int64_t)N * 4;
+  L.cnt = align16(b);
+  b = L.cnt + (counters ? (int64_t)replicas * N * kC * 8 : 0);
+  L.total = align16(b);
+  return L;
+}
+
 struct SimParams {
   int64_t B;
   int32_t N, K, E, mech;
-  int32_t items_stride;   // doubles between agents in the LDS catalogue (odd: bank spread)
-  int32_t values_stride;
   int32_t replicas;       // LDS counter replicas (lane % replicas) to cut atomic conflicts
   int32_t want_counters;
+  LdsLayout lds;
   const double *items;    // global [N][K][D]
   const double *values;   // global [N][K]
   ag_batch_in in;
@@ -128,44 +163,117 @@ struct SimParams {
   int64_t *partials;      // [grid][N][C]
 };
 
-// Dynamic LDS carve (16-B aligned pieces): exp table | items | values | counters.
-__host__ __device__ inline size_t lds_bytes(int N, int K, int items_stride, int values_stride,
-                                            int replicas, int want_counters) {
-  size_t b = 256 * 8;
-  b += (size_t)N * items_stride * 8;
-  b = (b + 15) & ~(size_t)15;
-  b += (size_t)N * values_stride * 8;
-  b = (b + 15) & ~(size_t)15;
-  if (want_counters) b += (size_t)replicas * N * kC * 8;
-  return b;
+// Pruning margin of the item search (see select_item). With S = sum_d |a_d x_d| <= 256
+// the f32 score of every item is within eps <= 1.5e-4 (relative) of its exact score, so
+// any item whose exact score is the maximum has f32 score >= max_f32 * (1 - 2 eps / (1 +
+// eps)) > max_f32 * (1 - kPruneDelta): keeping every item above that threshold keeps the
+// exact argmax and all its exact ties.
+constexpr float kPruneDelta = 0x1p-10f;
+constexpr float kPruneMaxS = 256.0f;
+constexpr int kPruneMaxK = 16;
+
+// Agent.select_item (src/Agent.py:29-42) for an OracleAllocator agent: the first k that
+// maximises sigmoid(items_k . x) * value_k, with the reference's exact FP64 arithmetic.
+// PRUNE: a cheap f32 pass scores all K items; only items within kPruneDelta of the f32
+// maximum are re-scored exactly (usually one), in increasing k, so the first-max rule and
+// every bit of the chosen item's CTR / score are the reference's.
+template <int D, bool PRUNE>
+__device__ __forceinline__ int select_item(const double *__restrict__ itm, const double *__restrict__ vv,
+                                           const float *__restrict__ itf, const float *__restrict__ vf,
+                                           float amax, int K, const double (&x)[kMaxD],
+                                           const float (&xf)[8], float xabs, const uint64_t *tab,
+                                           double &ctr_best, double &score_best) {
+  int best = 0;
+  double best_s = 0.0, best_c = 0.0;
+  bool have = false;
+  auto exact = [&](int k) {
+    const double c = agexp::sigmoid(dot_ref<D>(itm + k * D, x), tab);
+    const double sc = c * vv[k];
+    if (!have || sc > best_s) {
+      best = k;
+      best_s = sc;
+      best_c = c;
+      have = true;
+    }
+  };
+  if constexpr (PRUNE) {
+    float sf[kPruneMaxK];
+    float mx = 0.0f;
+#pragma unroll
+    for (int k = 0; k < kPruneMaxK; ++k) {
+      if (k < K) {
+        const float4 a0 = *reinterpret_cast<const float4 *>(itf + k * 8);
+        const float4 a1 = *reinterpret_cast<const float4 *>(itf + k * 8 + 4);
+        float z = a0.x * xf[0];
+        z = fmaf(a0.y, xf[1], z);
+        z = fmaf(a0.z, xf[2], z);
+        z = fmaf(a0.w, xf[3], z);
+        z = fmaf(a1.x, xf[4], z);
+        z = fmaf(a1.y, xf[5], z);
+        z = fmaf(a1.z, xf[6], z);
+        z = fmaf(a1.w, xf[7], z);
+        const float sg = __frcp_rn(1.0f + __expf(-z));
+        sf[k] = sg * vf[k];
+        mx = fmaxf(mx, sf[k]);
+      }
+    }
+    const bool ok = (amax * xabs <= kPruneMaxS) && (mx >= 1e-30f);
+    const float thr = ok ? mx * (1.0f - kPruneDelta) : -1.0f;
+    uint32_t cand = 0;
+#pragma unroll
+    for (int k = 0; k < kPruneMaxK; ++k)
+      if (k < K && sf[k] >= thr) cand |= 1u << k;
+    while (cand) {
+      const int k = __builtin_ctz(cand);
+      cand &= cand - 1;
+      exact(k);
+    }
+  } else {
+    for (int k = 0; k < K; ++k) exact(k);
+  }
+  ctr_best = best_c;
+  score_best = best_s;
+  return best;
 }
 
 // ------------------------------------------------------------------------------------
 // fused simulate kernel
 // ------------------------------------------------------------------------------------
-template <int P, int D>
+template <int P, int D, bool PRUNE>
 __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = prm.N, K = prm.K;
   const int64_t B = prm.B;
-  uint64_t *s_tab = reinterpret_cast<uint64_t *>(smem);
-  double *s_items = reinterpret_cast<double *>(smem + 256 * 8);
-  size_t off = 256 * 8 + (size_t)N * prm.items_stride * 8;
-  off = (off + 15) & ~(size_t)15;
-  double *s_vals = reinterpret_cast<double *>(smem + off);
-  off += (size_t)N * prm.values_stride * 8;
-  off = (off + 15) & ~(size_t)15;
-  unsigned long long *s_cnt = reinterpret_cast<unsigned long long *>(smem + off);
+  const LdsLayout &L = prm.lds;
+  uint64_t *s_tab = reinterpret_cast<uint64_t *>(smem + L.tab);
+  double *s_items = reinterpret_cast<double *>(smem + L.items);
+  double *s_vals = reinterpret_cast<double *>(smem + L.values);
+  float *s_items_f = reinterpret_cast<float *>(smem + L.items_f);
+  float *s_vals_f = reinterpret_cast<float *>(smem + L.values_f);
+  float *s_amax = reinterpret_cast<float *>(smem + L.amax);
+  unsigned long long *s_cnt = reinterpret_cast<unsigned long long *>(smem + L.cnt);
 
   const int tid = threadIdx.x;
   for (int i = tid; i < 256; i += kThreads) s_tab[i] = ag_exp_tab[i];
   for (int i = tid; i < N * K * D; i += kThreads) {
-    int a = i / (K * D), r = i - a * (K * D);
-    s_items[a * prm.items_stride + r] = prm.items[i];
+    const int a = i / (K * D), r = i - a * (K * D);
+    s_items[a * L.items_stride + r] = prm.items[i];
   }
   for (int i = tid; i < N * K; i += kThreads) {
-    int a = i / K, r = i - a * K;
-    s_vals[a * prm.values_stride + r] = prm.values[i];
+    const int a = i / K, r = i - a * K;
+    s_vals[a * L.values_stride + r] = prm.values[i];
+    s_vals_f[a * L.values_f_stride + r] = (float)prm.values[i];
+  }
+  if (PRUNE) {
+    for (int i = tid; i < N * K * 8; i += kThreads) {
+      const int a = i / (K * 8), r = i - a * (K * 8), k = r >> 3, d = r & 7;
+      s_items_f[a * L.items_f_stride + r] = d < D ? (float)prm.items[((size_t)a * K + k) * D + d] : 0.0f;
+    }
+    for (int a = tid; a < N; a += kThreads) {
+      float m = 0.0f;
+      for (int r = 0; r < K * D; ++r) m = fmaxf(m, (float)fabs(prm.items[(size_t)a * K * D + r]));
+      s_amax[a] = m * 1.001f;
+    }
   }
   const int ncnt = prm.replicas * N * kC;
   if (prm.want_counters)
@@ -181,12 +289,21 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
     if (i >= B) continue;
 
     double x[kMaxD];
+    float xf[8];
+    float xabs = 1.0f;
 #pragma unroll
-    for (int e = 0; e < D - 1; ++e) x[e] = in.ctx[(int64_t)e * B + i];
+    for (int e = 0; e < D - 1; ++e) {
+      x[e] = in.ctx[(int64_t)e * B + i];
+      if (e < 8) xf[e] = (float)x[e];
+      xabs += fabsf((float)x[e]);
+    }
     x[D - 1] = 1.0;  // intercept (src/Auction.py:33)
+#pragma unroll
+    for (int e = D - 1; e < 8; ++e) xf[e] = e == D - 1 ? 1.0f : 0.0f;
+    xabs *= 1.001f;
     const double u = in.u[i];
 
-    int ag[P], it[P];
+    int ag[P];
     double val[P], bid[P], ctr[P], bev[P];
     int w = 0;
     double m1 = 0.0, m2 = -INFINITY;
@@ -195,33 +312,23 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
     for (int s = 0; s < P; ++s) {
       const int a = in.part[(int64_t)s * B + i];
       ag[s] = a;
-      const double *itm = s_items + a * prm.items_stride;
-      const double *vv = s_vals + a * prm.values_stride;
-      // Agent.select_item: first argmax over k of sigmoid(items_k . x) * value_k.
-      int best = 0;
-      double best_s = 0.0, best_c = 0.0;
-      for (int k = 0; k < K; ++k) {
-        const double c = agexp::sigmoid(dot_ref<D>(itm + k * D, x), s_tab);
-        const double sc = c * vv[k];
-        if (k == 0 || sc > best_s) {
-          best = k;
-          best_s = sc;
-          best_c = c;
-        }
-      }
-      const double v = vv[best];
-      const double b = v * best_c;  // TruthfulBidder.bid
-      it[s] = best;
+      double c, bs;
+      const int best = select_item<D, PRUNE>(s_items + a * L.items_stride, s_vals + a * L.values_stride,
+                                             s_items_f + a * L.items_f_stride,
+                                             s_vals_f + a * L.values_f_stride, PRUNE ? s_amax[a] : 0.0f,
+                                             K, x, xf, xabs, s_tab, c, bs);
+      const double v = s_vals[a * L.values_stride + best];
+      const double b = v * c;  // TruthfulBidder.bid
       val[s] = v;
       bid[s] = b;
-      ctr[s] = best_c;  // Oracle: estimated CTR == true CTR, bit for bit
-      bev[s] = best_s;  // max_k true_CTR_k * value_k
+      ctr[s] = c;   // Oracle: estimated CTR == true CTR, bit for bit
+      bev[s] = bs;  // max_k true_CTR_k * value_k
       const int64_t o = (int64_t)s * B + i;
       if (out.item) out.item[o] = best;
       if (out.bid) out.bid[o] = b;
-      if (out.est_ctr) out.est_ctr[o] = best_c;
-      if (out.true_ctr) out.true_ctr[o] = best_c;
-      if (out.best_ev) out.best_ev[o] = best_s;
+      if (out.est_ctr) out.est_ctr[o] = c;
+      if (out.true_ctr) out.true_ctr[o] = c;
+      if (out.best_ev) out.best_ev[o] = bs;
       // streaming top-2, ties -> lowest slot
       if (s == 0) {
         m1 = b;
@@ -248,6 +355,9 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
     if (out.outcome) out.outcome[i] = (uint8_t)oc;
 
     if (prm.want_counters) {
+      // Oracle agents: est == true CTR and best_ev == true_ctr * value bit for bit, so the
+      // allocation / estimation regrets and the CTR error terms are exactly 0 and the CTR
+      // bias term is exactly 1 per won record (N_WON carries it; see ag_simulate).
 #pragma unroll
       for (int s = 0; s < P; ++s) {
         unsigned long long *C = s_cnt + ((size_t)rep * N + ag[s]) * kC;
@@ -261,20 +371,14 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
           atomicAdd(C + AG_C_GROSS, to_fx(last_value));
           atomicAdd(C + AG_C_N_WON, to_fx(1.0));
           atomicAdd(C + AG_C_PAID, to_fx(price));
-          atomicAdd(C + AG_C_CTR_BIAS, to_fx(ctr[s] / ctr[s]));
           atomicAdd(C + AG_C_OVERBID, to_fx(lp - lsp));
         } else {
           atomicAdd(C + AG_C_UNDERBID, to_fx((lp - bid[s]) * (double)(lp < tv)));
         }
-        atomicAdd(C + AG_C_ALLOC_REGRET, to_fx(bev[s] - tv));
-        atomicAdd(C + AG_C_EST_REGRET, to_fx(ctr[s] * val[s] - tv));
-        const double d = ctr[s] - ctr[s];
-        atomicAdd(C + AG_C_CTR_SQERR, to_fx(d * d));
         atomicAdd(C + AG_C_BEST_EV, to_fx(bev[s]));
         atomicAdd(C + AG_C_N_LOGS, to_fx(1.0));
       }
     }
-    (void)it;
   }
 
   if (prm.want_counters) {
@@ -282,6 +386,10 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
     for (int j = tid; j < N * kC; j += kThreads) {
       unsigned long long acc = 0ull;
       for (int r = 0; r < prm.replicas; ++r) acc += s_cnt[(size_t)r * N * kC + j];
+      if (j % kC == AG_C_CTR_BIAS) {  // Oracle: est/true == 1 per won record
+        acc = 0ull;
+        for (int r = 0; r < prm.replicas; ++r) acc += s_cnt[(size_t)r * N * kC + j - AG_C_CTR_BIAS + AG_C_N_WON];
+      }
       prm.partials[(size_t)blockIdx.x * N * kC + j] = (int64_t)acc;
     }
   }
@@ -486,34 +594,44 @@ __global__ __launch_bounds__(kThreads) void k_exp_kat(const double *x, double *y
 // ------------------------------------------------------------------------------------
 typedef void (*SimKernel)(SimParams);
 
-template <int P>
+template <int P, bool PRUNE>
 SimKernel pick_d(int D) {
   switch (D) {
-    case 2: return k_simulate<P, 2>;
-    case 3: return k_simulate<P, 3>;
-    case 4: return k_simulate<P, 4>;
-    case 5: return k_simulate<P, 5>;
-    case 6: return k_simulate<P, 6>;
-    case 7: return k_simulate<P, 7>;
-    case 8: return k_simulate<P, 8>;
-    case 9: return k_simulate<P, 9>;
-    case 11: return k_simulate<P, 11>;
-    case 13: return k_simulate<P, 13>;
-    case 16: return k_simulate<P, 16>;
+    case 2: return k_simulate<P, 2, PRUNE>;
+    case 3: return k_simulate<P, 3, PRUNE>;
+    case 4: return k_simulate<P, 4, PRUNE>;
+    case 5: return k_simulate<P, 5, PRUNE>;
+    case 6: return k_simulate<P, 6, PRUNE>;
+    case 7: return k_simulate<P, 7, PRUNE>;
+    case 8: return k_simulate<P, 8, PRUNE>;
     default: return nullptr;
   }
 }
 
-SimKernel pick_kernel(int P, int D) {
+template <int P>
+SimKernel pick_prune(int D, bool prune) {
+  if (prune) return pick_d<P, true>(D);
+  if (D <= 8) return pick_d<P, false>(D);
+  switch (D) {
+    case 9: return k_simulate<P, 9, false>;
+    case 11: return k_simulate<P, 11, false>;
+    case 13: return k_simulate<P, 13, false>;
+    case 16: return k_simulate<P, 16, false>;
+    default: return nullptr;
+  }
+}
+
+// prune: the f32-screened item search (D <= 8, K <= kPruneMaxK); otherwise exact scan.
+SimKernel pick_kernel(int P, int D, bool prune) {
   switch (P) {
-    case 1: return pick_d<1>(D);
-    case 2: return pick_d<2>(D);
-    case 3: return pick_d<3>(D);
-    case 4: return pick_d<4>(D);
-    case 5: return pick_d<5>(D);
-    case 6: return pick_d<6>(D);
-    case 7: return pick_d<7>(D);
-    case 8: return pick_d<8>(D);
+    case 1: return pick_prune<1>(D, prune);
+    case 2: return pick_prune<2>(D, prune);
+    case 3: return pick_prune<3>(D, prune);
+    case 4: return pick_prune<4>(D, prune);
+    case 5: return pick_prune<5>(D, prune);
+    case 6: return pick_prune<6>(D, prune);
+    case 7: return pick_prune<7>(D, prune);
+    case 8: return pick_prune<8>(D, prune);
     default: return nullptr;
   }
 }
@@ -534,7 +652,9 @@ struct ag_ctx {
   int32_t device;
   ag_shape shape;
   int32_t D;
-  int32_t items_stride, values_stride, replicas;
+  int32_t replicas;
+  int32_t item_search = AG_ITEM_SEARCH_AUTO;
+  bool can_simulate = false;
   double *d_items = nullptr;
   double *d_values = nullptr;
   int64_t *d_partials = nullptr;
@@ -576,26 +696,22 @@ int ag_create(int32_t device, const ag_shape *s, ag_ctx **out) {
   if (s->num_slots != 1)
     return set_error(AG_ERR_UNSUPPORTED, "ag_create: num_slots must be 1 (src/main.py:37)");
   const int D = s->embedding_size + 1;
-  if (s->num_participants > kMaxP || !pick_kernel(s->num_participants, D))
-    return set_error(AG_ERR_UNSUPPORTED,
-                     "ag_create: simulate supports P in [1,%d] and E+1 in {2..9,11,13,16} (P=%d, D=%d)",
-                     kMaxP, s->num_participants, D);
+  if (s->num_participants > 4096)
+    return set_error(AG_ERR_UNSUPPORTED, "ag_create: P=%d > 4096", s->num_participants);
   if (s->obs_embedding_size < 0 || s->obs_embedding_size > s->embedding_size)
     return set_error(AG_ERR_INVALID, "ag_create: obs_embedding_size out of range");
   ag_ctx *c = new ag_ctx();
   c->device = device;
   c->shape = *s;
   c->D = D;
-  c->items_stride = (s->num_items * D) | 1;
-  c->values_stride = s->num_items | 1;
   const int nc = s->num_agents * kC;
   int rep = 16384 / (nc * 8);
   c->replicas = rep < 1 ? 1 : (rep > 16 ? 16 : rep);
-  size_t lds = lds_bytes(s->num_agents, s->num_items, c->items_stride, c->values_stride, c->replicas, 1);
-  if (lds > 160 * 1024) {
-    delete c;
-    return set_error(AG_ERR_UNSUPPORTED, "ag_create: catalogue needs %zu B of LDS (> 160 KiB)", lds);
-  }
+  // simulate needs a kernel for (P, D) and the catalogue in LDS; allocate-only contexts
+  // (any P) do not.
+  const LdsLayout lay = make_layout(s->num_agents, s->num_items, D, c->replicas, true);
+  c->can_simulate = s->num_participants <= kMaxP && pick_kernel(s->num_participants, D, false) &&
+                    lay.total <= 160 * 1024;
   DeviceGuard g(device);
   hipError_t e = hipMalloc(&c->d_items, sizeof(double) * s->num_agents * s->num_items * D);
   if (e == hipSuccess) e = hipMalloc(&c->d_values, sizeof(double) * s->num_agents * s->num_items);
@@ -635,6 +751,19 @@ int ag_set_agent_kinds(ag_ctx *c, const int32_t *alloc_kind, const int32_t *bid_
   return AG_OK;
 }
 
+int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
+  if (!c) return set_error(AG_ERR_INVALID, "ag_set_option: null ctx");
+  switch (option) {
+    case AG_OPT_ITEM_SEARCH:
+      if (value != AG_ITEM_SEARCH_AUTO && value != AG_ITEM_SEARCH_EXACT)
+        return set_error(AG_ERR_INVALID, "ag_set_option: bad item search mode %lld", (long long)value);
+      c->item_search = (int32_t)value;
+      return AG_OK;
+    default:
+      return set_error(AG_ERR_INVALID, "ag_set_option: unknown option %d", option);
+  }
+}
+
 int ag_load_catalog(ag_ctx *c, const double *item_emb, const double *item_val) {
   if (!c || !item_emb || !item_val) return set_error(AG_ERR_INVALID, "ag_load_catalog: null argument");
   DeviceGuard g(c->device);
@@ -672,6 +801,11 @@ int ag_allocate(ag_ctx *c, const double *bids, int64_t B, int32_t *winner, doubl
 int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, int64_t *counters_fx,
                 void *stream) {
   if (!c || !in || !out) return set_error(AG_ERR_INVALID, "ag_simulate: null argument");
+  if (!c->can_simulate)
+    return set_error(AG_ERR_UNSUPPORTED,
+                     "ag_simulate: supports P in [1,%d], E+1 in {2..9,11,13,16} and a catalogue "
+                     "that fits LDS (P=%d, D=%d, N=%d, K=%d)",
+                     kMaxP, c->shape.num_participants, c->D, c->shape.num_agents, c->shape.num_items);
   if (!c->catalog) return set_error(AG_ERR_STATE, "ag_simulate: ag_load_catalog not called");
   if (B < 0) return set_error(AG_ERR_INVALID, "ag_simulate: B < 0");
   if (B == 0) return AG_OK;
@@ -686,24 +820,24 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
                      "(<= %lld auctions per call)",
                      (long long)B, grid, c->partial_blocks,
                      (long long)c->partial_blocks * kMaxAuctionsPerBlock);
+  const int D = c->D;
+  const bool prune = c->item_search == AG_ITEM_SEARCH_AUTO && D <= 8 && s.num_items <= kPruneMaxK;
   SimParams prm;
   prm.B = B;
   prm.N = s.num_agents;
   prm.K = s.num_items;
   prm.E = s.embedding_size;
   prm.mech = s.mechanism;
-  prm.items_stride = c->items_stride;
-  prm.values_stride = c->values_stride;
   prm.replicas = c->replicas;
   prm.want_counters = counters_fx != nullptr;
+  prm.lds = make_layout(s.num_agents, s.num_items, D, c->replicas, prm.want_counters);
   prm.items = c->d_items;
   prm.values = c->d_values;
   prm.in = *in;
   prm.out = *out;
   prm.partials = c->d_partials;
-  SimKernel k = pick_kernel(s.num_participants, c->D);
-  const size_t lds = lds_bytes(s.num_agents, s.num_items, c->items_stride, c->values_stride, c->replicas,
-                               prm.want_counters);
+  SimKernel k = pick_kernel(s.num_participants, D, prune);
+  const size_t lds = (size_t)prm.lds.total;
   hipStream_t st = (hipStream_t)stream;
   if (lds > 64 * 1024)
     AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

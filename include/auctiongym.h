@@ -121,6 +121,19 @@ int ag_destroy(ag_ctx *ctx);
  * allocator/bidder class names). Default: all OracleAllocator + TruthfulBidder. */
 int ag_set_agent_kinds(ag_ctx *ctx, const int32_t *allocator_kind, const int32_t *bidder_kind);
 
+/* Options (ag_set_option). */
+typedef enum ag_option {
+  AG_OPT_ITEM_SEARCH = 0 /* value: ag_item_search */
+} ag_option;
+
+typedef enum ag_item_search {
+  AG_ITEM_SEARCH_AUTO = 0,  /* f32 screen of all K items, exact FP64 re-score of the items
+                               within 2^-10 of the best (same results, bit for bit) */
+  AG_ITEM_SEARCH_EXACT = 1  /* exact FP64 score of every item (the reference's loop) */
+} ag_item_search;
+
+int ag_set_option(ag_ctx *ctx, int32_t option, int64_t value);
+
 /* Item catalogue, host: item_emb [N][K][E+1] (embeddings with the intercept column,
  * src/main.py:60-72) and item_val [N][K]; replaces OracleAllocator.update_item_embeddings
  * (src/BidderAllocation.py:78-79) and Auction.agent2items / agents2item_values. */

@@ -103,10 +103,12 @@ def test_allocate_ragged_and_large(gpu, oracle):
             eng.close()
 
 
+@pytest.mark.parametrize("exact", [False, True], ids=["screened", "exact"])
 @pytest.mark.parametrize("name", CAPTURES)
-def test_simulate_replay_matches_reference(gpu, oracle, name):
+def test_simulate_replay_matches_reference(gpu, oracle, name, exact):
     d, meta, agg = load_capture(name)
     eng = _engine(meta, gpu)
+    eng.set_item_search(exact)
     eng.load_catalog(d["items"], d["values"])
     o = _run(eng, d["ctx"], d["part"], d["u"])
     for mine, ref in (("item", "item"), ("bid", "slot_bid"), ("est_ctr", "slot_est_ctr"),
@@ -182,6 +184,15 @@ def test_full_size_synthetic_batch_bit_exact(gpu, oracle):
     assert np.array_equal(out["best_ev"].cpu().numpy().T, orc["best_ev"])
     assert np.array_equal(out["outcome"].cpu().numpy(), orc["outcome"])
     assert np.array_equal(cnt.cpu().numpy(), orc["counters_fx"])
+    # the exact item scan gives the same bits as the screened search
+    eng.set_item_search(True)
+    out_x = eng.alloc_outputs(B)
+    cnt_x = eng.new_counters()
+    eng.simulate(inp, out_x, cnt_x)
+    for k in out:
+        assert torch.equal(out[k], out_x[k]), k
+    assert torch.equal(cnt, cnt_x)
+    eng.set_item_search(False)
     # batch split invariance: two halves accumulate to the same exact counters
     cnt2 = eng.new_counters()
     for lo, hi in ((0, B // 3), (B // 3, B)):
@@ -272,3 +283,44 @@ def test_empty_batch(gpu):
     w, p, s = eng.allocate(torch.empty((2, 0), dtype=torch.float64, device=gpu))
     assert w.numel() == 0
     eng.close()
+
+
+def test_screened_search_adversarial_catalogues(gpu, oracle):
+    """Catalogues built to stress the f32 screen: exact duplicate items (ties -> first max),
+    near-ties 1 ulp apart, huge embeddings (guard -> exact scan), intercepts so negative
+    that f32 exp overflows, and values differing in the last bits."""
+    import torch
+    from auctiongym_amd.engine import AuctionEngine
+    g = np.random.default_rng(11)
+    N, K, E, P, B = 8, 12, 5, 3, 1 << 18
+    base = np.concatenate([g.normal(0, 1, (N, K, E)), -3.0 - g.random((N, K, 1))], axis=2)
+    values = g.lognormal(0.1, 0.2, (N, K))
+    cats = []
+    c = base.copy(); v = values.copy()
+    c[:, 5] = c[:, 2]; v[:, 5] = v[:, 2]                        # exact duplicates
+    c[:, 7] = c[:, 1]; v[:, 7] = np.nextafter(v[:, 1], 10)      # 1-ulp value near-ties
+    cats.append((c, v))
+    c = base.copy(); c[:4] *= 40.0                               # |a| large: guard path
+    cats.append((c, values))
+    c = base.copy(); c[:, :, -1] = -150.0 - g.random((N, K))     # sigmoid ~ e^-150
+    cats.append((c, values))
+    c = base.copy(); c[:, :, :E] *= 1e-9                         # all items ~ equal z
+    cats.append((c, values * (1 + 1e-15 * g.random((N, K)))))
+    for items, vals in cats:
+        eng = AuctionEngine(N, P, K, E, 4, 0, 1.0)
+        eng.load_catalog(items, vals)
+        inp = eng.alloc_inputs(B)
+        eng.generate(7, 0, inp)
+        out = eng.alloc_outputs(B)
+        cnt = eng.new_counters()
+        eng.simulate(inp, out, cnt)
+        ctx = np.ascontiguousarray(inp["ctx"].cpu().numpy().T)
+        part = np.ascontiguousarray(inp["part"].cpu().numpy().T)
+        u = inp["u"].cpu().numpy()
+        orc = oracle.simulate(0, items, vals, ctx, part, u, nthreads=16)
+        assert np.array_equal(out["item"].cpu().numpy().T, orc["item"])
+        assert np.array_equal(out["bid"].cpu().numpy().T, orc["bid"])
+        assert np.array_equal(out["best_ev"].cpu().numpy().T, orc["best_ev"])
+        assert np.array_equal(out["price"].cpu().numpy(), orc["price"])
+        assert np.array_equal(cnt.cpu().numpy(), orc["counters_fx"])
+        eng.close()
