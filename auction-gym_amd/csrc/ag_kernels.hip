@@ -57,8 +57,9 @@ namespace {
 
 constexpr int kThreads = 256;              // 4 waves of 64 lanes
 constexpr int kC = AG_NUM_COUNTERS;
-constexpr int kMaxAuctionsPerBlock = 8192; // keeps a block's int64 counter partials exact
+constexpr int kMaxAuctionsPerBlock = 65536; // per launch: keeps a replica's int64 sum exact
 constexpr int kMinGrid = 2048;             // 256 CUs x 8
+constexpr int kMaxSimGrid = 2048;          // partial-sum workspace (>= resident blocks)
 constexpr int kMaxP = 8;                   // per-lane slot registers (template range)
 constexpr int kMaxD = 16;
 constexpr double kFxScale = 0x1p36;        // 2^AG_FX_FRAC_BITS
@@ -116,21 +117,39 @@ __device__ __forceinline__ unsigned long long to_fx(double x) {
 
 // LDS carve of k_simulate (all pieces 16-B aligned; offsets in bytes).
 struct LdsLayout {
-  int32_t tab, items, values, items_f, values_f, amax, cnt, total;
+  int32_t tab, items, values, scr, scr_val, amax, cnt, total;
   int32_t items_stride;    // doubles between agents (odd: spreads agents over banks)
   int32_t values_stride;   // doubles
-  int32_t items_f_stride;  // floats between agents ([K][8] rows + 4: 16-B slots spread)
-  int32_t values_f_stride; // floats
+  int32_t scr_stride;      // floats between agents in the screening catalogue
+  int32_t scr_val_stride;  // floats
+  int32_t kpairs;          // item pairs in the screening catalogue (K rounded up to even)
+  int32_t replicas;        // per-lane counter replicas (power of 2, <= 64)
+  int32_t ncnt;            // counter slots held in LDS
 };
 
 __host__ inline int32_t align16(int64_t b) { return (int32_t)((b + 15) & ~(int64_t)15); }
 
-__host__ inline LdsLayout make_layout(int N, int K, int D, int replicas, bool counters) {
+// Counter slots accumulated in LDS for OracleAllocator + TruthfulBidder populations:
+//   0 GROSS, 1 PAID, 2 OVERBID (FirstPrice only: price - second_price == 0 under SP),
+//   3 UNDERBID, 4 BEST_EV, 5 packed counts (n_logs in bits 0-31, n_won in bits 32-63).
+// Derived at write-out: NET = GROSS - PAID (both exact fixed-point sums), CTR_BIAS =
+// N_WON (est/true == 1 for Oracle agents); ALLOC / EST regrets and CTR_SQERR are
+// identically zero for them (estimated CTR == true CTR, best_ev == true_ctr * value).
+constexpr int kOracleSlots = 6;
+enum { kSlotGross = 0, kSlotPaid, kSlotOverbid, kSlotUnderbid, kSlotBestEv, kSlotCounts };
+
+__host__ inline LdsLayout make_layout(int N, int K, int D, bool counters) {
   LdsLayout L;
   L.items_stride = (K * D) | 1;
   L.values_stride = K | 1;
-  L.items_f_stride = K * 8 + 4;
-  L.values_f_stride = K + 1;
+  L.kpairs = (K + 1) / 2;
+  // [pair][dim 0..7][2 items] floats; + 4 floats so agents start on different 16-B slots
+  L.scr_stride = L.kpairs * 16 + 4;
+  L.scr_val_stride = L.kpairs * 2 + 2;
+  L.ncnt = kOracleSlots;
+  int R = 64;
+  while (R > 1 && (int64_t)R * N * L.ncnt * 8 > 32768) R >>= 1;
+  L.replicas = R;
   int64_t b = 0;
   L.tab = 0;
   b += 256 * 8;
@@ -138,95 +157,108 @@ __host__ inline LdsLayout make_layout(int N, int K, int D, int replicas, bool co
   b = L.items + (int64_t)N * L.items_stride * 8;
   L.values = align16(b);
   b = L.values + (int64_t)N * L.values_stride * 8;
-  L.items_f = align16(b);
-  b = L.items_f + (int64_t)N * L.items_f_stride * 4;
-  L.values_f = align16(b);
-  b = L.values_f + (int64_t)N * L.values_f_stride * 4;
+  L.scr = align16(b);
+  b = L.scr + (int64_t)N * L.scr_stride * 4;
+  L.scr_val = align16(b);
+  b = L.scr_val + (int64_t)N * L.scr_val_stride * 4;
   L.amax = align16(b);
   b = L.amax + (int64_t)N * 4;
   L.cnt = align16(b);
-  b = L.cnt + (counters ? (int64_t)replicas * N * kC * 8 : 0);
+  b = L.cnt + (counters ? (int64_t)R * N * L.ncnt * 8 : 0);
   L.total = align16(b);
   return L;
 }
 
 struct SimParams {
-  int64_t B;
-  int32_t N, K, E, mech;
-  int32_t replicas;       // LDS counter replicas (lane % replicas) to cut atomic conflicts
+  int32_t B;              // auctions in this launch (< 2^28: 32-bit SoA indexing)
+  int32_t N, K, mech;
   int32_t want_counters;
   LdsLayout lds;
   const double *items;    // global [N][K][D]
   const double *values;   // global [N][K]
   ag_batch_in in;
   ag_batch_out out;
-  int64_t *partials;      // [grid][N][C]
+  int64_t *partials;      // [grid][N][AG_NUM_COUNTERS]
 };
 
-// Pruning margin of the item search (see select_item). With S = sum_d |a_d x_d| <= 256
-// the f32 score of every item is within eps <= 1.5e-4 (relative) of its exact score, so
-// any item whose exact score is the maximum has f32 score >= max_f32 * (1 - 2 eps / (1 +
-// eps)) > max_f32 * (1 - kPruneDelta): keeping every item above that threshold keeps the
-// exact argmax and all its exact ties.
-constexpr float kPruneDelta = 0x1p-10f;
-constexpr float kPruneMaxS = 256.0f;
-constexpr int kPruneMaxK = 16;
+// Screening margin. The f32 score of item k is v_k / (1 + 2^(z'_k)) with z'_k the f32 dot
+// of the catalogue row pre-scaled by -log2(e). With S = sum_d |a_d x_d| <= kPruneMaxS its
+// relative error is eps <= S 2^-21 (inputs rounded to f32, D <= 8 FMAs) + |z| 2^-23 (exp2
+// argument) + 2^-21 (exp2, add, rcp, mul) < 4.2e-5, so every item whose EXACT score is the
+// maximum has f32 score >= max_f32 (1 - eps)/(1 + eps) > max_f32 (1 - kPruneDelta) with
+// kPruneDelta = 2^-13 = 1.22e-4 > 2 eps: re-scoring every item above that threshold
+// exactly keeps the exact argmax and all its exact ties. Lanes outside the bound (or with
+// a vanishing f32 maximum) re-score every item exactly.
+constexpr float kPruneDelta = 0x1p-13f;
+constexpr float kPruneMaxS = 64.0f;
+constexpr int kMaxKPairs = 8;  // screened search for K <= 16
+constexpr float kNegLog2e = -1.4426950408889634f;
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Agent.select_item (src/Agent.py:29-42) for an OracleAllocator agent: the first k that
 // maximises sigmoid(items_k . x) * value_k, with the reference's exact FP64 arithmetic.
-// PRUNE: a cheap f32 pass scores all K items; only items within kPruneDelta of the f32
-// maximum are re-scored exactly (usually one), in increasing k, so the first-max rule and
-// every bit of the chosen item's CTR / score are the reference's.
+// PRUNE: a packed-f32 pass scores all items two at a time; the f32 leader and any item
+// within kPruneDelta of it are re-scored exactly, so the first-max rule and every bit of
+// the chosen item's CTR / score are the reference's.
 template <int D, bool PRUNE>
 __device__ __forceinline__ int select_item(const double *__restrict__ itm, const double *__restrict__ vv,
-                                           const float *__restrict__ itf, const float *__restrict__ vf,
-                                           float amax, int K, const double (&x)[kMaxD],
-                                           const float (&xf)[8], float xabs, const uint64_t *tab,
+                                           const float *__restrict__ scr, const float *__restrict__ sv,
+                                           float amax, int K, int kpairs, const double (&x)[kMaxD],
+                                           const float (&xf)[kMaxD], float xabs, const uint64_t *tab,
                                            double &ctr_best, double &score_best) {
-  int best = 0;
+  int best = -1;
   double best_s = 0.0, best_c = 0.0;
-  bool have = false;
   auto exact = [&](int k) {
     const double c = agexp::sigmoid(dot_ref<D>(itm + k * D, x), tab);
     const double sc = c * vv[k];
-    if (!have || sc > best_s) {
+    if (best < 0 || sc > best_s || (sc == best_s && k < best)) {
       best = k;
       best_s = sc;
       best_c = c;
-      have = true;
     }
   };
   if constexpr (PRUNE) {
-    float sf[kPruneMaxK];
-    float mx = 0.0f;
+    // f32 screen of one item pair: scores of items 2p, 2p+1 (padding items score 0)
+    auto screen = [&](int p) -> f32x2 {
+      const float *row = scr + p * 16;
+      f32x2 z = {0.0f, 0.0f};
 #pragma unroll
-    for (int k = 0; k < kPruneMaxK; ++k) {
-      if (k < K) {
-        const float4 a0 = *reinterpret_cast<const float4 *>(itf + k * 8);
-        const float4 a1 = *reinterpret_cast<const float4 *>(itf + k * 8 + 4);
-        float z = a0.x * xf[0];
-        z = fmaf(a0.y, xf[1], z);
-        z = fmaf(a0.z, xf[2], z);
-        z = fmaf(a0.w, xf[3], z);
-        z = fmaf(a1.x, xf[4], z);
-        z = fmaf(a1.y, xf[5], z);
-        z = fmaf(a1.z, xf[6], z);
-        z = fmaf(a1.w, xf[7], z);
-        const float sg = __frcp_rn(1.0f + __expf(-z));
-        sf[k] = sg * vf[k];
-        mx = fmaxf(mx, sf[k]);
+      for (int d = 0; d < D; ++d) {
+        const f32x2 a = *reinterpret_cast<const f32x2 *>(row + 2 * d);
+        const f32x2 xd = {xf[d], xf[d]};
+        z = __builtin_elementwise_fma(a, xd, z);
+      }
+      const f32x2 one = {1.0f, 1.0f};
+      const f32x2 t = f32x2{__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)} + one;
+      const f32x2 r = {__builtin_amdgcn_rcpf(t.x), __builtin_amdgcn_rcpf(t.y)};
+      return *reinterpret_cast<const f32x2 *>(sv + 2 * p) * r;
+    };
+    // pass 1: f32 leader kf, its score and the runner-up score
+    float mx = 0.0f, m2 = 0.0f;
+    int kf = 0;
+    for (int p = 0; p < kpairs; ++p) {
+      const f32x2 sc = screen(p);
+      const float lo = fminf(sc.x, sc.y), hi = fmaxf(sc.x, sc.y);
+      const int khi = sc.y > sc.x ? 2 * p + 1 : 2 * p;
+      if (hi > mx) {
+        m2 = fmaxf(mx, lo);
+        mx = hi;
+        kf = khi;
+      } else {
+        m2 = fmaxf(m2, hi);
       }
     }
     const bool ok = (amax * xabs <= kPruneMaxS) && (mx >= 1e-30f);
     const float thr = ok ? mx * (1.0f - kPruneDelta) : -1.0f;
-    uint32_t cand = 0;
-#pragma unroll
-    for (int k = 0; k < kPruneMaxK; ++k)
-      if (k < K && sf[k] >= thr) cand |= 1u << k;
-    while (cand) {
-      const int k = __builtin_ctz(cand);
-      cand &= cand - 1;
-      exact(k);
+    exact(kf);  // the f32 leader: every lane, no divergence
+    if (m2 >= thr) {
+      // near-tie (rare) or unscreenable lane: re-score every other item above thr
+      for (int p = 0; p < kpairs; ++p) {
+        const f32x2 sc = screen(p);
+        if (2 * p != kf && sc.x >= thr) exact(2 * p);
+        if (2 * p + 1 != kf && 2 * p + 1 < K && sc.y >= thr) exact(2 * p + 1);
+      }
     }
   } else {
     for (int k = 0; k < K; ++k) exact(k);
@@ -243,13 +275,13 @@ template <int P, int D, bool PRUNE>
 __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = prm.N, K = prm.K;
-  const int64_t B = prm.B;
-  const LdsLayout &L = prm.lds;
+  const uint32_t B = (uint32_t)prm.B;
+  const LdsLayout L = prm.lds;
   uint64_t *s_tab = reinterpret_cast<uint64_t *>(smem + L.tab);
   double *s_items = reinterpret_cast<double *>(smem + L.items);
   double *s_vals = reinterpret_cast<double *>(smem + L.values);
-  float *s_items_f = reinterpret_cast<float *>(smem + L.items_f);
-  float *s_vals_f = reinterpret_cast<float *>(smem + L.values_f);
+  float *s_scr = reinterpret_cast<float *>(smem + L.scr);
+  float *s_scr_val = reinterpret_cast<float *>(smem + L.scr_val);
   float *s_amax = reinterpret_cast<float *>(smem + L.amax);
   unsigned long long *s_cnt = reinterpret_cast<unsigned long long *>(smem + L.cnt);
 
@@ -262,12 +294,19 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
   for (int i = tid; i < N * K; i += kThreads) {
     const int a = i / K, r = i - a * K;
     s_vals[a * L.values_stride + r] = prm.values[i];
-    s_vals_f[a * L.values_f_stride + r] = (float)prm.values[i];
   }
   if (PRUNE) {
-    for (int i = tid; i < N * K * 8; i += kThreads) {
-      const int a = i / (K * 8), r = i - a * (K * 8), k = r >> 3, d = r & 7;
-      s_items_f[a * L.items_f_stride + r] = d < D ? (float)prm.items[((size_t)a * K + k) * D + d] : 0.0f;
+    // screening rows: [pair p][dim d][item 2p, 2p+1], coefficients * -log2(e); padded
+    // dims and the odd item's partner are 0 (value 0 -> score 0, never the leader)
+    for (int i = tid; i < N * L.kpairs * 16; i += kThreads) {
+      const int a = i / (L.kpairs * 16), r = i - a * (L.kpairs * 16);
+      const int p = r >> 4, d = (r >> 1) & 7, k = 2 * p + (r & 1);
+      const float c = (d < D && k < K) ? (float)prm.items[((size_t)a * K + k) * D + d] : 0.0f;
+      s_scr[a * L.scr_stride + r] = c * kNegLog2e;
+    }
+    for (int i = tid; i < N * L.kpairs * 2; i += kThreads) {
+      const int a = i / (L.kpairs * 2), k = i - a * (L.kpairs * 2);
+      s_scr_val[a * L.scr_val_stride + k] = k < K ? (float)prm.values[(size_t)a * K + k] : 0.0f;
     }
     for (int a = tid; a < N; a += kThreads) {
       float m = 0.0f;
@@ -275,31 +314,30 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
       s_amax[a] = m * 1.001f;
     }
   }
-  const int ncnt = prm.replicas * N * kC;
+  const int R = L.replicas;
   if (prm.want_counters)
-    for (int i = tid; i < ncnt; i += kThreads) s_cnt[i] = 0ull;
+    for (int i = tid; i < R * N * L.ncnt; i += kThreads) s_cnt[i] = 0ull;
   __syncthreads();
 
-  const int rep = tid % prm.replicas;
+  const int rep = tid & (R - 1);
   const ag_batch_in in = prm.in;
   const ag_batch_out out = prm.out;
 
-  for (int64_t base = (int64_t)blockIdx.x * kThreads; base < B; base += (int64_t)gridDim.x * kThreads) {
-    const int64_t i = base + tid;
+  for (uint32_t base = blockIdx.x * kThreads; base < B; base += gridDim.x * kThreads) {
+    const uint32_t i = base + tid;
     if (i >= B) continue;
 
     double x[kMaxD];
-    float xf[8];
+    float xf[kMaxD];
     float xabs = 1.0f;
 #pragma unroll
     for (int e = 0; e < D - 1; ++e) {
-      x[e] = in.ctx[(int64_t)e * B + i];
-      if (e < 8) xf[e] = (float)x[e];
-      xabs += fabsf((float)x[e]);
+      x[e] = in.ctx[e * B + i];
+      xf[e] = (float)x[e];
+      xabs += fabsf(xf[e]);
     }
     x[D - 1] = 1.0;  // intercept (src/Auction.py:33)
-#pragma unroll
-    for (int e = D - 1; e < 8; ++e) xf[e] = e == D - 1 ? 1.0f : 0.0f;
+    xf[D - 1] = 1.0f;
     xabs *= 1.001f;
     const double u = in.u[i];
 
@@ -310,20 +348,20 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
 
 #pragma unroll
     for (int s = 0; s < P; ++s) {
-      const int a = in.part[(int64_t)s * B + i];
+      const int a = in.part[s * B + i];
       ag[s] = a;
       double c, bs;
       const int best = select_item<D, PRUNE>(s_items + a * L.items_stride, s_vals + a * L.values_stride,
-                                             s_items_f + a * L.items_f_stride,
-                                             s_vals_f + a * L.values_f_stride, PRUNE ? s_amax[a] : 0.0f,
-                                             K, x, xf, xabs, s_tab, c, bs);
+                                             s_scr + a * L.scr_stride, s_scr_val + a * L.scr_val_stride,
+                                             PRUNE ? s_amax[a] : 0.0f, K, L.kpairs, x, xf, xabs, s_tab,
+                                             c, bs);
       const double v = s_vals[a * L.values_stride + best];
       const double b = v * c;  // TruthfulBidder.bid
       val[s] = v;
       bid[s] = b;
       ctr[s] = c;   // Oracle: estimated CTR == true CTR, bit for bit
       bev[s] = bs;  // max_k true_CTR_k * value_k
-      const int64_t o = (int64_t)s * B + i;
+      const uint32_t o = s * B + i;
       if (out.item) out.item[o] = best;
       if (out.bid) out.bid[o] = b;
       if (out.est_ctr) out.est_ctr[o] = c;
@@ -355,48 +393,74 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
     if (out.outcome) out.outcome[i] = (uint8_t)oc;
 
     if (prm.want_counters) {
-      // Oracle agents: est == true CTR and best_ev == true_ctr * value bit for bit, so the
-      // allocation / estimation regrets and the CTR error terms are exactly 0 and the CTR
-      // bias term is exactly 1 per won record (N_WON carries it; see ag_simulate).
+      // [slot j][agent a][replica]: lane-private replicas, conflict-free 8-B atomics
+      auto add_raw = [&](int j, int a, unsigned long long v) {
+        atomicAdd(s_cnt + ((size_t)(j * N + a) * R + rep), v);
+      };
 #pragma unroll
       for (int s = 0; s < P; ++s) {
-        unsigned long long *C = s_cnt + ((size_t)rep * N + ag[s]) * kC;
         const bool won = charged && s == w;
         const double lp = charged ? price : 0.0;
-        const double lsp = won ? second : 0.0;
         const double tv = ctr[s] * val[s];
         if (won) {
-          const double last_value = val[s] * (double)oc;
-          atomicAdd(C + AG_C_NET, to_fx(last_value - price));
-          atomicAdd(C + AG_C_GROSS, to_fx(last_value));
-          atomicAdd(C + AG_C_N_WON, to_fx(1.0));
-          atomicAdd(C + AG_C_PAID, to_fx(price));
-          atomicAdd(C + AG_C_OVERBID, to_fx(lp - lsp));
+          add_raw(kSlotGross, ag[s], to_fx(val[s] * (double)oc));
+          add_raw(kSlotPaid, ag[s], to_fx(price));
+          if (prm.mech == AG_FIRST_PRICE) add_raw(kSlotOverbid, ag[s], to_fx(lp - second));
         } else {
-          atomicAdd(C + AG_C_UNDERBID, to_fx((lp - bid[s]) * (double)(lp < tv)));
+          add_raw(kSlotUnderbid, ag[s], to_fx((lp - bid[s]) * (double)(lp < tv)));
         }
-        atomicAdd(C + AG_C_BEST_EV, to_fx(bev[s]));
-        atomicAdd(C + AG_C_N_LOGS, to_fx(1.0));
+        add_raw(kSlotBestEv, ag[s], to_fx(bev[s]));
+        add_raw(kSlotCounts, ag[s], won ? 0x100000001ull : 1ull);
       }
     }
   }
 
   if (prm.want_counters) {
     __syncthreads();
-    for (int j = tid; j < N * kC; j += kThreads) {
-      unsigned long long acc = 0ull;
-      for (int r = 0; r < prm.replicas; ++r) acc += s_cnt[(size_t)r * N * kC + j];
-      if (j % kC == AG_C_CTR_BIAS) {  // Oracle: est/true == 1 per won record
-        acc = 0ull;
-        for (int r = 0; r < prm.replicas; ++r) acc += s_cnt[(size_t)r * N * kC + j - AG_C_CTR_BIAS + AG_C_N_WON];
+    for (int a = tid; a < N; a += kThreads) {
+      long long lo[kOracleSlots], hi[kOracleSlots];
+      unsigned long long nlogs = 0, nwon = 0;
+      for (int j = 0; j < kOracleSlots; ++j) {
+        lo[j] = 0;
+        hi[j] = 0;
+        for (int r = 0; r < R; ++r) {
+          const unsigned long long c = s_cnt[(size_t)(j * N + a) * R + r];
+          if (j == kSlotCounts) {
+            nlogs += c & 0xffffffffull;
+            nwon += c >> 32;
+          } else {
+            lo[j] += (long long)c & kLimbMask;
+            hi[j] += (long long)c >> AG_FX_LIMB_BITS;
+          }
+        }
       }
-      prm.partials[(size_t)blockIdx.x * N * kC + j] = (int64_t)acc;
+      // two limbs per counter (value = lo + hi * 2^42): no block total can overflow
+      int64_t *dst = prm.partials + ((size_t)blockIdx.x * N + a) * kC * 2;
+      auto put = [&](int c, long long lo, long long hi) {
+        dst[2 * c] = lo;
+        dst[2 * c + 1] = hi;
+      };
+      auto put_count = [&](int c, unsigned long long n) {
+        put(c, (long long)((n & 63ull) << AG_FX_FRAC_BITS), (long long)(n >> 6));
+      };
+      put(AG_C_NET, lo[kSlotGross] - lo[kSlotPaid], hi[kSlotGross] - hi[kSlotPaid]);
+      put(AG_C_GROSS, lo[kSlotGross], hi[kSlotGross]);
+      put(AG_C_ALLOC_REGRET, 0, 0);
+      put(AG_C_EST_REGRET, 0, 0);
+      put(AG_C_OVERBID, lo[kSlotOverbid], hi[kSlotOverbid]);
+      put(AG_C_UNDERBID, lo[kSlotUnderbid], hi[kSlotUnderbid]);
+      put(AG_C_CTR_SQERR, 0, 0);
+      put_count(AG_C_CTR_BIAS, nwon);
+      put(AG_C_BEST_EV, lo[kSlotBestEv], hi[kSlotBestEv]);
+      put_count(AG_C_N_LOGS, nlogs);
+      put_count(AG_C_N_WON, nwon);
+      put(AG_C_PAID, lo[kSlotPaid], hi[kSlotPaid]);
     }
   }
 }
 
-// Sum the per-block partials of one counter exactly into its limbs (one block per
-// (agent, counter)). Integer sums: any order gives the same bits.
+// Sum the per-block partials (two limbs each) of one counter exactly into its limbs
+// (one block per (agent, counter)). Integer sums: any order gives the same bits.
 __global__ __launch_bounds__(kThreads) void k_reduce_counters(const int64_t *__restrict__ partials,
                                                               int nblocks, int ncounters,
                                                               int64_t *__restrict__ limbs) {
@@ -404,9 +468,8 @@ __global__ __launch_bounds__(kThreads) void k_reduce_counters(const int64_t *__r
   const int j = blockIdx.x;
   long long a0 = 0, a1 = 0;
   for (int b = threadIdx.x; b < nblocks; b += kThreads) {
-    const long long p = partials[(size_t)b * ncounters + j];
-    a0 += p & kLimbMask;
-    a1 += p >> AG_FX_LIMB_BITS;
+    a0 += partials[((size_t)b * ncounters + j) * 2];
+    a1 += partials[((size_t)b * ncounters + j) * 2 + 1];
   }
   s0[threadIdx.x] = a0;
   s1[threadIdx.x] = a1;
@@ -652,13 +715,13 @@ struct ag_ctx {
   int32_t device;
   ag_shape shape;
   int32_t D;
-  int32_t replicas;
   int32_t item_search = AG_ITEM_SEARCH_AUTO;
   bool can_simulate = false;
   double *d_items = nullptr;
   double *d_values = nullptr;
   int64_t *d_partials = nullptr;
   int32_t partial_blocks = 0;
+  int32_t resident[4] = {0, 0, 0, 0};  // resident k_simulate blocks [screened][counters]
   bool catalog = false;
 };
 
@@ -705,11 +768,9 @@ int ag_create(int32_t device, const ag_shape *s, ag_ctx **out) {
   c->shape = *s;
   c->D = D;
   const int nc = s->num_agents * kC;
-  int rep = 16384 / (nc * 8);
-  c->replicas = rep < 1 ? 1 : (rep > 16 ? 16 : rep);
   // simulate needs a kernel for (P, D) and the catalogue in LDS; allocate-only contexts
   // (any P) do not.
-  const LdsLayout lay = make_layout(s->num_agents, s->num_items, D, c->replicas, true);
+  const LdsLayout lay = make_layout(s->num_agents, s->num_items, D, true);
   c->can_simulate = s->num_participants <= kMaxP && pick_kernel(s->num_participants, D, false) &&
                     lay.total <= 160 * 1024;
   DeviceGuard g(device);
@@ -717,8 +778,8 @@ int ag_create(int32_t device, const ag_shape *s, ag_ctx **out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_values, sizeof(double) * s->num_agents * s->num_items);
   // partials for the largest grid a call can use: grids grow past kMinGrid only to keep
   // <= kMaxAuctionsPerBlock auctions per block; allocate lazily beyond the default.
-  c->partial_blocks = kMinGrid;
-  if (e == hipSuccess) e = hipMalloc(&c->d_partials, sizeof(int64_t) * (size_t)kMinGrid * nc);
+  c->partial_blocks = kMaxSimGrid;
+  if (e == hipSuccess) e = hipMalloc(&c->d_partials, sizeof(int64_t) * 2 * (size_t)kMaxSimGrid * nc);
   if (e != hipSuccess) {
     (void)hipFree(c->d_items);
     (void)hipFree(c->d_values);
@@ -810,27 +871,21 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   if (B < 0) return set_error(AG_ERR_INVALID, "ag_simulate: B < 0");
   if (B == 0) return AG_OK;
   if (!in->ctx || !in->part || !in->u) return set_error(AG_ERR_INVALID, "ag_simulate: null input array");
+  if (B * c->shape.num_participants > INT32_MAX)
+    return set_error(AG_ERR_UNSUPPORTED, "ag_simulate: B * P must be < 2^31 (32-bit SoA indexing); "
+                     "split the batch");
   DeviceGuard g(c->device);
   const ag_shape &s = c->shape;
   const int nc = s.num_agents * kC;
-  const int grid = grid_for(B, kMaxAuctionsPerBlock);
-  if (counters_fx && grid > c->partial_blocks)
-    return set_error(AG_ERR_UNSUPPORTED,
-                     "ag_simulate: B=%lld needs %d blocks > %d of workspace; split the batch "
-                     "(<= %lld auctions per call)",
-                     (long long)B, grid, c->partial_blocks,
-                     (long long)c->partial_blocks * kMaxAuctionsPerBlock);
   const int D = c->D;
-  const bool prune = c->item_search == AG_ITEM_SEARCH_AUTO && D <= 8 && s.num_items <= kPruneMaxK;
+  const bool prune = c->item_search == AG_ITEM_SEARCH_AUTO && D <= 8 && s.num_items <= 2 * kMaxKPairs;
   SimParams prm;
   prm.B = B;
   prm.N = s.num_agents;
   prm.K = s.num_items;
-  prm.E = s.embedding_size;
   prm.mech = s.mechanism;
-  prm.replicas = c->replicas;
   prm.want_counters = counters_fx != nullptr;
-  prm.lds = make_layout(s.num_agents, s.num_items, D, c->replicas, prm.want_counters);
+  prm.lds = make_layout(s.num_agents, s.num_items, D, prm.want_counters);
   prm.items = c->d_items;
   prm.values = c->d_values;
   prm.in = *in;
@@ -841,6 +896,22 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   hipStream_t st = (hipStream_t)stream;
   if (lds > 64 * 1024)
     AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  // Persistent grid: exactly the blocks the device keeps resident (no partial last round),
+  // each striding over 256-auction tiles.
+  int &res = c->resident[(prune ? 2 : 0) + (prm.want_counters ? 1 : 0)];
+  if (res == 0) {
+    int per_cu = 0, cus = 0;
+    AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k, kThreads, lds));
+    AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    res = per_cu * cus;
+    if (res < 1) res = 1;
+    if (res > c->partial_blocks) res = c->partial_blocks;
+  }
+  const int64_t tiles = (B + kThreads - 1) / kThreads;
+  const int grid = (int)(tiles < res ? tiles : res);
+  if (B > (int64_t)grid * kMaxAuctionsPerBlock)
+    return set_error(AG_ERR_UNSUPPORTED, "ag_simulate: B=%lld > %lld auctions per call; split the batch",
+                     (long long)B, (long long)grid * kMaxAuctionsPerBlock);
   hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), lds, st, prm);
   AG_HIP(hipGetLastError());
   if (counters_fx) {

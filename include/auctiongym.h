@@ -72,7 +72,9 @@ typedef enum ag_counter {
  * to a multiple of 2^-AG_FX_FRAC_BITS and the sum is held in AG_FX_LIMBS int64 limbs of
  * AG_FX_LIMB_BITS bits (value = sum_j limb_j * 2^(j*AG_FX_LIMB_BITS - AG_FX_FRAC_BITS)),
  * so results are independent of grid size, block order, batch split and GPU count.
- * Limb arrays can be summed across GPUs with an int64 all-reduce and then normalised. */
+ * Limb arrays can be summed across GPUs with an int64 all-reduce and then normalised.
+ * AG_C_NET is held as AG_C_GROSS - AG_C_PAID (each record's net term value*outcome -
+ * price is then rounded as two terms). */
 #define AG_FX_FRAC_BITS 36
 #define AG_FX_LIMB_BITS 42
 #define AG_FX_LIMBS 3

@@ -221,6 +221,8 @@ static void simulate_range(const ora_shape *sh, const double *items, const doubl
       if (fx) {
         __int128 *F = fx + (int64_t)a * ORA_NUM_COUNTERS;
         for (int c = 0; c < ORA_NUM_COUNTERS; ++c) F[c] += ora_to_fx(t[c]);
+        /* fixed-point NET is defined as GROSS - PAID (include/auctiongym.h) */
+        F[ORA_C_NET] += -ora_to_fx(t[ORA_C_NET]) + ora_to_fx(t[ORA_C_GROSS]) - ora_to_fx(t[ORA_C_PAID]);
       }
     }
   }
