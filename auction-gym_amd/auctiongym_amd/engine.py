@@ -10,7 +10,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import AgBatchIn, AgBatchOut, AgShape, check
+from ._lib import AgBatchIn, AgBatchOut, AgShape
+from ._lib import check as _check
 
 COUNTERS = _lib.COUNTERS
 NUM_COUNTERS = _lib.NUM_COUNTERS
@@ -38,9 +39,9 @@ class AuctionEngine:
     """Batched Auction.simulate_opportunity for N agents, P participants, K items, E dims."""
 
     def __init__(self, num_agents, num_participants, num_items, embedding_size,
-                 obs_embedding_size, mechanism, embedding_var=1.0, device=None):
+                 obs_embedding_size, mechanism, embedding_var=1.0, device=None, lib_path=None):
         require_gpu()
-        self.L = _lib.load()
+        self.L = _lib.load(lib_path)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         self.N, self.P, self.K = int(num_agents), int(num_participants), int(num_items)
         self.E, self.OE = int(embedding_size), int(obs_embedding_size)
@@ -51,9 +52,12 @@ class AuctionEngine:
                         self.embedding_var)
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            check(self.L.ag_create(self.device.index, ctypes.byref(shape), ctypes.byref(h)),
+            self._check(self.L.ag_create(self.device.index, ctypes.byref(shape), ctypes.byref(h)),
                   "ag_create")
         self._h = h
+
+    def _check(self, rc, what):
+        _check(rc, what, self.L)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -71,13 +75,18 @@ class AuctionEngine:
         a = np.ascontiguousarray(allocator_kinds, np.int32)
         b = np.ascontiguousarray(bidder_kinds, np.int32)
         assert a.shape == (self.N,) and b.shape == (self.N,)
-        check(self.L.ag_set_agent_kinds(self._h, a.ctypes.data, b.ctypes.data), "ag_set_agent_kinds")
+        self._check(self.L.ag_set_agent_kinds(self._h, a.ctypes.data, b.ctypes.data), "ag_set_agent_kinds")
 
     def set_item_search(self, exact):
         """exact=True: score every item in FP64 (the reference loop); False (default): f32
         screen + exact re-score of the near-best items -- identical results."""
         mode = _lib.ITEM_SEARCH_EXACT if exact else _lib.ITEM_SEARCH_AUTO
-        check(self.L.ag_set_option(self._h, _lib.OPT_ITEM_SEARCH, mode), "ag_set_option")
+        self._check(self.L.ag_set_option(self._h, _lib.OPT_ITEM_SEARCH, mode), "ag_set_option")
+
+    def set_lane_auctions(self, n):
+        """Auctions per lane in the screened kernel: 2 (default; 16-B SoA accesses when B
+        is even) or 1. Same results either way."""
+        self._check(self.L.ag_set_option(self._h, _lib.OPT_LANE_AUCTIONS, int(n)), "ag_set_option")
 
     def load_catalog(self, items, values):
         items = np.ascontiguousarray(items, np.float64)
@@ -85,7 +94,7 @@ class AuctionEngine:
         if items.shape != (self.N, self.K, self.D) or values.shape != (self.N, self.K):
             raise ValueError(f"catalogue shapes {items.shape}/{values.shape} != "
                              f"({self.N},{self.K},{self.D})/({self.N},{self.K})")
-        check(self.L.ag_load_catalog(self._h, items.ctypes.data, values.ctypes.data),
+        self._check(self.L.ag_load_catalog(self._h, items.ctypes.data, values.ctypes.data),
               "ag_load_catalog")
 
     # ---------------------------------------------------------------- buffers
@@ -117,12 +126,12 @@ class AuctionEngine:
             raise ValueError("inputs must be SoA: ctx [E][B], part [P][B], u [B]")
         bi = AgBatchIn(_ptr(inputs["ctx"]).value, _ptr(inputs["part"]).value, _ptr(inputs["u"]).value)
         bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
-        check(self.L.ag_simulate(self._h, B, ctypes.byref(bi), ctypes.byref(bo),
+        self._check(self.L.ag_simulate(self._h, B, ctypes.byref(bi), ctypes.byref(bo),
                                  _ptr(counters), _stream()), "ag_simulate")
 
     def generate(self, seed, first_auction, inputs):
         B = inputs["u"].shape[0]
-        check(self.L.ag_generate(self._h, int(seed), int(first_auction), B, _ptr(inputs["ctx"]),
+        self._check(self.L.ag_generate(self._h, int(seed), int(first_auction), B, _ptr(inputs["ctx"]),
                                  _ptr(inputs["part"]), _ptr(inputs["u"]), _stream()), "ag_generate")
 
     def allocate(self, bids):
@@ -134,7 +143,7 @@ class AuctionEngine:
         w = torch.empty(B, dtype=torch.int32, device=self.device)
         p = torch.empty(B, dtype=torch.float64, device=self.device)
         s = torch.empty(B, dtype=torch.float64, device=self.device)
-        check(self.L.ag_allocate(self._h, _ptr(bids), B, _ptr(w), _ptr(p), _ptr(s), _stream()),
+        self._check(self.L.ag_allocate(self._h, _ptr(bids), B, _ptr(w), _ptr(p), _ptr(s), _stream()),
               "ag_allocate")
         return w, p, s
 
@@ -146,8 +155,8 @@ class AuctionEngine:
         fx = np.ascontiguousarray(fx, np.int64)
         n = fx.size // FX_LIMBS
         out = np.empty(n, np.float64)
-        check(_lib.load().ag_counters_to_double(fx.ctypes.data, n, out.ctypes.data),
-              "ag_counters_to_double")
+        _check(_lib.load().ag_counters_to_double(fx.ctypes.data, n, out.ctypes.data),
+               "ag_counters_to_double")
         return out.reshape(fx.shape[:-1])
 
 
@@ -158,5 +167,5 @@ def device_exp(x, sigmoid=False):
     x = x.contiguous()
     y = torch.empty_like(x)
     f = L.ag_sigmoid if sigmoid else L.ag_exp
-    check(f(_ptr(x), _ptr(y), x.numel(), _stream()), "ag_exp")
+    _check(f(_ptr(x), _ptr(y), x.numel(), _stream()), "ag_exp")
     return y

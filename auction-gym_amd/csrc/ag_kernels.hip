@@ -25,9 +25,7 @@
 
 #include <string>
 
-#include "auctiongym.h"
-#include "ag_exp.h"
-#include "ag_exp_table.h"
+#include "ag_sim.h"
 
 // ------------------------------------------------------------------------------------
 // error plumbing
@@ -54,410 +52,7 @@ static int set_error(int code, const char *fmt, ...) {
   } while (0)
 
 namespace {
-
-constexpr int kThreads = 256;              // 4 waves of 64 lanes
-constexpr int kC = AG_NUM_COUNTERS;
-constexpr int kMaxAuctionsPerBlock = 65536; // per launch: keeps a replica's int64 sum exact
-constexpr int kMinGrid = 2048;             // 256 CUs x 8
-constexpr int kMaxSimGrid = 2048;          // partial-sum workspace (>= resident blocks)
-constexpr int kMaxP = 8;                   // per-lane slot registers (template range)
-constexpr int kMaxD = 16;
-constexpr double kFxScale = 0x1p36;        // 2^AG_FX_FRAC_BITS
-constexpr double kMagic = 0x1.8p52;
-constexpr int64_t kLimbMask = (int64_t(1) << AG_FX_LIMB_BITS) - 1;
-
-// ------------------------------------------------------------------------------------
-// reference arithmetic
-// ------------------------------------------------------------------------------------
-
-// numpy `items @ ctx` -> OpenBLAS dgemv_t (SURVEY §8 a5'; oracle/ag_oracle.c ora_dot):
-// rows in blocks of 4 with one FMA accumulator per lane, lanes reduced (l0+l2)+(l1+l3),
-// 1-3 tail rows added by contracted scalar code. `a` is in LDS, `x` in registers.
-template <int D>
-__device__ __forceinline__ double dot_ref(const double *__restrict__ a, const double (&x)[kMaxD]) {
-  constexpr int m3 = D & 3, m1 = D - m3;
-  double y = 0.0;
-  if constexpr (m1 > 0) {
-    double l0 = 0.0, l1 = 0.0, l2 = 0.0, l3 = 0.0;
-#pragma unroll
-    for (int i = 0; i < m1; i += 4) {
-      l0 = fma(a[i + 0], x[i + 0], l0);
-      l1 = fma(a[i + 1], x[i + 1], l1);
-      l2 = fma(a[i + 2], x[i + 2], l2);
-      l3 = fma(a[i + 3], x[i + 3], l3);
-    }
-    y = (l0 + l2) + (l1 + l3);
-  }
-  if constexpr (m3 == 1) y = fma(a[m1], x[m1], y);
-  if constexpr (m3 == 2) y = y + fma(a[m1], x[m1], a[m1 + 1] * x[m1 + 1]);
-  if constexpr (m3 == 3)
-    y = y + fma(a[m1 + 2], x[m1 + 2], fma(a[m1], x[m1], a[m1 + 1] * x[m1 + 1]));
-  return y;
-}
-
-// numpy Generator.binomial(1, p) from its single next_double U (src/Auction.py:65;
-// numpy's inversion sampler for n = 1). The sampler compares U with exp(log(1 - p)); this
-// uses 1 - p (resp. p), which differs from it by at most one ulp: the outcome can differ
-// only when U lands on that ulp, probability <= 2^-53 per auction.
-__device__ __forceinline__ int bernoulli(double p, double u) {
-  if (p == 0.0) return 0;
-  if (p <= 0.5) return u > (1.0 - p) ? 1 : 0;
-  return u > p ? 0 : 1;
-}
-
-// Round x * 2^36 to the nearest integer (ties-to-even), exactly.
-__device__ __forceinline__ unsigned long long to_fx(double x) {
-  if (fabs(x) < 0x1p14) {
-    double y = fma(x, kFxScale, kMagic);
-    return (unsigned long long)(__double_as_longlong(y) - __double_as_longlong(kMagic));
-  }
-  if (!(fabs(x) < 0x1p26)) return 0ull;  // non-finite / absurd term: dropped
-  return (unsigned long long)(long long)rint(x * kFxScale);
-}
-
-// LDS carve of k_simulate (all pieces 16-B aligned; offsets in bytes).
-struct LdsLayout {
-  int32_t tab, items, values, scr, scr_val, amax, cnt, total;
-  int32_t items_stride;    // doubles between agents (odd: spreads agents over banks)
-  int32_t values_stride;   // doubles
-  int32_t scr_stride;      // floats between agents in the screening catalogue
-  int32_t scr_val_stride;  // floats
-  int32_t kpairs;          // item pairs in the screening catalogue (K rounded up to even)
-  int32_t replicas;        // per-lane counter replicas (power of 2, <= 64)
-  int32_t ncnt;            // counter slots held in LDS
-};
-
-__host__ inline int32_t align16(int64_t b) { return (int32_t)((b + 15) & ~(int64_t)15); }
-
-// Counter slots accumulated in LDS for OracleAllocator + TruthfulBidder populations:
-//   0 GROSS, 1 PAID, 2 OVERBID (FirstPrice only: price - second_price == 0 under SP),
-//   3 UNDERBID, 4 BEST_EV, 5 packed counts (n_logs in bits 0-31, n_won in bits 32-63).
-// Derived at write-out: NET = GROSS - PAID (both exact fixed-point sums), CTR_BIAS =
-// N_WON (est/true == 1 for Oracle agents); ALLOC / EST regrets and CTR_SQERR are
-// identically zero for them (estimated CTR == true CTR, best_ev == true_ctr * value).
-constexpr int kOracleSlots = 6;
-enum { kSlotGross = 0, kSlotPaid, kSlotOverbid, kSlotUnderbid, kSlotBestEv, kSlotCounts };
-
-__host__ inline LdsLayout make_layout(int N, int K, int D, bool counters) {
-  LdsLayout L;
-  L.items_stride = (K * D) | 1;
-  L.values_stride = K | 1;
-  L.kpairs = (K + 1) / 2;
-  // [pair][dim 0..7][2 items] floats; + 4 floats so agents start on different 16-B slots
-  L.scr_stride = L.kpairs * 16 + 4;
-  L.scr_val_stride = L.kpairs * 2 + 2;
-  L.ncnt = kOracleSlots;
-  int R = 64;
-  while (R > 1 && (int64_t)R * N * L.ncnt * 8 > 32768) R >>= 1;
-  L.replicas = R;
-  int64_t b = 0;
-  L.tab = 0;
-  b += 256 * 8;
-  L.items = align16(b);
-  b = L.items + (int64_t)N * L.items_stride * 8;
-  L.values = align16(b);
-  b = L.values + (int64_t)N * L.values_stride * 8;
-  L.scr = align16(b);
-  b = L.scr + (int64_t)N * L.scr_stride * 4;
-  L.scr_val = align16(b);
-  b = L.scr_val + (int64_t)N * L.scr_val_stride * 4;
-  L.amax = align16(b);
-  b = L.amax + (int64_t)N * 4;
-  L.cnt = align16(b);
-  b = L.cnt + (counters ? (int64_t)R * N * L.ncnt * 8 : 0);
-  L.total = align16(b);
-  return L;
-}
-
-struct SimParams {
-  int32_t B;              // auctions in this launch (< 2^28: 32-bit SoA indexing)
-  int32_t N, K, mech;
-  int32_t want_counters;
-  LdsLayout lds;
-  const double *items;    // global [N][K][D]
-  const double *values;   // global [N][K]
-  ag_batch_in in;
-  ag_batch_out out;
-  int64_t *partials;      // [grid][N][AG_NUM_COUNTERS]
-};
-
-// Screening margin. The f32 score of item k is v_k / (1 + 2^(z'_k)) with z'_k the f32 dot
-// of the catalogue row pre-scaled by -log2(e). With S = sum_d |a_d x_d| <= kPruneMaxS its
-// relative error is eps <= S 2^-21 (inputs rounded to f32, D <= 8 FMAs) + |z| 2^-23 (exp2
-// argument) + 2^-21 (exp2, add, rcp, mul) < 4.2e-5, so every item whose EXACT score is the
-// maximum has f32 score >= max_f32 (1 - eps)/(1 + eps) > max_f32 (1 - kPruneDelta) with
-// kPruneDelta = 2^-13 = 1.22e-4 > 2 eps: re-scoring every item above that threshold
-// exactly keeps the exact argmax and all its exact ties. Lanes outside the bound (or with
-// a vanishing f32 maximum) re-score every item exactly.
-constexpr float kPruneDelta = 0x1p-13f;
-constexpr float kPruneMaxS = 64.0f;
-constexpr int kMaxKPairs = 8;  // screened search for K <= 16
-constexpr float kNegLog2e = -1.4426950408889634f;
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-// Agent.select_item (src/Agent.py:29-42) for an OracleAllocator agent: the first k that
-// maximises sigmoid(items_k . x) * value_k, with the reference's exact FP64 arithmetic.
-// PRUNE: a packed-f32 pass scores all items two at a time; the f32 leader and any item
-// within kPruneDelta of it are re-scored exactly, so the first-max rule and every bit of
-// the chosen item's CTR / score are the reference's.
-template <int D, bool PRUNE>
-__device__ __forceinline__ int select_item(const double *__restrict__ itm, const double *__restrict__ vv,
-                                           const float *__restrict__ scr, const float *__restrict__ sv,
-                                           float amax, int K, int kpairs, const double (&x)[kMaxD],
-                                           const float (&xf)[kMaxD], float xabs, const uint64_t *tab,
-                                           double &ctr_best, double &score_best) {
-  int best = -1;
-  double best_s = 0.0, best_c = 0.0;
-  auto exact = [&](int k) {
-    const double c = agexp::sigmoid(dot_ref<D>(itm + k * D, x), tab);
-    const double sc = c * vv[k];
-    if (best < 0 || sc > best_s || (sc == best_s && k < best)) {
-      best = k;
-      best_s = sc;
-      best_c = c;
-    }
-  };
-  if constexpr (PRUNE) {
-    // f32 screen of one item pair: scores of items 2p, 2p+1 (padding items score 0)
-    auto screen = [&](int p) -> f32x2 {
-      const float *row = scr + p * 16;
-      f32x2 z = {0.0f, 0.0f};
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const f32x2 a = *reinterpret_cast<const f32x2 *>(row + 2 * d);
-        const f32x2 xd = {xf[d], xf[d]};
-        z = __builtin_elementwise_fma(a, xd, z);
-      }
-      const f32x2 one = {1.0f, 1.0f};
-      const f32x2 t = f32x2{__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)} + one;
-      const f32x2 r = {__builtin_amdgcn_rcpf(t.x), __builtin_amdgcn_rcpf(t.y)};
-      return *reinterpret_cast<const f32x2 *>(sv + 2 * p) * r;
-    };
-    // pass 1: f32 leader kf, its score and the runner-up score
-    float mx = 0.0f, m2 = 0.0f;
-    int kf = 0;
-    for (int p = 0; p < kpairs; ++p) {
-      const f32x2 sc = screen(p);
-      const float lo = fminf(sc.x, sc.y), hi = fmaxf(sc.x, sc.y);
-      const int khi = sc.y > sc.x ? 2 * p + 1 : 2 * p;
-      if (hi > mx) {
-        m2 = fmaxf(mx, lo);
-        mx = hi;
-        kf = khi;
-      } else {
-        m2 = fmaxf(m2, hi);
-      }
-    }
-    const bool ok = (amax * xabs <= kPruneMaxS) && (mx >= 1e-30f);
-    const float thr = ok ? mx * (1.0f - kPruneDelta) : -1.0f;
-    exact(kf);  // the f32 leader: every lane, no divergence
-    if (m2 >= thr) {
-      // near-tie (rare) or unscreenable lane: re-score every other item above thr
-      for (int p = 0; p < kpairs; ++p) {
-        const f32x2 sc = screen(p);
-        if (2 * p != kf && sc.x >= thr) exact(2 * p);
-        if (2 * p + 1 != kf && 2 * p + 1 < K && sc.y >= thr) exact(2 * p + 1);
-      }
-    }
-  } else {
-    for (int k = 0; k < K; ++k) exact(k);
-  }
-  ctr_best = best_c;
-  score_best = best_s;
-  return best;
-}
-
-// ------------------------------------------------------------------------------------
-// fused simulate kernel
-// ------------------------------------------------------------------------------------
-template <int P, int D, bool PRUNE>
-__global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int N = prm.N, K = prm.K;
-  const uint32_t B = (uint32_t)prm.B;
-  const LdsLayout L = prm.lds;
-  uint64_t *s_tab = reinterpret_cast<uint64_t *>(smem + L.tab);
-  double *s_items = reinterpret_cast<double *>(smem + L.items);
-  double *s_vals = reinterpret_cast<double *>(smem + L.values);
-  float *s_scr = reinterpret_cast<float *>(smem + L.scr);
-  float *s_scr_val = reinterpret_cast<float *>(smem + L.scr_val);
-  float *s_amax = reinterpret_cast<float *>(smem + L.amax);
-  unsigned long long *s_cnt = reinterpret_cast<unsigned long long *>(smem + L.cnt);
-
-  const int tid = threadIdx.x;
-  for (int i = tid; i < 256; i += kThreads) s_tab[i] = ag_exp_tab[i];
-  for (int i = tid; i < N * K * D; i += kThreads) {
-    const int a = i / (K * D), r = i - a * (K * D);
-    s_items[a * L.items_stride + r] = prm.items[i];
-  }
-  for (int i = tid; i < N * K; i += kThreads) {
-    const int a = i / K, r = i - a * K;
-    s_vals[a * L.values_stride + r] = prm.values[i];
-  }
-  if (PRUNE) {
-    // screening rows: [pair p][dim d][item 2p, 2p+1], coefficients * -log2(e); padded
-    // dims and the odd item's partner are 0 (value 0 -> score 0, never the leader)
-    for (int i = tid; i < N * L.kpairs * 16; i += kThreads) {
-      const int a = i / (L.kpairs * 16), r = i - a * (L.kpairs * 16);
-      const int p = r >> 4, d = (r >> 1) & 7, k = 2 * p + (r & 1);
-      const float c = (d < D && k < K) ? (float)prm.items[((size_t)a * K + k) * D + d] : 0.0f;
-      s_scr[a * L.scr_stride + r] = c * kNegLog2e;
-    }
-    for (int i = tid; i < N * L.kpairs * 2; i += kThreads) {
-      const int a = i / (L.kpairs * 2), k = i - a * (L.kpairs * 2);
-      s_scr_val[a * L.scr_val_stride + k] = k < K ? (float)prm.values[(size_t)a * K + k] : 0.0f;
-    }
-    for (int a = tid; a < N; a += kThreads) {
-      float m = 0.0f;
-      for (int r = 0; r < K * D; ++r) m = fmaxf(m, (float)fabs(prm.items[(size_t)a * K * D + r]));
-      s_amax[a] = m * 1.001f;
-    }
-  }
-  const int R = L.replicas;
-  if (prm.want_counters)
-    for (int i = tid; i < R * N * L.ncnt; i += kThreads) s_cnt[i] = 0ull;
-  __syncthreads();
-
-  const int rep = tid & (R - 1);
-  const ag_batch_in in = prm.in;
-  const ag_batch_out out = prm.out;
-
-  for (uint32_t base = blockIdx.x * kThreads; base < B; base += gridDim.x * kThreads) {
-    const uint32_t i = base + tid;
-    if (i >= B) continue;
-
-    double x[kMaxD];
-    float xf[kMaxD];
-    float xabs = 1.0f;
-#pragma unroll
-    for (int e = 0; e < D - 1; ++e) {
-      x[e] = in.ctx[e * B + i];
-      xf[e] = (float)x[e];
-      xabs += fabsf(xf[e]);
-    }
-    x[D - 1] = 1.0;  // intercept (src/Auction.py:33)
-    xf[D - 1] = 1.0f;
-    xabs *= 1.001f;
-    const double u = in.u[i];
-
-    int ag[P];
-    double val[P], bid[P], ctr[P], bev[P];
-    int w = 0;
-    double m1 = 0.0, m2 = -INFINITY;
-
-#pragma unroll
-    for (int s = 0; s < P; ++s) {
-      const int a = in.part[s * B + i];
-      ag[s] = a;
-      double c, bs;
-      const int best = select_item<D, PRUNE>(s_items + a * L.items_stride, s_vals + a * L.values_stride,
-                                             s_scr + a * L.scr_stride, s_scr_val + a * L.scr_val_stride,
-                                             PRUNE ? s_amax[a] : 0.0f, K, L.kpairs, x, xf, xabs, s_tab,
-                                             c, bs);
-      const double v = s_vals[a * L.values_stride + best];
-      const double b = v * c;  // TruthfulBidder.bid
-      val[s] = v;
-      bid[s] = b;
-      ctr[s] = c;   // Oracle: estimated CTR == true CTR, bit for bit
-      bev[s] = bs;  // max_k true_CTR_k * value_k
-      const uint32_t o = s * B + i;
-      if (out.item) out.item[o] = best;
-      if (out.bid) out.bid[o] = b;
-      if (out.est_ctr) out.est_ctr[o] = c;
-      if (out.true_ctr) out.true_ctr[o] = c;
-      if (out.best_ev) out.best_ev[o] = bs;
-      // streaming top-2, ties -> lowest slot
-      if (s == 0) {
-        m1 = b;
-      } else if (b > m1) {
-        m2 = m1;
-        m1 = b;
-        w = s;
-      } else if (b > m2) {
-        m2 = b;
-      }
-    }
-
-    const bool charged = P >= 2;  // P == 1: empty price arrays, nobody charged
-    const double price = prm.mech == AG_FIRST_PRICE ? m1 : m2;
-    const double second = m2;
-    double ctr_w = ctr[0];
-#pragma unroll
-    for (int s = 1; s < P; ++s)
-      if (s == w) ctr_w = ctr[s];
-    const int oc = bernoulli(ctr_w, u);
-    if (out.winner) out.winner[i] = w;
-    if (out.price) out.price[i] = charged ? price : NAN;
-    if (out.second_price) out.second_price[i] = charged ? second : NAN;
-    if (out.outcome) out.outcome[i] = (uint8_t)oc;
-
-    if (prm.want_counters) {
-      // [slot j][agent a][replica]: lane-private replicas, conflict-free 8-B atomics
-      auto add_raw = [&](int j, int a, unsigned long long v) {
-        atomicAdd(s_cnt + ((size_t)(j * N + a) * R + rep), v);
-      };
-#pragma unroll
-      for (int s = 0; s < P; ++s) {
-        const bool won = charged && s == w;
-        const double lp = charged ? price : 0.0;
-        const double tv = ctr[s] * val[s];
-        if (won) {
-          add_raw(kSlotGross, ag[s], to_fx(val[s] * (double)oc));
-          add_raw(kSlotPaid, ag[s], to_fx(price));
-          if (prm.mech == AG_FIRST_PRICE) add_raw(kSlotOverbid, ag[s], to_fx(lp - second));
-        } else {
-          add_raw(kSlotUnderbid, ag[s], to_fx((lp - bid[s]) * (double)(lp < tv)));
-        }
-        add_raw(kSlotBestEv, ag[s], to_fx(bev[s]));
-        add_raw(kSlotCounts, ag[s], won ? 0x100000001ull : 1ull);
-      }
-    }
-  }
-
-  if (prm.want_counters) {
-    __syncthreads();
-    for (int a = tid; a < N; a += kThreads) {
-      long long lo[kOracleSlots], hi[kOracleSlots];
-      unsigned long long nlogs = 0, nwon = 0;
-      for (int j = 0; j < kOracleSlots; ++j) {
-        lo[j] = 0;
-        hi[j] = 0;
-        for (int r = 0; r < R; ++r) {
-          const unsigned long long c = s_cnt[(size_t)(j * N + a) * R + r];
-          if (j == kSlotCounts) {
-            nlogs += c & 0xffffffffull;
-            nwon += c >> 32;
-          } else {
-            lo[j] += (long long)c & kLimbMask;
-            hi[j] += (long long)c >> AG_FX_LIMB_BITS;
-          }
-        }
-      }
-      // two limbs per counter (value = lo + hi * 2^42): no block total can overflow
-      int64_t *dst = prm.partials + ((size_t)blockIdx.x * N + a) * kC * 2;
-      auto put = [&](int c, long long lo, long long hi) {
-        dst[2 * c] = lo;
-        dst[2 * c + 1] = hi;
-      };
-      auto put_count = [&](int c, unsigned long long n) {
-        put(c, (long long)((n & 63ull) << AG_FX_FRAC_BITS), (long long)(n >> 6));
-      };
-      put(AG_C_NET, lo[kSlotGross] - lo[kSlotPaid], hi[kSlotGross] - hi[kSlotPaid]);
-      put(AG_C_GROSS, lo[kSlotGross], hi[kSlotGross]);
-      put(AG_C_ALLOC_REGRET, 0, 0);
-      put(AG_C_EST_REGRET, 0, 0);
-      put(AG_C_OVERBID, lo[kSlotOverbid], hi[kSlotOverbid]);
-      put(AG_C_UNDERBID, lo[kSlotUnderbid], hi[kSlotUnderbid]);
-      put(AG_C_CTR_SQERR, 0, 0);
-      put_count(AG_C_CTR_BIAS, nwon);
-      put(AG_C_BEST_EV, lo[kSlotBestEv], hi[kSlotBestEv]);
-      put_count(AG_C_N_LOGS, nlogs);
-      put_count(AG_C_N_WON, nwon);
-      put(AG_C_PAID, lo[kSlotPaid], hi[kSlotPaid]);
-    }
-  }
-}
+using namespace ag;
 
 // Sum the per-block partials (two limbs each) of one counter exactly into its limbs
 // (one block per (agent, counter)). Integer sums: any order gives the same bits.
@@ -655,46 +250,16 @@ __global__ __launch_bounds__(kThreads) void k_exp_kat(const double *x, double *y
 // ------------------------------------------------------------------------------------
 // dispatch
 // ------------------------------------------------------------------------------------
-typedef void (*SimKernel)(SimParams);
-
-template <int P, bool PRUNE>
-SimKernel pick_d(int D) {
-  switch (D) {
-    case 2: return k_simulate<P, 2, PRUNE>;
-    case 3: return k_simulate<P, 3, PRUNE>;
-    case 4: return k_simulate<P, 4, PRUNE>;
-    case 5: return k_simulate<P, 5, PRUNE>;
-    case 6: return k_simulate<P, 6, PRUNE>;
-    case 7: return k_simulate<P, 7, PRUNE>;
-    case 8: return k_simulate<P, 8, PRUNE>;
-    default: return nullptr;
-  }
-}
-
-template <int P>
-SimKernel pick_prune(int D, bool prune) {
-  if (prune) return pick_d<P, true>(D);
-  if (D <= 8) return pick_d<P, false>(D);
-  switch (D) {
-    case 9: return k_simulate<P, 9, false>;
-    case 11: return k_simulate<P, 11, false>;
-    case 13: return k_simulate<P, 13, false>;
-    case 16: return k_simulate<P, 16, false>;
-    default: return nullptr;
-  }
-}
-
-// prune: the f32-screened item search (D <= 8, K <= kPruneMaxK); otherwise exact scan.
-SimKernel pick_kernel(int P, int D, bool prune) {
+SimKernel pick_kernel(int P, int D, bool prune, int W) {
   switch (P) {
-    case 1: return pick_prune<1>(D, prune);
-    case 2: return pick_prune<2>(D, prune);
-    case 3: return pick_prune<3>(D, prune);
-    case 4: return pick_prune<4>(D, prune);
-    case 5: return pick_prune<5>(D, prune);
-    case 6: return pick_prune<6>(D, prune);
-    case 7: return pick_prune<7>(D, prune);
-    case 8: return pick_prune<8>(D, prune);
+    case 1: return pick_kernel_for<1>(D, prune, W);
+    case 2: return pick_kernel_for<2>(D, prune, W);
+    case 3: return pick_kernel_for<3>(D, prune, W);
+    case 4: return pick_kernel_for<4>(D, prune, W);
+    case 5: return pick_kernel_for<5>(D, prune, W);
+    case 6: return pick_kernel_for<6>(D, prune, W);
+    case 7: return pick_kernel_for<7>(D, prune, W);
+    case 8: return pick_kernel_for<8>(D, prune, W);
     default: return nullptr;
   }
 }
@@ -721,7 +286,8 @@ struct ag_ctx {
   double *d_values = nullptr;
   int64_t *d_partials = nullptr;
   int32_t partial_blocks = 0;
-  int32_t resident[4] = {0, 0, 0, 0};  // resident k_simulate blocks [screened][counters]
+  int32_t resident[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // resident blocks [W][screened][counters]
+  bool wide = true;
   bool catalog = false;
 };
 
@@ -729,11 +295,11 @@ namespace {
 struct DeviceGuard {
   int prev = -1;
   explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) == hipSuccess && prev != dev) hipSetDevice(dev);
+    if (hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
     else prev = -1;
   }
   ~DeviceGuard() {
-    if (prev >= 0) hipSetDevice(prev);
+    if (prev >= 0) (void)hipSetDevice(prev);
   }
 };
 }  // namespace
@@ -771,7 +337,7 @@ int ag_create(int32_t device, const ag_shape *s, ag_ctx **out) {
   // simulate needs a kernel for (P, D) and the catalogue in LDS; allocate-only contexts
   // (any P) do not.
   const LdsLayout lay = make_layout(s->num_agents, s->num_items, D, true);
-  c->can_simulate = s->num_participants <= kMaxP && pick_kernel(s->num_participants, D, false) &&
+  c->can_simulate = s->num_participants <= kMaxP && pick_kernel(s->num_participants, D, false, 1) &&
                     lay.total <= 160 * 1024;
   DeviceGuard g(device);
   hipError_t e = hipMalloc(&c->d_items, sizeof(double) * s->num_agents * s->num_items * D);
@@ -819,6 +385,11 @@ int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
       if (value != AG_ITEM_SEARCH_AUTO && value != AG_ITEM_SEARCH_EXACT)
         return set_error(AG_ERR_INVALID, "ag_set_option: bad item search mode %lld", (long long)value);
       c->item_search = (int32_t)value;
+      return AG_OK;
+    case AG_OPT_LANE_AUCTIONS:
+      if (value != 1 && value != 2)
+        return set_error(AG_ERR_INVALID, "ag_set_option: lane auctions must be 1 or 2");
+      c->wide = value == 2;
       return AG_OK;
     default:
       return set_error(AG_ERR_INVALID, "ag_set_option: unknown option %d", option);
@@ -891,14 +462,15 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   prm.in = *in;
   prm.out = *out;
   prm.partials = c->d_partials;
-  SimKernel k = pick_kernel(s.num_participants, D, prune);
+  const int W = (prune && (B % 2) == 0 && c->wide) ? 2 : 1;
+  SimKernel k = pick_kernel(s.num_participants, D, prune, W);
   const size_t lds = (size_t)prm.lds.total;
   hipStream_t st = (hipStream_t)stream;
   if (lds > 64 * 1024)
     AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   // Persistent grid: exactly the blocks the device keeps resident (no partial last round),
   // each striding over 256-auction tiles.
-  int &res = c->resident[(prune ? 2 : 0) + (prm.want_counters ? 1 : 0)];
+  int &res = c->resident[(W == 2 ? 4 : 0) + (prune ? 2 : 0) + (prm.want_counters ? 1 : 0)];
   if (res == 0) {
     int per_cu = 0, cus = 0;
     AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k, kThreads, lds));
@@ -907,7 +479,7 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
     if (res < 1) res = 1;
     if (res > c->partial_blocks) res = c->partial_blocks;
   }
-  const int64_t tiles = (B + kThreads - 1) / kThreads;
+  const int64_t tiles = (B + kThreads * W - 1) / (kThreads * W);
   const int grid = (int)(tiles < res ? tiles : res);
   if (B > (int64_t)grid * kMaxAuctionsPerBlock)
     return set_error(AG_ERR_UNSUPPORTED, "ag_simulate: B=%lld > %lld auctions per call; split the batch",

@@ -1,0 +1,564 @@
+// ag_sim.h -- the fused simulate kernel template (shared by the per-P translation units
+// ag_sim_p.hip and the C-ABI in ag_kernels.hip). See ag_kernels.hip for the overview.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+
+#include "auctiongym.h"
+#include "ag_exp.h"
+#include "ag_exp_table.h"
+
+namespace ag {
+
+constexpr int kThreads = 256;              // 4 waves of 64 lanes
+constexpr int kC = AG_NUM_COUNTERS;
+constexpr int kMaxAuctionsPerBlock = 65536; // per launch: keeps a replica's int64 sum exact
+constexpr int kMinGrid = 2048;             // 256 CUs x 8
+constexpr int kMaxSimGrid = 2048;          // partial-sum workspace (>= resident blocks)
+constexpr int kMaxP = 8;                   // per-lane slot registers (template range)
+constexpr int kMaxD = 16;
+constexpr double kFxScale = 0x1p36;        // 2^AG_FX_FRAC_BITS
+constexpr double kMagic = 0x1.8p52;
+constexpr int64_t kLimbMask = (int64_t(1) << AG_FX_LIMB_BITS) - 1;
+
+// ------------------------------------------------------------------------------------
+// reference arithmetic
+// ------------------------------------------------------------------------------------
+
+// numpy `items @ ctx` -> OpenBLAS dgemv_t (SURVEY §8 a5'; oracle/ag_oracle.c ora_dot):
+// rows in blocks of 4 with one FMA accumulator per lane, lanes reduced (l0+l2)+(l1+l3),
+// 1-3 tail rows added by contracted scalar code. `a` is in LDS, `x` in registers.
+template <int D>
+__device__ __forceinline__ double dot_ref(const double *__restrict__ a, const double (&x)[kMaxD]) {
+  constexpr int m3 = D & 3, m1 = D - m3;
+  double y = 0.0;
+  if constexpr (m1 > 0) {
+    double l0 = 0.0, l1 = 0.0, l2 = 0.0, l3 = 0.0;
+#pragma unroll
+    for (int i = 0; i < m1; i += 4) {
+      l0 = fma(a[i + 0], x[i + 0], l0);
+      l1 = fma(a[i + 1], x[i + 1], l1);
+      l2 = fma(a[i + 2], x[i + 2], l2);
+      l3 = fma(a[i + 3], x[i + 3], l3);
+    }
+    y = (l0 + l2) + (l1 + l3);
+  }
+  if constexpr (m3 == 1) y = fma(a[m1], x[m1], y);
+  if constexpr (m3 == 2) y = y + fma(a[m1], x[m1], a[m1 + 1] * x[m1 + 1]);
+  if constexpr (m3 == 3)
+    y = y + fma(a[m1 + 2], x[m1 + 2], fma(a[m1], x[m1], a[m1 + 1] * x[m1 + 1]));
+  return y;
+}
+
+// numpy Generator.binomial(1, p) from its single next_double U (src/Auction.py:65;
+// numpy's inversion sampler for n = 1). The sampler compares U with exp(log(1 - p)); this
+// uses 1 - p (resp. p), which differs from it by at most one ulp: the outcome can differ
+// only when U lands on that ulp, probability <= 2^-53 per auction.
+__device__ __forceinline__ int bernoulli(double p, double u) {
+  if (p == 0.0) return 0;
+  if (p <= 0.5) return u > (1.0 - p) ? 1 : 0;
+  return u > p ? 0 : 1;
+}
+
+// Round x * 2^36 to the nearest integer (ties-to-even), exactly.
+__device__ __forceinline__ unsigned long long to_fx(double x) {
+  if (fabs(x) < 0x1p14) {
+    double y = fma(x, kFxScale, kMagic);
+    return (unsigned long long)(__double_as_longlong(y) - __double_as_longlong(kMagic));
+  }
+  if (!(fabs(x) < 0x1p26)) return 0ull;  // non-finite / absurd term: dropped
+  return (unsigned long long)(long long)rint(x * kFxScale);
+}
+
+// LDS carve of k_simulate (all pieces 16-B aligned; offsets in bytes).
+struct LdsLayout {
+  int32_t tab, items, values, scr, scr_val, amax, cnt, total;
+  int32_t items_stride;    // doubles between agents (odd: spreads agents over banks)
+  int32_t values_stride;   // doubles
+  int32_t scr_stride;      // floats between agents in the screening catalogue
+  int32_t scr_val_stride;  // floats
+  int32_t kpairs;          // item pairs in the screening catalogue (K rounded up to even)
+  int32_t replicas;        // per-lane counter replicas (power of 2, <= 64)
+  int32_t ncnt;            // counter slots held in LDS
+};
+
+__host__ inline int32_t align16(int64_t b) { return (int32_t)((b + 15) & ~(int64_t)15); }
+
+// Counter slots accumulated in LDS for OracleAllocator + TruthfulBidder populations:
+//   0 GROSS, 1 PAID, 2 OVERBID (FirstPrice only: price - second_price == 0 under SP),
+//   3 UNDERBID, 4 BEST_EV, 5 packed counts (n_logs in bits 0-31, n_won in bits 32-63).
+// Derived at write-out: NET = GROSS - PAID (both exact fixed-point sums), CTR_BIAS =
+// N_WON (est/true == 1 for Oracle agents); ALLOC / EST regrets and CTR_SQERR are
+// identically zero for them (estimated CTR == true CTR, best_ev == true_ctr * value).
+constexpr int kOracleSlots = 6;
+enum { kSlotGross = 0, kSlotPaid, kSlotOverbid, kSlotUnderbid, kSlotBestEv, kSlotCounts };
+
+__host__ inline LdsLayout make_layout(int N, int K, int D, bool counters) {
+  LdsLayout L;
+  L.items_stride = (K * D) | 1;
+  L.values_stride = K | 1;
+  L.kpairs = (K + 1) / 2;
+  // [pair][dim 0..7][2 items] floats; + 4 floats so agents start on different 16-B slots
+  L.scr_stride = L.kpairs * 16 + 4;
+  L.scr_val_stride = L.kpairs * 2 + 2;
+  L.ncnt = kOracleSlots;
+  int R = 64;
+  while (R > 1 && (int64_t)R * N * L.ncnt * 8 > 32768) R >>= 1;
+  L.replicas = R;
+  int64_t b = 0;
+  L.tab = 0;
+  b += 256 * 8;
+  L.items = align16(b);
+  b = L.items + (int64_t)N * L.items_stride * 8;
+  L.values = align16(b);
+  b = L.values + (int64_t)N * L.values_stride * 8;
+  L.scr = align16(b);
+  b = L.scr + (int64_t)N * L.scr_stride * 4;
+  L.scr_val = align16(b);
+  b = L.scr_val + (int64_t)N * L.scr_val_stride * 4;
+  L.amax = align16(b);
+  b = L.amax + (int64_t)N * 4;
+  L.cnt = align16(b);
+  b = L.cnt + (counters ? (int64_t)R * N * L.ncnt * 8 : 0);
+  L.total = align16(b);
+  return L;
+}
+
+struct SimParams {
+  int32_t B;              // auctions in this launch (< 2^28: 32-bit SoA indexing)
+  int32_t N, K, mech;
+  int32_t want_counters;
+  LdsLayout lds;
+  const double *items;    // global [N][K][D]
+  const double *values;   // global [N][K]
+  ag_batch_in in;
+  ag_batch_out out;
+  int64_t *partials;      // [grid][N][AG_NUM_COUNTERS]
+};
+
+// Screening margin. The screen ranks items by t_k = (1 + 2^(z'_k)) / v_k = 1 / (exact
+// score) in f32, z'_k the f32 dot of the catalogue row pre-scaled by -log2(e), 1/v_k
+// precomputed. With S = sum_d |a_d x_d| <= kPruneMaxS its relative error is
+// eps <= S 2^-21 (inputs rounded to f32, D <= 8 FMAs) + |z| 2^-23 (exp2 argument) +
+// 2^-22 (exp2, fma, 1/v) < 4e-5, so every item whose EXACT score is the maximum has
+// t_k <= t_min (1 + eps)/(1 - eps) < t_min (1 + kPruneDelta), kPruneDelta = 2^-13 =
+// 1.22e-4 > 2.01 eps: re-scoring every item under that threshold exactly keeps the exact
+// argmax and all its exact ties. Lanes outside the bound (or with no finite t) re-score
+// every item exactly.
+constexpr float kPruneDelta = 0x1p-13f;
+constexpr float kPruneMaxS = 64.0f;
+constexpr int kMaxKPairs = 8;  // screened search for K <= 16
+constexpr float kNegLog2e = -1.4426950408889634f;
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Agent.select_item (src/Agent.py:29-42) for an OracleAllocator agent: the first k that
+// maximises sigmoid(items_k . x) * value_k, with the reference's exact FP64 arithmetic.
+// PRUNE: a packed-f32 pass scores all items two at a time; the f32 leader and any item
+// within kPruneDelta of it are re-scored exactly, so the first-max rule and every bit of
+// the chosen item's CTR / score are the reference's.
+template <int D, bool PRUNE>
+__device__ __forceinline__ int select_item(const double *__restrict__ itm, const double *__restrict__ vv,
+                                           const float *__restrict__ scr, const float *__restrict__ sv,
+                                           float amax, int K, int kpairs, const double (&x)[kMaxD],
+                                           const float (&xf)[kMaxD], float xabs, const uint64_t *tab,
+                                           double &ctr_best, double &score_best) {
+  int best = -1;
+  double best_s = 0.0, best_c = 0.0;
+  auto exact = [&](int k) {
+    const double c = agexp::sigmoid(dot_ref<D>(itm + k * D, x), tab);
+    const double sc = c * vv[k];
+    if (best < 0 || sc > best_s || (sc == best_s && k < best)) {
+      best = k;
+      best_s = sc;
+      best_c = c;
+    }
+  };
+  if constexpr (PRUNE) {
+    // f32 screen of one item pair: t = (1 + 2^z') / v of items 2p, 2p+1 (padding: +inf)
+    auto screen = [&](int p) -> f32x2 {
+      const float *row = scr + p * 16;
+      f32x2 z = {0.0f, 0.0f};
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const f32x2 a = *reinterpret_cast<const f32x2 *>(row + 2 * d);
+        const f32x2 xd = {xf[d], xf[d]};
+        z = __builtin_elementwise_fma(a, xd, z);
+      }
+      const f32x2 e = {__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)};
+      const f32x2 iv = *reinterpret_cast<const f32x2 *>(sv + 2 * p);
+      return __builtin_elementwise_fma(e, iv, iv);
+    };
+    // pass 1: f32 leader kf (smallest t), its t and the runner-up's
+    float t1 = INFINITY, t2 = INFINITY;
+    int kf = 0;
+    for (int p = 0; p < kpairs; ++p) {
+      const f32x2 t = screen(p);
+      const float lo = fminf(t.x, t.y), hi = fmaxf(t.x, t.y);
+      const int klo = t.y < t.x ? 2 * p + 1 : 2 * p;
+      if (lo < t1) {
+        t2 = fminf(t1, hi);
+        t1 = lo;
+        kf = klo;
+      } else {
+        t2 = fminf(t2, lo);
+      }
+    }
+    const bool ok = (amax * xabs <= kPruneMaxS) && (t1 <= 1e30f);
+    const float thr = ok ? t1 * (1.0f + kPruneDelta) : INFINITY;
+    exact(kf);  // the f32 leader: every lane, no divergence
+    if (!(t2 > thr)) {
+      // near-tie (rare) or unscreenable lane: re-score every other item under thr
+      for (int p = 0; p < kpairs; ++p) {
+        const f32x2 t = screen(p);
+        if (2 * p != kf && !(t.x > thr)) exact(2 * p);
+        if (2 * p + 1 != kf && 2 * p + 1 < K && !(t.y > thr)) exact(2 * p + 1);
+      }
+    }
+  } else {
+    for (int k = 0; k < K; ++k) exact(k);
+  }
+  ctr_best = best_c;
+  score_best = best_s;
+  return best;
+}
+
+// ------------------------------------------------------------------------------------
+// fused simulate kernel
+// ------------------------------------------------------------------------------------
+
+// W-wide SoA accesses (W = 2: one 16-B / 8-B / 2-B access per lane for two auctions).
+// AG_NT_LOADS / AG_NT_STORES (build variants for A/B timing): non-temporal streaming.
+#ifndef AG_NT_LOADS
+#define AG_NT_LOADS 0
+#endif
+#ifndef AG_NT_STORES
+#define AG_NT_STORES 0
+#endif
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+template <typename T>
+__device__ __forceinline__ T ldg(const T *p) {
+  if constexpr (AG_NT_LOADS) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <typename T>
+__device__ __forceinline__ void stg(T *p, T v) {
+  if constexpr (AG_NT_STORES) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+template <int W>
+__device__ __forceinline__ void ld_f64(const double *p, double (&v)[W]) {
+  if constexpr (W == 1) {
+    v[0] = ldg(p);
+  } else {
+    const f64x2 t = ldg(reinterpret_cast<const f64x2 *>(p));
+    v[0] = t.x;
+    v[1] = t.y;
+  }
+}
+template <int W>
+__device__ __forceinline__ void ld_i32(const int32_t *p, int (&v)[W]) {
+  if constexpr (W == 1) {
+    v[0] = ldg(p);
+  } else {
+    const i32x2 t = ldg(reinterpret_cast<const i32x2 *>(p));
+    v[0] = t.x;
+    v[1] = t.y;
+  }
+}
+template <int W>
+__device__ __forceinline__ void st_f64(double *p, const double (&v)[W]) {
+  if constexpr (W == 1) stg(p, v[0]);
+  else stg(reinterpret_cast<f64x2 *>(p), f64x2{v[0], v[1]});
+}
+template <int W>
+__device__ __forceinline__ void st_i32(int32_t *p, const int (&v)[W]) {
+  if constexpr (W == 1) stg(p, (int32_t)v[0]);
+  else stg(reinterpret_cast<i32x2 *>(p), i32x2{v[0], v[1]});
+}
+template <int W>
+__device__ __forceinline__ void st_u8(uint8_t *p, const int (&v)[W]) {
+  if constexpr (W == 1) stg(p, (uint8_t)v[0]);
+  else stg(reinterpret_cast<uint16_t *>(p), (uint16_t)((v[0] & 1) | ((v[1] & 1) << 8)));
+}
+
+// LDS views of the catalogue + tables for one block
+struct Lds {
+  const uint64_t *tab;
+  const double *items, *vals;
+  const float *scr, *scr_val, *amax;
+  int items_stride, values_stride, scr_stride, scr_val_stride, kpairs;
+};
+
+// One auction resolved (src/Auction.py:28-74 minus the draws).
+template <int P>
+struct Resolved {
+  int ag[P], item[P];
+  double val[P], bid[P], ctr[P], bev[P];
+  int w, oc;
+  double price, second;
+};
+
+template <int P, int D, bool PRUNE>
+__device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const double (&x)[kMaxD],
+                                        const float (&xf)[kMaxD], float xabs, const int (&ag)[P], double u,
+                                        Resolved<P> &r) {
+  double m1 = 0.0, m2 = -INFINITY;
+  int w = 0;
+#pragma unroll
+  for (int s = 0; s < P; ++s) {
+    const int a = ag[s];
+    r.ag[s] = a;
+    double c, bs;
+    const int best = select_item<D, PRUNE>(T.items + a * T.items_stride, T.vals + a * T.values_stride,
+                                           T.scr + a * T.scr_stride, T.scr_val + a * T.scr_val_stride,
+                                           PRUNE ? T.amax[a] : 0.0f, K, T.kpairs, x, xf, xabs, T.tab, c, bs);
+    const double v = T.vals[a * T.values_stride + best];
+    const double b = v * c;  // TruthfulBidder.bid (src/Bidder.py:34-35)
+    r.item[s] = best;
+    r.val[s] = v;
+    r.bid[s] = b;
+    r.ctr[s] = c;   // Oracle: estimated CTR == true CTR, bit for bit
+    r.bev[s] = bs;  // max_k true_CTR_k * value_k (src/Auction.py:52-53)
+    // streaming top-2, ties -> lowest slot (src/AuctionAllocation.py:19-34)
+    if (s == 0) {
+      m1 = b;
+    } else if (b > m1) {
+      m2 = m1;
+      m1 = b;
+      w = s;
+    } else if (b > m2) {
+      m2 = b;
+    }
+  }
+  r.w = w;
+  r.price = mech == AG_FIRST_PRICE ? m1 : m2;
+  r.second = m2;
+  double ctr_w = r.ctr[0];
+#pragma unroll
+  for (int s = 1; s < P; ++s)
+    if (s == w) ctr_w = r.ctr[s];
+  r.oc = bernoulli(ctr_w, u);  // src/Auction.py:65
+}
+
+template <int P, int D, bool PRUNE, int W>
+__global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int N = prm.N, K = prm.K;
+  const uint32_t B = (uint32_t)prm.B;
+  const LdsLayout L = prm.lds;
+  uint64_t *s_tab = reinterpret_cast<uint64_t *>(smem + L.tab);
+  double *s_items = reinterpret_cast<double *>(smem + L.items);
+  double *s_vals = reinterpret_cast<double *>(smem + L.values);
+  float *s_scr = reinterpret_cast<float *>(smem + L.scr);
+  float *s_scr_val = reinterpret_cast<float *>(smem + L.scr_val);
+  float *s_amax = reinterpret_cast<float *>(smem + L.amax);
+  unsigned long long *s_cnt = reinterpret_cast<unsigned long long *>(smem + L.cnt);
+
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 256; i += kThreads) s_tab[i] = ag_exp_tab[i];
+  for (int i = tid; i < N * K * D; i += kThreads) {
+    const int a = i / (K * D), r = i - a * (K * D);
+    s_items[a * L.items_stride + r] = prm.items[i];
+  }
+  for (int i = tid; i < N * K; i += kThreads) {
+    const int a = i / K, r = i - a * K;
+    s_vals[a * L.values_stride + r] = prm.values[i];
+  }
+  if (PRUNE) {
+    // screening rows: [pair p][dim d][item 2p, 2p+1], coefficients * -log2(e); padded
+    // dims and the odd item's partner are 0
+    for (int i = tid; i < N * L.kpairs * 16; i += kThreads) {
+      const int a = i / (L.kpairs * 16), r = i - a * (L.kpairs * 16);
+      const int p = r >> 4, d = (r >> 1) & 7, k = 2 * p + (r & 1);
+      const float c = (d < D && k < K) ? (float)prm.items[((size_t)a * K + k) * D + d] : 0.0f;
+      s_scr[a * L.scr_stride + r] = c * kNegLog2e;
+    }
+    for (int i = tid; i < N * L.kpairs * 2; i += kThreads) {  // 1/v (padding items: +inf)
+      const int a = i / (L.kpairs * 2), k = i - a * (L.kpairs * 2);
+      s_scr_val[a * L.scr_val_stride + k] = k < K ? 1.0f / (float)prm.values[(size_t)a * K + k] : INFINITY;
+    }
+    for (int a = tid; a < N; a += kThreads) {
+      float m = 0.0f;
+      for (int r = 0; r < K * D; ++r) m = fmaxf(m, (float)fabs(prm.items[(size_t)a * K * D + r]));
+      s_amax[a] = m * 1.001f;
+    }
+  }
+  const int R = L.replicas;
+  if (prm.want_counters)
+    for (int i = tid; i < R * N * L.ncnt; i += kThreads) s_cnt[i] = 0ull;
+  __syncthreads();
+
+  const Lds T{s_tab, s_items, s_vals, s_scr, s_scr_val, s_amax, L.items_stride, L.values_stride,
+              L.scr_stride, L.scr_val_stride, L.kpairs};
+  const int rep = tid & (R - 1);
+  const ag_batch_in in = prm.in;
+  const ag_batch_out out = prm.out;
+  const bool charged = P >= 2;  // P == 1: empty price arrays, nobody charged (Auction.py:68)
+
+  for (uint32_t base = blockIdx.x * (kThreads * W); base < B; base += gridDim.x * (kThreads * W)) {
+    const uint32_t i = base + tid * W;  // W consecutive auctions (B % W == 0)
+    if (i >= B) continue;
+
+    double xv[kMaxD][W];
+    int pv[P][W];
+    double uv[W];
+#pragma unroll
+    for (int e = 0; e < D - 1; ++e) ld_f64<W>(in.ctx + e * B + i, xv[e]);
+#pragma unroll
+    for (int s = 0; s < P; ++s) ld_i32<W>(in.part + s * B + i, pv[s]);
+    ld_f64<W>(in.u + i, uv);
+
+    Resolved<P> r[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      double x[kMaxD];
+      float xf[kMaxD];
+      float xabs = 1.0f;
+#pragma unroll
+      for (int e = 0; e < D - 1; ++e) {
+        x[e] = xv[e][q];
+        xf[e] = (float)x[e];
+        xabs += fabsf(xf[e]);
+      }
+      x[D - 1] = 1.0;  // intercept (src/Auction.py:33)
+      xf[D - 1] = 1.0f;
+      xabs *= 1.001f;
+      int ag[P];
+#pragma unroll
+      for (int s = 0; s < P; ++s) ag[s] = pv[s][q];
+      resolve<P, D, PRUNE>(T, K, prm.mech, x, xf, xabs, ag, uv[q], r[q]);
+    }
+
+    // SoA stores, W auctions per access
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+      const uint32_t o = s * B + i;
+      int iv[W];
+      double bv[W], cv[W], ev[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        iv[q] = r[q].item[s];
+        bv[q] = r[q].bid[s];
+        cv[q] = r[q].ctr[s];
+        ev[q] = r[q].bev[s];
+      }
+      if (out.item) st_i32<W>(out.item + o, iv);
+      if (out.bid) st_f64<W>(out.bid + o, bv);
+      if (out.est_ctr) st_f64<W>(out.est_ctr + o, cv);
+      if (out.true_ctr) st_f64<W>(out.true_ctr + o, cv);
+      if (out.best_ev) st_f64<W>(out.best_ev + o, ev);
+    }
+    {
+      int wv[W], ov[W];
+      double pr[W], sp[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        wv[q] = r[q].w;
+        ov[q] = r[q].oc;
+        pr[q] = charged ? r[q].price : NAN;
+        sp[q] = charged ? r[q].second : NAN;
+      }
+      if (out.winner) st_i32<W>(out.winner + i, wv);
+      if (out.price) st_f64<W>(out.price + i, pr);
+      if (out.second_price) st_f64<W>(out.second_price + i, sp);
+      if (out.outcome) st_u8<W>(out.outcome + i, ov);
+    }
+
+    if (prm.want_counters) {
+      // [slot j][agent a][replica]: lane-private replicas, conflict-free 8-B atomics
+      auto add_raw = [&](int j, int a, unsigned long long v) {
+        atomicAdd(s_cnt + ((size_t)(j * N + a) * R + rep), v);
+      };
+      // zero terms are skipped (a wave whose lanes all hold 0 issues no atomic): no clicks
+      // for GROSS, and under SecondPrice with P == 2 the loser's underbid term
+      // (price - bid) * [...] is exactly 0 because the price is its bid
+      auto add_nz = [&](int j, int a, unsigned long long v) {
+        if (v != 0ull) add_raw(j, a, v);
+      };
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        const Resolved<P> &rr = r[q];
+#pragma unroll
+        for (int s = 0; s < P; ++s) {
+          const bool won = charged && s == rr.w;
+          const double lp = charged ? rr.price : 0.0;
+          const double tv = rr.ctr[s] * rr.val[s];
+          if (won) {
+            add_nz(kSlotGross, rr.ag[s], to_fx(rr.val[s] * (double)rr.oc));
+            add_raw(kSlotPaid, rr.ag[s], to_fx(rr.price));
+            if (prm.mech == AG_FIRST_PRICE) add_nz(kSlotOverbid, rr.ag[s], to_fx(lp - rr.second));
+          } else {
+            add_nz(kSlotUnderbid, rr.ag[s], to_fx((lp - rr.bid[s]) * (double)(lp < tv)));
+          }
+          add_raw(kSlotBestEv, rr.ag[s], to_fx(rr.bev[s]));
+          add_raw(kSlotCounts, rr.ag[s], won ? 0x100000001ull : 1ull);
+        }
+      }
+    }
+  }
+
+  if (prm.want_counters) {
+    __syncthreads();
+    for (int a = tid; a < N; a += kThreads) {
+      long long lo[kOracleSlots], hi[kOracleSlots];
+      unsigned long long nlogs = 0, nwon = 0;
+      for (int j = 0; j < kOracleSlots; ++j) {
+        lo[j] = 0;
+        hi[j] = 0;
+        for (int r = 0; r < R; ++r) {
+          const unsigned long long c = s_cnt[(size_t)(j * N + a) * R + r];
+          if (j == kSlotCounts) {
+            nlogs += c & 0xffffffffull;
+            nwon += c >> 32;
+          } else {
+            lo[j] += (long long)c & kLimbMask;
+            hi[j] += (long long)c >> AG_FX_LIMB_BITS;
+          }
+        }
+      }
+      // two limbs per counter (value = lo + hi * 2^42): no block total can overflow
+      int64_t *dst = prm.partials + ((size_t)blockIdx.x * N + a) * kC * 2;
+      auto put = [&](int c, long long lo, long long hi) {
+        dst[2 * c] = lo;
+        dst[2 * c + 1] = hi;
+      };
+      auto put_count = [&](int c, unsigned long long n) {
+        put(c, (long long)((n & 63ull) << AG_FX_FRAC_BITS), (long long)(n >> 6));
+      };
+      put(AG_C_NET, lo[kSlotGross] - lo[kSlotPaid], hi[kSlotGross] - hi[kSlotPaid]);
+      put(AG_C_GROSS, lo[kSlotGross], hi[kSlotGross]);
+      put(AG_C_ALLOC_REGRET, 0, 0);
+      put(AG_C_EST_REGRET, 0, 0);
+      put(AG_C_OVERBID, lo[kSlotOverbid], hi[kSlotOverbid]);
+      put(AG_C_UNDERBID, lo[kSlotUnderbid], hi[kSlotUnderbid]);
+      put(AG_C_CTR_SQERR, 0, 0);
+      put_count(AG_C_CTR_BIAS, nwon);
+      put(AG_C_BEST_EV, lo[kSlotBestEv], hi[kSlotBestEv]);
+      put_count(AG_C_N_LOGS, nlogs);
+      put_count(AG_C_N_WON, nwon);
+      put(AG_C_PAID, lo[kSlotPaid], hi[kSlotPaid]);
+    }
+  }
+}
+
+
+typedef void (*SimKernel)(SimParams);
+
+// Defined per participant count P in ag_sim_p.hip (one translation unit per P, compiled
+// in parallel): the k_simulate instantiation for (D, screened search, auctions per lane).
+template <int P>
+SimKernel pick_kernel_for(int D, bool prune, int W);
+template <> SimKernel pick_kernel_for<1>(int, bool, int);
+template <> SimKernel pick_kernel_for<2>(int, bool, int);
+template <> SimKernel pick_kernel_for<3>(int, bool, int);
+template <> SimKernel pick_kernel_for<4>(int, bool, int);
+template <> SimKernel pick_kernel_for<5>(int, bool, int);
+template <> SimKernel pick_kernel_for<6>(int, bool, int);
+template <> SimKernel pick_kernel_for<7>(int, bool, int);
+template <> SimKernel pick_kernel_for<8>(int, bool, int);
+
+}  // namespace ag

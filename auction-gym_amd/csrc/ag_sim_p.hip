@@ -1,0 +1,44 @@
+// ag_sim_p.hip -- k_simulate instantiations for one participant count AG_P (the Makefile
+// compiles this file once per P = 1..8, in parallel).
+#include "ag_sim.h"
+
+#ifndef AG_P
+#error "compile with -DAG_P=<participants>"
+#endif
+
+namespace ag {
+namespace {
+
+template <int P, bool PRUNE, int W>
+SimKernel pick_d(int D) {
+  switch (D) {
+    case 2: return k_simulate<P, 2, PRUNE, W>;
+    case 3: return k_simulate<P, 3, PRUNE, W>;
+    case 4: return k_simulate<P, 4, PRUNE, W>;
+    case 5: return k_simulate<P, 5, PRUNE, W>;
+    case 6: return k_simulate<P, 6, PRUNE, W>;
+    case 7: return k_simulate<P, 7, PRUNE, W>;
+    case 8: return k_simulate<P, 8, PRUNE, W>;
+    default: return nullptr;
+  }
+}
+
+}  // namespace
+
+// prune: the f32-screened item search (D <= 8, K <= 2 kMaxKPairs), W auctions per lane
+// (2 when B is even: 16-B accesses); otherwise the exact scan, one auction per lane.
+template <>
+SimKernel pick_kernel_for<AG_P>(int D, bool prune, int W) {
+  constexpr int P = AG_P;
+  if (prune) return W == 2 ? pick_d<P, true, 2>(D) : pick_d<P, true, 1>(D);
+  if (D <= 8) return pick_d<P, false, 1>(D);
+  switch (D) {
+    case 9: return k_simulate<P, 9, false, 1>;
+    case 11: return k_simulate<P, 11, false, 1>;
+    case 13: return k_simulate<P, 13, false, 1>;
+    case 16: return k_simulate<P, 16, false, 1>;
+    default: return nullptr;
+  }
+}
+
+}  // namespace ag

@@ -108,6 +108,7 @@ def main():
 
     from auctiongym_amd import _lib
     from auctiongym_amd.engine import AuctionEngine
+    from auctiongym_amd.sharding import allreduce_counters, shard_range
 
     items, values = catalogue()
     N, K, D = items.shape
@@ -117,7 +118,8 @@ def main():
                         SP_ORACLE["embedding_var"], device=local)
     eng.load_catalog(items, values)
     inp = eng.alloc_inputs(B)
-    eng.generate(0, rank * B, inp)  # global auction indices: the shard of this rank
+    lo, hi = shard_range(B * world, rank, world)  # global auction indices of this rank
+    eng.generate(0, lo, inp)
     fields = ("winner", "price", "outcome", "item", "bid", "est_ctr", "true_ctr", "best_ev")
     out = eng.alloc_outputs(B, fields)
     cnt = eng.new_counters()
@@ -136,7 +138,7 @@ def main():
         if i is not None:
             ev[i][1].record(stream)
         if world > 1:
-            dist.all_reduce(cnt)  # exact int64 limb sums across shards
+            allreduce_counters(cnt)  # exact int64 limb sums across shards (RCCL)
 
     for _ in range(args.warmup):
         step()
@@ -164,12 +166,14 @@ def main():
     achieved = bpa * B / (kern_ms * 1e-3) / 1e9
 
     traffic = None
+    traffic_src = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tfile):
         with open(tfile) as f:
             tj = json.load(f)
         if tj.get("batch") == B:
             traffic = tj.get("hbm_bytes_per_launch")
+            traffic_src = tj.get("source")
 
     result = {
         "metric": "auctions resolved/sec (SP_Oracle-shaped batches)",
@@ -191,6 +195,8 @@ def main():
                    "parallelism": f"dp{world} (independent auction shards; int64 counter all-reduce)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                     "traffic_source": traffic_src,
                      "kernel": "ag_simulate (k_simulate + k_reduce_counters)",
                      "kernel_ms": kern_ms, "algorithmic_bytes_per_auction": bpa},
     }

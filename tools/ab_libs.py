@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""A/B timing of library builds of the same ABI (make variant NAME=... VFLAGS=...) on the
+bench workload, interleaved in ONE process (cdna_hip_programming.md rule 24).
+
+    python tools/ab_libs.py [variant names...]      (default: every build/variants/*.so)
+"""
+import glob
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "auction-gym_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from auctiongym_amd import _lib  # noqa: E402
+from auctiongym_amd.engine import AuctionEngine  # noqa: E402
+
+
+def main():
+    names = sys.argv[1:]
+    vdir = os.path.join(ROOT, "auction-gym_amd", "build", "variants")
+    paths = {"base": _lib.LIB_PATH}
+    if names:
+        for n in names:
+            paths[n] = os.path.join(vdir, f"libauctiongym_hip_{n}.so")
+    else:
+        for p in sorted(glob.glob(os.path.join(vdir, "*.so"))):
+            paths[os.path.basename(p)[len("libauctiongym_hip_"):-3]] = p
+    B = 1 << 24
+    items, values = bench.catalogue()
+    engs = {}
+    for n, p in paths.items():
+        e = AuctionEngine(6, 2, 12, 5, 4, _lib.SECOND_PRICE, 1.0, device=0, lib_path=p)
+        e.load_catalog(items, values)
+        engs[n] = e
+    base = engs["base"]
+    inp = base.alloc_inputs(B)
+    base.generate(0, 0, inp)
+    full = ("winner", "price", "outcome", "item", "bid", "est_ctr", "true_ctr", "best_ev")
+    ref = base.alloc_outputs(B, full)
+    cref = base.new_counters()
+    base.simulate(inp, ref, cref)
+    out = base.alloc_outputs(B, full)
+    cnt = base.new_counters()
+    st = torch.cuda.current_stream()
+    times = {n: [] for n in engs}
+    for r in range(25):
+        for n, e in engs.items():
+            cnt.zero_()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            e.simulate(inp, out, cnt)
+            b.record(st)
+            torch.cuda.synchronize()
+            if r >= 3:
+                times[n].append(a.elapsed_time(b))
+            if r == 0:
+                same = all(torch.equal(out[k], ref[k]) for k in full) and torch.equal(cnt, cref)
+                print(f"{n}: outputs identical to base: {same}")
+    bpa = bench.algorithmic_bytes_per_auction(5, 2, False)
+    for n, t in times.items():
+        ms, lo = float(np.median(t)), float(np.min(t))
+        print(f"{n:12s} median {ms:.4f} ms  min {lo:.4f} ms  {bpa * B / ms / 1e6:7.1f} GB/s")
+
+
+if __name__ == "__main__":
+    main()

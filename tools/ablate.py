@@ -29,17 +29,19 @@ def main():
     out = eng.alloc_outputs(B, full)
     cnt = eng.new_counters()
     variants = {
-        "bench (all outputs + counters)": (False, full, True),
-        "no counters": (False, full, False),
-        "counters, winner/price only": (False, ("winner", "price"), True),
-        "no outputs, no counters": (False, (), False),
-        "exact item scan": (True, full, True),
+        "bench (all outputs + counters)": (False, full, True, 2),
+        "bench, 1 auction per lane": (False, full, True, 1),
+        "no counters": (False, full, False, 2),
+        "counters, winner/price only": (False, ("winner", "price"), True, 2),
+        "no outputs, no counters": (False, (), False, 2),
+        "exact item scan": (True, full, True, 1),
     }
     times = {k: [] for k in variants}
     st = torch.cuda.current_stream()
     for r in range(rounds):
-        for name, (exact, fields, want_cnt) in variants.items():
+        for name, (exact, fields, want_cnt, lanes) in variants.items():
             eng.set_item_search(exact)
+            eng.set_lane_auctions(lanes)
             o = {k: out[k] for k in fields}
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(st)
@@ -51,7 +53,7 @@ def main():
     bpa = bench.algorithmic_bytes_per_auction(5, 2, False)
     for name, t in times.items():
         ms = float(np.median(t))
-        print(f"{name:34s} {ms:8.4f} ms  {B / ms / 1e6:9.1f} M auctions/s  "
+        print(f"{name:34s} {ms:8.4f} ms  {B / ms / 1e6:9.1f} G auctions/s  "
               f"{bpa * B / ms / 1e6:8.1f} GB/s(141B)")
     # pure streaming reference: read 56 B + write 85 B per auction with a copy
     src = torch.empty(B * 56 // 8, dtype=torch.float64, device="cuda")

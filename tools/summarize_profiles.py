@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Condense a tools/collect_profiles.sh run into profiles/<tag>_*.csv + profiles/pmc_traffic.json.
+
+    python tools/summarize_profiles.py <tag> [batch]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def pmc(path):
+    f = glob.glob(os.path.join(path, "*counter_collection.csv"))[0]
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    for r in csv.DictReader(open(f)):
+        per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
+    names = sorted({c for d in per.values() for c in d})
+    return {c: sum(d[c] for d in per.values()) / len(per) for c in names}, len(per)
+
+
+def main():
+    tag = sys.argv[1]
+    batch = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 24
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "stats", "*kernel_stats.csv"))[0]
+    shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    summary = {"tag": tag, "batch": batch}
+    for part in ("fetch", "write", "sq", "sq2"):
+        vals, n = pmc(os.path.join(src, part))
+        summary[part] = {"dispatches": n, "per_dispatch_mean": vals}
+    fetch_kb = summary["fetch"]["per_dispatch_mean"]["FETCH_SIZE"]
+    write_kb = summary["write"]["per_dispatch_mean"]["WRITE_SIZE"]
+    # gfx950: FETCH_SIZE reports half the bytes of a wide coalesced read (MI355X_MICROARCH.md)
+    hbm = fetch_kb * 1024 * 2 + write_kb * 1024
+    summary["hbm_bytes_per_launch"] = hbm
+    summary["algorithmic_bytes_per_launch"] = 141 * batch
+    with open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
+        json.dump({"batch": batch, "hbm_bytes_per_launch": hbm,
+                   "source": f"profiles/{tag}_pmc_summary.json (k_simulate, FETCH_SIZE*2*1024 + "
+                             "WRITE_SIZE*1024, mean over dispatches)"}, f, indent=1)
+    print(json.dumps({"hbm_bytes_per_launch": hbm, "algorithmic": 141 * batch,
+                      "ratio": hbm / (141 * batch)}))
+
+
+if __name__ == "__main__":
+    main()
