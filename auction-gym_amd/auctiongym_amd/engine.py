@@ -84,8 +84,8 @@ class AuctionEngine:
         self._check(self.L.ag_set_option(self._h, _lib.OPT_ITEM_SEARCH, mode), "ag_set_option")
 
     def set_lane_auctions(self, n):
-        """Auctions per lane in the screened kernel: 2 (default; 16-B SoA accesses when B
-        is even) or 1. Same results either way."""
+        """Auctions per lane in the screened kernel: 1 (default) or 2 (16-B SoA accesses when
+        B is even; lower occupancy, slower under sustained load). Same results either way."""
         self._check(self.L.ag_set_option(self._h, _lib.OPT_LANE_AUCTIONS, int(n)), "ag_set_option")
 
     def load_catalog(self, items, values):

@@ -287,7 +287,7 @@ struct ag_ctx {
   int64_t *d_partials = nullptr;
   int32_t partial_blocks = 0;
   int32_t resident[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // resident blocks [W][screened][counters]
-  bool wide = true;
+  bool wide = false;  // 1 auction per lane by default: higher occupancy, faster when sustained
   bool catalog = false;
 };
 

@@ -126,7 +126,7 @@ int ag_set_agent_kinds(ag_ctx *ctx, const int32_t *allocator_kind, const int32_t
 /* Options (ag_set_option). */
 typedef enum ag_option {
   AG_OPT_ITEM_SEARCH = 0,  /* value: ag_item_search */
-  AG_OPT_LANE_AUCTIONS = 1 /* value: 2 (default; 16-B SoA accesses when B is even) or 1 */
+  AG_OPT_LANE_AUCTIONS = 1 /* value: 1 (default) or 2 (16-B SoA accesses when B is even) */
 } ag_option;
 
 typedef enum ag_item_search {

@@ -185,7 +185,7 @@ def test_full_size_synthetic_batch_bit_exact(gpu, oracle):
     assert np.array_equal(out["outcome"].cpu().numpy(), orc["outcome"])
     assert np.array_equal(cnt.cpu().numpy(), orc["counters_fx"])
     # the exact item scan, and one auction per lane, give the same bits
-    for exact, lanes in ((True, 1), (False, 1)):
+    for exact, lanes in ((True, 1), (False, 2)):
         eng.set_item_search(exact)
         eng.set_lane_auctions(lanes)
         out_x = eng.alloc_outputs(B)
@@ -195,7 +195,7 @@ def test_full_size_synthetic_batch_bit_exact(gpu, oracle):
             assert torch.equal(out[k], out_x[k]), (k, exact, lanes)
         assert torch.equal(cnt, cnt_x)
     eng.set_item_search(False)
-    eng.set_lane_auctions(2)
+    eng.set_lane_auctions(1)
     # batch split invariance: two halves accumulate to the same exact counters
     cnt2 = eng.new_counters()
     for lo, hi in ((0, B // 3), (B // 3, B)):

@@ -55,6 +55,20 @@ def main():
         ms = float(np.median(t))
         print(f"{name:34s} {ms:8.4f} ms  {B / ms / 1e6:9.1f} G auctions/s  "
               f"{bpa * B / ms / 1e6:8.1f} GB/s(141B)")
+    # back-to-back (sustained, as in bench.py) vs isolated launches
+    for lanes in (2, 1):
+        eng.set_item_search(False)
+        eng.set_lane_auctions(lanes)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(20)]
+        for a, b in evs:
+            a.record(st)
+            eng.simulate(inp, out, cnt)
+            b.record(st)
+        torch.cuda.synchronize()
+        t = [a.elapsed_time(b) for a, b in evs[3:]]
+        print(f"back-to-back bench, {lanes} auct/lane     mean {np.mean(t):.4f} ms  median "
+              f"{np.median(t):.4f} ms  {bpa * B / np.mean(t) / 1e6:8.1f} GB/s")
     # pure streaming reference: read 56 B + write 85 B per auction with a copy
     src = torch.empty(B * 56 // 8, dtype=torch.float64, device="cuda")
     dst = torch.empty(B * 85 // 8, dtype=torch.float64, device="cuda")
@@ -70,6 +84,15 @@ def main():
             ts.append(a.elapsed_time(b))
     ms = float(np.median(ts))
     print(f"{'torch copy+fill same bytes':34s} {ms:8.4f} ms  {bpa * B / ms / 1e6:8.1f} GB/s")
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+    for a, b in evs:
+        a.record(st)
+        dst[: src.numel()].copy_(src)
+        dst[src.numel():].fill_(1.0)
+        b.record(st)
+    torch.cuda.synchronize()
+    t = [a.elapsed_time(b) for a, b in evs[3:]]
+    print(f"{'torch copy+fill back-to-back':34s} {np.mean(t):8.4f} ms  {bpa * B / np.mean(t) / 1e6:8.1f} GB/s")
 
 
 if __name__ == "__main__":
