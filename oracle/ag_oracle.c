@@ -122,8 +122,8 @@ static void add_limbs(int64_t *L, __int128 v) {
 }
 
 /* Agent.select_item (src/Agent.py:29-42) for an OracleAllocator agent: CTR for every
- * item, first argmax of CTR * value; the true CTR (src/Auction.py:52) is the same bits
- * because Oracle agents see the true context. Returns best item; *best_ev = max. */
+ * item, first argmax of CTR * value. The same loop gives the true CTRs of
+ * src/Auction.py:52-53 (true context): *ctr_best = sigmoid of the argmax, *best_ev = max. */
 static int32_t oracle_select(const double *items, const double *vals, int32_t K, int32_t D,
                              const double *x, double *ctr_best, double *best_ev) {
   int32_t best = 0;
@@ -142,34 +142,97 @@ static int32_t oracle_select(const double *items, const double *vals, int32_t K,
   return best;
 }
 
-static void simulate_range(const ora_shape *sh, const double *items, const double *values,
-                           int64_t r0, int64_t r1, const double *ctx, const int32_t *part,
-                           const double *u, int32_t *winner, double *price, double *second_price,
-                           uint8_t *outcome, int32_t *item, double *value, double *bid,
-                           double *est_ctr, double *true_ctr, double *best_ev, double *cnt,
-                           __int128 *fx) {
-  const int32_t N = sh->N, P = sh->P, K = sh->K, E = sh->E, D = E + 1;
+/* PyTorchLogisticRegression.forward (src/Models.py:28-33) in float32: z = x . w summed in
+ * order with separately rounded products, CTR = 1 / (1 + exp(-z)) in float32 with exp
+ * rounded from the glibc double exp. torch computes the same quantities with MKL sgemv
+ * and a SIMD expf: equal up to a few float32 ulps (parity by tolerance). */
+float ora_ts_ctr(const float *w, const float *x, int32_t Do) {
+  float z = w[0] * x[0];
+  for (int32_t d = 1; d < Do; ++d) z = z + w[d] * x[d];
+  float e = (float)exp(-(double)z);
+  return 1.0f / (1.0f + e);
+}
+
+/* Gaussian shading factor of an uninitialised shading bidder (src/Bidder.py:47-58,
+ * :174-179, :351-356, :458-463): gamma = rng.normal(prev_gamma, sigma) (given raw);
+ * EmpiricalShadedBidder clips it to [0, 1]; the others keep it and log the Gaussian
+ * density as the propensity. */
+static double shading_gamma(int32_t kind, double raw) {
+  if (kind == ORA_BIDDER_EMPIRICAL) {
+    double g = raw;
+    if (g < 0.0) g = 0.0;
+    if (g > 1.0) g = 1.0;
+    return g;
+  }
+  return raw;
+}
+
+double ora_propensity(double prev_gamma, double sigma, double g) {
+  double t = (prev_gamma - g) / sigma;
+  return exp(-(t * t) / 2.0) / (sigma * sqrt(2.0 * 3.141592653589793));
+}
+
+static void simulate_range(const ora_pop *pp, const double *items, const double *values,
+                           int64_t r0, int64_t r1, const ora_in *in, const ora_out *out,
+                           double *cnt, __int128 *fx) {
+  const int32_t P = pp->P, K = pp->K, E = pp->E, D = E + 1, OE = pp->OE, Do = OE + 1;
   double x[64];
+  float xo[64];
   double bids[256];
   for (int64_t r = r0; r < r1; ++r) {
-    /* src/Auction.py:33 true context = [draws, 1.0] */
-    for (int32_t e = 0; e < E; ++e) x[e] = ctx[r * E + e];
+    /* src/Auction.py:33-36 true context = [draws, 1.0]; observed = [first OE, 1.0] */
+    for (int32_t e = 0; e < E; ++e) x[e] = in->ctx[r * E + e];
     x[E] = 1.0;
+    for (int32_t e = 0; e < OE; ++e) xo[e] = (float)x[e];
+    xo[OE] = 1.0f;
     /* src/Auction.py:44-54 per participant, in slot order */
     for (int32_t s = 0; s < P; ++s) {
-      int32_t a = part[r * P + s];
-      double c, bev;
-      int32_t it = oracle_select(items + (int64_t)a * K * D, values + (int64_t)a * K, K, D, x,
-                                 &c, &bev);
-      double v = values[(int64_t)a * K + it];
-      double b = v * c; /* TruthfulBidder.bid, src/Bidder.py:34-35 */
-      int64_t o = r * P + s;
-      item[o] = it;
-      value[o] = v;
-      bid[o] = b;
-      est_ctr[o] = c;
-      true_ctr[o] = c;
-      best_ev[o] = bev;
+      const int64_t o = r * P + s;
+      const int32_t a = in->part[o];
+      const double *it_a = items + (int64_t)a * K * D;
+      const double *v_a = values + (int64_t)a * K;
+      double ctr_t, bev;
+      const int32_t it_t = oracle_select(it_a, v_a, K, D, x, &ctr_t, &bev);
+      int32_t it;
+      double est, tru;
+      if (pp->alloc_kind[a] == ORA_ALLOCATOR_ORACLE) {
+        it = it_t;
+        est = ctr_t;
+        tru = ctr_t;
+      } else { /* LR-TS: sampled CTRs pick the item, the MAP CTR of it is the estimate */
+        const float *m = pp->ts_m + (int64_t)a * K * Do;
+        const float *nz = in->ts_noise + o * K * Do;
+        float w[64];
+        double best_s = 0.0;
+        it = 0;
+        for (int32_t k = 0; k < K; ++k) {
+          for (int32_t d = 0; d < Do; ++d) w[d] = m[k * Do + d] + (pp->ts_sample ? nz[k * Do + d] : 0.0f);
+          const double sc = (double)ora_ts_ctr(w, xo, Do) * v_a[k];
+          if (k == 0 || sc > best_s) {
+            best_s = sc;
+            it = k;
+          }
+        }
+        est = (double)ora_ts_ctr(m + it * Do, xo, Do);
+        tru = it == it_t ? ctr_t : ora_sigmoid(ora_dot(it_a + (int64_t)it * D, x, D));
+      }
+      const double v = v_a[it];
+      double b = v * est; /* Bidder.bid: value * estimated CTR (src/Bidder.py:35,49,173,...) */
+      double g = NAN, prop = NAN;
+      const int32_t bk = pp->bid_kind[a];
+      if (bk != ORA_BIDDER_TRUTHFUL) {
+        g = shading_gamma(bk, in->gamma_raw[o]);
+        if (bk != ORA_BIDDER_EMPIRICAL) prop = ora_propensity(pp->prev_gamma[a], pp->gamma_sigma[a], g);
+        b = b * g;
+      }
+      out->item[o] = it;
+      out->value[o] = v;
+      out->bid[o] = b;
+      out->est_ctr[o] = est;
+      out->true_ctr[o] = tru;
+      out->best_ev[o] = bev;
+      if (out->gamma) out->gamma[o] = g;
+      if (out->propensity) out->propensity[o] = prop;
       bids[s] = b;
     }
     int32_t w;
@@ -177,26 +240,27 @@ static void simulate_range(const ora_shape *sh, const double *items, const doubl
     top2(bids, P, &w, &m1, &m2);
     double pr, sp;
     int charged = P >= 2; /* P == 1: empty price arrays -> nobody charged (Auction.py:68) */
-    if (sh->mech == ORA_FIRST_PRICE) {
+    if (pp->mech == ORA_FIRST_PRICE) {
       pr = m1;
       sp = m2;
     } else {
       pr = m2;
       sp = m2;
     }
-    winner[r] = w;
-    price[r] = charged ? pr : NAN;
-    second_price[r] = charged ? sp : NAN;
-    int32_t oc = ora_bernoulli(true_ctr[r * P + w], u[r]);
-    outcome[r] = (uint8_t)oc;
+    out->winner[r] = w;
+    out->price[r] = charged ? pr : NAN;
+    out->second_price[r] = charged ? sp : NAN;
+    int32_t oc = ora_bernoulli(out->true_ctr[r * P + w], in->u[r]);
+    out->outcome[r] = (uint8_t)oc;
     /* Agent.charge / set_price (src/Agent.py:70-77) and the metric getters
      * (src/Agent.py:96-118) per log record. */
     for (int32_t s = 0; s < P; ++s) {
       int64_t o = r * P + s;
-      int32_t a = part[o];
+      int32_t a = in->part[o];
       int won = charged && s == w;
       double lp = charged ? pr : 0.0;  /* logged price */
       double lsp = won ? sp : 0.0;     /* logged second price */
+      const double *est_ctr = out->est_ctr, *true_ctr = out->true_ctr, *value = out->value;
       double tv = true_ctr[o] * value[o];
       double t[ORA_NUM_COUNTERS];
       memset(t, 0, sizeof t);
@@ -208,13 +272,13 @@ static void simulate_range(const ora_shape *sh, const double *items, const doubl
         t[ORA_C_PAID] = pr;
         t[ORA_C_CTR_BIAS] = est_ctr[o] / true_ctr[o];
       }
-      t[ORA_C_ALLOC_REGRET] = best_ev[o] - tv;
+      t[ORA_C_ALLOC_REGRET] = out->best_ev[o] - tv;
       t[ORA_C_EST_REGRET] = est_ctr[o] * value[o] - tv;
       t[ORA_C_OVERBID] = (lp - lsp) * (double)won;
-      t[ORA_C_UNDERBID] = (lp - bid[o]) * (double)(!won) * (double)(lp < tv);
+      t[ORA_C_UNDERBID] = (lp - out->bid[o]) * (double)(!won) * (double)(lp < tv);
       double d = true_ctr[o] - est_ctr[o];
       t[ORA_C_CTR_SQERR] = d * d;
-      t[ORA_C_BEST_EV] = best_ev[o];
+      t[ORA_C_BEST_EV] = out->best_ev[o];
       t[ORA_C_N_LOGS] = 1.0;
       double *C = cnt + (int64_t)a * ORA_NUM_COUNTERS;
       for (int c = 0; c < ORA_NUM_COUNTERS; ++c) C[c] += t[c];
@@ -226,15 +290,12 @@ static void simulate_range(const ora_shape *sh, const double *items, const doubl
       }
     }
   }
-  (void)N;
 }
 
-void ora_simulate(const ora_shape *s, const double *items, const double *values, int64_t B,
-                  const double *ctx, const int32_t *part, const double *u, int32_t *winner,
-                  double *price, double *second_price, uint8_t *outcome, int32_t *item,
-                  double *value, double *bid, double *est_ctr, double *true_ctr, double *best_ev,
-                  double *counters, int64_t *counters_fx, int32_t nthreads) {
-  const int64_t NC = (int64_t)s->N * ORA_NUM_COUNTERS;
+void ora_simulate_pop(const ora_pop *pp, const double *items, const double *values, int64_t B,
+                      const ora_in *in, const ora_out *out, double *counters, int64_t *counters_fx,
+                      int32_t nthreads) {
+  const int64_t NC = (int64_t)pp->N * ORA_NUM_COUNTERS;
   if (nthreads < 1) nthreads = 1;
   double *part_cnt = (double *)calloc((size_t)nthreads * NC, sizeof(double));
   __int128 *part_fx = (__int128 *)calloc((size_t)nthreads * NC, sizeof(__int128));
@@ -246,8 +307,7 @@ void ora_simulate(const ora_shape *s, const double *items, const double *values,
     int t = 0, nt = 1;
 #endif
     int64_t r0 = B * t / nt, r1 = B * (t + 1) / nt;
-    simulate_range(s, items, values, r0, r1, ctx, part, u, winner, price, second_price, outcome,
-                   item, value, bid, est_ctr, true_ctr, best_ev, part_cnt + (int64_t)t * NC,
+    simulate_range(pp, items, values, r0, r1, in, out, part_cnt + (int64_t)t * NC,
                    part_fx + (int64_t)t * NC);
   }
   for (int t = 0; t < nthreads; ++t)
@@ -257,6 +317,22 @@ void ora_simulate(const ora_shape *s, const double *items, const double *values,
     }
   free(part_cnt);
   free(part_fx);
+}
+
+void ora_simulate(const ora_shape *s, const double *items, const double *values, int64_t B,
+                  const double *ctx, const int32_t *part, const double *u, int32_t *winner,
+                  double *price, double *second_price, uint8_t *outcome, int32_t *item,
+                  double *value, double *bid, double *est_ctr, double *true_ctr, double *best_ev,
+                  double *counters, int64_t *counters_fx, int32_t nthreads) {
+  int32_t *ak = (int32_t *)calloc((size_t)s->N, sizeof(int32_t));
+  int32_t *bk = (int32_t *)calloc((size_t)s->N, sizeof(int32_t));
+  ora_pop pp = {s->N, s->P, s->K, s->E, s->E, s->mech, ak, bk, NULL, NULL, NULL, 0};
+  ora_in in = {ctx, part, u, NULL, NULL};
+  ora_out out = {winner, price, second_price, outcome, item, value, bid, est_ctr, true_ctr,
+                 best_ev, NULL, NULL};
+  ora_simulate_pop(&pp, items, values, B, &in, &out, counters, counters_fx, nthreads);
+  free(ak);
+  free(bk);
 }
 
 /* ---- synthetic batch generator (integer part), restating ag_generate ---- */

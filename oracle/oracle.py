@@ -28,6 +28,24 @@ class _Shape(ctypes.Structure):
                 ("E", ctypes.c_int32), ("mech", ctypes.c_int32)]
 
 
+class _Pop(ctypes.Structure):
+    _fields_ = [("N", ctypes.c_int32), ("P", ctypes.c_int32), ("K", ctypes.c_int32),
+                ("E", ctypes.c_int32), ("OE", ctypes.c_int32), ("mech", ctypes.c_int32),
+                ("alloc_kind", ctypes.c_void_p), ("bid_kind", ctypes.c_void_p),
+                ("prev_gamma", ctypes.c_void_p), ("gamma_sigma", ctypes.c_void_p),
+                ("ts_m", ctypes.c_void_p), ("ts_sample", ctypes.c_int32)]
+
+
+class _In(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("ctx", "part", "u", "gamma_raw", "ts_noise")]
+
+
+class _Out(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("winner", "price", "second_price", "outcome",
+                                              "item", "value", "bid", "est_ctr", "true_ctr",
+                                              "best_ev", "gamma", "propensity")]
+
+
 def build():
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
 
@@ -50,6 +68,11 @@ def lib():
         L.ora_allocate.argtypes = [i32, vp, i64, i32, vp, vp, vp]
         L.ora_simulate.restype = None
         L.ora_simulate.argtypes = [ctypes.POINTER(_Shape), vp, vp, i64, vp, vp, vp] + [vp] * 12 + [i32]
+        L.ora_simulate_pop.restype = None
+        L.ora_simulate_pop.argtypes = [ctypes.POINTER(_Pop), vp, vp, i64, ctypes.POINTER(_In),
+                                       ctypes.POINTER(_Out), vp, vp, i32]
+        L.ora_ts_ctr.restype = ctypes.c_float
+        L.ora_ts_ctr.argtypes = [vp, vp, i32]
         L.ora_to_fx.restype = i64
         L.ora_to_fx.argtypes = [d]
         L.ora_gen_uniform.restype = d
@@ -104,6 +127,53 @@ def simulate(mech, items, values, ctx, part, u, nthreads=1):
                        _p(out["outcome"]), _p(out["item"]), _p(out["value"]), _p(out["bid"]),
                        _p(out["est_ctr"]), _p(out["true_ctr"]), _p(out["best_ev"]),
                        _p(out["counters"]), _p(out["counters_fx"]), int(nthreads))
+    return out
+
+
+def simulate_pop(mech, items, values, ctx, part, u, alloc_kind, bid_kind, prev_gamma=None,
+                 gamma_sigma=None, OE=None, ts_m=None, ts_noise=None, gamma_raw=None,
+                 ts_sample=True, nthreads=1):
+    """General population (OracleAllocator / LR-TS allocators; truthful / shading bidders in
+    their first iteration). Row-major replay inputs; returns outputs + counters."""
+    items = np.ascontiguousarray(items, np.float64)
+    values = np.ascontiguousarray(values, np.float64)
+    ctx = np.ascontiguousarray(ctx, np.float64)
+    part = np.ascontiguousarray(part, np.int32)
+    u = np.ascontiguousarray(u, np.float64)
+    N, K, D = items.shape
+    B, P = part.shape
+    E = ctx.shape[1]
+    OE = E if OE is None else OE
+    keep = []
+
+    def arr(a, dt):
+        if a is None:
+            return None
+        a = np.ascontiguousarray(a, dt)
+        keep.append(a)
+        return a
+
+    ak, bk = arr(alloc_kind, np.int32), arr(bid_kind, np.int32)
+    pg = arr(prev_gamma if prev_gamma is not None else np.ones(N), np.float64)
+    gs = arr(gamma_sigma if gamma_sigma is not None else np.ones(N), np.float64)
+    tm = arr(ts_m if ts_m is not None else np.zeros((N, K, OE + 1)), np.float32)
+    gr = arr(gamma_raw if gamma_raw is not None else np.full((B, P), np.nan), np.float64)
+    tn = arr(ts_noise if ts_noise is not None else np.zeros((B, P, K, OE + 1)), np.float32)
+    pop = _Pop(N, P, K, E, OE, int(mech), ak.ctypes.data, bk.ctypes.data, pg.ctypes.data,
+               gs.ctypes.data, tm.ctypes.data, int(bool(ts_sample)))
+    out = dict(winner=np.empty(B, np.int32), price=np.empty(B), second_price=np.empty(B),
+               outcome=np.empty(B, np.uint8), item=np.empty((B, P), np.int32),
+               value=np.empty((B, P)), bid=np.empty((B, P)), est_ctr=np.empty((B, P)),
+               true_ctr=np.empty((B, P)), best_ev=np.empty((B, P)), gamma=np.empty((B, P)),
+               propensity=np.empty((B, P)), counters=np.zeros((N, NUM_COUNTERS)),
+               counters_fx=np.zeros((N, NUM_COUNTERS, 3), np.int64))
+    cin = _In(ctx.ctypes.data, part.ctypes.data, u.ctypes.data, gr.ctypes.data, tn.ctypes.data)
+    cout = _Out(*[out[k].ctypes.data for k in ("winner", "price", "second_price", "outcome", "item",
+                                               "value", "bid", "est_ctr", "true_ctr", "best_ev",
+                                               "gamma", "propensity")])
+    lib().ora_simulate_pop(ctypes.byref(pop), _p(items), _p(values), B, ctypes.byref(cin),
+                           ctypes.byref(cout), _p(out["counters"]), _p(out["counters_fx"]),
+                           int(nthreads))
     return out
 
 

@@ -49,3 +49,15 @@ def gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU visible")
     return torch.device("cuda", 0)
+
+
+POP_CAPTURES = ("sp_ts_r2048", "fp_dr_ts_r1024", "fp_dm_ts_r1024", "fp_ips_ts_r1024",
+                "fp_dm_oracle_r1024", "fp_empirical_r2048")
+
+
+def pop_args(d, meta):
+    """Population + replay inputs of a capture, in the oracle's keyword form."""
+    from auctiongym_amd.population import kinds_from_names
+    ak, bk, pg, gs = kinds_from_names(meta["allocators"], meta["bidders"], meta["bidder_kwargs"])
+    return dict(alloc_kind=ak, bid_kind=bk, prev_gamma=pg, gamma_sigma=gs, OE=meta["OE"],
+                ts_m=d.get("ts_m"), ts_noise=d.get("ts_noise"), gamma_raw=d["gamma_raw"])

@@ -99,13 +99,26 @@ def oracle_truthful_cfg(n_agents, n_items, P, allocation, seed, E=5, OE=4, var=1
     }
 
 
-def capture(cfg, rounds):
-    """Run `rounds` reference rounds (one iteration) and record replay inputs + outputs."""
+def _bidder_kind(b):
+    return type(b).__name__
+
+
+def capture(cfg, rounds, torch_seed=0, keep=False):
+    """Run `rounds` reference rounds (one iteration) and record replay inputs + outputs.
+
+    Replay inputs beyond ctx/part/u, per (round, slot):
+      gamma_raw  the raw rng.normal(prev_gamma, gamma_sigma) draw of an uninitialised shading
+                 bidder (src/Bidder.py:51,177,354,461), NaN for bidders that draw nothing;
+      ts_noise   [K][OE+1] float32 output of torch.normal in PyTorchLogisticRegression.forward
+                 (src/Models.py:31) for Thompson-sampling agents, 0 otherwise.
+    """
     import main as M
+    import torch
     path = write_cfg(cfg)
     (rng, config, agent_configs, agents2items, agents2item_values, num_runs, max_slots,
      E, var, OE) = M.parse_config(path)
     os.unlink(path)
+    torch.manual_seed(torch_seed)
     agents = M.instantiate_agents(rng, agent_configs, agents2item_values, agents2items)
     auction, _, _, _ = M.instantiate_auction(rng, config, agents2items, agents2item_values,
                                              agents, max_slots, E, var, OE)
@@ -114,6 +127,19 @@ def capture(cfg, rounds):
     names = [a.name for a in agents]
     items = np.stack([agents2items[n] for n in names])          # [N][K][D]
     values = np.stack([agents2item_values[n] for n in names])   # [N][K]
+    K = items.shape[1]
+    is_ts = [type(a.allocator).__name__ == "PyTorchLogisticRegressionAllocator" for a in agents]
+    Do = None
+    ts_m = ts_q = None
+    if any(is_ts):
+        Do = agents[is_ts.index(True)].allocator.response_model.m.shape[1]
+        ts_m = np.zeros((N, K, Do), np.float32)
+        ts_q = np.ones((N, K, Do), np.float32)
+        for i, a in enumerate(agents):
+            if is_ts[i]:
+                ts_m[i] = a.allocator.response_model.m.detach().numpy()
+                ts_q[i] = a.allocator.response_model.q.numpy()
+    shading = [hasattr(a.bidder, "prev_gamma") for a in agents]
 
     clone = np.random.Generator(np.random.PCG64())
     clone.bit_generator.state = rng.bit_generator.state
@@ -127,12 +153,24 @@ def capture(cfg, rounds):
         return w, p, s
 
     auction.allocation.allocate = wrapped
+    noise_log = []
+    orig_normal = torch.normal
+
+    def rec_normal(*a, **k):
+        t = orig_normal(*a, **k)
+        noise_log.append(t.detach().numpy().copy())
+        return t
+
+    torch.normal = rec_normal
 
     ctx = np.zeros((rounds, E))
     part = np.zeros((rounds, P), np.int32)
     u = np.zeros(rounds)
+    gamma_raw = np.full((rounds, P), np.nan)
+    ts_noise = np.zeros((rounds, P, K, Do), np.float32) if Do else None
     rec = {k: np.zeros((rounds, P)) for k in
-           ("bid", "est_ctr", "true_ctr", "best_ev", "value", "price", "second_price")}
+           ("bid", "est_ctr", "true_ctr", "best_ev", "value", "price", "second_price", "gamma",
+            "propensity")}
     item = np.zeros((rounds, P), np.int32)
     won = np.zeros((rounds, P), np.int8)
     outcome_slot = np.zeros((rounds, P), np.int8)
@@ -141,37 +179,58 @@ def capture(cfg, rounds):
     second = np.full(rounds, np.nan)
     outcome = np.zeros(rounds, np.int8)
 
-    for r in range(rounds):
-        # replay order (see module docstring)
-        c = clone.normal(0, var, size=E)
-        pa = clone.choice(N, P, replace=False)
-        uu = clone.random()
-        auction.simulate_opportunity()
-        assert clone.bit_generator.state == rng.bit_generator.state, f"draw order diverged at round {r}"
-        ctx[r] = c
-        part[r] = pa
-        u[r] = uu
-        for s, a in enumerate(pa):
-            lg = agents[a].logs[-1]
-            rec["bid"][r, s] = lg.bid
-            rec["est_ctr"][r, s] = lg.estimated_CTR
-            rec["true_ctr"][r, s] = lg.true_CTR
-            rec["best_ev"][r, s] = lg.best_expected_value
-            rec["value"][r, s] = lg.value
-            rec["price"][r, s] = lg.price
-            rec["second_price"][r, s] = lg.second_price
-            item[r, s] = lg.item
-            won[r, s] = bool(lg.won)
-            outcome_slot[r, s] = bool(lg.outcome)
-        bids, w, p, s2 = alloc_log[-1]
-        assert np.array_equal(bids, rec["bid"][r])
-        winner[r] = w[0]
-        if len(p):
-            price[r] = p[0]
-        if len(s2):
-            second[r] = s2[0]
-        if len(p):
-            outcome[r] = outcome_slot[r, w[0]]
+    try:
+        for r in range(rounds):
+            # replay order (see module docstring)
+            c = clone.normal(0, var, size=E)
+            pa = clone.choice(N, P, replace=False)
+            for s_, a_ in enumerate(pa):
+                b = agents[a_].bidder
+                if shading[a_] and not getattr(b, "model_initialised", False):
+                    gamma_raw[r, s_] = clone.normal(b.prev_gamma, b.gamma_sigma)
+            uu = clone.random()
+            n0 = len(noise_log)
+            auction.simulate_opportunity()
+            assert clone.bit_generator.state == rng.bit_generator.state, f"draw order diverged at round {r}"
+            ctx[r] = c
+            part[r] = pa
+            u[r] = uu
+            nts = [s_ for s_, a_ in enumerate(pa) if is_ts[a_]]
+            assert len(noise_log) - n0 == len(nts)
+            for j, s_ in enumerate(nts):
+                ts_noise[r, s_] = noise_log[n0 + j]
+            for s, a in enumerate(pa):
+                lg = agents[a].logs[-1]
+                rec["bid"][r, s] = lg.bid
+                rec["est_ctr"][r, s] = lg.estimated_CTR
+                rec["true_ctr"][r, s] = lg.true_CTR
+                rec["best_ev"][r, s] = lg.best_expected_value
+                rec["value"][r, s] = lg.value
+                rec["price"][r, s] = lg.price
+                rec["second_price"][r, s] = lg.second_price
+                if shading[a]:
+                    g = agents[a].bidder.gammas[-1]
+                    rec["gamma"][r, s] = float(g)
+                    pr = getattr(agents[a].bidder, "propensities", [np.nan])[-1] \
+                        if hasattr(agents[a].bidder, "propensities") else np.nan
+                    rec["propensity"][r, s] = float(pr)
+                else:
+                    rec["gamma"][r, s] = np.nan
+                    rec["propensity"][r, s] = np.nan
+                item[r, s] = lg.item
+                won[r, s] = bool(lg.won)
+                outcome_slot[r, s] = bool(lg.outcome)
+            bids, w, p, s2 = alloc_log[-1]
+            assert np.array_equal(bids, rec["bid"][r])
+            winner[r] = w[0]
+            if len(p):
+                price[r] = p[0]
+            if len(s2):
+                second[r] = s2[0]
+            if len(p):
+                outcome[r] = outcome_slot[r, w[0]]
+    finally:
+        torch.normal = orig_normal
 
     agg = {
         "net_utility": [a.net_utility for a in agents],
@@ -190,10 +249,17 @@ def capture(cfg, rounds):
     }
     arrays = dict(items=items, values=values, ctx=ctx, part=part, u=u, item=item, won=won,
                   winner=winner, price=price, second_price=second, outcome=outcome,
-                  **{"slot_" + k: v for k, v in rec.items()})
-    meta = dict(N=N, P=P, K=items.shape[1], E=E, OE=OE, var=var, rounds=rounds,
-                allocation=config["allocation"], seed=config["random_seed"],
-                rng_state_after_setup=None)
+                  gamma_raw=gamma_raw, **{"slot_" + k: v for k, v in rec.items()})
+    if Do:
+        arrays.update(ts_noise=ts_noise, ts_m=ts_m, ts_q=ts_q)
+    meta = dict(N=N, P=P, K=K, E=E, OE=OE, var=var, rounds=rounds,
+                allocation=config["allocation"], seed=config["random_seed"], torch_seed=torch_seed,
+                allocators=[type(a.allocator).__name__ for a in agents],
+                bidders=[_bidder_kind(a.bidder) for a in agents],
+                bidder_kwargs=[c["bidder"]["kwargs"] for c in agent_configs],
+                ts_dim=Do)
+    if keep:
+        return arrays, agg, meta, (agents, auction, rng)
     return arrays, agg, meta
 
 
@@ -235,6 +301,61 @@ def alloc_kats():
         out[f"P{P}_bids"] = bids
     np.savez_compressed(os.path.join(OUT, "alloc_kat.npz"), **out)
     print("wrote alloc_kat", len(out))
+
+
+def lrts_update_kat(agents, out_name):
+    """LR-TS Agent.update (src/Agent.py:79-94 -> src/BidderAllocation.py:29-65) on the logs of
+    the captured iteration: inputs, the loss and gradient of the first epoch (the model's own
+    loss/backward), the per-epoch loss trajectory (recorded by the scheduler shim), and the
+    updated m, q, prev_m."""
+    import torch
+    import BidderAllocation as BA
+    traj = []
+
+    class RecRP(torch.optim.lr_scheduler.ReduceLROnPlateau):
+        def __init__(self, *a, verbose=None, **k):
+            super().__init__(*a, **k)
+
+        def step(self, metrics, *a, **k):
+            traj.append(float(metrics))
+            return super().step(metrics, *a, **k)
+
+    saved = torch.optim.lr_scheduler.ReduceLROnPlateau
+    torch.optim.lr_scheduler.ReduceLROnPlateau = RecRP
+    out = {}
+    try:
+        for i, a in enumerate(agents):
+            if not isinstance(a.allocator, BA.PyTorchLogisticRegressionAllocator):
+                continue
+            rm = a.allocator.response_model
+            contexts = np.array(list(opp.context for opp in a.logs))
+            items = np.array(list(opp.item for opp in a.logs))
+            outcomes = np.array(list(opp.outcome for opp in a.logs))
+            won = np.array(list(opp.won for opp in a.logs))
+            X, A, y = contexts[won], items[won], outcomes[won]
+            out[f"a{i}_X"] = X
+            out[f"a{i}_A"] = A.astype(np.int64)
+            out[f"a{i}_y"] = y.astype(np.float64)
+            out[f"a{i}_m0"] = rm.m.detach().numpy().copy()
+            out[f"a{i}_prevm0"] = rm.prev_iter_m.numpy().copy()
+            out[f"a{i}_q0"] = rm.q.numpy().copy()
+            # epoch-0 loss and gradient through the reference's own model code
+            Xt, At, yt = torch.Tensor(X), torch.LongTensor(A), torch.Tensor(y)
+            rm.zero_grad()
+            loss = rm.loss(torch.squeeze(rm.predict_item(Xt, At)), yt)
+            loss.backward()
+            out[f"a{i}_loss0"] = np.array(float(loss.item()))
+            out[f"a{i}_grad0"] = rm.m.grad.detach().numpy().copy()
+            rm.zero_grad()
+            traj.clear()
+            a.update(iteration=0)
+            out[f"a{i}_losses"] = np.array(traj, np.float64)
+            out[f"a{i}_m1"] = rm.m.detach().numpy().copy()
+            out[f"a{i}_q1"] = rm.q.numpy().copy()
+            print("lrts update agent", i, "samples", len(y), "epochs", len(traj), flush=True)
+    finally:
+        torch.optim.lr_scheduler.ReduceLROnPlateau = saved
+    np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
 
 
 def sigmoid_kats():
@@ -311,6 +432,23 @@ def main():
     # 5. Non-default catalogue shape: K=5 items, E=5.
     a, g, m = capture(oracle_truthful_cfg(5, 5, 2, "FirstPrice", seed=14), 1024)
     save_capture("fp_oracle_n5_k5", a, g, m)
+
+    # 6. SP_Truthful_TS.json as shipped: LR-TS Thompson sampling (torch seeded 0, noise
+    #    recorded), 2048 rounds of iteration 0, then the LR-TS update KATs on those logs.
+    a, g, m, (agents, _, _) = capture(load_cfg("SP_Truthful_TS.json"), 2048, keep=True)
+    save_capture("sp_ts_r2048", a, g, m)
+    lrts_update_kat(agents, "sp_ts_update_kat")
+    # 7. Learned bidders in their first (uninitialised) iteration: Gaussian shading draws.
+    for cfg_name, tag in (("FP_DR_TS.json", "fp_dr_ts_r1024"), ("FP_DM_TS.json", "fp_dm_ts_r1024"),
+                          ("FP_IPS_TS.json", "fp_ips_ts_r1024"), ("FP_DM_Oracle.json", "fp_dm_oracle_r1024")):
+        a, g, m = capture(load_cfg(cfg_name), 1024)
+        save_capture(tag, a, g, m)
+    # 8. EmpiricalShadedBidder with Oracle CTRs (clipped Gaussian shading, src/Bidder.py:38-58).
+    cfg = oracle_truthful_cfg(6, 12, 2, "FirstPrice", seed=15)
+    cfg["agents"][0]["bidder"] = {"type": "EmpiricalShadedBidder",
+                                  "kwargs": {"gamma_sigma": 0.05, "init_gamma": 0.9}}
+    a, g, m = capture(cfg, 2048)
+    save_capture("fp_empirical_r2048", a, g, m)
 
     if args.full:
         agg = full_run_aggregates("SP_Oracle.json")

@@ -141,3 +141,49 @@ def test_sp_oracle_full_run_known_answers(oracle, tmp_path):
             assert np.all(cnt[:, C["overbid_regret"]] == 0.0)
             total += cnt[:, C["paid"]].sum()
     np.testing.assert_allclose(total, 247455.77552418958, rtol=1e-12)
+
+
+# ---- populations beyond Oracle + Truthful (LR-TS allocators, shading bidders) ----
+from conftest import POP_CAPTURES, pop_args  # noqa: E402
+
+TS_EST_RTOL = 2.0 ** -21  # torch's float32 sgemv + SIMD sigmoid vs the restated float32 path
+
+
+@pytest.mark.parametrize("name", POP_CAPTURES)
+def test_population_matches_reference(oracle, name):
+    d, meta, agg = load_capture(name)
+    o = oracle.simulate_pop(mech_code(meta), d["items"], d["values"], d["ctx"], d["part"], d["u"],
+                            **pop_args(d, meta))
+    ts = any(a == "PyTorchLogisticRegressionAllocator" for a in meta["allocators"])
+    # the true-CTR side is FP64 libm arithmetic: bit-exact for every population
+    assert np.array_equal(o["true_ctr"], d["slot_true_ctr"])
+    assert np.array_equal(o["best_ev"], d["slot_best_ev"])
+    assert np.array_equal(o["item"], d["item"])
+    assert np.array_equal(o["winner"], d["winner"])
+    shading = ~np.isnan(d["slot_gamma"])
+    assert np.array_equal(o["gamma"][shading], d["slot_gamma"][shading])
+    prop = ~np.isnan(d["slot_propensity"])
+    np.testing.assert_allclose(o["propensity"][prop], d["slot_propensity"][prop], rtol=1e-15)
+    if ts:
+        # float32 dot of an LR-TS model: a few float32 ulps of the largest term
+        np.testing.assert_allclose(o["est_ctr"], d["slot_est_ctr"], rtol=TS_EST_RTOL, atol=1e-7)
+        np.testing.assert_allclose(o["bid"], d["slot_bid"], rtol=2 * TS_EST_RTOL, atol=2e-7)
+        np.testing.assert_allclose(o["price"], d["price"], rtol=2 * TS_EST_RTOL, atol=2e-7)
+        assert np.mean(o["est_ctr"] == d["slot_est_ctr"]) > 0.85  # most bits identical
+    else:
+        assert np.array_equal(o["bid"], d["slot_bid"])
+        assert np.array_equal(o["price"], d["price"], equal_nan=True)
+        assert np.array_equal(o["est_ctr"], d["slot_est_ctr"])
+    assert np.array_equal(o["outcome"], d["outcome"])
+    C = {n: i for i, n in enumerate(oracle.COUNTERS)}
+    cnt = o["counters"]
+    rt = dict(rtol=1e-5, atol=1e-6)  # north star: 1e-5 relative for welfare / regret
+    np.testing.assert_allclose(cnt[:, C["net"]], agg["net_utility"], **rt)
+    np.testing.assert_allclose(cnt[:, C["gross"]], agg["gross_utility"], **rt)
+    np.testing.assert_allclose(cnt[:, C["paid"]].sum(), agg["revenue"], **rt)
+    for c in ("allocation_regret", "estimation_regret", "overbid_regret", "underbid_regret"):
+        np.testing.assert_allclose(cnt[:, C[c]], agg[c], **rt)
+    n = cnt[:, C["n_logs"]]
+    np.testing.assert_allclose(np.sqrt(cnt[:, C["ctr_sqerr"]] / n), agg["ctr_rmse"], rtol=1e-5)
+    won = cnt[:, C["n_won"]]
+    np.testing.assert_allclose(cnt[:, C["ctr_bias_sum"]] / won, agg["ctr_bias"], rtol=1e-5)
