@@ -11,8 +11,9 @@ LIB_PATH = os.path.join(_HERE, "libauctiongym_hip.so")
 
 AG_OK, AG_ERR_INVALID, AG_ERR_UNSUPPORTED, AG_ERR_HIP, AG_ERR_STATE = 0, -1, -2, -3, -4
 FIRST_PRICE, SECOND_PRICE = 0, 1
-ALLOCATOR_ORACLE = 0
-BIDDER_TRUTHFUL = 0
+ALLOCATOR_ORACLE, ALLOCATOR_LRTS = 0, 1
+BIDDER_TRUTHFUL, BIDDER_EMPIRICAL_SHADED, BIDDER_VALUE_LEARNING = 0, 1, 2
+BIDDER_POLICY_LEARNING, BIDDER_DOUBLY_ROBUST = 3, 4
 OPT_ITEM_SEARCH = 0
 OPT_LANE_AUCTIONS = 1
 ITEM_SEARCH_AUTO, ITEM_SEARCH_EXACT = 0, 1
@@ -24,10 +25,11 @@ NUM_COUNTERS = len(COUNTERS)
 FX_FRAC_BITS, FX_LIMB_BITS, FX_LIMBS = 36, 42, 3
 
 # Every symbol include/auctiongym.h declares (tests check the .so exports all of them).
-EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_option", "ag_load_catalog",
-           "ag_allocate",
-           "ag_simulate", "ag_generate", "ag_counters_to_double", "ag_sigmoid", "ag_exp",
-           "ag_last_error", "ag_abi_version")
+EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params", "ag_load_lrts",
+           "ag_set_option", "ag_load_catalog", "ag_allocate", "ag_simulate", "ag_generate",
+           "ag_generate_noise", "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_last_error",
+           "ag_abi_version")
+ABI_VERSION = 2
 
 
 class AgShape(ctypes.Structure):
@@ -39,14 +41,16 @@ class AgShape(ctypes.Structure):
 
 
 class AgBatchIn(ctypes.Structure):
-    _fields_ = [("ctx", ctypes.c_void_p), ("part", ctypes.c_void_p), ("u", ctypes.c_void_p)]
+    _fields_ = [("ctx", ctypes.c_void_p), ("part", ctypes.c_void_p), ("u", ctypes.c_void_p),
+                ("gamma_raw", ctypes.c_void_p), ("ts_noise", ctypes.c_void_p)]
 
 
 class AgBatchOut(ctypes.Structure):
     _fields_ = [("winner", ctypes.c_void_p), ("price", ctypes.c_void_p),
                 ("second_price", ctypes.c_void_p), ("outcome", ctypes.c_void_p),
                 ("item", ctypes.c_void_p), ("bid", ctypes.c_void_p), ("est_ctr", ctypes.c_void_p),
-                ("true_ctr", ctypes.c_void_p), ("best_ev", ctypes.c_void_p)]
+                ("true_ctr", ctypes.c_void_p), ("best_ev", ctypes.c_void_p),
+                ("gamma", ctypes.c_void_p), ("propensity", ctypes.c_void_p)]
 
 
 class AgError(RuntimeError):
@@ -66,6 +70,8 @@ def load(path=None):
         raise AgError(f"{path} is missing: build it with `make -C auction-gym_amd` "
                       "(or __graft_entry__.build()); there is no CPU fallback")
     L = ctypes.CDLL(path)
+    if L.ag_abi_version() != ABI_VERSION:
+        raise AgError(f"{path}: ABI {L.ag_abi_version()} != {ABI_VERSION}; rebuild it")
     vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
     sig = {
         "ag_create": (ctypes.c_int, [i32, ctypes.POINTER(AgShape), ctypes.POINTER(vp)]),
@@ -73,6 +79,9 @@ def load(path=None):
         "ag_set_agent_kinds": (ctypes.c_int, [vp, vp, vp]),
         "ag_load_catalog": (ctypes.c_int, [vp, vp, vp]),
         "ag_set_option": (ctypes.c_int, [vp, i32, i64]),
+        "ag_set_agent_params": (ctypes.c_int, [vp, vp, vp, vp, vp]),
+        "ag_load_lrts": (ctypes.c_int, [vp, vp, vp, i32]),
+        "ag_generate_noise": (ctypes.c_int, [vp, u64, u64, i64, vp, vp, vp, vp]),
         "ag_allocate": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, vp]),
         "ag_simulate": (ctypes.c_int, [vp, i64, ctypes.POINTER(AgBatchIn),
                                        ctypes.POINTER(AgBatchOut), vp, vp]),

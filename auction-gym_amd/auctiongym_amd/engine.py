@@ -18,7 +18,8 @@ NUM_COUNTERS = _lib.NUM_COUNTERS
 FX_LIMBS = _lib.FX_LIMBS
 
 _OUT_FIELDS = ("winner", "price", "second_price", "outcome", "item", "bid", "est_ctr",
-               "true_ctr", "best_ev")
+               "true_ctr", "best_ev", "gamma", "propensity")
+_CORE_FIELDS = _OUT_FIELDS[:9]
 
 
 def _ptr(t):
@@ -77,6 +78,29 @@ class AuctionEngine:
         assert a.shape == (self.N,) and b.shape == (self.N,)
         self._check(self.L.ag_set_agent_kinds(self._h, a.ctypes.data, b.ctypes.data), "ag_set_agent_kinds")
 
+    def set_agent_params(self, allocator_kinds, bidder_kinds, prev_gamma=None, gamma_sigma=None):
+        """Plugin kinds + shading parameters (ag_set_agent_params)."""
+        a = np.ascontiguousarray(allocator_kinds, np.int32)
+        b = np.ascontiguousarray(bidder_kinds, np.int32)
+        pg = None if prev_gamma is None else np.ascontiguousarray(prev_gamma, np.float64)
+        gs = None if gamma_sigma is None else np.ascontiguousarray(gamma_sigma, np.float64)
+        self.shading = bool((b != _lib.BIDDER_TRUTHFUL).any())
+        self.lrts = bool((a == _lib.ALLOCATOR_LRTS).any())
+        self._check(self.L.ag_set_agent_params(self._h, a.ctypes.data, b.ctypes.data,
+                                               None if pg is None else pg.ctypes.data,
+                                               None if gs is None else gs.ctypes.data),
+                    "ag_set_agent_params")
+
+    def load_lrts(self, m, q, thompson_sampling=True):
+        """LR-TS posteriors m, q float32 [N][K][OE+1] (ag_load_lrts)."""
+        m = np.ascontiguousarray(m, np.float32)
+        q = np.ascontiguousarray(q, np.float32)
+        if m.shape != (self.N, self.K, self.OE + 1) or q.shape != m.shape:
+            raise ValueError(f"LR-TS params must be [N][K][OE+1] = ({self.N},{self.K},{self.OE + 1})")
+        self.ts_sample = bool(thompson_sampling)
+        self._check(self.L.ag_load_lrts(self._h, m.ctypes.data, q.ctypes.data, int(self.ts_sample)),
+                    "ag_load_lrts")
+
     def set_item_search(self, exact):
         """exact=True: score every item in FP64 (the reference loop); False (default): f32
         screen + exact re-score of the near-best items -- identical results."""
@@ -100,17 +124,26 @@ class AuctionEngine:
     # ---------------------------------------------------------------- buffers
     def alloc_inputs(self, B):
         d = self.device
-        return {"ctx": torch.empty((self.E, B), dtype=torch.float64, device=d),
-                "part": torch.empty((self.P, B), dtype=torch.int32, device=d),
-                "u": torch.empty((B,), dtype=torch.float64, device=d)}
+        inp = {"ctx": torch.empty((self.E, B), dtype=torch.float64, device=d),
+               "part": torch.empty((self.P, B), dtype=torch.int32, device=d),
+               "u": torch.empty((B,), dtype=torch.float64, device=d)}
+        if getattr(self, "shading", False):
+            inp["gamma_raw"] = torch.empty((self.P, B), dtype=torch.float64, device=d)
+        if getattr(self, "lrts", False) and getattr(self, "ts_sample", True):
+            inp["ts_noise"] = torch.empty((self.P, self.K * (self.OE + 1), B), dtype=torch.float32,
+                                          device=d)
+        return inp
 
-    def alloc_outputs(self, B, fields=_OUT_FIELDS):
+    def alloc_outputs(self, B, fields=None):
+        if fields is None:
+            fields = _OUT_FIELDS if getattr(self, "shading", False) else _CORE_FIELDS
         d, P = self.device, self.P
         spec = {"winner": ((B,), torch.int32), "price": ((B,), torch.float64),
                 "second_price": ((B,), torch.float64), "outcome": ((B,), torch.uint8),
                 "item": ((P, B), torch.int32), "bid": ((P, B), torch.float64),
                 "est_ctr": ((P, B), torch.float64), "true_ctr": ((P, B), torch.float64),
-                "best_ev": ((P, B), torch.float64)}
+                "best_ev": ((P, B), torch.float64), "gamma": ((P, B), torch.float64),
+                "propensity": ((P, B), torch.float64)}
         return {k: torch.empty(spec[k][0], dtype=spec[k][1], device=d) for k in fields}
 
     def new_counters(self):
@@ -124,7 +157,8 @@ class AuctionEngine:
                 raise ValueError(f"input {k} must be a contiguous tensor on {self.device}")
         if inputs["ctx"].shape != (self.E, B) or inputs["part"].shape != (self.P, B):
             raise ValueError("inputs must be SoA: ctx [E][B], part [P][B], u [B]")
-        bi = AgBatchIn(_ptr(inputs["ctx"]).value, _ptr(inputs["part"]).value, _ptr(inputs["u"]).value)
+        bi = AgBatchIn(_ptr(inputs["ctx"]).value, _ptr(inputs["part"]).value, _ptr(inputs["u"]).value,
+                       _ptr(inputs.get("gamma_raw")).value, _ptr(inputs.get("ts_noise")).value)
         bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
         self._check(self.L.ag_simulate(self._h, B, ctypes.byref(bi), ctypes.byref(bo),
                                  _ptr(counters), _stream()), "ag_simulate")
@@ -133,6 +167,14 @@ class AuctionEngine:
         B = inputs["u"].shape[0]
         self._check(self.L.ag_generate(self._h, int(seed), int(first_auction), B, _ptr(inputs["ctx"]),
                                  _ptr(inputs["part"]), _ptr(inputs["u"]), _stream()), "ag_generate")
+
+    def generate_noise(self, seed, first_auction, inputs):
+        """Synthetic gamma_raw / ts_noise for the participants already in inputs["part"]."""
+        B = inputs["u"].shape[0]
+        self._check(self.L.ag_generate_noise(self._h, int(seed), int(first_auction), B,
+                                             _ptr(inputs["part"]), _ptr(inputs.get("gamma_raw")),
+                                             _ptr(inputs.get("ts_noise")), _stream()),
+                    "ag_generate_noise")
 
     def allocate(self, bids):
         """Batched allocate: bids [P][B] (device, float64) -> winner, price, second_price."""

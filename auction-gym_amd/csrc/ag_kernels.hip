@@ -236,6 +236,62 @@ __global__ __launch_bounds__(kThreads) void k_generate(uint64_t seed, uint64_t f
   }
 }
 
+// Synthetic per-participant noise (streams 3 and 4 + slot of the same Philox key/counter
+// scheme): shading bidders' gamma_raw = prev_gamma + sigma * z (numpy normal(loc, scale)),
+// LR-TS agents' ts_noise = z * (1 / sqrt(q)) (torch.normal(0, 1 / sqrt(q)), src/Models.py:31).
+__device__ __forceinline__ void box_muller(const uint32_t (&w)[4], double &z0, double &z1) {
+  const double u1 = (double)(((((uint64_t)w[0] << 32) | w[1]) >> 11) + 1) * 0x1p-53;
+  const double u2 = (double)((((uint64_t)w[2] << 32) | w[3]) >> 11) * 0x1p-53;
+  const double r = sqrt(-2.0 * log(u1));
+  double sn, cs;
+  sincospi(2.0 * u2, &sn, &cs);
+  z0 = r * cs;
+  z1 = r * sn;
+}
+
+__global__ __launch_bounds__(kThreads) void k_generate_noise(uint64_t seed, uint64_t first, int64_t B, int P,
+                                                            int KDo, const int32_t *part,
+                                                            const int32_t *akind, const int32_t *bkind,
+                                                            const double *pg, const double *gs,
+                                                            const float *q, double *gamma_raw,
+                                                            float *ts_noise) {
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < B;
+       i += (int64_t)gridDim.x * kThreads) {
+    const uint64_t idx = first + (uint64_t)i;
+    const uint32_t c0 = (uint32_t)idx, c1 = (uint32_t)(idx >> 32);
+    for (int s = 0; s < P; ++s) {
+      const int a = part[(int64_t)s * B + i];
+      uint32_t w[4];
+      double z0, z1;
+      if (gamma_raw) {
+        if (bkind[a] != AG_BIDDER_TRUTHFUL) {
+          philox(c0, c1, (uint32_t)s, 3, k0, k1, w);
+          box_muller(w, z0, z1);
+          gamma_raw[(int64_t)s * B + i] = pg[a] + gs[a] * z0;
+        } else {
+          gamma_raw[(int64_t)s * B + i] = NAN;
+        }
+      }
+      if (ts_noise) {
+        const bool lr = akind[a] == AG_ALLOCATOR_LRTS;
+        for (int j = 0; j < KDo; j += 2) {
+          if (lr) {
+            philox(c0, c1, (uint32_t)(j >> 1), 4 + (uint32_t)s, k0, k1, w);
+            box_muller(w, z0, z1);
+          } else {
+            z0 = z1 = 0.0;
+          }
+          const float *qa = q + (size_t)a * KDo;
+          ts_noise[((int64_t)s * KDo + j) * B + i] = lr ? (float)z0 * (1.0f / sqrtf(qa[j])) : 0.0f;
+          if (j + 1 < KDo)
+            ts_noise[((int64_t)s * KDo + j + 1) * B + i] = lr ? (float)z1 * (1.0f / sqrtf(qa[j + 1])) : 0.0f;
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // known-answer kernels
 // ------------------------------------------------------------------------------------
@@ -250,16 +306,16 @@ __global__ __launch_bounds__(kThreads) void k_exp_kat(const double *x, double *y
 // ------------------------------------------------------------------------------------
 // dispatch
 // ------------------------------------------------------------------------------------
-SimKernel pick_kernel(int P, int D, bool prune, int W) {
+SimKernel pick_kernel(int P, int D, bool prune, int W, bool general) {
   switch (P) {
-    case 1: return pick_kernel_for<1>(D, prune, W);
-    case 2: return pick_kernel_for<2>(D, prune, W);
-    case 3: return pick_kernel_for<3>(D, prune, W);
-    case 4: return pick_kernel_for<4>(D, prune, W);
-    case 5: return pick_kernel_for<5>(D, prune, W);
-    case 6: return pick_kernel_for<6>(D, prune, W);
-    case 7: return pick_kernel_for<7>(D, prune, W);
-    case 8: return pick_kernel_for<8>(D, prune, W);
+    case 1: return pick_kernel_for<1>(D, prune, W, general);
+    case 2: return pick_kernel_for<2>(D, prune, W, general);
+    case 3: return pick_kernel_for<3>(D, prune, W, general);
+    case 4: return pick_kernel_for<4>(D, prune, W, general);
+    case 5: return pick_kernel_for<5>(D, prune, W, general);
+    case 6: return pick_kernel_for<6>(D, prune, W, general);
+    case 7: return pick_kernel_for<7>(D, prune, W, general);
+    case 8: return pick_kernel_for<8>(D, prune, W, general);
     default: return nullptr;
   }
 }
@@ -286,9 +342,16 @@ struct ag_ctx {
   double *d_values = nullptr;
   int64_t *d_partials = nullptr;
   int32_t partial_blocks = 0;
-  int32_t resident[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // resident blocks [W][screened][counters]
+  int32_t resident[16] = {};  // resident blocks [general][W][screened][counters]
   bool wide = false;  // 1 auction per lane by default: higher occupancy, faster when sustained
   bool catalog = false;
+  // general populations (anything beyond OracleAllocator + TruthfulBidder)
+  bool general = false, has_lrts = false, has_shading = false, lrts_loaded = false;
+  int32_t ts_sample = 1;
+  int32_t *d_akind = nullptr, *d_bkind = nullptr;
+  double *d_pg = nullptr, *d_gs = nullptr;
+  float *d_tsm = nullptr, *d_tsq = nullptr;
+  float *h_tsq = nullptr;  // host copy of q for the synthetic generator
 };
 
 namespace {
@@ -337,7 +400,7 @@ int ag_create(int32_t device, const ag_shape *s, ag_ctx **out) {
   // simulate needs a kernel for (P, D) and the catalogue in LDS; allocate-only contexts
   // (any P) do not.
   const LdsLayout lay = make_layout(s->num_agents, s->num_items, D, true);
-  c->can_simulate = s->num_participants <= kMaxP && pick_kernel(s->num_participants, D, false, 1) &&
+  c->can_simulate = s->num_participants <= kMaxP && pick_kernel(s->num_participants, D, false, 1, false) &&
                     lay.total <= 160 * 1024;
   DeviceGuard g(device);
   hipError_t e = hipMalloc(&c->d_items, sizeof(double) * s->num_agents * s->num_items * D);
@@ -346,10 +409,23 @@ int ag_create(int32_t device, const ag_shape *s, ag_ctx **out) {
   // <= kMaxAuctionsPerBlock auctions per block; allocate lazily beyond the default.
   c->partial_blocks = kMaxSimGrid;
   if (e == hipSuccess) e = hipMalloc(&c->d_partials, sizeof(int64_t) * 2 * (size_t)kMaxSimGrid * nc);
+  const size_t nkd = (size_t)s->num_agents * s->num_items * (s->obs_embedding_size + 1);
+  if (e == hipSuccess) e = hipMalloc(&c->d_akind, sizeof(int32_t) * s->num_agents);
+  if (e == hipSuccess) e = hipMalloc(&c->d_bkind, sizeof(int32_t) * s->num_agents);
+  if (e == hipSuccess) e = hipMalloc(&c->d_pg, sizeof(double) * s->num_agents);
+  if (e == hipSuccess) e = hipMalloc(&c->d_gs, sizeof(double) * s->num_agents);
+  if (e == hipSuccess) e = hipMalloc(&c->d_tsm, sizeof(float) * nkd);
+  if (e == hipSuccess) e = hipMalloc(&c->d_tsq, sizeof(float) * nkd);
   if (e != hipSuccess) {
     (void)hipFree(c->d_items);
     (void)hipFree(c->d_values);
     (void)hipFree(c->d_partials);
+    (void)hipFree(c->d_akind);
+    (void)hipFree(c->d_bkind);
+    (void)hipFree(c->d_pg);
+    (void)hipFree(c->d_gs);
+    (void)hipFree(c->d_tsm);
+    (void)hipFree(c->d_tsq);
     delete c;
     return set_error(AG_ERR_HIP, "ag_create: hipMalloc: %s", hipGetErrorString(e));
   }
@@ -363,18 +439,81 @@ int ag_destroy(ag_ctx *c) {
   (void)hipFree(c->d_items);
   (void)hipFree(c->d_values);
   (void)hipFree(c->d_partials);
+  (void)hipFree(c->d_akind);
+  (void)hipFree(c->d_bkind);
+  (void)hipFree(c->d_pg);
+  (void)hipFree(c->d_gs);
+  (void)hipFree(c->d_tsm);
+  (void)hipFree(c->d_tsq);
+  delete[] c->h_tsq;
   delete c;
+  return AG_OK;
+}
+
+int ag_set_agent_params(ag_ctx *c, const int32_t *alloc_kind, const int32_t *bid_kind,
+                        const double *prev_gamma, const double *gamma_sigma) {
+  if (!c) return set_error(AG_ERR_INVALID, "ag_set_agent_params: null ctx");
+  const int N = c->shape.num_agents;
+  bool general = false, lrts = false, shading = false;
+  for (int a = 0; a < N; ++a) {
+    const int ak = alloc_kind ? alloc_kind[a] : AG_ALLOCATOR_ORACLE;
+    const int bk = bid_kind ? bid_kind[a] : AG_BIDDER_TRUTHFUL;
+    if (ak != AG_ALLOCATOR_ORACLE && ak != AG_ALLOCATOR_LRTS)
+      return set_error(AG_ERR_UNSUPPORTED, "agent %d: allocator kind %d not implemented", a, ak);
+    if (bk < AG_BIDDER_TRUTHFUL || bk > AG_BIDDER_DOUBLY_ROBUST)
+      return set_error(AG_ERR_UNSUPPORTED, "agent %d: bidder kind %d not implemented", a, bk);
+    if (bk != AG_BIDDER_TRUTHFUL && (!prev_gamma || !gamma_sigma))
+      return set_error(AG_ERR_INVALID, "agent %d: shading bidder needs prev_gamma and gamma_sigma", a);
+    if (bk != AG_BIDDER_TRUTHFUL && !(gamma_sigma[a] > 0.0))
+      return set_error(AG_ERR_INVALID, "agent %d: gamma_sigma must be > 0", a);
+    lrts |= ak == AG_ALLOCATOR_LRTS;
+    shading |= bk != AG_BIDDER_TRUTHFUL;
+  }
+  general = lrts || shading;
+  if (general && (c->D > 8 || c->shape.obs_embedding_size + 1 > kMaxD))
+    return set_error(AG_ERR_UNSUPPORTED, "general populations support E+1 <= 8 (D=%d)", c->D);
+  DeviceGuard g(c->device);
+  int32_t *ak = new int32_t[N], *bk = new int32_t[N];
+  double *pg = new double[N], *gs = new double[N];
+  for (int a = 0; a < N; ++a) {
+    ak[a] = alloc_kind ? alloc_kind[a] : AG_ALLOCATOR_ORACLE;
+    bk[a] = bid_kind ? bid_kind[a] : AG_BIDDER_TRUTHFUL;
+    pg[a] = prev_gamma ? prev_gamma[a] : 1.0;
+    gs[a] = gamma_sigma ? gamma_sigma[a] : 1.0;
+  }
+  hipError_t e = hipMemcpy(c->d_akind, ak, sizeof(int32_t) * N, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c->d_bkind, bk, sizeof(int32_t) * N, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c->d_pg, pg, sizeof(double) * N, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c->d_gs, gs, sizeof(double) * N, hipMemcpyHostToDevice);
+  delete[] ak;
+  delete[] bk;
+  delete[] pg;
+  delete[] gs;
+  if (e != hipSuccess) return set_error(AG_ERR_HIP, "ag_set_agent_params: %s", hipGetErrorString(e));
+  c->general = general;
+  c->has_lrts = lrts;
+  c->has_shading = shading;
   return AG_OK;
 }
 
 int ag_set_agent_kinds(ag_ctx *c, const int32_t *alloc_kind, const int32_t *bid_kind) {
   if (!c) return set_error(AG_ERR_INVALID, "ag_set_agent_kinds: null ctx");
-  for (int a = 0; a < c->shape.num_agents; ++a) {
-    if (alloc_kind && alloc_kind[a] != AG_ALLOCATOR_ORACLE)
-      return set_error(AG_ERR_UNSUPPORTED, "agent %d: allocator kind %d not implemented", a, alloc_kind[a]);
+  for (int a = 0; a < c->shape.num_agents; ++a)
     if (bid_kind && bid_kind[a] != AG_BIDDER_TRUTHFUL)
-      return set_error(AG_ERR_UNSUPPORTED, "agent %d: bidder kind %d not implemented", a, bid_kind[a]);
-  }
+      return set_error(AG_ERR_INVALID, "agent %d: shading bidders need ag_set_agent_params", a);
+  return ag_set_agent_params(c, alloc_kind, bid_kind, nullptr, nullptr);
+}
+
+int ag_load_lrts(ag_ctx *c, const float *m, const float *q, int32_t thompson_sampling) {
+  if (!c || !m || !q) return set_error(AG_ERR_INVALID, "ag_load_lrts: null argument");
+  DeviceGuard g(c->device);
+  const size_t n = (size_t)c->shape.num_agents * c->shape.num_items * (c->shape.obs_embedding_size + 1);
+  AG_HIP(hipMemcpy(c->d_tsm, m, n * sizeof(float), hipMemcpyHostToDevice));
+  AG_HIP(hipMemcpy(c->d_tsq, q, n * sizeof(float), hipMemcpyHostToDevice));
+  if (!c->h_tsq) c->h_tsq = new float[n];
+  memcpy(c->h_tsq, q, n * sizeof(float));
+  c->ts_sample = thompson_sampling ? 1 : 0;
+  c->lrts_loaded = true;
   return AG_OK;
 }
 
@@ -450,27 +589,43 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   const int nc = s.num_agents * kC;
   const int D = c->D;
   const bool prune = c->item_search == AG_ITEM_SEARCH_AUTO && D <= 8 && s.num_items <= 2 * kMaxKPairs;
+  if (c->has_lrts && !c->lrts_loaded)
+    return set_error(AG_ERR_STATE, "ag_simulate: LR-TS agents need ag_load_lrts");
+  if (c->has_lrts && c->ts_sample && !in->ts_noise)
+    return set_error(AG_ERR_INVALID, "ag_simulate: Thompson sampling needs ts_noise");
+  if (c->has_shading && !in->gamma_raw)
+    return set_error(AG_ERR_INVALID, "ag_simulate: shading bidders need gamma_raw");
   SimParams prm;
   prm.B = B;
   prm.N = s.num_agents;
   prm.K = s.num_items;
   prm.mech = s.mechanism;
   prm.want_counters = counters_fx != nullptr;
-  prm.lds = make_layout(s.num_agents, s.num_items, D, prm.want_counters);
+  prm.lds = make_layout(s.num_agents, s.num_items, D, prm.want_counters, c->general,
+                        s.obs_embedding_size + 1);
+  prm.ts_sample = c->ts_sample;
+  prm.akind = c->d_akind;
+  prm.bkind = c->d_bkind;
+  prm.pg = c->d_pg;
+  prm.gs = c->d_gs;
+  prm.tsm = c->d_tsm;
   prm.items = c->d_items;
   prm.values = c->d_values;
   prm.in = *in;
   prm.out = *out;
   prm.partials = c->d_partials;
-  const int W = (prune && (B % 2) == 0 && c->wide) ? 2 : 1;
-  SimKernel k = pick_kernel(s.num_participants, D, prune, W);
+  const int W = (prune && (B % 2) == 0 && c->wide && !c->general) ? 2 : 1;
+  SimKernel k = pick_kernel(s.num_participants, D, prune, W, c->general);
+  if (!k) return set_error(AG_ERR_UNSUPPORTED, "ag_simulate: no kernel for P=%d D=%d", s.num_participants, D);
   const size_t lds = (size_t)prm.lds.total;
+  if (lds > 160 * 1024)
+    return set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
   hipStream_t st = (hipStream_t)stream;
   if (lds > 64 * 1024)
     AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   // Persistent grid: exactly the blocks the device keeps resident (no partial last round),
   // each striding over 256-auction tiles.
-  int &res = c->resident[(W == 2 ? 4 : 0) + (prune ? 2 : 0) + (prm.want_counters ? 1 : 0)];
+  int &res = c->resident[(c->general ? 8 : 0) + (W == 2 ? 4 : 0) + (prune ? 2 : 0) + (prm.want_counters ? 1 : 0)];
   if (res == 0) {
     int per_cu = 0, cus = 0;
     AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k, kThreads, lds));
@@ -505,6 +660,22 @@ int ag_generate(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, double *ctx
   hipLaunchKernelGGL(k_generate, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, seed, first, B,
                      c->shape.num_agents, c->shape.num_participants, c->shape.embedding_size,
                      c->shape.embedding_var, ctx_out, part_out, u_out);
+  AG_HIP(hipGetLastError());
+  return AG_OK;
+}
+
+int ag_generate_noise(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, const int32_t *part,
+                      double *gamma_raw, float *ts_noise, void *stream) {
+  if (!c || !part) return set_error(AG_ERR_INVALID, "ag_generate_noise: null argument");
+  if (B < 0) return set_error(AG_ERR_INVALID, "ag_generate_noise: B < 0");
+  if (B == 0) return AG_OK;
+  if (ts_noise && !c->lrts_loaded) return set_error(AG_ERR_STATE, "ag_generate_noise: ag_load_lrts first");
+  DeviceGuard g(c->device);
+  const int grid = grid_for(B, (int64_t)1 << 40);
+  const int KDo = c->shape.num_items * (c->shape.obs_embedding_size + 1);
+  hipLaunchKernelGGL(k_generate_noise, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, seed, first, B,
+                     c->shape.num_participants, KDo, part, c->d_akind, c->d_bkind, c->d_pg, c->d_gs,
+                     c->d_tsq, gamma_raw, ts_noise);
   AG_HIP(hipGetLastError());
   return AG_OK;
 }

@@ -74,7 +74,7 @@ __device__ __forceinline__ unsigned long long to_fx(double x) {
 
 // LDS carve of k_simulate (all pieces 16-B aligned; offsets in bytes).
 struct LdsLayout {
-  int32_t tab, items, values, scr, scr_val, amax, cnt, total;
+  int32_t tab, items, values, scr, scr_val, amax, akind, bkind, pg, gs, tsm, cnt, total;
   int32_t items_stride;    // doubles between agents (odd: spreads agents over banks)
   int32_t values_stride;   // doubles
   int32_t scr_stride;      // floats between agents in the screening catalogue
@@ -82,20 +82,25 @@ struct LdsLayout {
   int32_t kpairs;          // item pairs in the screening catalogue (K rounded up to even)
   int32_t replicas;        // per-lane counter replicas (power of 2, <= 64)
   int32_t ncnt;            // counter slots held in LDS
+  int32_t ts_do;           // LR-TS model width OE + 1 (general populations)
 };
 
 __host__ inline int32_t align16(int64_t b) { return (int32_t)((b + 15) & ~(int64_t)15); }
 
-// Counter slots accumulated in LDS for OracleAllocator + TruthfulBidder populations:
+// Counter slots accumulated in LDS (all exact fixed-point sums):
 //   0 GROSS, 1 PAID, 2 OVERBID (FirstPrice only: price - second_price == 0 under SP),
-//   3 UNDERBID, 4 BEST_EV, 5 packed counts (n_logs in bits 0-31, n_won in bits 32-63).
-// Derived at write-out: NET = GROSS - PAID (both exact fixed-point sums), CTR_BIAS =
-// N_WON (est/true == 1 for Oracle agents); ALLOC / EST regrets and CTR_SQERR are
-// identically zero for them (estimated CTR == true CTR, best_ev == true_ctr * value).
+//   3 UNDERBID, 4 BEST_EV, 5 packed counts (n_logs in bits 0-31, n_won in bits 32-63),
+//   general populations only: 6 ALLOC_REGRET, 7 EST_REGRET, 8 CTR_SQERR, 9 CTR_BIAS.
+// Derived at write-out: NET = GROSS - PAID. For OracleAllocator + TruthfulBidder
+// populations the general slots are identically 0 (estimated CTR == true CTR and best_ev
+// == true_ctr * value bit for bit) and CTR_BIAS == N_WON (est/true == 1): not accumulated.
 constexpr int kOracleSlots = 6;
-enum { kSlotGross = 0, kSlotPaid, kSlotOverbid, kSlotUnderbid, kSlotBestEv, kSlotCounts };
+constexpr int kGeneralSlots = 10;
+enum { kSlotGross = 0, kSlotPaid, kSlotOverbid, kSlotUnderbid, kSlotBestEv, kSlotCounts,
+       kSlotAlloc, kSlotEst, kSlotSqerr, kSlotBias };
 
-__host__ inline LdsLayout make_layout(int N, int K, int D, bool counters) {
+__host__ inline LdsLayout make_layout(int N, int K, int D, bool counters, bool general = false,
+                                      int ts_do = 0) {
   LdsLayout L;
   L.items_stride = (K * D) | 1;
   L.values_stride = K | 1;
@@ -103,7 +108,8 @@ __host__ inline LdsLayout make_layout(int N, int K, int D, bool counters) {
   // [pair][dim 0..7][2 items] floats; + 4 floats so agents start on different 16-B slots
   L.scr_stride = L.kpairs * 16 + 4;
   L.scr_val_stride = L.kpairs * 2 + 2;
-  L.ncnt = kOracleSlots;
+  L.ncnt = general ? kGeneralSlots : kOracleSlots;
+  L.ts_do = general ? ts_do : 0;
   int R = 64;
   while (R > 1 && (int64_t)R * N * L.ncnt * 8 > 32768) R >>= 1;
   L.replicas = R;
@@ -120,6 +126,16 @@ __host__ inline LdsLayout make_layout(int N, int K, int D, bool counters) {
   b = L.scr_val + (int64_t)N * L.scr_val_stride * 4;
   L.amax = align16(b);
   b = L.amax + (int64_t)N * 4;
+  L.akind = align16(b);
+  b = L.akind + (general ? (int64_t)N * 4 : 0);
+  L.bkind = align16(b);
+  b = L.bkind + (general ? (int64_t)N * 4 : 0);
+  L.pg = align16(b);
+  b = L.pg + (general ? (int64_t)N * 8 : 0);
+  L.gs = align16(b);
+  b = L.gs + (general ? (int64_t)N * 8 : 0);
+  L.tsm = align16(b);
+  b = L.tsm + (general ? (int64_t)N * K * ts_do * 4 : 0);
   L.cnt = align16(b);
   b = L.cnt + (counters ? (int64_t)R * N * L.ncnt * 8 : 0);
   L.total = align16(b);
@@ -130,12 +146,18 @@ struct SimParams {
   int32_t B;              // auctions in this launch (< 2^28: 32-bit SoA indexing)
   int32_t N, K, mech;
   int32_t want_counters;
+  int32_t ts_sample;      // general: LR-TS agents add ts_noise to m for the item choice
   LdsLayout lds;
   const double *items;    // global [N][K][D]
   const double *values;   // global [N][K]
+  const int32_t *akind;   // general: [N] ag_allocator_kind
+  const int32_t *bkind;   // general: [N] ag_bidder_kind
+  const double *pg;       // general: [N] prev_gamma of shading bidders
+  const double *gs;       // general: [N] gamma_sigma
+  const float *tsm;       // general: [N][K][OE+1] LR-TS posterior means
   ag_batch_in in;
   ag_batch_out out;
-  int64_t *partials;      // [grid][N][AG_NUM_COUNTERS]
+  int64_t *partials;      // [grid][N][AG_NUM_COUNTERS][2]
 };
 
 // Screening margin. The screen ranks items by t_k = (1 + 2^(z'_k)) / v_k = 1 / (exact
@@ -291,20 +313,48 @@ struct Lds {
   const double *items, *vals;
   const float *scr, *scr_val, *amax;
   int items_stride, values_stride, scr_stride, scr_val_stride, kpairs;
+  // general populations
+  const int32_t *akind, *bkind;
+  const double *pg, *gs;
+  const float *tsm;
+  int ts_do;
 };
 
 // One auction resolved (src/Auction.py:28-74 minus the draws).
 template <int P>
 struct Resolved {
   int ag[P], item[P];
-  double val[P], bid[P], ctr[P], bev[P];
+  double val[P], bid[P], ctr[P], est[P], bev[P], gamma[P], prop[P];
   int w, oc;
   double price, second;
 };
 
-template <int P, int D, bool PRUNE>
+// PyTorchLogisticRegression forward CTR in float32 (src/Models.py:28-33), the oracle's
+// ora_ts_ctr: products rounded separately and summed in order, exp from the glibc-identical
+// double exp rounded to float, then 1 / (1 + e) in float.
+__device__ __forceinline__ float ts_ctr(const float *w, const float *x, int Do, const float *nz,
+                                        uint32_t nz_stride, const uint64_t *tab) {
+  float z = 0.0f;
+  for (int d = 0; d < Do; ++d) {
+    const float wd = nz ? w[d] + nz[(uint32_t)d * nz_stride] : w[d];
+    const float t = wd * x[d];
+    z = d == 0 ? t : z + t;
+  }
+  const float e = (float)agexp::exp(-(double)z, tab);
+  return 1.0f / (1.0f + e);
+}
+
+// Gaussian density of a shading factor (src/Bidder.py:178, :355, :462).
+__device__ __forceinline__ double shading_propensity(double pg, double sigma, double g,
+                                                     const uint64_t *tab) {
+  const double t = (pg - g) / sigma;
+  return agexp::exp(-(t * t) / 2.0, tab) / (sigma * 2.5066282746310002);  // sqrt(2 pi)
+}
+
+template <int P, int D, bool PRUNE, bool GENERAL>
 __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const double (&x)[kMaxD],
                                         const float (&xf)[kMaxD], float xabs, const int (&ag)[P], double u,
+                                        const ag_batch_in &in, uint32_t B, uint32_t i, bool ts_sample,
                                         Resolved<P> &r) {
   double m1 = 0.0, m2 = -INFINITY;
   int w = 0;
@@ -312,17 +362,64 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
   for (int s = 0; s < P; ++s) {
     const int a = ag[s];
     r.ag[s] = a;
+    // true CTRs (src/Auction.py:52-53): exact search on the true context; for an Oracle
+    // agent this IS Agent.select_item (src/BidderAllocation.py:81-82)
     double c, bs;
-    const int best = select_item<D, PRUNE>(T.items + a * T.items_stride, T.vals + a * T.values_stride,
-                                           T.scr + a * T.scr_stride, T.scr_val + a * T.scr_val_stride,
-                                           PRUNE ? T.amax[a] : 0.0f, K, T.kpairs, x, xf, xabs, T.tab, c, bs);
+    const double *itm = T.items + a * T.items_stride;
+    const int best_t = select_item<D, PRUNE>(itm, T.vals + a * T.values_stride,
+                                             T.scr + a * T.scr_stride, T.scr_val + a * T.scr_val_stride,
+                                             PRUNE ? T.amax[a] : 0.0f, K, T.kpairs, x, xf, xabs, T.tab, c, bs);
+    int best = best_t;
+    double est = c, tru = c;
+    double g = NAN, prop = NAN;
+    if constexpr (GENERAL) {
+      if (T.akind[a] == AG_ALLOCATOR_LRTS) {
+        // LR-TS (src/Agent.py:29-42): the sampled CTRs on the observed context pick the
+        // item by first argmax of CTR * value (float32 CTR widened to double), the MAP CTR
+        // of that item is the estimate
+        const int Do = T.ts_do;
+        float xo[kMaxD];
+        for (int d = 0; d < Do - 1; ++d) xo[d] = (float)x[d];
+        xo[Do - 1] = 1.0f;
+        const float *m = T.tsm + (size_t)a * K * Do;
+        const float *nz = (ts_sample && in.ts_noise) ? in.ts_noise + (size_t)s * K * Do * B + i : nullptr;
+        double best_sc = 0.0;
+        best = 0;
+        for (int k = 0; k < K; ++k) {
+          const float ck = ts_ctr(m + k * Do, xo, Do, nz ? nz + (size_t)k * Do * B : nullptr, B, T.tab);
+          const double sc = (double)ck * T.vals[a * T.values_stride + k];
+          if (k == 0 || sc > best_sc) {
+            best_sc = sc;
+            best = k;
+          }
+        }
+        est = (double)ts_ctr(m + best * Do, xo, Do, nullptr, 0, T.tab);
+        tru = best == best_t ? c : agexp::sigmoid(dot_ref<D>(itm + best * D, x), T.tab);
+      }
+    }
     const double v = T.vals[a * T.values_stride + best];
-    const double b = v * c;  // TruthfulBidder.bid (src/Bidder.py:34-35)
+    double b = v * est;  // Bidder.bid: value * estimated CTR (src/Bidder.py:35, :49, :173, ...)
+    if constexpr (GENERAL) {
+      const int bk = T.bkind[a];
+      if (bk != AG_BIDDER_TRUTHFUL) {
+        g = in.gamma_raw[s * B + i];
+        if (bk == AG_BIDDER_EMPIRICAL_SHADED) {  // clipped to [0, 1] (src/Bidder.py:52-55)
+          if (g < 0.0) g = 0.0;
+          if (g > 1.0) g = 1.0;
+        } else {
+          prop = shading_propensity(T.pg[a], T.gs[a], g, T.tab);
+        }
+        b = b * g;  // bid *= gamma
+      }
+    }
     r.item[s] = best;
     r.val[s] = v;
     r.bid[s] = b;
-    r.ctr[s] = c;   // Oracle: estimated CTR == true CTR, bit for bit
-    r.bev[s] = bs;  // max_k true_CTR_k * value_k (src/Auction.py:52-53)
+    r.ctr[s] = tru;
+    r.est[s] = est;
+    r.bev[s] = bs;  // max_k true_CTR_k * value_k (src/Auction.py:53)
+    r.gamma[s] = g;
+    r.prop[s] = prop;
     // streaming top-2, ties -> lowest slot (src/AuctionAllocation.py:19-34)
     if (s == 0) {
       m1 = b;
@@ -341,10 +438,10 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
 #pragma unroll
   for (int s = 1; s < P; ++s)
     if (s == w) ctr_w = r.ctr[s];
-  r.oc = bernoulli(ctr_w, u);  // src/Auction.py:65
+  r.oc = bernoulli(ctr_w, u);  // src/Auction.py:65 (true CTR of the winner's item)
 }
 
-template <int P, int D, bool PRUNE, int W>
+template <int P, int D, bool PRUNE, int W, bool GENERAL>
 __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = prm.N, K = prm.K;
@@ -356,9 +453,23 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
   float *s_scr = reinterpret_cast<float *>(smem + L.scr);
   float *s_scr_val = reinterpret_cast<float *>(smem + L.scr_val);
   float *s_amax = reinterpret_cast<float *>(smem + L.amax);
+  int32_t *s_akind = reinterpret_cast<int32_t *>(smem + L.akind);
+  int32_t *s_bkind = reinterpret_cast<int32_t *>(smem + L.bkind);
+  double *s_pg = reinterpret_cast<double *>(smem + L.pg);
+  double *s_gs = reinterpret_cast<double *>(smem + L.gs);
+  float *s_tsm = reinterpret_cast<float *>(smem + L.tsm);
   unsigned long long *s_cnt = reinterpret_cast<unsigned long long *>(smem + L.cnt);
 
   const int tid = threadIdx.x;
+  if constexpr (GENERAL) {
+    for (int a = tid; a < N; a += kThreads) {
+      s_akind[a] = prm.akind[a];
+      s_bkind[a] = prm.bkind[a];
+      s_pg[a] = prm.pg[a];
+      s_gs[a] = prm.gs[a];
+    }
+    for (int j = tid; j < N * K * L.ts_do; j += kThreads) s_tsm[j] = prm.tsm[j];
+  }
   for (int i = tid; i < 256; i += kThreads) s_tab[i] = ag_exp_tab[i];
   for (int i = tid; i < N * K * D; i += kThreads) {
     const int a = i / (K * D), r = i - a * (K * D);
@@ -393,7 +504,7 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
   __syncthreads();
 
   const Lds T{s_tab, s_items, s_vals, s_scr, s_scr_val, s_amax, L.items_stride, L.values_stride,
-              L.scr_stride, L.scr_val_stride, L.kpairs};
+              L.scr_stride, L.scr_val_stride, L.kpairs, s_akind, s_bkind, s_pg, s_gs, s_tsm, L.ts_do};
   const int rep = tid & (R - 1);
   const ag_batch_in in = prm.in;
   const ag_batch_out out = prm.out;
@@ -430,7 +541,8 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
       int ag[P];
 #pragma unroll
       for (int s = 0; s < P; ++s) ag[s] = pv[s][q];
-      resolve<P, D, PRUNE>(T, K, prm.mech, x, xf, xabs, ag, uv[q], r[q]);
+      resolve<P, D, PRUNE, GENERAL>(T, K, prm.mech, x, xf, xabs, ag, uv[q], in, B, i + q,
+                                    prm.ts_sample != 0, r[q]);
     }
 
     // SoA stores, W auctions per access
@@ -438,19 +550,24 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
     for (int s = 0; s < P; ++s) {
       const uint32_t o = s * B + i;
       int iv[W];
-      double bv[W], cv[W], ev[W];
+      double bv[W], cv[W], sv[W], ev[W], gv[W], pv2[W];
 #pragma unroll
       for (int q = 0; q < W; ++q) {
         iv[q] = r[q].item[s];
         bv[q] = r[q].bid[s];
         cv[q] = r[q].ctr[s];
+        sv[q] = r[q].est[s];
         ev[q] = r[q].bev[s];
+        gv[q] = r[q].gamma[s];
+        pv2[q] = r[q].prop[s];
       }
       if (out.item) st_i32<W>(out.item + o, iv);
       if (out.bid) st_f64<W>(out.bid + o, bv);
-      if (out.est_ctr) st_f64<W>(out.est_ctr + o, cv);
+      if (out.est_ctr) st_f64<W>(out.est_ctr + o, sv);
       if (out.true_ctr) st_f64<W>(out.true_ctr + o, cv);
       if (out.best_ev) st_f64<W>(out.best_ev + o, ev);
+      if (out.gamma) st_f64<W>(out.gamma + o, gv);
+      if (out.propensity) st_f64<W>(out.propensity + o, pv2);
     }
     {
       int wv[W], ov[W];
@@ -496,6 +613,13 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
           }
           add_raw(kSlotBestEv, rr.ag[s], to_fx(rr.bev[s]));
           add_raw(kSlotCounts, rr.ag[s], won ? 0x100000001ull : 1ull);
+          if constexpr (GENERAL) {  // src/Agent.py:96-118 terms that vanish for Oracle agents
+            add_nz(kSlotAlloc, rr.ag[s], to_fx(rr.bev[s] - tv));
+            add_nz(kSlotEst, rr.ag[s], to_fx(rr.est[s] * rr.val[s] - tv));
+            const double dd = rr.ctr[s] - rr.est[s];
+            add_nz(kSlotSqerr, rr.ag[s], to_fx(dd * dd));
+            if (won) add_raw(kSlotBias, rr.ag[s], to_fx(rr.est[s] / rr.ctr[s]));
+          }
         }
       }
     }
@@ -504,9 +628,12 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
   if (prm.want_counters) {
     __syncthreads();
     for (int a = tid; a < N; a += kThreads) {
-      long long lo[kOracleSlots], hi[kOracleSlots];
+      long long lo[kGeneralSlots], hi[kGeneralSlots];
       unsigned long long nlogs = 0, nwon = 0;
-      for (int j = 0; j < kOracleSlots; ++j) {
+      for (int j = 0; j < kGeneralSlots; ++j) {
+        lo[j] = 0;
+        hi[j] = 0;
+        if (j >= L.ncnt) continue;
         lo[j] = 0;
         hi[j] = 0;
         for (int r = 0; r < R; ++r) {
@@ -531,12 +658,15 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
       };
       put(AG_C_NET, lo[kSlotGross] - lo[kSlotPaid], hi[kSlotGross] - hi[kSlotPaid]);
       put(AG_C_GROSS, lo[kSlotGross], hi[kSlotGross]);
-      put(AG_C_ALLOC_REGRET, 0, 0);
-      put(AG_C_EST_REGRET, 0, 0);
+      put(AG_C_ALLOC_REGRET, lo[kSlotAlloc], hi[kSlotAlloc]);
+      put(AG_C_EST_REGRET, lo[kSlotEst], hi[kSlotEst]);
       put(AG_C_OVERBID, lo[kSlotOverbid], hi[kSlotOverbid]);
       put(AG_C_UNDERBID, lo[kSlotUnderbid], hi[kSlotUnderbid]);
-      put(AG_C_CTR_SQERR, 0, 0);
-      put_count(AG_C_CTR_BIAS, nwon);
+      put(AG_C_CTR_SQERR, lo[kSlotSqerr], hi[kSlotSqerr]);
+      if (GENERAL)
+        put(AG_C_CTR_BIAS, lo[kSlotBias], hi[kSlotBias]);
+      else
+        put_count(AG_C_CTR_BIAS, nwon);
       put(AG_C_BEST_EV, lo[kSlotBestEv], hi[kSlotBestEv]);
       put_count(AG_C_N_LOGS, nlogs);
       put_count(AG_C_N_WON, nwon);
@@ -551,14 +681,14 @@ typedef void (*SimKernel)(SimParams);
 // Defined per participant count P in ag_sim_p.hip (one translation unit per P, compiled
 // in parallel): the k_simulate instantiation for (D, screened search, auctions per lane).
 template <int P>
-SimKernel pick_kernel_for(int D, bool prune, int W);
-template <> SimKernel pick_kernel_for<1>(int, bool, int);
-template <> SimKernel pick_kernel_for<2>(int, bool, int);
-template <> SimKernel pick_kernel_for<3>(int, bool, int);
-template <> SimKernel pick_kernel_for<4>(int, bool, int);
-template <> SimKernel pick_kernel_for<5>(int, bool, int);
-template <> SimKernel pick_kernel_for<6>(int, bool, int);
-template <> SimKernel pick_kernel_for<7>(int, bool, int);
-template <> SimKernel pick_kernel_for<8>(int, bool, int);
+SimKernel pick_kernel_for(int D, bool prune, int W, bool general);
+template <> SimKernel pick_kernel_for<1>(int, bool, int, bool);
+template <> SimKernel pick_kernel_for<2>(int, bool, int, bool);
+template <> SimKernel pick_kernel_for<3>(int, bool, int, bool);
+template <> SimKernel pick_kernel_for<4>(int, bool, int, bool);
+template <> SimKernel pick_kernel_for<5>(int, bool, int, bool);
+template <> SimKernel pick_kernel_for<6>(int, bool, int, bool);
+template <> SimKernel pick_kernel_for<7>(int, bool, int, bool);
+template <> SimKernel pick_kernel_for<8>(int, bool, int, bool);
 
 }  // namespace ag

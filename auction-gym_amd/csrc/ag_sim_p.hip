@@ -9,16 +9,16 @@
 namespace ag {
 namespace {
 
-template <int P, bool PRUNE, int W>
+template <int P, bool PRUNE, int W, bool G>
 SimKernel pick_d(int D) {
   switch (D) {
-    case 2: return k_simulate<P, 2, PRUNE, W>;
-    case 3: return k_simulate<P, 3, PRUNE, W>;
-    case 4: return k_simulate<P, 4, PRUNE, W>;
-    case 5: return k_simulate<P, 5, PRUNE, W>;
-    case 6: return k_simulate<P, 6, PRUNE, W>;
-    case 7: return k_simulate<P, 7, PRUNE, W>;
-    case 8: return k_simulate<P, 8, PRUNE, W>;
+    case 2: return k_simulate<P, 2, PRUNE, W, G>;
+    case 3: return k_simulate<P, 3, PRUNE, W, G>;
+    case 4: return k_simulate<P, 4, PRUNE, W, G>;
+    case 5: return k_simulate<P, 5, PRUNE, W, G>;
+    case 6: return k_simulate<P, 6, PRUNE, W, G>;
+    case 7: return k_simulate<P, 7, PRUNE, W, G>;
+    case 8: return k_simulate<P, 8, PRUNE, W, G>;
     default: return nullptr;
   }
 }
@@ -27,16 +27,21 @@ SimKernel pick_d(int D) {
 
 // prune: the f32-screened item search (D <= 8, K <= 2 kMaxKPairs), W auctions per lane
 // (2 when B is even: 16-B accesses); otherwise the exact scan, one auction per lane.
+// general: populations beyond OracleAllocator + TruthfulBidder (one auction per lane).
 template <>
-SimKernel pick_kernel_for<AG_P>(int D, bool prune, int W) {
+SimKernel pick_kernel_for<AG_P>(int D, bool prune, int W, bool general) {
   constexpr int P = AG_P;
-  if (prune) return W == 2 ? pick_d<P, true, 2>(D) : pick_d<P, true, 1>(D);
-  if (D <= 8) return pick_d<P, false, 1>(D);
+  if (general) {
+    if (D > 8) return nullptr;
+    return prune ? pick_d<P, true, 1, true>(D) : pick_d<P, false, 1, true>(D);
+  }
+  if (prune) return W == 2 ? pick_d<P, true, 2, false>(D) : pick_d<P, true, 1, false>(D);
+  if (D <= 8) return pick_d<P, false, 1, false>(D);
   switch (D) {
-    case 9: return k_simulate<P, 9, false, 1>;
-    case 11: return k_simulate<P, 11, false, 1>;
-    case 13: return k_simulate<P, 13, false, 1>;
-    case 16: return k_simulate<P, 16, false, 1>;
+    case 9: return k_simulate<P, 9, false, 1, false>;
+    case 11: return k_simulate<P, 11, false, 1, false>;
+    case 13: return k_simulate<P, 13, false, 1, false>;
+    case 16: return k_simulate<P, 16, false, 1, false>;
     default: return nullptr;
   }
 }

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define AG_ABI_VERSION 1
+#define AG_ABI_VERSION 2
 
 typedef enum ag_status {
   AG_OK = 0,
@@ -42,12 +42,18 @@ typedef enum ag_mechanism { AG_FIRST_PRICE = 0, AG_SECOND_PRICE = 1 } ag_mechani
 
 /* Allocator plugins (src/BidderAllocation.py). */
 typedef enum ag_allocator_kind {
-  AG_ALLOCATOR_ORACLE = 0 /* OracleAllocator, src/BidderAllocation.py:71-82 */
+  AG_ALLOCATOR_ORACLE = 0, /* OracleAllocator, src/BidderAllocation.py:71-82 */
+  AG_ALLOCATOR_LRTS = 1    /* PyTorchLogisticRegressionAllocator (Thompson sampling),
+                              src/BidderAllocation.py:21-68, src/Models.py:18-48 */
 } ag_allocator_kind;
 
 /* Bidder plugins (src/Bidder.py). */
 typedef enum ag_bidder_kind {
-  AG_BIDDER_TRUTHFUL = 0 /* TruthfulBidder, src/Bidder.py:28-35 */
+  AG_BIDDER_TRUTHFUL = 0,         /* TruthfulBidder, src/Bidder.py:28-35 */
+  AG_BIDDER_EMPIRICAL_SHADED = 1, /* EmpiricalShadedBidder, src/Bidder.py:38-58 */
+  AG_BIDDER_VALUE_LEARNING = 2,   /* ValueLearningBidder (uninitialised), src/Bidder.py:171-179 */
+  AG_BIDDER_POLICY_LEARNING = 3,  /* PolicyLearningBidder (uninitialised), src/Bidder.py:348-356 */
+  AG_BIDDER_DOUBLY_ROBUST = 4     /* DoublyRobustBidder (uninitialised), src/Bidder.py:455-463 */
 } ag_bidder_kind;
 
 /* Per-agent counters produced by ag_simulate: the quantities src/main.py:131-147 reads
@@ -99,6 +105,10 @@ typedef struct ag_batch_in {
   const double *ctx;   /* [E][B] true context without the intercept                      */
   const int32_t *part; /* [P][B] participating agent index per slot, P distinct of N     */
   const double *u;     /* [B]    uniform in [0,1) consumed by binomial(1, CTR[winner])   */
+  const double *gamma_raw; /* [P][B] raw rng.normal(prev_gamma, gamma_sigma) draw of a
+                              shading bidder (src/Bidder.py:51,177,354,461); NULL if none */
+  const float *ts_noise;   /* [P][K*(OE+1)][B] torch.normal(0, 1/sqrt(q)) of an LR-TS
+                              participant (src/Models.py:31); NULL if none / no sampling */
 } ag_batch_in;
 
 /* Outputs of B auctions (dev). Any pointer may be NULL to skip that array. */
@@ -112,6 +122,8 @@ typedef struct ag_batch_out {
   double *est_ctr;       /* [P][B] estimated CTR of the chosen item                     */
   double *true_ctr;      /* [P][B] true CTR of the chosen item (src/Auction.py:52-53)    */
   double *best_ev;       /* [P][B] max_k true_CTR_k * value_k                           */
+  double *gamma;         /* [P][B] shading factor of shading bidders (NaN otherwise)     */
+  double *propensity;    /* [P][B] Gaussian density of gamma (learning bidders; NaN else)*/
 } ag_batch_out;
 
 /* Create a context on `device` for one auction population (src/main.py:98-109
@@ -122,6 +134,16 @@ int ag_destroy(ag_ctx *ctx);
 /* Per-agent plugin kinds, host [N] (src/main.py:77-95 instantiate_agents: the eval of
  * allocator/bidder class names). Default: all OracleAllocator + TruthfulBidder. */
 int ag_set_agent_kinds(ag_ctx *ctx, const int32_t *allocator_kind, const int32_t *bidder_kind);
+
+/* Per-agent plugin parameters, host [N]: kinds as above; prev_gamma / gamma_sigma of
+ * shading bidders (init_gamma, gamma_sigma kwargs; may be NULL when there are none). */
+int ag_set_agent_params(ag_ctx *ctx, const int32_t *allocator_kind, const int32_t *bidder_kind,
+                        const double *prev_gamma, const double *gamma_sigma);
+
+/* LR-TS posterior of every AG_ALLOCATOR_LRTS agent, host float32 [N][K][OE+1] m and q
+ * (PyTorchLogisticRegression.m / .q, src/Models.py:21-24; rows of other agents ignored);
+ * thompson_sampling: add the batch's ts_noise to m for the item choice (src/Models.py:30-31). */
+int ag_load_lrts(ag_ctx *ctx, const float *m, const float *q, int32_t thompson_sampling);
 
 /* Options (ag_set_option). */
 typedef enum ag_option {
@@ -161,6 +183,13 @@ int ag_simulate(ag_ctx *ctx, int64_t B, const ag_batch_in *in, ag_batch_out *out
  * P distinct of N (Floyd), u ~ U[0,1) with 53 bits. */
 int ag_generate(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B, double *ctx_out,
                 int32_t *part_out, double *u_out, void *stream);
+
+/* Synthetic per-participant noise for the participants `part` (dev [P][B]) of auctions
+ * [first_auction, first_auction + B): gamma_raw [P][B] = prev_gamma + gamma_sigma * z for
+ * shading bidders (NaN otherwise), ts_noise [P][K*(OE+1)][B] = z / sqrt(q) for LR-TS agents
+ * (0 otherwise); either output may be NULL. Same Philox key / counter scheme. */
+int ag_generate_noise(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B,
+                      const int32_t *part, double *gamma_raw, float *ts_noise, void *stream);
 
 /* Exact counters (host int64 [n][AG_FX_LIMBS], e.g. copied back or all-reduced)
  * -> doubles (host [n]), correctly rounded from the exact fixed-point sum. */

@@ -327,3 +327,115 @@ def test_screened_search_adversarial_catalogues(gpu, oracle):
         assert np.array_equal(out["price"].cpu().numpy(), orc["price"])
         assert np.array_equal(cnt.cpu().numpy(), orc["counters_fx"])
         eng.close()
+
+
+# ---- general populations: LR-TS allocators, shading bidders (first iteration) ----
+from conftest import POP_CAPTURES, pop_args  # noqa: E402
+
+
+def _pop_engine(meta, d, gpu):
+    from auctiongym_amd.engine import AuctionEngine
+    args = pop_args(d, meta)
+    eng = AuctionEngine(meta["N"], meta["P"], meta["K"], meta["E"], meta["OE"], mech_code(meta),
+                        meta["var"])
+    eng.set_agent_params(args["alloc_kind"], args["bid_kind"], args["prev_gamma"], args["gamma_sigma"])
+    eng.load_catalog(d["items"], d["values"])
+    if args["ts_m"] is not None:
+        eng.load_lrts(args["ts_m"], np.ones_like(args["ts_m"]), True)
+    return eng, args
+
+
+def _pop_run(eng, ctx, part, u, gamma_raw=None, ts_noise=None):
+    """Row-major host replay inputs -> outputs in row-major host layout + fx counters."""
+    import torch
+    d = eng.device
+    B = len(u)
+    inp = {"ctx": torch.from_numpy(np.ascontiguousarray(ctx.T)).to(d),
+           "part": torch.from_numpy(np.ascontiguousarray(part.T.astype(np.int32))).to(d),
+           "u": torch.from_numpy(np.ascontiguousarray(u)).to(d)}
+    if gamma_raw is not None:
+        inp["gamma_raw"] = torch.from_numpy(np.ascontiguousarray(gamma_raw.T)).to(d)
+    if ts_noise is not None:
+        P = part.shape[1]
+        tn = np.ascontiguousarray(ts_noise.reshape(B, P, -1).transpose(1, 2, 0))
+        inp["ts_noise"] = torch.from_numpy(tn).to(d)
+    out = eng.alloc_outputs(B, ("winner", "price", "second_price", "outcome", "item", "bid",
+                                "est_ctr", "true_ctr", "best_ev", "gamma", "propensity"))
+    cnt = eng.new_counters()
+    eng.simulate(inp, out, cnt)
+    torch.cuda.synchronize()
+    o = {k: v.cpu().numpy() for k, v in out.items()}
+    for k in ("item", "bid", "est_ctr", "true_ctr", "best_ev", "gamma", "propensity"):
+        o[k] = np.ascontiguousarray(o[k].T)
+    o["counters_fx"] = cnt.cpu().numpy()
+    return o
+
+
+@pytest.mark.parametrize("name", POP_CAPTURES)
+def test_population_replay_matches_oracle_and_reference(gpu, oracle, name):
+    d, meta, agg = load_capture(name)
+    eng, args = _pop_engine(meta, d, gpu)
+    o = _pop_run(eng, d["ctx"], d["part"], d["u"], d["gamma_raw"], d.get("ts_noise"))
+    orc = oracle.simulate_pop(mech_code(meta), d["items"], d["values"], d["ctx"], d["part"], d["u"],
+                              **args)
+    for k in ("item", "bid", "est_ctr", "true_ctr", "best_ev", "winner", "price", "second_price",
+              "outcome"):
+        assert np.array_equal(o[k], orc[k], equal_nan=True), k
+    sh = ~np.isnan(orc["gamma"])
+    assert np.array_equal(o["gamma"][sh], orc["gamma"][sh])
+    pr = ~np.isnan(orc["propensity"])
+    assert np.array_equal(o["propensity"][pr], orc["propensity"][pr])
+    assert np.array_equal(o["counters_fx"], orc["counters_fx"])
+    # and the reference itself (the oracle's own pinning): exact except LR-TS float32 CTRs
+    assert np.array_equal(o["item"], d["item"]) and np.array_equal(o["winner"], d["winner"])
+    assert np.array_equal(o["true_ctr"], d["slot_true_ctr"])
+    np.testing.assert_allclose(o["bid"], d["slot_bid"], rtol=2.0 ** -20, atol=2e-7)
+    eng.close()
+
+
+def test_mixed_population_full_size(gpu, oracle):
+    """Mixed population (Oracle / LR-TS allocators x truthful / shading bidders), 32 agents,
+    P = 8, FirstPrice: synthetic inputs and noise generated on the GPU, every output
+    compared with the oracle on the same inputs (2^20 auctions)."""
+    import torch
+    from auctiongym_amd.engine import AuctionEngine
+    N, P, K, E, OE, B = 32, 8, 12, 5, 4, 1 << 20
+    g = np.random.default_rng(21)
+    items = np.concatenate([g.normal(0, 1, (N, K, E)), -3.0 - g.random((N, K, 1))], axis=2)
+    values = g.lognormal(0.1, 0.2, (N, K))
+    ak = np.array([i % 2 for i in range(N)], np.int32)             # Oracle / LR-TS
+    bk = np.array([(i // 2) % 5 for i in range(N)], np.int32)      # all five bidder kinds
+    pg = 0.5 + 0.5 * g.random(N)
+    gs = 0.01 + 0.05 * g.random(N)
+    m = g.normal(0, 1, (N, K, OE + 1)).astype(np.float32)
+    q = (1.0 + 3.0 * g.random((N, K, OE + 1))).astype(np.float32)
+    eng = AuctionEngine(N, P, K, E, OE, 0, 1.0)
+    eng.set_agent_params(ak, bk, pg, gs)
+    eng.load_catalog(items, values)
+    eng.load_lrts(m, q, True)
+    inp = eng.alloc_inputs(B)
+    eng.generate(5, 0, inp)
+    eng.generate_noise(5, 0, inp)
+    out = eng.alloc_outputs(B)
+    cnt = eng.new_counters()
+    eng.simulate(inp, out, cnt)
+    torch.cuda.synchronize()
+    ctx = np.ascontiguousarray(inp["ctx"].cpu().numpy().T)
+    part = np.ascontiguousarray(inp["part"].cpu().numpy().T)
+    u = inp["u"].cpu().numpy()
+    gr = np.ascontiguousarray(inp["gamma_raw"].cpu().numpy().T)
+    tn = np.ascontiguousarray(inp["ts_noise"].cpu().numpy().transpose(2, 0, 1)).reshape(B, P, K, OE + 1)
+    # generator sanity: shading draws ~ N(prev_gamma, sigma), LR-TS noise ~ N(0, 1/q)
+    a0 = part[:, 0]
+    zs = (gr[:, 0] - pg[a0]) / gs[a0]
+    zs = zs[bk[a0] != 0]
+    assert abs(zs.mean()) < 0.01 and abs(zs.std() - 1) < 0.01
+    orc = oracle.simulate_pop(0, items, values, ctx, part, u, ak, bk, pg, gs, OE=OE, ts_m=m,
+                              ts_noise=tn, gamma_raw=gr, nthreads=16)
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    for k in ("item", "bid", "est_ctr", "true_ctr", "best_ev", "gamma", "propensity"):
+        assert np.array_equal(np.ascontiguousarray(got[k].T), orc[k], equal_nan=True), k
+    for k in ("winner", "price", "second_price", "outcome"):
+        assert np.array_equal(got[k], orc[k], equal_nan=True), k
+    assert np.array_equal(cnt.cpu().numpy(), orc["counters_fx"])
+    eng.close()
