@@ -270,7 +270,14 @@ def test_errors_are_loud(gpu):
     with pytest.raises(RuntimeError):
         eng.simulate(inp, eng.alloc_outputs(8))  # catalogue not loaded
     with pytest.raises(NotImplementedError):
-        eng.set_agent_kinds([1, 0, 0, 0], [0, 0, 0, 0])
+        eng.set_agent_kinds([7, 0, 0, 0], [0, 0, 0, 0])  # no such allocator kind
+    with pytest.raises(ValueError):
+        eng.set_agent_params([0] * 4, [1, 0, 0, 0])  # shading bidder without its parameters
+    eng.set_agent_params([1, 0, 0, 0], [0] * 4)
+    g = np.random.default_rng(1)
+    eng.load_catalog(g.normal(size=(4, 12, 6)), g.random((4, 12)))
+    with pytest.raises(RuntimeError):
+        eng.simulate(eng.alloc_inputs(8), eng.alloc_outputs(8))  # LR-TS posterior not loaded
     eng.close()
 
 
