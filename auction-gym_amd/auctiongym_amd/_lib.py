@@ -27,9 +27,11 @@ FX_FRAC_BITS, FX_LIMB_BITS, FX_LIMBS = 36, 42, 3
 # Every symbol include/auctiongym.h declares (tests check the .so exports all of them).
 EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params", "ag_load_lrts",
            "ag_set_option", "ag_load_catalog", "ag_allocate", "ag_simulate", "ag_generate",
-           "ag_generate_noise", "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_last_error",
-           "ag_abi_version")
-ABI_VERSION = 2
+           "ag_generate_noise", "ag_lrts_collect", "ag_lrts_update", "ag_lrts_read",
+           "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_last_error", "ag_abi_version")
+ABI_VERSION = 3
+LRTS_MAX_EPOCHS = 16384
+LRTS_MAX_DO = 8
 
 
 class AgShape(ctypes.Structure):
@@ -51,6 +53,11 @@ class AgBatchOut(ctypes.Structure):
                 ("item", ctypes.c_void_p), ("bid", ctypes.c_void_p), ("est_ctr", ctypes.c_void_p),
                 ("true_ctr", ctypes.c_void_p), ("best_ev", ctypes.c_void_p),
                 ("gamma", ctypes.c_void_p), ("propensity", ctypes.c_void_p)]
+
+
+class AgLrtsSamples(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_void_p), ("x", ctypes.c_void_p), ("capacity", ctypes.c_int64),
+                ("count", ctypes.c_void_p)]
 
 
 class AgError(RuntimeError):
@@ -80,7 +87,11 @@ def load(path=None):
         "ag_load_catalog": (ctypes.c_int, [vp, vp, vp]),
         "ag_set_option": (ctypes.c_int, [vp, i32, i64]),
         "ag_set_agent_params": (ctypes.c_int, [vp, vp, vp, vp, vp]),
-        "ag_load_lrts": (ctypes.c_int, [vp, vp, vp, i32]),
+        "ag_load_lrts": (ctypes.c_int, [vp, vp, vp, vp, i32]),
+        "ag_lrts_collect": (ctypes.c_int, [vp, i64, ctypes.POINTER(AgBatchIn),
+                                           ctypes.POINTER(AgBatchOut), ctypes.POINTER(AgLrtsSamples), vp]),
+        "ag_lrts_update": (ctypes.c_int, [vp, ctypes.POINTER(AgLrtsSamples), vp, vp, vp]),
+        "ag_lrts_read": (ctypes.c_int, [vp, vp, vp, vp]),
         "ag_generate_noise": (ctypes.c_int, [vp, u64, u64, i64, vp, vp, vp, vp]),
         "ag_allocate": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, vp]),
         "ag_simulate": (ctypes.c_int, [vp, i64, ctypes.POINTER(AgBatchIn),

@@ -10,7 +10,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import AgBatchIn, AgBatchOut, AgShape
+from ._lib import AgBatchIn, AgBatchOut, AgLrtsSamples, AgShape
 from ._lib import check as _check
 
 COUNTERS = _lib.COUNTERS
@@ -91,15 +91,62 @@ class AuctionEngine:
                                                None if gs is None else gs.ctypes.data),
                     "ag_set_agent_params")
 
-    def load_lrts(self, m, q, thompson_sampling=True):
-        """LR-TS posteriors m, q float32 [N][K][OE+1] (ag_load_lrts)."""
+    def load_lrts(self, m, q, prev_m=None, thompson_sampling=True):
+        """LR-TS posteriors m, q, prev_m float32 [N][K][OE+1] (ag_load_lrts; prev_m None = m)."""
+        shape = (self.N, self.K, self.OE + 1)
         m = np.ascontiguousarray(m, np.float32)
         q = np.ascontiguousarray(q, np.float32)
-        if m.shape != (self.N, self.K, self.OE + 1) or q.shape != m.shape:
-            raise ValueError(f"LR-TS params must be [N][K][OE+1] = ({self.N},{self.K},{self.OE + 1})")
+        pm = None if prev_m is None else np.ascontiguousarray(prev_m, np.float32)
+        if m.shape != shape or q.shape != shape or (pm is not None and pm.shape != shape):
+            raise ValueError(f"LR-TS params must be [N][K][OE+1] = {shape}")
         self.ts_sample = bool(thompson_sampling)
-        self._check(self.L.ag_load_lrts(self._h, m.ctypes.data, q.ctypes.data, int(self.ts_sample)),
+        self._check(self.L.ag_load_lrts(self._h, m.ctypes.data, q.ctypes.data,
+                                        None if pm is None else pm.ctypes.data, int(self.ts_sample)),
                     "ag_load_lrts")
+
+    def lrts_state(self):
+        """(m, q, prev_m) float32 [N][K][OE+1] as they are on the device (ag_lrts_read)."""
+        shape = (self.N, self.K, self.OE + 1)
+        m, q, pm = (np.empty(shape, np.float32) for _ in range(3))
+        self._check(self.L.ag_lrts_read(self._h, m.ctypes.data, q.ctypes.data, pm.ctypes.data),
+                    "ag_lrts_read")
+        return m, q, pm
+
+    # ---------------------------------------------------------------- LR-TS update
+    def new_lrts_samples(self, capacity):
+        """Device store of won LR-TS samples (ag_lrts_samples): key [cap] uint32 (as int32),
+        x [OE+1][cap] float32, count [1]."""
+        d = self.device
+        return {"key": torch.empty((capacity,), dtype=torch.int32, device=d),
+                "x": torch.empty((self.OE + 1, capacity), dtype=torch.float32, device=d),
+                "count": torch.zeros((1,), dtype=torch.int64, device=d)}
+
+    @staticmethod
+    def _samples(st):
+        return AgLrtsSamples(_ptr(st["key"]).value, _ptr(st["x"]).value, st["key"].shape[0],
+                             _ptr(st["count"]).value)
+
+    def lrts_collect(self, inputs, outputs, store):
+        """Append the won LR-TS samples of a simulated batch (ag_lrts_collect)."""
+        B = inputs["u"].shape[0]
+        bi = AgBatchIn(_ptr(inputs["ctx"]).value, _ptr(inputs["part"]).value, _ptr(inputs["u"]).value,
+                       _ptr(inputs.get("gamma_raw")).value, _ptr(inputs.get("ts_noise")).value)
+        bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
+        st = self._samples(store)
+        self._check(self.L.ag_lrts_collect(self._h, B, ctypes.byref(bi), ctypes.byref(bo),
+                                           ctypes.byref(st), _stream()), "ag_lrts_collect")
+
+    def lrts_update(self, store, trace=False):
+        """Train every LR-TS agent on the store (ag_lrts_update). Returns epochs [N] and, with
+        trace=True, the per-epoch losses as a float32 [N][16384] device tensor."""
+        ep = np.zeros(self.N, np.int32)
+        tr = None
+        if trace:
+            tr = torch.zeros((self.N, _lib.LRTS_MAX_EPOCHS), dtype=torch.float32, device=self.device)
+        st = self._samples(store)
+        self._check(self.L.ag_lrts_update(self._h, ctypes.byref(st), ep.ctypes.data, _ptr(tr),
+                                          _stream()), "ag_lrts_update")
+        return (ep, tr) if trace else ep
 
     def set_item_search(self, exact):
         """exact=True: score every item in FP64 (the reference loop); False (default): f32

@@ -1,0 +1,65 @@
+// ag_host.h -- host-side state shared by the C-ABI translation units (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "auctiongym.h"
+
+// Sets the thread-local ag_last_error() text; returns `code`.
+int ag_set_error(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+
+#define AG_HIP(call)                                                                    \
+  do {                                                                                  \
+    hipError_t e_ = (call);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return ag_set_error(AG_ERR_HIP, "%s: %s (%s:%d)", #call, hipGetErrorString(e_),   \
+                          __FILE__, __LINE__);                                          \
+  } while (0)
+
+// LR-TS training workspace (ag_lrts.hip), grown on demand by ag_lrts_update.
+struct ag_lrts_ws {
+  int64_t cap = 0;            // samples the bucket arrays hold
+  uint32_t *key = nullptr;    // [cap] samples bucketed by agent
+  float *x = nullptr;         // [Do][cap]
+  int64_t *offsets = nullptr; // [N + 1] bucket offsets, then per-agent cursors [N]
+  double *adam_tab = nullptr; // [2][kLrEpochs]: 1 - 0.9^t, (1 - 0.999^t)^0.5 (host pow)
+  int32_t *epochs = nullptr;  // [N]
+  int32_t *status = nullptr;  // [1] device-side error flags
+};
+
+struct ag_ctx {
+  int32_t device;
+  ag_shape shape;
+  int32_t D;
+  int32_t item_search = AG_ITEM_SEARCH_AUTO;
+  bool can_simulate = false;
+  double *d_items = nullptr;
+  double *d_values = nullptr;
+  int64_t *d_partials = nullptr;
+  int32_t partial_blocks = 0;
+  int32_t resident[16] = {};  // resident blocks [general][W][screened][counters]
+  bool wide = false;  // 1 auction per lane by default: higher occupancy, faster when sustained
+  bool catalog = false;
+  // general populations (anything beyond OracleAllocator + TruthfulBidder)
+  bool general = false, has_lrts = false, has_shading = false, lrts_loaded = false;
+  int32_t ts_sample = 1;
+  int32_t *h_akind = nullptr;  // host copy of the allocator kinds [N]
+  int32_t *d_akind = nullptr, *d_bkind = nullptr;
+  double *d_pg = nullptr, *d_gs = nullptr;
+  float *d_tsm = nullptr, *d_tsq = nullptr, *d_tsprev = nullptr;  // LR-TS m, q, prev_iter_m
+  ag_lrts_ws lrts;
+};
+
+// Frees the LR-TS training workspace (ag_lrts.hip).
+void ag_lrts_release(ag_ctx *c);
+
+struct AgDeviceGuard {
+  int prev = -1;
+  explicit AgDeviceGuard(int dev) {
+    if (hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
+    else prev = -1;
+  }
+  ~AgDeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};

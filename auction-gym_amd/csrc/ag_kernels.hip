@@ -25,15 +25,15 @@
 
 #include <string>
 
+#include "ag_host.h"
 #include "ag_sim.h"
 
 // ------------------------------------------------------------------------------------
-// error plumbing
+// error plumbing (declared in ag_host.h)
 // ------------------------------------------------------------------------------------
 static thread_local std::string g_last_error;
 
-static int set_error(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
-static int set_error(int code, const char *fmt, ...) {
+int ag_set_error(int code, const char *fmt, ...) {
   char buf[512];
   va_list ap;
   va_start(ap, fmt);
@@ -42,14 +42,6 @@ static int set_error(int code, const char *fmt, ...) {
   g_last_error = buf;
   return code;
 }
-
-#define AG_HIP(call)                                                                    \
-  do {                                                                                  \
-    hipError_t e_ = (call);                                                             \
-    if (e_ != hipSuccess)                                                               \
-      return set_error(AG_ERR_HIP, "%s: %s (%s:%d)", #call, hipGetErrorString(e_),      \
-                       __FILE__, __LINE__);                                             \
-  } while (0)
 
 namespace {
 using namespace ag;
@@ -332,66 +324,31 @@ int grid_for(int64_t B, int64_t per_block_cap) {
 // ------------------------------------------------------------------------------------
 // C-ABI
 // ------------------------------------------------------------------------------------
-struct ag_ctx {
-  int32_t device;
-  ag_shape shape;
-  int32_t D;
-  int32_t item_search = AG_ITEM_SEARCH_AUTO;
-  bool can_simulate = false;
-  double *d_items = nullptr;
-  double *d_values = nullptr;
-  int64_t *d_partials = nullptr;
-  int32_t partial_blocks = 0;
-  int32_t resident[16] = {};  // resident blocks [general][W][screened][counters]
-  bool wide = false;  // 1 auction per lane by default: higher occupancy, faster when sustained
-  bool catalog = false;
-  // general populations (anything beyond OracleAllocator + TruthfulBidder)
-  bool general = false, has_lrts = false, has_shading = false, lrts_loaded = false;
-  int32_t ts_sample = 1;
-  int32_t *d_akind = nullptr, *d_bkind = nullptr;
-  double *d_pg = nullptr, *d_gs = nullptr;
-  float *d_tsm = nullptr, *d_tsq = nullptr;
-  float *h_tsq = nullptr;  // host copy of q for the synthetic generator
-};
-
-namespace {
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
-    else prev = -1;
-  }
-  ~DeviceGuard() {
-    if (prev >= 0) (void)hipSetDevice(prev);
-  }
-};
-}  // namespace
-
 extern "C" {
 
 const char *ag_last_error(void) { return g_last_error.c_str(); }
 int32_t ag_abi_version(void) { return AG_ABI_VERSION; }
 
 int ag_create(int32_t device, const ag_shape *s, ag_ctx **out) {
-  if (!s || !out) return set_error(AG_ERR_INVALID, "ag_create: null argument");
+  if (!s || !out) return ag_set_error(AG_ERR_INVALID, "ag_create: null argument");
   *out = nullptr;
   if (s->num_agents < 1 || s->num_items < 1 || s->embedding_size < 1)
-    return set_error(AG_ERR_INVALID, "ag_create: N, K, E must be >= 1 (N=%d K=%d E=%d)",
+    return ag_set_error(AG_ERR_INVALID, "ag_create: N, K, E must be >= 1 (N=%d K=%d E=%d)",
                      s->num_agents, s->num_items, s->embedding_size);
   if (s->num_participants < 1 || s->num_participants > s->num_agents)
-    return set_error(AG_ERR_INVALID,
+    return ag_set_error(AG_ERR_INVALID,
                      "ag_create: Cannot take a larger sample than population when replace is "
                      "False (P=%d, N=%d; src/Auction.py:42)",
                      s->num_participants, s->num_agents);
   if (s->mechanism != AG_FIRST_PRICE && s->mechanism != AG_SECOND_PRICE)
-    return set_error(AG_ERR_INVALID, "ag_create: unknown mechanism %d", s->mechanism);
+    return ag_set_error(AG_ERR_INVALID, "ag_create: unknown mechanism %d", s->mechanism);
   if (s->num_slots != 1)
-    return set_error(AG_ERR_UNSUPPORTED, "ag_create: num_slots must be 1 (src/main.py:37)");
+    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_create: num_slots must be 1 (src/main.py:37)");
   const int D = s->embedding_size + 1;
   if (s->num_participants > 4096)
-    return set_error(AG_ERR_UNSUPPORTED, "ag_create: P=%d > 4096", s->num_participants);
+    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_create: P=%d > 4096", s->num_participants);
   if (s->obs_embedding_size < 0 || s->obs_embedding_size > s->embedding_size)
-    return set_error(AG_ERR_INVALID, "ag_create: obs_embedding_size out of range");
+    return ag_set_error(AG_ERR_INVALID, "ag_create: obs_embedding_size out of range");
   ag_ctx *c = new ag_ctx();
   c->device = device;
   c->shape = *s;
@@ -402,7 +359,7 @@ int ag_create(int32_t device, const ag_shape *s, ag_ctx **out) {
   const LdsLayout lay = make_layout(s->num_agents, s->num_items, D, true);
   c->can_simulate = s->num_participants <= kMaxP && pick_kernel(s->num_participants, D, false, 1, false) &&
                     lay.total <= 160 * 1024;
-  DeviceGuard g(device);
+  AgDeviceGuard g(device);
   hipError_t e = hipMalloc(&c->d_items, sizeof(double) * s->num_agents * s->num_items * D);
   if (e == hipSuccess) e = hipMalloc(&c->d_values, sizeof(double) * s->num_agents * s->num_items);
   // partials for the largest grid a call can use: grids grow past kMinGrid only to keep
@@ -416,6 +373,7 @@ int ag_create(int32_t device, const ag_shape *s, ag_ctx **out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_gs, sizeof(double) * s->num_agents);
   if (e == hipSuccess) e = hipMalloc(&c->d_tsm, sizeof(float) * nkd);
   if (e == hipSuccess) e = hipMalloc(&c->d_tsq, sizeof(float) * nkd);
+  if (e == hipSuccess) e = hipMalloc(&c->d_tsprev, sizeof(float) * nkd);
   if (e != hipSuccess) {
     (void)hipFree(c->d_items);
     (void)hipFree(c->d_values);
@@ -426,8 +384,9 @@ int ag_create(int32_t device, const ag_shape *s, ag_ctx **out) {
     (void)hipFree(c->d_gs);
     (void)hipFree(c->d_tsm);
     (void)hipFree(c->d_tsq);
+    (void)hipFree(c->d_tsprev);
     delete c;
-    return set_error(AG_ERR_HIP, "ag_create: hipMalloc: %s", hipGetErrorString(e));
+    return ag_set_error(AG_ERR_HIP, "ag_create: hipMalloc: %s", hipGetErrorString(e));
   }
   *out = c;
   return AG_OK;
@@ -435,7 +394,7 @@ int ag_create(int32_t device, const ag_shape *s, ag_ctx **out) {
 
 int ag_destroy(ag_ctx *c) {
   if (!c) return AG_OK;
-  DeviceGuard g(c->device);
+  AgDeviceGuard g(c->device);
   (void)hipFree(c->d_items);
   (void)hipFree(c->d_values);
   (void)hipFree(c->d_partials);
@@ -445,34 +404,36 @@ int ag_destroy(ag_ctx *c) {
   (void)hipFree(c->d_gs);
   (void)hipFree(c->d_tsm);
   (void)hipFree(c->d_tsq);
-  delete[] c->h_tsq;
+  (void)hipFree(c->d_tsprev);
+  ag_lrts_release(c);
+  delete[] c->h_akind;
   delete c;
   return AG_OK;
 }
 
 int ag_set_agent_params(ag_ctx *c, const int32_t *alloc_kind, const int32_t *bid_kind,
                         const double *prev_gamma, const double *gamma_sigma) {
-  if (!c) return set_error(AG_ERR_INVALID, "ag_set_agent_params: null ctx");
+  if (!c) return ag_set_error(AG_ERR_INVALID, "ag_set_agent_params: null ctx");
   const int N = c->shape.num_agents;
   bool general = false, lrts = false, shading = false;
   for (int a = 0; a < N; ++a) {
     const int ak = alloc_kind ? alloc_kind[a] : AG_ALLOCATOR_ORACLE;
     const int bk = bid_kind ? bid_kind[a] : AG_BIDDER_TRUTHFUL;
     if (ak != AG_ALLOCATOR_ORACLE && ak != AG_ALLOCATOR_LRTS)
-      return set_error(AG_ERR_UNSUPPORTED, "agent %d: allocator kind %d not implemented", a, ak);
+      return ag_set_error(AG_ERR_UNSUPPORTED, "agent %d: allocator kind %d not implemented", a, ak);
     if (bk < AG_BIDDER_TRUTHFUL || bk > AG_BIDDER_DOUBLY_ROBUST)
-      return set_error(AG_ERR_UNSUPPORTED, "agent %d: bidder kind %d not implemented", a, bk);
+      return ag_set_error(AG_ERR_UNSUPPORTED, "agent %d: bidder kind %d not implemented", a, bk);
     if (bk != AG_BIDDER_TRUTHFUL && (!prev_gamma || !gamma_sigma))
-      return set_error(AG_ERR_INVALID, "agent %d: shading bidder needs prev_gamma and gamma_sigma", a);
+      return ag_set_error(AG_ERR_INVALID, "agent %d: shading bidder needs prev_gamma and gamma_sigma", a);
     if (bk != AG_BIDDER_TRUTHFUL && !(gamma_sigma[a] > 0.0))
-      return set_error(AG_ERR_INVALID, "agent %d: gamma_sigma must be > 0", a);
+      return ag_set_error(AG_ERR_INVALID, "agent %d: gamma_sigma must be > 0", a);
     lrts |= ak == AG_ALLOCATOR_LRTS;
     shading |= bk != AG_BIDDER_TRUTHFUL;
   }
   general = lrts || shading;
   if (general && (c->D > 8 || c->shape.obs_embedding_size + 1 > kMaxD))
-    return set_error(AG_ERR_UNSUPPORTED, "general populations support E+1 <= 8 (D=%d)", c->D);
-  DeviceGuard g(c->device);
+    return ag_set_error(AG_ERR_UNSUPPORTED, "general populations support E+1 <= 8 (D=%d)", c->D);
+  AgDeviceGuard g(c->device);
   int32_t *ak = new int32_t[N], *bk = new int32_t[N];
   double *pg = new double[N], *gs = new double[N];
   for (int a = 0; a < N; ++a) {
@@ -485,11 +446,15 @@ int ag_set_agent_params(ag_ctx *c, const int32_t *alloc_kind, const int32_t *bid
   if (e == hipSuccess) e = hipMemcpy(c->d_bkind, bk, sizeof(int32_t) * N, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_pg, pg, sizeof(double) * N, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_gs, gs, sizeof(double) * N, hipMemcpyHostToDevice);
-  delete[] ak;
   delete[] bk;
   delete[] pg;
   delete[] gs;
-  if (e != hipSuccess) return set_error(AG_ERR_HIP, "ag_set_agent_params: %s", hipGetErrorString(e));
+  if (e != hipSuccess) {
+    delete[] ak;
+    return ag_set_error(AG_ERR_HIP, "ag_set_agent_params: %s", hipGetErrorString(e));
+  }
+  delete[] c->h_akind;
+  c->h_akind = ak;
   c->general = general;
   c->has_lrts = lrts;
   c->has_shading = shading;
@@ -497,47 +462,47 @@ int ag_set_agent_params(ag_ctx *c, const int32_t *alloc_kind, const int32_t *bid
 }
 
 int ag_set_agent_kinds(ag_ctx *c, const int32_t *alloc_kind, const int32_t *bid_kind) {
-  if (!c) return set_error(AG_ERR_INVALID, "ag_set_agent_kinds: null ctx");
+  if (!c) return ag_set_error(AG_ERR_INVALID, "ag_set_agent_kinds: null ctx");
   for (int a = 0; a < c->shape.num_agents; ++a)
     if (bid_kind && bid_kind[a] != AG_BIDDER_TRUTHFUL)
-      return set_error(AG_ERR_INVALID, "agent %d: shading bidders need ag_set_agent_params", a);
+      return ag_set_error(AG_ERR_INVALID, "agent %d: shading bidders need ag_set_agent_params", a);
   return ag_set_agent_params(c, alloc_kind, bid_kind, nullptr, nullptr);
 }
 
-int ag_load_lrts(ag_ctx *c, const float *m, const float *q, int32_t thompson_sampling) {
-  if (!c || !m || !q) return set_error(AG_ERR_INVALID, "ag_load_lrts: null argument");
-  DeviceGuard g(c->device);
+int ag_load_lrts(ag_ctx *c, const float *m, const float *q, const float *prev_m,
+                 int32_t thompson_sampling) {
+  if (!c || !m || !q) return ag_set_error(AG_ERR_INVALID, "ag_load_lrts: null argument");
+  AgDeviceGuard g(c->device);
   const size_t n = (size_t)c->shape.num_agents * c->shape.num_items * (c->shape.obs_embedding_size + 1);
   AG_HIP(hipMemcpy(c->d_tsm, m, n * sizeof(float), hipMemcpyHostToDevice));
   AG_HIP(hipMemcpy(c->d_tsq, q, n * sizeof(float), hipMemcpyHostToDevice));
-  if (!c->h_tsq) c->h_tsq = new float[n];
-  memcpy(c->h_tsq, q, n * sizeof(float));
+  AG_HIP(hipMemcpy(c->d_tsprev, prev_m ? prev_m : m, n * sizeof(float), hipMemcpyHostToDevice));
   c->ts_sample = thompson_sampling ? 1 : 0;
   c->lrts_loaded = true;
   return AG_OK;
 }
 
 int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
-  if (!c) return set_error(AG_ERR_INVALID, "ag_set_option: null ctx");
+  if (!c) return ag_set_error(AG_ERR_INVALID, "ag_set_option: null ctx");
   switch (option) {
     case AG_OPT_ITEM_SEARCH:
       if (value != AG_ITEM_SEARCH_AUTO && value != AG_ITEM_SEARCH_EXACT)
-        return set_error(AG_ERR_INVALID, "ag_set_option: bad item search mode %lld", (long long)value);
+        return ag_set_error(AG_ERR_INVALID, "ag_set_option: bad item search mode %lld", (long long)value);
       c->item_search = (int32_t)value;
       return AG_OK;
     case AG_OPT_LANE_AUCTIONS:
       if (value != 1 && value != 2)
-        return set_error(AG_ERR_INVALID, "ag_set_option: lane auctions must be 1 or 2");
+        return ag_set_error(AG_ERR_INVALID, "ag_set_option: lane auctions must be 1 or 2");
       c->wide = value == 2;
       return AG_OK;
     default:
-      return set_error(AG_ERR_INVALID, "ag_set_option: unknown option %d", option);
+      return ag_set_error(AG_ERR_INVALID, "ag_set_option: unknown option %d", option);
   }
 }
 
 int ag_load_catalog(ag_ctx *c, const double *item_emb, const double *item_val) {
-  if (!c || !item_emb || !item_val) return set_error(AG_ERR_INVALID, "ag_load_catalog: null argument");
-  DeviceGuard g(c->device);
+  if (!c || !item_emb || !item_val) return ag_set_error(AG_ERR_INVALID, "ag_load_catalog: null argument");
+  AgDeviceGuard g(c->device);
   const size_t n = (size_t)c->shape.num_agents * c->shape.num_items;
   AG_HIP(hipMemcpy(c->d_items, item_emb, n * c->D * sizeof(double), hipMemcpyHostToDevice));
   AG_HIP(hipMemcpy(c->d_values, item_val, n * sizeof(double), hipMemcpyHostToDevice));
@@ -547,10 +512,10 @@ int ag_load_catalog(ag_ctx *c, const double *item_emb, const double *item_val) {
 
 int ag_allocate(ag_ctx *c, const double *bids, int64_t B, int32_t *winner, double *price,
                 double *second_price, void *stream) {
-  if (!c || (!bids && B > 0)) return set_error(AG_ERR_INVALID, "ag_allocate: null argument");
-  if (B < 0) return set_error(AG_ERR_INVALID, "ag_allocate: B < 0");
+  if (!c || (!bids && B > 0)) return ag_set_error(AG_ERR_INVALID, "ag_allocate: null argument");
+  if (B < 0) return ag_set_error(AG_ERR_INVALID, "ag_allocate: B < 0");
   if (B == 0) return AG_OK;
-  DeviceGuard g(c->device);
+  AgDeviceGuard g(c->device);
   const int P = c->shape.num_participants, mech = c->shape.mechanism;
   hipStream_t st = (hipStream_t)stream;
   if (P <= 16) {
@@ -571,30 +536,30 @@ int ag_allocate(ag_ctx *c, const double *bids, int64_t B, int32_t *winner, doubl
 
 int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, int64_t *counters_fx,
                 void *stream) {
-  if (!c || !in || !out) return set_error(AG_ERR_INVALID, "ag_simulate: null argument");
+  if (!c || !in || !out) return ag_set_error(AG_ERR_INVALID, "ag_simulate: null argument");
   if (!c->can_simulate)
-    return set_error(AG_ERR_UNSUPPORTED,
+    return ag_set_error(AG_ERR_UNSUPPORTED,
                      "ag_simulate: supports P in [1,%d], E+1 in {2..9,11,13,16} and a catalogue "
                      "that fits LDS (P=%d, D=%d, N=%d, K=%d)",
                      kMaxP, c->shape.num_participants, c->D, c->shape.num_agents, c->shape.num_items);
-  if (!c->catalog) return set_error(AG_ERR_STATE, "ag_simulate: ag_load_catalog not called");
-  if (B < 0) return set_error(AG_ERR_INVALID, "ag_simulate: B < 0");
+  if (!c->catalog) return ag_set_error(AG_ERR_STATE, "ag_simulate: ag_load_catalog not called");
+  if (B < 0) return ag_set_error(AG_ERR_INVALID, "ag_simulate: B < 0");
   if (B == 0) return AG_OK;
-  if (!in->ctx || !in->part || !in->u) return set_error(AG_ERR_INVALID, "ag_simulate: null input array");
+  if (!in->ctx || !in->part || !in->u) return ag_set_error(AG_ERR_INVALID, "ag_simulate: null input array");
   if (B * c->shape.num_participants > INT32_MAX)
-    return set_error(AG_ERR_UNSUPPORTED, "ag_simulate: B * P must be < 2^31 (32-bit SoA indexing); "
+    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: B * P must be < 2^31 (32-bit SoA indexing); "
                      "split the batch");
-  DeviceGuard g(c->device);
+  AgDeviceGuard g(c->device);
   const ag_shape &s = c->shape;
   const int nc = s.num_agents * kC;
   const int D = c->D;
   const bool prune = c->item_search == AG_ITEM_SEARCH_AUTO && D <= 8 && s.num_items <= 2 * kMaxKPairs;
   if (c->has_lrts && !c->lrts_loaded)
-    return set_error(AG_ERR_STATE, "ag_simulate: LR-TS agents need ag_load_lrts");
+    return ag_set_error(AG_ERR_STATE, "ag_simulate: LR-TS agents need ag_load_lrts");
   if (c->has_lrts && c->ts_sample && !in->ts_noise)
-    return set_error(AG_ERR_INVALID, "ag_simulate: Thompson sampling needs ts_noise");
+    return ag_set_error(AG_ERR_INVALID, "ag_simulate: Thompson sampling needs ts_noise");
   if (c->has_shading && !in->gamma_raw)
-    return set_error(AG_ERR_INVALID, "ag_simulate: shading bidders need gamma_raw");
+    return ag_set_error(AG_ERR_INVALID, "ag_simulate: shading bidders need gamma_raw");
   SimParams prm;
   prm.B = B;
   prm.N = s.num_agents;
@@ -616,10 +581,10 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   prm.partials = c->d_partials;
   const int W = (prune && (B % 2) == 0 && c->wide && !c->general) ? 2 : 1;
   SimKernel k = pick_kernel(s.num_participants, D, prune, W, c->general);
-  if (!k) return set_error(AG_ERR_UNSUPPORTED, "ag_simulate: no kernel for P=%d D=%d", s.num_participants, D);
+  if (!k) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: no kernel for P=%d D=%d", s.num_participants, D);
   const size_t lds = (size_t)prm.lds.total;
   if (lds > 160 * 1024)
-    return set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
+    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
   hipStream_t st = (hipStream_t)stream;
   if (lds > 64 * 1024)
     AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -637,7 +602,7 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   const int64_t tiles = (B + kThreads * W - 1) / (kThreads * W);
   const int grid = (int)(tiles < res ? tiles : res);
   if (B > (int64_t)grid * kMaxAuctionsPerBlock)
-    return set_error(AG_ERR_UNSUPPORTED, "ag_simulate: B=%lld > %lld auctions per call; split the batch",
+    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: B=%lld > %lld auctions per call; split the batch",
                      (long long)B, (long long)grid * kMaxAuctionsPerBlock);
   hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), lds, st, prm);
   AG_HIP(hipGetLastError());
@@ -651,11 +616,11 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
 
 int ag_generate(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, double *ctx_out, int32_t *part_out,
                 double *u_out, void *stream) {
-  if (!c || !ctx_out || !part_out || !u_out) return set_error(AG_ERR_INVALID, "ag_generate: null argument");
-  if (B < 0) return set_error(AG_ERR_INVALID, "ag_generate: B < 0");
+  if (!c || !ctx_out || !part_out || !u_out) return ag_set_error(AG_ERR_INVALID, "ag_generate: null argument");
+  if (B < 0) return ag_set_error(AG_ERR_INVALID, "ag_generate: B < 0");
   if (B == 0) return AG_OK;
-  if (c->shape.num_participants > 64) return set_error(AG_ERR_UNSUPPORTED, "ag_generate: P > 64");
-  DeviceGuard g(c->device);
+  if (c->shape.num_participants > 64) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_generate: P > 64");
+  AgDeviceGuard g(c->device);
   const int grid = grid_for(B, (int64_t)1 << 40);
   hipLaunchKernelGGL(k_generate, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, seed, first, B,
                      c->shape.num_agents, c->shape.num_participants, c->shape.embedding_size,
@@ -666,11 +631,11 @@ int ag_generate(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, double *ctx
 
 int ag_generate_noise(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, const int32_t *part,
                       double *gamma_raw, float *ts_noise, void *stream) {
-  if (!c || !part) return set_error(AG_ERR_INVALID, "ag_generate_noise: null argument");
-  if (B < 0) return set_error(AG_ERR_INVALID, "ag_generate_noise: B < 0");
+  if (!c || !part) return ag_set_error(AG_ERR_INVALID, "ag_generate_noise: null argument");
+  if (B < 0) return ag_set_error(AG_ERR_INVALID, "ag_generate_noise: B < 0");
   if (B == 0) return AG_OK;
-  if (ts_noise && !c->lrts_loaded) return set_error(AG_ERR_STATE, "ag_generate_noise: ag_load_lrts first");
-  DeviceGuard g(c->device);
+  if (ts_noise && !c->lrts_loaded) return ag_set_error(AG_ERR_STATE, "ag_generate_noise: ag_load_lrts first");
+  AgDeviceGuard g(c->device);
   const int grid = grid_for(B, (int64_t)1 << 40);
   const int KDo = c->shape.num_items * (c->shape.obs_embedding_size + 1);
   hipLaunchKernelGGL(k_generate_noise, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, seed, first, B,
@@ -681,7 +646,7 @@ int ag_generate_noise(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, const
 }
 
 int ag_counters_to_double(const int64_t *fx, int64_t n, double *out) {
-  if ((!fx || !out) && n > 0) return set_error(AG_ERR_INVALID, "ag_counters_to_double: null argument");
+  if ((!fx || !out) && n > 0) return ag_set_error(AG_ERR_INVALID, "ag_counters_to_double: null argument");
   for (int64_t j = 0; j < n; ++j) {
     const int64_t *L = fx + j * AG_FX_LIMBS;
     __int128 t = (__int128)L[2];

@@ -1,0 +1,537 @@
+// ag_lrts.hip -- LR-TS allocator update on the GPU (Agent.update -> PyTorchLogistic-
+// RegressionAllocator.update, src/Agent.py:79-91, src/BidderAllocation.py:29-65,
+// src/Models.py:35-48), plus the won-sample collection that feeds it.
+//
+//  1. k_lrts_collect   after each ag_simulate: every auction won by an LR-TS agent
+//                      appends (agent, item, outcome, observed context + 1) to a
+//                      caller-owned store (one atomic per wave).
+//  2. bucket           histogram -> exclusive scan -> scatter: samples grouped by agent.
+//  3. k_lrts_train     one workgroup per agent, persistent over the epochs: forward, BCE +
+//                      prior loss, gradient, Adam, ReduceLROnPlateau and the early stop all
+//                      on the device (no host round trip per epoch), then the Laplace
+//                      update of q and prev_m = m.
+//
+// Every sum over samples is exact (fixed-point terms added as integers: oracle/ag_oracle.c
+// ora_lrts_update states the arithmetic), so results do not depend on sample order,
+// bucket order or the lane a sample lands on: the update is bit-identical to the oracle
+// and identical on every rank of a multi-GPU job that trains on the gathered samples.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "ag_exp.h"
+#include "ag_exp_table.h"
+#include "ag_host.h"
+
+namespace {
+
+constexpr int kLrThreads = 256;        // 4 waves; one sample per lane per pass
+constexpr int kLrEpochs = AG_LRTS_MAX_EPOCHS;
+constexpr int kLrMaxKD = 64;           // K * (OE + 1) columns of the accumulator tile
+constexpr int kLrCache = 4;            // samples per lane kept in registers
+constexpr int kAccStride = kLrThreads + 1;  // [column][lane] int64 tile, padded: the column
+                                            // reduction (lanes = columns) is conflict-free
+constexpr int kHistory = 100;          // losses[-100] of the early stop
+constexpr double kGradScale = 0x1p40, kLossScale = 0x1p32;
+constexpr int64_t kLo24 = (int64_t(1) << 24) - 1;
+
+__device__ __forceinline__ int64_t fx_round(double v, double scale) {
+  return (int64_t)__builtin_rint(v * scale);
+}
+// (hi, lo) partial sums of values split at bit 24 -> the exact sum S read back as
+// (double)(S >> 24) * 2^24 + (double)(S & (2^24 - 1)) (ora_lrts_update's fx_read).
+__device__ __forceinline__ double fx_read(int64_t hi, int64_t lo, double inv_scale) {
+  hi += lo >> 24;
+  lo &= kLo24;
+  return ((double)hi * 0x1p24 + (double)lo) * inv_scale;
+}
+
+__device__ __forceinline__ int64_t wave_sum(int64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// 1. collection: Agent.update's won_mask (src/Agent.py:90) over one simulated batch
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kLrThreads) void k_lrts_collect(
+    int64_t B, int P, int OE, const double *__restrict__ ctx, const int32_t *__restrict__ part,
+    const int32_t *__restrict__ winner, const int32_t *__restrict__ item, const uint8_t *__restrict__ outcome,
+    const int32_t *__restrict__ akind, uint32_t *__restrict__ key, float *__restrict__ x, int64_t cap,
+    unsigned long long *__restrict__ count) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t base = (int64_t)blockIdx.x * kLrThreads; base < B; base += (int64_t)gridDim.x * kLrThreads) {
+    const int64_t i = base + threadIdx.x;
+    bool take = false;
+    uint32_t k = 0;
+    if (i < B && P >= 2) {  // P == 1: nobody is charged, no record is won (src/Auction.py:68)
+      const int w = winner[i];
+      const int a = part[(size_t)w * B + i];
+      if (akind[a] == AG_ALLOCATOR_LRTS) {
+        take = true;
+        k = ((uint32_t)a << 16) | ((uint32_t)item[(size_t)w * B + i] << 1) | (outcome[i] ? 1u : 0u);
+      }
+    }
+    const uint64_t ballot = __ballot(take);
+    if (ballot == 0) continue;
+    unsigned long long first = 0;
+    const int leader = __ffsll((unsigned long long)ballot) - 1;
+    if (lane == leader) first = atomicAdd(count, (unsigned long long)__popcll(ballot));
+    first = __shfl(first, leader, 64);
+    if (!take) continue;
+    const int64_t slot = (int64_t)first + __popcll(ballot & ((1ull << lane) - 1));
+    if (slot >= cap) continue;  // overflow: reported by ag_lrts_update
+    key[slot] = k;
+    for (int d = 0; d < OE; ++d) x[(size_t)d * cap + slot] = (float)ctx[(size_t)d * B + i];
+    x[(size_t)OE * cap + slot] = 1.0f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// 2. bucket by agent
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kLrThreads) void k_lrts_hist(const uint32_t *__restrict__ key, int64_t n, int N,
+                                                          int64_t *__restrict__ counts) {
+  extern __shared__ unsigned int s_hist[];
+  for (int a = threadIdx.x; a < N; a += kLrThreads) s_hist[a] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * kLrThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kLrThreads)
+    atomicAdd(&s_hist[key[i] >> 16], 1u);
+  __syncthreads();
+  for (int a = threadIdx.x; a < N; a += kLrThreads)
+    if (s_hist[a]) atomicAdd((unsigned long long *)&counts[a], (unsigned long long)s_hist[a]);
+}
+
+// counts [N] -> offsets [N + 1] (exclusive scan) and cursors [N] = offsets; one block.
+__global__ __launch_bounds__(kLrThreads) void k_lrts_scan(int64_t *__restrict__ counts, int N,
+                                                          int64_t *__restrict__ offsets,
+                                                          int64_t *__restrict__ cursors) {
+  __shared__ int64_t s_carry;
+  __shared__ int64_t s_w[kLrThreads / 64];
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int base = 0; base < N; base += kLrThreads) {
+    const int a = base + threadIdx.x;
+    const int64_t v = a < N ? counts[a] : 0;
+    int64_t incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_w[wv] = incl;
+    __syncthreads();
+    int64_t pre = s_carry;
+    for (int j = 0; j < wv; ++j) pre += s_w[j];
+    if (a < N) {
+      offsets[a] = pre + incl - v;
+      cursors[a] = pre + incl - v;
+    }
+    __syncthreads();
+    if (threadIdx.x == kLrThreads - 1) s_carry = pre + incl;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) offsets[N] = s_carry;
+}
+
+__global__ __launch_bounds__(kLrThreads) void k_lrts_scatter(const uint32_t *__restrict__ key,
+                                                             const float *__restrict__ x, int64_t n,
+                                                             int64_t cap_in, int Do,
+                                                             int64_t *__restrict__ cursors,
+                                                             uint32_t *__restrict__ okey,
+                                                             float *__restrict__ ox, int64_t cap_out) {
+  for (int64_t i = (int64_t)blockIdx.x * kLrThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kLrThreads) {
+    const uint32_t k = key[i];
+    const int64_t pos = (int64_t)atomicAdd((unsigned long long *)&cursors[k >> 16], 1ull);
+    okey[pos] = k;
+    for (int d = 0; d < Do; ++d) ox[(size_t)d * cap_out + pos] = x[(size_t)d * cap_in + i];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// 3. training: one workgroup per agent
+// ---------------------------------------------------------------------------------------
+struct LrSample {
+  float x[AG_LRTS_MAX_DO];
+  int item;
+  int y;
+};
+
+template <int DO>
+__device__ __forceinline__ float lr_logit(const float *__restrict__ w, const float (&x)[AG_LRTS_MAX_DO]) {
+  float z = w[0] * x[0];
+#pragma unroll
+  for (int d = 1; d < DO; ++d) z = z + w[d] * x[d];
+  return z;
+}
+
+template <int DO>
+__device__ __forceinline__ void lr_load(const uint32_t *__restrict__ key, const float *__restrict__ x,
+                                        int64_t cap, int64_t i, LrSample &s) {
+  const uint32_t k = key[i];
+  s.item = (int)((k >> 1) & 0x7fffu);
+  s.y = (int)(k & 1u);
+#pragma unroll
+  for (int d = 0; d < DO; ++d) s.x[d] = x[(size_t)d * cap + i];
+}
+
+// One sample's contribution to the epoch: BCE term (fixed point, returned) and gradient
+// terms added to this lane's accumulator column.
+template <int DO>
+__device__ __forceinline__ int64_t lr_epoch_sample(const LrSample &s, const float *__restrict__ sm,
+                                                   int64_t *__restrict__ acc, const uint64_t *tab) {
+  const float z = lr_logit<DO>(sm + s.item * DO, s.x);
+  const float p = 1.0f / (1.0f + (float)agexp::exp(-(double)z, tab));
+  const double t = s.y ? -fmax(log((double)p), -100.0) : -fmax(log1p(-(double)p), -100.0);
+  const double gz = (double)p - (double)s.y;
+#pragma unroll
+  for (int d = 0; d < DO; ++d) acc[(s.item * DO + d) * kAccStride] += fx_round(gz * (double)s.x[d], kGradScale);
+  return fx_round(t, kLossScale);
+}
+
+template <int DO>
+__device__ __forceinline__ void lr_laplace_sample(const LrSample &s, const float *__restrict__ sm,
+                                                  int64_t *__restrict__ acc, const uint64_t *tab) {
+  const float z = lr_logit<DO>(sm + s.item * DO, s.x);
+  const float P = 1.0f / (1.0f + (float)agexp::exp((double)(1.0f - z), tab));
+  const float w = P * (1.0f - P);
+#pragma unroll
+  for (int d = 0; d < DO; ++d)
+    acc[(s.item * DO + d) * kAccStride] += fx_round((double)w * (double)(s.x[d] * s.x[d]), kGradScale);
+}
+
+template <int DO>
+__global__ __launch_bounds__(kLrThreads) void k_lrts_train(
+    int K, const int32_t *__restrict__ akind, const int64_t *__restrict__ offsets,
+    const uint32_t *__restrict__ key, const float *__restrict__ xs, int64_t cap,
+    float *__restrict__ gm, float *__restrict__ gq, float *__restrict__ gpm,
+    const double *__restrict__ adam_tab, int32_t *__restrict__ epochs_out, float *__restrict__ loss_trace) {
+  const int a = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (akind[a] != AG_ALLOCATOR_LRTS) return;
+  const int64_t s0 = offsets[a], n = offsets[a + 1] - s0;
+  if (n < 2) {  // src/BidderAllocation.py:33-34: nothing changes, not even prev_m
+    if (tid == 0) epochs_out[a] = 0;
+    return;
+  }
+  const int KD = K * DO;
+  extern __shared__ int64_t s_acc[];  // [KD][kAccStride]
+  __shared__ uint64_t s_tab[256];
+  __shared__ float s_m[kLrMaxKD], s_pm[kLrMaxKD], s_q[kLrMaxKD], s_ea[kLrMaxKD], s_es[kLrMaxKD];
+  __shared__ int64_t s_hi[4][kLrMaxKD], s_lo[4][kLrMaxKD];
+  __shared__ int64_t s_lhi[4], s_llo[4];
+  __shared__ float s_hist[kHistory];
+  __shared__ float s_loss, s_negstep, s_bc2;
+  __shared__ double s_lr, s_best;
+  __shared__ int s_bad, s_stop;
+
+  for (int i = tid; i < 256; i += kLrThreads) s_tab[i] = ag_exp_tab[i];
+  float *m_g = gm + (size_t)a * KD, *q_g = gq + (size_t)a * KD, *pm_g = gpm + (size_t)a * KD;
+  for (int c = tid; c < KD; c += kLrThreads) {
+    s_m[c] = m_g[c];
+    s_pm[c] = pm_g[c];
+    s_q[c] = q_g[c];
+    s_ea[c] = 0.0f;
+    s_es[c] = 0.0f;
+  }
+  for (int i = tid; i < KD * kAccStride; i += kLrThreads) s_acc[i] = 0;
+  if (tid == 0) {
+    s_lr = 2e-3;
+    s_best = INFINITY;
+    s_bad = 0;
+    s_stop = 0;
+  }
+  // this lane's samples: the first kLrCache passes live in registers
+  LrSample cache[kLrCache];
+  int ncached = 0;
+#pragma unroll
+  for (int j = 0; j < kLrCache; ++j) {
+    const int64_t i = (int64_t)j * kLrThreads + tid;
+    if (i < n) {
+      lr_load<DO>(key, xs, cap, s0 + i, cache[j]);
+      ncached = j + 1;
+    }
+  }
+  const int64_t stream_from = (int64_t)kLrCache * kLrThreads;
+  int64_t *acc = s_acc + tid;
+  __syncthreads();
+
+  int epoch = 0;
+  for (; epoch < kLrEpochs; ++epoch) {
+    // ---- A: forward + BCE + gradient terms of this lane's samples
+    int64_t lsum = 0;
+#pragma unroll
+    for (int j = 0; j < kLrCache; ++j)
+      if (j < ncached) lsum += lr_epoch_sample<DO>(cache[j], s_m, acc, s_tab);
+    for (int64_t i = stream_from + tid; i < n; i += kLrThreads) {
+      LrSample s;
+      lr_load<DO>(key, xs, cap, s0 + i, s);
+      lsum += lr_epoch_sample<DO>(s, s_m, acc, s_tab);
+    }
+    {
+      const int64_t h = wave_sum(lsum >> 24), l = wave_sum(lsum & kLo24);
+      if (lane == 0) {
+        s_lhi[wv] = h;
+        s_llo[wv] = l;
+      }
+    }
+    __syncthreads();
+    // ---- B: column sums (thread = column c, row group r) and the loss
+    {
+      const int c = tid & 63, r = tid >> 6;
+      if (c < KD) {
+        int64_t h = 0, l = 0;
+        int64_t *col = s_acc + c * kAccStride + r * 64;
+        for (int j = 0; j < 64; ++j) {
+          const int64_t v = col[j];
+          col[j] = 0;
+          h += v >> 24;
+          l += v & kLo24;
+        }
+        s_hi[r][c] = h;
+        s_lo[r][c] = l;
+      }
+      if (tid == 0) {
+        double prior = 0.0;
+        for (int k = 0; k < K; ++k)
+          for (int d = 0; d < DO - 1; ++d) {
+            const double df = (double)s_pm[k * DO + d] - (double)s_m[k * DO + d];
+            prior += (double)s_q[k * DO + d] * (df * df);
+          }
+        const int64_t h = s_lhi[0] + s_lhi[1] + s_lhi[2] + s_lhi[3];
+        const int64_t l = s_llo[0] + s_llo[1] + s_llo[2] + s_llo[3];
+        s_loss = (float)(0.5 * prior + fx_read(h, l, 1.0 / kLossScale));
+        s_negstep = (float)(-(s_lr / adam_tab[epoch]));
+        s_bc2 = (float)adam_tab[kLrEpochs + epoch];
+      }
+    }
+    __syncthreads();
+    // ---- C: Adam on each parameter; scheduler and early stop on thread 0
+    if (tid < KD) {
+      const int c = tid;
+      const int64_t h = s_hi[0][c] + s_hi[1][c] + s_hi[2][c] + s_hi[3][c];
+      const int64_t l = s_lo[0][c] + s_lo[1][c] + s_lo[2][c] + s_lo[3][c];
+      const double gp = (c % DO) < DO - 1 ? -(double)s_q[c] * ((double)s_pm[c] - (double)s_m[c]) : 0.0;
+      const float g = (float)(fx_read(h, l, 1.0 / kGradScale) + gp);
+      const float ea = s_ea[c] + 0.1f * (g - s_ea[c]);
+      const float es = s_es[c] * 0.999f + (0.001f * g) * g;
+      // float32 sqrt correctly rounded (as the CPU sqrtss): via the refined FP64 sqrt --
+      // double rounding is innocuous for sqrt (53 >= 2 * 24 + 2); v_sqrt_f32 is 1 ulp.
+      const float den = (float)__builtin_sqrt((double)es) / s_bc2 + 1e-8f;
+      s_ea[c] = ea;
+      s_es[c] = es;
+      s_m[c] = s_m[c] + s_negstep * (ea / den);
+    }
+    if (tid == 0) {
+      const float loss = s_loss;
+      if (loss_trace) loss_trace[(size_t)a * kLrEpochs + epoch] = loss;
+      s_hist[epoch % kHistory] = loss;
+      if ((double)loss < s_best * (1.0 - 1e-4)) {
+        s_best = (double)loss;
+        s_bad = 0;
+      } else {
+        s_bad += 1;
+      }
+      if (s_bad > 10) {
+        const double nl = s_lr * 0.5;
+        if (s_lr - nl > 1e-8) s_lr = nl;
+        s_bad = 0;
+      }
+      if (epoch > 1024 && fabs((double)s_hist[(epoch - 99) % kHistory] - (double)loss) < 1e-6) s_stop = 1;
+    }
+    __syncthreads();
+    if (s_stop) {
+      ++epoch;
+      break;
+    }
+  }
+
+  // ---- Laplace approximation of q (src/Models.py:43-45), then prev_m = m
+#pragma unroll
+  for (int j = 0; j < kLrCache; ++j)
+    if (j < ncached) lr_laplace_sample<DO>(cache[j], s_m, acc, s_tab);
+  for (int64_t i = stream_from + tid; i < n; i += kLrThreads) {
+    LrSample s;
+    lr_load<DO>(key, xs, cap, s0 + i, s);
+    lr_laplace_sample<DO>(s, s_m, acc, s_tab);
+  }
+  __syncthreads();
+  {
+    const int c = tid & 63, r = tid >> 6;
+    if (c < KD) {
+      int64_t h = 0, l = 0;
+      const int64_t *col = s_acc + c * kAccStride + r * 64;
+      for (int j = 0; j < 64; ++j) {
+        h += col[j] >> 24;
+        l += col[j] & kLo24;
+      }
+      s_hi[r][c] = h;
+      s_lo[r][c] = l;
+    }
+  }
+  __syncthreads();
+  if (tid < KD) {
+    const int c = tid;
+    const int64_t h = s_hi[0][c] + s_hi[1][c] + s_hi[2][c] + s_hi[3][c];
+    const int64_t l = s_lo[0][c] + s_lo[1][c] + s_lo[2][c] + s_lo[3][c];
+    q_g[c] = s_q[c] + (float)fx_read(h, l, 1.0 / kGradScale);
+    m_g[c] = s_m[c];
+    pm_g[c] = s_m[c];
+  }
+  if (tid == 0) epochs_out[a] = epoch;
+}
+
+using TrainKernel = void (*)(int, const int32_t *, const int64_t *, const uint32_t *, const float *, int64_t,
+                             float *, float *, float *, const double *, int32_t *, float *);
+
+TrainKernel pick_train(int Do) {
+  switch (Do) {
+    case 1: return k_lrts_train<1>;
+    case 2: return k_lrts_train<2>;
+    case 3: return k_lrts_train<3>;
+    case 4: return k_lrts_train<4>;
+    case 5: return k_lrts_train<5>;
+    case 6: return k_lrts_train<6>;
+    case 7: return k_lrts_train<7>;
+    case 8: return k_lrts_train<8>;
+    default: return nullptr;
+  }
+}
+
+int grid_over(int64_t n) {
+  int64_t g = (n + kLrThreads - 1) / kLrThreads;
+  if (g > 4096) g = 4096;
+  return (int)(g < 1 ? 1 : g);
+}
+
+int check_store(const ag_ctx *c, const ag_lrts_samples *s, const char *who) {
+  if (!c || !s) return ag_set_error(AG_ERR_INVALID, "%s: null argument", who);
+  if (!s->key || !s->x || !s->count || s->capacity < 0)
+    return ag_set_error(AG_ERR_INVALID, "%s: sample store needs key, x, count and capacity >= 0", who);
+  return AG_OK;
+}
+
+}  // namespace
+
+void ag_lrts_release(ag_ctx *c) {
+  ag_lrts_ws &w = c->lrts;
+  (void)hipFree(w.key);
+  (void)hipFree(w.x);
+  (void)hipFree(w.offsets);
+  (void)hipFree(w.adam_tab);
+  (void)hipFree(w.epochs);
+  w = ag_lrts_ws();
+}
+
+extern "C" {
+
+int ag_lrts_collect(ag_ctx *c, int64_t B, const ag_batch_in *in, const ag_batch_out *out,
+                    const ag_lrts_samples *s, void *stream) {
+  if (int rc = check_store(c, s, "ag_lrts_collect")) return rc;
+  if (!in || !out) return ag_set_error(AG_ERR_INVALID, "ag_lrts_collect: null argument");
+  if (B < 0) return ag_set_error(AG_ERR_INVALID, "ag_lrts_collect: B < 0");
+  if (B == 0 || !c->has_lrts) return AG_OK;
+  if (c->shape.num_agents > 65536 || c->shape.num_items > 32768)
+    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_lrts_collect: sample keys hold N <= 65536, K <= 32768");
+  if (!in->ctx || !in->part || !out->winner || !out->item || !out->outcome)
+    return ag_set_error(AG_ERR_INVALID, "ag_lrts_collect: needs in.ctx, in.part, out.winner, out.item, "
+                                        "out.outcome");
+  AgDeviceGuard g(c->device);
+  hipLaunchKernelGGL(k_lrts_collect, dim3(grid_over(B)), dim3(kLrThreads), 0, (hipStream_t)stream, B,
+                     c->shape.num_participants, c->shape.obs_embedding_size, in->ctx, in->part, out->winner,
+                     out->item, out->outcome, c->d_akind, s->key, s->x, s->capacity,
+                     (unsigned long long *)s->count);
+  AG_HIP(hipGetLastError());
+  return AG_OK;
+}
+
+int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *loss_trace, void *stream) {
+  if (int rc = check_store(c, s, "ag_lrts_update")) return rc;
+  if (!c->has_lrts) return AG_OK;
+  if (!c->lrts_loaded) return ag_set_error(AG_ERR_STATE, "ag_lrts_update: ag_load_lrts not called");
+  const int N = c->shape.num_agents, K = c->shape.num_items, Do = c->shape.obs_embedding_size + 1;
+  TrainKernel train = pick_train(Do);
+  if (!train || K * Do > kLrMaxKD)
+    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_lrts_update: needs OE+1 <= %d and K*(OE+1) <= %d (K=%d, OE+1=%d)",
+                        AG_LRTS_MAX_DO, kLrMaxKD, K, Do);
+  AgDeviceGuard g(c->device);
+  hipStream_t st = (hipStream_t)stream;
+  uint64_t n = 0;
+  AG_HIP(hipMemcpyAsync(&n, s->count, sizeof n, hipMemcpyDeviceToHost, st));
+  AG_HIP(hipStreamSynchronize(st));
+  if ((int64_t)n > s->capacity)
+    return ag_set_error(AG_ERR_INVALID, "ag_lrts_update: %llu won samples overflowed the store (capacity %lld)",
+                        (unsigned long long)n, (long long)s->capacity);
+  ag_lrts_ws &w = c->lrts;
+  if (!w.adam_tab) {
+    double *tab = new double[2 * kLrEpochs];
+    for (int t = 0; t < kLrEpochs; ++t) {  // torch.optim.Adam: Python floats, libm pow
+      tab[t] = 1.0 - pow(0.9, (double)(t + 1));
+      tab[kLrEpochs + t] = pow(1.0 - pow(0.999, (double)(t + 1)), 0.5);
+    }
+    hipError_t e = hipMalloc(&w.adam_tab, sizeof(double) * 2 * kLrEpochs);
+    if (e == hipSuccess) e = hipMemcpy(w.adam_tab, tab, sizeof(double) * 2 * kLrEpochs, hipMemcpyHostToDevice);
+    delete[] tab;
+    if (e == hipSuccess) e = hipMalloc(&w.offsets, sizeof(int64_t) * (3 * (size_t)N + 1));
+    if (e == hipSuccess) e = hipMalloc(&w.epochs, sizeof(int32_t) * N);
+    if (e != hipSuccess) {
+      ag_lrts_release(c);
+      return ag_set_error(AG_ERR_HIP, "ag_lrts_update: workspace: %s", hipGetErrorString(e));
+    }
+  }
+  if ((int64_t)n > w.cap) {
+    (void)hipFree(w.key);
+    (void)hipFree(w.x);
+    w.key = nullptr;
+    w.x = nullptr;
+    const int64_t cap = (int64_t)n + ((int64_t)n >> 2) + 1024;
+    hipError_t e = hipMalloc(&w.key, sizeof(uint32_t) * cap);
+    if (e == hipSuccess) e = hipMalloc(&w.x, sizeof(float) * (size_t)Do * cap);
+    if (e != hipSuccess) {
+      w.cap = 0;
+      return ag_set_error(AG_ERR_HIP, "ag_lrts_update: sample workspace: %s", hipGetErrorString(e));
+    }
+    w.cap = cap;
+  }
+  int64_t *counts = w.offsets + N + 1, *cursors = counts + N;
+  AG_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * N, st));
+  if (n > 0) {
+    if ((size_t)N * 4 > 64 * 1024)
+      return ag_set_error(AG_ERR_UNSUPPORTED, "ag_lrts_update: N=%d agents > 16384", N);
+    hipLaunchKernelGGL(k_lrts_hist, dim3(grid_over((int64_t)n)), dim3(kLrThreads), (size_t)N * 4, st, s->key,
+                       (int64_t)n, N, counts);
+    AG_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_lrts_scan, dim3(1), dim3(kLrThreads), 0, st, counts, N, w.offsets, cursors);
+  AG_HIP(hipGetLastError());
+  if (n > 0) {
+    hipLaunchKernelGGL(k_lrts_scatter, dim3(grid_over((int64_t)n)), dim3(kLrThreads), 0, st, s->key, s->x,
+                       (int64_t)n, s->capacity, Do, cursors, w.key, w.x, w.cap);
+    AG_HIP(hipGetLastError());
+  }
+  const size_t lds = sizeof(int64_t) * (size_t)K * Do * kAccStride;
+  AG_HIP(hipFuncSetAttribute((const void *)train, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(train, dim3(N), dim3(kLrThreads), lds, st, K, c->d_akind, w.offsets, w.key, w.x, w.cap,
+                     c->d_tsm, c->d_tsq, c->d_tsprev, w.adam_tab, w.epochs, loss_trace);
+  AG_HIP(hipGetLastError());
+  if (epochs) {
+    AG_HIP(hipMemcpyAsync(epochs, w.epochs, sizeof(int32_t) * N, hipMemcpyDeviceToHost, st));
+    AG_HIP(hipStreamSynchronize(st));
+  }
+  return AG_OK;
+}
+
+int ag_lrts_read(ag_ctx *c, float *m, float *q, float *prev_m) {
+  if (!c) return ag_set_error(AG_ERR_INVALID, "ag_lrts_read: null ctx");
+  AgDeviceGuard g(c->device);
+  const size_t n = (size_t)c->shape.num_agents * c->shape.num_items * (c->shape.obs_embedding_size + 1);
+  AG_HIP(hipDeviceSynchronize());
+  if (m) AG_HIP(hipMemcpy(m, c->d_tsm, n * sizeof(float), hipMemcpyDeviceToHost));
+  if (q) AG_HIP(hipMemcpy(q, c->d_tsq, n * sizeof(float), hipMemcpyDeviceToHost));
+  if (prev_m) AG_HIP(hipMemcpy(prev_m, c->d_tsprev, n * sizeof(float), hipMemcpyDeviceToHost));
+  return AG_OK;
+}
+
+}  // extern "C"

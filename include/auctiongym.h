@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define AG_ABI_VERSION 2
+#define AG_ABI_VERSION 3
 
 typedef enum ag_status {
   AG_OK = 0,
@@ -140,10 +140,12 @@ int ag_set_agent_kinds(ag_ctx *ctx, const int32_t *allocator_kind, const int32_t
 int ag_set_agent_params(ag_ctx *ctx, const int32_t *allocator_kind, const int32_t *bidder_kind,
                         const double *prev_gamma, const double *gamma_sigma);
 
-/* LR-TS posterior of every AG_ALLOCATOR_LRTS agent, host float32 [N][K][OE+1] m and q
- * (PyTorchLogisticRegression.m / .q, src/Models.py:21-24; rows of other agents ignored);
- * thompson_sampling: add the batch's ts_noise to m for the item choice (src/Models.py:30-31). */
-int ag_load_lrts(ag_ctx *ctx, const float *m, const float *q, int32_t thompson_sampling);
+/* LR-TS posterior of every AG_ALLOCATOR_LRTS agent, host float32 [N][K][OE+1] m, q and
+ * prev_m (PyTorchLogisticRegression.m / .q / .prev_iter_m, src/Models.py:21-24; rows of
+ * other agents ignored; prev_m NULL = m, as at construction); thompson_sampling: add the
+ * batch's ts_noise to m for the item choice (src/Models.py:30-31). */
+int ag_load_lrts(ag_ctx *ctx, const float *m, const float *q, const float *prev_m,
+                 int32_t thompson_sampling);
 
 /* Options (ag_set_option). */
 typedef enum ag_option {
@@ -190,6 +192,40 @@ int ag_generate(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B, d
  * (0 otherwise); either output may be NULL. Same Philox key / counter scheme. */
 int ag_generate_noise(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B,
                       const int32_t *part, double *gamma_raw, float *ts_noise, void *stream);
+
+/* ---- LR-TS allocator update (Agent.update -> PyTorchLogisticRegressionAllocator.update,
+ * src/Agent.py:79-91, src/BidderAllocation.py:29-65) ------------------------------------
+ * The won samples of LR-TS agents (Agent.update's won_mask) accumulate in a caller-owned
+ * device store between updates; reset *count to 0 where the reference calls
+ * Agent.clear_logs. Records are unordered: the update's sums are exact, so the order
+ * samples arrive in (or the rank that collected them) cannot change the result. */
+#define AG_LRTS_MAX_EPOCHS 16384 /* epochs = 8192 * 2 (src/BidderAllocation.py:38) */
+#define AG_LRTS_MAX_DO 8         /* OE + 1 <= 8; K * (OE + 1) <= 64 */
+
+typedef struct ag_lrts_samples {
+  uint32_t *key;     /* dev [capacity]: agent << 16 | item << 1 | outcome               */
+  float *x;          /* dev [OE+1][capacity]: float32(observed context), 1.0             */
+  int64_t capacity;
+  uint64_t *count;   /* dev [1]: records appended; > capacity = overflow (update fails)  */
+} ag_lrts_samples;
+
+/* Append the won LR-TS samples of one simulated batch (the in/out of ag_simulate; needs
+ * in.ctx, in.part, out.winner, out.item, out.outcome). Hot call: stream-ordered. */
+int ag_lrts_collect(ag_ctx *ctx, int64_t B, const ag_batch_in *in, const ag_batch_out *out,
+                    const ag_lrts_samples *samples, void *stream);
+
+/* Train every LR-TS agent on its samples in the store: the reference's epoch loop (Adam
+ * lr 2e-3, ReduceLROnPlateau, early stop), the Laplace update of q and prev_m = m; agents
+ * with < 2 samples are left unchanged. The updated posterior stays on the device for the
+ * next ag_simulate. Synchronises `stream` (reads the sample count). epochs: host [N]
+ * epochs run per agent (0: not trained), may be NULL; loss_trace: dev float32
+ * [N][AG_LRTS_MAX_EPOCHS] per-epoch loss.item(), may be NULL. Arithmetic:
+ * oracle/ag_oracle.c ora_lrts_update. */
+int ag_lrts_update(ag_ctx *ctx, const ag_lrts_samples *samples, int32_t *epochs,
+                   float *loss_trace, void *stream);
+
+/* Current LR-TS posterior, host float32 [N][K][OE+1] (any may be NULL). Synchronises. */
+int ag_lrts_read(ag_ctx *ctx, float *m, float *q, float *prev_m);
 
 /* Exact counters (host int64 [n][AG_FX_LIMBS], e.g. copied back or all-reduced)
  * -> doubles (host [n]), correctly rounded from the exact fixed-point sum. */

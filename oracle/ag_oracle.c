@@ -391,3 +391,139 @@ void ora_gen_participants(uint64_t seed, uint64_t idx, int32_t N, int32_t P, int
     part_out[n++] = pick;
   }
 }
+
+/* ---------------------------------------------------------------------------------------
+ * LR-TS allocator update (PyTorchLogisticRegressionAllocator.update,
+ * src/BidderAllocation.py:29-65; model src/Models.py:35-48), restated with exact sums.
+ *
+ * Per epoch (src/BidderAllocation.py:44-55): forward on every won sample, loss = prior +
+ * BCE (sum), backward, Adam(lr 2e-3) step, ReduceLROnPlateau('min', factor 0.5) on the
+ * loss, early stop when epoch > 1024 and |loss[-100] - loss[-1]| < 1e-6. Then the Laplace
+ * update of q per item (:58-61, src/Models.py:43-45) and prev_m = m (:62).
+ *
+ * Arithmetic (the definition the device kernel follows bit for bit):
+ *  - z = x . m[a] in float32, products rounded separately, summed in order (as
+ *    ora_ts_ctr); p = 1 / (1 + (float)exp(-(double)z)) in float32.
+ *  - BCE term (torch.nn.BCELoss, logs clamped at -100) in double: y ? -max(log p, -100)
+ *    : -max(log1p(-p), -100); gradient term (p - y) * x_d, exact in double.
+ *  - Sums over samples are EXACT: every term is rounded to a fixed-point grid (BCE 2^-32,
+ *    gradient and Laplace 2^-40) and added as integers, so no summation order exists;
+ *    a sum S is read back as (double)(S >> 24) * 2^24 + (double)(S & (2^24-1)).
+ *  - prior loss 0.5 * sum q (pm - m)^2 and its gradient -q (pm - m) in double (row-major
+ *    order); gradient and loss are rounded to float32 once.
+ *  - Adam (torch.optim.Adam defaults, single-tensor CPU path) in float32:
+ *    ea += 0.1f * (g - ea); es = es * 0.999f + (0.001f * g) * g;
+ *    m += (float)(-lr / bc1) * (ea / (sqrtf(es) / (float)pow(bc2, 0.5) + 1e-8f)),
+ *    bc1 = 1 - pow(0.9, t), bc2 = 1 - pow(0.999, t) in double (Python floats).
+ *  - Laplace: P = 1 / (1 + (float)exp((double)(1 - z))) with z as above (float32),
+ *    q[k][d] += (float)sum P (1 - P) x_d^2 (products float32, sum exact).
+ * torch sums in float32 in its own order: the reference agrees to float32 rounding per
+ * epoch (tests/test_oracle_golden.py pins loss0 / grad0 and the trajectory).
+ * ------------------------------------------------------------------------------------- */
+#define ORA_LR_EPOCHS 16384
+
+static int64_t fx_round(double v, double scale) { return (int64_t)nearbyint(v * scale); }
+
+static double fx_read(__int128 s, double inv_scale) {
+  /* the device holds these sums split at bit 24; same read-back */
+  int64_t hi = (int64_t)(s >> 24), lo = (int64_t)(s & 0xFFFFFF);
+  return ((double)hi * 0x1p24 + (double)lo) * inv_scale;
+}
+
+/* One epoch's loss (loss.item()) and float32 gradient g [K][Do] at m. */
+static float lrts_loss_grad(int64_t n, int32_t K, int32_t Do, const float *X, const int32_t *A,
+                            const uint8_t *y, const float *m, const float *pm, const float *q,
+                            __int128 *G, float *g) {
+  const int32_t KD = K * Do;
+  __int128 L = 0;
+  for (int32_t c = 0; c < KD; ++c) G[c] = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const float *x = X + i * Do, *w = m + (int64_t)A[i] * Do;
+    float z = w[0] * x[0];
+    for (int32_t d = 1; d < Do; ++d) z = z + w[d] * x[d];
+    float p = 1.0f / (1.0f + (float)exp(-(double)z));
+    double t = y[i] ? -fmax(log((double)p), -100.0) : -fmax(log1p(-(double)p), -100.0);
+    L += fx_round(t, 0x1p32);
+    double gz = (double)p - (double)y[i];
+    for (int32_t d = 0; d < Do; ++d) G[A[i] * Do + d] += fx_round(gz * (double)x[d], 0x1p40);
+  }
+  double prior = 0.0;
+  for (int32_t k = 0; k < K; ++k)
+    for (int32_t d = 0; d < Do - 1; ++d) {
+      double df = (double)pm[k * Do + d] - (double)m[k * Do + d];
+      prior += (double)q[k * Do + d] * (df * df);
+    }
+  for (int32_t c = 0; c < KD; ++c) {
+    double gp = (c % Do) < Do - 1 ? -(double)q[c] * ((double)pm[c] - (double)m[c]) : 0.0;
+    g[c] = (float)(fx_read(G[c], 0x1p-40) + gp);
+  }
+  return (float)(0.5 * prior + fx_read(L, 0x1p-32));
+}
+
+float ora_lrts_loss_grad(int64_t n, int32_t K, int32_t Do, const float *X, const int32_t *A,
+                         const uint8_t *y, const float *m, const float *pm, const float *q, float *g) {
+  __int128 *G = malloc((size_t)K * Do * sizeof(__int128));
+  float loss = lrts_loss_grad(n, K, Do, X, A, y, m, pm, q, G, g);
+  free(G);
+  return loss;
+}
+
+int32_t ora_lrts_update(int64_t n, int32_t K, int32_t Do, const float *X, const int32_t *A,
+                        const uint8_t *y, float *m, float *pm, float *q, float *loss_trace) {
+  if (n < 2) return 0;
+  const int32_t KD = K * Do;
+  float *ea = calloc(KD, sizeof(float)), *es = calloc(KD, sizeof(float)), *g = malloc(KD * sizeof(float));
+  __int128 *G = malloc(KD * sizeof(__int128));
+  double lr = 2e-3, best = INFINITY;
+  int32_t bad = 0, epoch = 0;
+  float hist[100];
+  for (epoch = 0; epoch < ORA_LR_EPOCHS; ++epoch) {
+    float loss = lrts_loss_grad(n, K, Do, X, A, y, m, pm, q, G, g);
+    const double step = (double)(epoch + 1);
+    const double bc1 = 1.0 - pow(0.9, step), bc2s = pow(1.0 - pow(0.999, step), 0.5);
+    const float neg_step = (float)(-(lr / bc1)), bc2f = (float)bc2s;
+    for (int32_t c = 0; c < KD; ++c) {
+      ea[c] = ea[c] + 0.1f * (g[c] - ea[c]);
+      es[c] = es[c] * 0.999f + (0.001f * g[c]) * g[c];
+      float den = sqrtf(es[c]) / bc2f + 1e-8f;
+      m[c] = m[c] + neg_step * (ea[c] / den);
+    }
+    if (loss_trace) loss_trace[epoch] = loss;
+    hist[epoch % 100] = loss;
+    /* ReduceLROnPlateau(mode min, threshold 1e-4 rel, patience 10, factor 0.5, eps 1e-8) */
+    if ((double)loss < best * (1.0 - 1e-4)) {
+      best = (double)loss;
+      bad = 0;
+    } else {
+      ++bad;
+    }
+    if (bad > 10) {
+      double nl = lr * 0.5;
+      if (lr - nl > 1e-8) lr = nl;
+      bad = 0;
+    }
+    if (epoch > 1024 && fabs((double)hist[(epoch - 99) % 100] - (double)loss) < 1e-6) {
+      ++epoch;
+      break;
+    }
+  }
+  /* Laplace approximation of q per item, then the prior update */
+  for (int32_t c = 0; c < KD; ++c) G[c] = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const float *x = X + i * Do, *w = m + (int64_t)A[i] * Do;
+    float z = w[0] * x[0];
+    for (int32_t d = 1; d < Do; ++d) z = z + w[d] * x[d];
+    float P = 1.0f / (1.0f + (float)exp((double)(1.0f - z)));
+    float wgt = P * (1.0f - P);
+    for (int32_t d = 0; d < Do; ++d) G[A[i] * Do + d] += fx_round((double)wgt * (double)(x[d] * x[d]), 0x1p40);
+  }
+  for (int32_t c = 0; c < KD; ++c) {
+    q[c] = q[c] + (float)fx_read(G[c], 0x1p-40);
+    pm[c] = m[c];
+  }
+  free(ea);
+  free(es);
+  free(g);
+  free(G);
+  return epoch;
+}

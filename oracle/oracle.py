@@ -81,6 +81,10 @@ def lib():
         L.ora_gen_participants.argtypes = [u64, u64, i32, i32, vp]
         L.ora_philox4x32_10.restype = None
         L.ora_philox4x32_10.argtypes = [vp, vp, vp]
+        L.ora_lrts_loss_grad.restype = ctypes.c_float
+        L.ora_lrts_loss_grad.argtypes = [i64, i32, i32, vp, vp, vp, vp, vp, vp, vp]
+        L.ora_lrts_update.restype = i32
+        L.ora_lrts_update.argtypes = [i64, i32, i32, vp, vp, vp, vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -201,3 +205,34 @@ def philox(ctr, key):
     o = np.empty(4, np.uint32)
     lib().ora_philox4x32_10(_p(c), _p(k), _p(o))
     return o
+
+
+def lrts_update(X, A, y, m, prev_m, q, trace=True):
+    """PyTorchLogisticRegressionAllocator.update (src/BidderAllocation.py:29-65) of one
+    agent on its won samples X [n][Do], A [n], y [n]; returns (m, prev_m, q, epochs,
+    losses) after the update (inputs are not modified)."""
+    X = np.ascontiguousarray(X, np.float32)
+    A = np.ascontiguousarray(A, np.int32)
+    y = np.ascontiguousarray(np.asarray(y) != 0, np.uint8)
+    m = np.array(m, np.float32, order="C")
+    pm = np.array(prev_m, np.float32, order="C")
+    q = np.array(q, np.float32, order="C")
+    K, Do = m.shape
+    tr = np.zeros(16384, np.float32)
+    ep = lib().ora_lrts_update(len(y), K, Do, _p(X), _p(A), _p(y), _p(m), _p(pm), _p(q),
+                               _p(tr) if trace else None)
+    return m, pm, q, int(ep), tr[:ep].astype(np.float64)
+
+
+def lrts_loss_grad(X, A, y, m, prev_m, q):
+    """Loss and float32 gradient of one epoch of the LR-TS update at m."""
+    X = np.ascontiguousarray(X, np.float32)
+    A = np.ascontiguousarray(A, np.int32)
+    y = np.ascontiguousarray(np.asarray(y) != 0, np.uint8)
+    m = np.ascontiguousarray(m, np.float32)
+    pm = np.ascontiguousarray(prev_m, np.float32)
+    q = np.ascontiguousarray(q, np.float32)
+    g = np.empty_like(m)
+    loss = lib().ora_lrts_loss_grad(len(y), m.shape[0], m.shape[1], _p(X), _p(A), _p(y), _p(m),
+                                    _p(pm), _p(q), _p(g))
+    return float(loss), g

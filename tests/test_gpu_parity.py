@@ -348,7 +348,7 @@ def _pop_engine(meta, d, gpu):
     eng.set_agent_params(args["alloc_kind"], args["bid_kind"], args["prev_gamma"], args["gamma_sigma"])
     eng.load_catalog(d["items"], d["values"])
     if args["ts_m"] is not None:
-        eng.load_lrts(args["ts_m"], np.ones_like(args["ts_m"]), True)
+        eng.load_lrts(args["ts_m"], np.ones_like(args["ts_m"]), thompson_sampling=True)
     return eng, args
 
 
@@ -419,7 +419,7 @@ def test_mixed_population_full_size(gpu, oracle):
     eng = AuctionEngine(N, P, K, E, OE, 0, 1.0)
     eng.set_agent_params(ak, bk, pg, gs)
     eng.load_catalog(items, values)
-    eng.load_lrts(m, q, True)
+    eng.load_lrts(m, q, thompson_sampling=True)
     inp = eng.alloc_inputs(B)
     eng.generate(5, 0, inp)
     eng.generate_noise(5, 0, inp)
@@ -445,4 +445,178 @@ def test_mixed_population_full_size(gpu, oracle):
     for k in ("winner", "price", "second_price", "outcome"):
         assert np.array_equal(got[k], orc[k], equal_nan=True), k
     assert np.array_equal(cnt.cpu().numpy(), orc["counters_fx"])
+    eng.close()
+
+
+# ---- LR-TS allocator update (Agent.update -> PyTorchLogisticRegressionAllocator.update) ----
+def _kat_population():
+    kat = np.load(os.path.join(GOLDEN, "sp_ts_update_kat.npz"))
+    stack = lambda n: np.stack([kat[f"a{a}_{n}"] for a in range(6)]).astype(np.float32)  # noqa: E731
+    return kat, stack("m0"), stack("q0"), stack("prevm0")
+
+
+def _fill_store(eng, per_agent, capacity=None, seed=0):
+    """Caller-owned sample store holding `per_agent` {agent: (X, A, y)}, shuffled."""
+    import torch
+    keys, xs = [], []
+    for a, (X, A, y) in per_agent.items():
+        keys.append((np.int64(a) << 16) | (np.asarray(A, np.int64) << 1) | (np.asarray(y) != 0))
+        xs.append(np.asarray(X, np.float32))
+    key = np.concatenate(keys).astype(np.uint32)
+    x = np.concatenate(xs)
+    perm = np.random.default_rng(seed).permutation(len(key))
+    key, x = key[perm], x[perm]
+    cap = capacity or len(key)
+    st = eng.new_lrts_samples(cap)
+    n = min(len(key), cap)
+    st["key"][:n] = torch.from_numpy(key[:n].view(np.int32)).to(eng.device)
+    st["x"][:, :n] = torch.from_numpy(np.ascontiguousarray(x[:n].T)).to(eng.device)
+    st["count"][0] = len(key)
+    return st
+
+
+def _lrts_engine(N=6, P=2, K=12, E=5, OE=4, lrts=None):
+    from auctiongym_amd.engine import AuctionEngine
+    d, meta, _ = load_capture("sp_ts_r2048")
+    eng = AuctionEngine(N, P, K, E, OE, 1, 1.0)
+    ak = np.ones(N, np.int32) if lrts is None else np.asarray(lrts, np.int32)
+    eng.set_agent_params(ak, np.zeros(N, np.int32))
+    if N == 6:
+        eng.load_catalog(d["items"], d["values"])
+    return eng
+
+
+def test_lrts_update_matches_oracle_and_reference(gpu, oracle):
+    """The six SP_Truthful_TS agents' iteration-0 updates on the GPU (one workgroup per
+    agent, all six at once) vs the oracle, bit for bit: epochs run, every epoch's loss,
+    m, q and prev_m; and vs the reference within the oracle's pinned tolerances."""
+    kat, m0, q0, pm0 = _kat_population()
+    eng = _lrts_engine()
+    eng.load_lrts(m0, q0, pm0, thompson_sampling=True)
+    st = _fill_store(eng, {a: (kat[f"a{a}_X"], kat[f"a{a}_A"], kat[f"a{a}_y"]) for a in range(6)})
+    ep, tr = eng.lrts_update(st, trace=True)
+    m, q, pm = eng.lrts_state()
+    tr = tr.cpu().numpy()
+    for a in range(6):
+        k = lambda n: kat[f"a{a}_{n}"]  # noqa: E731
+        om, opm, oq, oep, oL = oracle.lrts_update(k("X"), k("A"), k("y"), k("m0"), k("prevm0"), k("q0"))
+        assert ep[a] == oep
+        assert np.array_equal(tr[a, :oep], oL.astype(np.float32))
+        assert np.array_equal(m[a], om) and np.array_equal(q[a], oq) and np.array_equal(pm[a], opm)
+        np.testing.assert_allclose(m[a], k("m1"), atol=2e-2)
+        np.testing.assert_allclose(q[a], k("q1"), rtol=2e-3)
+    eng.close()
+
+
+def test_lrts_collect_from_replay_and_update(gpu, oracle):
+    """Replay the SP_Truthful_TS capture, collect the won samples on the GPU: the store holds
+    exactly the reference's Agent.update samples (as a multiset; float32 contexts); the
+    update from that store equals the update from the reference's own samples."""
+    import torch
+    d, meta, _ = load_capture("sp_ts_r2048")
+    kat, m0, q0, pm0 = _kat_population()
+    eng, args = _pop_engine(meta, d, gpu)
+    eng.load_lrts(np.asarray(d["ts_m"], np.float32), q0, pm0, thompson_sampling=True)
+    B, P, Do = len(d["u"]), meta["P"], meta["OE"] + 1
+    dev = eng.device
+    inp = {"ctx": torch.from_numpy(np.ascontiguousarray(d["ctx"].T)).to(dev),
+           "part": torch.from_numpy(np.ascontiguousarray(d["part"].T.astype(np.int32))).to(dev),
+           "u": torch.from_numpy(np.ascontiguousarray(d["u"])).to(dev),
+           "gamma_raw": torch.from_numpy(np.ascontiguousarray(d["gamma_raw"].T)).to(dev),
+           "ts_noise": torch.from_numpy(np.ascontiguousarray(
+               d["ts_noise"].reshape(B, P, -1).transpose(1, 2, 0))).to(dev)}
+    out = eng.alloc_outputs(B)
+    st = eng.new_lrts_samples(B)
+    half = B // 2  # two batches, as two flushes of one iteration
+    for lo, hi in ((0, half), (half, B)):
+        bi = {k: v[..., lo:hi].contiguous() for k, v in inp.items()}
+        bo = eng.alloc_outputs(hi - lo)
+        eng.simulate(bi, bo)
+        eng.lrts_collect(bi, bo, st)
+    torch.cuda.synchronize()
+    n = int(st["count"][0])
+    key = st["key"][:n].cpu().numpy().view(np.uint32)
+    x = st["x"][:, :n].cpu().numpy().T
+    got = sorted(zip(key.tolist(), map(tuple, x.tolist())))
+    want = []
+    for a in range(6):
+        X, A, y = kat[f"a{a}_X"], kat[f"a{a}_A"], kat[f"a{a}_y"]
+        Xf = X.astype(np.float32)
+        for j in range(len(y)):
+            want.append(((a << 16) | (int(A[j]) << 1) | int(y[j]), tuple(Xf[j].tolist())))
+    assert got == sorted(want)
+    # the update from the collected store == the update from the reference's samples
+    eng.load_lrts(m0, q0, pm0, thompson_sampling=True)
+    ep = eng.lrts_update(st)
+    m, q, pm = eng.lrts_state()
+    for a in range(6):
+        k = lambda n: kat[f"a{a}_{n}"]  # noqa: E731
+        om, opm, oq, oep, _ = oracle.lrts_update(k("X"), k("A"), k("y"), k("m0"), k("prevm0"), k("q0"))
+        assert ep[a] == oep and np.array_equal(m[a], om) and np.array_equal(q[a], oq)
+    eng.close()
+
+
+def test_lrts_update_edge_cases(gpu, oracle):
+    """< 2 samples: unchanged (src/BidderAllocation.py:33-34); non-LR-TS agents untouched;
+    an overflowed store is an error, not a silent truncation."""
+    g = np.random.default_rng(3)
+    N, K, Do = 4, 12, 5
+    eng = _lrts_engine(N=N, lrts=[1, 1, 0, 1])
+    m0 = g.normal(0, 1, (N, K, Do)).astype(np.float32)
+    q0 = (1 + g.random((N, K, Do))).astype(np.float32)
+    pm0 = (m0 + 0.5).astype(np.float32)
+    eng.load_lrts(m0, q0, pm0)
+    X = np.concatenate([g.normal(0, 1, (200, Do - 1)), np.ones((200, 1))], axis=1)
+    A, y = g.integers(0, K, 200), g.random(200) < 0.3
+    st = _fill_store(eng, {0: (X[:1], A[:1], y[:1]), 3: (X, A, y)})
+    ep = eng.lrts_update(st)
+    m, q, pm = eng.lrts_state()
+    assert ep[0] == 0 and ep[1] == 0 and ep[2] == 0 and ep[3] > 0
+    for a in (0, 1, 2):
+        assert np.array_equal(m[a], m0[a]) and np.array_equal(q[a], q0[a]) and np.array_equal(pm[a], pm0[a])
+    om, opm, oq, oep, _ = oracle.lrts_update(X, A, y, m0[3], pm0[3], q0[3])
+    assert ep[3] == oep and np.array_equal(m[3], om) and np.array_equal(q[3], oq)
+    over = _fill_store(eng, {3: (X, A, y)}, capacity=100)
+    with pytest.raises(ValueError, match="overflow"):
+        eng.lrts_update(over)
+    eng.close()
+
+
+def test_lrts_update_at_scale(gpu, oracle):
+    """A mixed 32-agent population simulated on 2^16 synthetic auctions, collected and
+    trained on the GPU (16 LR-TS agents, ~1.4k samples each); four agents re-trained by the
+    oracle on the collected samples, bit for bit."""
+    import torch
+    from auctiongym_amd.engine import AuctionEngine
+    N, P, K, E, OE, B = 32, 8, 12, 5, 4, 1 << 16
+    g = np.random.default_rng(22)
+    items = np.concatenate([g.normal(0, 1, (N, K, E)), -3.0 - g.random((N, K, 1))], axis=2)
+    values = g.lognormal(0.1, 0.2, (N, K))
+    ak = np.array([i % 2 for i in range(N)], np.int32)
+    bk = np.zeros(N, np.int32)
+    m0 = g.normal(0, 1, (N, K, OE + 1)).astype(np.float32)
+    q0 = np.ones((N, K, OE + 1), np.float32)
+    eng = AuctionEngine(N, P, K, E, OE, 0, 1.0)
+    eng.set_agent_params(ak, bk)
+    eng.load_catalog(items, values)
+    eng.load_lrts(m0, q0)
+    inp = eng.alloc_inputs(B)
+    eng.generate(9, 0, inp)
+    eng.generate_noise(9, 0, inp)
+    out = eng.alloc_outputs(B)
+    eng.simulate(inp, out)
+    st = eng.new_lrts_samples(B)
+    eng.lrts_collect(inp, out, st)
+    torch.cuda.synchronize()
+    n = int(st["count"][0])
+    key = st["key"][:n].cpu().numpy().view(np.uint32)
+    x = np.ascontiguousarray(st["x"][:, :n].cpu().numpy().T)
+    ep = eng.lrts_update(st)
+    m, q, pm = eng.lrts_state()
+    assert (ep[ak == 1] > 0).all() and (ep[ak == 0] == 0).all()
+    for a in (1, 7, 21, 31):
+        sel = (key >> 16) == a
+        om, opm, oq, oep, _ = oracle.lrts_update(x[sel], (key[sel] >> 1) & 0x7FFF, key[sel] & 1,
+                                                 m0[a], m0[a], q0[a])
+        assert ep[a] == oep and np.array_equal(m[a], om) and np.array_equal(q[a], oq)
     eng.close()
