@@ -72,11 +72,12 @@ class Agent:
 
     def update(self, iteration, plot=False, figsize=(8, 5), fontsize=14):
         """src/Agent.py:79-94. Oracle / Truthful updates are no-ops (src/BidderAllocation.py:
-        17-18, src/Bidder.py:21-22); learned plugins are refused at engine creation."""
+        17-18, src/Bidder.py:21-22); the LR-TS allocator trains on the GPU over this agent's
+        won samples (Auction._update_agent); shading bidders' updates are not built yet and
+        raise NotImplementedError."""
         self._sync()
-        self.allocator.update(None, None, None, iteration, plot, figsize, fontsize, self.name)
-        self.bidder.update(None, None, None, None, None, None, None, iteration, plot, figsize,
-                           fontsize, self.name)
+        if self._auction is not None:
+            self._auction._update_agent(self._index, iteration)
 
     def get_allocation_regret(self):
         return self._get("allocation_regret")
@@ -120,6 +121,7 @@ class Agent:
             self._fx[i] = 0
         if self._auction is not None:
             self._log_start = self._auction._log_rounds()
+            self._auction._cleared_logs(self._index)
         self.bidder.clear_logs(memory=self.memory)
 
     def __repr__(self):

@@ -4,13 +4,19 @@ Rounds within an iteration are independent given agent state (agent state change
 in Agent.update, between iterations), so the round loop is a data-parallel batch:
 
 * `simulate_opportunity()` -- the reference's per-round call. It draws the round's
-  random inputs from the shared numpy Generator in the reference's order (src/Auction.py:
-  30, 33, 42, then the one next_double binomial consumes at :65) and queues them; the
-  queued rounds run as ONE fused kernel launch the first time anything reads state
-  (net_utility, revenue, update, ...). Same draws, same results, one launch.
+  random inputs in the reference's order (src/Auction.py:30, 33, 42; the bidders' and
+  Thompson samplers' draws in slot order; then the one next_double binomial consumes at
+  :65) and queues them; the queued rounds run as ONE fused kernel launch the first time
+  anything reads state (net_utility, revenue, update, ...). Same draws, same results.
 * `simulate_batch(B)` -- the same, for B rounds at once.
 * `simulate_synthetic(B, seed)` -- B rounds whose inputs are generated on the GPU
   (Philox4x32-10 keyed by the global auction index); the rng is not touched.
+
+Agent.update of learning plugins (src/Agent.py:79-94) runs on the GPU too: the won
+samples of LR-TS agents are collected on the device after every batch
+(ag_lrts_collect), and the first LR-TS agent's update() trains every LR-TS agent of the
+auction in one launch (ag_lrts_update; the agents' updates are independent, so batching
+them is the reference's per-agent loop, src/main.py:127-152).
 """
 import numpy as np
 import torch
@@ -18,7 +24,7 @@ import torch
 from . import Agent as _agent_mod
 from . import _lib
 from .engine import AuctionEngine
-from .replay import draw_round
+from .replay import draw_round, draw_round_population
 
 C = _agent_mod.C
 
@@ -27,6 +33,7 @@ class Auction:
     """Base class for auctions (src/Auction.py:9-26)."""
 
     FLUSH_ROUNDS = 1 << 20
+    FLUSH_ROUNDS_TS = 1 << 16  # Thompson-sampling rounds carry K*(OE+1) floats per slot
 
     def __init__(self, rng, allocation, agents, agent2items, agents2item_values, max_slots,
                  embedding_size, embedding_var, obs_embedding_size, num_participants_per_round):
@@ -47,46 +54,94 @@ class Auction:
         if len(ks) != 1:
             raise NotImplementedError("all agents must have the same num_items")
         K = ks.pop()
+        N = len(agents)
         for a in agents:
             if a.allocator.kind is None or a.bidder.kind is None:
                 raise NotImplementedError(
                     f"agent {a.name!r}: {type(a.allocator).__name__} + {type(a.bidder).__name__} "
-                    "is not on the GPU path yet (built: OracleAllocator + TruthfulBidder)")
-        self._engine = AuctionEngine(len(agents), num_participants_per_round, K, embedding_size,
-                                     obs_embedding_size, allocation.code, embedding_var)
-        self._engine.set_agent_kinds([a.allocator.kind for a in agents],
-                                     [a.bidder.kind for a in agents])
+                    "is not on the GPU path")
+        ak = np.array([a.allocator.kind for a in agents], np.int32)
+        bk = np.array([a.bidder.kind for a in agents], np.int32)
+        self._shading = bk != _lib.BIDDER_TRUTHFUL
+        self._lrts = ak == _lib.ALLOCATOR_LRTS
+        self._engine = eng = AuctionEngine(N, num_participants_per_round, K, embedding_size,
+                                           obs_embedding_size, allocation.code, embedding_var)
+        pg = np.array([getattr(a.bidder, "prev_gamma", 1.0) for a in agents], np.float64)
+        gs = np.array([getattr(a.bidder, "gamma_sigma", 1.0) for a in agents], np.float64)
+        eng.set_agent_params(ak, bk, pg if self._shading.any() else None,
+                             gs if self._shading.any() else None)
         self._values = np.stack([np.asarray(agents2item_values[a.name], np.float64) for a in agents])
-        self._engine.load_catalog(np.stack([np.asarray(agent2items[a.name], np.float64)
-                                            for a in agents]), self._values)
+        eng.load_catalog(np.stack([np.asarray(agent2items[a.name], np.float64)
+                                   for a in agents]), self._values)
+        self._ts = False
+        if self._lrts.any():
+            lr = [a.allocator for a in agents if a.allocator.kind == _lib.ALLOCATOR_LRTS]
+            for al in lr:
+                if al.embedding_size != obs_embedding_size or al.num_items != K:
+                    raise ValueError(
+                        f"PyTorchLogisticRegressionAllocator(embedding_size={al.embedding_size}, "
+                        f"num_items={al.num_items}) must model the observed context "
+                        f"(obs_embedding_size={obs_embedding_size}) and the K={K} items")
+            ts = {bool(al.thompson_sampling) for al in lr}
+            if len(ts) != 1:
+                raise NotImplementedError("LR-TS agents must all sample or all not sample")
+            self._ts = ts.pop()
+            self._load_lrts()
         for i, a in enumerate(agents):
             a._attach(self, i)
         self._revenue_fx = 0
-        self._pending_ctx, self._pending_part, self._pending_u = [], [], []
+        self._pending = []
         self._log_batches = []
         self._log_base = 0
         self._logged_rounds = 0
         self.keep_logs = True
+        # LR-TS update bookkeeping (see _update_agent)
+        self._store = None
+        self._store_bound = 0       # upper bound of the records in the store
+        self._trained = False       # the store's samples were trained on
+        self._claimed = set()       # LR-TS agents whose update() consumed the training
+        self._cleared = set()       # ... and that cleared their logs since
+
+    def _load_lrts(self):
+        K, Do = self._engine.K, self.obs_embedding_size + 1
+        shape = (len(self.agents), K, Do)
+        m, q, pm = np.zeros(shape, np.float32), np.ones(shape, np.float32), np.zeros(shape, np.float32)
+        for i, a in enumerate(self.agents):
+            if self._lrts[i]:
+                rm = a.allocator.response_model
+                m[i], q[i], pm[i] = rm.m.numpy(), rm.q.numpy(), rm.prev_iter_m.numpy()
+        self._engine.load_lrts(m, q, pm, thompson_sampling=self._ts)
 
     # ------------------------------------------------------------------ rounds
     def _draw_round(self):
-        ctx, part, u = draw_round(self.rng, len(self.agents), self.num_participants_per_round,
-                                  self.embedding_size, self.embedding_var, self.max_slots)
-        self._pending_ctx.append(ctx)
-        self._pending_part.append(part)
-        self._pending_u.append(u)
+        N, P = len(self.agents), self.num_participants_per_round
+        if not (self._shading.any() or (self._lrts.any() and self._ts)):
+            ctx, part, u = draw_round(self.rng, N, P, self.embedding_size, self.embedding_var,
+                                      self.max_slots)
+            self._pending.append((ctx, part, u, None, None))
+            return
+        shading = [(a.bidder.prev_gamma, a.bidder.gamma_sigma) if self._shading[i] else None
+                   for i, a in enumerate(self.agents)]
+        models = [a.allocator.response_model if (self._lrts[i] and self._ts) else None
+                  for i, a in enumerate(self.agents)]
+        ctx, part, g, u, noise = draw_round_population(
+            self.rng, N, P, self.embedding_size, self.embedding_var, shading, models, self.max_slots)
+        self._pending.append((ctx, part, u, g, noise))
+
+    def _flush_limit(self):
+        return self.FLUSH_ROUNDS_TS if (self._lrts.any() and self._ts) else self.FLUSH_ROUNDS
 
     def simulate_opportunity(self):
         """One round (src/Auction.py:28-74), queued into the next batched launch."""
         self._draw_round()
-        if len(self._pending_u) >= self.FLUSH_ROUNDS:
+        if len(self._pending) >= self._flush_limit():
             self._flush()
 
     def simulate_batch(self, B):
         """B rounds with the reference's draws, run as one batch."""
         for _ in range(int(B)):
             self._draw_round()
-            if len(self._pending_u) >= self.FLUSH_ROUNDS:
+            if len(self._pending) >= self._flush_limit():
                 self._flush()
         self._flush()
 
@@ -96,18 +151,35 @@ class Auction:
         eng = self._engine
         inp = eng.alloc_inputs(int(B))
         eng.generate(seed, first_auction, inp)
+        if "gamma_raw" in inp or "ts_noise" in inp:
+            eng.generate_noise(seed, first_auction, inp)
         self._run(inp)
 
     # ------------------------------------------------------------------ engine
     def _flush(self):
-        if not self._pending_u:
+        if not self._pending:
             return
-        d = self._engine.device
-        ctx = torch.from_numpy(np.ascontiguousarray(np.array(self._pending_ctx, np.float64).T)).to(d)
-        part = torch.from_numpy(np.ascontiguousarray(np.array(self._pending_part, np.int32).T)).to(d)
-        u = torch.from_numpy(np.array(self._pending_u, np.float64)).to(d)
-        self._pending_ctx, self._pending_part, self._pending_u = [], [], []
-        self._run({"ctx": ctx, "part": part, "u": u})
+        d, P = self._engine.device, self.num_participants_per_round
+        rows, self._pending = self._pending, []
+        B = len(rows)
+        ctx = np.empty((self.embedding_size, B))
+        part = np.empty((P, B), np.int32)
+        u = np.empty(B)
+        for r, (c, p, uu, _, _) in enumerate(rows):
+            ctx[:, r], part[:, r], u[r] = c, p, uu
+        inp = {"ctx": torch.from_numpy(ctx).to(d), "part": torch.from_numpy(part).to(d),
+               "u": torch.from_numpy(u).to(d)}
+        if self._shading.any():
+            g = np.stack([row[3] for row in rows], axis=1)
+            inp["gamma_raw"] = torch.from_numpy(np.ascontiguousarray(g)).to(d)
+        if self._lrts.any() and self._ts:
+            KDo = self._engine.K * (self.obs_embedding_size + 1)
+            z = np.zeros((P, KDo, B), np.float32)
+            for r, row in enumerate(rows):
+                if row[4] is not None:
+                    z[:, :, r] = row[4]
+            inp["ts_noise"] = torch.from_numpy(z).to(d)
+        self._run(inp)
 
     def _run(self, inp):
         eng = self._engine
@@ -117,15 +189,18 @@ class Auction:
         max_b = 2048 * 8192
         for lo in range(0, B, max_b):
             hi = min(B, lo + max_b)
-            sl_in = {"ctx": inp["ctx"][:, lo:hi].contiguous(), "part": inp["part"][:, lo:hi].contiguous(),
-                     "u": inp["u"][lo:hi]}
-            sl_out = {k: (v[:, lo:hi] if v.dim() == 2 else v[lo:hi]) for k, v in out.items()}
-            if hi - lo != B:  # kernels need contiguous slices
-                sl_out = {k: torch.empty_like(v) for k, v in sl_out.items()}
+            if hi - lo == B:
+                sl_in, sl_out = inp, out
+            else:  # kernels need contiguous SoA slices
+                sl_in = {k: v[..., lo:hi].contiguous() for k, v in inp.items()}
+                sl_out = {k: torch.empty(v[..., lo:hi].shape, dtype=v.dtype, device=v.device)
+                          for k, v in out.items()}
             eng.simulate(sl_in, sl_out, cnt)
-            if hi - lo != B:
+            if self._lrts.any():
+                self._collect(sl_in, sl_out, hi - lo)
+            if sl_out is not out:
                 for k, v in out.items():
-                    (v[:, lo:hi] if v.dim() == 2 else v[lo:hi]).copy_(sl_out[k])
+                    v[..., lo:hi].copy_(sl_out[k])
         limbs = cnt.cpu().numpy()
         paid = 0
         for a, agent in enumerate(self.agents):
@@ -139,6 +214,65 @@ class Auction:
         if self.keep_logs:
             self._log_batches.append((inp["part"], out))
         self._logged_rounds += B
+
+    # ------------------------------------------------------------------ LR-TS update
+    def _collect(self, inp, out, B):
+        """Append this batch's won LR-TS samples to the device store (grown as needed)."""
+        if self._trained:
+            raise NotImplementedError(
+                "rounds were simulated after an LR-TS update before every LR-TS agent called "
+                "update() and clear_logs() (log memory across updates is not supported)")
+        eng = self._engine
+        need = self._store_bound + B
+        if self._store is None or self._store["key"].shape[0] < need:
+            cap = max(need, 2 * (self._store["key"].shape[0] if self._store else 0), 1 << 14)
+            new = eng.new_lrts_samples(cap)
+            if self._store is not None:
+                old = self._store
+                n = self._store_bound
+                new["key"][:n].copy_(old["key"][:n])
+                new["x"][:, :n].copy_(old["x"][:, :n])
+                new["count"].copy_(old["count"])
+            self._store = new
+        eng.lrts_collect(inp, out, self._store)
+        self._store_bound = need
+
+    def _update_agent(self, index, iteration):
+        """Agent.update (src/Agent.py:79-94) of agent `index` on the GPU."""
+        a = self.agents[index]
+        if self._lrts[index]:
+            self._flush()
+            if index in self._claimed:
+                raise NotImplementedError("a second update() of the same LR-TS logs")
+            if not self._trained:
+                if self._store is not None:
+                    ep = self._engine.lrts_update(self._store)
+                    m, q, pm = self._engine.lrts_state()
+                    for i, ag in enumerate(self.agents):
+                        if self._lrts[i]:
+                            rm = ag.allocator.response_model
+                            rm.m = torch.from_numpy(m[i].copy())
+                            rm.q = torch.from_numpy(q[i].copy())
+                            rm.prev_iter_m = torch.from_numpy(pm[i].copy())
+                            ag.allocator.epochs = int(ep[i])
+                self._trained = True
+            self._claimed.add(index)
+        if a.bidder.kind != _lib.BIDDER_TRUTHFUL:
+            raise NotImplementedError(
+                f"{type(a.bidder).__name__}.update (src/Bidder.py) is not on the GPU path yet")
+
+    def _cleared_logs(self, index):
+        if not self._lrts[index]:
+            return
+        if index in self._claimed:
+            self._cleared.add(index)
+        if self._trained and len(self._cleared) == int(self._lrts.sum()):
+            # every LR-TS agent consumed its update and dropped its logs: empty the store
+            if self._store is not None:
+                self._store["count"].zero_()
+            self._store_bound = 0
+            self._trained = False
+            self._claimed, self._cleared = set(), set()
 
     # ------------------------------------------------------------------ logs
     def _log_rounds(self):

@@ -1,9 +1,12 @@
-"""Bidder plugins: the surface of src/Bidder.py:15-35 (+ the learned bidders' names).
+"""Bidder plugins: the surface of src/Bidder.py:15-35 (+ the shading bidders).
 
 Bidders are descriptors here: `kind` selects the bid rule the fused kernel applies per
-participant. TruthfulBidder (bid = value * estimated CTR, src/Bidder.py:34-35) is built;
-the shading / learning bidders keep their constructors so configs parse, and the engine
-refuses them with NotImplementedError until their kernels land (f).
+participant. TruthfulBidder (bid = value * estimated CTR, src/Bidder.py:34-35) is
+complete. The shading bidders bid on the GPU in their uninitialised state -- gamma ~
+N(prev_gamma, gamma_sigma), clipped to [0, 1] for EmpiricalShadedBidder (src/Bidder.py:
+47-58), unclipped with its Gaussian propensity for the learning bidders (:174-179,
+:351-356, :458-463) -- which is every bid of their first iteration; their update()
+is not built yet (Agent.update raises NotImplementedError).
 """
 from . import _lib
 
@@ -38,7 +41,7 @@ class TruthfulBidder(Bidder):
         return value * estimated_CTR
 
 
-class _NotYetBuilt(Bidder):
+class _ShadingBidder(Bidder):
     kind = None
 
     def __init__(self, rng, gamma_sigma, init_gamma=1.0, **kw):
@@ -49,24 +52,32 @@ class _NotYetBuilt(Bidder):
         self.gammas = []
 
 
-class EmpiricalShadedBidder(_NotYetBuilt):
-    """src/Bidder.py:38-153 (not yet on the GPU path)."""
+class EmpiricalShadedBidder(_ShadingBidder):
+    """src/Bidder.py:38-153."""
+
+    kind = _lib.BIDDER_EMPIRICAL_SHADED
 
 
-class ValueLearningBidder(_NotYetBuilt):
-    """src/Bidder.py:156-333 (not yet on the GPU path)."""
+class ValueLearningBidder(_ShadingBidder):
+    """src/Bidder.py:156-333 (uninitialised state)."""
+
+    kind = _lib.BIDDER_VALUE_LEARNING
 
     def __init__(self, rng, gamma_sigma, init_gamma=1.0, inference="search"):
         assert inference in ["search", "policy"]
         super().__init__(rng, gamma_sigma, init_gamma, inference=inference)
 
 
-class PolicyLearningBidder(_NotYetBuilt):
-    """src/Bidder.py:336-439 (not yet on the GPU path)."""
+class PolicyLearningBidder(_ShadingBidder):
+    """src/Bidder.py:336-439 (uninitialised state)."""
+
+    kind = _lib.BIDDER_POLICY_LEARNING
 
     def __init__(self, rng, gamma_sigma, loss, init_gamma=1.0):
         super().__init__(rng, gamma_sigma, init_gamma, loss=loss)
 
 
-class DoublyRobustBidder(_NotYetBuilt):
-    """src/Bidder.py:442-623 (not yet on the GPU path)."""
+class DoublyRobustBidder(_ShadingBidder):
+    """src/Bidder.py:442-623 (uninitialised state)."""
+
+    kind = _lib.BIDDER_DOUBLY_ROBUST

@@ -2,9 +2,13 @@
 
 OracleAllocator's estimate_CTR (sigmoid(items @ ctx), src/BidderAllocation.py:81-82) runs
 inside the fused simulate kernel with the reference's exact FP64 arithmetic.
-PyTorchLogisticRegressionAllocator keeps its constructor so configs parse; the engine
-refuses it with NotImplementedError until the LR-TS kernels land.
+PyTorchLogisticRegressionAllocator's Thompson-sampling forward (src/Models.py:28-33) runs
+there too, and its update (src/BidderAllocation.py:29-65) is the GPU training kernel of
+ag_lrts_update, batched over every LR-TS agent of the auction (Agent.update). The model
+tensors here are host mirrors of the device posterior, refreshed after each update.
 """
+import torch
+
 from . import _lib
 
 
@@ -33,14 +37,30 @@ class OracleAllocator(Allocator):
         self.item_embeddings = item_embeddings
 
 
-class PyTorchLogisticRegressionAllocator(Allocator):
-    """Bayesian logistic regression with Thompson sampling (src/BidderAllocation.py:21-68);
-    not yet on the GPU path."""
+class PyTorchLogisticRegression:
+    """Parameters of src/Models.py:18-26: m [K][n_dim+1] ~ N(0, 1) (drawn from torch's global
+    generator exactly as the reference's constructor does), prev_iter_m = m, q = 1."""
 
-    kind = None
+    def __init__(self, n_dim, n_items):
+        self.m = torch.empty(n_items, n_dim + 1)
+        torch.nn.init.normal_(self.m, mean=0.0, std=1.0)
+        self.prev_iter_m = self.m.detach().clone()
+        self.q = torch.ones((n_items, n_dim + 1))
+
+    def sample_noise(self):
+        """The Thompson-sampling draw of src/Models.py:31 (same torch call, same stream)."""
+        return torch.normal(mean=0.0, std=1.0 / torch.sqrt(self.q))
+
+
+class PyTorchLogisticRegressionAllocator(Allocator):
+    """Bayesian logistic regression with Thompson sampling (src/BidderAllocation.py:21-68)."""
+
+    kind = _lib.ALLOCATOR_LRTS
 
     def __init__(self, rng, embedding_size, num_items, thompson_sampling=True):
-        super().__init__(rng)
+        self.response_model = PyTorchLogisticRegression(n_dim=embedding_size, n_items=num_items)
+        self.thompson_sampling = thompson_sampling
         self.embedding_size = embedding_size
         self.num_items = num_items
-        self.thompson_sampling = thompson_sampling
+        self.epochs = None  # epochs run by the last update (None: not updated yet)
+        super().__init__(rng)

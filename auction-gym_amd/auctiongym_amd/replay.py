@@ -9,6 +9,12 @@ leaves the Generator in the same state as the reference after every round
 (tests/golden/make_golden.py asserts that on every captured round), so a batch of
 rounds can be drawn up front and resolved on the GPU.
 
+Populations with shading bidders or Thompson-sampling allocators draw more per round, in
+slot order after the participants (src/Agent.py:44-53): a shading bidder in its
+uninitialised state draws rng.normal(prev_gamma, gamma_sigma) (src/Bidder.py:51, 177, 354,
+461); an LR-TS allocator draws torch.normal(0, 1/sqrt(q)) from torch's own global
+generator (src/Models.py:31). draw_round_population makes the same calls in the same order.
+
 (The one exception: numpy's binomial draws nothing when p == 0.0 exactly, i.e. when a
 winner's sigmoid underflows to 0, which needs items . ctx < -745.)
 """
@@ -35,3 +41,28 @@ def draw_rounds(rng, B, num_agents, num_participants, embedding_size, embedding_
         part[:, r] = p
         u[r] = uu
     return ctx, part, u
+
+
+def draw_round_population(rng, num_agents, num_participants, embedding_size, embedding_var,
+                          shading, ts_models, max_slots=1):
+    """One round of a general population. shading[a] = (prev_gamma, gamma_sigma) of a shading
+    bidder in its uninitialised state (else None); ts_models[a] = the LR-TS model whose
+    Thompson draw the round makes (else None). Returns ctx [E], part [P], gamma_raw [P]
+    (NaN where nothing is drawn), u, ts_noise [P][K*Do] float32 or None."""
+    rng.integers(1, max_slots + 1)
+    ctx = rng.normal(0, embedding_var, size=embedding_size)
+    part = rng.choice(num_agents, num_participants, replace=False)
+    gamma_raw = np.full(num_participants, np.nan)
+    noise = None
+    for s, a in enumerate(part):
+        m = ts_models[a]
+        if m is not None:
+            z = m.sample_noise().numpy().ravel()
+            if noise is None:
+                noise = np.zeros((num_participants, z.size), np.float32)
+            noise[s] = z
+        sh = shading[a]
+        if sh is not None:
+            gamma_raw[s] = rng.normal(sh[0], sh[1])
+    u = rng.random()
+    return ctx, part, gamma_raw, u, noise

@@ -210,9 +210,10 @@ __global__ __launch_bounds__(kLrThreads) void k_lrts_train(
     const double *__restrict__ adam_tab, int32_t *__restrict__ epochs_out, float *__restrict__ loss_trace) {
   const int a = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (akind[a] != AG_ALLOCATOR_LRTS) return;
   const int64_t s0 = offsets[a], n = offsets[a + 1] - s0;
-  if (n < 2) {  // src/BidderAllocation.py:33-34: nothing changes, not even prev_m
+  // not an LR-TS agent, or < 2 samples (src/BidderAllocation.py:33-34): nothing changes,
+  // not even prev_m
+  if (akind[a] != AG_ALLOCATOR_LRTS || n < 2) {
     if (tid == 0) epochs_out[a] = 0;
     return;
   }

@@ -620,3 +620,69 @@ def test_lrts_update_at_scale(gpu, oracle):
                                                  m0[a], m0[a], q0[a])
         assert ep[a] == oep and np.array_equal(m[a], om) and np.array_equal(q[a], oq)
     eng.close()
+
+
+SP_TRUTHFUL_TS = {  # config/SP_Truthful_TS.json as shipped
+    "random_seed": 0, "num_runs": 3, "num_iter": 20, "rounds_per_iter": 10000,
+    "num_participants_per_round": 2, "embedding_size": 5, "embedding_var": 1.0,
+    "obs_embedding_size": 4, "allocation": "SecondPrice",
+    "agents": [{"name": "Truthful Learnt", "num_copies": 6, "num_items": 12,
+                "allocator": {"type": "PyTorchLogisticRegressionAllocator",
+                              "kwargs": {"embedding_size": 4, "num_items": 12}},
+                "bidder": {"type": "TruthfulBidder", "kwargs": {}}}],
+    "output_dir": "results/SP_Truthful_TS/"}
+
+
+def test_driver_sp_truthful_ts_iteration(gpu, oracle, tmp_path):
+    """SP_Truthful_TS.json through the drop-in classes with torch seeded as the capture was:
+    the same LR-TS initial models (torch.nn.init.normal_), the same Thompson draws
+    (torch.normal in slot order), the reference's rounds (capture sp_ts_r2048: winners and
+    items exact, utilities within float32 CTR tolerance); then Agent.update trains all six
+    LR-TS agents on the GPU (== the oracle on the reference's own update samples); the next
+    iteration samples with the updated posterior."""
+    import torch
+
+    import auctiongym_amd.main as M
+    d, meta, agg = load_capture("sp_ts_r2048")
+    kat = np.load(os.path.join(GOLDEN, "sp_ts_update_kat.npz"))
+    p = tmp_path / "SP_Truthful_TS.json"
+    p.write_text(json.dumps(SP_TRUTHFUL_TS))
+    rng, config, agent_configs, a2i, a2v, _, max_slots, E, var, OE = M.parse_config(str(p))
+    torch.manual_seed(meta["torch_seed"])
+    agents = M.instantiate_agents(rng, agent_configs, a2v, a2i)
+    for i, a in enumerate(agents):
+        assert np.array_equal(a.allocator.response_model.m.numpy(), d["ts_m"][i])
+    auction, _, _, _ = M.instantiate_auction(rng, config, a2i, a2v, agents, max_slots, E, var, OE)
+    for _ in range(meta["rounds"]):
+        auction.simulate_opportunity()
+    rt = dict(rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose([a.net_utility for a in agents], agg["net_utility"], **rt)
+    np.testing.assert_allclose([a.gross_utility for a in agents], agg["gross_utility"], **rt)
+    np.testing.assert_allclose(auction.revenue, agg["revenue"], **rt)
+    assert [a.num_logs() for a in agents] == list(agg["n_logs"])
+    items = [[o.item for o in a.logs] for a in agents]
+    for i in range(6):
+        rows, slots = np.nonzero(d["part"] == i)
+        assert items[i] == list(d["item"][rows, slots])
+    for a in agents:
+        a.update(iteration=0)
+        a.clear_utility()
+        a.clear_logs()
+    auction.clear_revenue()
+    for i, a in enumerate(agents):
+        k = lambda n: kat[f"a{i}_{n}"]  # noqa: E731
+        om, opm, oq, oep, _ = oracle.lrts_update(k("X"), k("A"), k("y"), k("m0"), k("prevm0"), k("q0"))
+        rm = a.allocator.response_model
+        assert a.allocator.epochs == oep
+        assert np.array_equal(rm.m.numpy(), om) and np.array_equal(rm.q.numpy(), oq)
+        assert np.array_equal(rm.prev_iter_m.numpy(), opm)
+        np.testing.assert_allclose(rm.m.numpy(), k("m1"), atol=2e-2)
+    # iteration 1: Thompson draws now use the updated q (std = 1/sqrt(q))
+    auction.simulate_batch(1024)
+    assert sum(a.num_logs() for a in agents) == 2 * 1024
+    assert auction.revenue > 0
+    for a in agents:
+        a.update(iteration=1)
+        a.clear_utility()
+        a.clear_logs()
+    assert all(a.allocator.epochs > 0 for a in agents)

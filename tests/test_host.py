@@ -103,9 +103,13 @@ def test_plugin_factory_semantics(tmp_path):
     assert mech.code == 1
 
 
-def test_unbuilt_plugins_are_refused_not_faked(tmp_path):
-    """Learned bidders parse but the GPU path refuses them (no silent CPU path)."""
+def test_plugins_parse_and_no_cpu_fallback(tmp_path):
+    """Learning plugins parse with the reference's kwargs and carry their kernel kinds;
+    without a GPU the auction refuses to run (no silent CPU path)."""
+    import torch
+
     import auctiongym_amd.main as M
+    from auctiongym_amd import _lib
     from auctiongym_amd.Auction import Auction
     from auctiongym_amd.AuctionAllocation import FirstPrice
     cfg = {"random_seed": 0, "num_runs": 1, "num_iter": 1, "rounds_per_iter": 10,
@@ -119,9 +123,19 @@ def test_unbuilt_plugins_are_refused_not_faked(tmp_path):
     p = tmp_path / "c.json"
     p.write_text(json.dumps(cfg))
     rng, config, ac, a2i, a2v, _, ms, E, var, OE = M.parse_config(str(p))
+    torch.manual_seed(0)
     agents = M.instantiate_agents(rng, ac, a2v, a2i)
-    with pytest.raises(NotImplementedError):
-        Auction(rng, FirstPrice(), agents, a2i, a2v, ms, E, var, OE, 2)
+    assert all(a.allocator.kind == _lib.ALLOCATOR_LRTS for a in agents)
+    assert all(a.bidder.kind == _lib.BIDDER_DOUBLY_ROBUST for a in agents)
+    # the LR-TS model draws m from torch's global generator as src/Models.py:21-22 does
+    torch.manual_seed(0)
+    ref = torch.empty(12, 5)
+    torch.nn.init.normal_(ref, mean=0.0, std=1.0)
+    assert torch.equal(agents[0].allocator.response_model.m, ref)
+    assert torch.equal(agents[0].allocator.response_model.prev_iter_m, ref)
+    if not torch.cuda.is_available():
+        with pytest.raises(RuntimeError, match="no CPU fallback"):
+            Auction(rng, FirstPrice(), agents, a2i, a2v, ms, E, var, OE, 2)
 
 
 def test_graft_entry_build_is_idempotent():
