@@ -95,11 +95,14 @@ class Auction:
         self._log_base = 0
         self._logged_rounds = 0
         self.keep_logs = True
-        # LR-TS update bookkeeping (see _update_agent)
-        self._store = None
-        self._store_bound = 0       # upper bound of the records in the store
-        self._trained = False       # the store's samples were trained on
-        self._claimed = set()       # LR-TS agents whose update() consumed the training
+        # Agent.update bookkeeping (see _update_agent)
+        self._empirical = bk == _lib.BIDDER_EMPIRICAL_SHADED
+        self._learner = self._lrts | self._empirical
+        self._stores = {}                       # device record stores, by learner family
+        self._bounds = {"lrts": 0, "shading": 0}  # upper bounds of the records they hold
+        self._trained = False       # the stores' records were trained on
+        self._pending_state = {}    # trained state not yet applied to the host mirrors
+        self._claimed = set()       # learners whose update() consumed the training
         self._cleared = set()       # ... and that cleared their logs since
 
     def _load_lrts(self):
@@ -196,7 +199,7 @@ class Auction:
                 sl_out = {k: torch.empty(v[..., lo:hi].shape, dtype=v.dtype, device=v.device)
                           for k, v in out.items()}
             eng.simulate(sl_in, sl_out, cnt)
-            if self._lrts.any():
+            if self._learner.any():
                 self._collect(sl_in, sl_out, hi - lo)
             if sl_out is not out:
                 for k, v in out.items():
@@ -215,62 +218,103 @@ class Auction:
             self._log_batches.append((inp["part"], out))
         self._logged_rounds += B
 
-    # ------------------------------------------------------------------ LR-TS update
+    # ------------------------------------------------------------------ Agent.update
+    # Learners (LR-TS allocators, EmpiricalShadedBidder) update from their logs of the
+    # iteration. Their records are collected on the device after every batch; the first
+    # learner's update() trains every learner at once (agents' updates are independent:
+    # same results as the reference's per-agent loop, src/main.py:127-152); the stores are
+    # emptied once every learner has called update() and clear_logs().
+    _CAP_KEY = {"lrts": "key", "shading": "agent"}
+
+    def _grow(self, name, need, make):
+        """The `name` store with room for `need` records (grown by copying)."""
+        old = self._stores.get(name)
+        cap = old[self._CAP_KEY[name]].shape[0] if old is not None else 0
+        if cap >= need:
+            return old
+        st = make(max(need, 2 * cap, 1 << 14))
+        if old is not None:
+            n = self._bounds[name]
+            for k, v in old.items():
+                if k == "count":
+                    st[k].copy_(v)
+                else:
+                    st[k][..., :n].copy_(v[..., :n])
+        self._stores[name] = st
+        return st
+
     def _collect(self, inp, out, B):
-        """Append this batch's won LR-TS samples to the device store (grown as needed)."""
         if self._trained:
             raise NotImplementedError(
-                "rounds were simulated after an LR-TS update before every LR-TS agent called "
+                "rounds were simulated after an update before every learning agent called "
                 "update() and clear_logs() (log memory across updates is not supported)")
         eng = self._engine
-        need = self._store_bound + B
-        if self._store is None or self._store["key"].shape[0] < need:
-            cap = max(need, 2 * (self._store["key"].shape[0] if self._store else 0), 1 << 14)
-            new = eng.new_lrts_samples(cap)
-            if self._store is not None:
-                old = self._store
-                n = self._store_bound
-                new["key"][:n].copy_(old["key"][:n])
-                new["x"][:, :n].copy_(old["x"][:, :n])
-                new["count"].copy_(old["count"])
-            self._store = new
-        eng.lrts_collect(inp, out, self._store)
-        self._store_bound = need
+        if self._lrts.any():
+            need = self._bounds["lrts"] + B
+            st = self._grow("lrts", need, eng.new_lrts_samples)
+            eng.lrts_collect(inp, out, st)
+            self._bounds["lrts"] = need
+        if self._empirical.any():
+            need = self._bounds["shading"] + B * self.num_participants_per_round
+            st = self._grow("shading", need, eng.new_shading_samples)
+            eng.shading_collect(inp, out, st)
+            self._bounds["shading"] = need
+
+    def _train_all(self):
+        """One launch per learner family; each agent's new host-side state is applied when
+        that agent's own update() runs (the device state is only read by the next batch,
+        which the reference also runs after every update)."""
+        eng = self._engine
+        self._pending_state = {}
+        if self._lrts.any() and "lrts" in self._stores:
+            ep = eng.lrts_update(self._stores["lrts"])
+            m, q, pm = eng.lrts_state()
+            for i in np.nonzero(self._lrts)[0]:
+                self._pending_state.setdefault(int(i), {})["lrts"] = (m[i].copy(), q[i].copy(),
+                                                                      pm[i].copy(), int(ep[i]))
+        if self._empirical.any():
+            st = self._stores.get("shading") or eng.new_shading_samples(1)
+            pg = eng.empirical_update(st)
+            for i in np.nonzero(self._empirical)[0]:
+                self._pending_state.setdefault(int(i), {})["prev_gamma"] = float(pg[i])
+
+    def _apply_state(self, index):
+        ag = self.agents[index]
+        state = self._pending_state.pop(index, {})
+        if "lrts" in state:
+            m, q, pm, ep = state["lrts"]
+            rm = ag.allocator.response_model
+            rm.m, rm.q, rm.prev_iter_m = torch.from_numpy(m), torch.from_numpy(q), torch.from_numpy(pm)
+            ag.allocator.epochs = ep
+        if "prev_gamma" in state:
+            ag.bidder.prev_gamma = state["prev_gamma"]
 
     def _update_agent(self, index, iteration):
         """Agent.update (src/Agent.py:79-94) of agent `index` on the GPU."""
         a = self.agents[index]
-        if self._lrts[index]:
-            self._flush()
-            if index in self._claimed:
-                raise NotImplementedError("a second update() of the same LR-TS logs")
-            if not self._trained:
-                if self._store is not None:
-                    ep = self._engine.lrts_update(self._store)
-                    m, q, pm = self._engine.lrts_state()
-                    for i, ag in enumerate(self.agents):
-                        if self._lrts[i]:
-                            rm = ag.allocator.response_model
-                            rm.m = torch.from_numpy(m[i].copy())
-                            rm.q = torch.from_numpy(q[i].copy())
-                            rm.prev_iter_m = torch.from_numpy(pm[i].copy())
-                            ag.allocator.epochs = int(ep[i])
-                self._trained = True
-            self._claimed.add(index)
-        if a.bidder.kind != _lib.BIDDER_TRUTHFUL:
+        if a.bidder.kind not in (_lib.BIDDER_TRUTHFUL, _lib.BIDDER_EMPIRICAL_SHADED):
             raise NotImplementedError(
                 f"{type(a.bidder).__name__}.update (src/Bidder.py) is not on the GPU path yet")
+        if not self._learner[index]:
+            return
+        self._flush()
+        if index in self._claimed:
+            raise NotImplementedError("a second update() of the same logs")
+        if not self._trained:
+            self._train_all()
+            self._trained = True
+        self._apply_state(index)
+        self._claimed.add(index)
 
     def _cleared_logs(self, index):
-        if not self._lrts[index]:
+        if not self._learner[index]:
             return
         if index in self._claimed:
             self._cleared.add(index)
-        if self._trained and len(self._cleared) == int(self._lrts.sum()):
-            # every LR-TS agent consumed its update and dropped its logs: empty the store
-            if self._store is not None:
-                self._store["count"].zero_()
-            self._store_bound = 0
+        if self._trained and len(self._cleared) == int(self._learner.sum()):
+            for st in self._stores.values():
+                st["count"].zero_()
+            self._bounds = {"lrts": 0, "shading": 0}
             self._trained = False
             self._claimed, self._cleared = set(), set()
 

@@ -28,8 +28,9 @@ FX_FRAC_BITS, FX_LIMB_BITS, FX_LIMBS = 36, 42, 3
 EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params", "ag_load_lrts",
            "ag_set_option", "ag_load_catalog", "ag_allocate", "ag_simulate", "ag_generate",
            "ag_generate_noise", "ag_lrts_collect", "ag_lrts_update", "ag_lrts_read",
+           "ag_shading_collect", "ag_empirical_update",
            "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_last_error", "ag_abi_version")
-ABI_VERSION = 3
+ABI_VERSION = 4
 LRTS_MAX_EPOCHS = 16384
 LRTS_MAX_DO = 8
 
@@ -58,6 +59,11 @@ class AgBatchOut(ctypes.Structure):
 class AgLrtsSamples(ctypes.Structure):
     _fields_ = [("key", ctypes.c_void_p), ("x", ctypes.c_void_p), ("capacity", ctypes.c_int64),
                 ("count", ctypes.c_void_p)]
+
+
+class AgShadingSamples(ctypes.Structure):
+    _fields_ = [("agent", ctypes.c_void_p), ("gamma", ctypes.c_void_p), ("utility", ctypes.c_void_p),
+                ("capacity", ctypes.c_int64), ("count", ctypes.c_void_p)]
 
 
 class AgError(RuntimeError):
@@ -92,6 +98,9 @@ def load(path=None):
                                            ctypes.POINTER(AgBatchOut), ctypes.POINTER(AgLrtsSamples), vp]),
         "ag_lrts_update": (ctypes.c_int, [vp, ctypes.POINTER(AgLrtsSamples), vp, vp, vp]),
         "ag_lrts_read": (ctypes.c_int, [vp, vp, vp, vp]),
+        "ag_shading_collect": (ctypes.c_int, [vp, i64, ctypes.POINTER(AgBatchIn),
+                                              ctypes.POINTER(AgBatchOut), ctypes.POINTER(AgShadingSamples), vp]),
+        "ag_empirical_update": (ctypes.c_int, [vp, ctypes.POINTER(AgShadingSamples), vp, vp]),
         "ag_generate_noise": (ctypes.c_int, [vp, u64, u64, i64, vp, vp, vp, vp]),
         "ag_allocate": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, vp]),
         "ag_simulate": (ctypes.c_int, [vp, i64, ctypes.POINTER(AgBatchIn),

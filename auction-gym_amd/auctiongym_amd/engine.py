@@ -10,7 +10,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import AgBatchIn, AgBatchOut, AgLrtsSamples, AgShape
+from ._lib import AgBatchIn, AgBatchOut, AgLrtsSamples, AgShadingSamples, AgShape
 from ._lib import check as _check
 
 COUNTERS = _lib.COUNTERS
@@ -235,6 +235,39 @@ class AuctionEngine:
         self._check(self.L.ag_allocate(self._h, _ptr(bids), B, _ptr(w), _ptr(p), _ptr(s), _stream()),
               "ag_allocate")
         return w, p, s
+
+    # ---------------------------------------------------------------- shading update
+    def new_shading_samples(self, capacity):
+        """Device store of shading-bidder records (ag_shading_samples)."""
+        d = self.device
+        return {"agent": torch.empty((capacity,), dtype=torch.int32, device=d),
+                "gamma": torch.empty((capacity,), dtype=torch.float64, device=d),
+                "utility": torch.empty((capacity,), dtype=torch.float64, device=d),
+                "count": torch.zeros((1,), dtype=torch.int64, device=d)}
+
+    @staticmethod
+    def _shading(st):
+        return AgShadingSamples(_ptr(st["agent"]).value, _ptr(st["gamma"]).value,
+                                _ptr(st["utility"]).value, st["agent"].shape[0], _ptr(st["count"]).value)
+
+    def shading_collect(self, inputs, outputs, store):
+        """Append the shading-bidder records of a simulated batch (ag_shading_collect)."""
+        B = inputs["u"].shape[0]
+        bi = AgBatchIn(_ptr(inputs["ctx"]).value, _ptr(inputs["part"]).value, _ptr(inputs["u"]).value,
+                       _ptr(inputs.get("gamma_raw")).value, _ptr(inputs.get("ts_noise")).value)
+        bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
+        st = self._shading(store)
+        self._check(self.L.ag_shading_collect(self._h, B, ctypes.byref(bi), ctypes.byref(bo),
+                                              ctypes.byref(st), _stream()), "ag_shading_collect")
+
+    def empirical_update(self, store):
+        """EmpiricalShadedBidder.update of every such agent (ag_empirical_update); returns the
+        prev_gamma of all agents [N] after the update."""
+        pg = np.zeros(self.N, np.float64)
+        st = self._shading(store)
+        self._check(self.L.ag_empirical_update(self._h, ctypes.byref(st), pg.ctypes.data, _stream()),
+                    "ag_empirical_update")
+        return pg
 
     # ---------------------------------------------------------------- counters
     @staticmethod

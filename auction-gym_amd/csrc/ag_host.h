@@ -48,6 +48,7 @@ struct ag_ctx {
   double *d_pg = nullptr, *d_gs = nullptr;
   float *d_tsm = nullptr, *d_tsq = nullptr, *d_tsprev = nullptr;  // LR-TS m, q, prev_iter_m
   ag_lrts_ws lrts;
+  int32_t *d_status = nullptr;  // [N] per-agent update status (ag_empirical_update)
 };
 
 // Frees the LR-TS training workspace (ag_lrts.hip).

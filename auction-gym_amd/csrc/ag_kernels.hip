@@ -406,6 +406,7 @@ int ag_destroy(ag_ctx *c) {
   (void)hipFree(c->d_tsq);
   (void)hipFree(c->d_tsprev);
   ag_lrts_release(c);
+  (void)hipFree(c->d_status);
   delete[] c->h_akind;
   delete c;
   return AG_OK;

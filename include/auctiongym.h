@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define AG_ABI_VERSION 3
+#define AG_ABI_VERSION 4
 
 typedef enum ag_status {
   AG_OK = 0,
@@ -226,6 +226,32 @@ int ag_lrts_update(ag_ctx *ctx, const ag_lrts_samples *samples, int32_t *epochs,
 
 /* Current LR-TS posterior, host float32 [N][K][OE+1] (any may be NULL). Synchronises. */
 int ag_lrts_read(ag_ctx *ctx, float *m, float *q, float *prev_m);
+
+/* ---- Shading bidders' update (Agent.update -> EmpiricalShadedBidder.update,
+ * src/Agent.py:79-94, src/Bidder.py:60-147) ------------------------------------------
+ * Every participation of a shading bidder (its `gammas` and the net utilities the update
+ * derives from the logs, src/Bidder.py:62-63) accumulates in a caller-owned store;
+ * reset *count where the reference calls Agent.clear_logs. Records are unordered. */
+typedef struct ag_shading_samples {
+  int32_t *agent;    /* dev [capacity]                                                   */
+  double *gamma;     /* dev [capacity]: the shading factor of the bid                    */
+  double *utility;   /* dev [capacity]: value * outcome - price if won, else 0           */
+  int64_t capacity;
+  uint64_t *count;   /* dev [1]: records appended; > capacity = overflow (update fails)  */
+} ag_shading_samples;
+
+/* Append the shading-bidder records of one simulated batch (needs in.part, out.winner,
+ * out.item, out.outcome, out.price, out.gamma). Hot call: stream-ordered. */
+int ag_shading_collect(ag_ctx *ctx, int64_t B, const ag_batch_in *in, const ag_batch_out *out,
+                       const ag_shading_samples *samples, void *stream);
+
+/* EmpiricalShadedBidder.update of every such agent from the store: the new prev_gamma is
+ * written where ag_simulate reads it and, when prev_gamma (host [N]) is not NULL, copied
+ * out (other agents' entries unchanged). Synchronises `stream`. AG_ERR_INVALID with the
+ * reference's numpy message where the reference raises (no samples, one bucket, no bucket
+ * with two samples). Arithmetic: oracle/ag_oracle.c ora_empirical_update. */
+int ag_empirical_update(ag_ctx *ctx, const ag_shading_samples *samples, double *prev_gamma,
+                        void *stream);
 
 /* Exact counters (host int64 [n][AG_FX_LIMBS], e.g. copied back or all-reduced)
  * -> doubles (host [n]), correctly rounded from the exact fixed-point sum. */

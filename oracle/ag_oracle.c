@@ -527,3 +527,99 @@ int32_t ora_lrts_update(int64_t n, int32_t K, int32_t Do, const float *X, const 
   free(G);
   return epoch;
 }
+
+/* ---------------------------------------------------------------------------------------
+ * EmpiricalShadedBidder.update (src/Bidder.py:60-147): bucketise the iteration's shading
+ * factors on a 0.005 grid, lower confidence bound of the mean net utility per bucket,
+ * move prev_gamma to the best bucket's midpoint.
+ *  - num_buckets = int((max - min) // 0.005) + 1 with Python's float floor division,
+ *    edges = numpy.linspace(min, max, num_buckets): i * step + min, last = max;
+ *  - bucket j holds edge_j <= gamma < edge_{j+1} (the maximum itself falls in none);
+ *  - buckets with > 1 sample: mean = S / n, stderr = sqrt(S2 / n) / sqrt(n) with S, S2
+ *    exact fixed-point sums (2^-40 grid) of u and (u - mean)^2; U = mean - 1.96 stderr;
+ *  - best = the LAST bucket with the largest U (the reference's reversed nanargmax);
+ *    prev_gamma = clip(midpoint (hi - lo) / 2 + lo, 0, 1).
+ * numpy sums pairwise in float64: means agree to ~1e-16 relative, so the chosen bucket
+ * (and prev_gamma, computed from the same edges) is identical unless two buckets' bounds
+ * tie within that (tests/test_oracle_golden.py: every case of empirical_update_kat.npz).
+ * Returns 0, or the reference's exception: -1 empty logs (np.min of an empty array),
+ * -2 no bucket (argmax of an empty sequence), -3 all buckets NaN (All-NaN slice).
+ * ------------------------------------------------------------------------------------- */
+static double py_floordiv(double vx, double wx) { /* CPython float floor division */
+  double mod = fmod(vx, wx);
+  double div = (vx - mod) / wx;
+  if (mod != 0.0) {
+    if ((wx < 0) != (mod < 0)) div -= 1.0;
+  }
+  double fd;
+  if (div != 0.0) {
+    fd = floor(div);
+    if (div - fd > 0.5) fd += 1.0;
+  } else {
+    fd = copysign(0.0, vx / wx);
+  }
+  return fd;
+}
+
+int32_t ora_empirical_update(int64_t n, const double *gamma, const double *util, double *prev_gamma) {
+  if (n < 1) return -1;
+  double lo_g = gamma[0], hi_g = gamma[0];
+  for (int64_t i = 1; i < n; ++i) {
+    if (gamma[i] < lo_g) lo_g = gamma[i];
+    if (gamma[i] > hi_g) hi_g = gamma[i];
+  }
+  const int64_t nb = (int64_t)py_floordiv(hi_g - lo_g, 0.005) + 1;
+  if (nb < 2) return -2;
+  const double step = (hi_g - lo_g) / (double)(nb - 1);
+  double *edge = malloc(nb * sizeof(double));
+  for (int64_t j = 0; j < nb - 1; ++j) edge[j] = (double)j * step + lo_g;
+  edge[nb - 1] = hi_g;
+  const int64_t M = nb - 1;
+  int64_t *cnt = calloc(M, sizeof(int64_t));
+  __int128 *S = calloc(M, sizeof(__int128)), *S2 = calloc(M, sizeof(__int128));
+  int64_t *bk = malloc(n * sizeof(int64_t));
+  for (int64_t i = 0; i < n; ++i) {
+    int64_t j = -1;
+    for (int64_t b = 0; b < M; ++b)
+      if (edge[b] <= gamma[i] && gamma[i] < edge[b + 1]) { j = b; break; }
+    bk[i] = j;
+    if (j >= 0) {
+      cnt[j] += 1;
+      S[j] += fx_round(util[i], 0x1p40);
+    }
+  }
+  double *mean = malloc(M * sizeof(double));
+  for (int64_t b = 0; b < M; ++b) mean[b] = cnt[b] > 1 ? fx_read(S[b], 0x1p-40) / (double)cnt[b] : 0.0;
+  for (int64_t i = 0; i < n; ++i)
+    if (bk[i] >= 0 && cnt[bk[i]] > 1) {
+      double d = util[i] - mean[bk[i]];
+      S2[bk[i]] += fx_round(d * d, 0x1p40);
+    }
+  int64_t best = -1;
+  double bestU = 0.0;
+  for (int64_t b = 0; b < M; ++b) {
+    if (cnt[b] <= 1) continue;
+    double se = sqrt(fx_read(S2[b], 0x1p-40) / (double)cnt[b]) / sqrt((double)cnt[b]);
+    double U = mean[b] - 1.96 * se;
+    if (best < 0 || U >= bestU) {
+      best = b;
+      bestU = U;
+    }
+  }
+  int32_t rc = 0;
+  if (best < 0) {
+    rc = -3;
+  } else {
+    double g = (edge[best + 1] - edge[best]) / 2.0 + edge[best];
+    if (g < 0) g = 0;
+    if (g > 1.0) g = 1.0;
+    *prev_gamma = g;
+  }
+  free(edge);
+  free(cnt);
+  free(S);
+  free(S2);
+  free(bk);
+  free(mean);
+  return rc;
+}

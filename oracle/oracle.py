@@ -83,6 +83,8 @@ def lib():
         L.ora_philox4x32_10.argtypes = [vp, vp, vp]
         L.ora_lrts_loss_grad.restype = ctypes.c_float
         L.ora_lrts_loss_grad.argtypes = [i64, i32, i32, vp, vp, vp, vp, vp, vp, vp]
+        L.ora_empirical_update.restype = i32
+        L.ora_empirical_update.argtypes = [i64, vp, vp, vp]
         L.ora_lrts_update.restype = i32
         L.ora_lrts_update.argtypes = [i64, i32, i32, vp, vp, vp, vp, vp, vp, vp]
         _lib = L
@@ -236,3 +238,20 @@ def lrts_loss_grad(X, A, y, m, prev_m, q):
     loss = lib().ora_lrts_loss_grad(len(y), m.shape[0], m.shape[1], _p(X), _p(A), _p(y), _p(m),
                                     _p(pm), _p(q), _p(g))
     return float(loss), g
+
+
+EMPIRICAL_ERRORS = {-1: "zero-size array to reduction operation minimum which has no identity",
+                    -2: "attempt to get argmax of an empty sequence",
+                    -3: "All-NaN slice encountered"}
+
+
+def empirical_update(gammas, utilities):
+    """EmpiricalShadedBidder.update (src/Bidder.py:60-147) -> new prev_gamma; raises
+    ValueError where the reference does."""
+    g = np.ascontiguousarray(gammas, np.float64)
+    u = np.ascontiguousarray(utilities, np.float64)
+    out = np.zeros(1)
+    rc = lib().ora_empirical_update(len(g), _p(g), _p(u), _p(out))
+    if rc:
+        raise ValueError(EMPIRICAL_ERRORS[rc])
+    return float(out[0])

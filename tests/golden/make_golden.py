@@ -408,11 +408,64 @@ def full_run_aggregates(cfg_name, runs=None, iters=None, rounds=None):
     return {"config": cfg, "iterations": res}
 
 
+EMPIRICAL_CASES = (  # (gamma_sigma, init_gamma, P, allocation, seed, rounds)
+    (0.05, 0.9, 2, "FirstPrice", 15, 2048),
+    (0.2, 0.6, 3, "FirstPrice", 16, 4096),
+    (0.5, 1.0, 2, "SecondPrice", 17, 4096),
+)
+
+
+def empirical_update_kat(out_name="empirical_update_kat", iters=3):
+    """EmpiricalShadedBidder.update (src/Bidder.py:60-147) through the reference's own driver
+    loop (src/main.py:113-155): per case and iteration, every agent's inputs to the update
+    (gammas, and the utilities it computes from the logs) and prev_gamma before / after."""
+    import main as M
+    out = {}
+    for ci, (sigma, init, P, alloc, seed, rounds) in enumerate(EMPIRICAL_CASES):
+        cfg = oracle_truthful_cfg(6, 12, P, alloc, seed=seed)
+        cfg["agents"][0]["bidder"] = {"type": "EmpiricalShadedBidder",
+                                      "kwargs": {"gamma_sigma": sigma, "init_gamma": init}}
+        cfg["rounds_per_iter"], cfg["num_iter"] = rounds, iters
+        out[f"c{ci}_cfg"] = np.array(json.dumps(cfg))
+        path = write_cfg(cfg)
+        (rng, config, agent_configs, a2i, a2v, _, max_slots, E, var, OE) = M.parse_config(path)
+        os.unlink(path)
+        agents = M.instantiate_agents(rng, agent_configs, a2v, a2i)
+        auction, _, _, _ = M.instantiate_auction(rng, config, a2i, a2v, agents, max_slots, E, var, OE)
+        for it in range(iters):
+            for _ in range(rounds):
+                auction.simulate_opportunity()
+            out[f"c{ci}_it{it}_revenue"] = np.array(auction.revenue)
+            out[f"c{ci}_it{it}_net"] = np.array([a.net_utility for a in agents])
+            for i, a in enumerate(agents):
+                won = np.array([o.won for o in a.logs])
+                util = np.zeros(len(a.logs))
+                vals = np.array([o.value for o in a.logs])
+                outc = np.array([o.outcome for o in a.logs])
+                pr = np.array([o.price for o in a.logs])
+                util[won] = vals[won] * outc[won] - pr[won]
+                k = f"c{ci}_it{it}_a{i}"
+                out[k + "_gammas"] = np.array(a.bidder.gammas, np.float64)
+                out[k + "_util"] = util
+                out[k + "_pg0"] = np.array(float(a.bidder.prev_gamma))
+                a.update(iteration=it)
+                out[k + "_pg1"] = np.array(float(a.bidder.prev_gamma))
+                a.clear_utility()
+                a.clear_logs()
+            auction.clear_revenue()
+            print("empirical", ci, it, [float(out[f"c{ci}_it{it}_a{i}_pg1"]) for i in range(6)], flush=True)
+    np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also run SP_Oracle as shipped (3x20x10k rounds, ~1 min)")
+    ap.add_argument("--only", choices=["empirical"], help="regenerate one fixture family only")
     args = ap.parse_args()
     install_shims()
+    if args.only == "empirical":
+        empirical_update_kat()
+        return
 
     sigmoid_kats()
     alloc_kats()
@@ -449,6 +502,8 @@ def main():
                                   "kwargs": {"gamma_sigma": 0.05, "init_gamma": 0.9}}
     a, g, m = capture(cfg, 2048)
     save_capture("fp_empirical_r2048", a, g, m)
+    # 9. EmpiricalShadedBidder.update over three iterations of three populations.
+    empirical_update_kat()
 
     if args.full:
         agg = full_run_aggregates("SP_Oracle.json")

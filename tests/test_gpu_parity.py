@@ -686,3 +686,83 @@ def test_driver_sp_truthful_ts_iteration(gpu, oracle, tmp_path):
         a.clear_utility()
         a.clear_logs()
     assert all(a.allocator.epochs > 0 for a in agents)
+
+
+# ---- EmpiricalShadedBidder.update (src/Bidder.py:60-147) ----
+def _empirical_engine(N=6):
+    from auctiongym_amd.engine import AuctionEngine
+    eng = AuctionEngine(N, 2, 12, 5, 4, 0, 1.0)
+    eng.set_agent_params(np.zeros(N, np.int32), np.ones(N, np.int32), np.full(N, 0.9), np.full(N, 0.05))
+    g = np.random.default_rng(0)
+    eng.load_catalog(g.normal(size=(N, 12, 6)), g.random((N, 12)))
+    return eng
+
+
+def _fill_shading(eng, per_agent, seed=0):
+    import torch
+    ag = np.concatenate([np.full(len(gm), a, np.int32) for a, (gm, _) in per_agent.items()])
+    gm = np.concatenate([np.asarray(gm, np.float64) for gm, _ in per_agent.values()])
+    ut = np.concatenate([np.asarray(u, np.float64) for _, u in per_agent.values()])
+    perm = np.random.default_rng(seed).permutation(len(ag))
+    st = eng.new_shading_samples(max(len(ag), 1))
+    if len(ag):
+        st["agent"][:len(ag)] = torch.from_numpy(ag[perm]).to(eng.device)
+        st["gamma"][:len(ag)] = torch.from_numpy(gm[perm]).to(eng.device)
+        st["utility"][:len(ag)] = torch.from_numpy(ut[perm]).to(eng.device)
+    st["count"][0] = len(ag)
+    return st
+
+
+def test_empirical_update_matches_oracle_and_reference(gpu, oracle):
+    """Every (population, iteration) of empirical_update_kat.npz: the six agents' updates in
+    one launch == the oracle == the reference's prev_gamma, bit for bit."""
+    k = np.load(os.path.join(GOLDEN, "empirical_update_kat.npz"))
+    eng = _empirical_engine()
+    for ci in range(3):
+        for it in range(3):
+            per = {a: (k[f"c{ci}_it{it}_a{a}_gammas"], k[f"c{ci}_it{it}_a{a}_util"]) for a in range(6)}
+            pg = eng.empirical_update(_fill_shading(eng, per, seed=ci * 3 + it))
+            for a in range(6):
+                want = float(k[f"c{ci}_it{it}_a{a}_pg1"])
+                assert pg[a] == want == oracle.empirical_update(*per[a]), (ci, it, a)
+    eng.close()
+
+
+def test_empirical_update_errors(gpu):
+    eng = _empirical_engine(N=2)
+    g = np.random.default_rng(1)
+    ok = (0.5 + 0.05 * g.standard_normal(500), g.normal(0, 0.1, 500))
+    with pytest.raises(ValueError, match="All-NaN"):
+        eng.empirical_update(_fill_shading(eng, {0: ok, 1: ([0.1, 0.2, 0.3], [0.0, 1.0, 0.0])}))
+    with pytest.raises(ValueError, match="empty sequence"):
+        eng.empirical_update(_fill_shading(eng, {0: ok, 1: ([0.5, 0.501], [0.1, 0.2])}))
+    with pytest.raises(ValueError, match="zero-size"):
+        eng.empirical_update(_fill_shading(eng, {0: ok}))
+    eng.close()
+
+
+@pytest.mark.parametrize("case", range(3))
+def test_driver_empirical_three_iterations(gpu, tmp_path, case):
+    """The reference's driver loop on an EmpiricalShadedBidder population for three
+    iterations through the drop-in classes: each iteration's revenue and net utilities, and
+    every agent's prev_gamma after each GPU update, equal the reference's."""
+    import auctiongym_amd.main as M
+    k = np.load(os.path.join(GOLDEN, "empirical_update_kat.npz"))
+    cfg = json.loads(str(k[f"c{case}_cfg"]))
+    p = tmp_path / "c.json"
+    p.write_text(json.dumps(cfg))
+    rng, config, agent_configs, a2i, a2v, _, max_slots, E, var, OE = M.parse_config(str(p))
+    agents = M.instantiate_agents(rng, agent_configs, a2v, a2i)
+    auction, num_iter, rounds, _ = M.instantiate_auction(rng, config, a2i, a2v, agents, max_slots, E, var, OE)
+    for it in range(num_iter):
+        auction.simulate_batch(rounds)
+        np.testing.assert_allclose(auction.revenue, float(k[f"c{case}_it{it}_revenue"]), rtol=1e-9)
+        # reference: sequential float64 sums; here exact sums (north star: 1e-5 relative)
+        np.testing.assert_allclose([a.net_utility for a in agents], k[f"c{case}_it{it}_net"], rtol=1e-9)
+        for i, a in enumerate(agents):
+            assert a.bidder.prev_gamma == float(k[f"c{case}_it{it}_a{i}_pg0"])
+            a.update(iteration=it)
+            assert a.bidder.prev_gamma == float(k[f"c{case}_it{it}_a{i}_pg1"]), (it, i)
+            a.clear_utility()
+            a.clear_logs()
+        auction.clear_revenue()

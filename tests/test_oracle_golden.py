@@ -266,3 +266,27 @@ def test_lrts_update_needs_two_samples(oracle):
     m1, pm1, q1, ep, L = oracle.lrts_update(g.normal(0, 1, (1, 5)), [2], [1], m, pm, q)
     assert ep == 0 and len(L) == 0
     assert np.array_equal(m1, m) and np.array_equal(pm1, pm) and np.array_equal(q1, q)
+
+
+# ---- EmpiricalShadedBidder.update (src/Bidder.py:60-147) ----
+def test_empirical_update_matches_reference(oracle):
+    """Three populations x three iterations x six agents of the reference's own driver loop:
+    the new prev_gamma equals the reference's, bit for bit."""
+    k = np.load(os.path.join(GOLDEN, "empirical_update_kat.npz"))
+    n = 0
+    for ci in range(3):
+        for it in range(3):
+            for a in range(6):
+                p = f"c{ci}_it{it}_a{a}"
+                assert oracle.empirical_update(k[p + "_gammas"], k[p + "_util"]) == float(k[p + "_pg1"]), p
+                n += 1
+    assert n == 54
+
+
+def test_empirical_update_errors_like_reference(oracle):
+    with pytest.raises(ValueError, match="zero-size"):
+        oracle.empirical_update([], [])
+    with pytest.raises(ValueError, match="empty sequence"):     # all gammas within one grid step
+        oracle.empirical_update([0.5, 0.501, 0.502], [0.1, 0.2, 0.3])
+    with pytest.raises(ValueError, match="All-NaN"):            # no bucket holds 2 samples
+        oracle.empirical_update([0.1, 0.2, 0.3], [0.0, 1.0, 0.0])
