@@ -55,12 +55,12 @@ def algorithmic_bytes_per_auction(E, P, first_price):
     return reads + writes
 
 
-def catalogue():
+def catalogue(cfg=None):
     import tempfile
 
     import auctiongym_amd.main as M
     with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
-        json.dump(SP_ORACLE, f)
+        json.dump(cfg or SP_ORACLE, f)
     try:
         rng, config, agent_configs, a2i, a2v, *_ = M.parse_config(f.name)
     finally:
@@ -85,6 +85,107 @@ def cpu_baseline(items, values, inp, sample, threads):
     return sample / dt, dt, o
 
 
+SP_TS = dict(SP_ORACLE, agents=[{"name": "Truthful TS", "num_copies": 8, "num_items": 12,
+                                  "allocator": {"type": "PyTorchLogisticRegressionAllocator",
+                                                "kwargs": {"embedding_size": 4, "num_items": 12}},
+                                  "bidder": {"type": "TruthfulBidder", "kwargs": {}}}],
+             output_dir="results/SP_Truthful_TS/")
+
+
+def algorithmic_bytes_ts(E, P, K, Do):
+    """SP_Truthful_TS replay: the Thompson noise of both participants is read from HBM."""
+    return algorithmic_bytes_per_auction(E, P, first_price=False) + P * K * Do * 4
+
+
+def timed_steps(step, steps, warmup, world, stream):
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    for _ in range(warmup):
+        step(None)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(ev[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=stream.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    return elapsed, kern_ms
+
+
+def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True):
+    """configs[1]: SP_Truthful_TS, 8 LR-TS truthful bidders, 1M auctions per GPU, SecondPrice.
+    Inputs (contexts, participants, uniforms AND the Thompson noise z / sqrt(q) of both
+    participants) generated on the GPU and resident in HBM; initial models as
+    src/Models.py:21-24 (m ~ N(0,1) from torch seeded 0, q = 1). One step = ag_simulate.
+    Then one Agent.update of all 8 agents on the last batch's won samples (collect + the
+    GPU training loop), timed separately (the reference: 14.3 s per 10k-round iteration)."""
+    from auctiongym_amd import _lib
+    from auctiongym_amd.engine import AuctionEngine
+    from auctiongym_amd.sharding import allreduce_counters, shard_range
+    items, values = catalogue(SP_TS)
+    N, K, D = items.shape
+    E, P, OE = D - 1, SP_TS["num_participants_per_round"], SP_TS["obs_embedding_size"]
+    Do = OE + 1
+    dev = torch.device("cuda", local)
+    eng = AuctionEngine(N, P, K, E, OE, _lib.SECOND_PRICE, SP_TS["embedding_var"], device=local)
+    eng.set_agent_params(np.ones(N, np.int32), np.zeros(N, np.int32))
+    eng.load_catalog(items, values)
+    g = torch.Generator().manual_seed(0)
+    m = torch.empty(N, K, Do)
+    for a in range(N):
+        m[a].normal_(0.0, 1.0, generator=g)
+    eng.load_lrts(m.numpy(), np.ones((N, K, Do), np.float32), thompson_sampling=True)
+    inp = eng.alloc_inputs(B)
+    lo, hi = shard_range(B * world, rank, world)
+    eng.generate(0, lo, inp)
+    eng.generate_noise(0, lo, inp)
+    out = eng.alloc_outputs(B)
+    cnt = eng.new_counters()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+
+    def step(ev):
+        cnt.zero_()
+        if ev is not None:
+            ev[0].record(stream)
+        eng.simulate(inp, out, cnt)
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:
+            allreduce_counters(cnt)
+
+    elapsed, kern_ms = timed_steps(step, steps, warmup, world, stream)
+    bpa = algorithmic_bytes_ts(E, P, K, Do)
+    res = {"workload": "SP_Truthful_TS (configs[1]): 8 LR-TS Thompson-sampling truthful bidders, "
+                       "K=12, E=5, OE=4, P=2, SecondPrice",
+           "value": B * world * steps / elapsed, "unit": "auctions/s", "ms_per_step": elapsed / steps * 1e3,
+           "auctions_per_gpu_per_step": B, "kernel_ms": kern_ms, "algorithmic_bytes_per_auction": bpa,
+           "roofline": {"bound": "hbm", "achieved": bpa * B / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": bpa * B / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}}
+    if with_update:
+        st = eng.new_lrts_samples(B)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.lrts_collect(inp, out, st)
+        ep = eng.lrts_update(st)  # synchronises
+        torch.cuda.synchronize()
+        res["agent_update"] = {"ms": (time.perf_counter() - t0) * 1e3, "won_samples": int(st["count"][0]),
+                               "epochs": [int(e) for e in ep],
+                               "what": "Agent.update of all 8 LR-TS agents (ag_lrts_collect + "
+                                       "ag_lrts_update: Adam, ReduceLROnPlateau, early stop, Laplace q)"}
+    eng.close()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -94,6 +195,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 23)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu_count)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ts-batch", type=int, default=1 << 20, help="SP_Truthful_TS auctions per GPU per step")
+    ap.add_argument("--no-ts", action="store_true", help="skip the SP_Truthful_TS (configs[1]) line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -200,6 +303,10 @@ def main():
                      "kernel": "ag_simulate (k_simulate + k_reduce_counters)",
                      "kernel_ms": kern_ms, "algorithmic_bytes_per_auction": bpa},
     }
+
+    if not args.no_ts:
+        result["configs_1"] = run_sp_ts(args.ts_batch, args.steps, args.warmup, world, rank, local,
+                                        with_update=(world == 1))
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
