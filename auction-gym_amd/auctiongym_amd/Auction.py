@@ -177,11 +177,11 @@ class Auction:
             inp["gamma_raw"] = torch.from_numpy(np.ascontiguousarray(g)).to(d)
         if self._lrts.any() and self._ts:
             KDo = self._engine.K * (self.obs_embedding_size + 1)
-            z = np.zeros((P, KDo, B), np.float32)
+            z = np.zeros((B, P, KDo), np.float32)
             for r, row in enumerate(rows):
                 if row[4] is not None:
-                    z[:, :, r] = row[4]
-            inp["ts_noise"] = torch.from_numpy(z).to(d)
+                    z[r] = row[4]
+            inp["ts_noise"] = torch.from_numpy(AuctionEngine.tile_ts_noise(z)).to(d)
         self._run(inp)
 
     def _run(self, inp):
@@ -195,7 +195,8 @@ class Auction:
             if hi - lo == B:
                 sl_in, sl_out = inp, out
             else:  # kernels need contiguous SoA slices
-                sl_in = {k: v[..., lo:hi].contiguous() for k, v in inp.items()}
+                sl_in = {k: (v[..., lo:hi].contiguous() if k != "ts_noise"
+                             else v[:, lo // 64:(hi + 63) // 64].contiguous()) for k, v in inp.items()}
                 sl_out = {k: torch.empty(v[..., lo:hi].shape, dtype=v.dtype, device=v.device)
                           for k, v in out.items()}
             eng.simulate(sl_in, sl_out, cnt)

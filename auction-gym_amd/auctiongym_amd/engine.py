@@ -159,6 +159,11 @@ class AuctionEngine:
         B is even; lower occupancy, slower under sustained load). Same results either way."""
         self._check(self.L.ag_set_option(self._h, _lib.OPT_LANE_AUCTIONS, int(n)), "ag_set_option")
 
+    def set_launch_auctions(self, n):
+        """Cap on auctions per k_simulate launch (0: the resident grid's exact-counter
+        capacity); larger batches run as consecutive launches, same results."""
+        self._check(self.L.ag_set_option(self._h, _lib.OPT_LAUNCH_AUCTIONS, int(n)), "ag_set_option")
+
     def load_catalog(self, items, values):
         items = np.ascontiguousarray(items, np.float64)
         values = np.ascontiguousarray(values, np.float64)
@@ -177,9 +182,28 @@ class AuctionEngine:
         if getattr(self, "shading", False):
             inp["gamma_raw"] = torch.empty((self.P, B), dtype=torch.float64, device=d)
         if getattr(self, "lrts", False) and getattr(self, "ts_sample", True):
-            inp["ts_noise"] = torch.empty((self.P, self.K * (self.OE + 1), B), dtype=torch.float32,
-                                          device=d)
+            inp["ts_noise"] = torch.empty((self.P, (B + 63) // 64, self.K * (self.OE + 1), 64),
+                                          dtype=torch.float32, device=d)
         return inp
+
+    @staticmethod
+    def tile_ts_noise(noise):
+        """Thompson noise per (auction, slot) [B][P][K*Do] (or [B][P][K][Do]) -> the kernel's
+        64-auction tiles [P][T][K*Do][64] (include/auctiongym.h ag_batch_in.ts_noise)."""
+        z = np.asarray(noise, np.float32)
+        B, P = z.shape[:2]
+        z = z.reshape(B, P, -1)
+        T = (B + 63) // 64
+        pad = np.zeros((T * 64, P, z.shape[2]), np.float32)
+        pad[:B] = z
+        return np.ascontiguousarray(pad.reshape(T, 64, P, -1).transpose(2, 0, 3, 1))
+
+    @staticmethod
+    def untile_ts_noise(tiles, B):
+        """Inverse of tile_ts_noise: [P][T][K*Do][64] -> [B][P][K*Do]."""
+        t = tiles.detach().cpu().numpy() if torch.is_tensor(tiles) else np.asarray(tiles)
+        P, T, KDo, _ = t.shape
+        return np.ascontiguousarray(t.transpose(1, 3, 0, 2).reshape(T * 64, P, KDo)[:B])
 
     def alloc_outputs(self, B, fields=None):
         if fields is None:

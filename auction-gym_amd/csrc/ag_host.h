@@ -38,6 +38,7 @@ struct ag_ctx {
   int64_t *d_partials = nullptr;
   int32_t partial_blocks = 0;
   int32_t resident[16] = {};  // resident blocks [general][W][screened][counters]
+  int64_t launch_cap = 0;  // AG_OPT_LAUNCH_AUCTIONS
   bool wide = false;  // 1 auction per lane by default: higher occupancy, faster when sustained
   bool catalog = false;
   // general populations (anything beyond OracleAllocator + TruthfulBidder)

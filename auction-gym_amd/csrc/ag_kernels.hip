@@ -248,6 +248,7 @@ __global__ __launch_bounds__(kThreads) void k_generate_noise(uint64_t seed, uint
                                                             const float *q, double *gamma_raw,
                                                             float *ts_noise) {
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  const int64_t T = (B + 63) >> 6;  // 64-auction tiles of ts_noise
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < B;
        i += (int64_t)gridDim.x * kThreads) {
     const uint64_t idx = first + (uint64_t)i;
@@ -275,9 +276,9 @@ __global__ __launch_bounds__(kThreads) void k_generate_noise(uint64_t seed, uint
             z0 = z1 = 0.0;
           }
           const float *qa = q + (size_t)a * KDo;
-          ts_noise[((int64_t)s * KDo + j) * B + i] = lr ? (float)z0 * (1.0f / sqrtf(qa[j])) : 0.0f;
-          if (j + 1 < KDo)
-            ts_noise[((int64_t)s * KDo + j + 1) * B + i] = lr ? (float)z1 * (1.0f / sqrtf(qa[j + 1])) : 0.0f;
+          float *row = ts_noise + (((int64_t)s * T + (i >> 6)) * KDo + j) * 64 + (i & 63);
+          row[0] = lr ? (float)z0 * (1.0f / sqrtf(qa[j])) : 0.0f;
+          if (j + 1 < KDo) row[64] = lr ? (float)z1 * (1.0f / sqrtf(qa[j + 1])) : 0.0f;
         }
       }
     }
@@ -363,7 +364,7 @@ int ag_create(int32_t device, const ag_shape *s, ag_ctx **out) {
   hipError_t e = hipMalloc(&c->d_items, sizeof(double) * s->num_agents * s->num_items * D);
   if (e == hipSuccess) e = hipMalloc(&c->d_values, sizeof(double) * s->num_agents * s->num_items);
   // partials for the largest grid a call can use: grids grow past kMinGrid only to keep
-  // <= kMaxAuctionsPerBlock auctions per block; allocate lazily beyond the default.
+  // <= kAuctionsPerReplica * replicas auctions per block; allocate lazily beyond the default.
   c->partial_blocks = kMaxSimGrid;
   if (e == hipSuccess) e = hipMalloc(&c->d_partials, sizeof(int64_t) * 2 * (size_t)kMaxSimGrid * nc);
   const size_t nkd = (size_t)s->num_agents * s->num_items * (s->obs_embedding_size + 1);
@@ -496,6 +497,10 @@ int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
         return ag_set_error(AG_ERR_INVALID, "ag_set_option: lane auctions must be 1 or 2");
       c->wide = value == 2;
       return AG_OK;
+    case AG_OPT_LAUNCH_AUCTIONS:
+      if (value < 0) return ag_set_error(AG_ERR_INVALID, "ag_set_option: launch auctions must be >= 0");
+      c->launch_cap = value;
+      return AG_OK;
     default:
       return ag_set_error(AG_ERR_INVALID, "ag_set_option: unknown option %d", option);
   }
@@ -600,17 +605,26 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
     if (res < 1) res = 1;
     if (res > c->partial_blocks) res = c->partial_blocks;
   }
-  const int64_t tiles = (B + kThreads * W - 1) / (kThreads * W);
-  const int grid = (int)(tiles < res ? tiles : res);
-  if (B > (int64_t)grid * kMaxAuctionsPerBlock)
-    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: B=%lld > %lld auctions per call; split the batch",
-                     (long long)B, (long long)grid * kMaxAuctionsPerBlock);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), lds, st, prm);
-  AG_HIP(hipGetLastError());
-  if (counters_fx) {
-    hipLaunchKernelGGL(k_reduce_counters, dim3(nc), dim3(kThreads), 0, st, c->d_partials, grid, nc,
-                       counters_fx);
+  // Batches larger than one launch's exact-counter capacity (resident blocks x
+  // kAuctionsPerReplica x replicas) run as consecutive launches over auction ranges.
+  const int64_t per_block = (int64_t)kAuctionsPerReplica * prm.lds.replicas;
+  int64_t chunk_max = (int64_t)res * per_block;
+  if (c->launch_cap > 0 && c->launch_cap < chunk_max) chunk_max = c->launch_cap;
+  chunk_max &= ~(int64_t)1;
+  if (chunk_max < 2) chunk_max = 2;
+  for (int64_t lo = 0; lo < B; lo += chunk_max) {
+    const int64_t hi = lo + chunk_max < B ? lo + chunk_max : B;
+    const int64_t tiles = (hi - lo + kThreads * W - 1) / (kThreads * W);
+    const int grid = (int)(tiles < res ? tiles : res);
+    prm.lo = (int32_t)lo;
+    prm.hi = (int32_t)hi;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), lds, st, prm);
     AG_HIP(hipGetLastError());
+    if (counters_fx) {
+      hipLaunchKernelGGL(k_reduce_counters, dim3(nc), dim3(kThreads), 0, st, c->d_partials, grid, nc,
+                         counters_fx);
+      AG_HIP(hipGetLastError());
+    }
   }
   return AG_OK;
 }

@@ -12,9 +12,24 @@
 
 namespace ag {
 
+// Build knobs (A/B variants, `make variant`): AG_PREFETCH software-pipelines the next
+// tile's input loads; AG_MIN_WAVES caps VGPRs via launch bounds; AG_MAX_REPLICAS caps the
+// per-lane counter replicas (LDS per block).
+#ifndef AG_PREFETCH
+#define AG_PREFETCH 0
+#endif
+#ifndef AG_MIN_WAVES
+#define AG_MIN_WAVES 1
+#endif
+#ifndef AG_MAX_REPLICAS
+#define AG_MAX_REPLICAS 16
+#endif
+
 constexpr int kThreads = 256;              // 4 waves of 64 lanes
 constexpr int kC = AG_NUM_COUNTERS;
-constexpr int kMaxAuctionsPerBlock = 65536; // per launch: keeps a replica's int64 sum exact
+// Auctions one block may resolve per launch: 1024 per counter replica keeps every replica's
+// int64 sum exact (<= 1024 * P terms of magnitude < 2^50, to_fx).
+constexpr int kAuctionsPerReplica = 1024;
 constexpr int kMinGrid = 2048;             // 256 CUs x 8
 constexpr int kMaxSimGrid = 2048;          // partial-sum workspace (>= resident blocks)
 constexpr int kMaxP = 8;                   // per-lane slot registers (template range)
@@ -110,7 +125,7 @@ __host__ inline LdsLayout make_layout(int N, int K, int D, bool counters, bool g
   L.scr_val_stride = L.kpairs * 2 + 2;
   L.ncnt = general ? kGeneralSlots : kOracleSlots;
   L.ts_do = general ? ts_do : 0;
-  int R = 64;
+  int R = AG_MAX_REPLICAS;
   while (R > 1 && (int64_t)R * N * L.ncnt * 8 > 32768) R >>= 1;
   L.replicas = R;
   int64_t b = 0;
@@ -143,7 +158,8 @@ __host__ inline LdsLayout make_layout(int N, int K, int D, bool counters, bool g
 }
 
 struct SimParams {
-  int32_t B;              // auctions in this launch (< 2^28: 32-bit SoA indexing)
+  int32_t B;              // auctions in the batch = SoA leading dimension (B * P < 2^31)
+  int32_t lo, hi;         // the auctions [lo, hi) this launch resolves
   int32_t N, K, mech;
   int32_t want_counters;
   int32_t ts_sample;      // general: LR-TS agents add ts_noise to m for the item choice
@@ -344,6 +360,57 @@ __device__ __forceinline__ float ts_ctr(const float *w, const float *x, int Do, 
   return 1.0f / (1.0f + e);
 }
 
+// ts_ctr over a compile-time register width DW >= Do (the runtime model width): the terms
+// d >= Do are skipped, so the float32 sum is the same sequence of roundings as ts_ctr's.
+// nzv: the coefficients' noise, already in registers (noisy = false: the MAP CTR).
+template <int DW>
+__device__ __forceinline__ float ts_ctr_k(const float *w, const float (&x)[DW], const float (&nzv)[DW],
+                                          bool noisy, int Do, const uint64_t *tab) {
+  float z = 0.0f;
+#pragma unroll
+  for (int d = 0; d < DW; ++d) {
+    if (d < Do) {
+      const float wd = noisy ? w[d] + nzv[d] : w[d];
+      const float t = wd * x[d];
+      z = d == 0 ? t : z + t;
+    }
+  }
+  const float e = (float)agexp::exp(-(double)z, tab);
+  return 1.0f / (1.0f + e);
+}
+
+// Thompson-sampling item choice of an LR-TS agent (src/Agent.py:29-42): first argmax of
+// sampled CTR * value. The noise of kTsGroup items is loaded together (one memory latency
+// per group instead of one per item), then the group is scored.
+constexpr int kTsGroup = 4;
+template <int DW>
+__device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], const float *nz, int K, int Do,
+                                         const double *vals, const uint64_t *tab) {
+  double best_sc = 0.0;
+  int best = 0;
+  for (int k0 = 0; k0 < K; k0 += kTsGroup) {
+    float nzv[kTsGroup][DW];
+#pragma unroll
+    for (int g = 0; g < kTsGroup; ++g)
+#pragma unroll
+      for (int d = 0; d < DW; ++d)
+        nzv[g][d] = (nz && k0 + g < K && d < Do) ? nz[(size_t)((k0 + g) * Do + d) * 64] : 0.0f;
+#pragma unroll
+    for (int g = 0; g < kTsGroup; ++g) {
+      const int k = k0 + g;
+      if (k < K) {
+        const float ck = ts_ctr_k<DW>(m + k * Do, xo, nzv[g], nz != nullptr, Do, tab);
+        const double sc = (double)ck * vals[k];
+        if (k == 0 || sc > best_sc) {
+          best_sc = sc;
+          best = k;
+        }
+      }
+    }
+  }
+  return best;
+}
+
 // Gaussian density of a shading factor (src/Bidder.py:178, :355, :462).
 __device__ __forceinline__ double shading_propensity(double pg, double sigma, double g,
                                                      const uint64_t *tab) {
@@ -378,22 +445,17 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
         // item by first argmax of CTR * value (float32 CTR widened to double), the MAP CTR
         // of that item is the estimate
         const int Do = T.ts_do;
-        float xo[kMaxD];
-        for (int d = 0; d < Do - 1; ++d) xo[d] = (float)x[d];
-        xo[Do - 1] = 1.0f;
         const float *m = T.tsm + (size_t)a * K * Do;
-        const float *nz = (ts_sample && in.ts_noise) ? in.ts_noise + (size_t)s * K * Do * B + i : nullptr;
-        double best_sc = 0.0;
-        best = 0;
-        for (int k = 0; k < K; ++k) {
-          const float ck = ts_ctr(m + k * Do, xo, Do, nz ? nz + (size_t)k * Do * B : nullptr, B, T.tab);
-          const double sc = (double)ck * T.vals[a * T.values_stride + k];
-          if (k == 0 || sc > best_sc) {
-            best_sc = sc;
-            best = k;
-          }
-        }
-        est = (double)ts_ctr(m + best * Do, xo, Do, nullptr, 0, T.tab);
+        // tiled noise: coefficient c of auction i at ((s*T + i/64)*K*Do + c)*64 + i%64
+        const float *nz = (ts_sample && in.ts_noise)
+                              ? in.ts_noise + ((size_t)(s * ((B + 63) >> 6) + (i >> 6)) * K * Do) * 64 + (i & 63)
+                              : nullptr;
+        // observed context (src/Auction.py:36) in a register row of width D >= Do
+        float xo[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) xo[d] = d < Do - 1 ? (float)x[d] : (d == Do - 1 ? 1.0f : 0.0f);
+        best = ts_select<D>(m, xo, nz, K, Do, T.vals + a * T.values_stride, T.tab);
+        est = (double)ts_ctr_k<D>(m + best * Do, xo, xo, false, Do, T.tab);
         tru = best == best_t ? c : agexp::sigmoid(dot_ref<D>(itm + best * D, x), T.tab);
       }
     }
@@ -442,10 +504,11 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
 }
 
 template <int P, int D, bool PRUNE, int W, bool GENERAL>
-__global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
+__global__ __launch_bounds__(kThreads, AG_MIN_WAVES) void k_simulate(SimParams prm) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = prm.N, K = prm.K;
-  const uint32_t B = (uint32_t)prm.B;
+  const uint32_t B = (uint32_t)prm.B;  // SoA leading dimension (auctions in the batch)
+  const uint32_t lo = (uint32_t)prm.lo, hi = (uint32_t)prm.hi;  // this launch's auctions
   const LdsLayout L = prm.lds;
   uint64_t *s_tab = reinterpret_cast<uint64_t *>(smem + L.tab);
   double *s_items = reinterpret_cast<double *>(smem + L.items);
@@ -510,18 +573,50 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
   const ag_batch_out out = prm.out;
   const bool charged = P >= 2;  // P == 1: empty price arrays, nobody charged (Auction.py:68)
 
-  for (uint32_t base = blockIdx.x * (kThreads * W); base < B; base += gridDim.x * (kThreads * W)) {
-    const uint32_t i = base + tid * W;  // W consecutive auctions (B % W == 0)
-    if (i >= B) continue;
-
-    double xv[kMaxD][W];
-    int pv[P][W];
-    double uv[W];
+  // inputs of one tile: the context, participants and uniform of W consecutive auctions
+  double xv[kMaxD][W];
+  int pv[P][W];
+  double uv[W];
+  auto load_tile = [&](uint32_t i) {
 #pragma unroll
     for (int e = 0; e < D - 1; ++e) ld_f64<W>(in.ctx + e * B + i, xv[e]);
 #pragma unroll
     for (int s = 0; s < P; ++s) ld_i32<W>(in.part + s * B + i, pv[s]);
     ld_f64<W>(in.u + i, uv);
+  };
+  const uint32_t stride = gridDim.x * (kThreads * W);
+#if AG_PREFETCH
+  // software pipelining: the next tile's loads are in flight while this tile computes
+  double xn[kMaxD][W];
+  int pn[P][W];
+  double un[W];
+  if (lo + blockIdx.x * (kThreads * W) + tid * W < hi) load_tile(lo + blockIdx.x * (kThreads * W) + tid * W);
+#endif
+  for (uint32_t base = lo + blockIdx.x * (kThreads * W); base < hi; base += stride) {
+    const uint32_t i = base + tid * W;  // W consecutive auctions (even chunk bounds when W = 2)
+#if AG_PREFETCH
+    if (i >= hi) continue;
+#pragma unroll
+    for (int e = 0; e < D - 1; ++e)
+#pragma unroll
+      for (int q = 0; q < W; ++q) xn[e][q] = xv[e][q];
+#pragma unroll
+    for (int s = 0; s < P; ++s)
+#pragma unroll
+      for (int q = 0; q < W; ++q) pn[s][q] = pv[s][q];
+#pragma unroll
+    for (int q = 0; q < W; ++q) un[q] = uv[q];
+    if (i + stride < hi) load_tile(i + stride);
+#define XV xn
+#define PV pn
+#define UV un
+#else
+    if (i >= hi) continue;
+    load_tile(i);
+#define XV xv
+#define PV pv
+#define UV uv
+#endif
 
     Resolved<P> r[W];
 #pragma unroll
@@ -531,7 +626,7 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
       float xabs = 1.0f;
 #pragma unroll
       for (int e = 0; e < D - 1; ++e) {
-        x[e] = xv[e][q];
+        x[e] = XV[e][q];
         xf[e] = (float)x[e];
         xabs += fabsf(xf[e]);
       }
@@ -540,8 +635,8 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
       xabs *= 1.001f;
       int ag[P];
 #pragma unroll
-      for (int s = 0; s < P; ++s) ag[s] = pv[s][q];
-      resolve<P, D, PRUNE, GENERAL>(T, K, prm.mech, x, xf, xabs, ag, uv[q], in, B, i + q,
+      for (int s = 0; s < P; ++s) ag[s] = PV[s][q];
+      resolve<P, D, PRUNE, GENERAL>(T, K, prm.mech, x, xf, xabs, ag, UV[q], in, B, i + q,
                                     prm.ts_sample != 0, r[q]);
     }
 
@@ -625,6 +720,9 @@ __global__ __launch_bounds__(kThreads) void k_simulate(SimParams prm) {
     }
   }
 
+#undef XV
+#undef PV
+#undef UV
   if (prm.want_counters) {
     __syncthreads();
     for (int a = tid; a < N; a += kThreads) {

@@ -189,8 +189,9 @@ def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=60,
+                    help="untimed steps first (lets the clocks settle under sustained load)")
     ap.add_argument("--batch", type=int, default=1 << 24, help="auctions per GPU per step")
     ap.add_argument("--cpu-sample", type=int, default=1 << 23)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu_count)")

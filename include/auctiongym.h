@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define AG_ABI_VERSION 4
+#define AG_ABI_VERSION 6
 
 typedef enum ag_status {
   AG_OK = 0,
@@ -107,8 +107,12 @@ typedef struct ag_batch_in {
   const double *u;     /* [B]    uniform in [0,1) consumed by binomial(1, CTR[winner])   */
   const double *gamma_raw; /* [P][B] raw rng.normal(prev_gamma, gamma_sigma) draw of a
                               shading bidder (src/Bidder.py:51,177,354,461); NULL if none */
-  const float *ts_noise;   /* [P][K*(OE+1)][B] torch.normal(0, 1/sqrt(q)) of an LR-TS
-                              participant (src/Models.py:31); NULL if none / no sampling */
+  const float *ts_noise;   /* [P][T][K*(OE+1)][64], T = ceil(B/64): torch.normal(0,
+                              1/sqrt(q)) of an LR-TS participant (src/Models.py:31) in tiles
+                              of 64 auctions -- element (slot s, auction i, coefficient c)
+                              at ((s*T + i/64)*K*(OE+1) + c)*64 + i%64, so a wave reads each
+                              coefficient of its 64 auctions as one 256-B row and a tile's
+                              rows are contiguous; NULL if none / no sampling */
 } ag_batch_in;
 
 /* Outputs of B auctions (dev). Any pointer may be NULL to skip that array. */
@@ -150,7 +154,10 @@ int ag_load_lrts(ag_ctx *ctx, const float *m, const float *q, const float *prev_
 /* Options (ag_set_option). */
 typedef enum ag_option {
   AG_OPT_ITEM_SEARCH = 0,  /* value: ag_item_search */
-  AG_OPT_LANE_AUCTIONS = 1 /* value: 1 (default) or 2 (16-B SoA accesses when B is even) */
+  AG_OPT_LANE_AUCTIONS = 1, /* value: 1 (default) or 2 (16-B SoA accesses when B is even) */
+  AG_OPT_LAUNCH_AUCTIONS = 2 /* value: cap on auctions per k_simulate launch (0 = the exact-
+                                counter capacity of the resident grid); larger batches run
+                                as consecutive launches with identical results */
 } ag_option;
 
 typedef enum ag_item_search {
@@ -188,8 +195,8 @@ int ag_generate(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B, d
 
 /* Synthetic per-participant noise for the participants `part` (dev [P][B]) of auctions
  * [first_auction, first_auction + B): gamma_raw [P][B] = prev_gamma + gamma_sigma * z for
- * shading bidders (NaN otherwise), ts_noise [P][K*(OE+1)][B] = z / sqrt(q) for LR-TS agents
- * (0 otherwise); either output may be NULL. Same Philox key / counter scheme. */
+ * shading bidders (NaN otherwise), ts_noise (tiled as in ag_batch_in) = z / sqrt(q) for
+ * LR-TS agents (0 otherwise); either output may be NULL. Same Philox key / counter scheme. */
 int ag_generate_noise(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B,
                       const int32_t *part, double *gamma_raw, float *ts_noise, void *stream);
 

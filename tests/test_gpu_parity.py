@@ -184,18 +184,21 @@ def test_full_size_synthetic_batch_bit_exact(gpu, oracle):
     assert np.array_equal(out["best_ev"].cpu().numpy().T, orc["best_ev"])
     assert np.array_equal(out["outcome"].cpu().numpy(), orc["outcome"])
     assert np.array_equal(cnt.cpu().numpy(), orc["counters_fx"])
-    # the exact item scan, and one auction per lane, give the same bits
-    for exact, lanes in ((True, 1), (False, 2)):
+    # the exact item scan, two auctions per lane, and a batch run as several launches
+    # (odd-sized auction ranges) give the same bits
+    for exact, lanes, cap in ((True, 1, 0), (False, 2, 0), (False, 1, 1000002), (False, 2, 777778)):
         eng.set_item_search(exact)
         eng.set_lane_auctions(lanes)
+        eng.set_launch_auctions(cap)
         out_x = eng.alloc_outputs(B)
         cnt_x = eng.new_counters()
         eng.simulate(inp, out_x, cnt_x)
         for k in out:
-            assert torch.equal(out[k], out_x[k]), (k, exact, lanes)
+            assert torch.equal(out[k], out_x[k]), (k, exact, lanes, cap)
         assert torch.equal(cnt, cnt_x)
     eng.set_item_search(False)
     eng.set_lane_auctions(1)
+    eng.set_launch_auctions(0)
     # batch split invariance: two halves accumulate to the same exact counters
     cnt2 = eng.new_counters()
     for lo, hi in ((0, B // 3), (B // 3, B)):
@@ -363,9 +366,7 @@ def _pop_run(eng, ctx, part, u, gamma_raw=None, ts_noise=None):
     if gamma_raw is not None:
         inp["gamma_raw"] = torch.from_numpy(np.ascontiguousarray(gamma_raw.T)).to(d)
     if ts_noise is not None:
-        P = part.shape[1]
-        tn = np.ascontiguousarray(ts_noise.reshape(B, P, -1).transpose(1, 2, 0))
-        inp["ts_noise"] = torch.from_numpy(tn).to(d)
+        inp["ts_noise"] = torch.from_numpy(eng.tile_ts_noise(ts_noise)).to(d)
     out = eng.alloc_outputs(B, ("winner", "price", "second_price", "outcome", "item", "bid",
                                 "est_ctr", "true_ctr", "best_ev", "gamma", "propensity"))
     cnt = eng.new_counters()
@@ -431,7 +432,7 @@ def test_mixed_population_full_size(gpu, oracle):
     part = np.ascontiguousarray(inp["part"].cpu().numpy().T)
     u = inp["u"].cpu().numpy()
     gr = np.ascontiguousarray(inp["gamma_raw"].cpu().numpy().T)
-    tn = np.ascontiguousarray(inp["ts_noise"].cpu().numpy().transpose(2, 0, 1)).reshape(B, P, K, OE + 1)
+    tn = eng.untile_ts_noise(inp["ts_noise"], B).reshape(B, P, K, OE + 1)
     # generator sanity: shading draws ~ N(prev_gamma, sigma), LR-TS noise ~ N(0, 1/q)
     a0 = part[:, 0]
     zs = (gr[:, 0] - pg[a0]) / gs[a0]
@@ -523,13 +524,13 @@ def test_lrts_collect_from_replay_and_update(gpu, oracle):
            "part": torch.from_numpy(np.ascontiguousarray(d["part"].T.astype(np.int32))).to(dev),
            "u": torch.from_numpy(np.ascontiguousarray(d["u"])).to(dev),
            "gamma_raw": torch.from_numpy(np.ascontiguousarray(d["gamma_raw"].T)).to(dev),
-           "ts_noise": torch.from_numpy(np.ascontiguousarray(
-               d["ts_noise"].reshape(B, P, -1).transpose(1, 2, 0))).to(dev)}
+           "ts_noise": torch.from_numpy(eng.tile_ts_noise(d["ts_noise"])).to(dev)}
     out = eng.alloc_outputs(B)
     st = eng.new_lrts_samples(B)
     half = B // 2  # two batches, as two flushes of one iteration
     for lo, hi in ((0, half), (half, B)):
-        bi = {k: v[..., lo:hi].contiguous() for k, v in inp.items()}
+        bi = {k: (v[..., lo:hi] if k != "ts_noise" else v[:, lo // 64:hi // 64]).contiguous()
+              for k, v in inp.items()}
         bo = eng.alloc_outputs(hi - lo)
         eng.simulate(bi, bo)
         eng.lrts_collect(bi, bo, st)

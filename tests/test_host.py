@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 def test_library_loads_without_gpu_and_reports_abi():
     from auctiongym_amd import _lib
     L = _lib.load()
-    assert L.ag_abi_version() == _lib.ABI_VERSION == 4
+    assert L.ag_abi_version() == _lib.ABI_VERSION == 6
 
 
 def test_counters_to_double_host_helper():
@@ -142,3 +142,20 @@ def test_graft_entry_build_is_idempotent():
     import __graft_entry__ as G
     G.build()
     assert os.path.exists(LIB)
+
+
+def test_ts_noise_tiling_roundtrip():
+    """The 64-auction tile layout of ag_batch_in.ts_noise (include/auctiongym.h)."""
+    from auctiongym_amd.engine import AuctionEngine
+    g = np.random.default_rng(0)
+    for B in (1, 63, 64, 65, 200):
+        z = g.normal(size=(B, 2, 12, 5)).astype(np.float32)
+        t = AuctionEngine.tile_ts_noise(z)
+        T = (B + 63) // 64
+        assert t.shape == (2, T, 60, 64)
+        flat = t.ravel()
+        for i in (0, B // 2, B - 1):
+            for s in (0, 1):
+                for c in (0, 17, 59):
+                    assert flat[((s * T + i // 64) * 60 + c) * 64 + i % 64] == z[i, s].ravel()[c]
+        assert np.array_equal(AuctionEngine.untile_ts_noise(t, B), z.reshape(B, 2, 60))

@@ -62,10 +62,25 @@ def main():
             if r == 0:
                 same = all(torch.equal(out[k], ref[k]) for k in full) and torch.equal(cnt, cref)
                 print(f"{n}: outputs identical to base: {same}")
+    # sustained: 20 launches back to back per variant (as bench.py times them), interleaved
+    sus = {n: [] for n in engs}
+    for r in range(6):
+        for n, e in engs.items():
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            for _ in range(20):
+                cnt.zero_()
+                e.simulate(inp, out, cnt)
+            b.record(st)
+            torch.cuda.synchronize()
+            if r >= 1:
+                sus[n].append(a.elapsed_time(b) / 20)
     bpa = bench.algorithmic_bytes_per_auction(5, 2, False)
     for n, t in times.items():
         ms, lo = float(np.median(t)), float(np.min(t))
-        print(f"{n:12s} median {ms:.4f} ms  min {lo:.4f} ms  {bpa * B / ms / 1e6:7.1f} GB/s")
+        ss = float(np.median(sus[n]))
+        print(f"{n:12s} isolated median {ms:.4f} ms  min {lo:.4f} ms  {bpa * B / ms / 1e6:7.1f} GB/s | "
+              f"sustained {ss:.4f} ms  {bpa * B / ss / 1e6:7.1f} GB/s")
 
 
 if __name__ == "__main__":
