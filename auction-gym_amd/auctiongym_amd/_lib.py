@@ -16,6 +16,7 @@ BIDDER_TRUTHFUL, BIDDER_EMPIRICAL_SHADED, BIDDER_VALUE_LEARNING = 0, 1, 2
 BIDDER_POLICY_LEARNING, BIDDER_DOUBLY_ROBUST = 3, 4
 OPT_ITEM_SEARCH = 0
 OPT_LAUNCH_AUCTIONS = 2
+OPT_LRTS_BLOCK_SAMPLES = 3
 OPT_LANE_AUCTIONS = 1
 ITEM_SEARCH_AUTO, ITEM_SEARCH_EXACT = 0, 1
 
@@ -31,7 +32,7 @@ EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params
            "ag_generate_noise", "ag_lrts_collect", "ag_lrts_update", "ag_lrts_read",
            "ag_shading_collect", "ag_empirical_update",
            "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_last_error", "ag_abi_version")
-ABI_VERSION = 6
+ABI_VERSION = 7
 LRTS_MAX_EPOCHS = 16384
 LRTS_MAX_DO = 8
 

@@ -164,6 +164,10 @@ class AuctionEngine:
         capacity); larger batches run as consecutive launches, same results."""
         self._check(self.L.ag_set_option(self._h, _lib.OPT_LAUNCH_AUCTIONS, int(n)), "ag_set_option")
 
+    def set_lrts_block_samples(self, n):
+        """Samples per workgroup of the LR-TS training kernel (0: 4096); same results."""
+        self._check(self.L.ag_set_option(self._h, _lib.OPT_LRTS_BLOCK_SAMPLES, int(n)), "ag_set_option")
+
     def load_catalog(self, items, values):
         items = np.ascontiguousarray(items, np.float64)
         values = np.ascontiguousarray(values, np.float64)

@@ -24,6 +24,10 @@ struct ag_lrts_ws {
   int64_t *offsets = nullptr; // [N + 1] bucket offsets, then per-agent cursors [N]
   double *adam_tab = nullptr; // [2][kLrEpochs]: 1 - 0.9^t, (1 - 0.999^t)^0.5 (host pow)
   int32_t *epochs = nullptr;  // [N]
+  void *tables = nullptr;     // workgroup -> (agent, rank) tables + per-agent barriers
+  int64_t *partials = nullptr;  // per-workgroup exact partial sums, 2 epoch parities
+  size_t tab_cap = 0, part_cap = 0;
+  int coop_blocks = 0;        // co-resident workgroups of the training kernel
   int32_t *status = nullptr;  // [1] device-side error flags
 };
 
@@ -39,6 +43,7 @@ struct ag_ctx {
   int32_t partial_blocks = 0;
   int32_t resident[16] = {};  // resident blocks [general][W][screened][counters]
   int64_t launch_cap = 0;  // AG_OPT_LAUNCH_AUCTIONS
+  int64_t lrts_chunk = 0;  // AG_OPT_LRTS_BLOCK_SAMPLES
   bool wide = false;  // 1 auction per lane by default: higher occupancy, faster when sustained
   bool catalog = false;
   // general populations (anything beyond OracleAllocator + TruthfulBidder)

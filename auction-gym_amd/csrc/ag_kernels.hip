@@ -501,6 +501,10 @@ int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
       if (value < 0) return ag_set_error(AG_ERR_INVALID, "ag_set_option: launch auctions must be >= 0");
       c->launch_cap = value;
       return AG_OK;
+    case AG_OPT_LRTS_BLOCK_SAMPLES:
+      if (value < 0) return ag_set_error(AG_ERR_INVALID, "ag_set_option: block samples must be >= 0");
+      c->lrts_chunk = value;
+      return AG_OK;
     default:
       return ag_set_error(AG_ERR_INVALID, "ag_set_option: unknown option %d", option);
   }

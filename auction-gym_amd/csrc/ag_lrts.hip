@@ -21,6 +21,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <vector>
+
 #include "ag_exp.h"
 #include "ag_exp_table.h"
 #include "ag_host.h"
@@ -30,7 +32,7 @@ namespace {
 constexpr int kLrThreads = 256;        // 4 waves; one sample per lane per pass
 constexpr int kLrEpochs = AG_LRTS_MAX_EPOCHS;
 constexpr int kLrMaxKD = 64;           // K * (OE + 1) columns of the accumulator tile
-constexpr int kLrCache = 4;            // samples per lane kept in registers
+constexpr int kLrCache = 16;           // samples per lane kept in registers (1 workgroup / CU)
 constexpr int kAccStride = kLrThreads + 1;  // [column][lane] int64 tile, padded: the column
                                             // reduction (lanes = columns) is conflict-free
 constexpr int kHistory = 100;          // losses[-100] of the early stop
@@ -151,7 +153,7 @@ __global__ __launch_bounds__(kLrThreads) void k_lrts_scatter(const uint32_t *__r
 }
 
 // ---------------------------------------------------------------------------------------
-// 3. training: one workgroup per agent
+// 3. training: up to kLrCache * 256 samples per workgroup, several workgroups per agent
 // ---------------------------------------------------------------------------------------
 struct LrSample {
   float x[AG_LRTS_MAX_DO];
@@ -202,27 +204,89 @@ __device__ __forceinline__ void lr_laplace_sample(const LrSample &s, const float
     acc[(s.item * DO + d) * kAccStride] += fx_round((double)w * (double)(s.x[d] * s.x[d]), kGradScale);
 }
 
+// Barrier of the `nblk` workgroups training one agent (all co-resident: cooperative
+// launch). Thread 0 reads the generation, arrives, and the last arrival opens the next
+// generation; agent-scope release / acquire make the partials written before the barrier
+// (by any workgroup, on any XCD) visible to every workgroup after it.
+__device__ __forceinline__ void agent_barrier(unsigned *count, unsigned *gen, int nblk) {
+  __syncthreads();
+  if (nblk > 1 && threadIdx.x == 0) {
+    const unsigned g = __hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (__hip_atomic_fetch_add(count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nblk - 1) {
+      __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      while (__hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+
+// Per-block column sums of the lane accumulator tile (thread = column c, row group r;
+// each value split at bit 24 so no partial can overflow) into the block's slot of the
+// agent's partials [rank][KD + 1][2] (column KD: the loss); the tile is zeroed for reuse.
+__device__ __forceinline__ void lr_block_partials(int64_t *__restrict__ s_acc, int KD, int64_t lsum_hi,
+                                                  int64_t lsum_lo, int64_t (*s_hi)[kLrMaxKD + 1],
+                                                  int64_t (*s_lo)[kLrMaxKD + 1], int64_t *__restrict__ dst) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  {
+    const int64_t h = wave_sum(lsum_hi), l = wave_sum(lsum_lo);
+    if (lane == 0) {
+      s_hi[wv][KD] = h;
+      s_lo[wv][KD] = l;
+    }
+  }
+  const int c = tid & 63, r = tid >> 6;
+  if (c < KD) {
+    int64_t h = 0, l = 0;
+    int64_t *col = s_acc + c * kAccStride + r * 64;
+    for (int j = 0; j < 64; ++j) {
+      const int64_t v = col[j];
+      col[j] = 0;
+      h += v >> 24;
+      l += v & kLo24;
+    }
+    s_hi[r][c] = h;
+    s_lo[r][c] = l;
+  }
+  __syncthreads();
+  if (tid <= KD) {
+    dst[2 * tid] = s_hi[0][tid] + s_hi[1][tid] + s_hi[2][tid] + s_hi[3][tid];
+    dst[2 * tid + 1] = s_lo[0][tid] + s_lo[1][tid] + s_lo[2][tid] + s_lo[3][tid];
+  }
+}
+
+// The training of one LR-TS agent is spread over `nblk` co-resident workgroups, each
+// owning a contiguous chunk of the agent's samples (the first kLrCache per lane in
+// registers). Every epoch each workgroup writes its exact partial sums; after the agent
+// barrier EVERY workgroup adds all partials (integers: identical totals everywhere) and
+// runs the same Adam / scheduler / early-stop step on its LDS copy of the parameters, so
+// the workgroups stay in lockstep without a second barrier. Partials are double-buffered
+// by epoch parity.
 template <int DO>
 __global__ __launch_bounds__(kLrThreads) void k_lrts_train(
-    int K, const int32_t *__restrict__ akind, const int64_t *__restrict__ offsets,
-    const uint32_t *__restrict__ key, const float *__restrict__ xs, int64_t cap,
-    float *__restrict__ gm, float *__restrict__ gq, float *__restrict__ gpm,
-    const double *__restrict__ adam_tab, int32_t *__restrict__ epochs_out, float *__restrict__ loss_trace) {
-  const int a = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int K, const int32_t *__restrict__ blk_agent, const int32_t *__restrict__ blk_rank,
+    const int32_t *__restrict__ agent_nblk, const int64_t *__restrict__ agent_pbase,
+    const int64_t *__restrict__ offsets, const uint32_t *__restrict__ key, const float *__restrict__ xs,
+    int64_t cap, float *__restrict__ gm, float *__restrict__ gq, float *__restrict__ gpm,
+    const double *__restrict__ adam_tab, int32_t *__restrict__ epochs_out, float *__restrict__ loss_trace,
+    int64_t *__restrict__ partials, unsigned *__restrict__ barriers) {
+  const int a = blk_agent[blockIdx.x], rank = blk_rank[blockIdx.x], nblk = agent_nblk[a];
+  const int tid = threadIdx.x;
   const int64_t s0 = offsets[a], n = offsets[a + 1] - s0;
-  // not an LR-TS agent, or < 2 samples (src/BidderAllocation.py:33-34): nothing changes,
-  // not even prev_m
-  if (akind[a] != AG_ALLOCATOR_LRTS || n < 2) {
-    if (tid == 0) epochs_out[a] = 0;
-    return;
-  }
   const int KD = K * DO;
+  const int PW = 2 * (KD + 1);  // int64 per partial record
+  int64_t *pbase = partials + agent_pbase[a];  // [2 parities][nblk][KD + 1][2]
+  unsigned *bar_count = barriers + 2 * a, *bar_gen = bar_count + 1;
+  // this workgroup's samples: [c0, c1) of the agent's n
+  const int64_t per = (n + nblk - 1) / nblk;
+  const int64_t c0 = (int64_t)rank * per, c1 = c0 + per < n ? c0 + per : n;
+  const int64_t nb = c1 > c0 ? c1 - c0 : 0;
+
   extern __shared__ int64_t s_acc[];  // [KD][kAccStride]
   __shared__ uint64_t s_tab[256];
   __shared__ float s_m[kLrMaxKD], s_pm[kLrMaxKD], s_q[kLrMaxKD], s_ea[kLrMaxKD], s_es[kLrMaxKD];
-  __shared__ int64_t s_hi[4][kLrMaxKD], s_lo[4][kLrMaxKD];
-  __shared__ int64_t s_lhi[4], s_llo[4];
+  __shared__ int64_t s_hi[4][kLrMaxKD + 1], s_lo[4][kLrMaxKD + 1];
   __shared__ float s_hist[kHistory];
   __shared__ float s_loss, s_negstep, s_bc2;
   __shared__ double s_lr, s_best;
@@ -244,14 +308,13 @@ __global__ __launch_bounds__(kLrThreads) void k_lrts_train(
     s_bad = 0;
     s_stop = 0;
   }
-  // this lane's samples: the first kLrCache passes live in registers
   LrSample cache[kLrCache];
   int ncached = 0;
 #pragma unroll
   for (int j = 0; j < kLrCache; ++j) {
     const int64_t i = (int64_t)j * kLrThreads + tid;
-    if (i < n) {
-      lr_load<DO>(key, xs, cap, s0 + i, cache[j]);
+    if (i < nb) {
+      lr_load<DO>(key, xs, cap, s0 + c0 + i, cache[j]);
       ncached = j + 1;
     }
   }
@@ -266,54 +329,41 @@ __global__ __launch_bounds__(kLrThreads) void k_lrts_train(
 #pragma unroll
     for (int j = 0; j < kLrCache; ++j)
       if (j < ncached) lsum += lr_epoch_sample<DO>(cache[j], s_m, acc, s_tab);
-    for (int64_t i = stream_from + tid; i < n; i += kLrThreads) {
-      LrSample s;
-      lr_load<DO>(key, xs, cap, s0 + i, s);
-      lsum += lr_epoch_sample<DO>(s, s_m, acc, s_tab);
-    }
-    {
-      const int64_t h = wave_sum(lsum >> 24), l = wave_sum(lsum & kLo24);
-      if (lane == 0) {
-        s_lhi[wv] = h;
-        s_llo[wv] = l;
-      }
+    for (int64_t i = stream_from + tid; i < nb; i += kLrThreads) {
+      LrSample sm;
+      lr_load<DO>(key, xs, cap, s0 + c0 + i, sm);
+      lsum += lr_epoch_sample<DO>(sm, s_m, acc, s_tab);
     }
     __syncthreads();
-    // ---- B: column sums (thread = column c, row group r) and the loss
-    {
-      const int c = tid & 63, r = tid >> 6;
-      if (c < KD) {
-        int64_t h = 0, l = 0;
-        int64_t *col = s_acc + c * kAccStride + r * 64;
-        for (int j = 0; j < 64; ++j) {
-          const int64_t v = col[j];
-          col[j] = 0;
-          h += v >> 24;
-          l += v & kLo24;
+    // ---- B: this workgroup's exact partials -> global (parity buffer), agent barrier
+    int64_t *pp = pbase + (size_t)(epoch & 1) * nblk * PW;
+    lr_block_partials(s_acc, KD, lsum >> 24, lsum & kLo24, s_hi, s_lo, pp + (size_t)rank * PW);
+    agent_barrier(bar_count, bar_gen, nblk);
+    // ---- C: totals (identical in every workgroup), loss, Adam; scheduler on thread 0
+    if (tid == 0) {
+      int64_t h = 0, l = 0;
+      for (int b = 0; b < nblk; ++b) {
+        h += pp[(size_t)b * PW + 2 * KD];
+        l += pp[(size_t)b * PW + 2 * KD + 1];
+      }
+      double prior = 0.0;
+      for (int k = 0; k < K; ++k)
+        for (int d = 0; d < DO - 1; ++d) {
+          const double df = (double)s_pm[k * DO + d] - (double)s_m[k * DO + d];
+          prior += (double)s_q[k * DO + d] * (df * df);
         }
-        s_hi[r][c] = h;
-        s_lo[r][c] = l;
-      }
-      if (tid == 0) {
-        double prior = 0.0;
-        for (int k = 0; k < K; ++k)
-          for (int d = 0; d < DO - 1; ++d) {
-            const double df = (double)s_pm[k * DO + d] - (double)s_m[k * DO + d];
-            prior += (double)s_q[k * DO + d] * (df * df);
-          }
-        const int64_t h = s_lhi[0] + s_lhi[1] + s_lhi[2] + s_lhi[3];
-        const int64_t l = s_llo[0] + s_llo[1] + s_llo[2] + s_llo[3];
-        s_loss = (float)(0.5 * prior + fx_read(h, l, 1.0 / kLossScale));
-        s_negstep = (float)(-(s_lr / adam_tab[epoch]));
-        s_bc2 = (float)adam_tab[kLrEpochs + epoch];
-      }
+      s_loss = (float)(0.5 * prior + fx_read(h, l, 1.0 / kLossScale));
+      s_negstep = (float)(-(s_lr / adam_tab[epoch]));
+      s_bc2 = (float)adam_tab[kLrEpochs + epoch];
     }
     __syncthreads();
-    // ---- C: Adam on each parameter; scheduler and early stop on thread 0
     if (tid < KD) {
       const int c = tid;
-      const int64_t h = s_hi[0][c] + s_hi[1][c] + s_hi[2][c] + s_hi[3][c];
-      const int64_t l = s_lo[0][c] + s_lo[1][c] + s_lo[2][c] + s_lo[3][c];
+      int64_t h = 0, l = 0;
+      for (int b = 0; b < nblk; ++b) {
+        h += pp[(size_t)b * PW + 2 * c];
+        l += pp[(size_t)b * PW + 2 * c + 1];
+      }
       const double gp = (c % DO) < DO - 1 ? -(double)s_q[c] * ((double)s_pm[c] - (double)s_m[c]) : 0.0;
       const float g = (float)(fx_read(h, l, 1.0 / kGradScale) + gp);
       const float ea = s_ea[c] + 0.1f * (g - s_ea[c]);
@@ -327,7 +377,7 @@ __global__ __launch_bounds__(kLrThreads) void k_lrts_train(
     }
     if (tid == 0) {
       const float loss = s_loss;
-      if (loss_trace) loss_trace[(size_t)a * kLrEpochs + epoch] = loss;
+      if (loss_trace && rank == 0) loss_trace[(size_t)a * kLrEpochs + epoch] = loss;
       s_hist[epoch % kHistory] = loss;
       if ((double)loss < s_best * (1.0 - 1e-4)) {
         s_best = (double)loss;
@@ -353,39 +403,34 @@ __global__ __launch_bounds__(kLrThreads) void k_lrts_train(
 #pragma unroll
   for (int j = 0; j < kLrCache; ++j)
     if (j < ncached) lr_laplace_sample<DO>(cache[j], s_m, acc, s_tab);
-  for (int64_t i = stream_from + tid; i < n; i += kLrThreads) {
-    LrSample s;
-    lr_load<DO>(key, xs, cap, s0 + i, s);
-    lr_laplace_sample<DO>(s, s_m, acc, s_tab);
+  for (int64_t i = stream_from + tid; i < nb; i += kLrThreads) {
+    LrSample sm;
+    lr_load<DO>(key, xs, cap, s0 + c0 + i, sm);
+    lr_laplace_sample<DO>(sm, s_m, acc, s_tab);
   }
   __syncthreads();
-  {
-    const int c = tid & 63, r = tid >> 6;
-    if (c < KD) {
+  int64_t *pp = pbase + (size_t)(epoch & 1) * nblk * PW;
+  lr_block_partials(s_acc, KD, 0, 0, s_hi, s_lo, pp + (size_t)rank * PW);
+  agent_barrier(bar_count, bar_gen, nblk);
+  if (rank == 0) {
+    if (tid < KD) {
+      const int c = tid;
       int64_t h = 0, l = 0;
-      const int64_t *col = s_acc + c * kAccStride + r * 64;
-      for (int j = 0; j < 64; ++j) {
-        h += col[j] >> 24;
-        l += col[j] & kLo24;
+      for (int b = 0; b < nblk; ++b) {
+        h += pp[(size_t)b * PW + 2 * c];
+        l += pp[(size_t)b * PW + 2 * c + 1];
       }
-      s_hi[r][c] = h;
-      s_lo[r][c] = l;
+      q_g[c] = s_q[c] + (float)fx_read(h, l, 1.0 / kGradScale);
+      m_g[c] = s_m[c];
+      pm_g[c] = s_m[c];
     }
+    if (tid == 0) epochs_out[a] = epoch;
   }
-  __syncthreads();
-  if (tid < KD) {
-    const int c = tid;
-    const int64_t h = s_hi[0][c] + s_hi[1][c] + s_hi[2][c] + s_hi[3][c];
-    const int64_t l = s_lo[0][c] + s_lo[1][c] + s_lo[2][c] + s_lo[3][c];
-    q_g[c] = s_q[c] + (float)fx_read(h, l, 1.0 / kGradScale);
-    m_g[c] = s_m[c];
-    pm_g[c] = s_m[c];
-  }
-  if (tid == 0) epochs_out[a] = epoch;
 }
 
-using TrainKernel = void (*)(int, const int32_t *, const int64_t *, const uint32_t *, const float *, int64_t,
-                             float *, float *, float *, const double *, int32_t *, float *);
+using TrainKernel = void (*)(int, const int32_t *, const int32_t *, const int32_t *, const int64_t *,
+                             const int64_t *, const uint32_t *, const float *, int64_t, float *, float *,
+                             float *, const double *, int32_t *, float *, int64_t *, unsigned *);
 
 TrainKernel pick_train(int Do) {
   switch (Do) {
@@ -423,6 +468,8 @@ void ag_lrts_release(ag_ctx *c) {
   (void)hipFree(w.offsets);
   (void)hipFree(w.adam_tab);
   (void)hipFree(w.epochs);
+  (void)hipFree(w.tables);
+  (void)hipFree(w.partials);
   w = ag_lrts_ws();
 }
 
@@ -512,11 +559,108 @@ int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *
                        (int64_t)n, s->capacity, Do, cursors, w.key, w.x, w.cap);
     AG_HIP(hipGetLastError());
   }
+  // agents' sample counts -> workgroups per agent (kLrCache samples per lane each)
+  int64_t *h_off = new int64_t[N + 1];
+  hipError_t e = hipMemcpyAsync(h_off, w.offsets, sizeof(int64_t) * (N + 1), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) {
+    delete[] h_off;
+    return ag_set_error(AG_ERR_HIP, "ag_lrts_update: %s", hipGetErrorString(e));
+  }
   const size_t lds = sizeof(int64_t) * (size_t)K * Do * kAccStride;
   AG_HIP(hipFuncSetAttribute((const void *)train, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(train, dim3(N), dim3(kLrThreads), lds, st, K, c->d_akind, w.offsets, w.key, w.x, w.cap,
-                     c->d_tsm, c->d_tsq, c->d_tsprev, w.adam_tab, w.epochs, loss_trace);
-  AG_HIP(hipGetLastError());
+  if (!w.coop_blocks) {
+    int per_cu = 0, cus = 0;
+    AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)train, kLrThreads, lds));
+    AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    w.coop_blocks = per_cu * cus > 0 ? per_cu * cus : 1;
+  }
+  std::vector<int32_t> nblk(N, 0), blk_agent, blk_rank;
+  std::vector<int64_t> pbase(N, 0);
+  int64_t want = 0;
+  int agents = 0;
+  const int64_t chunk = c->lrts_chunk > 0 ? c->lrts_chunk : (int64_t)kLrCache * kLrThreads;
+  for (int a = 0; a < N; ++a) {
+    const int64_t na = h_off[a + 1] - h_off[a];
+    if (c->h_akind[a] != AG_ALLOCATOR_LRTS || na < 2) continue;
+    nblk[a] = (int32_t)((na + chunk - 1) / chunk);
+    want += nblk[a];
+    ++agents;
+  }
+  delete[] h_off;
+  if (want > w.coop_blocks) {  // more samples than the resident grid caches: share it out
+    const double f = (double)w.coop_blocks / (double)want;
+    want = 0;
+    for (int a = 0; a < N; ++a)
+      if (nblk[a] > 0) {
+        nblk[a] = (int32_t)(nblk[a] * f) > 1 ? (int32_t)(nblk[a] * f) : 1;
+        want += nblk[a];
+      }
+  }
+  int64_t pwords = 0;
+  bool multi = false;
+  for (int a = 0; a < N; ++a) {
+    pbase[a] = pwords;
+    pwords += 2 * (int64_t)nblk[a] * 2 * (K * Do + 1);
+    multi |= nblk[a] > 1;
+    for (int r = 0; r < nblk[a]; ++r) {
+      blk_agent.push_back(a);
+      blk_rank.push_back(r);
+    }
+  }
+  AG_HIP(hipMemsetAsync(w.epochs, 0, sizeof(int32_t) * N, st));
+  const int G = (int)blk_agent.size();
+  if (G > 0) {
+    if (multi && G > w.coop_blocks)
+      return ag_set_error(AG_ERR_UNSUPPORTED, "ag_lrts_update: %d agents need more co-resident workgroups "
+                                              "(%d) than the device holds (%d)", agents, G, w.coop_blocks);
+    if ((size_t)G > w.tab_cap || (size_t)pwords > w.part_cap) {
+      (void)hipFree(w.tables);
+      (void)hipFree(w.partials);
+      w.tables = nullptr;
+      w.partials = nullptr;
+      w.tab_cap = (size_t)G + 256;
+      w.part_cap = (size_t)pwords + 4096;
+      hipError_t e2 = hipMalloc(&w.tables, sizeof(int64_t) * (w.tab_cap + 2 * (size_t)N) +
+                                               sizeof(unsigned) * 2 * (size_t)N);
+      if (e2 == hipSuccess) e2 = hipMalloc(&w.partials, sizeof(int64_t) * w.part_cap);
+      if (e2 != hipSuccess) {
+        w.tab_cap = w.part_cap = 0;
+        return ag_set_error(AG_ERR_HIP, "ag_lrts_update: tables: %s", hipGetErrorString(e2));
+      }
+    }
+    // tables: blk_agent [G] i32, blk_rank [G] i32, agent_nblk [N] i32, agent_pbase [N] i64,
+    // barriers [N][2] u32 (all inside w.tables)
+    char *tb = (char *)w.tables;
+    int32_t *d_bagent = (int32_t *)tb;
+    int32_t *d_brank = d_bagent + w.tab_cap;
+    int32_t *d_nblk = d_brank + w.tab_cap;
+    int64_t *d_pbase = (int64_t *)(d_nblk + 2 * (size_t)N);  // 8-B aligned (even count of i32 before)
+    unsigned *d_bar = (unsigned *)(d_pbase + N);
+    AG_HIP(hipMemcpyAsync(d_bagent, blk_agent.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
+    AG_HIP(hipMemcpyAsync(d_brank, blk_rank.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
+    AG_HIP(hipMemcpyAsync(d_nblk, nblk.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
+    AG_HIP(hipMemcpyAsync(d_pbase, pbase.data(), sizeof(int64_t) * N, hipMemcpyHostToDevice, st));
+    AG_HIP(hipMemsetAsync(d_bar, 0, sizeof(unsigned) * 2 * N, st));
+    int Kv = K;
+    const int32_t *cbagent = d_bagent, *cbrank = d_brank, *cnblk = d_nblk;
+    const int64_t *cpbase = d_pbase, *coffsets = w.offsets;
+    const uint32_t *ckey = w.key;
+    const float *cx = w.x;
+    int64_t ccap = w.cap;
+    float *gm = c->d_tsm, *gq = c->d_tsq, *gpm = c->d_tsprev;
+    const double *ctab = w.adam_tab;
+    int32_t *cep = w.epochs;
+    float *ctr = loss_trace;
+    int64_t *cpart = w.partials;
+    unsigned *cbar = d_bar;
+    void *args[] = {&Kv, &cbagent, &cbrank, &cnblk, &cpbase, &coffsets, &ckey, &cx, &ccap, &gm, &gq, &gpm,
+                    &ctab, &cep, &ctr, &cpart, &cbar};
+    if (multi)  // workgroups of one agent wait for each other: they must all be resident
+      AG_HIP(hipLaunchCooperativeKernel((const void *)train, dim3(G), dim3(kLrThreads), args, (unsigned)lds, st));
+    else
+      AG_HIP(hipLaunchKernel((const void *)train, dim3(G), dim3(kLrThreads), args, lds, st));
+  }
   if (epochs) {
     AG_HIP(hipMemcpyAsync(epochs, w.epochs, sizeof(int32_t) * N, hipMemcpyDeviceToHost, st));
     AG_HIP(hipStreamSynchronize(st));

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define AG_ABI_VERSION 6
+#define AG_ABI_VERSION 7
 
 typedef enum ag_status {
   AG_OK = 0,
@@ -155,9 +155,12 @@ int ag_load_lrts(ag_ctx *ctx, const float *m, const float *q, const float *prev_
 typedef enum ag_option {
   AG_OPT_ITEM_SEARCH = 0,  /* value: ag_item_search */
   AG_OPT_LANE_AUCTIONS = 1, /* value: 1 (default) or 2 (16-B SoA accesses when B is even) */
-  AG_OPT_LAUNCH_AUCTIONS = 2 /* value: cap on auctions per k_simulate launch (0 = the exact-
-                                counter capacity of the resident grid); larger batches run
-                                as consecutive launches with identical results */
+  AG_OPT_LAUNCH_AUCTIONS = 2, /* value: cap on auctions per k_simulate launch (0 = the exact-
+                                 counter capacity of the resident grid); larger batches run
+                                 as consecutive launches with identical results */
+  AG_OPT_LRTS_BLOCK_SAMPLES = 3 /* value: samples per workgroup of the LR-TS training kernel
+                                   (0 = 16 per lane = 4096); fewer spreads an agent over more
+                                   workgroups -- identical results (exact sums) */
 } ag_option;
 
 typedef enum ag_item_search {

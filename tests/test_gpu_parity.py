@@ -488,9 +488,10 @@ def _lrts_engine(N=6, P=2, K=12, E=5, OE=4, lrts=None):
 
 
 def test_lrts_update_matches_oracle_and_reference(gpu, oracle):
-    """The six SP_Truthful_TS agents' iteration-0 updates on the GPU (one workgroup per
-    agent, all six at once) vs the oracle, bit for bit: epochs run, every epoch's loss,
-    m, q and prev_m; and vs the reference within the oracle's pinned tolerances."""
+    """The six SP_Truthful_TS agents' iteration-0 updates on the GPU (all six at once) vs
+    the oracle, bit for bit: epochs run, every epoch's loss, m, q and prev_m; and vs the
+    reference within the oracle's pinned tolerances."""
+    import torch
     kat, m0, q0, pm0 = _kat_population()
     eng = _lrts_engine()
     eng.load_lrts(m0, q0, pm0, thompson_sampling=True)
@@ -498,6 +499,16 @@ def test_lrts_update_matches_oracle_and_reference(gpu, oracle):
     ep, tr = eng.lrts_update(st, trace=True)
     m, q, pm = eng.lrts_state()
     tr = tr.cpu().numpy()
+    # the same update spread over several cooperating workgroups per agent (64 or 100
+    # samples each: 3-8 workgroups, one barrier per epoch): bit-identical
+    for chunk in (64, 100):
+        eng.set_lrts_block_samples(chunk)
+        eng.load_lrts(m0, q0, pm0, thompson_sampling=True)
+        ep2, tr2 = eng.lrts_update(st, trace=True)
+        m2, q2, pm2 = eng.lrts_state()
+        assert np.array_equal(ep2, ep) and torch.equal(tr2.cpu(), torch.from_numpy(tr))
+        assert np.array_equal(m2, m) and np.array_equal(q2, q) and np.array_equal(pm2, pm)
+    eng.set_lrts_block_samples(0)
     for a in range(6):
         k = lambda n: kat[f"a{a}_{n}"]  # noqa: E731
         om, opm, oq, oep, oL = oracle.lrts_update(k("X"), k("A"), k("y"), k("m0"), k("prevm0"), k("q0"))
