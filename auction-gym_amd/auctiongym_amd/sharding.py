@@ -44,3 +44,39 @@ def normalize_limbs(limbs):
         out[i, 1] = (v >> LIMB_BITS) & LIMB_MASK
         out[i, 2] = v >> (2 * LIMB_BITS)
     return out.reshape(np.shape(limbs))
+
+
+def gather_records(store, group=None):
+    """All-gather a record store across ranks (LR-TS won samples: key [cap], x [Do][cap],
+    count [1]; or shading records: agent / gamma / utility [cap], count [1]) into one store
+    holding every rank's records, on every rank. The updates' sums are exact, so training on
+    the gathered records gives bit-identical results on every rank and equals a single
+    process training on the whole batch -- the update needs no per-epoch collective.
+    One all-gather of the counts, one of each record array (padded to the largest count)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return store
+    world = dist.get_world_size(group)
+    n = store["count"].clone()
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n, group=group)
+    counts = [int(c.item()) for c in counts]
+    mx = max(max(counts), 1)
+    total = sum(counts)
+    fields = [k for k in store if k != "count"]
+    out = {}
+    for k in fields:
+        v = store[k]
+        lead = v.shape[:-1]
+        if v.shape[-1] < mx:
+            raise ValueError(f"store field {k} holds {v.shape[-1]} < {mx} records")
+        part = v[..., :mx].contiguous()
+        bufs = [torch.empty_like(part) for _ in range(world)]
+        dist.all_gather(bufs, part, group=group)
+        merged = torch.empty(lead + (max(total, 1),), dtype=v.dtype, device=v.device)
+        off = 0
+        for c, b in zip(counts, bufs):
+            merged[..., off:off + c] = b[..., :c]
+            off += c
+        out[k] = merged
+    out["count"] = torch.tensor([total], dtype=store["count"].dtype, device=store["count"].device)
+    return out

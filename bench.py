@@ -165,23 +165,42 @@ def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True):
 
     elapsed, kern_ms = timed_steps(step, steps, warmup, world, stream)
     bpa = algorithmic_bytes_ts(E, P, K, Do)
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            tj = json.load(f).get("configs_1", {})
+        if tj.get("batch") == B:
+            traffic = tj.get("hbm_bytes_per_launch")
     res = {"workload": "SP_Truthful_TS (configs[1]): 8 LR-TS Thompson-sampling truthful bidders, "
                        "K=12, E=5, OE=4, P=2, SecondPrice",
            "value": B * world * steps / elapsed, "unit": "auctions/s", "ms_per_step": elapsed / steps * 1e3,
            "auctions_per_gpu_per_step": B, "kernel_ms": kern_ms, "algorithmic_bytes_per_auction": bpa,
            "roofline": {"bound": "hbm", "achieved": bpa * B / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": bpa * B / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}}
+                        "unit": "GB/s", "frac": bpa * B / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                        "traffic": traffic}}
     if with_update:
+        from auctiongym_amd.sharding import gather_records
         st = eng.new_lrts_samples(B)
         torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
         t0 = time.perf_counter()
         eng.lrts_collect(inp, out, st)
+        if world > 1:  # every rank trains on all ranks' samples: identical models everywhere
+            st = gather_records(st)
         ep = eng.lrts_update(st)  # synchronises
         torch.cuda.synchronize()
-        res["agent_update"] = {"ms": (time.perf_counter() - t0) * 1e3, "won_samples": int(st["count"][0]),
+        ms = (time.perf_counter() - t0) * 1e3
+        if world > 1:
+            t = torch.tensor([ms], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ms = float(t[0])
+        res["agent_update"] = {"ms": ms, "won_samples": int(st["count"][0]),
                                "epochs": [int(e) for e in ep],
-                               "what": "Agent.update of all 8 LR-TS agents (ag_lrts_collect + "
-                                       "ag_lrts_update: Adam, ReduceLROnPlateau, early stop, Laplace q)"}
+                               "what": "Agent.update of all 8 LR-TS agents (ag_lrts_collect"
+                                       + (" + all-gather of the won samples over RCCL" if world > 1 else "")
+                                       + " + ag_lrts_update: Adam, ReduceLROnPlateau, early stop, Laplace q)"}
     eng.close()
     return res
 
@@ -306,8 +325,7 @@ def main():
     }
 
     if not args.no_ts:
-        result["configs_1"] = run_sp_ts(args.ts_batch, args.steps, args.warmup, world, rank, local,
-                                        with_update=(world == 1))
+        result["configs_1"] = run_sp_ts(args.ts_batch, args.steps, args.warmup, world, rank, local)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)

@@ -81,3 +81,46 @@ def test_normalize_limbs_roundtrip():
     back = [int(a) + (int(b) << 42) + (int(c) << 84) for a, b, c in n]
     assert back == vals
     assert (n[:, 0] >= 0).all() and (n[:, 0] < (1 << 42)).all()
+
+
+def _lrts_worker(rank, world, port, out_path):
+    import sys
+    for p in (os.path.join(ROOT, "auction-gym_amd"), os.path.join(ROOT, "oracle")):
+        sys.path.insert(0, p)
+    import oracle as O
+    from auctiongym_amd.sharding import gather_records, shard_range
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    kat = np.load(os.path.join(ROOT, "tests", "golden", "sp_ts_update_kat.npz"))
+    X, A, y = kat["a2_X"], kat["a2_A"], kat["a2_y"]
+    lo, hi = shard_range(len(y), rank, world)          # this rank's share of the won samples
+    key = (2 << 16) | (A[lo:hi].astype(np.int64) << 1) | (y[lo:hi] != 0)
+    cap = hi - lo + 7
+    st = {"key": torch.zeros(cap, dtype=torch.int32), "x": torch.zeros((5, cap), dtype=torch.float32),
+          "count": torch.tensor([hi - lo], dtype=torch.int64)}
+    st["key"][:hi - lo] = torch.from_numpy(key.astype(np.uint32).view(np.int32))
+    st["x"][:, :hi - lo] = torch.from_numpy(X[lo:hi].astype(np.float32).T)
+    g = gather_records(st)
+    n = int(g["count"][0])
+    k = g["key"][:n].numpy().view(np.uint32)
+    xs = g["x"][:, :n].numpy().T
+    m, pm, q, ep, _ = O.lrts_update(xs, (k >> 1) & 0x7FFF, k & 1, kat["a2_m0"], kat["a2_prevm0"], kat["a2_q0"])
+    np.save(out_path + f".{rank}.npy", np.concatenate([m.ravel(), q.ravel(), [ep]]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_lrts_update_on_gathered_samples_is_rank_independent(tmp_path, oracle, world):
+    """Each rank holds a shard of the won samples; after gather_records every rank trains on
+    the same multiset: identical m, q, epochs on every rank, equal to one process training
+    on all samples (exact sums: order-free)."""
+    out = str(tmp_path / "lrts")
+    mp.spawn(_lrts_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    got = [np.load(out + f".{r}.npy") for r in range(world)]
+    kat = np.load(os.path.join(ROOT, "tests", "golden", "sp_ts_update_kat.npz"))
+    m, pm, q, ep, _ = oracle.lrts_update(kat["a2_X"], kat["a2_A"], kat["a2_y"], kat["a2_m0"],
+                                         kat["a2_prevm0"], kat["a2_q0"])
+    want = np.concatenate([m.ravel(), q.ravel(), [ep]])
+    for g in got:
+        assert np.array_equal(g, want)

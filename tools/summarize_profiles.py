@@ -32,7 +32,9 @@ def main():
     stats = glob.glob(os.path.join(src, "stats", "*kernel_stats.csv"))[0]
     shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
     summary = {"tag": tag, "batch": batch}
-    for part in ("fetch", "write", "sq", "sq2"):
+    for part in ("fetch", "write", "sq", "sq2", "ts_fetch", "ts_write"):
+        if not os.path.isdir(os.path.join(src, part)):
+            continue
         vals, n = pmc(os.path.join(src, part))
         summary[part] = {"dispatches": n, "per_dispatch_mean": vals}
     fetch_kb = summary["fetch"]["per_dispatch_mean"]["FETCH_SIZE"]
@@ -41,12 +43,21 @@ def main():
     hbm = fetch_kb * 1024 * 2 + write_kb * 1024
     summary["hbm_bytes_per_launch"] = hbm
     summary["algorithmic_bytes_per_launch"] = 141 * batch
+    traffic = {"batch": batch, "hbm_bytes_per_launch": hbm,
+               "source": f"profiles/{tag}_pmc_summary.json (k_simulate<2,6,true,1,false>, "
+                         "FETCH_SIZE*2*1024 + WRITE_SIZE*1024, mean over dispatches)"}
+    if "ts_fetch" in summary and "ts_write" in summary:
+        ts_b = 1 << 20
+        ts_hbm = (summary["ts_fetch"]["per_dispatch_mean"]["FETCH_SIZE"] * 1024 * 2 +
+                  summary["ts_write"]["per_dispatch_mean"]["WRITE_SIZE"] * 1024)
+        summary["ts_hbm_bytes_per_launch"] = ts_hbm
+        summary["ts_algorithmic_bytes_per_launch"] = 621 * ts_b
+        traffic["configs_1"] = {"batch": ts_b, "hbm_bytes_per_launch": ts_hbm,
+                                "source": f"profiles/{tag}_pmc_summary.json (k_simulate<2,6,true,1,true>)"}
     with open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
-        json.dump({"batch": batch, "hbm_bytes_per_launch": hbm,
-                   "source": f"profiles/{tag}_pmc_summary.json (k_simulate, FETCH_SIZE*2*1024 + "
-                             "WRITE_SIZE*1024, mean over dispatches)"}, f, indent=1)
+        json.dump(traffic, f, indent=1)
     print(json.dumps({"hbm_bytes_per_launch": hbm, "algorithmic": 141 * batch,
                       "ratio": hbm / (141 * batch)}))
 
