@@ -217,6 +217,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ts-batch", type=int, default=1 << 20, help="SP_Truthful_TS auctions per GPU per step")
     ap.add_argument("--no-ts", action="store_true", help="skip the SP_Truthful_TS (configs[1]) line")
+    ap.add_argument("--no-update", action="store_true", help="skip timing the LR-TS Agent.update")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -325,7 +326,8 @@ def main():
     }
 
     if not args.no_ts:
-        result["configs_1"] = run_sp_ts(args.ts_batch, args.steps, args.warmup, world, rank, local)
+        result["configs_1"] = run_sp_ts(args.ts_batch, args.steps, args.warmup, world, rank, local,
+                                        with_update=not args.no_update)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)

@@ -59,7 +59,9 @@ def install_shims():
 
     nb.jit = jit
     sys.modules["numba"] = nb
-    sys.modules["seaborn"] = types.ModuleType("seaborn")
+    sns = types.ModuleType("seaborn")
+    sns.lineplot = lambda *a, **k: None  # plots only (src/main.py:239-326)
+    sys.modules["seaborn"] = sns
     import matplotlib
     matplotlib.use("Agg")
     import torch
@@ -457,14 +459,59 @@ def empirical_update_kat(out_name="empirical_update_kat", iters=3):
     np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
 
 
+CSV_CASES = {
+    # name: config overrides on oracle_truthful_cfg(...) (both populations run end to end on
+    # the GPU path, so main.py's CSV files can be compared cell by cell)
+    "sp_oracle": (dict(n_agents=6, n_items=12, P=2, allocation="SecondPrice", seed=0), None),
+    "fp_empirical": (dict(n_agents=6, n_items=12, P=2, allocation="FirstPrice", seed=21),
+                     {"type": "EmpiricalShadedBidder", "kwargs": {"gamma_sigma": 0.05, "init_gamma": 0.9}}),
+}
+
+
+def csv_outputs(runs=2, iters=3, rounds=2000):
+    """The reference's own __main__ (src/main.py:157-345) on small configs; its CSV files are
+    the fixtures (tests/golden/csv/<case>/), with the config used."""
+    import runpy
+    import shutil
+    for name, (kw, bidder) in CSV_CASES.items():
+        cfg = oracle_truthful_cfg(**kw)
+        if bidder:
+            cfg["agents"][0]["bidder"] = bidder
+        cfg.update(num_runs=runs, num_iter=iters, rounds_per_iter=rounds)
+        work = tempfile.mkdtemp()
+        cfg["output_dir"] = os.path.join(work, "out")
+        path = os.path.join(work, "cfg.json")
+        with open(path, "w") as f:
+            json.dump(cfg, f)
+        argv = sys.argv
+        sys.argv = ["main.py", path]
+        try:
+            runpy.run_path(os.path.join(REF_SRC, "main.py"), run_name="__main__")
+        finally:
+            sys.argv = argv
+        dst = os.path.join(OUT, "csv", name)
+        os.makedirs(dst, exist_ok=True)
+        for f in os.listdir(cfg["output_dir"]):
+            if f.endswith(".csv"):
+                shutil.copy(os.path.join(cfg["output_dir"], f), dst)
+        cfg["output_dir"] = "OUTPUT_DIR"
+        with open(os.path.join(dst, "config.json"), "w") as f:
+            json.dump(cfg, f, indent=1)
+        shutil.rmtree(work)
+        print("csv", name, sorted(os.listdir(dst)), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also run SP_Oracle as shipped (3x20x10k rounds, ~1 min)")
-    ap.add_argument("--only", choices=["empirical"], help="regenerate one fixture family only")
+    ap.add_argument("--only", choices=["empirical", "csv"], help="regenerate one fixture family only")
     args = ap.parse_args()
     install_shims()
     if args.only == "empirical":
         empirical_update_kat()
+        return
+    if args.only == "csv":
+        csv_outputs()
         return
 
     sigmoid_kats()
@@ -504,6 +551,8 @@ def main():
     save_capture("fp_empirical_r2048", a, g, m)
     # 9. EmpiricalShadedBidder.update over three iterations of three populations.
     empirical_update_kat()
+    # 10. main.py's CSV outputs (SP_Oracle-shaped and EmpiricalShaded, 2 runs x 3 iterations).
+    csv_outputs()
 
     if args.full:
         agg = full_run_aggregates("SP_Oracle.json")
