@@ -1,0 +1,403 @@
+/*
+ * ag_oracle_dr.c -- TEST INFRASTRUCTURE ONLY (part of the oracle, see ag_oracle.h).
+ *
+ * CPU restatement of DoublyRobustBidder.update (src/Bidder.py:473-615) with its models
+ * (src/Models.py:51-62 PyTorchWinRateEstimator, :92-218 BidShadingContextualBandit):
+ *   1. win-rate fit: sigmoid(w . [ctr, value, gamma] + b) by BCE (mean) on the logs plus
+ *      the "shade 100% -> lose" augmentation (gamma = 0, y = 0) (:500-514), Adam(lr 3e-3,
+ *      weight decay 1e-6, AMSGrad), ReduceLROnPlateau(patience 256, factor 0.2, min_lr
+ *      1e-7), early stop after 1024 epochs without a 1e-6 improvement, <= 32768 epochs;
+ *   2. estimated utilities W (V - P) of the logged bids with the fitted model (:541-546);
+ *   3. first update only: imitation of the logging policy (src/Models.py:106-137): MSE of
+ *      mu to the logged gammas + MSE of sigma to 0.05, Adam(lr 1e-3, wd 1e-4, AMSGrad),
+ *      early stop after 512 epochs, <= 16384 epochs;
+ *   4. DR policy fit (:562-590, src/Models.py:201-218): loss -mean((u - u_hat) clip(pi/pi0,
+ *      1/50, 50) + W(ctr, value, clip(mu + sigma eps, 0, 1)) (V - P)), eps the per-epoch
+ *      rsample noise (given), Adam(lr 7e-3, wd 1e-4, AMSGrad), ReduceLROnPlateau(patience
+ *      100, factor 0.2, min_lr 1e-8, threshold 5e-3), early stop after 512, <= 32768.
+ *
+ * Arithmetic (the definition the device kernel follows bit for bit): parameters and their
+ * Adam state in float32 with torch's single-tensor update (weight decay added to the
+ * gradient, AMSGrad max of the second moments); per-sample forward / backward in double
+ * from the float32 features and parameters, exp from libm (glibc; the device uses its
+ * glibc-identical restatement), log1p inside softplus from the fdlibm algorithm restated
+ * below (so host and device agree bit for bit); sums over samples EXACT (terms on a 2^-40
+ * grid, added as integers) and divided by the sample count once. torch computes all of
+ * this in float32 in its own order, so trajectories agree to float32 rounding per epoch
+ * and drift apart chaotically late in long fits (tests pin loss0 / gradients and the
+ * trajectories within measured tolerances).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "ag_oracle.h"
+
+/* fdlibm log1p (public-domain algorithm: reduction to 1+f in [sqrt(2)/2, sqrt(2)),
+ * s = f/(2+f), odd minimax polynomial in s, correction term c), restated. */
+static double fl_log1p(double x) {
+  static const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                      Lp1 = 6.666666666666735130e-01, Lp2 = 3.999999999940941908e-01,
+                      Lp3 = 2.857142874366239149e-01, Lp4 = 2.222219843214978396e-01,
+                      Lp5 = 1.818357216161805012e-01, Lp6 = 1.531383769920937332e-01,
+                      Lp7 = 1.479819860511658591e-01;
+  uint64_t bits;
+  memcpy(&bits, &x, 8);
+  int32_t hx = (int32_t)(bits >> 32), ax = hx & 0x7fffffff, hu = 0, k = 1;
+  double f = 0.0, c = 0.0;
+  if (hx < 0x3FDA827A) {                    /* 1 + x < sqrt(2)+ */
+    if (ax >= 0x3ff00000) return x == -1.0 ? -INFINITY : NAN;
+    if (ax < 0x3e200000) {                  /* |x| < 2^-29 */
+      if (ax < 0x3c900000) return x;
+      return x - x * x * 0.5;
+    }
+    if (hx > 0 || hx <= (int32_t)0xbfd2bec4) { /* sqrt(2)/2- <= 1 + x < sqrt(2)+ */
+      k = 0;
+      f = x;
+      hu = 1;
+    }
+  }
+  if (hx >= 0x7ff00000) return x + x;
+  if (k != 0) {
+    double u;
+    if (hx < 0x43400000) {
+      u = 1.0 + x;
+      uint64_t ub;
+      memcpy(&ub, &u, 8);
+      hu = (int32_t)(ub >> 32);
+      k = (hu >> 20) - 1023;
+      c = (k > 0) ? 1.0 - (u - x) : x - (u - 1.0);
+      c /= u;
+    } else {
+      u = x;
+      uint64_t ub;
+      memcpy(&ub, &u, 8);
+      hu = (int32_t)(ub >> 32);
+      k = (hu >> 20) - 1023;
+      c = 0;
+    }
+    hu &= 0x000fffff;
+    uint64_t ub;
+    memcpy(&ub, &u, 8);
+    if (hu < 0x6a09e) {
+      ub = ((uint64_t)(uint32_t)(hu | 0x3ff00000) << 32) | (ub & 0xffffffffull);
+    } else {
+      k += 1;
+      ub = ((uint64_t)(uint32_t)(hu | 0x3fe00000) << 32) | (ub & 0xffffffffull);
+      hu = (0x00100000 - hu) >> 2;
+    }
+    memcpy(&u, &ub, 8);
+    f = u - 1.0;
+  }
+  const double hfsq = 0.5 * f * f;
+  if (hu == 0) { /* |f| < 2^-20 */
+    if (f == 0.0) {
+      if (k == 0) return 0.0;
+      c += k * ln2_lo;
+      return k * ln2_hi + c;
+    }
+    const double R = hfsq * (1.0 - 0.66666666666666666 * f);
+    if (k == 0) return f - R;
+    return k * ln2_hi - ((R - (k * ln2_lo + c)) - f);
+  }
+  const double s = f / (2.0 + f), z = s * s;
+  const double R = z * (Lp1 + z * (Lp2 + z * (Lp3 + z * (Lp4 + z * (Lp5 + z * (Lp6 + z * Lp7))))));
+  if (k == 0) return f - (hfsq - s * (hfsq + R));
+  return k * ln2_hi - ((hfsq - (s * (hfsq + R) + (k * ln2_lo + c))) - f);
+}
+
+double ora_log1p_restated(double x) { return fl_log1p(x); }
+
+/* torch.nn.Softplus (beta 1, threshold 20) and its derivative */
+static double softplus(double u) { return u > 20.0 ? u : fl_log1p(exp(u)); }
+static double dsoftplus(double u) {
+  if (u > 20.0) return 1.0;
+  const double e = exp(u);
+  return e / (e + 1.0);
+}
+
+#define DR_GRID 0x1p40
+#define DR_INV 0x1p-40
+
+static int64_t fxr(double v) { return (int64_t)nearbyint(v * DR_GRID); }
+static double fxv(__int128 s) {
+  int64_t hi = (int64_t)(s >> 24), lo = (int64_t)(s & 0xFFFFFF);
+  return ((double)hi * 0x1p24 + (double)lo) * DR_INV;
+}
+
+/* torch.optim.Adam, single-tensor CPU path, weight decay, AMSGrad (tensors < 16 elements:
+ * the scalar loops, no fused multiply-adds) */
+typedef struct {
+  int32_t np;
+  float ea[16], es[16], mx[16];
+  double lr, wd;
+  int64_t step;
+} adam_t;
+
+static void adam_init(adam_t *a, int32_t np, double lr, double wd) {
+  memset(a, 0, sizeof *a);
+  a->np = np;
+  a->lr = lr;
+  a->wd = wd;
+}
+
+static void adam_step(adam_t *a, float *p, const float *grad) {
+  a->step += 1;
+  const double t = (double)a->step;
+  const double bc1 = 1.0 - pow(0.9, t), bc2s = pow(1.0 - pow(0.999, t), 0.5);
+  const float neg_step = (float)(-(a->lr / bc1)), bc2f = (float)bc2s, wdf = (float)a->wd;
+  for (int32_t j = 0; j < a->np; ++j) {
+    const float g = grad[j] + wdf * p[j];
+    a->ea[j] = a->ea[j] + 0.1f * (g - a->ea[j]);
+    a->es[j] = a->es[j] * 0.999f + (0.001f * g) * g;
+    a->mx[j] = a->mx[j] > a->es[j] ? a->mx[j] : a->es[j];
+    const float den = sqrtf(a->mx[j]) / bc2f + 1e-8f;
+    p[j] = p[j] + neg_step * (a->ea[j] / den);
+  }
+}
+
+/* torch.optim.lr_scheduler.ReduceLROnPlateau, mode 'min', threshold_mode 'rel' */
+typedef struct {
+  double best, threshold, factor, min_lr;
+  int32_t bad, patience;
+} plateau_t;
+
+static void plateau_init(plateau_t *s, int32_t patience, double factor, double min_lr, double threshold) {
+  s->best = INFINITY;
+  s->bad = 0;
+  s->patience = patience;
+  s->factor = factor;
+  s->min_lr = min_lr;
+  s->threshold = threshold;
+}
+
+static void plateau_step(plateau_t *s, float loss, double *lr) {
+  if ((double)loss < s->best * (1.0 - s->threshold)) {
+    s->best = (double)loss;
+    s->bad = 0;
+  } else {
+    s->bad += 1;
+  }
+  if (s->bad > s->patience) {
+    double nl = *lr * s->factor;
+    if (nl < s->min_lr) nl = s->min_lr;
+    if (*lr - nl > 1e-8) *lr = nl;
+    s->bad = 0;
+  }
+}
+
+/* the reference's early stop: (best - loss) > 1e-6 resets; stop when epoch - best > wait */
+typedef struct {
+  double best;
+  int32_t best_epoch, wait;
+} stopper_t;
+
+static int stop_step(stopper_t *s, int32_t epoch, float loss) {
+  if (s->best - (double)loss > 1e-6) {
+    s->best_epoch = epoch;
+    s->best = (double)loss;
+    return 0;
+  }
+  return epoch - s->best_epoch > s->wait;
+}
+
+/* win-rate model W(x) = sigmoid(w0 c + w1 v + w2 g + b) */
+static double winrate(const float *wr, double c, double v, double g) {
+  const double z = c * (double)wr[0] + v * (double)wr[1] + g * (double)wr[2] + (double)wr[3];
+  return 1.0 / (1.0 + exp(-z));
+}
+
+/* policy forward: p = [W1 (2x2 row-major), b1 (2), wm (2), bm, ws (2), bs] (the order of
+ * BidShadingContextualBandit.parameters()) */
+typedef struct {
+  double h[2], s[2], am, as, mu, sp_sigma, sigma;
+} polf_t;
+
+static void policy_fwd(const float *p, double c, double v, polf_t *f) {
+  for (int j = 0; j < 2; ++j) {
+    f->h[j] = c * (double)p[2 * j] + v * (double)p[2 * j + 1] + (double)p[4 + j];
+    f->s[j] = softplus(f->h[j]);
+  }
+  f->am = f->s[0] * (double)p[6] + f->s[1] * (double)p[7] + (double)p[8];
+  f->as = f->s[0] * (double)p[9] + f->s[1] * (double)p[10] + (double)p[11];
+  f->mu = softplus(f->am);
+  f->sp_sigma = softplus(f->as);
+  f->sigma = f->sp_sigma + 0.01;  /* min_sigma (src/Models.py:104) */
+}
+
+/* d(loss_i)/d(params) from d/dmu and d/dsigma of one sample, accumulated as fixed point */
+static void policy_bwd(const float *p, double c, double v, const polf_t *f, double dmu, double dsigma,
+                       __int128 *G) {
+  const double dam = dmu * dsoftplus(f->am), das = dsigma * dsoftplus(f->as);
+  double ds[2];
+  ds[0] = dam * (double)p[6] + das * (double)p[9];
+  ds[1] = dam * (double)p[7] + das * (double)p[10];
+  G[6] += fxr(dam * f->s[0]);
+  G[7] += fxr(dam * f->s[1]);
+  G[8] += fxr(dam);
+  G[9] += fxr(das * f->s[0]);
+  G[10] += fxr(das * f->s[1]);
+  G[11] += fxr(das);
+  for (int j = 0; j < 2; ++j) {
+    const double dh = ds[j] * dsoftplus(f->h[j]);
+    G[2 * j] += fxr(dh * c);
+    G[2 * j + 1] += fxr(dh * v);
+    G[4 + j] += fxr(dh);
+  }
+}
+
+int32_t ora_dr_update(int64_t n, const double *ctr, const double *value, const double *gamma,
+                      const double *prop, const uint8_t *won, const double *util, float *wr, float *pol,
+                      int32_t initialised, const float *noise, int64_t noise_epochs, int32_t *epochs,
+                      float *wr_trace, float *init_trace, float *dr_trace, double *est_util_out) {
+  if (n < 1) return -1;
+  float *cf = malloc(n * sizeof(float)), *vf = malloc(n * sizeof(float)), *gf = malloc(n * sizeof(float));
+  double *eu = malloc(n * sizeof(double));
+  for (int64_t i = 0; i < n; ++i) {
+    cf[i] = (float)ctr[i];
+    vf[i] = (float)value[i];
+    gf[i] = (float)gamma[i];
+  }
+  const double M = 2.0 * (double)n;
+  /* ---- 1. win-rate fit */
+  {
+    adam_t ad;
+    adam_init(&ad, 4, 3e-3, 1e-6);
+    plateau_t pl;
+    plateau_init(&pl, 256, 0.2, 1e-7, 1e-4);
+    stopper_t st = {INFINITY, -1, 1024};
+    int32_t e = 0;
+    for (; e < 32768; ++e) {
+      __int128 L = 0, G[4] = {0, 0, 0, 0};
+      for (int64_t r = 0; r < 2 * n; ++r) {
+        const int64_t i = r < n ? r : r - n;
+        const double c = cf[i], v = vf[i], g = r < n ? gf[i] : 0.0;
+        const double y = r < n ? (double)won[i] : 0.0;
+        const double z = c * (double)wr[0] + v * (double)wr[1] + g * (double)wr[2] + (double)wr[3];
+        const double pw = 1.0 / (1.0 + exp(-z));
+        /* BCE with torch's clamp of the logs at -100: -log(p) = softplus(-z), -log(1-p) =
+         * softplus(z) (exp + the restated log1p: the same bits on the device) */
+        const double t = y > 0.0 ? fmin(softplus(-z), 100.0) : fmin(softplus(z), 100.0);
+        L += fxr(t);
+        const double gz = pw - y;
+        G[0] += fxr(gz * c);
+        G[1] += fxr(gz * v);
+        G[2] += fxr(gz * g);
+        G[3] += fxr(gz);
+      }
+      const float loss = (float)(fxv(L) / M);
+      float grad[4];
+      for (int j = 0; j < 4; ++j) grad[j] = (float)(fxv(G[j]) / M);
+      adam_step(&ad, wr, grad);
+      if (wr_trace) wr_trace[e] = loss;
+      plateau_step(&pl, loss, &ad.lr);
+      if (stop_step(&st, e, loss)) {
+        ++e;
+        break;
+      }
+    }
+    epochs[0] = e;
+  }
+  /* ---- 2. estimated utilities with the fitted model (float32 W, as .numpy() of it) */
+  for (int64_t i = 0; i < n; ++i) {
+    const float W = (float)winrate(wr, cf[i], vf[i], gf[i]);
+    const double V = ctr[i] * value[i], P = ctr[i] * value[i] * gamma[i];
+    eu[i] = (double)W * (V - P);
+    if (est_util_out) est_util_out[i] = eu[i];
+  }
+  /* ---- 3. imitation of the logging policy (first update only) */
+  epochs[1] = 0;
+  if (!initialised) {
+    adam_t ad;
+    adam_init(&ad, 12, 1e-3, 1e-4);
+    stopper_t st = {INFINITY, -1, 512};
+    int32_t e = 0;
+    for (; e < 16384; ++e) {
+      __int128 L1 = 0, L2 = 0, G[12];
+      memset(G, 0, sizeof G);
+      for (int64_t i = 0; i < n; ++i) {
+        polf_t f;
+        policy_fwd(pol, cf[i], vf[i], &f);
+        /* predicted sigma WITHOUT min_sigma here (src/Models.py:118) */
+        const double dm = f.mu - (double)gf[i], dsg = f.sp_sigma - 0.05;
+        L1 += fxr(dm * dm);
+        L2 += fxr(dsg * dsg);
+        policy_bwd(pol, cf[i], vf[i], &f, 2.0 * dm, 2.0 * dsg, G);
+      }
+      const float loss = (float)(fxv(L1) / (double)n + fxv(L2) / (double)n);
+      float grad[12];
+      for (int j = 0; j < 12; ++j) grad[j] = (float)(fxv(G[j]) / (double)n);
+      adam_step(&ad, pol, grad);
+      if (init_trace) init_trace[e] = loss;
+      if (stop_step(&st, e, loss)) {
+        ++e;
+        break;
+      }
+    }
+    epochs[1] = e;
+  }
+  /* ---- 4. doubly robust policy fit */
+  {
+    adam_t ad;
+    adam_init(&ad, 12, 7e-3, 1e-4);
+    plateau_t pl;
+    plateau_init(&pl, 100, 0.2, 1e-8, 5e-3);
+    stopper_t st = {INFINITY, -1, 512};
+    const double inv_sqrt2pi = 1.0 / sqrt(2.0 * 3.141592653589793);
+    int32_t e = 0;
+    for (; e < 32768 && e < noise_epochs; ++e) {
+      const float *eps = noise + (int64_t)e * n;
+      __int128 L = 0, G[12];
+      memset(G, 0, sizeof G);
+      for (int64_t i = 0; i < n; ++i) {
+        polf_t f;
+        policy_fwd(pol, cf[i], vf[i], &f);
+        const double mu = f.mu, sg = f.sigma, g = (double)gf[i];
+        const double zz = (mu - g) / sg;
+        const double pdf_raw = exp(-(zz * zz) / 2.0) / sg * inv_sqrt2pi;
+        const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
+        const double p0 = (double)fmaxf((float)prop[i], 1e-15f);
+        const double iw = pi / p0;
+        const double iwc = iw < 1.0 / 50.0 ? 1.0 / 50.0 : (iw > 50.0 ? 50.0 : iw);
+        const double du = (double)(float)util[i] - (double)(float)eu[i];
+        const double raw = mu + sg * (double)eps[i];
+        const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
+        const double c = cf[i], v = vf[i];
+        const double Wv = winrate(wr, c, v, gs);
+        const double V = c * v;
+        const double dm_term = Wv * (V - V * gs);
+        L += fxr(-(du * iwc + dm_term));
+        /* d(-term)/dmu, d(-term)/dsigma */
+        double dpi_dmu = 0.0, dpi_dsg = 0.0;
+        if (pdf_raw >= 1e-30 && iw >= 1.0 / 50.0 && iw <= 50.0) {
+          const double k = du / p0;              /* d(du * iw)/dpi */
+          dpi_dmu = k * pdf_raw * (g - mu) / (sg * sg);
+          dpi_dsg = k * pdf_raw * ((g - mu) * (g - mu) / (sg * sg * sg) - 1.0 / sg);
+        }
+        double ddm_dgs = 0.0;
+        if (raw >= 0.0 && raw <= 1.0)
+          ddm_dgs = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)wr[2];
+        const double dmu = -(dpi_dmu + ddm_dgs);
+        const double dsg = -(dpi_dsg + ddm_dgs * (double)eps[i]);
+        policy_bwd(pol, c, v, &f, dmu, dsg, G);
+      }
+      const float loss = (float)(fxv(L) / (double)n);
+      float grad[12];
+      for (int j = 0; j < 12; ++j) grad[j] = (float)(fxv(G[j]) / (double)n);
+      adam_step(&ad, pol, grad);
+      if (dr_trace) dr_trace[e] = loss;
+      plateau_step(&pl, loss, &ad.lr);
+      if (stop_step(&st, e, loss)) {
+        ++e;
+        break;
+      }
+    }
+    epochs[2] = e;
+  }
+  free(cf);
+  free(vf);
+  free(gf);
+  free(eu);
+  return 0;
+}

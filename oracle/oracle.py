@@ -85,6 +85,10 @@ def lib():
         L.ora_lrts_loss_grad.argtypes = [i64, i32, i32, vp, vp, vp, vp, vp, vp, vp]
         L.ora_empirical_update.restype = i32
         L.ora_empirical_update.argtypes = [i64, vp, vp, vp]
+        L.ora_dr_update.restype = i32
+        L.ora_dr_update.argtypes = [i64] + [vp] * 8 + [i32, vp, i64] + [vp] * 5
+        L.ora_log1p_restated.restype = d
+        L.ora_log1p_restated.argtypes = [d]
         L.ora_lrts_update.restype = i32
         L.ora_lrts_update.argtypes = [i64, i32, i32, vp, vp, vp, vp, vp, vp, vp]
         _lib = L
@@ -255,3 +259,27 @@ def empirical_update(gammas, utilities):
     if rc:
         raise ValueError(EMPIRICAL_ERRORS[rc])
     return float(out[0])
+
+
+def dr_update(ctr, value, gamma, prop, won, util, wr, pol, initialised, noise, trace=True):
+    """DoublyRobustBidder.update (src/Bidder.py:473-615) of one agent; noise [E][n] float32
+    per-epoch rsample draws of the DR fit. Returns dict(wr, pol, epochs, wr_losses,
+    init_losses, dr_losses, est_util)."""
+    n = len(ctr)
+    a = [np.ascontiguousarray(v, np.float64) for v in (ctr, value, gamma, prop)]
+    w = np.ascontiguousarray(np.asarray(won) != 0, np.uint8)
+    u = np.ascontiguousarray(util, np.float64)
+    wr = np.array(wr, np.float32).ravel().copy()
+    pol = np.array(pol, np.float32).ravel().copy()
+    noise = np.ascontiguousarray(noise, np.float32)
+    E = noise.shape[0] if noise.size else 0
+    ep = np.zeros(3, np.int32)
+    tr = [np.zeros(32768, np.float32), np.zeros(16384, np.float32), np.zeros(32768, np.float32)]
+    eu = np.zeros(n)
+    rc = lib().ora_dr_update(n, *[_p(v) for v in a], _p(w), _p(u), _p(wr), _p(pol), int(bool(initialised)),
+                             _p(noise), E, _p(ep), *[(_p(t) if trace else None) for t in tr], _p(eu))
+    if rc:
+        raise ValueError("DoublyRobustBidder.update without logs")
+    return {"wr": wr, "pol": pol, "epochs": ep.copy(), "wr_losses": tr[0][:ep[0]].astype(np.float64),
+            "init_losses": tr[1][:ep[1]].astype(np.float64), "dr_losses": tr[2][:ep[2]].astype(np.float64),
+            "est_util": eu}

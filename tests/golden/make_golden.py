@@ -360,6 +360,132 @@ def lrts_update_kat(agents, out_name):
     np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
 
 
+def dr_update_kat(out_name="dr_update_kat", rounds=2048):
+    """DoublyRobustBidder.update (src/Bidder.py:473-615; src/Models.py:51-218) on the logs of
+    FP_DR_TS.json's first iteration, through the reference's own classes: the update's
+    inputs, the models' initial parameters, epoch-0 loss and gradients of the three fits
+    (win-rate BCE, policy imitation MSE, DR policy loss at its starting point with the
+    recorded torch RNG state), the per-epoch scheduler losses of the two scheduled fits, the
+    torch RNG state at the start of the DR fit (its per-epoch rsample noise), and the
+    parameters after each fit."""
+    import copy
+
+    import torch
+    import Models
+    _, _, _, (agents, _, _) = capture(load_cfg("FP_DR_TS.json"), rounds, keep=True)
+    recs = []
+
+    class RecRP(torch.optim.lr_scheduler.ReduceLROnPlateau):
+        def __init__(self, *a, verbose=None, **k):
+            super().__init__(*a, **k)
+            self.rec = {"rng": torch.get_rng_state().clone(), "losses": []}
+            recs.append(self.rec)
+
+        def step(self, metrics, *a, **k):
+            self.rec["losses"].append(float(metrics))
+            return super().step(metrics, *a, **k)
+
+    init_snap = {}
+    orig_init = Models.BidShadingContextualBandit.initialise_policy
+
+    def rec_init(self, X, gammas):
+        orig_init(self, X, gammas)
+        init_snap["params"] = [p.detach().numpy().copy() for p in self.parameters()]
+
+    def params(mod):
+        return [p.detach().numpy().copy() for p in mod.parameters()]
+
+    saved = torch.optim.lr_scheduler.ReduceLROnPlateau
+    torch.optim.lr_scheduler.ReduceLROnPlateau = RecRP
+    Models.BidShadingContextualBandit.initialise_policy = rec_init
+    out = {}
+    try:
+        for i, ag in enumerate(agents):
+            b = ag.bidder
+            L = ag.logs
+            est = np.array([o.estimated_CTR for o in L])
+            vals = np.array([o.value for o in L])
+            prices = np.array([o.price for o in L])
+            outc = np.array([o.outcome for o in L])
+            won = np.array([o.won for o in L])
+            k = f"a{i}_"
+            out[k + "est_ctr"], out[k + "value"], out[k + "price"] = est, vals, prices
+            out[k + "outcome"], out[k + "won"] = outc.astype(np.int8), won.astype(np.int8)
+            out[k + "gamma"] = np.array([float(g) for g in b.gammas])
+            out[k + "propensity"] = np.array([float(p) for p in b.propensities])
+            for j, p in enumerate(params(b.winrate_model)):
+                out[k + f"wr0_{j}"] = p
+            for j, p in enumerate(params(b.bidding_policy)):
+                out[k + f"pol0_{j}"] = p
+            # epoch-0 KATs of the win-rate BCE fit and the imitation MSE, on the data the
+            # update builds (src/Bidder.py:500-514, src/Models.py:114-121)
+            X = np.hstack((est.reshape(-1, 1), vals.reshape(-1, 1), out[k + "gamma"].reshape(-1, 1)))
+            Xn = X.copy()
+            Xn[:, -1] = 0.0
+            Xt = torch.Tensor(np.vstack((X, Xn)))
+            y = won.astype(np.uint8).reshape(-1, 1)
+            yt = torch.Tensor(np.concatenate((y, np.zeros_like(y))))
+            wm = copy.deepcopy(b.winrate_model)
+            loss = torch.nn.BCELoss()(wm(Xt), yt)
+            loss.backward()
+            out[k + "wr_loss0"] = np.array(loss.item())
+            for j, p in enumerate(wm.parameters()):
+                out[k + f"wr_grad0_{j}"] = p.grad.numpy().copy()
+            pol = copy.deepcopy(b.bidding_policy)
+            Xc = torch.Tensor(np.hstack((est.reshape(-1, 1), vals.reshape(-1, 1))))
+            gt = torch.Tensor(b.gammas)
+            sp = torch.nn.Softplus()
+            mu = sp(pol.mu_linear_out(sp(pol.shared_linear(Xc))))
+            sg = sp(pol.sigma_linear_out(sp(pol.shared_linear(Xc))))
+            crit = torch.nn.MSELoss()
+            loss = crit(mu.squeeze(), gt) + crit(sg.squeeze(), torch.ones_like(gt) * .05)
+            loss.backward()
+            out[k + "init_loss0"] = np.array(loss.item())
+            for j, p in enumerate(pol.parameters()):
+                out[k + f"init_grad0_{j}"] = p.grad.numpy().copy()
+            recs.clear()
+            init_snap.clear()
+            ag.update(iteration=0)  # LR-TS allocator update, then the DR bidder's
+            # recs: [LR-TS allocator, win-rate fit, DR policy fit]
+            assert len(recs) == 3, len(recs)
+            out[k + "wr_losses"] = np.array(recs[1]["losses"])
+            out[k + "dr_losses"] = np.array(recs[2]["losses"])
+            out[k + "dr_rng_state"] = recs[2]["rng"].numpy()
+            for j, p in enumerate(init_snap["params"]):
+                out[k + f"pol_init_{j}"] = p
+            for j, p in enumerate(params(b.winrate_model)):
+                out[k + f"wr1_{j}"] = p
+            for j, p in enumerate(params(b.bidding_policy)):
+                out[k + f"pol1_{j}"] = p
+            # epoch-0 KAT of the DR loss at its starting point (post-imitation policy, fitted
+            # win-rate model, the RNG state the fit started from)
+            after = torch.get_rng_state()
+            pol = copy.deepcopy(b.bidding_policy)
+            with torch.no_grad():
+                for p, v in zip(pol.parameters(), init_snap["params"]):
+                    p.copy_(torch.from_numpy(v))
+            W = b.winrate_model(torch.Tensor(X)).squeeze().detach().numpy()
+            util = np.zeros_like(vals)
+            util[won] = vals[won] * outc[won] - prices[won]
+            est_u = W * (est * vals - est * vals * out[k + "gamma"])
+            out[k + "util"], out[k + "est_util"] = util, est_u
+            torch.set_rng_state(recs[2]["rng"])
+            loss = pol.loss(Xc, gt, torch.clip(torch.Tensor(b.propensities), min=1e-15), torch.Tensor(util),
+                            utility_estimates=torch.Tensor(est_u), winrate_model=b.winrate_model,
+                            importance_weight_clipping_eps=50.0)
+            loss.backward()
+            out[k + "dr_loss0"] = np.array(loss.item())
+            for j, p in enumerate(pol.parameters()):
+                out[k + f"dr_grad0_{j}"] = p.grad.numpy().copy()
+            torch.set_rng_state(after)
+            print("dr update agent", i, "n", len(L), "wr epochs", len(out[k + "wr_losses"]),
+                  "dr epochs", len(out[k + "dr_losses"]), flush=True)
+    finally:
+        torch.optim.lr_scheduler.ReduceLROnPlateau = saved
+        Models.BidShadingContextualBandit.initialise_policy = orig_init
+    np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
+
+
 def sigmoid_kats():
     """Reference sigmoid (numba-faithful shim) on OracleAllocator-shaped dots."""
     import Models
@@ -504,7 +630,7 @@ def csv_outputs(runs=2, iters=3, rounds=2000):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also run SP_Oracle as shipped (3x20x10k rounds, ~1 min)")
-    ap.add_argument("--only", choices=["empirical", "csv"], help="regenerate one fixture family only")
+    ap.add_argument("--only", choices=["empirical", "csv", "dr"], help="regenerate one fixture family only")
     args = ap.parse_args()
     install_shims()
     if args.only == "empirical":
@@ -512,6 +638,9 @@ def main():
         return
     if args.only == "csv":
         csv_outputs()
+        return
+    if args.only == "dr":
+        dr_update_kat()
         return
 
     sigmoid_kats()
@@ -553,6 +682,8 @@ def main():
     empirical_update_kat()
     # 10. main.py's CSV outputs (SP_Oracle-shaped and EmpiricalShaded, 2 runs x 3 iterations).
     csv_outputs()
+    # 11. DoublyRobustBidder.update KATs (FP_DR_TS.json, iteration 0).
+    dr_update_kat()
 
     if args.full:
         agg = full_run_aggregates("SP_Oracle.json")

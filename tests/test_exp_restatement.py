@@ -4,6 +4,7 @@ double range (the device build is compared with libm in tests/test_gpu_parity.py
 import os
 import subprocess
 
+import numpy as np
 import pytest
 
 from conftest import ROOT
@@ -46,3 +47,22 @@ def test_host_build_of_device_exp_matches_glibc(tmp_path):
                     "-lm"], check=True)
     r = subprocess.run([str(exe), "40000000"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout
+
+
+def test_log1p_restatement_accuracy():
+    """The fdlibm log1p the DR bidder's softplus uses (oracle/ag_oracle_dr.c; the device's
+    csrc/ag_log1p.h is the same algorithm): within 1 ulp of libm over its whole use range."""
+    import math
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    L = O.lib()
+    g = np.random.default_rng(0)
+    xs = np.concatenate([np.exp(g.uniform(-40, 20, 100000)), g.uniform(-0.99, 1, 50000),
+                         [0.0, 1e-300, 1e-20, 0.4142135, -0.29289, 1e300, 2.0 ** -29, 2.0 ** -54]])
+    worst = 0.0
+    for x in xs:
+        a, b = L.ora_log1p_restated(float(x)), math.log1p(x)
+        if a != b:
+            worst = max(worst, abs(a - b) / abs(b))
+    assert worst < 2.3e-16
