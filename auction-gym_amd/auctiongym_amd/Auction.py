@@ -201,7 +201,7 @@ class Auction:
                           for k, v in out.items()}
             eng.simulate(sl_in, sl_out, cnt)
             if self._learner.any():
-                self._collect(sl_in, sl_out, hi - lo)
+                self._collect(sl_in, sl_out, hi - lo, self._logged_rounds + lo)
             if sl_out is not out:
                 for k, v in out.items():
                     v[..., lo:hi].copy_(sl_out[k])
@@ -244,7 +244,7 @@ class Auction:
         self._stores[name] = st
         return st
 
-    def _collect(self, inp, out, B):
+    def _collect(self, inp, out, B, first_auction):
         if self._trained:
             raise NotImplementedError(
                 "rounds were simulated after an update before every learning agent called "
@@ -258,7 +258,7 @@ class Auction:
         if self._empirical.any():
             need = self._bounds["shading"] + B * self.num_participants_per_round
             st = self._grow("shading", need, eng.new_shading_samples)
-            eng.shading_collect(inp, out, st)
+            eng.shading_collect(inp, out, st, first_auction=first_auction)
             self._bounds["shading"] = need
 
     def _train_all(self):

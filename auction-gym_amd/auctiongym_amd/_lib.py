@@ -30,9 +30,10 @@ FX_FRAC_BITS, FX_LIMB_BITS, FX_LIMBS = 36, 42, 3
 EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params", "ag_load_lrts",
            "ag_set_option", "ag_load_catalog", "ag_allocate", "ag_simulate", "ag_generate",
            "ag_generate_noise", "ag_lrts_collect", "ag_lrts_update", "ag_lrts_read",
-           "ag_shading_collect", "ag_empirical_update",
+           "ag_shading_collect", "ag_empirical_update", "ag_set_dr_state", "ag_get_dr_state",
+           "ag_shading_counts", "ag_dr_update",
            "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_last_error", "ag_abi_version")
-ABI_VERSION = 7
+ABI_VERSION = 9
 LRTS_MAX_EPOCHS = 16384
 LRTS_MAX_DO = 8
 
@@ -65,7 +66,9 @@ class AgLrtsSamples(ctypes.Structure):
 
 class AgShadingSamples(ctypes.Structure):
     _fields_ = [("agent", ctypes.c_void_p), ("gamma", ctypes.c_void_p), ("utility", ctypes.c_void_p),
-                ("capacity", ctypes.c_int64), ("count", ctypes.c_void_p)]
+                ("capacity", ctypes.c_int64), ("count", ctypes.c_void_p), ("ctr", ctypes.c_void_p),
+                ("value", ctypes.c_void_p), ("propensity", ctypes.c_void_p), ("won", ctypes.c_void_p),
+                ("order", ctypes.c_void_p)]
 
 
 class AgError(RuntimeError):
@@ -100,9 +103,13 @@ def load(path=None):
                                            ctypes.POINTER(AgBatchOut), ctypes.POINTER(AgLrtsSamples), vp]),
         "ag_lrts_update": (ctypes.c_int, [vp, ctypes.POINTER(AgLrtsSamples), vp, vp, vp]),
         "ag_lrts_read": (ctypes.c_int, [vp, vp, vp, vp]),
-        "ag_shading_collect": (ctypes.c_int, [vp, i64, ctypes.POINTER(AgBatchIn),
+        "ag_shading_collect": (ctypes.c_int, [vp, i64, i64, ctypes.POINTER(AgBatchIn),
                                               ctypes.POINTER(AgBatchOut), ctypes.POINTER(AgShadingSamples), vp]),
         "ag_empirical_update": (ctypes.c_int, [vp, ctypes.POINTER(AgShadingSamples), vp, vp]),
+        "ag_set_dr_state": (ctypes.c_int, [vp, vp, vp]),
+        "ag_get_dr_state": (ctypes.c_int, [vp, vp, vp]),
+        "ag_shading_counts": (ctypes.c_int, [vp, ctypes.POINTER(AgShadingSamples), vp, vp]),
+        "ag_dr_update": (ctypes.c_int, [vp, ctypes.POINTER(AgShadingSamples), vp, vp, i32, vp, vp, vp]),
         "ag_generate_noise": (ctypes.c_int, [vp, u64, u64, i64, vp, vp, vp, vp]),
         "ag_allocate": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, vp]),
         "ag_simulate": (ctypes.c_int, [vp, i64, ctypes.POINTER(AgBatchIn),

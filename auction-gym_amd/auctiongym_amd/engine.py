@@ -265,27 +265,69 @@ class AuctionEngine:
         return w, p, s
 
     # ---------------------------------------------------------------- shading update
-    def new_shading_samples(self, capacity):
-        """Device store of shading-bidder records (ag_shading_samples)."""
+    def new_shading_samples(self, capacity, learning=False):
+        """Device store of shading-bidder records (ag_shading_samples); learning=True adds
+        the fields the DoublyRobustBidder update needs (ctr, value, propensity, won)."""
         d = self.device
-        return {"agent": torch.empty((capacity,), dtype=torch.int32, device=d),
-                "gamma": torch.empty((capacity,), dtype=torch.float64, device=d),
-                "utility": torch.empty((capacity,), dtype=torch.float64, device=d),
-                "count": torch.zeros((1,), dtype=torch.int64, device=d)}
+        st = {"agent": torch.empty((capacity,), dtype=torch.int32, device=d),
+              "gamma": torch.empty((capacity,), dtype=torch.float64, device=d),
+              "utility": torch.empty((capacity,), dtype=torch.float64, device=d),
+              "count": torch.zeros((1,), dtype=torch.int64, device=d)}
+        if learning:
+            for k in ("ctr", "value", "propensity"):
+                st[k] = torch.empty((capacity,), dtype=torch.float64, device=d)
+            st["won"] = torch.empty((capacity,), dtype=torch.uint8, device=d)
+            st["order"] = torch.empty((capacity,), dtype=torch.int64, device=d)  # uint64 bits
+        return st
 
     @staticmethod
     def _shading(st):
         return AgShadingSamples(_ptr(st["agent"]).value, _ptr(st["gamma"]).value,
-                                _ptr(st["utility"]).value, st["agent"].shape[0], _ptr(st["count"]).value)
+                                _ptr(st["utility"]).value, st["agent"].shape[0], _ptr(st["count"]).value,
+                                _ptr(st.get("ctr")).value, _ptr(st.get("value")).value,
+                                _ptr(st.get("propensity")).value, _ptr(st.get("won")).value,
+                                _ptr(st.get("order")).value)
 
-    def shading_collect(self, inputs, outputs, store):
-        """Append the shading-bidder records of a simulated batch (ag_shading_collect)."""
+    def shading_counts(self, store):
+        """Records per agent in a shading store (ag_shading_counts)."""
+        c = np.zeros(self.N, np.int64)
+        self._check(self.L.ag_shading_counts(self._h, ctypes.byref(self._shading(store)), c.ctypes.data,
+                                             _stream()), "ag_shading_counts")
+        return c
+
+    def set_dr_state(self, state, initialised):
+        """DoublyRobustBidder models, float32 [N][16] (win-rate w0 w1 w2 b, policy 12)."""
+        st = np.ascontiguousarray(state, np.float32).reshape(self.N, 16)
+        ini = np.ascontiguousarray(initialised, np.int32).reshape(self.N)
+        self._check(self.L.ag_set_dr_state(self._h, st.ctypes.data, ini.ctypes.data), "ag_set_dr_state")
+
+    def dr_state(self):
+        st = np.zeros((self.N, 16), np.float32)
+        ini = np.zeros(self.N, np.int32)
+        self._check(self.L.ag_get_dr_state(self._h, st.ctypes.data, ini.ctypes.data), "ag_get_dr_state")
+        return st, ini
+
+    def dr_update(self, store, noise, noise_offsets, noise_epochs, trace=False):
+        """DoublyRobustBidder.update of every DR agent (ag_dr_update). noise: float32 device
+        tensor holding agent a's per-epoch rsample draws at noise_offsets[a] (rows of its
+        record count). Returns epochs [N][3] (and traces [N][3][32768] with trace=True)."""
+        ep = np.zeros((self.N, 3), np.int32)
+        off = np.ascontiguousarray(noise_offsets, np.int64)
+        tr = torch.zeros((self.N, 3, 32768), dtype=torch.float32, device=self.device) if trace else None
+        self._check(self.L.ag_dr_update(self._h, ctypes.byref(self._shading(store)), _ptr(noise),
+                                        off.ctypes.data, int(noise_epochs), ep.ctypes.data, _ptr(tr),
+                                        _stream()), "ag_dr_update")
+        return (ep, tr) if trace else ep
+
+    def shading_collect(self, inputs, outputs, store, first_auction=0):
+        """Append the shading-bidder records of a simulated batch of auctions
+        [first_auction, first_auction + B) (ag_shading_collect)."""
         B = inputs["u"].shape[0]
         bi = AgBatchIn(_ptr(inputs["ctx"]).value, _ptr(inputs["part"]).value, _ptr(inputs["u"]).value,
                        _ptr(inputs.get("gamma_raw")).value, _ptr(inputs.get("ts_noise")).value)
         bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
         st = self._shading(store)
-        self._check(self.L.ag_shading_collect(self._h, B, ctypes.byref(bi), ctypes.byref(bo),
+        self._check(self.L.ag_shading_collect(self._h, int(first_auction), B, ctypes.byref(bi), ctypes.byref(bo),
                                               ctypes.byref(st), _stream()), "ag_shading_collect")
 
     def empirical_update(self, store):

@@ -1,0 +1,594 @@
+// ag_dr.hip -- DoublyRobustBidder.update on the GPU (Agent.update -> src/Bidder.py:473-615,
+// models src/Models.py:51-62, :92-218).
+//
+// One workgroup per DR agent, persistent over the three fits the reference runs one after
+// the other: the win-rate model (BCE on the logs + the gamma = 0 augmentation, <= 32768
+// epochs), the policy's imitation of the logging policy (first update only, <= 16384) and
+// the doubly robust policy fit (<= 32768, rsample noise per epoch supplied by the caller).
+// Everything a fit needs per epoch (Adam with weight decay + AMSGrad, ReduceLROnPlateau,
+// the reference's early stop) runs on the device. Sums over the agent's records are exact
+// (fixed-point terms added as integers), so the result is independent of record order and
+// lane assignment; the arithmetic is oracle/ag_oracle_dr.c ora_dr_update, bit for bit.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include <hipcub/hipcub.hpp>
+
+#include "ag_exp.h"
+#include "ag_exp_table.h"
+#include "ag_host.h"
+#include "ag_log1p.h"
+
+namespace {
+
+constexpr int kDrThreads = 256;
+constexpr int kWrEpochs = 32768, kInitEpochs = 16384, kDrEpochs = 32768;
+constexpr double kGrid = 0x1p40, kInv = 0x1p-40;
+constexpr int64_t kLo24 = (int64_t(1) << 24) - 1;
+
+__device__ __forceinline__ int64_t fxr(double v) { return (int64_t)__builtin_rint(v * kGrid); }
+
+__device__ __forceinline__ double fxv(int64_t hi, int64_t lo) {
+  hi += lo >> 24;
+  lo &= kLo24;
+  return ((double)hi * 0x1p24 + (double)lo) * kInv;
+}
+
+__device__ __forceinline__ double softplus(double u, const uint64_t *tab) {
+  return u > 20.0 ? u : aglog1p::log1p(agexp::exp(u, tab));
+}
+__device__ __forceinline__ double dsoftplus(double u, const uint64_t *tab) {
+  if (u > 20.0) return 1.0;
+  const double e = agexp::exp(u, tab);
+  return e / (e + 1.0);
+}
+
+// Exact block sum of NV per-lane int64 accumulators (each split at bit 24 so nothing can
+// overflow): every thread gets the totals as (hi, lo) pairs in s_out.
+template <int NV>
+__device__ __forceinline__ void block_sums(const int64_t (&v)[NV], int64_t (*s_w)[32], int64_t *s_out) {
+  static_assert(2 * NV <= 32, "block_sums: at most 16 sums");
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    int64_t h = v[j] >> 24, l = v[j] & kLo24;
+    for (int o = 32; o > 0; o >>= 1) {
+      h += __shfl_xor(h, o, 64);
+      l += __shfl_xor(l, o, 64);
+    }
+    if (lane == 0) {
+      s_w[wv][2 * j] = h;
+      s_w[wv][2 * j + 1] = l;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * NV) {
+    int64_t t = 0;
+    for (int w = 0; w < kDrThreads / 64; ++w) t += s_w[w][threadIdx.x];
+    s_out[threadIdx.x] = t;
+  }
+  __syncthreads();
+}
+
+// torch.optim.Adam single-tensor step with weight decay and AMSGrad (thread j: param j)
+struct AdamState {
+  float ea[16], es[16], mx[16];
+};
+
+__device__ __forceinline__ void adam_param(float &p, float grad, int j, AdamState &a, float neg_step, float bc2f,
+                                           float wdf) {
+  const float g = grad + wdf * p;
+  a.ea[j] = a.ea[j] + 0.1f * (g - a.ea[j]);
+  a.es[j] = a.es[j] * 0.999f + (0.001f * g) * g;
+  a.mx[j] = a.mx[j] > a.es[j] ? a.mx[j] : a.es[j];
+  // float32 sqrt correctly rounded (as the CPU's sqrtss): via the refined FP64 sqrt
+  const float den = (float)__builtin_sqrt((double)a.mx[j]) / bc2f + 1e-8f;
+  p = p + neg_step * (a.ea[j] / den);
+}
+
+struct Plateau {
+  double best, threshold, factor, min_lr;
+  int bad, patience;
+};
+__device__ __forceinline__ void plateau_step(Plateau &s, float loss, double &lr) {
+  if ((double)loss < s.best * (1.0 - s.threshold)) {
+    s.best = (double)loss;
+    s.bad = 0;
+  } else {
+    s.bad += 1;
+  }
+  if (s.bad > s.patience) {
+    double nl = lr * s.factor;
+    if (nl < s.min_lr) nl = s.min_lr;
+    if (lr - nl > 1e-8) lr = nl;
+    s.bad = 0;
+  }
+}
+struct Stopper {
+  double best;
+  int best_epoch, wait;
+};
+__device__ __forceinline__ bool stop_step(Stopper &s, int epoch, float loss) {
+  if (s.best - (double)loss > 1e-6) {
+    s.best_epoch = epoch;
+    s.best = (double)loss;
+    return false;
+  }
+  return epoch - s.best_epoch > s.wait;
+}
+
+struct PolF {
+  double h[2], s[2], am, as, mu, sp_sigma, sigma;
+};
+__device__ __forceinline__ void policy_fwd(const float *p, double c, double v, PolF &f, const uint64_t *tab) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    f.h[j] = c * (double)p[2 * j] + v * (double)p[2 * j + 1] + (double)p[4 + j];
+    f.s[j] = softplus(f.h[j], tab);
+  }
+  f.am = f.s[0] * (double)p[6] + f.s[1] * (double)p[7] + (double)p[8];
+  f.as = f.s[0] * (double)p[9] + f.s[1] * (double)p[10] + (double)p[11];
+  f.mu = softplus(f.am, tab);
+  f.sp_sigma = softplus(f.as, tab);
+  f.sigma = f.sp_sigma + 0.01;  // min_sigma (src/Models.py:104)
+}
+__device__ __forceinline__ void policy_bwd(const float *p, double c, double v, const PolF &f, double dmu,
+                                           double dsigma, int64_t (&G)[16], int off, const uint64_t *tab) {
+  const double dam = dmu * dsoftplus(f.am, tab), das = dsigma * dsoftplus(f.as, tab);
+  double ds[2];
+  ds[0] = dam * (double)p[6] + das * (double)p[9];
+  ds[1] = dam * (double)p[7] + das * (double)p[10];
+  G[off + 6] += fxr(dam * f.s[0]);
+  G[off + 7] += fxr(dam * f.s[1]);
+  G[off + 8] += fxr(dam);
+  G[off + 9] += fxr(das * f.s[0]);
+  G[off + 10] += fxr(das * f.s[1]);
+  G[off + 11] += fxr(das);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const double dh = ds[j] * dsoftplus(f.h[j], tab);
+    G[off + 2 * j] += fxr(dh * c);
+    G[off + 2 * j + 1] += fxr(dh * v);
+    G[off + 4 + j] += fxr(dh);
+  }
+}
+
+__device__ __forceinline__ void bias_corrections(int step, const double *adam_tab, float &bc2f, double &bc1) {
+  // adam_tab: [0, kDrEpochs): 1 - 0.9^t; [kDrEpochs, 2 kDrEpochs): (1 - 0.999^t)^0.5 (libm pow)
+  bc1 = adam_tab[step];
+  bc2f = (float)adam_tab[kDrEpochs + step];
+}
+
+// records of agent a: SoA, bucketed: ctr, value, gamma, prop, util (f64), won (u8)
+struct DrRecords {
+  const double *ctr, *value, *gamma, *prop, *util;
+  const uint8_t *won;
+};
+
+__global__ __launch_bounds__(kDrThreads) void k_dr_train(
+    const int32_t *__restrict__ bkind, const int64_t *__restrict__ offsets, DrRecords R,
+    double *__restrict__ eu_ws, float *__restrict__ state, const int32_t *__restrict__ initialised,
+    const float *__restrict__ noise, const int64_t *__restrict__ noise_off, int noise_epochs,
+    const double *__restrict__ adam_tab, int32_t *__restrict__ epochs_out, int32_t *__restrict__ status,
+    float *__restrict__ traces) {
+  const int a = blockIdx.x, tid = threadIdx.x;
+  const int64_t s0 = offsets[a], n = offsets[a + 1] - s0;
+  if (bkind[a] != AG_BIDDER_DOUBLY_ROBUST || n == 0) {
+    if (tid == 0) {
+      epochs_out[3 * a] = epochs_out[3 * a + 1] = epochs_out[3 * a + 2] = 0;
+      status[a] = (bkind[a] == AG_BIDDER_DOUBLY_ROBUST) ? -1 : 0;
+    }
+    return;
+  }
+  __shared__ uint64_t s_tab[256];
+  __shared__ float s_wr[4], s_pol[12];
+  __shared__ int64_t s_w[kDrThreads / 64][32];
+  __shared__ int64_t s_tot[32];
+  __shared__ AdamState s_adam;
+  __shared__ int s_stop;
+  for (int i = tid; i < 256; i += kDrThreads) s_tab[i] = ag_exp_tab[i];
+  float *st = state + (size_t)a * 16;
+  if (tid < 4) s_wr[tid] = st[tid];
+  if (tid < 12) s_pol[tid] = st[4 + tid];
+  if (tid < 16) s_adam.ea[tid] = s_adam.es[tid] = s_adam.mx[tid] = 0.0f;
+  if (tid == 0) s_stop = 0;
+  __syncthreads();
+  const double *ctr = R.ctr + s0, *val = R.value + s0, *gam = R.gamma + s0, *prop = R.prop + s0,
+               *util = R.util + s0;
+  const uint8_t *won = R.won + s0;
+  double *eu = eu_ws + s0;
+  float *tr = traces ? traces + (size_t)a * 3 * kDrEpochs : nullptr;
+
+  // ---------------- 1. win-rate fit
+  {
+    double lr = 3e-3;
+    Plateau pl{INFINITY, 1e-4, 0.2, 1e-7, 0, 256};
+    Stopper sp{INFINITY, -1, 1024};
+    const double M = 2.0 * (double)n;
+    int e = 0;
+    for (; e < kWrEpochs; ++e) {
+      int64_t acc[5] = {0, 0, 0, 0, 0};
+      for (int64_t r = tid; r < 2 * n; r += kDrThreads) {
+        const int64_t i = r < n ? r : r - n;
+        const double c = (double)(float)ctr[i], v = (double)(float)val[i];
+        const double g = r < n ? (double)(float)gam[i] : 0.0;
+        const double y = r < n ? (double)won[i] : 0.0;
+        const double z = c * (double)s_wr[0] + v * (double)s_wr[1] + g * (double)s_wr[2] + (double)s_wr[3];
+        const double pw = 1.0 / (1.0 + agexp::exp(-z, s_tab));
+        const double t = y > 0.0 ? fmin(softplus(-z, s_tab), 100.0) : fmin(softplus(z, s_tab), 100.0);
+        acc[0] += fxr(t);
+        const double gz = pw - y;
+        acc[1] += fxr(gz * c);
+        acc[2] += fxr(gz * v);
+        acc[3] += fxr(gz * g);
+        acc[4] += fxr(gz);
+      }
+      block_sums<5>(acc, s_w, s_tot);
+      // every thread: the same loss; threads 0..3 step their parameter
+      const float loss = (float)(fxv(s_tot[0], s_tot[1]) / M);
+      double bc1;
+      float bc2f;
+      bias_corrections(e, adam_tab, bc2f, bc1);
+      const float neg_step = (float)(-(lr / bc1));
+      if (tid < 4) {
+        const float g = (float)(fxv(s_tot[2 + 2 * tid], s_tot[3 + 2 * tid]) / M);
+        float p = s_wr[tid];
+        adam_param(p, g, tid, s_adam, neg_step, bc2f, (float)1e-6);
+        s_wr[tid] = p;
+      }
+      if (tid == 0 && tr) tr[e] = loss;
+      plateau_step(pl, loss, lr);  // every thread keeps the same scheduler state
+      const bool stop = stop_step(sp, e, loss);
+      __syncthreads();
+      if (stop) {
+        ++e;
+        break;
+      }
+    }
+    if (tid == 0) epochs_out[3 * a] = e;
+  }
+  // ---------------- 2. estimated utilities with the fitted model
+  for (int64_t i = tid; i < n; i += kDrThreads) {
+    const double c = (double)(float)ctr[i], v = (double)(float)val[i], g = (double)(float)gam[i];
+    const double z = c * (double)s_wr[0] + v * (double)s_wr[1] + g * (double)s_wr[2] + (double)s_wr[3];
+    const float W = (float)(1.0 / (1.0 + agexp::exp(-z, s_tab)));
+    const double V = ctr[i] * val[i], P = ctr[i] * val[i] * gam[i];
+    eu[i] = (double)W * (V - P);
+  }
+  // ---------------- 3. imitation of the logging policy (first update)
+  if (tid == 0) epochs_out[3 * a + 1] = 0;
+  if (!initialised[a]) {
+    if (tid < 16) s_adam.ea[tid] = s_adam.es[tid] = s_adam.mx[tid] = 0.0f;
+    __syncthreads();
+    Stopper sp{INFINITY, -1, 512};
+    int e = 0;
+    for (; e < kInitEpochs; ++e) {
+      int64_t acc[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[j] = 0;
+      for (int64_t i = tid; i < n; i += kDrThreads) {
+        const double c = (double)(float)ctr[i], v = (double)(float)val[i];
+        PolF f;
+        policy_fwd(s_pol, c, v, f, s_tab);
+        const double dm = f.mu - (double)(float)gam[i], dsg = f.sp_sigma - 0.05;
+        acc[12] += fxr(dm * dm);
+        acc[13] += fxr(dsg * dsg);
+        policy_bwd(s_pol, c, v, f, 2.0 * dm, 2.0 * dsg, acc, 0, s_tab);
+      }
+      block_sums<16>(acc, s_w, s_tot);
+      const float loss = (float)(fxv(s_tot[24], s_tot[25]) / (double)n + fxv(s_tot[26], s_tot[27]) / (double)n);
+      double bc1;
+      float bc2f;
+      bias_corrections(e, adam_tab, bc2f, bc1);
+      const float neg_step = (float)(-(1e-3 / bc1));
+      if (tid < 12) {
+        const float g = (float)(fxv(s_tot[2 * tid], s_tot[2 * tid + 1]) / (double)n);
+        float p = s_pol[tid];
+        adam_param(p, g, tid, s_adam, neg_step, bc2f, (float)1e-4);
+        s_pol[tid] = p;
+      }
+      if (tid == 0 && tr) tr[kDrEpochs + e] = loss;
+      const bool stop = stop_step(sp, e, loss);
+      __syncthreads();
+      if (stop) {
+        ++e;
+        break;
+      }
+    }
+    if (tid == 0) epochs_out[3 * a + 1] = e;
+  }
+  // ---------------- 4. doubly robust policy fit
+  {
+    if (tid < 16) s_adam.ea[tid] = s_adam.es[tid] = s_adam.mx[tid] = 0.0f;
+    __syncthreads();
+    double lr = 7e-3;
+    Plateau pl{INFINITY, 5e-3, 0.2, 1e-8, 0, 100};
+    Stopper sp{INFINITY, -1, 512};
+    const double inv_sqrt2pi = 1.0 / __builtin_sqrt(2.0 * 3.141592653589793);
+    const float *nz = noise + noise_off[a];
+    int e = 0;
+    for (; e < kDrEpochs && e < noise_epochs; ++e) {
+      const float *eps = nz + (int64_t)e * n;
+      int64_t acc[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[j] = 0;
+      for (int64_t i = tid; i < n; i += kDrThreads) {
+        const double c = (double)(float)ctr[i], v = (double)(float)val[i], g = (double)(float)gam[i];
+        PolF f;
+        policy_fwd(s_pol, c, v, f, s_tab);
+        const double mu = f.mu, sg = f.sigma;
+        const double zz = (mu - g) / sg;
+        const double pdf_raw = agexp::exp(-(zz * zz) / 2.0, s_tab) / sg * inv_sqrt2pi;
+        const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
+        const double p0 = (double)fmaxf((float)prop[i], 1e-15f);
+        const double iw = pi / p0;
+        const double iwc = iw < 1.0 / 50.0 ? 1.0 / 50.0 : (iw > 50.0 ? 50.0 : iw);
+        const double du = (double)(float)util[i] - (double)(float)eu[i];
+        const double ep = (double)eps[i];
+        const double raw = mu + sg * ep;
+        const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
+        const double zw = c * (double)s_wr[0] + v * (double)s_wr[1] + gs * (double)s_wr[2] + (double)s_wr[3];
+        const double Wv = 1.0 / (1.0 + agexp::exp(-zw, s_tab));
+        const double V = c * v;
+        acc[12] += fxr(-(du * iwc + Wv * (V - V * gs)));
+        double dpi_dmu = 0.0, dpi_dsg = 0.0;
+        if (pdf_raw >= 1e-30 && iw >= 1.0 / 50.0 && iw <= 50.0) {
+          const double k = du / p0;
+          dpi_dmu = k * pdf_raw * (g - mu) / (sg * sg);
+          dpi_dsg = k * pdf_raw * ((g - mu) * (g - mu) / (sg * sg * sg) - 1.0 / sg);
+        }
+        double ddm = 0.0;
+        if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)s_wr[2];
+        policy_bwd(s_pol, c, v, f, -(dpi_dmu + ddm), -(dpi_dsg + ddm * ep), acc, 0, s_tab);
+      }
+      block_sums<16>(acc, s_w, s_tot);
+      const float loss = (float)(fxv(s_tot[24], s_tot[25]) / (double)n);
+      double bc1;
+      float bc2f;
+      bias_corrections(e, adam_tab, bc2f, bc1);
+      const float neg_step = (float)(-(lr / bc1));
+      if (tid < 12) {
+        const float g = (float)(fxv(s_tot[2 * tid], s_tot[2 * tid + 1]) / (double)n);
+        float p = s_pol[tid];
+        adam_param(p, g, tid, s_adam, neg_step, bc2f, (float)1e-4);
+        s_pol[tid] = p;
+      }
+      if (tid == 0 && tr) tr[2 * kDrEpochs + e] = loss;
+      plateau_step(pl, loss, lr);
+      const bool stop = stop_step(sp, e, loss);
+      if (tid == 0 && loss != loss) s_stop = 1;  // NaN: the reference exits (src/Bidder.py:592-600)
+      __syncthreads();
+      if (stop || s_stop) {
+        ++e;
+        break;
+      }
+    }
+    if (tid == 0) {
+      epochs_out[3 * a + 2] = e;
+      status[a] = s_stop ? -2 : 0;
+    }
+  }
+  __syncthreads();
+  if (tid < 4) st[tid] = s_wr[tid];
+  if (tid < 12) st[4 + tid] = s_pol[tid];
+}
+
+// bucket the shading store by agent: histogram, scan, scatter of every record field
+__global__ __launch_bounds__(kDrThreads) void k_sh_hist(const int32_t *__restrict__ agent, int64_t n, int N,
+                                                        int64_t *__restrict__ counts) {
+  extern __shared__ unsigned int s_hist[];
+  for (int a = threadIdx.x; a < N; a += kDrThreads) s_hist[a] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * kDrThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kDrThreads)
+    atomicAdd(&s_hist[agent[i]], 1u);
+  __syncthreads();
+  for (int a = threadIdx.x; a < N; a += kDrThreads)
+    if (s_hist[a]) atomicAdd((unsigned long long *)&counts[a], (unsigned long long)s_hist[a]);
+}
+
+// records in (agent, log order): sort keys agent << 40 | order, gather every field
+__global__ __launch_bounds__(kDrThreads) void k_sh_keys(ag_shading_samples s, int64_t n, uint64_t *__restrict__ key,
+                                                        uint32_t *__restrict__ idx) {
+  for (int64_t i = (int64_t)blockIdx.x * kDrThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kDrThreads) {
+    key[i] = ((uint64_t)(uint32_t)s.agent[i] << 40) | (s.order[i] & ((1ull << 40) - 1));
+    idx[i] = (uint32_t)i;
+  }
+}
+
+__global__ __launch_bounds__(kDrThreads) void k_sh_gather(ag_shading_samples s, int64_t n,
+                                                          const uint32_t *__restrict__ idx,
+                                                          double *__restrict__ o_ctr, double *__restrict__ o_val,
+                                                          double *__restrict__ o_gam, double *__restrict__ o_prop,
+                                                          double *__restrict__ o_util, uint8_t *__restrict__ o_won) {
+  for (int64_t j = (int64_t)blockIdx.x * kDrThreads + threadIdx.x; j < n; j += (int64_t)gridDim.x * kDrThreads) {
+    const uint32_t i = idx[j];
+    o_ctr[j] = s.ctr[i];
+    o_val[j] = s.value[i];
+    o_gam[j] = s.gamma[i];
+    o_prop[j] = s.propensity[i];
+    o_util[j] = s.utility[i];
+    o_won[j] = s.won[i];
+  }
+}
+
+int grid_over(int64_t n) {
+  int64_t g = (n + kDrThreads - 1) / kDrThreads;
+  if (g > 4096) g = 4096;
+  return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace
+
+void ag_dr_release(ag_ctx *c) {
+  ag_dr_ws &w = c->dr;
+  (void)hipFree(w.buf);
+  (void)hipFree(w.counts);
+  (void)hipFree(w.adam_tab);
+  (void)hipFree(w.state);
+  (void)hipFree(w.init);
+  (void)hipFree(w.scratch);
+  w = ag_dr_ws();
+}
+
+// workspace: counts / offsets / cursors, the Adam bias-correction table, the DR state
+static int dr_ws_ready(ag_ctx *c) {
+  ag_dr_ws &w = c->dr;
+  if (w.adam_tab) return AG_OK;
+  const int N = c->shape.num_agents;
+  double *tab = new double[2 * kDrEpochs];
+  for (int t = 0; t < kDrEpochs; ++t) {  // torch.optim.Adam: Python floats, libm pow
+    tab[t] = 1.0 - pow(0.9, (double)(t + 1));
+    tab[kDrEpochs + t] = pow(1.0 - pow(0.999, (double)(t + 1)), 0.5);
+  }
+  hipError_t e = hipMalloc(&w.adam_tab, sizeof(double) * 2 * kDrEpochs);
+  if (e == hipSuccess) e = hipMemcpy(w.adam_tab, tab, sizeof(double) * 2 * kDrEpochs, hipMemcpyHostToDevice);
+  delete[] tab;
+  if (e == hipSuccess) e = hipMalloc(&w.counts, sizeof(int64_t) * (3 * (size_t)N + 1));
+  if (e == hipSuccess) e = hipMalloc(&w.state, sizeof(float) * 16 * (size_t)N);
+  if (e == hipSuccess) e = hipMemset(w.state, 0, sizeof(float) * 16 * (size_t)N);
+  if (e == hipSuccess) e = hipMalloc(&w.init, sizeof(int32_t) * (size_t)N);
+  if (e == hipSuccess) e = hipMemset(w.init, 0, sizeof(int32_t) * (size_t)N);
+  if (e == hipSuccess) e = hipMalloc(&w.scratch, sizeof(int64_t) * (size_t)N + sizeof(int32_t) * 4 * (size_t)N);
+  if (e != hipSuccess) {
+    ag_dr_release(c);
+    return ag_set_error(AG_ERR_HIP, "DR workspace: %s", hipGetErrorString(e));
+  }
+  return AG_OK;
+}
+
+extern "C" {
+
+int ag_set_dr_state(ag_ctx *c, const float *state, const int32_t *initialised) {
+  if (!c || !state || !initialised) return ag_set_error(AG_ERR_INVALID, "ag_set_dr_state: null argument");
+  AgDeviceGuard g(c->device);
+  if (int rc = dr_ws_ready(c)) return rc;
+  const int N = c->shape.num_agents;
+  AG_HIP(hipMemcpy(c->dr.state, state, sizeof(float) * 16 * N, hipMemcpyHostToDevice));
+  AG_HIP(hipMemcpy(c->dr.init, initialised, sizeof(int32_t) * N, hipMemcpyHostToDevice));
+  c->dr_loaded = true;
+  return AG_OK;
+}
+
+int ag_get_dr_state(ag_ctx *c, float *state, int32_t *initialised) {
+  if (!c) return ag_set_error(AG_ERR_INVALID, "ag_get_dr_state: null ctx");
+  AgDeviceGuard g(c->device);
+  if (int rc = dr_ws_ready(c)) return rc;
+  const int N = c->shape.num_agents;
+  AG_HIP(hipDeviceSynchronize());
+  if (state) AG_HIP(hipMemcpy(state, c->dr.state, sizeof(float) * 16 * N, hipMemcpyDeviceToHost));
+  if (initialised) AG_HIP(hipMemcpy(initialised, c->dr.init, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
+  return AG_OK;
+}
+
+int ag_shading_counts(ag_ctx *c, const ag_shading_samples *s, int64_t *counts, void *stream) {
+  if (!c || !s || !counts) return ag_set_error(AG_ERR_INVALID, "ag_shading_counts: null argument");
+  AgDeviceGuard g(c->device);
+  if (int rc = dr_ws_ready(c)) return rc;
+  const int N = c->shape.num_agents;
+  hipStream_t st = (hipStream_t)stream;
+  uint64_t n = 0;
+  AG_HIP(hipMemcpyAsync(&n, s->count, sizeof n, hipMemcpyDeviceToHost, st));
+  AG_HIP(hipStreamSynchronize(st));
+  if ((int64_t)n > s->capacity)
+    return ag_set_error(AG_ERR_INVALID, "ag_shading_counts: %llu records overflowed the store (capacity %lld)",
+                        (unsigned long long)n, (long long)s->capacity);
+  int64_t *d_counts = c->dr.counts;
+  AG_HIP(hipMemsetAsync(d_counts, 0, sizeof(int64_t) * N, st));
+  if (n > 0) {
+    if ((size_t)N * 4 > 64 * 1024) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_shading_counts: N > 16384");
+    hipLaunchKernelGGL(k_sh_hist, dim3(grid_over((int64_t)n)), dim3(kDrThreads), (size_t)N * 4, st, s->agent,
+                       (int64_t)n, N, d_counts);
+    AG_HIP(hipGetLastError());
+  }
+  AG_HIP(hipMemcpyAsync(counts, d_counts, sizeof(int64_t) * N, hipMemcpyDeviceToHost, st));
+  AG_HIP(hipStreamSynchronize(st));
+  return AG_OK;
+}
+
+int ag_dr_update(ag_ctx *c, const ag_shading_samples *s, const float *noise, const int64_t *noise_offsets,
+                 int32_t noise_epochs, int32_t *epochs, float *traces, void *stream) {
+  if (!c || !s || !noise_offsets || (!noise && noise_epochs > 0))
+    return ag_set_error(AG_ERR_INVALID, "ag_dr_update: null argument");
+  if (!s->ctr || !s->value || !s->propensity || !s->won || !s->order)
+    return ag_set_error(AG_ERR_INVALID, "ag_dr_update: the store needs ctr, value, propensity, won, order");
+  if (!c->dr_loaded) return ag_set_error(AG_ERR_STATE, "ag_dr_update: ag_set_dr_state not called");
+  AgDeviceGuard g(c->device);
+  const int N = c->shape.num_agents;
+  hipStream_t st = (hipStream_t)stream;
+  std::vector<int64_t> cnt(N);
+  if (int rc = ag_shading_counts(c, s, cnt.data(), stream)) return rc;
+  int64_t n = 0;
+  for (int a = 0; a < N; ++a) n += cnt[a];
+  ag_dr_ws &w = c->dr;
+  // offsets (exclusive scan, host)
+  std::vector<int64_t> off((size_t)N + 1);
+  off[0] = 0;
+  for (int a = 0; a < N; ++a) off[a + 1] = off[a] + cnt[a];
+  int64_t *d_off = w.counts + N;  // [N + 1] offsets
+  AG_HIP(hipMemcpyAsync(d_off, off.data(), sizeof(int64_t) * ((size_t)N + 1), hipMemcpyHostToDevice, st));
+  if (n >= ((int64_t)1 << 32)) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_dr_update: >= 2^32 records");
+  // radix-sort workspace: keys in/out (8 B), indices in/out (4 B), then hipcub's temp
+  size_t sort_tmp = 0;
+  AG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint64_t *)nullptr, (uint64_t *)nullptr,
+                                            (uint32_t *)nullptr, (uint32_t *)nullptr, (int)(n > 0 ? n : 1), 0, 64,
+                                            st));
+  const size_t rec_bytes = (size_t)6 * sizeof(double) + 1;
+  const size_t need = (size_t)(n > 0 ? n : 1) * (rec_bytes + 24) + sort_tmp + 256;
+  if (need > w.buf_bytes) {
+    (void)hipFree(w.buf);
+    w.buf = nullptr;
+    const size_t bytes = need + (need >> 2);
+    AG_HIP(hipMalloc(&w.buf, bytes));
+    w.buf_bytes = bytes;
+  }
+  const size_t cap = (size_t)(n > 0 ? n : 1);
+  double *b_ctr = (double *)w.buf, *b_val = b_ctr + cap, *b_gam = b_val + cap, *b_prop = b_gam + cap,
+         *b_util = b_prop + cap, *b_eu = b_util + cap;
+  uint64_t *k_in = (uint64_t *)(b_eu + cap), *k_out = k_in + cap;
+  uint32_t *i_in = (uint32_t *)(k_out + cap), *i_out = i_in + cap;
+  uint8_t *b_won = (uint8_t *)(i_out + cap);
+  void *tmp = (void *)(((uintptr_t)(b_won + cap) + 255) & ~(uintptr_t)255);
+  if (n > 0) {
+    if (!s->order) return ag_set_error(AG_ERR_INVALID, "ag_dr_update: the store needs order");
+    hipLaunchKernelGGL(k_sh_keys, dim3(grid_over(n)), dim3(kDrThreads), 0, st, *s, n, k_in, i_in);
+    AG_HIP(hipGetLastError());
+    int end_bit = 40;
+    while ((1ll << (end_bit - 40)) < N) ++end_bit;
+    AG_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, sort_tmp, k_in, k_out, i_in, i_out, (int)n, 0, end_bit, st));
+    hipLaunchKernelGGL(k_sh_gather, dim3(grid_over(n)), dim3(kDrThreads), 0, st, *s, n, i_out, b_ctr, b_val, b_gam,
+                       b_prop, b_util, b_won);
+    AG_HIP(hipGetLastError());
+  }
+  int64_t *d_noff = w.scratch;                       // [N] noise offsets
+  int32_t *d_epochs = (int32_t *)(w.scratch + N);     // [N][3] epochs, then [N] status
+  int32_t *d_stat = d_epochs + 3 * (size_t)N;
+  AG_HIP(hipMemcpyAsync(d_noff, noise_offsets, sizeof(int64_t) * N, hipMemcpyHostToDevice, st));
+  DrRecords R{b_ctr, b_val, b_gam, b_prop, b_util, b_won};
+  hipLaunchKernelGGL(k_dr_train, dim3(N), dim3(kDrThreads), 0, st, c->d_bkind, d_off, R, b_eu, w.state, w.init,
+                     noise, d_noff, noise_epochs, w.adam_tab, d_epochs, d_stat, traces);
+  AG_HIP(hipGetLastError());
+  std::vector<int32_t> h(4 * (size_t)N);
+  AG_HIP(hipMemcpyAsync(h.data(), d_epochs, sizeof(int32_t) * 4 * N, hipMemcpyDeviceToHost, st));
+  AG_HIP(hipStreamSynchronize(st));
+  if (epochs) memcpy(epochs, h.data(), sizeof(int32_t) * 3 * N);
+  for (int a = 0; a < N; ++a) {
+    if (h[3 * N + a] == -1)
+      return ag_set_error(AG_ERR_INVALID, "agent %d: DoublyRobustBidder.update without logs", a);
+    if (h[3 * N + a] == -2)
+      return ag_set_error(AG_ERR_INVALID, "agent %d: NAN DETECTED! in losses (src/Bidder.py:592)", a);
+  }
+  // the fitted policies bid from now on (src/Bidder.py:612-613)
+  std::vector<int32_t> init(N);
+  AG_HIP(hipMemcpy(init.data(), w.init, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
+  for (int a = 0; a < N; ++a)
+    if (c->h_bkind[a] == AG_BIDDER_DOUBLY_ROBUST) init[a] = 1;
+  AG_HIP(hipMemcpy(w.init, init.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice));
+  return AG_OK;
+}
+
+}  // extern "C"

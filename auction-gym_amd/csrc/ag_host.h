@@ -31,6 +31,18 @@ struct ag_lrts_ws {
   int32_t *status = nullptr;  // [1] device-side error flags
 };
 
+// DoublyRobustBidder workspace (ag_dr.hip)
+struct ag_dr_ws {
+  void *buf = nullptr;          // records in log order (ctr, value, gamma, prop, util, est_util,
+                                // won), sort keys / indices, hipcub temp
+  size_t buf_bytes = 0;
+  int64_t *counts = nullptr;    // [N] counts, [N + 1] offsets
+  double *adam_tab = nullptr;   // [2][32768] Adam bias corrections (libm pow)
+  float *state = nullptr;       // [N][16]: win-rate w0 w1 w2 b, policy (12)
+  int32_t *init = nullptr;      // [N] policy initialised
+  int64_t *scratch = nullptr;   // [N] noise offsets + [N][4] epochs / status
+};
+
 struct ag_ctx {
   int32_t device;
   ag_shape shape;
@@ -50,6 +62,9 @@ struct ag_ctx {
   bool general = false, has_lrts = false, has_shading = false, lrts_loaded = false;
   int32_t ts_sample = 1;
   int32_t *h_akind = nullptr;  // host copy of the allocator kinds [N]
+  int32_t *h_bkind = nullptr;  // host copy of the bidder kinds [N]
+  bool dr_loaded = false;
+  ag_dr_ws dr;
   int32_t *d_akind = nullptr, *d_bkind = nullptr;
   double *d_pg = nullptr, *d_gs = nullptr;
   float *d_tsm = nullptr, *d_tsq = nullptr, *d_tsprev = nullptr;  // LR-TS m, q, prev_iter_m
@@ -59,6 +74,8 @@ struct ag_ctx {
 
 // Frees the LR-TS training workspace (ag_lrts.hip).
 void ag_lrts_release(ag_ctx *c);
+// Frees the DoublyRobustBidder workspace (ag_dr.hip).
+void ag_dr_release(ag_ctx *c);
 
 struct AgDeviceGuard {
   int prev = -1;

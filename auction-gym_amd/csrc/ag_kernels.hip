@@ -407,8 +407,10 @@ int ag_destroy(ag_ctx *c) {
   (void)hipFree(c->d_tsq);
   (void)hipFree(c->d_tsprev);
   ag_lrts_release(c);
+  ag_dr_release(c);
   (void)hipFree(c->d_status);
   delete[] c->h_akind;
+  delete[] c->h_bkind;
   delete c;
   return AG_OK;
 }
@@ -448,15 +450,17 @@ int ag_set_agent_params(ag_ctx *c, const int32_t *alloc_kind, const int32_t *bid
   if (e == hipSuccess) e = hipMemcpy(c->d_bkind, bk, sizeof(int32_t) * N, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_pg, pg, sizeof(double) * N, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_gs, gs, sizeof(double) * N, hipMemcpyHostToDevice);
-  delete[] bk;
   delete[] pg;
   delete[] gs;
   if (e != hipSuccess) {
     delete[] ak;
+    delete[] bk;
     return ag_set_error(AG_ERR_HIP, "ag_set_agent_params: %s", hipGetErrorString(e));
   }
   delete[] c->h_akind;
   c->h_akind = ak;
+  delete[] c->h_bkind;
+  c->h_bkind = bk;
   c->general = general;
   c->has_lrts = lrts;
   c->has_shading = shading;

@@ -26,23 +26,21 @@ constexpr double kFx = 0x1p40;
 constexpr int64_t kLo24 = (int64_t(1) << 24) - 1;
 
 __global__ __launch_bounds__(kShThreads) void k_shading_collect(
-    int64_t B, int P, int K, const int32_t *__restrict__ part, const int32_t *__restrict__ winner,
-    const int32_t *__restrict__ item, const uint8_t *__restrict__ outcome, const double *__restrict__ price,
-    const double *__restrict__ gamma, const int32_t *__restrict__ bkind, const double *__restrict__ values,
-    int32_t *__restrict__ s_agent, double *__restrict__ s_gamma, double *__restrict__ s_util, int64_t cap,
+    int64_t first, int64_t B, int P, int K, const int32_t *__restrict__ part, ag_batch_out out,
+    const int32_t *__restrict__ bkind, const double *__restrict__ values, ag_shading_samples st,
     unsigned long long *__restrict__ count) {
   const int lane = threadIdx.x & 63;
   const bool charged = P >= 2;  // P == 1: nobody is charged (src/Auction.py:68)
   for (int64_t base = (int64_t)blockIdx.x * kShThreads; base < B; base += (int64_t)gridDim.x * kShThreads) {
     const int64_t i = base + threadIdx.x;
     const bool live = i < B;
-    const int w = live ? winner[i] : -1;
+    const int w = live ? out.winner[i] : -1;
     for (int s = 0; s < P; ++s) {
       int a = -1;
       bool take = false;
       if (live) {
         a = part[(size_t)s * B + i];
-        take = bkind[a] == AG_BIDDER_EMPIRICAL_SHADED;
+        take = bkind[a] == AG_BIDDER_EMPIRICAL_SHADED || bkind[a] == AG_BIDDER_DOUBLY_ROBUST;
       }
       const uint64_t ballot = __ballot(take);
       if (ballot == 0) continue;
@@ -52,15 +50,18 @@ __global__ __launch_bounds__(kShThreads) void k_shading_collect(
       first = __shfl(first, leader, 64);
       if (!take) continue;
       const int64_t slot = (int64_t)first + __popcll(ballot & ((1ull << lane) - 1));
-      if (slot >= cap) continue;  // overflow: reported by the update
-      double u = 0.0;             // src/Bidder.py:62-63
-      if (charged && s == w) {
-        const double v = values[(size_t)a * K + item[(size_t)s * B + i]];
-        u = v * (outcome[i] ? 1.0 : 0.0) - price[i];
-      }
-      s_agent[slot] = a;
-      s_gamma[slot] = gamma[(size_t)s * B + i];
-      s_util[slot] = u;
+      if (slot >= st.capacity) continue;  // overflow: reported by the update
+      const size_t o = (size_t)s * B + i;
+      const bool won = charged && s == w;
+      const double v = values[(size_t)a * K + out.item[o]];
+      st.agent[slot] = a;
+      st.gamma[slot] = out.gamma[o];
+      st.utility[slot] = won ? v * (out.outcome[i] ? 1.0 : 0.0) - out.price[i] : 0.0;  // src/Bidder.py:62-63
+      if (st.ctr) st.ctr[slot] = out.est_ctr[o];
+      if (st.value) st.value[slot] = v;
+      if (st.propensity) st.propensity[slot] = out.propensity[o];
+      if (st.won) st.won[slot] = won ? 1 : 0;
+      if (st.order) st.order[slot] = (uint64_t)(first + i) * (uint64_t)P + (uint64_t)s;
     }
   }
 }
@@ -234,7 +235,7 @@ int check_store(const ag_ctx *c, const ag_shading_samples *s, const char *who) {
 
 extern "C" {
 
-int ag_shading_collect(ag_ctx *c, int64_t B, const ag_batch_in *in, const ag_batch_out *out,
+int ag_shading_collect(ag_ctx *c, int64_t first, int64_t B, const ag_batch_in *in, const ag_batch_out *out,
                        const ag_shading_samples *s, void *stream) {
   if (int rc = check_store(c, s, "ag_shading_collect")) return rc;
   if (!in || !out) return ag_set_error(AG_ERR_INVALID, "ag_shading_collect: null argument");
@@ -243,11 +244,13 @@ int ag_shading_collect(ag_ctx *c, int64_t B, const ag_batch_in *in, const ag_bat
   if (!in->part || !out->winner || !out->item || !out->outcome || !out->price || !out->gamma)
     return ag_set_error(AG_ERR_INVALID, "ag_shading_collect: needs in.part, out.winner, out.item, "
                                         "out.outcome, out.price, out.gamma");
+  if ((s->ctr && !out->est_ctr) || (s->propensity && !out->propensity))
+    return ag_set_error(AG_ERR_INVALID, "ag_shading_collect: the store's ctr / propensity need "
+                                        "out.est_ctr / out.propensity");
   AgDeviceGuard g(c->device);
-  hipLaunchKernelGGL(k_shading_collect, dim3(grid_over(B)), dim3(kShThreads), 0, (hipStream_t)stream, B,
-                     c->shape.num_participants, c->shape.num_items, in->part, out->winner, out->item,
-                     out->outcome, out->price, out->gamma, c->d_bkind, c->d_values, s->agent, s->gamma,
-                     s->utility, s->capacity, (unsigned long long *)s->count);
+  hipLaunchKernelGGL(k_shading_collect, dim3(grid_over(B)), dim3(kShThreads), 0, (hipStream_t)stream, first, B,
+                     c->shape.num_participants, c->shape.num_items, in->part, *out, c->d_bkind, c->d_values, *s,
+                     (unsigned long long *)s->count);
   AG_HIP(hipGetLastError());
   return AG_OK;
 }

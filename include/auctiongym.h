@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define AG_ABI_VERSION 7
+#define AG_ABI_VERSION 9
 
 typedef enum ag_status {
   AG_OK = 0,
@@ -248,12 +248,21 @@ typedef struct ag_shading_samples {
   double *utility;   /* dev [capacity]: value * outcome - price if won, else 0           */
   int64_t capacity;
   uint64_t *count;   /* dev [1]: records appended; > capacity = overflow (update fails)  */
+  /* the learning bidders' update also needs (may be NULL for EmpiricalShaded only): */
+  double *ctr;       /* dev [capacity]: estimated CTR of the bid                         */
+  double *value;     /* dev [capacity]: value of the chosen item                         */
+  double *propensity;/* dev [capacity]: logging propensity of gamma                      */
+  uint8_t *won;      /* dev [capacity]                                                   */
+  uint64_t *order;   /* dev [capacity]: (global auction index) * P + slot -- the record's
+                        place in the agent's log order (the DR fit's noise follows it)    */
 } ag_shading_samples;
 
-/* Append the shading-bidder records of one simulated batch (needs in.part, out.winner,
- * out.item, out.outcome, out.price, out.gamma). Hot call: stream-ordered. */
-int ag_shading_collect(ag_ctx *ctx, int64_t B, const ag_batch_in *in, const ag_batch_out *out,
-                       const ag_shading_samples *samples, void *stream);
+/* Append the records of EmpiricalShaded and DoublyRobust bidders of one simulated batch of
+ * auctions [first_auction, first_auction + B) (needs in.part, out.winner, out.item,
+ * out.outcome, out.price, out.gamma; out.est_ctr and out.propensity when the store has ctr /
+ * propensity). Hot call: stream-ordered. */
+int ag_shading_collect(ag_ctx *ctx, int64_t first_auction, int64_t B, const ag_batch_in *in,
+                       const ag_batch_out *out, const ag_shading_samples *samples, void *stream);
 
 /* EmpiricalShadedBidder.update of every such agent from the store: the new prev_gamma is
  * written where ag_simulate reads it and, when prev_gamma (host [N]) is not NULL, copied
@@ -262,6 +271,29 @@ int ag_shading_collect(ag_ctx *ctx, int64_t B, const ag_batch_in *in, const ag_b
  * with two samples). Arithmetic: oracle/ag_oracle.c ora_empirical_update. */
 int ag_empirical_update(ag_ctx *ctx, const ag_shading_samples *samples, double *prev_gamma,
                         void *stream);
+
+/* ---- DoublyRobustBidder (src/Bidder.py:442-623) ---------------------------------------
+ * Per-agent model state, host float32 [N][16]: PyTorchWinRateEstimator weight (3) and bias,
+ * then BidShadingContextualBandit.parameters() (shared W 2x2, b 2; mu w 2, b; sigma w 2, b);
+ * initialised [N]: the policy was fitted (its bids come from the policy). */
+int ag_set_dr_state(ag_ctx *ctx, const float *state, const int32_t *initialised);
+int ag_get_dr_state(ag_ctx *ctx, float *state, int32_t *initialised);
+
+/* Records per agent in a shading store (host int64 [N]); synchronises. */
+int ag_shading_counts(ag_ctx *ctx, const ag_shading_samples *samples, int64_t *counts, void *stream);
+
+/* DoublyRobustBidder.update of every DR agent from the store (Agent.update, src/Agent.py:
+ * 79-94 -> src/Bidder.py:473-615): win-rate fit, imitation of the logging policy (first
+ * update), doubly robust policy fit; afterwards the agents bid from their policies. The
+ * store needs ctr, value, propensity, won and order; records are put in each agent's log
+ * order (radix sort on agent, order). noise: dev float32, agent a's DR-fit rsample draws
+ * at noise[noise_offsets[a] + e * n_a + i] for its i-th record in log order (n_a = its
+ * record count, e < noise_epochs); epochs: host int32 [N][3] epochs run per fit
+ * (may be NULL); traces: dev float32 [N][3][32768] per-epoch losses (may be NULL).
+ * Synchronises. Arithmetic: oracle/ag_oracle_dr.c ora_dr_update. */
+int ag_dr_update(ag_ctx *ctx, const ag_shading_samples *samples, const float *noise,
+                 const int64_t *noise_offsets, int32_t noise_epochs, int32_t *epochs, float *traces,
+                 void *stream);
 
 /* Exact counters (host int64 [n][AG_FX_LIMBS], e.g. copied back or all-reduced)
  * -> doubles (host [n]), correctly rounded from the exact fixed-point sum. */

@@ -1,0 +1,46 @@
+"""Dump the GPU DR update of the FP_DR_TS KAT agents (traces, states) to gpurun_out/."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "auction-gym_amd"), os.path.join(ROOT, "tests")]
+import torch  # noqa: E402
+
+import test_gpu_parity as T  # noqa: E402
+from auctiongym_amd.engine import AuctionEngine  # noqa: E402
+
+kat = np.load(os.path.join(ROOT, "tests", "golden", "dr_update_kat.npz"))
+N, E = 3, 10300
+eng = AuctionEngine(N, 2, 12, 5, 4, 0, 1.0)
+eng.set_agent_params(np.ones(N, np.int32), np.full(N, 4, np.int32), np.ones(N), np.full(N, 0.02))
+state0 = np.zeros((N, 16), np.float32)
+recs = {f: [] for f in ("agent", "gamma", "utility", "ctr", "value", "propensity", "won", "order")}
+noises, offs, off = [], [], 0
+for a in range(N):
+    k = lambda s: kat[f"a{a}_{s}"]  # noqa: E731
+    n = len(k("est_ctr"))
+    state0[a, :4] = np.concatenate([k("wr0_0").ravel(), k("wr0_1").ravel()])
+    state0[a, 4:] = np.concatenate([k(f"pol0_{j}").ravel() for j in range(6)])
+    for f, v in (("agent", np.full(n, a)), ("gamma", k("gamma")), ("utility", k("util")), ("ctr", k("est_ctr")),
+                 ("value", k("value")), ("propensity", k("propensity")), ("won", k("won")),
+                 ("order", 7 * np.arange(n) + a)):
+        recs[f].append(v)
+    z = T._dr_noise(k("dr_rng_state"), n, E)
+    noises.append(z.ravel())
+    offs.append(off)
+    off += z.size
+eng.set_dr_state(state0, np.zeros(N, np.int32))
+n_tot = sum(len(v) for v in recs["agent"])
+st = eng.new_shading_samples(n_tot, learning=True)
+dt = {"agent": np.int32, "won": np.uint8, "order": np.int64}
+for f, parts in recs.items():
+    st[f][:n_tot] = torch.from_numpy(np.concatenate(parts).astype(dt.get(f, np.float64))).to(eng.device)
+st["count"][0] = n_tot
+noise = torch.from_numpy(np.concatenate(noises)).to(eng.device)
+ep, tr = eng.dr_update(st, noise, offs, E, trace=True)
+state, ini = eng.dr_state()
+os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+np.savez(os.path.join(ROOT, "gpurun_out", "dr_dump.npz"), ep=ep, tr=tr.cpu().numpy(), state=state)
+print(ep)
