@@ -33,7 +33,7 @@ EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params
            "ag_shading_collect", "ag_empirical_update", "ag_set_dr_state", "ag_get_dr_state",
            "ag_shading_counts", "ag_dr_update",
            "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_last_error", "ag_abi_version")
-ABI_VERSION = 9
+ABI_VERSION = 10
 LRTS_MAX_EPOCHS = 16384
 LRTS_MAX_DO = 8
 
@@ -48,7 +48,8 @@ class AgShape(ctypes.Structure):
 
 class AgBatchIn(ctypes.Structure):
     _fields_ = [("ctx", ctypes.c_void_p), ("part", ctypes.c_void_p), ("u", ctypes.c_void_p),
-                ("gamma_raw", ctypes.c_void_p), ("ts_noise", ctypes.c_void_p)]
+                ("gamma_raw", ctypes.c_void_p), ("ts_noise", ctypes.c_void_p),
+                ("policy_eps", ctypes.c_void_p)]
 
 
 class AgBatchOut(ctypes.Structure):
@@ -110,7 +111,7 @@ def load(path=None):
         "ag_get_dr_state": (ctypes.c_int, [vp, vp, vp]),
         "ag_shading_counts": (ctypes.c_int, [vp, ctypes.POINTER(AgShadingSamples), vp, vp]),
         "ag_dr_update": (ctypes.c_int, [vp, ctypes.POINTER(AgShadingSamples), vp, vp, i32, vp, vp, vp]),
-        "ag_generate_noise": (ctypes.c_int, [vp, u64, u64, i64, vp, vp, vp, vp]),
+        "ag_generate_noise": (ctypes.c_int, [vp, u64, u64, i64, vp, vp, vp, vp, vp]),
         "ag_allocate": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, vp]),
         "ag_simulate": (ctypes.c_int, [vp, i64, ctypes.POINTER(AgBatchIn),
                                        ctypes.POINTER(AgBatchOut), vp, vp]),

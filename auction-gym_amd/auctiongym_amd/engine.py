@@ -85,6 +85,7 @@ class AuctionEngine:
         pg = None if prev_gamma is None else np.ascontiguousarray(prev_gamma, np.float64)
         gs = None if gamma_sigma is None else np.ascontiguousarray(gamma_sigma, np.float64)
         self.shading = bool((b != _lib.BIDDER_TRUTHFUL).any())
+        self.dr = bool((b == _lib.BIDDER_DOUBLY_ROBUST).any())
         self.lrts = bool((a == _lib.ALLOCATOR_LRTS).any())
         self._check(self.L.ag_set_agent_params(self._h, a.ctypes.data, b.ctypes.data,
                                                None if pg is None else pg.ctypes.data,
@@ -130,7 +131,8 @@ class AuctionEngine:
         """Append the won LR-TS samples of a simulated batch (ag_lrts_collect)."""
         B = inputs["u"].shape[0]
         bi = AgBatchIn(_ptr(inputs["ctx"]).value, _ptr(inputs["part"]).value, _ptr(inputs["u"]).value,
-                       _ptr(inputs.get("gamma_raw")).value, _ptr(inputs.get("ts_noise")).value)
+                       _ptr(inputs.get("gamma_raw")).value, _ptr(inputs.get("ts_noise")).value,
+                       _ptr(inputs.get("policy_eps")).value)
         bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
         st = self._samples(store)
         self._check(self.L.ag_lrts_collect(self._h, B, ctypes.byref(bi), ctypes.byref(bo),
@@ -185,6 +187,8 @@ class AuctionEngine:
                "u": torch.empty((B,), dtype=torch.float64, device=d)}
         if getattr(self, "shading", False):
             inp["gamma_raw"] = torch.empty((self.P, B), dtype=torch.float64, device=d)
+        if getattr(self, "dr", False):
+            inp["policy_eps"] = torch.empty((self.P, B), dtype=torch.float32, device=d)
         if getattr(self, "lrts", False) and getattr(self, "ts_sample", True):
             inp["ts_noise"] = torch.empty((self.P, (B + 63) // 64, self.K * (self.OE + 1), 64),
                                           dtype=torch.float32, device=d)
@@ -233,7 +237,8 @@ class AuctionEngine:
         if inputs["ctx"].shape != (self.E, B) or inputs["part"].shape != (self.P, B):
             raise ValueError("inputs must be SoA: ctx [E][B], part [P][B], u [B]")
         bi = AgBatchIn(_ptr(inputs["ctx"]).value, _ptr(inputs["part"]).value, _ptr(inputs["u"]).value,
-                       _ptr(inputs.get("gamma_raw")).value, _ptr(inputs.get("ts_noise")).value)
+                       _ptr(inputs.get("gamma_raw")).value, _ptr(inputs.get("ts_noise")).value,
+                       _ptr(inputs.get("policy_eps")).value)
         bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
         self._check(self.L.ag_simulate(self._h, B, ctypes.byref(bi), ctypes.byref(bo),
                                  _ptr(counters), _stream()), "ag_simulate")
@@ -248,7 +253,8 @@ class AuctionEngine:
         B = inputs["u"].shape[0]
         self._check(self.L.ag_generate_noise(self._h, int(seed), int(first_auction), B,
                                              _ptr(inputs["part"]), _ptr(inputs.get("gamma_raw")),
-                                             _ptr(inputs.get("ts_noise")), _stream()),
+                                             _ptr(inputs.get("ts_noise")), _ptr(inputs.get("policy_eps")),
+                                             _stream()),
                     "ag_generate_noise")
 
     def allocate(self, bids):
@@ -324,7 +330,8 @@ class AuctionEngine:
         [first_auction, first_auction + B) (ag_shading_collect)."""
         B = inputs["u"].shape[0]
         bi = AgBatchIn(_ptr(inputs["ctx"]).value, _ptr(inputs["part"]).value, _ptr(inputs["u"]).value,
-                       _ptr(inputs.get("gamma_raw")).value, _ptr(inputs.get("ts_noise")).value)
+                       _ptr(inputs.get("gamma_raw")).value, _ptr(inputs.get("ts_noise")).value,
+                       _ptr(inputs.get("policy_eps")).value)
         bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
         st = self._shading(store)
         self._check(self.L.ag_shading_collect(self._h, int(first_auction), B, ctypes.byref(bi), ctypes.byref(bo),

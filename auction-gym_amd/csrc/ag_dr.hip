@@ -471,6 +471,8 @@ int ag_set_dr_state(ag_ctx *c, const float *state, const int32_t *initialised) {
   AG_HIP(hipMemcpy(c->dr.state, state, sizeof(float) * 16 * N, hipMemcpyHostToDevice));
   AG_HIP(hipMemcpy(c->dr.init, initialised, sizeof(int32_t) * N, hipMemcpyHostToDevice));
   c->dr_loaded = true;
+  c->dr_any_init = false;
+  for (int a = 0; a < N; ++a) c->dr_any_init |= initialised[a] != 0 && c->h_bkind && c->h_bkind[a] == AG_BIDDER_DOUBLY_ROBUST;
   return AG_OK;
 }
 
@@ -586,7 +588,10 @@ int ag_dr_update(ag_ctx *c, const ag_shading_samples *s, const float *noise, con
   std::vector<int32_t> init(N);
   AG_HIP(hipMemcpy(init.data(), w.init, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
   for (int a = 0; a < N; ++a)
-    if (c->h_bkind[a] == AG_BIDDER_DOUBLY_ROBUST) init[a] = 1;
+    if (c->h_bkind[a] == AG_BIDDER_DOUBLY_ROBUST) {
+      init[a] = 1;
+      c->dr_any_init = true;
+    }
   AG_HIP(hipMemcpy(w.init, init.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice));
   return AG_OK;
 }

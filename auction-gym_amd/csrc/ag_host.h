@@ -63,7 +63,7 @@ struct ag_ctx {
   int32_t ts_sample = 1;
   int32_t *h_akind = nullptr;  // host copy of the allocator kinds [N]
   int32_t *h_bkind = nullptr;  // host copy of the bidder kinds [N]
-  bool dr_loaded = false;
+  bool dr_loaded = false, dr_any_init = false;  // DR models loaded; some bid from a policy
   ag_dr_ws dr;
   int32_t *d_akind = nullptr, *d_bkind = nullptr;
   double *d_pg = nullptr, *d_gs = nullptr;

@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kThreads) void k_generate_noise(uint64_t seed, uint
                                                             const int32_t *akind, const int32_t *bkind,
                                                             const double *pg, const double *gs,
                                                             const float *q, double *gamma_raw,
-                                                            float *ts_noise) {
+                                                            float *ts_noise, float *policy_eps) {
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const int64_t T = (B + 63) >> 6;  // 64-auction tiles of ts_noise
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < B;
@@ -265,6 +265,11 @@ __global__ __launch_bounds__(kThreads) void k_generate_noise(uint64_t seed, uint
         } else {
           gamma_raw[(int64_t)s * B + i] = NAN;
         }
+      }
+      if (policy_eps) {  // the rsample draw of a fitted DR policy
+        philox(c0, c1, 0, 16 + (uint32_t)s, k0, k1, w);
+        box_muller(w, z0, z1);
+        policy_eps[(int64_t)s * B + i] = (float)z0;
       }
       if (ts_noise) {
         const bool lr = akind[a] == AG_ALLOCATOR_LRTS;
@@ -574,6 +579,8 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
     return ag_set_error(AG_ERR_INVALID, "ag_simulate: Thompson sampling needs ts_noise");
   if (c->has_shading && !in->gamma_raw)
     return ag_set_error(AG_ERR_INVALID, "ag_simulate: shading bidders need gamma_raw");
+  if (c->dr_any_init && !in->policy_eps)
+    return ag_set_error(AG_ERR_INVALID, "ag_simulate: DoublyRobustBidders with a fitted policy need policy_eps");
   SimParams prm;
   prm.B = B;
   prm.N = s.num_agents;
@@ -588,6 +595,8 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   prm.pg = c->d_pg;
   prm.gs = c->d_gs;
   prm.tsm = c->d_tsm;
+  prm.drs = c->dr_loaded ? c->dr.state : nullptr;
+  prm.dri = c->dr_loaded ? c->dr.init : nullptr;
   prm.items = c->d_items;
   prm.values = c->d_values;
   prm.in = *in;
@@ -653,7 +662,7 @@ int ag_generate(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, double *ctx
 }
 
 int ag_generate_noise(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, const int32_t *part,
-                      double *gamma_raw, float *ts_noise, void *stream) {
+                      double *gamma_raw, float *ts_noise, float *policy_eps, void *stream) {
   if (!c || !part) return ag_set_error(AG_ERR_INVALID, "ag_generate_noise: null argument");
   if (B < 0) return ag_set_error(AG_ERR_INVALID, "ag_generate_noise: B < 0");
   if (B == 0) return AG_OK;
@@ -663,7 +672,7 @@ int ag_generate_noise(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, const
   const int KDo = c->shape.num_items * (c->shape.obs_embedding_size + 1);
   hipLaunchKernelGGL(k_generate_noise, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, seed, first, B,
                      c->shape.num_participants, KDo, part, c->d_akind, c->d_bkind, c->d_pg, c->d_gs,
-                     c->d_tsq, gamma_raw, ts_noise);
+                     c->d_tsq, gamma_raw, ts_noise, policy_eps);
   AG_HIP(hipGetLastError());
   return AG_OK;
 }

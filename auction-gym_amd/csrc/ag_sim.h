@@ -9,6 +9,7 @@
 #include "auctiongym.h"
 #include "ag_exp.h"
 #include "ag_exp_table.h"
+#include "ag_log1p.h"
 
 namespace ag {
 
@@ -89,7 +90,7 @@ __device__ __forceinline__ unsigned long long to_fx(double x) {
 
 // LDS carve of k_simulate (all pieces 16-B aligned; offsets in bytes).
 struct LdsLayout {
-  int32_t tab, items, values, scr, scr_val, amax, akind, bkind, pg, gs, tsm, cnt, total;
+  int32_t tab, items, values, scr, scr_val, amax, akind, bkind, pg, gs, tsm, drs, dri, cnt, total;
   int32_t items_stride;    // doubles between agents (odd: spreads agents over banks)
   int32_t values_stride;   // doubles
   int32_t scr_stride;      // floats between agents in the screening catalogue
@@ -151,6 +152,10 @@ __host__ inline LdsLayout make_layout(int N, int K, int D, bool counters, bool g
   b = L.gs + (general ? (int64_t)N * 8 : 0);
   L.tsm = align16(b);
   b = L.tsm + (general ? (int64_t)N * K * ts_do * 4 : 0);
+  L.drs = align16(b);
+  b = L.drs + (general ? (int64_t)N * 16 * 4 : 0);
+  L.dri = align16(b);
+  b = L.dri + (general ? (int64_t)N * 4 : 0);
   L.cnt = align16(b);
   b = L.cnt + (counters ? (int64_t)R * N * L.ncnt * 8 : 0);
   L.total = align16(b);
@@ -171,6 +176,8 @@ struct SimParams {
   const double *pg;       // general: [N] prev_gamma of shading bidders
   const double *gs;       // general: [N] gamma_sigma
   const float *tsm;       // general: [N][K][OE+1] LR-TS posterior means
+  const float *drs;       // general: [N][16] DoublyRobustBidder models (NULL: none)
+  const int32_t *dri;     // general: [N] fitted policy flags
   ag_batch_in in;
   ag_batch_out out;
   int64_t *partials;      // [grid][N][AG_NUM_COUNTERS][2]
@@ -334,6 +341,8 @@ struct Lds {
   const double *pg, *gs;
   const float *tsm;
   int ts_do;
+  const float *drs;
+  const int32_t *dri;
 };
 
 // One auction resolved (src/Auction.py:28-74 minus the draws).
@@ -411,6 +420,30 @@ __device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], 
   return best;
 }
 
+// DoublyRobustBidder.bid with a fitted policy (src/Bidder.py:466-470, src/Models.py:155-164):
+// ora_policy_bid (oracle/ag_oracle_dr.c) bit for bit -- the policy forward in double
+// (softplus = log1p(exp), the restated log1p), mu / sigma rounded to float32, the rsample
+// mu + sigma * eps in float32, exp(log_prob) rounded to float32, gamma = clip(sample, 0, 1).
+__device__ __forceinline__ double policy_softplus(double u, const uint64_t *tab) {
+  return u > 20.0 ? u : aglog1p::log1p(agexp::exp(u, tab));
+}
+__device__ __forceinline__ void policy_bid(const float *p, double ctr, double value, float eps,
+                                           const uint64_t *tab, double &gamma, double &prop) {
+  const double c = (double)(float)ctr, v = (double)(float)value;
+  double sft[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    sft[j] = policy_softplus(c * (double)p[2 * j] + v * (double)p[2 * j + 1] + (double)p[4 + j], tab);
+  const double am = sft[0] * (double)p[6] + sft[1] * (double)p[7] + (double)p[8];
+  const double as = sft[0] * (double)p[9] + sft[1] * (double)p[10] + (double)p[11];
+  const float mu = (float)policy_softplus(am, tab), sg = (float)(policy_softplus(as, tab) + 0.01);
+  const float raw = mu + sg * eps;
+  const double z = ((double)raw - (double)mu) / (double)sg;
+  const double logp = -(z * z) / 2.0 - aglog1p::log1p((double)sg - 1.0) - 0.91893853320467274178;
+  prop = (double)(float)agexp::exp(logp, tab);
+  gamma = raw < 0.0f ? 0.0 : (raw > 1.0f ? 1.0 : (double)raw);
+}
+
 // Gaussian density of a shading factor (src/Bidder.py:178, :355, :462).
 __device__ __forceinline__ double shading_propensity(double pg, double sigma, double g,
                                                      const uint64_t *tab) {
@@ -463,7 +496,10 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
     double b = v * est;  // Bidder.bid: value * estimated CTR (src/Bidder.py:35, :49, :173, ...)
     if constexpr (GENERAL) {
       const int bk = T.bkind[a];
-      if (bk != AG_BIDDER_TRUTHFUL) {
+      if (bk == AG_BIDDER_DOUBLY_ROBUST && T.drs && T.dri[a]) {  // bids from the fitted policy
+        policy_bid(T.drs + a * 16 + 4, est, v, in.policy_eps[s * B + i], T.tab, g, prop);
+        b = b * g;
+      } else if (bk != AG_BIDDER_TRUTHFUL) {
         g = in.gamma_raw[s * B + i];
         if (bk == AG_BIDDER_EMPIRICAL_SHADED) {  // clipped to [0, 1] (src/Bidder.py:52-55)
           if (g < 0.0) g = 0.0;
@@ -521,6 +557,8 @@ __global__ __launch_bounds__(kThreads, AG_MIN_WAVES) void k_simulate(SimParams p
   double *s_pg = reinterpret_cast<double *>(smem + L.pg);
   double *s_gs = reinterpret_cast<double *>(smem + L.gs);
   float *s_tsm = reinterpret_cast<float *>(smem + L.tsm);
+  float *s_drs = reinterpret_cast<float *>(smem + L.drs);
+  int32_t *s_dri = reinterpret_cast<int32_t *>(smem + L.dri);
   unsigned long long *s_cnt = reinterpret_cast<unsigned long long *>(smem + L.cnt);
 
   const int tid = threadIdx.x;
@@ -532,6 +570,10 @@ __global__ __launch_bounds__(kThreads, AG_MIN_WAVES) void k_simulate(SimParams p
       s_gs[a] = prm.gs[a];
     }
     for (int j = tid; j < N * K * L.ts_do; j += kThreads) s_tsm[j] = prm.tsm[j];
+    if (prm.drs) {
+      for (int j = tid; j < N * 16; j += kThreads) s_drs[j] = prm.drs[j];
+      for (int a = tid; a < N; a += kThreads) s_dri[a] = prm.dri[a];
+    }
   }
   for (int i = tid; i < 256; i += kThreads) s_tab[i] = ag_exp_tab[i];
   for (int i = tid; i < N * K * D; i += kThreads) {
@@ -567,7 +609,8 @@ __global__ __launch_bounds__(kThreads, AG_MIN_WAVES) void k_simulate(SimParams p
   __syncthreads();
 
   const Lds T{s_tab, s_items, s_vals, s_scr, s_scr_val, s_amax, L.items_stride, L.values_stride,
-              L.scr_stride, L.scr_val_stride, L.kpairs, s_akind, s_bkind, s_pg, s_gs, s_tsm, L.ts_do};
+              L.scr_stride, L.scr_val_stride, L.kpairs, s_akind, s_bkind, s_pg, s_gs, s_tsm, L.ts_do,
+              (GENERAL && prm.drs) ? s_drs : nullptr, s_dri};
   const int rep = tid & (R - 1);
   const ag_batch_in in = prm.in;
   const ag_batch_out out = prm.out;

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define AG_ABI_VERSION 9
+#define AG_ABI_VERSION 10
 
 typedef enum ag_status {
   AG_OK = 0,
@@ -113,6 +113,9 @@ typedef struct ag_batch_in {
                               at ((s*T + i/64)*K*(OE+1) + c)*64 + i%64, so a wave reads each
                               coefficient of its 64 auctions as one 256-B row and a tile's
                               rows are contiguous; NULL if none / no sampling */
+  const float *policy_eps; /* [P][B] the rsample draw (torch, standard normal) of a
+                              DoublyRobustBidder bidding from its fitted policy
+                              (src/Bidder.py:466-470); NULL if none */
 } ag_batch_in;
 
 /* Outputs of B auctions (dev). Any pointer may be NULL to skip that array. */
@@ -127,7 +130,9 @@ typedef struct ag_batch_out {
   double *true_ctr;      /* [P][B] true CTR of the chosen item (src/Auction.py:52-53)    */
   double *best_ev;       /* [P][B] max_k true_CTR_k * value_k                           */
   double *gamma;         /* [P][B] shading factor of shading bidders (NaN otherwise)     */
-  double *propensity;    /* [P][B] Gaussian density of gamma (learning bidders; NaN else)*/
+  double *propensity;    /* [P][B] density of gamma under the bidder's logging policy:
+                            the Gaussian around prev_gamma (uninitialised learning
+                            bidders) or the fitted policy's (DR); NaN otherwise          */
 } ag_batch_out;
 
 /* Create a context on `device` for one auction population (src/main.py:98-109
@@ -199,9 +204,11 @@ int ag_generate(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B, d
 /* Synthetic per-participant noise for the participants `part` (dev [P][B]) of auctions
  * [first_auction, first_auction + B): gamma_raw [P][B] = prev_gamma + gamma_sigma * z for
  * shading bidders (NaN otherwise), ts_noise (tiled as in ag_batch_in) = z / sqrt(q) for
- * LR-TS agents (0 otherwise); either output may be NULL. Same Philox key / counter scheme. */
+ * LR-TS agents (0 otherwise), policy_eps [P][B] = z for every slot; any output may be NULL.
+ * Same Philox key / counter scheme. */
 int ag_generate_noise(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B,
-                      const int32_t *part, double *gamma_raw, float *ts_noise, void *stream);
+                      const int32_t *part, double *gamma_raw, float *ts_noise, float *policy_eps,
+                      void *stream);
 
 /* ---- LR-TS allocator update (Agent.update -> PyTorchLogisticRegressionAllocator.update,
  * src/Agent.py:79-91, src/BidderAllocation.py:29-65) ------------------------------------

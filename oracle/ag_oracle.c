@@ -220,7 +220,10 @@ static void simulate_range(const ora_pop *pp, const double *items, const double 
       double b = v * est; /* Bidder.bid: value * estimated CTR (src/Bidder.py:35,49,173,...) */
       double g = NAN, prop = NAN;
       const int32_t bk = pp->bid_kind[a];
-      if (bk != ORA_BIDDER_TRUTHFUL) {
+      if (bk == ORA_BIDDER_DOUBLY_ROBUST && pp->dr_init && pp->dr_init[a]) {
+        ora_policy_bid(pp->dr_state + (int64_t)a * 16 + 4, est, v, in->policy_eps[o], &g, &prop);
+        b = b * g;
+      } else if (bk != ORA_BIDDER_TRUTHFUL) {
         g = shading_gamma(bk, in->gamma_raw[o]);
         if (bk != ORA_BIDDER_EMPIRICAL) prop = ora_propensity(pp->prev_gamma[a], pp->gamma_sigma[a], g);
         b = b * g;
@@ -326,8 +329,8 @@ void ora_simulate(const ora_shape *s, const double *items, const double *values,
                   double *counters, int64_t *counters_fx, int32_t nthreads) {
   int32_t *ak = (int32_t *)calloc((size_t)s->N, sizeof(int32_t));
   int32_t *bk = (int32_t *)calloc((size_t)s->N, sizeof(int32_t));
-  ora_pop pp = {s->N, s->P, s->K, s->E, s->E, s->mech, ak, bk, NULL, NULL, NULL, 0};
-  ora_in in = {ctx, part, u, NULL, NULL};
+  ora_pop pp = {s->N, s->P, s->K, s->E, s->E, s->mech, ak, bk, NULL, NULL, NULL, 0, NULL, NULL};
+  ora_in in = {ctx, part, u, NULL, NULL, NULL};
   ora_out out = {winner, price, second_price, outcome, item, value, bid, est_ctr, true_ctr,
                  best_ev, NULL, NULL};
   ora_simulate_pop(&pp, items, values, B, &in, &out, counters, counters_fx, nthreads);

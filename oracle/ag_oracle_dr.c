@@ -401,3 +401,19 @@ int32_t ora_dr_update(int64_t n, const double *ctr, const double *value, const d
   free(eu);
   return 0;
 }
+
+/* DoublyRobustBidder.bid with a fitted policy (src/Bidder.py:466-470, src/Models.py:155-164):
+ * x = float32 [estimated CTR, value]; the policy's mu and sigma (double, as in the fit, then
+ * rounded to float32 like torch's tensors), the rsample mu + sigma * eps in float32, its
+ * Gaussian density exp(log_prob) rounded to float32 (log via the restated log1p), gamma =
+ * clip(sample, 0, 1). torch computes every step in float32: bids agree to float32 rounding. */
+void ora_policy_bid(const float *p, double ctr, double value, float eps, double *gamma, double *prop) {
+  polf_t f;
+  policy_fwd(p, (double)(float)ctr, (double)(float)value, &f);
+  const float mu = (float)f.mu, sg = (float)f.sigma;
+  const float raw = mu + sg * eps;
+  const double z = ((double)raw - (double)mu) / (double)sg;
+  const double logp = -(z * z) / 2.0 - fl_log1p((double)sg - 1.0) - 0.91893853320467274178;
+  *prop = (double)(float)exp(logp);
+  *gamma = raw < 0.0f ? 0.0 : (raw > 1.0f ? 1.0 : (double)raw);
+}

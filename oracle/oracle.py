@@ -33,11 +33,12 @@ class _Pop(ctypes.Structure):
                 ("E", ctypes.c_int32), ("OE", ctypes.c_int32), ("mech", ctypes.c_int32),
                 ("alloc_kind", ctypes.c_void_p), ("bid_kind", ctypes.c_void_p),
                 ("prev_gamma", ctypes.c_void_p), ("gamma_sigma", ctypes.c_void_p),
-                ("ts_m", ctypes.c_void_p), ("ts_sample", ctypes.c_int32)]
+                ("ts_m", ctypes.c_void_p), ("ts_sample", ctypes.c_int32),
+                ("dr_state", ctypes.c_void_p), ("dr_init", ctypes.c_void_p)]
 
 
 class _In(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("ctx", "part", "u", "gamma_raw", "ts_noise")]
+    _fields_ = [(n, ctypes.c_void_p) for n in ("ctx", "part", "u", "gamma_raw", "ts_noise", "policy_eps")]
 
 
 class _Out(ctypes.Structure):
@@ -142,7 +143,7 @@ def simulate(mech, items, values, ctx, part, u, nthreads=1):
 
 def simulate_pop(mech, items, values, ctx, part, u, alloc_kind, bid_kind, prev_gamma=None,
                  gamma_sigma=None, OE=None, ts_m=None, ts_noise=None, gamma_raw=None,
-                 ts_sample=True, nthreads=1):
+                 ts_sample=True, dr_state=None, dr_init=None, policy_eps=None, nthreads=1):
     """General population (OracleAllocator / LR-TS allocators; truthful / shading bidders in
     their first iteration). Row-major replay inputs; returns outputs + counters."""
     items = np.ascontiguousarray(items, np.float64)
@@ -169,15 +170,19 @@ def simulate_pop(mech, items, values, ctx, part, u, alloc_kind, bid_kind, prev_g
     tm = arr(ts_m if ts_m is not None else np.zeros((N, K, OE + 1)), np.float32)
     gr = arr(gamma_raw if gamma_raw is not None else np.full((B, P), np.nan), np.float64)
     tn = arr(ts_noise if ts_noise is not None else np.zeros((B, P, K, OE + 1)), np.float32)
+    ds = arr(dr_state if dr_state is not None else np.zeros((N, 16)), np.float32)
+    di = arr(dr_init if dr_init is not None else np.zeros(N), np.int32)
+    pe = arr(policy_eps if policy_eps is not None else np.zeros((B, P)), np.float32)
     pop = _Pop(N, P, K, E, OE, int(mech), ak.ctypes.data, bk.ctypes.data, pg.ctypes.data,
-               gs.ctypes.data, tm.ctypes.data, int(bool(ts_sample)))
+               gs.ctypes.data, tm.ctypes.data, int(bool(ts_sample)), ds.ctypes.data, di.ctypes.data)
     out = dict(winner=np.empty(B, np.int32), price=np.empty(B), second_price=np.empty(B),
                outcome=np.empty(B, np.uint8), item=np.empty((B, P), np.int32),
                value=np.empty((B, P)), bid=np.empty((B, P)), est_ctr=np.empty((B, P)),
                true_ctr=np.empty((B, P)), best_ev=np.empty((B, P)), gamma=np.empty((B, P)),
                propensity=np.empty((B, P)), counters=np.zeros((N, NUM_COUNTERS)),
                counters_fx=np.zeros((N, NUM_COUNTERS, 3), np.int64))
-    cin = _In(ctx.ctypes.data, part.ctypes.data, u.ctypes.data, gr.ctypes.data, tn.ctypes.data)
+    cin = _In(ctx.ctypes.data, part.ctypes.data, u.ctypes.data, gr.ctypes.data, tn.ctypes.data,
+              pe.ctypes.data)
     cout = _Out(*[out[k].ctypes.data for k in ("winner", "price", "second_price", "outcome", "item",
                                                "value", "bid", "est_ctr", "true_ctr", "best_ev",
                                                "gamma", "propensity")])

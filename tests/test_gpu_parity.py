@@ -449,6 +449,65 @@ def test_mixed_population_full_size(gpu, oracle):
     eng.close()
 
 
+def test_fitted_dr_policy_bids_match_oracle(gpu, oracle):
+    """DoublyRobustBidder.bid with a fitted policy (src/Bidder.py:440-470): the gamma is the
+    policy's rsample on (estimated CTR, value), the propensity its Normal density. Mixed
+    population where half of the DR agents bid from random fitted policies; every output
+    compared with the oracle on the same inputs and the same generated rsample draws."""
+    import torch
+    from auctiongym_amd.engine import AuctionEngine
+    N, P, K, E, OE, B = 20, 4, 12, 5, 4, 1 << 18
+    g = np.random.default_rng(33)
+    items = np.concatenate([g.normal(0, 1, (N, K, E)), -3.0 - g.random((N, K, 1))], axis=2)
+    values = g.lognormal(0.1, 0.2, (N, K))
+    ak = np.array([i % 2 for i in range(N)], np.int32)
+    bk = np.array([4 if i % 3 else (i // 3) % 4 for i in range(N)], np.int32)
+    pg = 0.5 + 0.5 * g.random(N)
+    gs = 0.01 + 0.05 * g.random(N)
+    m = g.normal(0, 1, (N, K, OE + 1)).astype(np.float32)
+    q = (1.0 + 3.0 * g.random((N, K, OE + 1))).astype(np.float32)
+    state = g.normal(0, 0.7, (N, 16)).astype(np.float32)
+    init = np.array([1 if (bk[a] == 4 and a % 2 == 0) else 0 for a in range(N)], np.int32)
+    assert init.sum() >= 4 and ((bk == 4) & (init == 0)).sum() >= 4
+    eng = AuctionEngine(N, P, K, E, OE, 1, 1.0)
+    eng.set_agent_params(ak, bk, pg, gs)
+    eng.load_catalog(items, values)
+    eng.load_lrts(m, q, thompson_sampling=True)
+    eng.set_dr_state(state, init)
+    inp = eng.alloc_inputs(B)
+    assert "policy_eps" in inp
+    eng.generate(9, 0, inp)
+    eng.generate_noise(9, 0, inp)
+    out = eng.alloc_outputs(B)
+    cnt = eng.new_counters()
+    eng.simulate(inp, out, cnt)
+    torch.cuda.synchronize()
+    T = lambda t: np.ascontiguousarray(t.cpu().numpy().T)  # noqa: E731
+    pe = T(inp["policy_eps"])
+    assert abs(pe.mean()) < 0.01 and abs(pe.std() - 1) < 0.01
+    orc = oracle.simulate_pop(1, items, values, T(inp["ctx"]), T(inp["part"]), inp["u"].cpu().numpy(),
+                              ak, bk, pg, gs, OE=OE, ts_m=m,
+                              ts_noise=eng.untile_ts_noise(inp["ts_noise"], B).reshape(B, P, K, OE + 1),
+                              gamma_raw=T(inp["gamma_raw"]), dr_state=state, dr_init=init,
+                              policy_eps=pe, nthreads=16)
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    for k in ("item", "bid", "est_ctr", "true_ctr", "best_ev", "gamma", "propensity"):
+        assert np.array_equal(np.ascontiguousarray(got[k].T), orc[k], equal_nan=True), k
+    for k in ("winner", "price", "second_price", "outcome"):
+        assert np.array_equal(got[k], orc[k], equal_nan=True), k
+    assert np.array_equal(cnt.cpu().numpy(), orc["counters_fx"])
+    # fitted agents' gammas are clipped policy draws, not N(prev_gamma, sigma) draws
+    part = T(inp["part"])
+    fitted = init[part] == 1
+    gam = np.ascontiguousarray(got["gamma"].T)
+    assert fitted.any() and (gam[fitted] >= 0).all() and (gam[fitted] <= 1).all()
+    # without policy_eps the launch is refused
+    del inp["policy_eps"]
+    with pytest.raises(ValueError, match="policy_eps"):
+        eng.simulate(inp, out, eng.new_counters())
+    eng.close()
+
+
 # ---- LR-TS allocator update (Agent.update -> PyTorchLogisticRegressionAllocator.update) ----
 def _kat_population():
     kat = np.load(os.path.join(GOLDEN, "sp_ts_update_kat.npz"))
