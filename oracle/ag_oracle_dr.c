@@ -247,6 +247,85 @@ static void policy_bwd(const float *p, double c, double v, const polf_t *f, doub
   }
 }
 
+/* PyTorchWinRateEstimator fit (src/Bidder.py:229-252 ValueLearningBidder, :500-530
+ * DoublyRobustBidder): BCE (mean) over the logs plus the gamma = 0, y = 0 augmentation,
+ * Adam(lr 3e-3, weight decay 1e-6, AMSGrad), ReduceLROnPlateau(patience, factor, min_lr
+ * 1e-7), early stop after `wait` epochs without a 1e-6 improvement, <= 32768 epochs. */
+static int32_t fit_winrate(int64_t n, const float *cf, const float *vf, const float *gf, const uint8_t *won,
+                           float *wr, int32_t patience, double factor, int32_t wait, float *trace) {
+  const double M = 2.0 * (double)n;
+  adam_t ad;
+  adam_init(&ad, 4, 3e-3, 1e-6);
+  plateau_t pl;
+  plateau_init(&pl, patience, factor, 1e-7, 1e-4);
+  stopper_t st = {INFINITY, -1, wait};
+  int32_t e = 0;
+  for (; e < 32768; ++e) {
+    __int128 L = 0, G[4] = {0, 0, 0, 0};
+    for (int64_t r = 0; r < 2 * n; ++r) {
+      const int64_t i = r < n ? r : r - n;
+      const double c = cf[i], v = vf[i], g = r < n ? gf[i] : 0.0;
+      const double y = r < n ? (double)won[i] : 0.0;
+      const double z = c * (double)wr[0] + v * (double)wr[1] + g * (double)wr[2] + (double)wr[3];
+      const double pw = 1.0 / (1.0 + exp(-z));
+      /* BCE with torch's clamp of the logs at -100: -log(p) = softplus(-z), -log(1-p) =
+       * softplus(z) (exp + the restated log1p: the same bits on the device) */
+      const double t = y > 0.0 ? fmin(softplus(-z), 100.0) : fmin(softplus(z), 100.0);
+      L += fxr(t);
+      const double gz = pw - y;
+      G[0] += fxr(gz * c);
+      G[1] += fxr(gz * v);
+      G[2] += fxr(gz * g);
+      G[3] += fxr(gz);
+    }
+    const float loss = (float)(fxv(L) / M);
+    float grad[4];
+    for (int j = 0; j < 4; ++j) grad[j] = (float)(fxv(G[j]) / M);
+    adam_step(&ad, wr, grad);
+    if (trace) trace[e] = loss;
+    plateau_step(&pl, loss, &ad.lr);
+    if (stop_step(&st, e, loss)) {
+      ++e;
+      break;
+    }
+  }
+  return e;
+}
+
+/* BidShadingContextualBandit.initialise_policy (src/Models.py:106-137): imitation of the
+ * logging policy -- MSE of mu to the logged gammas + MSE of softplus(sigma) (WITHOUT
+ * min_sigma, :118) to 0.05, Adam(lr 1e-3, wd 1e-4, AMSGrad), no scheduler, early stop
+ * after 512 epochs, <= 16384 epochs. */
+static int32_t fit_imitation(int64_t n, const float *cf, const float *vf, const float *gf, float *pol,
+                             float *trace) {
+  adam_t ad;
+  adam_init(&ad, 12, 1e-3, 1e-4);
+  stopper_t st = {INFINITY, -1, 512};
+  int32_t e = 0;
+  for (; e < 16384; ++e) {
+    __int128 L1 = 0, L2 = 0, G[12];
+    memset(G, 0, sizeof G);
+    for (int64_t i = 0; i < n; ++i) {
+      polf_t f;
+      policy_fwd(pol, cf[i], vf[i], &f);
+      const double dm = f.mu - (double)gf[i], dsg = f.sp_sigma - 0.05;
+      L1 += fxr(dm * dm);
+      L2 += fxr(dsg * dsg);
+      policy_bwd(pol, cf[i], vf[i], &f, 2.0 * dm, 2.0 * dsg, G);
+    }
+    const float loss = (float)(fxv(L1) / (double)n + fxv(L2) / (double)n);
+    float grad[12];
+    for (int j = 0; j < 12; ++j) grad[j] = (float)(fxv(G[j]) / (double)n);
+    adam_step(&ad, pol, grad);
+    if (trace) trace[e] = loss;
+    if (stop_step(&st, e, loss)) {
+      ++e;
+      break;
+    }
+  }
+  return e;
+}
+
 int32_t ora_dr_update(int64_t n, const double *ctr, const double *value, const double *gamma,
                       const double *prop, const uint8_t *won, const double *util, float *wr, float *pol,
                       int32_t initialised, const float *noise, int64_t noise_epochs, int32_t *epochs,
@@ -259,46 +338,8 @@ int32_t ora_dr_update(int64_t n, const double *ctr, const double *value, const d
     vf[i] = (float)value[i];
     gf[i] = (float)gamma[i];
   }
-  const double M = 2.0 * (double)n;
   /* ---- 1. win-rate fit */
-  {
-    adam_t ad;
-    adam_init(&ad, 4, 3e-3, 1e-6);
-    plateau_t pl;
-    plateau_init(&pl, 256, 0.2, 1e-7, 1e-4);
-    stopper_t st = {INFINITY, -1, 1024};
-    int32_t e = 0;
-    for (; e < 32768; ++e) {
-      __int128 L = 0, G[4] = {0, 0, 0, 0};
-      for (int64_t r = 0; r < 2 * n; ++r) {
-        const int64_t i = r < n ? r : r - n;
-        const double c = cf[i], v = vf[i], g = r < n ? gf[i] : 0.0;
-        const double y = r < n ? (double)won[i] : 0.0;
-        const double z = c * (double)wr[0] + v * (double)wr[1] + g * (double)wr[2] + (double)wr[3];
-        const double pw = 1.0 / (1.0 + exp(-z));
-        /* BCE with torch's clamp of the logs at -100: -log(p) = softplus(-z), -log(1-p) =
-         * softplus(z) (exp + the restated log1p: the same bits on the device) */
-        const double t = y > 0.0 ? fmin(softplus(-z), 100.0) : fmin(softplus(z), 100.0);
-        L += fxr(t);
-        const double gz = pw - y;
-        G[0] += fxr(gz * c);
-        G[1] += fxr(gz * v);
-        G[2] += fxr(gz * g);
-        G[3] += fxr(gz);
-      }
-      const float loss = (float)(fxv(L) / M);
-      float grad[4];
-      for (int j = 0; j < 4; ++j) grad[j] = (float)(fxv(G[j]) / M);
-      adam_step(&ad, wr, grad);
-      if (wr_trace) wr_trace[e] = loss;
-      plateau_step(&pl, loss, &ad.lr);
-      if (stop_step(&st, e, loss)) {
-        ++e;
-        break;
-      }
-    }
-    epochs[0] = e;
-  }
+  epochs[0] = fit_winrate(n, cf, vf, gf, won, wr, 256, 0.2, 1024, wr_trace);
   /* ---- 2. estimated utilities with the fitted model (float32 W, as .numpy() of it) */
   for (int64_t i = 0; i < n; ++i) {
     const float W = (float)winrate(wr, cf[i], vf[i], gf[i]);
@@ -307,36 +348,7 @@ int32_t ora_dr_update(int64_t n, const double *ctr, const double *value, const d
     if (est_util_out) est_util_out[i] = eu[i];
   }
   /* ---- 3. imitation of the logging policy (first update only) */
-  epochs[1] = 0;
-  if (!initialised) {
-    adam_t ad;
-    adam_init(&ad, 12, 1e-3, 1e-4);
-    stopper_t st = {INFINITY, -1, 512};
-    int32_t e = 0;
-    for (; e < 16384; ++e) {
-      __int128 L1 = 0, L2 = 0, G[12];
-      memset(G, 0, sizeof G);
-      for (int64_t i = 0; i < n; ++i) {
-        polf_t f;
-        policy_fwd(pol, cf[i], vf[i], &f);
-        /* predicted sigma WITHOUT min_sigma here (src/Models.py:118) */
-        const double dm = f.mu - (double)gf[i], dsg = f.sp_sigma - 0.05;
-        L1 += fxr(dm * dm);
-        L2 += fxr(dsg * dsg);
-        policy_bwd(pol, cf[i], vf[i], &f, 2.0 * dm, 2.0 * dsg, G);
-      }
-      const float loss = (float)(fxv(L1) / (double)n + fxv(L2) / (double)n);
-      float grad[12];
-      for (int j = 0; j < 12; ++j) grad[j] = (float)(fxv(G[j]) / (double)n);
-      adam_step(&ad, pol, grad);
-      if (init_trace) init_trace[e] = loss;
-      if (stop_step(&st, e, loss)) {
-        ++e;
-        break;
-      }
-    }
-    epochs[1] = e;
-  }
+  epochs[1] = initialised ? 0 : fit_imitation(n, cf, vf, gf, pol, init_trace);
   /* ---- 4. doubly robust policy fit */
   {
     adam_t ad;
@@ -416,4 +428,235 @@ void ora_policy_bid(const float *p, double ctr, double value, float eps, double 
   const double logp = -(z * z) / 2.0 - fl_log1p((double)sg - 1.0) - 0.91893853320467274178;
   *prop = (double)(float)exp(logp);
   *gamma = raw < 0.0f ? 0.0 : (raw > 1.0f ? 1.0 : (double)raw);
+}
+
+/* ValueLearningBidder.update for one agent (src/Bidder.py:204-325): no wins -> the
+ * reference's fallback (model_initialised = False, nothing trained; returns 1); else the
+ * win-rate fit (ReduceLROnPlateau patience 100, factor 0.1; early stop after 512 epochs)
+ * and, with inference 'policy', the policy fit (:258-303): loss -mean(W(ctr, value, g~) (V -
+ * V g~)), g~ = clip(mu + sigma eps, 0, 1) with the per-epoch rsample noise (given), V = ctr
+ * value; Adam(lr 2e-3, wd 1e-6, AMSGrad), ReduceLROnPlateau(patience 100, factor 0.1,
+ * min_lr 1e-7), early stop after 256 epochs, <= 16384 epochs. BidShadingPolicy's hidden
+ * layers (src/Models.py:72-76) are not on the forward path: they get no gradient and Adam
+ * skips them, so pol holds the 12 parameters of the path (shared, mu out, sigma out).
+ * Sums as in ora_dr_update (exact fixed point). epochs [3] = (win-rate, 0, policy). */
+int32_t ora_vl_update(int64_t n, const double *ctr, const double *value, const double *gamma,
+                      const uint8_t *won, float *wr, float *pol, int32_t policy, const float *noise,
+                      int64_t noise_epochs, int32_t *epochs, float *wr_trace, float *pol_trace) {
+  epochs[0] = epochs[1] = epochs[2] = 0;
+  if (n < 1) return -1;
+  int64_t wins = 0;
+  for (int64_t i = 0; i < n; ++i) wins += won[i] != 0;
+  if (!wins) return 1;
+  float *cf = malloc(n * sizeof(float)), *vf = malloc(n * sizeof(float)), *gf = malloc(n * sizeof(float));
+  for (int64_t i = 0; i < n; ++i) {
+    cf[i] = (float)ctr[i];
+    vf[i] = (float)value[i];
+    gf[i] = (float)gamma[i];
+  }
+  epochs[0] = fit_winrate(n, cf, vf, gf, won, wr, 100, 0.1, 512, wr_trace);
+  if (policy) {
+    adam_t ad;
+    adam_init(&ad, 12, 2e-3, 1e-6);
+    plateau_t pl;
+    plateau_init(&pl, 100, 0.1, 1e-7, 1e-4);
+    stopper_t st = {INFINITY, -1, 256};
+    int32_t e = 0;
+    for (; e < 16384 && e < noise_epochs; ++e) {
+      const float *eps = noise + (int64_t)e * n;
+      __int128 L = 0, G[12];
+      memset(G, 0, sizeof G);
+      for (int64_t i = 0; i < n; ++i) {
+        polf_t f;
+        const double c = cf[i], v = vf[i];
+        policy_fwd(pol, c, v, &f);
+        const double raw = f.mu + f.sigma * (double)eps[i];
+        const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
+        const double Wv = winrate(wr, c, v, gs);
+        const double V = c * v;
+        L += fxr(-(Wv * (V - V * gs)));
+        double ddm_dgs = 0.0;
+        if (raw >= 0.0 && raw <= 1.0) ddm_dgs = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)wr[2];
+        policy_bwd(pol, c, v, &f, -ddm_dgs, -(ddm_dgs * (double)eps[i]), G);
+      }
+      const float loss = (float)(fxv(L) / (double)n);
+      float grad[12];
+      for (int j = 0; j < 12; ++j) grad[j] = (float)(fxv(G[j]) / (double)n);
+      adam_step(&ad, pol, grad);
+      if (pol_trace) pol_trace[e] = loss;
+      plateau_step(&pl, loss, &ad.lr);
+      if (stop_step(&st, e, loss)) {
+        ++e;
+        break;
+      }
+    }
+    epochs[2] = e;
+  }
+  free(cf);
+  free(vf);
+  free(gf);
+  return 0;
+}
+
+/* Fixed-order double sums of the policy-learning fits (importance weights are unbounded,
+ * so their terms do not fit a fixed-point grid): record i goes to lane i mod 256 and is
+ * added in record order; each 64-lane wave is combined by the butterfly v[l] + v[l ^ o],
+ * o = 32, 16, ..., 1 (identical on every lane); the four wave totals are added to 0.0 in
+ * wave order. This is the device's reduction order exactly (csrc/ag_dr.hip). */
+#define PL_LANES 256
+#define PL_NV 14
+static void pl_lane_sums(double (*acc)[PL_NV], double *tot) {
+  for (int j = 0; j < PL_NV; ++j) {
+    double t = 0.0;
+    for (int w = 0; w < PL_LANES / 64; ++w) {
+      double v[64], nv[64];
+      for (int l = 0; l < 64; ++l) v[l] = acc[w * 64 + l][j];
+      for (int o = 32; o > 0; o >>= 1) {
+        for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ o];
+        memcpy(v, nv, sizeof v);
+      }
+      t += v[0];
+    }
+    tot[j] = t;
+  }
+}
+
+/* per-record gradient of a policy loss term given d/dmu and d/dsigma (the order of
+ * policy_bwd, in double) */
+static void policy_grad(const float *p, double c, double v, const polf_t *f, double dmu, double dsigma,
+                        double *g) {
+  const double dam = dmu * dsoftplus(f->am), das = dsigma * dsoftplus(f->as);
+  double ds[2];
+  ds[0] = dam * (double)p[6] + das * (double)p[9];
+  ds[1] = dam * (double)p[7] + das * (double)p[10];
+  g[6] = dam * f->s[0];
+  g[7] = dam * f->s[1];
+  g[8] = dam;
+  g[9] = das * f->s[0];
+  g[10] = das * f->s[1];
+  g[11] = das;
+  for (int j = 0; j < 2; ++j) {
+    const double dh = ds[j] * dsoftplus(f->h[j]);
+    g[2 * j] = dh * c;
+    g[2 * j + 1] = dh * v;
+    g[4 + j] = dh;
+  }
+}
+
+/* PolicyLearningBidder.update for one agent (src/Bidder.py:364-431, the losses of
+ * src/Models.py:174-199): imitation of the logging policy on the first update, then the
+ * policy fit with Adam(lr 2e-3, wd 1e-4, AMSGrad), ReduceLROnPlateau(patience 100, factor
+ * 0.2, min_lr 1e-8), early stop after 512 epochs, <= 16384 epochs, importance-weight
+ * clipping eps 50, KL weight 5e-2. loss_kind: 0 REINFORCE, 1 REINFORCE_offpolicy, 2 TRPO,
+ * 3 PPO (AG_PL_LOSS_*). Target propensities are clip(pdf, min 1e-30), logging ones
+ * clip(float32, min 1e-15). torch.min's gradient on ties is split half and half, which for
+ * PPO makes the gradient flow through iw u whenever iw is inside the clip range or iw u <
+ * clip(iw) u. Returns 0, -1 without logs, -2 on a NaN loss (the reference exits). epochs
+ * [3] = (0, imitation, policy). */
+/* one epoch of a policy-learning loss: the float32 loss and gradient (mean over the n
+ * records) at pol */
+static float pl_epoch(int64_t n, const float *cf, const float *vf, const float *gf, const double *prop,
+                      const double *util, const float *pol, int32_t loss_kind, double (*acc)[PL_NV],
+                      float *grad) {
+  const double inv_sqrt2pi = 1.0 / sqrt(2.0 * 3.141592653589793);
+  memset(acc, 0, sizeof(double[PL_LANES][PL_NV]));
+  for (int64_t i = 0; i < n; ++i) {
+    polf_t f;
+    const double c = cf[i], v = vf[i], g = (double)gf[i];
+    policy_fwd(pol, c, v, &f);
+    const double mu = f.mu, sg = f.sigma;
+    const double zz = (mu - g) / sg;
+    const double pdf_raw = exp(-(zz * zz) / 2.0) / sg * inv_sqrt2pi;
+    const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
+    const double p0 = (double)fmaxf((float)prop[i], 1e-15f);
+    const double u = (double)(float)util[i];
+    double term = 0.0, kl = 0.0, dpi = 0.0, dmu = 0.0, dsg = 0.0;
+    if (loss_kind == 0) {
+      term = -(pi * u);
+      dpi = -u;
+    } else if (loss_kind == 1 || loss_kind == 2) {
+      term = -((pi / p0) * u);
+      dpi = -u / p0;
+      if (loss_kind == 2) {
+        kl = (sg * sg + (mu - g) * (mu - g)) / (2.0 * sg * sg) - 0.5;
+        dmu = 5e-2 * ((mu - g) / (sg * sg));
+        dsg = 5e-2 * (-((mu - g) * (mu - g)) / (sg * sg * sg));
+      }
+    } else {
+      const double iw = pi / p0;
+      const int in_range = iw >= 1.0 / 50.0 && iw <= 50.0;
+      const double iwc = iw < 1.0 / 50.0 ? 1.0 / 50.0 : (iw > 50.0 ? 50.0 : iw);
+      const double A = iw * u, Bc = iwc * u;
+      term = -(A < Bc ? A : Bc);
+      dpi = (in_range || A < Bc) ? -u / p0 : 0.0;
+    }
+    if (pdf_raw >= 1e-30 && dpi != 0.0) {
+      dmu += dpi * pdf_raw * (g - mu) / (sg * sg);
+      dsg += dpi * pdf_raw * ((g - mu) * (g - mu) / (sg * sg * sg) - 1.0 / sg);
+    }
+    double gr[12];
+    policy_grad(pol, c, v, &f, dmu, dsg, gr);
+    double *a = acc[i % PL_LANES];
+    for (int j = 0; j < 12; ++j) a[j] += gr[j];
+    a[12] += term;
+    a[13] += kl;
+  }
+  double tot[PL_NV];
+  pl_lane_sums(acc, tot);
+  for (int j = 0; j < 12; ++j) grad[j] = (float)(tot[j] / (double)n);
+  return (float)(tot[12] / (double)n + (tot[13] / (double)n) * 5e-2);
+}
+
+static float *to_f32(int64_t n, const double *x) {
+  float *f = malloc(n * sizeof(float));
+  for (int64_t i = 0; i < n; ++i) f[i] = (float)x[i];
+  return f;
+}
+
+float ora_pl_loss_grad(int64_t n, const double *ctr, const double *value, const double *gamma,
+                       const double *prop, const double *util, const float *pol, int32_t loss_kind,
+                       float *grad) {
+  float *cf = to_f32(n, ctr), *vf = to_f32(n, value), *gf = to_f32(n, gamma);
+  double (*acc)[PL_NV] = malloc(sizeof(double[PL_LANES][PL_NV]));
+  const float loss = pl_epoch(n, cf, vf, gf, prop, util, pol, loss_kind, acc, grad);
+  free(acc);
+  free(cf);
+  free(vf);
+  free(gf);
+  return loss;
+}
+
+int32_t ora_pl_update(int64_t n, const double *ctr, const double *value, const double *gamma,
+                      const double *prop, const double *util, float *pol, int32_t initialised,
+                      int32_t loss_kind, int32_t *epochs, float *init_trace, float *pl_trace) {
+  epochs[0] = epochs[1] = epochs[2] = 0;
+  if (n < 1) return -1;
+  float *cf = to_f32(n, ctr), *vf = to_f32(n, value), *gf = to_f32(n, gamma);
+  if (!initialised) epochs[1] = fit_imitation(n, cf, vf, gf, pol, init_trace);
+  double (*acc)[PL_NV] = malloc(sizeof(double[PL_LANES][PL_NV]));
+  adam_t ad;
+  adam_init(&ad, 12, 2e-3, 1e-4);
+  plateau_t pl;
+  plateau_init(&pl, 100, 0.2, 1e-8, 1e-4);
+  stopper_t st = {INFINITY, -1, 512};
+  int32_t e = 0, rc = 0;
+  for (; e < 16384; ++e) {
+    float grad[12];
+    const float loss = pl_epoch(n, cf, vf, gf, prop, util, pol, loss_kind, acc, grad);
+    adam_step(&ad, pol, grad);
+    if (pl_trace) pl_trace[e] = loss;
+    plateau_step(&pl, loss, &ad.lr);
+    const int stop = stop_step(&st, e, loss);
+    if (loss != loss) rc = -2;
+    if (stop || rc) {
+      ++e;
+      break;
+    }
+  }
+  epochs[2] = e;
+  free(acc);
+  free(cf);
+  free(vf);
+  free(gf);
+  return rc;
 }

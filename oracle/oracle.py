@@ -88,6 +88,12 @@ def lib():
         L.ora_empirical_update.argtypes = [i64, vp, vp, vp]
         L.ora_dr_update.restype = i32
         L.ora_dr_update.argtypes = [i64] + [vp] * 8 + [i32, vp, i64] + [vp] * 5
+        L.ora_vl_update.restype = i32
+        L.ora_vl_update.argtypes = [i64] + [vp] * 6 + [i32, vp, i64] + [vp] * 3
+        L.ora_pl_update.restype = i32
+        L.ora_pl_update.argtypes = [i64] + [vp] * 6 + [i32, i32] + [vp] * 3
+        L.ora_pl_loss_grad.restype = ctypes.c_float
+        L.ora_pl_loss_grad.argtypes = [i64] + [vp] * 6 + [i32, vp]
         L.ora_log1p_restated.restype = d
         L.ora_log1p_restated.argtypes = [d]
         L.ora_lrts_update.restype = i32
@@ -288,3 +294,53 @@ def dr_update(ctr, value, gamma, prop, won, util, wr, pol, initialised, noise, t
     return {"wr": wr, "pol": pol, "epochs": ep.copy(), "wr_losses": tr[0][:ep[0]].astype(np.float64),
             "init_losses": tr[1][:ep[1]].astype(np.float64), "dr_losses": tr[2][:ep[2]].astype(np.float64),
             "est_util": eu}
+
+
+PL_LOSSES = {"REINFORCE": 0, "REINFORCE_offpolicy": 1, "TRPO": 2, "PPO": 3}
+
+
+def vl_update(ctr, value, gamma, won, wr, pol, policy, noise, trace=True):
+    """ValueLearningBidder.update (src/Bidder.py:204-325) of one agent; noise [E][n] float32
+    per-epoch rsample draws of the policy fit (policy=True). Returns dict(wr, pol, epochs,
+    wr_losses, pol_losses, fallback)."""
+    n = len(ctr)
+    a = [np.ascontiguousarray(v, np.float64) for v in (ctr, value, gamma)]
+    w = np.ascontiguousarray(np.asarray(won) != 0, np.uint8)
+    wr = np.array(wr, np.float32).ravel().copy()
+    pol = np.array(pol, np.float32).ravel().copy()
+    noise = np.ascontiguousarray(noise if noise is not None else np.zeros((0, n)), np.float32)
+    E = noise.shape[0] if noise.size else 0
+    ep = np.zeros(3, np.int32)
+    tr = [np.zeros(32768, np.float32), np.zeros(16384, np.float32)]
+    rc = lib().ora_vl_update(n, *[_p(v) for v in a], _p(w), _p(wr), _p(pol), int(bool(policy)), _p(noise), E,
+                             _p(ep), *[(_p(t) if trace else None) for t in tr])
+    if rc < 0:
+        raise ValueError("ValueLearningBidder.update without logs")
+    return {"wr": wr, "pol": pol, "epochs": ep.copy(), "fallback": rc == 1,
+            "wr_losses": tr[0][:ep[0]].astype(np.float64), "pol_losses": tr[1][:ep[2]].astype(np.float64)}
+
+
+def pl_update(ctr, value, gamma, prop, util, pol, initialised, loss="PPO", trace=True):
+    """PolicyLearningBidder.update (src/Bidder.py:364-431) of one agent. Returns dict(pol,
+    epochs, init_losses, pl_losses, nan)."""
+    n = len(ctr)
+    a = [np.ascontiguousarray(v, np.float64) for v in (ctr, value, gamma, prop, util)]
+    pol = np.array(pol, np.float32).ravel().copy()
+    ep = np.zeros(3, np.int32)
+    tr = [np.zeros(16384, np.float32), np.zeros(16384, np.float32)]
+    rc = lib().ora_pl_update(n, *[_p(v) for v in a], _p(pol), int(bool(initialised)), PL_LOSSES[loss], _p(ep),
+                             *[(_p(t) if trace else None) for t in tr])
+    if rc == -1:
+        raise ValueError("PolicyLearningBidder.update without logs")
+    return {"pol": pol, "epochs": ep.copy(), "nan": rc == -2,
+            "init_losses": tr[0][:ep[1]].astype(np.float64), "pl_losses": tr[1][:ep[2]].astype(np.float64)}
+
+
+def pl_loss_grad(ctr, value, gamma, prop, util, pol, loss="PPO"):
+    """One epoch of a PolicyLearningBidder loss (src/Models.py:174-199) at pol: (loss, grad[12])."""
+    n = len(ctr)
+    a = [np.ascontiguousarray(v, np.float64) for v in (ctr, value, gamma, prop, util)]
+    pol = np.ascontiguousarray(pol, np.float32).ravel()
+    g = np.zeros(12, np.float32)
+    loss_v = lib().ora_pl_loss_grad(n, *[_p(v) for v in a], _p(pol), PL_LOSSES[loss], _p(g))
+    return float(loss_v), g

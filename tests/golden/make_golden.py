@@ -486,6 +486,116 @@ def dr_update_kat(out_name="dr_update_kat", rounds=2048):
     np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
 
 
+def learner_update_kat(cfg_name, out_name, rounds=2048):
+    """ValueLearningBidder (FP_DM_TS.json, inference 'policy') and PolicyLearningBidder
+    (FP_IPS_TS.json, loss 'PPO') .update (src/Bidder.py:204-325, :364-431) on the logs of the
+    config's first iteration, through the reference's own classes: the update's inputs, the
+    models' parameters before / after, every scheduled fit's per-epoch losses and the torch
+    RNG state it started from (the DM policy fit's per-epoch rsample noise), the imitation
+    result (first PolicyLearningBidder update), and the torch RNG state after the update
+    (PolicyLearningBidder draws one rsample per record after its fit, :423)."""
+    import torch
+    import Models
+    _, _, _, (agents, _, _) = capture(load_cfg(cfg_name), rounds, keep=True)
+    recs = []
+
+    class RecRP(torch.optim.lr_scheduler.ReduceLROnPlateau):
+        def __init__(self, *a, verbose=None, **k):
+            super().__init__(*a, **k)
+            self.rec = {"rng": torch.get_rng_state().clone(), "losses": []}
+            recs.append(self.rec)
+
+        def step(self, metrics, *a, **k):
+            self.rec["losses"].append(float(metrics))
+            return super().step(metrics, *a, **k)
+
+    init_snap = {}
+    orig_init = Models.BidShadingContextualBandit.initialise_policy
+
+    def rec_init(self, X, gammas):
+        orig_init(self, X, gammas)
+        init_snap["params"] = [p.detach().numpy().copy() for p in self.parameters()]
+
+    def params(mod):
+        return [p.detach().numpy().copy() for p in mod.parameters()]
+
+    mse_log = []
+
+    class RecMSE(torch.nn.MSELoss):  # the imitation's two MSE terms per epoch (no scheduler)
+        def forward(self, a, b):
+            r = super().forward(a, b)
+            mse_log.append(r.detach().clone())
+            return r
+
+    saved = torch.optim.lr_scheduler.ReduceLROnPlateau
+    saved_mse = torch.nn.MSELoss
+    torch.optim.lr_scheduler.ReduceLROnPlateau = RecRP
+    torch.nn.MSELoss = RecMSE
+    Models.BidShadingContextualBandit.initialise_policy = rec_init
+    out = {}
+    try:
+        for i, ag in enumerate(agents):
+            b = ag.bidder
+            L = ag.logs
+            k = f"a{i}_"
+            mse_log.clear()
+            out[k + "est_ctr"] = np.array([o.estimated_CTR for o in L])
+            out[k + "value"] = np.array([o.value for o in L])
+            out[k + "price"] = np.array([o.price for o in L])
+            out[k + "outcome"] = np.array([o.outcome for o in L]).astype(np.int8)
+            won = np.array([o.won for o in L])
+            out[k + "won"] = won.astype(np.int8)
+            out[k + "gamma"] = np.array([float(g) for g in b.gammas])
+            out[k + "propensity"] = np.array([float(p) for p in b.propensities])
+            util = np.zeros(len(L))
+            util[won] = out[k + "value"][won] * out[k + "outcome"][won] - out[k + "price"][won]
+            out[k + "util"] = util
+            mods = {"wr": getattr(b, "winrate_model", None),
+                    "pol": getattr(b, "bidding_policy", None) or getattr(b, "model", None)}
+            for name, mod in mods.items():
+                if mod is not None:
+                    for j, p in enumerate(params(mod)):
+                        out[k + f"{name}0_{j}"] = p
+            recs.clear()
+            init_snap.clear()
+            ag.update(iteration=0)  # LR-TS allocator update, then the bidder's
+            out[k + "rng_after"] = torch.get_rng_state().numpy()
+            fits = recs[1:]  # recs[0]: the LR-TS allocator's scheduler
+            for j, r in enumerate(fits):
+                out[k + f"fit{j}_losses"] = np.array(r["losses"])
+                out[k + f"fit{j}_rng"] = r["rng"].numpy()
+            if init_snap:
+                for j, p in enumerate(init_snap["params"]):
+                    out[k + f"pol_init_{j}"] = p
+                out[k + "init_losses"] = np.array([(mse_log[2 * e] + mse_log[2 * e + 1]).item()
+                                                   for e in range(len(mse_log) // 2)])
+            if hasattr(b, "model"):  # every PolicyLearningBidder loss at the imitation result
+                import copy
+                Xc = torch.Tensor(np.hstack((out[k + "est_ctr"].reshape(-1, 1), out[k + "value"].reshape(-1, 1))))
+                gt = torch.Tensor(out[k + "gamma"])
+                pr = torch.clip(torch.Tensor(out[k + "propensity"]), min=1e-15)
+                for name in ("REINFORCE", "REINFORCE_offpolicy", "TRPO", "PPO"):
+                    m = copy.deepcopy(b.model)
+                    with torch.no_grad():
+                        for p, v in zip(m.parameters(), init_snap["params"]):
+                            p.copy_(torch.from_numpy(v))
+                    m.loss_name = name
+                    loss = m.loss(Xc, gt, pr, torch.Tensor(util), importance_weight_clipping_eps=50.0)
+                    loss.backward()
+                    out[k + f"loss0_{name}"] = np.array(loss.item())
+                    out[k + f"grad0_{name}"] = np.concatenate([p.grad.numpy().ravel() for p in m.parameters()])
+            for name, mod in mods.items():
+                if mod is not None:
+                    for j, p in enumerate(params(mod)):
+                        out[k + f"{name}1_{j}"] = p
+            print(cfg_name, "agent", i, "n", len(L), "fits", [len(r["losses"]) for r in fits], flush=True)
+    finally:
+        torch.optim.lr_scheduler.ReduceLROnPlateau = saved
+        torch.nn.MSELoss = saved_mse
+        Models.BidShadingContextualBandit.initialise_policy = orig_init
+    np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
+
+
 def sigmoid_kats():
     """Reference sigmoid (numba-faithful shim) on OracleAllocator-shaped dots."""
     import Models
@@ -630,7 +740,8 @@ def csv_outputs(runs=2, iters=3, rounds=2000):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also run SP_Oracle as shipped (3x20x10k rounds, ~1 min)")
-    ap.add_argument("--only", choices=["empirical", "csv", "dr"], help="regenerate one fixture family only")
+    ap.add_argument("--which", choices=["dm", "ips"], help="with --only learners: one config")
+    ap.add_argument("--only", choices=["empirical", "csv", "dr", "learners"], help="regenerate one fixture family only")
     args = ap.parse_args()
     install_shims()
     if args.only == "empirical":
@@ -641,6 +752,11 @@ def main():
         return
     if args.only == "dr":
         dr_update_kat()
+    if args.only == "learners":
+        if args.which in (None, "dm"):
+            learner_update_kat("FP_DM_TS.json", "dm_update_kat")
+        if args.which in (None, "ips"):
+            learner_update_kat("FP_IPS_TS.json", "ips_update_kat")
         return
 
     sigmoid_kats()
