@@ -85,7 +85,8 @@ class AuctionEngine:
         pg = None if prev_gamma is None else np.ascontiguousarray(prev_gamma, np.float64)
         gs = None if gamma_sigma is None else np.ascontiguousarray(gamma_sigma, np.float64)
         self.shading = bool((b != _lib.BIDDER_TRUTHFUL).any())
-        self.dr = bool((b == _lib.BIDDER_DOUBLY_ROBUST).any())
+        self.dr = bool(np.isin(b, (_lib.BIDDER_VALUE_LEARNING, _lib.BIDDER_POLICY_LEARNING,
+                                   _lib.BIDDER_DOUBLY_ROBUST)).any())  # learning bidders
         self.lrts = bool((a == _lib.ALLOCATOR_LRTS).any())
         self._check(self.L.ag_set_agent_params(self._h, a.ctypes.data, b.ctypes.data,
                                                None if pg is None else pg.ctypes.data,
@@ -302,7 +303,8 @@ class AuctionEngine:
         return c
 
     def set_dr_state(self, state, initialised):
-        """DoublyRobustBidder models, float32 [N][16] (win-rate w0 w1 w2 b, policy 12)."""
+        """Learning bidders' models, float32 [N][16] (win-rate w0 w1 w2 b, policy 12), and what
+        each bids from (LEARNER_*)."""
         st = np.ascontiguousarray(state, np.float32).reshape(self.N, 16)
         ini = np.ascontiguousarray(initialised, np.int32).reshape(self.N)
         self._check(self.L.ag_set_dr_state(self._h, st.ctypes.data, ini.ctypes.data), "ag_set_dr_state")
@@ -324,6 +326,26 @@ class AuctionEngine:
                                         off.ctypes.data, int(noise_epochs), ep.ctypes.data, _ptr(tr),
                                         _stream()), "ag_dr_update")
         return (ep, tr) if trace else ep
+
+    def set_bidder_modes(self, modes):
+        """ValueLearningBidder inference (VL_SEARCH / VL_POLICY) / PolicyLearningBidder loss
+        (PL_LOSSES) per agent, int32 [N] (ag_set_bidder_modes)."""
+        m = np.ascontiguousarray(modes, np.int32).reshape(self.N)
+        self._check(self.L.ag_set_bidder_modes(self._h, m.ctypes.data), "ag_set_bidder_modes")
+
+    def bidder_update(self, store, noise=None, noise_offsets=None, noise_epochs=0, trace=False):
+        """Bidder.update of every learning bidder (ag_bidder_update). noise: float32 device
+        tensor with agent a's per-epoch rsample draws at noise_offsets[a] (rows of its record
+        count), for DoublyRobust / ValueLearning 'policy' agents. Returns (epochs [N][3],
+        status [N]) and, with trace=True, the traces [N][3][32768]."""
+        ep = np.zeros((self.N, 3), np.int32)
+        stat = np.zeros(self.N, np.int32)
+        off = np.ascontiguousarray(noise_offsets if noise_offsets is not None else np.zeros(self.N), np.int64)
+        tr = torch.zeros((self.N, 3, 32768), dtype=torch.float32, device=self.device) if trace else None
+        self._check(self.L.ag_bidder_update(self._h, ctypes.byref(self._shading(store)), _ptr(noise),
+                                            off.ctypes.data, int(noise_epochs), ep.ctypes.data, stat.ctypes.data,
+                                            _ptr(tr), _stream()), "ag_bidder_update")
+        return (ep, stat, tr) if trace else (ep, stat)
 
     def shading_collect(self, inputs, outputs, store, first_auction=0):
         """Append the shading-bidder records of a simulated batch of auctions

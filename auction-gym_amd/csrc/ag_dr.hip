@@ -170,212 +170,410 @@ struct DrRecords {
   const uint8_t *won;
 };
 
-__global__ __launch_bounds__(kDrThreads) void k_dr_train(
-    const int32_t *__restrict__ bkind, const int64_t *__restrict__ offsets, DrRecords R,
-    double *__restrict__ eu_ws, float *__restrict__ state, const int32_t *__restrict__ initialised,
+// LDS of one agent's workgroup
+struct TrainLds {
+  uint64_t tab[256];
+  float wr[4], pol[12];
+  int64_t w[kDrThreads / 64][32];
+  int64_t tot[32];
+  double wf[kDrThreads / 64][16];
+  double ftot[16];
+  AdamState adam;
+  int stop;
+};
+
+__device__ __forceinline__ void adam_reset(TrainLds &S) {
+  if (threadIdx.x < 16) S.adam.ea[threadIdx.x] = S.adam.es[threadIdx.x] = S.adam.mx[threadIdx.x] = 0.0f;
+  __syncthreads();
+}
+
+// Fixed-order double sums (the policy-learning fits: importance weights are unbounded, so
+// their terms do not fit a fixed-point grid). Record i is added by thread i mod 256 in
+// record order; each wave combines by the butterfly v + shfl_xor(v, o), o = 32 .. 1 (the
+// same value on every lane); the wave totals are added to 0.0 in wave order. oracle/
+// ag_oracle_dr.c pl_lane_sums is this order exactly.
+template <int NV>
+__device__ __forceinline__ void block_fsums(const double (&v)[NV], TrainLds &S) {
+  static_assert(NV <= 16, "block_fsums: at most 16 sums");
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    double x = v[j];
+    for (int o = 32; o > 0; o >>= 1) x = x + __shfl_xor(x, o, 64);
+    if (lane == 0) S.wf[wv][j] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    double t = 0.0;
+    for (int w = 0; w < kDrThreads / 64; ++w) t += S.wf[w][threadIdx.x];
+    S.ftot[threadIdx.x] = t;
+  }
+  __syncthreads();
+}
+
+// one Adam step of the first np parameters of `par` (thread j: parameter j)
+__device__ __forceinline__ void adam_step_block(TrainLds &S, float *par, int np, float grad, int step, double lr,
+                                                float wd, const double *adam_tab) {
+  double bc1;
+  float bc2f;
+  bias_corrections(step, adam_tab, bc2f, bc1);
+  const float neg_step = (float)(-(lr / bc1));
+  if ((int)threadIdx.x < np) {
+    float p = par[threadIdx.x];
+    adam_param(p, grad, threadIdx.x, S.adam, neg_step, bc2f, wd);
+    par[threadIdx.x] = p;
+  }
+}
+
+// PyTorchWinRateEstimator fit (src/Bidder.py:229-252 ValueLearningBidder, :500-530
+// DoublyRobustBidder): BCE (mean) over the logs plus the gamma = 0, y = 0 augmentation,
+// Adam(lr 3e-3, wd 1e-6, AMSGrad), ReduceLROnPlateau(patience, factor, min_lr 1e-7),
+// early stop after `wait` epochs without a 1e-6 improvement, <= 32768 epochs.
+__device__ int fit_winrate(const DrRecords &R, int64_t n, TrainLds &S, int patience, double factor, int wait,
+                           const double *adam_tab, float *tr) {
+  const int tid = threadIdx.x;
+  adam_reset(S);
+  double lr = 3e-3;
+  Plateau pl{INFINITY, 1e-4, factor, 1e-7, 0, patience};
+  Stopper sp{INFINITY, -1, wait};
+  const double M = 2.0 * (double)n;
+  int e = 0;
+  for (; e < kWrEpochs; ++e) {
+    int64_t acc[5] = {0, 0, 0, 0, 0};
+    for (int64_t r = tid; r < 2 * n; r += kDrThreads) {
+      const int64_t i = r < n ? r : r - n;
+      const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i];
+      const double g = r < n ? (double)(float)R.gamma[i] : 0.0;
+      const double y = r < n ? (double)R.won[i] : 0.0;
+      const double z = c * (double)S.wr[0] + v * (double)S.wr[1] + g * (double)S.wr[2] + (double)S.wr[3];
+      const double pw = 1.0 / (1.0 + agexp::exp(-z, S.tab));
+      const double t = y > 0.0 ? fmin(softplus(-z, S.tab), 100.0) : fmin(softplus(z, S.tab), 100.0);
+      acc[0] += fxr(t);
+      const double gz = pw - y;
+      acc[1] += fxr(gz * c);
+      acc[2] += fxr(gz * v);
+      acc[3] += fxr(gz * g);
+      acc[4] += fxr(gz);
+    }
+    block_sums<5>(acc, S.w, S.tot);
+    // every thread: the same loss; threads 0..3 step their parameter
+    const float loss = (float)(fxv(S.tot[0], S.tot[1]) / M);
+    const float g = tid < 4 ? (float)(fxv(S.tot[2 + 2 * tid], S.tot[3 + 2 * tid]) / M) : 0.0f;
+    adam_step_block(S, S.wr, 4, g, e, lr, (float)1e-6, adam_tab);
+    if (tid == 0 && tr) tr[e] = loss;
+    plateau_step(pl, loss, lr);  // every thread keeps the same scheduler state
+    const bool stop = stop_step(sp, e, loss);
+    __syncthreads();
+    if (stop) return e + 1;
+  }
+  return e;
+}
+
+// BidShadingContextualBandit.initialise_policy (src/Models.py:106-137): imitation of the
+// logging policy, MSE of mu to the logged gammas + MSE of softplus(sigma) (without
+// min_sigma) to 0.05; Adam(lr 1e-3, wd 1e-4, AMSGrad), early stop after 512 epochs.
+__device__ int fit_imitation(const DrRecords &R, int64_t n, TrainLds &S, const double *adam_tab, float *tr) {
+  const int tid = threadIdx.x;
+  adam_reset(S);
+  Stopper sp{INFINITY, -1, 512};
+  int e = 0;
+  for (; e < kInitEpochs; ++e) {
+    int64_t acc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0;
+    for (int64_t i = tid; i < n; i += kDrThreads) {
+      const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i];
+      PolF f;
+      policy_fwd(S.pol, c, v, f, S.tab);
+      const double dm = f.mu - (double)(float)R.gamma[i], dsg = f.sp_sigma - 0.05;
+      acc[12] += fxr(dm * dm);
+      acc[13] += fxr(dsg * dsg);
+      policy_bwd(S.pol, c, v, f, 2.0 * dm, 2.0 * dsg, acc, 0, S.tab);
+    }
+    block_sums<16>(acc, S.w, S.tot);
+    const float loss = (float)(fxv(S.tot[24], S.tot[25]) / (double)n + fxv(S.tot[26], S.tot[27]) / (double)n);
+    const float g = tid < 12 ? (float)(fxv(S.tot[2 * tid], S.tot[2 * tid + 1]) / (double)n) : 0.0f;
+    adam_step_block(S, S.pol, 12, g, e, 1e-3, (float)1e-4, adam_tab);
+    if (tid == 0 && tr) tr[e] = loss;
+    const bool stop = stop_step(sp, e, loss);
+    __syncthreads();
+    if (stop) return e + 1;
+  }
+  return e;
+}
+
+// DoublyRobustBidder's policy fit (src/Bidder.py:562-590, src/Models.py:201-218): loss
+// -mean((u - u^) clip(pi / pi0, 1/50, 50) + W(ctr, value, g~) (V - V g~)), g~ = clip(mu +
+// sigma eps, 0, 1); Adam(lr 7e-3, wd 1e-4, AMSGrad), ReduceLROnPlateau(patience 100, factor
+// 0.2, min_lr 1e-8, threshold 5e-3), early stop after 512 epochs, <= 32768 epochs.
+__device__ int fit_dr(const DrRecords &R, const double *eu, int64_t n, TrainLds &S, const float *nz,
+                      int noise_epochs, const double *adam_tab, float *tr) {
+  const int tid = threadIdx.x;
+  adam_reset(S);
+  double lr = 7e-3;
+  Plateau pl{INFINITY, 5e-3, 0.2, 1e-8, 0, 100};
+  Stopper sp{INFINITY, -1, 512};
+  const double inv_sqrt2pi = 1.0 / __builtin_sqrt(2.0 * 3.141592653589793);
+  int e = 0;
+  for (; e < kDrEpochs && e < noise_epochs; ++e) {
+    const float *eps = nz + (int64_t)e * n;
+    int64_t acc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0;
+    for (int64_t i = tid; i < n; i += kDrThreads) {
+      const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i], g = (double)(float)R.gamma[i];
+      PolF f;
+      policy_fwd(S.pol, c, v, f, S.tab);
+      const double mu = f.mu, sg = f.sigma;
+      const double zz = (mu - g) / sg;
+      const double pdf_raw = agexp::exp(-(zz * zz) / 2.0, S.tab) / sg * inv_sqrt2pi;
+      const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
+      const double p0 = (double)fmaxf((float)R.prop[i], 1e-15f);
+      const double iw = pi / p0;
+      const double iwc = iw < 1.0 / 50.0 ? 1.0 / 50.0 : (iw > 50.0 ? 50.0 : iw);
+      const double du = (double)(float)R.util[i] - (double)(float)eu[i];
+      const double ep = (double)eps[i];
+      const double raw = mu + sg * ep;
+      const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
+      const double zw = c * (double)S.wr[0] + v * (double)S.wr[1] + gs * (double)S.wr[2] + (double)S.wr[3];
+      const double Wv = 1.0 / (1.0 + agexp::exp(-zw, S.tab));
+      const double V = c * v;
+      acc[12] += fxr(-(du * iwc + Wv * (V - V * gs)));
+      double dpi_dmu = 0.0, dpi_dsg = 0.0;
+      if (pdf_raw >= 1e-30 && iw >= 1.0 / 50.0 && iw <= 50.0) {
+        const double k = du / p0;
+        dpi_dmu = k * pdf_raw * (g - mu) / (sg * sg);
+        dpi_dsg = k * pdf_raw * ((g - mu) * (g - mu) / (sg * sg * sg) - 1.0 / sg);
+      }
+      double ddm = 0.0;
+      if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)S.wr[2];
+      policy_bwd(S.pol, c, v, f, -(dpi_dmu + ddm), -(dpi_dsg + ddm * ep), acc, 0, S.tab);
+    }
+    block_sums<16>(acc, S.w, S.tot);
+    const float loss = (float)(fxv(S.tot[24], S.tot[25]) / (double)n);
+    const float g = tid < 12 ? (float)(fxv(S.tot[2 * tid], S.tot[2 * tid + 1]) / (double)n) : 0.0f;
+    adam_step_block(S, S.pol, 12, g, e, lr, (float)1e-4, adam_tab);
+    if (tid == 0 && tr) tr[e] = loss;
+    plateau_step(pl, loss, lr);
+    const bool stop = stop_step(sp, e, loss);
+    if (tid == 0 && loss != loss) S.stop = 1;  // NaN: the reference exits (src/Bidder.py:592-600)
+    __syncthreads();
+    if (stop || S.stop) return e + 1;
+  }
+  return e;
+}
+
+// ValueLearningBidder's policy fit (inference 'policy', src/Bidder.py:258-303): loss
+// -mean(W(ctr, value, g~) (V - V g~)), g~ = clip(mu + sigma eps, 0, 1); Adam(lr 2e-3, wd
+// 1e-6, AMSGrad), ReduceLROnPlateau(patience 100, factor 0.1, min_lr 1e-7), early stop after
+// 256 epochs, <= 16384 epochs. Exact fixed-point sums (bounded terms).
+__device__ int fit_dm(const DrRecords &R, int64_t n, TrainLds &S, const float *nz, int noise_epochs,
+                      const double *adam_tab, float *tr) {
+  const int tid = threadIdx.x;
+  adam_reset(S);
+  double lr = 2e-3;
+  Plateau pl{INFINITY, 1e-4, 0.1, 1e-7, 0, 100};
+  Stopper sp{INFINITY, -1, 256};
+  int e = 0;
+  for (; e < kInitEpochs && e < noise_epochs; ++e) {
+    const float *eps = nz + (int64_t)e * n;
+    int64_t acc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0;
+    for (int64_t i = tid; i < n; i += kDrThreads) {
+      const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i];
+      PolF f;
+      policy_fwd(S.pol, c, v, f, S.tab);
+      const double ep = (double)eps[i];
+      const double raw = f.mu + f.sigma * ep;
+      const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
+      const double zw = c * (double)S.wr[0] + v * (double)S.wr[1] + gs * (double)S.wr[2] + (double)S.wr[3];
+      const double Wv = 1.0 / (1.0 + agexp::exp(-zw, S.tab));
+      const double V = c * v;
+      acc[12] += fxr(-(Wv * (V - V * gs)));
+      double ddm = 0.0;
+      if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)S.wr[2];
+      policy_bwd(S.pol, c, v, f, -ddm, -(ddm * ep), acc, 0, S.tab);
+    }
+    block_sums<16>(acc, S.w, S.tot);
+    const float loss = (float)(fxv(S.tot[24], S.tot[25]) / (double)n);
+    const float g = tid < 12 ? (float)(fxv(S.tot[2 * tid], S.tot[2 * tid + 1]) / (double)n) : 0.0f;
+    adam_step_block(S, S.pol, 12, g, e, lr, (float)1e-6, adam_tab);
+    if (tid == 0 && tr) tr[e] = loss;
+    plateau_step(pl, loss, lr);
+    const bool stop = stop_step(sp, e, loss);
+    __syncthreads();
+    if (stop) return e + 1;
+  }
+  return e;
+}
+
+// per-record gradient of a policy loss term from d/dmu and d/dsigma (policy_bwd's order)
+__device__ __forceinline__ void policy_grad(const float *p, double c, double v, const PolF &f, double dmu,
+                                            double dsigma, double (&G)[14], const uint64_t *tab) {
+  const double dam = dmu * dsoftplus(f.am, tab), das = dsigma * dsoftplus(f.as, tab);
+  double ds[2];
+  ds[0] = dam * (double)p[6] + das * (double)p[9];
+  ds[1] = dam * (double)p[7] + das * (double)p[10];
+  G[6] += dam * f.s[0];
+  G[7] += dam * f.s[1];
+  G[8] += dam;
+  G[9] += das * f.s[0];
+  G[10] += das * f.s[1];
+  G[11] += das;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const double dh = ds[j] * dsoftplus(f.h[j], tab);
+    G[2 * j] += dh * c;
+    G[2 * j + 1] += dh * v;
+    G[4 + j] += dh;
+  }
+}
+
+// PolicyLearningBidder's policy fit (src/Bidder.py:376-407, the losses of src/Models.py:
+// 174-199; AG_PL_LOSS_* kinds): Adam(lr 2e-3, wd 1e-4, AMSGrad), ReduceLROnPlateau
+// (patience 100, factor 0.2, min_lr 1e-8), early stop after 512 epochs, <= 16384 epochs.
+// oracle/ag_oracle_dr.c pl_epoch, term for term, with the same fixed-order sums.
+__device__ int fit_pl(const DrRecords &R, int64_t n, TrainLds &S, int kind, const double *adam_tab, float *tr) {
+  const int tid = threadIdx.x;
+  adam_reset(S);
+  double lr = 2e-3;
+  Plateau pl{INFINITY, 1e-4, 0.2, 1e-8, 0, 100};
+  Stopper sp{INFINITY, -1, 512};
+  const double inv_sqrt2pi = 1.0 / __builtin_sqrt(2.0 * 3.141592653589793);
+  int e = 0;
+  for (; e < kInitEpochs; ++e) {
+    double acc[14];
+#pragma unroll
+    for (int j = 0; j < 14; ++j) acc[j] = 0.0;
+    for (int64_t i = tid; i < n; i += kDrThreads) {
+      const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i], g = (double)(float)R.gamma[i];
+      PolF f;
+      policy_fwd(S.pol, c, v, f, S.tab);
+      const double mu = f.mu, sg = f.sigma;
+      const double zz = (mu - g) / sg;
+      const double pdf_raw = agexp::exp(-(zz * zz) / 2.0, S.tab) / sg * inv_sqrt2pi;
+      const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
+      const double p0 = (double)fmaxf((float)R.prop[i], 1e-15f);
+      const double u = (double)(float)R.util[i];
+      double term = 0.0, kl = 0.0, dpi = 0.0, dmu = 0.0, dsg = 0.0;
+      if (kind == AG_PL_LOSS_REINFORCE) {
+        term = -(pi * u);
+        dpi = -u;
+      } else if (kind == AG_PL_LOSS_REINFORCE_OFFPOLICY || kind == AG_PL_LOSS_TRPO) {
+        term = -((pi / p0) * u);
+        dpi = -u / p0;
+        if (kind == AG_PL_LOSS_TRPO) {
+          kl = (sg * sg + (mu - g) * (mu - g)) / (2.0 * sg * sg) - 0.5;
+          dmu = 5e-2 * ((mu - g) / (sg * sg));
+          dsg = 5e-2 * (-((mu - g) * (mu - g)) / (sg * sg * sg));
+        }
+      } else {  // PPO
+        const double iw = pi / p0;
+        const bool in_range = iw >= 1.0 / 50.0 && iw <= 50.0;
+        const double iwc = iw < 1.0 / 50.0 ? 1.0 / 50.0 : (iw > 50.0 ? 50.0 : iw);
+        const double A = iw * u, Bc = iwc * u;
+        term = -(A < Bc ? A : Bc);
+        dpi = (in_range || A < Bc) ? -u / p0 : 0.0;
+      }
+      if (pdf_raw >= 1e-30 && dpi != 0.0) {
+        dmu += dpi * pdf_raw * (g - mu) / (sg * sg);
+        dsg += dpi * pdf_raw * ((g - mu) * (g - mu) / (sg * sg * sg) - 1.0 / sg);
+      }
+      double gr[14];
+#pragma unroll
+      for (int j = 0; j < 14; ++j) gr[j] = 0.0;
+      policy_grad(S.pol, c, v, f, dmu, dsg, gr, S.tab);
+#pragma unroll
+      for (int j = 0; j < 12; ++j) acc[j] += gr[j];
+      acc[12] += term;
+      acc[13] += kl;
+    }
+    block_fsums<14>(acc, S);
+    const float loss = (float)(S.ftot[12] / (double)n + (S.ftot[13] / (double)n) * 5e-2);
+    const float g = tid < 12 ? (float)(S.ftot[tid] / (double)n) : 0.0f;
+    adam_step_block(S, S.pol, 12, g, e, lr, (float)1e-4, adam_tab);
+    if (tid == 0 && tr) tr[e] = loss;
+    plateau_step(pl, loss, lr);
+    const bool stop = stop_step(sp, e, loss);
+    if (tid == 0 && loss != loss) S.stop = 1;  // NaN: the reference exits (src/Bidder.py:409-417)
+    __syncthreads();
+    if (stop || S.stop) return e + 1;
+  }
+  return e;
+}
+
+// One workgroup per learning bidder (ValueLearning, PolicyLearning, DoublyRobust), the
+// fits of its update() in the reference's order. status: 0 trained, 1 ValueLearningBidder
+// fallback (no wins: nothing trained), -1 no logs, -2 NaN loss; epochs [3] = (win-rate,
+// imitation, policy fit); traces [3][32768].
+__global__ __launch_bounds__(kDrThreads) void k_bidder_train(
+    const int32_t *__restrict__ bkind, const int32_t *__restrict__ bmode, const int64_t *__restrict__ offsets,
+    DrRecords R0, double *__restrict__ eu_ws, float *__restrict__ state, const int32_t *__restrict__ initialised,
     const float *__restrict__ noise, const int64_t *__restrict__ noise_off, int noise_epochs,
     const double *__restrict__ adam_tab, int32_t *__restrict__ epochs_out, int32_t *__restrict__ status,
     float *__restrict__ traces) {
   const int a = blockIdx.x, tid = threadIdx.x;
+  const int bk = bkind[a];
+  const bool learner = bk == AG_BIDDER_VALUE_LEARNING || bk == AG_BIDDER_POLICY_LEARNING ||
+                       bk == AG_BIDDER_DOUBLY_ROBUST;
   const int64_t s0 = offsets[a], n = offsets[a + 1] - s0;
-  if (bkind[a] != AG_BIDDER_DOUBLY_ROBUST || n == 0) {
-    if (tid == 0) {
-      epochs_out[3 * a] = epochs_out[3 * a + 1] = epochs_out[3 * a + 2] = 0;
-      status[a] = (bkind[a] == AG_BIDDER_DOUBLY_ROBUST) ? -1 : 0;
-    }
+  if (tid == 0) epochs_out[3 * a] = epochs_out[3 * a + 1] = epochs_out[3 * a + 2] = 0;
+  if (!learner || n == 0) {
+    if (tid == 0) status[a] = learner ? -1 : 0;
     return;
   }
-  __shared__ uint64_t s_tab[256];
-  __shared__ float s_wr[4], s_pol[12];
-  __shared__ int64_t s_w[kDrThreads / 64][32];
-  __shared__ int64_t s_tot[32];
-  __shared__ AdamState s_adam;
-  __shared__ int s_stop;
-  for (int i = tid; i < 256; i += kDrThreads) s_tab[i] = ag_exp_tab[i];
+  __shared__ TrainLds S;
+  for (int i = tid; i < 256; i += kDrThreads) S.tab[i] = ag_exp_tab[i];
   float *st = state + (size_t)a * 16;
-  if (tid < 4) s_wr[tid] = st[tid];
-  if (tid < 12) s_pol[tid] = st[4 + tid];
-  if (tid < 16) s_adam.ea[tid] = s_adam.es[tid] = s_adam.mx[tid] = 0.0f;
-  if (tid == 0) s_stop = 0;
+  if (tid < 4) S.wr[tid] = st[tid];
+  if (tid < 12) S.pol[tid] = st[4 + tid];
+  if (tid == 0) S.stop = 0;
   __syncthreads();
-  const double *ctr = R.ctr + s0, *val = R.value + s0, *gam = R.gamma + s0, *prop = R.prop + s0,
-               *util = R.util + s0;
-  const uint8_t *won = R.won + s0;
-  double *eu = eu_ws + s0;
+  DrRecords R{R0.ctr + s0, R0.value + s0, R0.gamma + s0, R0.prop + s0, R0.util + s0, R0.won + s0};
   float *tr = traces ? traces + (size_t)a * 3 * kDrEpochs : nullptr;
-
-  // ---------------- 1. win-rate fit
-  {
-    double lr = 3e-3;
-    Plateau pl{INFINITY, 1e-4, 0.2, 1e-7, 0, 256};
-    Stopper sp{INFINITY, -1, 1024};
-    const double M = 2.0 * (double)n;
-    int e = 0;
-    for (; e < kWrEpochs; ++e) {
-      int64_t acc[5] = {0, 0, 0, 0, 0};
-      for (int64_t r = tid; r < 2 * n; r += kDrThreads) {
-        const int64_t i = r < n ? r : r - n;
-        const double c = (double)(float)ctr[i], v = (double)(float)val[i];
-        const double g = r < n ? (double)(float)gam[i] : 0.0;
-        const double y = r < n ? (double)won[i] : 0.0;
-        const double z = c * (double)s_wr[0] + v * (double)s_wr[1] + g * (double)s_wr[2] + (double)s_wr[3];
-        const double pw = 1.0 / (1.0 + agexp::exp(-z, s_tab));
-        const double t = y > 0.0 ? fmin(softplus(-z, s_tab), 100.0) : fmin(softplus(z, s_tab), 100.0);
-        acc[0] += fxr(t);
-        const double gz = pw - y;
-        acc[1] += fxr(gz * c);
-        acc[2] += fxr(gz * v);
-        acc[3] += fxr(gz * g);
-        acc[4] += fxr(gz);
-      }
-      block_sums<5>(acc, s_w, s_tot);
-      // every thread: the same loss; threads 0..3 step their parameter
-      const float loss = (float)(fxv(s_tot[0], s_tot[1]) / M);
-      double bc1;
-      float bc2f;
-      bias_corrections(e, adam_tab, bc2f, bc1);
-      const float neg_step = (float)(-(lr / bc1));
-      if (tid < 4) {
-        const float g = (float)(fxv(s_tot[2 + 2 * tid], s_tot[3 + 2 * tid]) / M);
-        float p = s_wr[tid];
-        adam_param(p, g, tid, s_adam, neg_step, bc2f, (float)1e-6);
-        s_wr[tid] = p;
-      }
-      if (tid == 0 && tr) tr[e] = loss;
-      plateau_step(pl, loss, lr);  // every thread keeps the same scheduler state
-      const bool stop = stop_step(sp, e, loss);
-      __syncthreads();
-      if (stop) {
-        ++e;
-        break;
-      }
+  int ep[3] = {0, 0, 0};
+  int stat = 0;
+  if (bk == AG_BIDDER_DOUBLY_ROBUST) {
+    ep[0] = fit_winrate(R, n, S, 256, 0.2, 1024, adam_tab, tr);
+    // estimated utilities with the fitted model (src/Bidder.py:541-546)
+    double *eu = eu_ws + s0;
+    for (int64_t i = tid; i < n; i += kDrThreads) {
+      const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i], g = (double)(float)R.gamma[i];
+      const double z = c * (double)S.wr[0] + v * (double)S.wr[1] + g * (double)S.wr[2] + (double)S.wr[3];
+      const float W = (float)(1.0 / (1.0 + agexp::exp(-z, S.tab)));
+      const double V = R.ctr[i] * R.value[i], P = R.ctr[i] * R.value[i] * R.gamma[i];
+      eu[i] = (double)W * (V - P);
     }
-    if (tid == 0) epochs_out[3 * a] = e;
-  }
-  // ---------------- 2. estimated utilities with the fitted model
-  for (int64_t i = tid; i < n; i += kDrThreads) {
-    const double c = (double)(float)ctr[i], v = (double)(float)val[i], g = (double)(float)gam[i];
-    const double z = c * (double)s_wr[0] + v * (double)s_wr[1] + g * (double)s_wr[2] + (double)s_wr[3];
-    const float W = (float)(1.0 / (1.0 + agexp::exp(-z, s_tab)));
-    const double V = ctr[i] * val[i], P = ctr[i] * val[i] * gam[i];
-    eu[i] = (double)W * (V - P);
-  }
-  // ---------------- 3. imitation of the logging policy (first update)
-  if (tid == 0) epochs_out[3 * a + 1] = 0;
-  if (!initialised[a]) {
-    if (tid < 16) s_adam.ea[tid] = s_adam.es[tid] = s_adam.mx[tid] = 0.0f;
     __syncthreads();
-    Stopper sp{INFINITY, -1, 512};
-    int e = 0;
-    for (; e < kInitEpochs; ++e) {
-      int64_t acc[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) acc[j] = 0;
-      for (int64_t i = tid; i < n; i += kDrThreads) {
-        const double c = (double)(float)ctr[i], v = (double)(float)val[i];
-        PolF f;
-        policy_fwd(s_pol, c, v, f, s_tab);
-        const double dm = f.mu - (double)(float)gam[i], dsg = f.sp_sigma - 0.05;
-        acc[12] += fxr(dm * dm);
-        acc[13] += fxr(dsg * dsg);
-        policy_bwd(s_pol, c, v, f, 2.0 * dm, 2.0 * dsg, acc, 0, s_tab);
-      }
-      block_sums<16>(acc, s_w, s_tot);
-      const float loss = (float)(fxv(s_tot[24], s_tot[25]) / (double)n + fxv(s_tot[26], s_tot[27]) / (double)n);
-      double bc1;
-      float bc2f;
-      bias_corrections(e, adam_tab, bc2f, bc1);
-      const float neg_step = (float)(-(1e-3 / bc1));
-      if (tid < 12) {
-        const float g = (float)(fxv(s_tot[2 * tid], s_tot[2 * tid + 1]) / (double)n);
-        float p = s_pol[tid];
-        adam_param(p, g, tid, s_adam, neg_step, bc2f, (float)1e-4);
-        s_pol[tid] = p;
-      }
-      if (tid == 0 && tr) tr[kDrEpochs + e] = loss;
-      const bool stop = stop_step(sp, e, loss);
-      __syncthreads();
-      if (stop) {
-        ++e;
-        break;
-      }
+    if (!initialised[a]) ep[1] = fit_imitation(R, n, S, adam_tab, tr ? tr + kDrEpochs : nullptr);
+    ep[2] = fit_dr(R, eu, n, S, noise + noise_off[a], noise_epochs, adam_tab, tr ? tr + 2 * kDrEpochs : nullptr);
+    stat = S.stop ? -2 : 0;
+  } else if (bk == AG_BIDDER_VALUE_LEARNING) {
+    int64_t acc[1] = {0};
+    for (int64_t i = tid; i < n; i += kDrThreads) acc[0] += R.won[i] ? 1 : 0;
+    block_sums<1>(acc, S.w, S.tot);
+    if (S.tot[0] == 0 && S.tot[1] == 0) {
+      stat = 1;  // src/Bidder.py:206-211: revert to Gaussian shading, nothing trained
+    } else {
+      ep[0] = fit_winrate(R, n, S, 100, 0.1, 512, adam_tab, tr);
+      if (bmode[a] == AG_VL_POLICY)
+        ep[2] = fit_dm(R, n, S, noise + noise_off[a], noise_epochs, adam_tab, tr ? tr + 2 * kDrEpochs : nullptr);
     }
-    if (tid == 0) epochs_out[3 * a + 1] = e;
-  }
-  // ---------------- 4. doubly robust policy fit
-  {
-    if (tid < 16) s_adam.ea[tid] = s_adam.es[tid] = s_adam.mx[tid] = 0.0f;
-    __syncthreads();
-    double lr = 7e-3;
-    Plateau pl{INFINITY, 5e-3, 0.2, 1e-8, 0, 100};
-    Stopper sp{INFINITY, -1, 512};
-    const double inv_sqrt2pi = 1.0 / __builtin_sqrt(2.0 * 3.141592653589793);
-    const float *nz = noise + noise_off[a];
-    int e = 0;
-    for (; e < kDrEpochs && e < noise_epochs; ++e) {
-      const float *eps = nz + (int64_t)e * n;
-      int64_t acc[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) acc[j] = 0;
-      for (int64_t i = tid; i < n; i += kDrThreads) {
-        const double c = (double)(float)ctr[i], v = (double)(float)val[i], g = (double)(float)gam[i];
-        PolF f;
-        policy_fwd(s_pol, c, v, f, s_tab);
-        const double mu = f.mu, sg = f.sigma;
-        const double zz = (mu - g) / sg;
-        const double pdf_raw = agexp::exp(-(zz * zz) / 2.0, s_tab) / sg * inv_sqrt2pi;
-        const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
-        const double p0 = (double)fmaxf((float)prop[i], 1e-15f);
-        const double iw = pi / p0;
-        const double iwc = iw < 1.0 / 50.0 ? 1.0 / 50.0 : (iw > 50.0 ? 50.0 : iw);
-        const double du = (double)(float)util[i] - (double)(float)eu[i];
-        const double ep = (double)eps[i];
-        const double raw = mu + sg * ep;
-        const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
-        const double zw = c * (double)s_wr[0] + v * (double)s_wr[1] + gs * (double)s_wr[2] + (double)s_wr[3];
-        const double Wv = 1.0 / (1.0 + agexp::exp(-zw, s_tab));
-        const double V = c * v;
-        acc[12] += fxr(-(du * iwc + Wv * (V - V * gs)));
-        double dpi_dmu = 0.0, dpi_dsg = 0.0;
-        if (pdf_raw >= 1e-30 && iw >= 1.0 / 50.0 && iw <= 50.0) {
-          const double k = du / p0;
-          dpi_dmu = k * pdf_raw * (g - mu) / (sg * sg);
-          dpi_dsg = k * pdf_raw * ((g - mu) * (g - mu) / (sg * sg * sg) - 1.0 / sg);
-        }
-        double ddm = 0.0;
-        if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)s_wr[2];
-        policy_bwd(s_pol, c, v, f, -(dpi_dmu + ddm), -(dpi_dsg + ddm * ep), acc, 0, s_tab);
-      }
-      block_sums<16>(acc, s_w, s_tot);
-      const float loss = (float)(fxv(s_tot[24], s_tot[25]) / (double)n);
-      double bc1;
-      float bc2f;
-      bias_corrections(e, adam_tab, bc2f, bc1);
-      const float neg_step = (float)(-(lr / bc1));
-      if (tid < 12) {
-        const float g = (float)(fxv(s_tot[2 * tid], s_tot[2 * tid + 1]) / (double)n);
-        float p = s_pol[tid];
-        adam_param(p, g, tid, s_adam, neg_step, bc2f, (float)1e-4);
-        s_pol[tid] = p;
-      }
-      if (tid == 0 && tr) tr[2 * kDrEpochs + e] = loss;
-      plateau_step(pl, loss, lr);
-      const bool stop = stop_step(sp, e, loss);
-      if (tid == 0 && loss != loss) s_stop = 1;  // NaN: the reference exits (src/Bidder.py:592-600)
-      __syncthreads();
-      if (stop || s_stop) {
-        ++e;
-        break;
-      }
-    }
-    if (tid == 0) {
-      epochs_out[3 * a + 2] = e;
-      status[a] = s_stop ? -2 : 0;
-    }
+  } else {  // PolicyLearningBidder
+    if (!initialised[a]) ep[1] = fit_imitation(R, n, S, adam_tab, tr ? tr + kDrEpochs : nullptr);
+    ep[2] = fit_pl(R, n, S, bmode[a], adam_tab, tr ? tr + 2 * kDrEpochs : nullptr);
+    stat = S.stop ? -2 : 0;
   }
   __syncthreads();
-  if (tid < 4) st[tid] = s_wr[tid];
-  if (tid < 12) st[4 + tid] = s_pol[tid];
+  if (tid == 0) {
+    epochs_out[3 * a] = ep[0];
+    epochs_out[3 * a + 1] = ep[1];
+    epochs_out[3 * a + 2] = ep[2];
+    status[a] = stat;
+  }
+  if (tid < 4) st[tid] = S.wr[tid];
+  if (tid < 12) st[4 + tid] = S.pol[tid];
 }
 
 // bucket the shading store by agent: histogram, scan, scatter of every record field
@@ -431,11 +629,23 @@ void ag_dr_release(ag_ctx *c) {
   (void)hipFree(w.adam_tab);
   (void)hipFree(w.state);
   (void)hipFree(w.init);
+  (void)hipFree(w.mode);
   (void)hipFree(w.scratch);
   w = ag_dr_ws();
 }
 
-// workspace: counts / offsets / cursors, the Adam bias-correction table, the DR state
+// which agents bid from a fitted policy / a win-rate search (ag_simulate checks its inputs)
+static void learner_flags(ag_ctx *c, const int32_t *init) {
+  c->dr_any_init = c->vl_any_search = false;
+  for (int a = 0; a < c->shape.num_agents; ++a) {
+    const int bk = c->h_bkind ? c->h_bkind[a] : -1;
+    const bool learner = bk == AG_BIDDER_VALUE_LEARNING || bk == AG_BIDDER_POLICY_LEARNING || bk == AG_BIDDER_DOUBLY_ROBUST;
+    if (learner && init[a] == AG_LEARNER_POLICY) c->dr_any_init = true;
+    if (bk == AG_BIDDER_VALUE_LEARNING && init[a] == AG_LEARNER_SEARCH) c->vl_any_search = true;
+  }
+}
+
+// workspace: counts / offsets / cursors, the Adam bias-correction table, the learner state
 static int dr_ws_ready(ag_ctx *c) {
   ag_dr_ws &w = c->dr;
   if (w.adam_tab) return AG_OK;
@@ -453,6 +663,13 @@ static int dr_ws_ready(ag_ctx *c) {
   if (e == hipSuccess) e = hipMemset(w.state, 0, sizeof(float) * 16 * (size_t)N);
   if (e == hipSuccess) e = hipMalloc(&w.init, sizeof(int32_t) * (size_t)N);
   if (e == hipSuccess) e = hipMemset(w.init, 0, sizeof(int32_t) * (size_t)N);
+  if (e == hipSuccess) e = hipMalloc(&w.mode, sizeof(int32_t) * (size_t)N);
+  if (e == hipSuccess) {  // defaults: ValueLearningBidder 'search', PolicyLearningBidder 'PPO'
+    std::vector<int32_t> m(N, AG_VL_SEARCH);
+    for (int a = 0; a < N; ++a)
+      if (c->h_bkind && c->h_bkind[a] == AG_BIDDER_POLICY_LEARNING) m[a] = AG_PL_LOSS_PPO;
+    e = hipMemcpy(w.mode, m.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) e = hipMalloc(&w.scratch, sizeof(int64_t) * (size_t)N + sizeof(int32_t) * 4 * (size_t)N);
   if (e != hipSuccess) {
     ag_dr_release(c);
@@ -471,8 +688,7 @@ int ag_set_dr_state(ag_ctx *c, const float *state, const int32_t *initialised) {
   AG_HIP(hipMemcpy(c->dr.state, state, sizeof(float) * 16 * N, hipMemcpyHostToDevice));
   AG_HIP(hipMemcpy(c->dr.init, initialised, sizeof(int32_t) * N, hipMemcpyHostToDevice));
   c->dr_loaded = true;
-  c->dr_any_init = false;
-  for (int a = 0; a < N; ++a) c->dr_any_init |= initialised[a] != 0 && c->h_bkind && c->h_bkind[a] == AG_BIDDER_DOUBLY_ROBUST;
+  learner_flags(c, initialised);
   return AG_OK;
 }
 
@@ -512,13 +728,13 @@ int ag_shading_counts(ag_ctx *c, const ag_shading_samples *s, int64_t *counts, v
   return AG_OK;
 }
 
-int ag_dr_update(ag_ctx *c, const ag_shading_samples *s, const float *noise, const int64_t *noise_offsets,
-                 int32_t noise_epochs, int32_t *epochs, float *traces, void *stream) {
+int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const float *noise, const int64_t *noise_offsets,
+                     int32_t noise_epochs, int32_t *epochs, int32_t *status, float *traces, void *stream) {
   if (!c || !s || !noise_offsets || (!noise && noise_epochs > 0))
-    return ag_set_error(AG_ERR_INVALID, "ag_dr_update: null argument");
+    return ag_set_error(AG_ERR_INVALID, "ag_bidder_update: null argument");
   if (!s->ctr || !s->value || !s->propensity || !s->won || !s->order)
-    return ag_set_error(AG_ERR_INVALID, "ag_dr_update: the store needs ctr, value, propensity, won, order");
-  if (!c->dr_loaded) return ag_set_error(AG_ERR_STATE, "ag_dr_update: ag_set_dr_state not called");
+    return ag_set_error(AG_ERR_INVALID, "ag_bidder_update: the store needs ctr, value, propensity, won, order");
+  if (!c->dr_loaded) return ag_set_error(AG_ERR_STATE, "ag_bidder_update: ag_set_dr_state not called");
   AgDeviceGuard g(c->device);
   const int N = c->shape.num_agents;
   hipStream_t st = (hipStream_t)stream;
@@ -533,7 +749,7 @@ int ag_dr_update(ag_ctx *c, const ag_shading_samples *s, const float *noise, con
   for (int a = 0; a < N; ++a) off[a + 1] = off[a] + cnt[a];
   int64_t *d_off = w.counts + N;  // [N + 1] offsets
   AG_HIP(hipMemcpyAsync(d_off, off.data(), sizeof(int64_t) * ((size_t)N + 1), hipMemcpyHostToDevice, st));
-  if (n >= ((int64_t)1 << 32)) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_dr_update: >= 2^32 records");
+  if (n >= ((int64_t)1 << 32)) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_bidder_update: >= 2^32 records");
   // radix-sort workspace: keys in/out (8 B), indices in/out (4 B), then hipcub's temp
   size_t sort_tmp = 0;
   AG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint64_t *)nullptr, (uint64_t *)nullptr,
@@ -556,7 +772,7 @@ int ag_dr_update(ag_ctx *c, const ag_shading_samples *s, const float *noise, con
   uint8_t *b_won = (uint8_t *)(i_out + cap);
   void *tmp = (void *)(((uintptr_t)(b_won + cap) + 255) & ~(uintptr_t)255);
   if (n > 0) {
-    if (!s->order) return ag_set_error(AG_ERR_INVALID, "ag_dr_update: the store needs order");
+    if (!s->order) return ag_set_error(AG_ERR_INVALID, "ag_bidder_update: the store needs order");
     hipLaunchKernelGGL(k_sh_keys, dim3(grid_over(n)), dim3(kDrThreads), 0, st, *s, n, k_in, i_in);
     AG_HIP(hipGetLastError());
     int end_bit = 40;
@@ -571,28 +787,62 @@ int ag_dr_update(ag_ctx *c, const ag_shading_samples *s, const float *noise, con
   int32_t *d_stat = d_epochs + 3 * (size_t)N;
   AG_HIP(hipMemcpyAsync(d_noff, noise_offsets, sizeof(int64_t) * N, hipMemcpyHostToDevice, st));
   DrRecords R{b_ctr, b_val, b_gam, b_prop, b_util, b_won};
-  hipLaunchKernelGGL(k_dr_train, dim3(N), dim3(kDrThreads), 0, st, c->d_bkind, d_off, R, b_eu, w.state, w.init,
-                     noise, d_noff, noise_epochs, w.adam_tab, d_epochs, d_stat, traces);
+  hipLaunchKernelGGL(k_bidder_train, dim3(N), dim3(kDrThreads), 0, st, c->d_bkind, w.mode, d_off, R, b_eu, w.state,
+                     w.init, noise, d_noff, noise_epochs, w.adam_tab, d_epochs, d_stat, traces);
   AG_HIP(hipGetLastError());
   std::vector<int32_t> h(4 * (size_t)N);
   AG_HIP(hipMemcpyAsync(h.data(), d_epochs, sizeof(int32_t) * 4 * N, hipMemcpyDeviceToHost, st));
   AG_HIP(hipStreamSynchronize(st));
   if (epochs) memcpy(epochs, h.data(), sizeof(int32_t) * 3 * N);
+  if (status) memcpy(status, h.data() + 3 * (size_t)N, sizeof(int32_t) * N);
+  static const char *names[] = {"", "", "ValueLearningBidder", "PolicyLearningBidder", "DoublyRobustBidder"};
   for (int a = 0; a < N; ++a) {
+    const int bk = c->h_bkind[a];
     if (h[3 * N + a] == -1)
-      return ag_set_error(AG_ERR_INVALID, "agent %d: DoublyRobustBidder.update without logs", a);
+      return ag_set_error(AG_ERR_INVALID, "agent %d: %s.update without logs", a, names[bk]);
     if (h[3 * N + a] == -2)
-      return ag_set_error(AG_ERR_INVALID, "agent %d: NAN DETECTED! in losses (src/Bidder.py:592)", a);
+      return ag_set_error(AG_ERR_INVALID, "agent %d: %s: NAN DETECTED! in losses (src/Bidder.py:%d)", a, names[bk],
+                          bk == AG_BIDDER_DOUBLY_ROBUST ? 592 : 409);
   }
-  // the fitted policies bid from now on (src/Bidder.py:612-613)
-  std::vector<int32_t> init(N);
+  // from now on the agents bid from what they fitted (src/Bidder.py:321, :430, :612-613):
+  // 1 = the policy, 2 = the win-rate search (ValueLearningBidder 'search'); 0 after the
+  // ValueLearningBidder's no-win fallback (:206-211)
+  std::vector<int32_t> init(N), mode(N);
   AG_HIP(hipMemcpy(init.data(), w.init, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
-  for (int a = 0; a < N; ++a)
-    if (c->h_bkind[a] == AG_BIDDER_DOUBLY_ROBUST) {
-      init[a] = 1;
-      c->dr_any_init = true;
-    }
+  AG_HIP(hipMemcpy(mode.data(), w.mode, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
+  for (int a = 0; a < N; ++a) {
+    const int bk = c->h_bkind[a];
+    if (bk == AG_BIDDER_DOUBLY_ROBUST || bk == AG_BIDDER_POLICY_LEARNING)
+      init[a] = AG_LEARNER_POLICY;
+    else if (bk == AG_BIDDER_VALUE_LEARNING)
+      init[a] = h[3 * N + a] == 1 ? AG_LEARNER_UNINITIALISED
+                                  : (mode[a] == AG_VL_POLICY ? AG_LEARNER_POLICY : AG_LEARNER_SEARCH);
+  }
   AG_HIP(hipMemcpy(w.init, init.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice));
+  learner_flags(c, init.data());
+  return AG_OK;
+}
+
+int ag_dr_update(ag_ctx *c, const ag_shading_samples *s, const float *noise, const int64_t *noise_offsets,
+                 int32_t noise_epochs, int32_t *epochs, float *traces, void *stream) {
+  return ag_bidder_update(c, s, noise, noise_offsets, noise_epochs, epochs, nullptr, traces, stream);
+}
+
+int ag_set_bidder_modes(ag_ctx *c, const int32_t *modes) {
+  if (!c || !modes) return ag_set_error(AG_ERR_INVALID, "ag_set_bidder_modes: null argument");
+  AgDeviceGuard g(c->device);
+  if (int rc = dr_ws_ready(c)) return rc;
+  const int N = c->shape.num_agents;
+  for (int a = 0; a < N; ++a) {
+    const int bk = c->h_bkind ? c->h_bkind[a] : -1;
+    if (bk == AG_BIDDER_VALUE_LEARNING && modes[a] != AG_VL_SEARCH && modes[a] != AG_VL_POLICY)
+      return ag_set_error(AG_ERR_INVALID, "agent %d: ValueLearningBidder inference must be 'search' or 'policy'", a);
+    if (bk == AG_BIDDER_POLICY_LEARNING && (modes[a] < AG_PL_LOSS_REINFORCE || modes[a] > AG_PL_LOSS_PPO))
+      return ag_set_error(AG_ERR_UNSUPPORTED,
+                          "agent %d: PolicyLearningBidder loss %d (REINFORCE, REINFORCE_offpolicy, TRPO, PPO are built)",
+                          a, modes[a]);
+  }
+  AG_HIP(hipMemcpy(c->dr.mode, modes, sizeof(int32_t) * N, hipMemcpyHostToDevice));
   return AG_OK;
 }
 

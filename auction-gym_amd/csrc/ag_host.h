@@ -39,7 +39,8 @@ struct ag_dr_ws {
   int64_t *counts = nullptr;    // [N] counts, [N + 1] offsets
   double *adam_tab = nullptr;   // [2][32768] Adam bias corrections (libm pow)
   float *state = nullptr;       // [N][16]: win-rate w0 w1 w2 b, policy (12)
-  int32_t *init = nullptr;      // [N] policy initialised
+  int32_t *init = nullptr;      // [N] AG_LEARNER_*: what the agent bids from
+  int32_t *mode = nullptr;      // [N] ValueLearningBidder inference / PolicyLearningBidder loss
   int64_t *scratch = nullptr;   // [N] noise offsets + [N][4] epochs / status
 };
 
@@ -63,7 +64,8 @@ struct ag_ctx {
   int32_t ts_sample = 1;
   int32_t *h_akind = nullptr;  // host copy of the allocator kinds [N]
   int32_t *h_bkind = nullptr;  // host copy of the bidder kinds [N]
-  bool dr_loaded = false, dr_any_init = false;  // DR models loaded; some bid from a policy
+  bool dr_loaded = false, dr_any_init = false;  // learner models loaded; some bid from a policy
+  bool vl_any_search = false;                    // some ValueLearningBidder bids by search
   ag_dr_ws dr;
   int32_t *d_akind = nullptr, *d_bkind = nullptr;
   double *d_pg = nullptr, *d_gs = nullptr;

@@ -580,7 +580,10 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   if (c->has_shading && !in->gamma_raw)
     return ag_set_error(AG_ERR_INVALID, "ag_simulate: shading bidders need gamma_raw");
   if (c->dr_any_init && !in->policy_eps)
-    return ag_set_error(AG_ERR_INVALID, "ag_simulate: DoublyRobustBidders with a fitted policy need policy_eps");
+    return ag_set_error(AG_ERR_INVALID, "ag_simulate: learning bidders with a fitted policy need policy_eps");
+  if (c->vl_any_search)
+    return ag_set_error(AG_ERR_UNSUPPORTED,
+                        "ag_simulate: ValueLearningBidder 'search' bids (src/Bidder.py:180-196) are not built");
   SimParams prm;
   prm.B = B;
   prm.N = s.num_agents;

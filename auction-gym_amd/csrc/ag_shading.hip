@@ -40,16 +40,16 @@ __global__ __launch_bounds__(kShThreads) void k_shading_collect(
       bool take = false;
       if (live) {
         a = part[(size_t)s * B + i];
-        take = bkind[a] == AG_BIDDER_EMPIRICAL_SHADED || bkind[a] == AG_BIDDER_DOUBLY_ROBUST;
+        take = bkind[a] != AG_BIDDER_TRUTHFUL;  // Empirical, ValueLearning, PolicyLearning, DR
       }
       const uint64_t ballot = __ballot(take);
       if (ballot == 0) continue;
-      unsigned long long first = 0;
+      unsigned long long base_slot = 0;
       const int leader = __ffsll((unsigned long long)ballot) - 1;
-      if (lane == leader) first = atomicAdd(count, (unsigned long long)__popcll(ballot));
-      first = __shfl(first, leader, 64);
+      if (lane == leader) base_slot = atomicAdd(count, (unsigned long long)__popcll(ballot));
+      base_slot = __shfl(base_slot, leader, 64);
       if (!take) continue;
-      const int64_t slot = (int64_t)first + __popcll(ballot & ((1ull << lane) - 1));
+      const int64_t slot = (int64_t)base_slot + __popcll(ballot & ((1ull << lane) - 1));
       if (slot >= st.capacity) continue;  // overflow: reported by the update
       const size_t o = (size_t)s * B + i;
       const bool won = charged && s == w;

@@ -420,7 +420,9 @@ __device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], 
   return best;
 }
 
-// DoublyRobustBidder.bid with a fitted policy (src/Bidder.py:466-470, src/Models.py:155-164):
+// A learning bidder's bid from its fitted policy (src/Bidder.py:198-203 ValueLearningBidder
+// 'policy', :358-362 PolicyLearningBidder, :466-470 DoublyRobustBidder; src/Models.py:82-90
+// and :155-164 -- the same forward):
 // ora_policy_bid (oracle/ag_oracle_dr.c) bit for bit -- the policy forward in double
 // (softplus = log1p(exp), the restated log1p), mu / sigma rounded to float32, the rsample
 // mu + sigma * eps in float32, exp(log_prob) rounded to float32, gamma = clip(sample, 0, 1).
@@ -496,7 +498,7 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
     double b = v * est;  // Bidder.bid: value * estimated CTR (src/Bidder.py:35, :49, :173, ...)
     if constexpr (GENERAL) {
       const int bk = T.bkind[a];
-      if (bk == AG_BIDDER_DOUBLY_ROBUST && T.drs && T.dri[a]) {  // bids from the fitted policy
+      if (bk >= AG_BIDDER_VALUE_LEARNING && T.drs && T.dri[a] == AG_LEARNER_POLICY) {  // the fitted policy
         policy_bid(T.drs + a * 16 + 4, est, v, in.policy_eps[s * B + i], T.tab, g, prop);
         b = b * g;
       } else if (bk != AG_BIDDER_TRUTHFUL) {

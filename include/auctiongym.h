@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define AG_ABI_VERSION 10
+#define AG_ABI_VERSION 11
 
 typedef enum ag_status {
   AG_OK = 0,
@@ -51,10 +51,32 @@ typedef enum ag_allocator_kind {
 typedef enum ag_bidder_kind {
   AG_BIDDER_TRUTHFUL = 0,         /* TruthfulBidder, src/Bidder.py:28-35 */
   AG_BIDDER_EMPIRICAL_SHADED = 1, /* EmpiricalShadedBidder, src/Bidder.py:38-58 */
-  AG_BIDDER_VALUE_LEARNING = 2,   /* ValueLearningBidder (uninitialised), src/Bidder.py:171-179 */
-  AG_BIDDER_POLICY_LEARNING = 3,  /* PolicyLearningBidder (uninitialised), src/Bidder.py:348-356 */
-  AG_BIDDER_DOUBLY_ROBUST = 4     /* DoublyRobustBidder (uninitialised), src/Bidder.py:455-463 */
+  AG_BIDDER_VALUE_LEARNING = 2,   /* ValueLearningBidder, src/Bidder.py:156-333 */
+  AG_BIDDER_POLICY_LEARNING = 3,  /* PolicyLearningBidder, src/Bidder.py:336-439 */
+  AG_BIDDER_DOUBLY_ROBUST = 4     /* DoublyRobustBidder, src/Bidder.py:442-623 */
 } ag_bidder_kind;
+
+/* What a learning bidder (ValueLearning / PolicyLearning / DoublyRobust) bids from
+ * (ag_set_dr_state `initialised`, set by ag_bidder_update): */
+typedef enum ag_learner_state {
+  AG_LEARNER_UNINITIALISED = 0, /* gamma ~ N(prev_gamma, gamma_sigma) (src/Bidder.py:174-179,
+                                   :351-356, :458-463): gamma_raw input */
+  AG_LEARNER_POLICY = 1,        /* the fitted policy's rsample (:198-203, :358-362, :464-470):
+                                   policy_eps input */
+  AG_LEARNER_SEARCH = 2         /* ValueLearningBidder 'search': argmax of the win-rate model's
+                                   utility over 128 sorted U(0.1, 1) gammas (:180-196) */
+} ag_learner_state;
+
+/* Per-agent bidder modes (ag_set_bidder_modes): ValueLearningBidder inference ... */
+typedef enum ag_vl_inference { AG_VL_SEARCH = 0, AG_VL_POLICY = 1 } ag_vl_inference;
+/* ... and PolicyLearningBidder loss (src/Models.py:174-199; 'Doubly Robust' needs utility
+ * estimates the PolicyLearningBidder never passes: the reference fails there). */
+typedef enum ag_pl_loss {
+  AG_PL_LOSS_REINFORCE = 0,
+  AG_PL_LOSS_REINFORCE_OFFPOLICY = 1,
+  AG_PL_LOSS_TRPO = 2,
+  AG_PL_LOSS_PPO = 3
+} ag_pl_loss;
 
 /* Per-agent counters produced by ag_simulate: the quantities src/main.py:131-147 reads
  * from Agent (src/Agent.py:70-118) after each iteration, as sums over the agent's logs. */
@@ -279,10 +301,12 @@ int ag_shading_collect(ag_ctx *ctx, int64_t first_auction, int64_t B, const ag_b
 int ag_empirical_update(ag_ctx *ctx, const ag_shading_samples *samples, double *prev_gamma,
                         void *stream);
 
-/* ---- DoublyRobustBidder (src/Bidder.py:442-623) ---------------------------------------
- * Per-agent model state, host float32 [N][16]: PyTorchWinRateEstimator weight (3) and bias,
- * then BidShadingContextualBandit.parameters() (shared W 2x2, b 2; mu w 2, b; sigma w 2, b);
- * initialised [N]: the policy was fitted (its bids come from the policy). */
+/* ---- Learning bidders: ValueLearningBidder, PolicyLearningBidder, DoublyRobustBidder ----
+ * (src/Bidder.py:156-623). Per-agent model state, host float32 [N][16]:
+ * PyTorchWinRateEstimator weight (3) and bias, then the policy's parameters on its forward
+ * path (BidShadingContextualBandit.parameters(); for BidShadingPolicy the same layers, its
+ * unused hidden layers left out): shared W 2x2, b 2; mu w 2, b; sigma w 2, b.
+ * initialised [N]: ag_learner_state. */
 int ag_set_dr_state(ag_ctx *ctx, const float *state, const int32_t *initialised);
 int ag_get_dr_state(ag_ctx *ctx, float *state, int32_t *initialised);
 
@@ -301,6 +325,28 @@ int ag_shading_counts(ag_ctx *ctx, const ag_shading_samples *samples, int64_t *c
 int ag_dr_update(ag_ctx *ctx, const ag_shading_samples *samples, const float *noise,
                  const int64_t *noise_offsets, int32_t noise_epochs, int32_t *epochs, float *traces,
                  void *stream);
+
+/* ValueLearningBidder inference (AG_VL_*) / PolicyLearningBidder loss (AG_PL_LOSS_*) per
+ * agent, host int32 [N] (entries of other agents ignored); the constructors' arguments
+ * (src/Bidder.py:159-167, :339-346). Defaults: 'search', 'PPO'. */
+int ag_set_bidder_modes(ag_ctx *ctx, const int32_t *modes);
+
+/* Agent.update -> Bidder.update of EVERY learning bidder from the store, one workgroup per
+ * agent running its fits in the reference's order (src/Agent.py:79-94):
+ *  - DoublyRobustBidder (src/Bidder.py:473-615): as ag_dr_update;
+ *  - ValueLearningBidder (:204-325): no won record -> the reference's fallback (nothing
+ *    trained, status 1, bids revert to Gaussian shading); else the win-rate fit and, with
+ *    inference 'policy', the policy fit (rsample noise as for DR, <= 16384 epochs);
+ *  - PolicyLearningBidder (:364-431): imitation of the logging policy (first update), then
+ *    the fit of its loss (no noise).
+ * epochs host int32 [N][3] = (win-rate, imitation, policy fit); status host int32 [N]: 0
+ * trained, 1 fallback (may be NULL); traces dev float32 [N][3][32768] (may be NULL).
+ * AG_ERR_INVALID where the reference fails (no logs; a NaN loss, where it exits).
+ * Synchronises. Arithmetic: oracle/ag_oracle_dr.c ora_dr_update / ora_vl_update /
+ * ora_pl_update. */
+int ag_bidder_update(ag_ctx *ctx, const ag_shading_samples *samples, const float *noise,
+                     const int64_t *noise_offsets, int32_t noise_epochs, int32_t *epochs, int32_t *status,
+                     float *traces, void *stream);
 
 /* Exact counters (host int64 [n][AG_FX_LIMBS], e.g. copied back or all-reduced)
  * -> doubles (host [n]), correctly rounded from the exact fixed-point sum. */

@@ -220,7 +220,7 @@ static void simulate_range(const ora_pop *pp, const double *items, const double 
       double b = v * est; /* Bidder.bid: value * estimated CTR (src/Bidder.py:35,49,173,...) */
       double g = NAN, prop = NAN;
       const int32_t bk = pp->bid_kind[a];
-      if (bk == ORA_BIDDER_DOUBLY_ROBUST && pp->dr_init && pp->dr_init[a]) {
+      if (bk >= ORA_BIDDER_VALUE_LEARNING && pp->dr_init && pp->dr_init[a] == 1) { /* fitted policy */
         ora_policy_bid(pp->dr_state + (int64_t)a * 16 + 4, est, v, in->policy_eps[o], &g, &prop);
         b = b * g;
       } else if (bk != ORA_BIDDER_TRUTHFUL) {

@@ -449,11 +449,12 @@ def test_mixed_population_full_size(gpu, oracle):
     eng.close()
 
 
-def test_fitted_dr_policy_bids_match_oracle(gpu, oracle):
-    """DoublyRobustBidder.bid with a fitted policy (src/Bidder.py:440-470): the gamma is the
+def test_fitted_policy_bids_match_oracle(gpu, oracle):
+    """Learning bidders bidding from a fitted policy (src/Bidder.py:198-203 ValueLearningBidder
+    'policy', :358-362 PolicyLearningBidder, :466-470 DoublyRobustBidder): the gamma is the
     policy's rsample on (estimated CTR, value), the propensity its Normal density. Mixed
-    population where half of the DR agents bid from random fitted policies; every output
-    compared with the oracle on the same inputs and the same generated rsample draws."""
+    population where half of the learning bidders bid from random fitted policies; every
+    output compared with the oracle on the same inputs and the same generated draws."""
     import torch
     from auctiongym_amd.engine import AuctionEngine
     N, P, K, E, OE, B = 20, 4, 12, 5, 4, 1 << 18
@@ -467,8 +468,9 @@ def test_fitted_dr_policy_bids_match_oracle(gpu, oracle):
     m = g.normal(0, 1, (N, K, OE + 1)).astype(np.float32)
     q = (1.0 + 3.0 * g.random((N, K, OE + 1))).astype(np.float32)
     state = g.normal(0, 0.7, (N, 16)).astype(np.float32)
-    init = np.array([1 if (bk[a] == 4 and a % 2 == 0) else 0 for a in range(N)], np.int32)
-    assert init.sum() >= 4 and ((bk == 4) & (init == 0)).sum() >= 4
+    init = np.array([1 if (bk[a] >= 2 and (a % 2 == 0 or a == 9)) else 0 for a in range(N)], np.int32)
+    assert init.sum() >= 4 and ((bk >= 2) & (init == 0)).sum() >= 4
+    assert {2, 3, 4} <= set(bk[init == 1].tolist())
     eng = AuctionEngine(N, P, K, E, OE, 1, 1.0)
     eng.set_agent_params(ak, bk, pg, gs)
     eng.load_catalog(items, values)
@@ -940,4 +942,107 @@ def test_dr_update_matches_oracle(gpu, oracle):
         assert ep[a, 2] == len(k("dr_losses"))
         pol1 = np.concatenate([k(f"pol1_{j}").ravel() for j in range(6)])
         np.testing.assert_allclose(state[a, 4:], pol1, atol=2e-6)
+    eng.close()
+
+
+# ---- ValueLearningBidder / PolicyLearningBidder updates (src/Bidder.py:204-325, :364-431) ----
+def test_vl_pl_update_matches_oracle(gpu, oracle):
+    """One ag_bidder_update launch over a population of FP_DM_TS's three ValueLearningBidders
+    ('policy'), FP_IPS_TS's three PolicyLearningBidders ('PPO') and a ValueLearningBidder that
+    won nothing (the reference's fallback), on the reference's own logs (tests/golden/
+    dm_update_kat.npz, ips_update_kat.npz), records shuffled: every fit's epochs and
+    per-epoch losses and the final models equal the oracle's bit for bit; the fallback
+    agent trains nothing and reverts to Gaussian shading; the fitted agents bid from their
+    policies afterwards. Against the reference: the pinned tolerances of
+    tests/test_oracle_golden.py (DM agent 2: same epochs, losses within 1e-7)."""
+    import torch
+    from auctiongym_amd import _lib
+    from auctiongym_amd.engine import AuctionEngine
+    dm = np.load(os.path.join(GOLDEN, "dm_update_kat.npz"))
+    ips = np.load(os.path.join(GOLDEN, "ips_update_kat.npz"))
+    N = 7
+    bk = np.array([2, 2, 2, 3, 3, 3, 2], np.int32)
+    modes = np.array([_lib.VL_POLICY] * 3 + [_lib.PL_LOSSES["PPO"]] * 3 + [_lib.VL_POLICY], np.int32)
+    eng = AuctionEngine(N, 2, 12, 5, 4, 0, 1.0)
+    eng.set_agent_params(np.ones(N, np.int32), bk, np.ones(N), np.full(N, 0.02))
+    state0 = np.zeros((N, 16), np.float32)
+    recs = {f: [] for f in ("agent", "gamma", "utility", "ctr", "value", "propensity", "won", "order")}
+    noises, offs, off, orc = [], [], 0, []
+    E = 0
+    for a in range(N):
+        kat, j = (dm, a) if a < 3 else ((ips, a - 3) if a < 6 else (dm, 1))
+        k = lambda s: kat[f"a{j}_{s}"]  # noqa: E731
+        n = len(k("est_ctr"))
+        won = k("won") if a < 6 else np.zeros(n, np.int8)
+        if a < 3 or a == 6:
+            state0[a, :4] = np.concatenate([k("wr0_0").ravel(), k("wr0_1").ravel()])
+            state0[a, 4:] = np.concatenate([k(f"pol0_{i}").ravel() for i in (0, 1, 4, 5, 8, 9)])
+            Ea = len(k("fit1_losses")) + 300
+            z = _dr_noise(k("fit1_rng"), n, 3800)
+            assert Ea <= 3800
+            E = 3800
+            orc.append(oracle.vl_update(k("est_ctr"), k("value"), k("gamma"), won, state0[a, :4], state0[a, 4:],
+                                        True, z))
+        else:
+            state0[a, 4:] = np.concatenate([k(f"pol0_{i}").ravel() for i in range(6)])
+            z = np.zeros((0, n), np.float32)
+            orc.append(oracle.pl_update(k("est_ctr"), k("value"), k("gamma"), k("propensity"), k("util"),
+                                        state0[a, 4:], False, "PPO"))
+        noises.append(z.ravel())
+        offs.append(off)
+        off += z.size
+        for f, v in (("agent", np.full(n, a)), ("gamma", k("gamma")), ("utility", k("util")),
+                     ("ctr", k("est_ctr")), ("value", k("value")), ("propensity", k("propensity")),
+                     ("won", won), ("order", 5 * np.arange(n) + a)):
+            recs[f].append(v)
+    eng.set_dr_state(state0, np.zeros(N, np.int32))
+    eng.set_bidder_modes(modes)
+    n_tot = sum(len(v) for v in recs["agent"])
+    st = eng.new_shading_samples(n_tot, learning=True)
+    perm = np.random.default_rng(6).permutation(n_tot)
+    dt = {"agent": np.int32, "won": np.uint8, "order": np.int64}
+    for f, parts in recs.items():
+        v = np.concatenate(parts).astype(dt.get(f, np.float64))[perm]
+        st[f][:n_tot] = torch.from_numpy(v).to(eng.device)
+    st["count"][0] = n_tot
+    noise = torch.from_numpy(np.concatenate(noises)).to(eng.device)
+    ep, stat, tr = eng.bidder_update(st, noise, offs, E, trace=True)
+    state, ini = eng.dr_state()
+    tr = tr.cpu().numpy()
+    assert list(stat) == [0, 0, 0, 0, 0, 0, 1]
+    assert list(ini) == [1, 1, 1, 1, 1, 1, 0]
+    for a in range(6):
+        r = orc[a]
+        assert list(ep[a]) == list(r["epochs"]), (a, ep[a], r["epochs"])
+        if a < 3:
+            assert np.array_equal(tr[a, 0, :ep[a, 0]], r["wr_losses"].astype(np.float32))
+            assert np.array_equal(tr[a, 2, :ep[a, 2]], r["pol_losses"].astype(np.float32))
+            assert np.array_equal(state[a, :4], r["wr"])
+        else:
+            assert np.array_equal(tr[a, 1, :ep[a, 1]], r["init_losses"].astype(np.float32))
+            assert np.array_equal(tr[a, 2, :ep[a, 2]], r["pl_losses"].astype(np.float32))
+        assert np.array_equal(state[a, 4:], r["pol"]), a
+    assert list(ep[6]) == [0, 0, 0] and np.array_equal(state[6], state0[6])
+    k = lambda s: dm[f"a2_{s}"]  # noqa: E731  the reference, DM agent 2
+    assert ep[2, 0] == len(k("fit0_losses")) and ep[2, 2] == len(k("fit1_losses"))
+    np.testing.assert_allclose(tr[2, 2, :ep[2, 2]], k("fit1_losses"), atol=1e-7)
+    eng.close()
+
+
+def test_bidder_update_errors(gpu):
+    """Loud failures where the reference fails: a learning bidder without logs, an unknown
+    PolicyLearningBidder loss, a ValueLearningBidder inference that is neither mode."""
+    import torch
+    from auctiongym_amd.engine import AuctionEngine
+    N = 3
+    eng = AuctionEngine(N, 2, 12, 5, 4, 0, 1.0)
+    eng.set_agent_params(np.zeros(N, np.int32), np.array([2, 3, 0], np.int32), np.ones(N), np.full(N, 0.02))
+    eng.set_dr_state(np.zeros((N, 16), np.float32), np.zeros(N, np.int32))
+    with pytest.raises(NotImplementedError, match="PolicyLearningBidder loss"):
+        eng.set_bidder_modes([0, 7, 0])
+    with pytest.raises(ValueError, match="inference"):
+        eng.set_bidder_modes([5, 3, 0])
+    st = eng.new_shading_samples(16, learning=True)
+    with pytest.raises(ValueError, match="without logs"):
+        eng.bidder_update(st, torch.zeros(1, device=eng.device), [0, 0, 0], 0)
     eng.close()
