@@ -87,6 +87,10 @@ class Auction:
                 raise NotImplementedError("LR-TS agents must all sample or all not sample")
             self._ts = ts.pop()
             self._load_lrts()
+        self._learning = np.isin(bk, (_lib.BIDDER_VALUE_LEARNING, _lib.BIDDER_POLICY_LEARNING,
+                                      _lib.BIDDER_DOUBLY_ROBUST))
+        if self._learning.any():
+            self._load_learners()
         for i, a in enumerate(agents):
             a._attach(self, i)
         self._revenue_fx = 0
@@ -97,7 +101,8 @@ class Auction:
         self.keep_logs = True
         # Agent.update bookkeeping (see _update_agent)
         self._empirical = bk == _lib.BIDDER_EMPIRICAL_SHADED
-        self._learner = self._lrts | self._empirical
+        self._shading_rec = self._empirical | self._learning  # agents whose records are kept
+        self._learner = self._lrts | self._shading_rec
         self._stores = {}                       # device record stores, by learner family
         self._bounds = {"lrts": 0, "shading": 0}  # upper bounds of the records they hold
         self._trained = False       # the stores' records were trained on
@@ -115,21 +120,44 @@ class Auction:
                 m[i], q[i], pm[i] = rm.m.numpy(), rm.q.numpy(), rm.prev_iter_m.numpy()
         self._engine.load_lrts(m, q, pm, thompson_sampling=self._ts)
 
+    def _load_learners(self):
+        """Learning bidders' models and modes onto the device (ag_set_dr_state,
+        ag_set_bidder_modes)."""
+        N = len(self.agents)
+        st = np.zeros((N, 16), np.float32)
+        init = np.zeros(N, np.int32)
+        modes = np.zeros(N, np.int32)
+        for i, a in enumerate(self.agents):
+            if self._learning[i]:
+                st[i] = a.bidder._state16()
+                init[i] = a.bidder._learner_state()
+                modes[i] = a.bidder._mode()
+        self._engine.set_dr_state(st, init)
+        self._engine.set_bidder_modes(modes)
+
     # ------------------------------------------------------------------ rounds
     def _draw_round(self):
         N, P = len(self.agents), self.num_participants_per_round
         if not (self._shading.any() or (self._lrts.any() and self._ts)):
             ctx, part, u = draw_round(self.rng, N, P, self.embedding_size, self.embedding_var,
                                       self.max_slots)
-            self._pending.append((ctx, part, u, None, None))
+            self._pending.append((ctx, part, u, None, None, None))
             return
         shading = [(a.bidder.prev_gamma, a.bidder.gamma_sigma) if self._shading[i] else None
                    for i, a in enumerate(self.agents)]
         models = [a.allocator.response_model if (self._lrts[i] and self._ts) else None
                   for i, a in enumerate(self.agents)]
-        ctx, part, g, u, noise = draw_round_population(
-            self.rng, N, P, self.embedding_size, self.embedding_var, shading, models, self.max_slots)
-        self._pending.append((ctx, part, u, g, noise))
+        policy = None
+        if self._learning.any():
+            ls = [a.bidder._learner_state() if self._learning[i] else 0 for i, a in enumerate(self.agents)]
+            if _lib.LEARNER_SEARCH in ls:
+                raise NotImplementedError("ValueLearningBidder 'search' bids (src/Bidder.py:180-196) "
+                                          "are not on the GPU path yet")
+            policy = [x == _lib.LEARNER_POLICY for x in ls]
+        ctx, part, g, u, noise, eps = draw_round_population(
+            self.rng, N, P, self.embedding_size, self.embedding_var, shading, models, self.max_slots,
+            policy)
+        self._pending.append((ctx, part, u, g, noise, eps))
 
     def _flush_limit(self):
         return self.FLUSH_ROUNDS_TS if (self._lrts.any() and self._ts) else self.FLUSH_ROUNDS
@@ -168,13 +196,19 @@ class Auction:
         ctx = np.empty((self.embedding_size, B))
         part = np.empty((P, B), np.int32)
         u = np.empty(B)
-        for r, (c, p, uu, _, _) in enumerate(rows):
+        for r, (c, p, uu, _, _, _) in enumerate(rows):
             ctx[:, r], part[:, r], u[r] = c, p, uu
         inp = {"ctx": torch.from_numpy(ctx).to(d), "part": torch.from_numpy(part).to(d),
                "u": torch.from_numpy(u).to(d)}
         if self._shading.any():
             g = np.stack([row[3] for row in rows], axis=1)
             inp["gamma_raw"] = torch.from_numpy(np.ascontiguousarray(g)).to(d)
+        if self._learning.any():
+            e = np.zeros((P, B), np.float32)
+            for r, row in enumerate(rows):
+                if row[5] is not None:
+                    e[:, r] = row[5]
+            inp["policy_eps"] = torch.from_numpy(e).to(d)
         if self._lrts.any() and self._ts:
             KDo = self._engine.K * (self.obs_embedding_size + 1)
             z = np.zeros((B, P, KDo), np.float32)
@@ -255,9 +289,10 @@ class Auction:
             st = self._grow("lrts", need, eng.new_lrts_samples)
             eng.lrts_collect(inp, out, st)
             self._bounds["lrts"] = need
-        if self._empirical.any():
+        if self._shading_rec.any():
             need = self._bounds["shading"] + B * self.num_participants_per_round
-            st = self._grow("shading", need, eng.new_shading_samples)
+            learning = bool(self._learning.any())
+            st = self._grow("shading", need, lambda cap: eng.new_shading_samples(cap, learning=learning))
             eng.shading_collect(inp, out, st, first_auction=first_auction)
             self._bounds["shading"] = need
 
@@ -274,7 +309,7 @@ class Auction:
                 self._pending_state.setdefault(int(i), {})["lrts"] = (m[i].copy(), q[i].copy(),
                                                                       pm[i].copy(), int(ep[i]))
         if self._empirical.any():
-            st = self._stores.get("shading") or eng.new_shading_samples(1)
+            st = self._stores.get("shading") or eng.new_shading_samples(1, learning=bool(self._learning.any()))
             pg = eng.empirical_update(st)
             for i in np.nonzero(self._empirical)[0]:
                 self._pending_state.setdefault(int(i), {})["prev_gamma"] = float(pg[i])
@@ -291,11 +326,9 @@ class Auction:
             ag.bidder.prev_gamma = state["prev_gamma"]
 
     def _update_agent(self, index, iteration):
-        """Agent.update (src/Agent.py:79-94) of agent `index` on the GPU."""
-        a = self.agents[index]
-        if a.bidder.kind not in (_lib.BIDDER_TRUTHFUL, _lib.BIDDER_EMPIRICAL_SHADED):
-            raise NotImplementedError(
-                f"{type(a.bidder).__name__}.update (src/Bidder.py) is not on the GPU path yet")
+        """Agent.update (src/Agent.py:79-94) of agent `index` on the GPU: its allocator's update
+        (LR-TS: batched over all LR-TS agents at the first update, they draw nothing), then its
+        bidder's."""
         if not self._learner[index]:
             return
         self._flush()
@@ -305,7 +338,49 @@ class Auction:
             self._train_all()
             self._trained = True
         self._apply_state(index)
+        if self._learning[index]:
+            self._update_learner(index)
         self._claimed.add(index)
+
+    NOISE_EPOCHS0 = 2048
+
+    def _update_learner(self, index):
+        """One learning bidder's update (ag_bidder_update with a one-agent mask). The DR and
+        ValueLearning 'policy' fits draw one rsample per record per epoch from torch's global
+        generator (src/Models.py:160, :87): the draws are made here, on the host, with the same
+        torch calls, for a growing epoch budget (the fit's length is only known after it ran;
+        a fit that exhausts its budget is re-run with twice as many epochs, same result), and
+        the generator is left exactly where the reference's is after the update (including the
+        rsample of every record after DR / PolicyLearning fits, src/Bidder.py:605, :423)."""
+        eng = self._engine
+        b = self.agents[index].bidder
+        st = self._stores.get("shading") or eng.new_shading_samples(1, learning=True)
+        n = int(eng.shading_counts(st)[index])
+        mask = np.zeros(len(self.agents), np.int32)
+        mask[index] = 1
+        offs = np.zeros(len(self.agents), np.int64)
+        noisy = b.kind == _lib.BIDDER_DOUBLY_ROBUST or (b.kind == _lib.BIDDER_VALUE_LEARNING
+                                                         and b.inference == "policy")
+        if noisy and n > 0:
+            max_ep = 32768 if b.kind == _lib.BIDDER_DOUBLY_ROBUST else 16384
+            stream = _TorchNoise(n, eng.device)
+            E = min(self.NOISE_EPOCHS0, max_ep)
+            while True:
+                ep, stat = eng.bidder_update(st, stream.upto(E), offs, E, agents=mask)
+                if stat[index] != -3 or E >= max_ep:
+                    break
+                E = min(2 * E, max_ep)
+            stream.rewind(int(ep[index, 2]))
+        else:
+            ep, stat = eng.bidder_update(st, None, offs, 0, agents=mask)
+        state, init = eng.dr_state()
+        b._load_state16(state[index])
+        b.model_initialised = bool(init[index] != _lib.LEARNER_UNINITIALISED)
+        b.epochs = ep[index].copy()
+        if stat[index] == 1:
+            print(f"! Fallback for {self.agents[index].name}")
+        if b.kind in (_lib.BIDDER_DOUBLY_ROBUST, _lib.BIDDER_POLICY_LEARNING) and n > 0:
+            torch.empty(n).normal_()  # pred_gammas = policy(X) after the fit
 
     def _cleared_logs(self, index):
         if not self._learner[index]:
@@ -341,3 +416,32 @@ class Auction:
     def clear_revenue(self):
         self._flush()
         self._revenue_fx = 0
+
+
+class _TorchNoise:
+    """Per-epoch rsample draws of one agent's fit, torch.empty(n).normal_() per epoch from
+    torch's global generator (torch.distributions.Normal.rsample of an [n, 1] batch), made on
+    demand; rewind(e) leaves the generator as if exactly e epochs had been drawn."""
+
+    SNAP = 256
+
+    def __init__(self, n, device):
+        self.n, self.device = n, device
+        self.snaps = [torch.get_rng_state()]
+        self.host = []
+        self.dev = None
+
+    def upto(self, E):
+        while len(self.host) < E:
+            if len(self.host) % self.SNAP == 0 and len(self.host) // self.SNAP >= len(self.snaps):
+                self.snaps.append(torch.get_rng_state())
+            self.host.append(torch.empty(self.n).normal_())
+        if self.dev is None or self.dev.numel() < E * self.n:
+            self.dev = torch.cat(self.host[:E]).to(self.device)
+        return self.dev
+
+    def rewind(self, e):
+        k = e // self.SNAP
+        torch.set_rng_state(self.snaps[k])
+        for _ in range(e - k * self.SNAP):
+            torch.empty(self.n).normal_()

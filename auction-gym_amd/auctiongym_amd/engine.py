@@ -333,16 +333,19 @@ class AuctionEngine:
         m = np.ascontiguousarray(modes, np.int32).reshape(self.N)
         self._check(self.L.ag_set_bidder_modes(self._h, m.ctypes.data), "ag_set_bidder_modes")
 
-    def bidder_update(self, store, noise=None, noise_offsets=None, noise_epochs=0, trace=False):
-        """Bidder.update of every learning bidder (ag_bidder_update). noise: float32 device
-        tensor with agent a's per-epoch rsample draws at noise_offsets[a] (rows of its record
-        count), for DoublyRobust / ValueLearning 'policy' agents. Returns (epochs [N][3],
-        status [N]) and, with trace=True, the traces [N][3][32768]."""
+    def bidder_update(self, store, noise=None, noise_offsets=None, noise_epochs=0, trace=False, agents=None):
+        """Bidder.update of the learning bidders (ag_bidder_update; agents: [N] mask, None =
+        all). noise: float32 device tensor with agent a's per-epoch rsample draws at
+        noise_offsets[a] (rows of its record count), for DoublyRobust / ValueLearning 'policy'
+        agents. Returns (epochs [N][3], status [N]) and, with trace=True, the traces
+        [N][3][32768]. status -3: the agent needs more noise epochs (left unchanged)."""
+        mask = None if agents is None else np.ascontiguousarray(agents, np.int32).reshape(self.N)
         ep = np.zeros((self.N, 3), np.int32)
         stat = np.zeros(self.N, np.int32)
         off = np.ascontiguousarray(noise_offsets if noise_offsets is not None else np.zeros(self.N), np.int64)
         tr = torch.zeros((self.N, 3, 32768), dtype=torch.float32, device=self.device) if trace else None
-        self._check(self.L.ag_bidder_update(self._h, ctypes.byref(self._shading(store)), _ptr(noise),
+        self._check(self.L.ag_bidder_update(self._h, ctypes.byref(self._shading(store)),
+                                            None if mask is None else mask.ctypes.data, _ptr(noise),
                                             off.ctypes.data, int(noise_epochs), ep.ctypes.data, stat.ctypes.data,
                                             _ptr(tr), _stream()), "ag_bidder_update")
         return (ep, stat, tr) if trace else (ep, stat)

@@ -19,6 +19,7 @@ generator (src/Models.py:31). draw_round_population makes the same calls in the 
 winner's sigmoid underflows to 0, which needs items . ctx < -745.)
 """
 import numpy as np
+import torch
 
 
 def draw_round(rng, num_agents, num_participants, embedding_size, embedding_var, max_slots=1):
@@ -44,25 +45,34 @@ def draw_rounds(rng, B, num_agents, num_participants, embedding_size, embedding_
 
 
 def draw_round_population(rng, num_agents, num_participants, embedding_size, embedding_var,
-                          shading, ts_models, max_slots=1):
+                          shading, ts_models, max_slots=1, policy=None):
     """One round of a general population. shading[a] = (prev_gamma, gamma_sigma) of a shading
     bidder in its uninitialised state (else None); ts_models[a] = the LR-TS model whose
-    Thompson draw the round makes (else None). Returns ctx [E], part [P], gamma_raw [P]
-    (NaN where nothing is drawn), u, ts_noise [P][K*Do] float32 or None."""
+    Thompson draw the round makes (else None); policy[a] = True for a learning bidder bidding
+    from its fitted policy, whose rsample draws one standard normal from torch's generator
+    (src/Models.py:87-88 / :160-161, via torch.distributions.Normal.rsample). Returns ctx [E],
+    part [P], gamma_raw [P] (NaN where nothing is drawn), u, ts_noise [P][K*Do] float32 or
+    None, policy_eps [P] float32 (0 where nothing is drawn) or None."""
     rng.integers(1, max_slots + 1)
     ctx = rng.normal(0, embedding_var, size=embedding_size)
     part = rng.choice(num_agents, num_participants, replace=False)
     gamma_raw = np.full(num_participants, np.nan)
     noise = None
+    eps = None
     for s, a in enumerate(part):
         m = ts_models[a]
-        if m is not None:
+        if m is not None:  # Agent.select_item: the allocator's Thompson draw first
             z = m.sample_noise().numpy().ravel()
             if noise is None:
                 noise = np.zeros((num_participants, z.size), np.float32)
             noise[s] = z
+        if policy is not None and policy[a]:  # then the bidder's
+            if eps is None:
+                eps = np.zeros(num_participants, np.float32)
+            eps[s] = torch.empty(1).normal_().item()
+            continue
         sh = shading[a]
         if sh is not None:
             gamma_raw[s] = rng.normal(sh[0], sh[1])
     u = rng.random()
-    return ctx, part, gamma_raw, u, noise
+    return ctx, part, gamma_raw, u, noise, eps

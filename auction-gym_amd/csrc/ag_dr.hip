@@ -179,7 +179,8 @@ struct TrainLds {
   double wf[kDrThreads / 64][16];
   double ftot[16];
   AdamState adam;
-  int stop;
+  int stop;       // a NaN loss
+  int exhausted;  // a noise-driven fit ran out of noise epochs before it stopped
 };
 
 __device__ __forceinline__ void adam_reset(TrainLds &S) {
@@ -360,6 +361,7 @@ __device__ int fit_dr(const DrRecords &R, const double *eu, int64_t n, TrainLds 
     __syncthreads();
     if (stop || S.stop) return e + 1;
   }
+  if (e < kDrEpochs && tid == 0) S.exhausted = 1;
   return e;
 }
 
@@ -405,6 +407,7 @@ __device__ int fit_dm(const DrRecords &R, int64_t n, TrainLds &S, const float *n
     __syncthreads();
     if (stop) return e + 1;
   }
+  if (e < kInitEpochs && tid == 0) S.exhausted = 1;
   return e;
 }
 
@@ -508,19 +511,22 @@ __device__ int fit_pl(const DrRecords &R, int64_t n, TrainLds &S, int kind, cons
 // fallback (no wins: nothing trained), -1 no logs, -2 NaN loss; epochs [3] = (win-rate,
 // imitation, policy fit); traces [3][32768].
 __global__ __launch_bounds__(kDrThreads) void k_bidder_train(
-    const int32_t *__restrict__ bkind, const int32_t *__restrict__ bmode, const int64_t *__restrict__ offsets,
+    const int32_t *__restrict__ bkind, const int32_t *__restrict__ bmode, const int32_t *__restrict__ mask,
+    const int64_t *__restrict__ offsets,
     DrRecords R0, double *__restrict__ eu_ws, float *__restrict__ state, const int32_t *__restrict__ initialised,
     const float *__restrict__ noise, const int64_t *__restrict__ noise_off, int noise_epochs,
     const double *__restrict__ adam_tab, int32_t *__restrict__ epochs_out, int32_t *__restrict__ status,
     float *__restrict__ traces) {
   const int a = blockIdx.x, tid = threadIdx.x;
   const int bk = bkind[a];
-  const bool learner = bk == AG_BIDDER_VALUE_LEARNING || bk == AG_BIDDER_POLICY_LEARNING ||
-                       bk == AG_BIDDER_DOUBLY_ROBUST;
+  const bool learner = (bk == AG_BIDDER_VALUE_LEARNING || bk == AG_BIDDER_POLICY_LEARNING ||
+                        bk == AG_BIDDER_DOUBLY_ROBUST) && (!mask || mask[a]);
   const int64_t s0 = offsets[a], n = offsets[a + 1] - s0;
   if (tid == 0) epochs_out[3 * a] = epochs_out[3 * a + 1] = epochs_out[3 * a + 2] = 0;
   if (!learner || n == 0) {
-    if (tid == 0) status[a] = learner ? -1 : 0;
+    // no logs: a ValueLearningBidder falls back (its won mask sums to 0, src/Bidder.py:206-
+    // 211); the other learners fail in the reference
+    if (tid == 0) status[a] = !learner ? 0 : (bk == AG_BIDDER_VALUE_LEARNING ? 1 : -1);
     return;
   }
   __shared__ TrainLds S;
@@ -528,7 +534,7 @@ __global__ __launch_bounds__(kDrThreads) void k_bidder_train(
   float *st = state + (size_t)a * 16;
   if (tid < 4) S.wr[tid] = st[tid];
   if (tid < 12) S.pol[tid] = st[4 + tid];
-  if (tid == 0) S.stop = 0;
+  if (tid == 0) S.stop = S.exhausted = 0;
   __syncthreads();
   DrRecords R{R0.ctr + s0, R0.value + s0, R0.gamma + s0, R0.prop + s0, R0.util + s0, R0.won + s0};
   float *tr = traces ? traces + (size_t)a * 3 * kDrEpochs : nullptr;
@@ -566,12 +572,14 @@ __global__ __launch_bounds__(kDrThreads) void k_bidder_train(
     stat = S.stop ? -2 : 0;
   }
   __syncthreads();
+  if (S.exhausted) stat = -3;  // not applied: the caller supplies more noise epochs
   if (tid == 0) {
     epochs_out[3 * a] = ep[0];
     epochs_out[3 * a + 1] = ep[1];
     epochs_out[3 * a + 2] = ep[2];
     status[a] = stat;
   }
+  if (stat == -3) return;
   if (tid < 4) st[tid] = S.wr[tid];
   if (tid < 12) st[4 + tid] = S.pol[tid];
 }
@@ -670,7 +678,7 @@ static int dr_ws_ready(ag_ctx *c) {
       if (c->h_bkind && c->h_bkind[a] == AG_BIDDER_POLICY_LEARNING) m[a] = AG_PL_LOSS_PPO;
     e = hipMemcpy(w.mode, m.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice);
   }
-  if (e == hipSuccess) e = hipMalloc(&w.scratch, sizeof(int64_t) * (size_t)N + sizeof(int32_t) * 4 * (size_t)N);
+  if (e == hipSuccess) e = hipMalloc(&w.scratch, sizeof(int64_t) * (size_t)N + sizeof(int32_t) * 5 * (size_t)N);
   if (e != hipSuccess) {
     ag_dr_release(c);
     return ag_set_error(AG_ERR_HIP, "DR workspace: %s", hipGetErrorString(e));
@@ -728,8 +736,9 @@ int ag_shading_counts(ag_ctx *c, const ag_shading_samples *s, int64_t *counts, v
   return AG_OK;
 }
 
-int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const float *noise, const int64_t *noise_offsets,
-                     int32_t noise_epochs, int32_t *epochs, int32_t *status, float *traces, void *stream) {
+int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agents, const float *noise,
+                     const int64_t *noise_offsets, int32_t noise_epochs, int32_t *epochs, int32_t *status,
+                     float *traces, void *stream) {
   if (!c || !s || !noise_offsets || (!noise && noise_epochs > 0))
     return ag_set_error(AG_ERR_INVALID, "ag_bidder_update: null argument");
   if (!s->ctr || !s->value || !s->propensity || !s->won || !s->order)
@@ -783,11 +792,13 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const float *noise,
     AG_HIP(hipGetLastError());
   }
   int64_t *d_noff = w.scratch;                       // [N] noise offsets
-  int32_t *d_epochs = (int32_t *)(w.scratch + N);     // [N][3] epochs, then [N] status
+  int32_t *d_epochs = (int32_t *)(w.scratch + N);     // [N][3] epochs, then [N] status, [N] mask
   int32_t *d_stat = d_epochs + 3 * (size_t)N;
+  int32_t *d_mask = agents ? d_stat + N : nullptr;
   AG_HIP(hipMemcpyAsync(d_noff, noise_offsets, sizeof(int64_t) * N, hipMemcpyHostToDevice, st));
+  if (agents) AG_HIP(hipMemcpyAsync(d_mask, agents, sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
   DrRecords R{b_ctr, b_val, b_gam, b_prop, b_util, b_won};
-  hipLaunchKernelGGL(k_bidder_train, dim3(N), dim3(kDrThreads), 0, st, c->d_bkind, w.mode, d_off, R, b_eu, w.state,
+  hipLaunchKernelGGL(k_bidder_train, dim3(N), dim3(kDrThreads), 0, st, c->d_bkind, w.mode, d_mask, d_off, R, b_eu, w.state,
                      w.init, noise, d_noff, noise_epochs, w.adam_tab, d_epochs, d_stat, traces);
   AG_HIP(hipGetLastError());
   std::vector<int32_t> h(4 * (size_t)N);
@@ -812,6 +823,7 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const float *noise,
   AG_HIP(hipMemcpy(mode.data(), w.mode, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
   for (int a = 0; a < N; ++a) {
     const int bk = c->h_bkind[a];
+    if ((agents && !agents[a]) || h[3 * N + a] == -3) continue;  // not updated
     if (bk == AG_BIDDER_DOUBLY_ROBUST || bk == AG_BIDDER_POLICY_LEARNING)
       init[a] = AG_LEARNER_POLICY;
     else if (bk == AG_BIDDER_VALUE_LEARNING)
@@ -825,7 +837,13 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const float *noise,
 
 int ag_dr_update(ag_ctx *c, const ag_shading_samples *s, const float *noise, const int64_t *noise_offsets,
                  int32_t noise_epochs, int32_t *epochs, float *traces, void *stream) {
-  return ag_bidder_update(c, s, noise, noise_offsets, noise_epochs, epochs, nullptr, traces, stream);
+  std::vector<int32_t> stat(c->shape.num_agents);
+  if (int rc = ag_bidder_update(c, s, nullptr, noise, noise_offsets, noise_epochs, epochs, stat.data(), traces, stream))
+    return rc;
+  for (int a = 0; a < c->shape.num_agents; ++a)
+    if (stat[a] == -3)
+      return ag_set_error(AG_ERR_INVALID, "agent %d: the DR fit needs more than %d noise epochs", a, noise_epochs);
+  return AG_OK;
 }
 
 int ag_set_bidder_modes(ag_ctx *c, const int32_t *modes) {

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define AG_ABI_VERSION 11
+#define AG_ABI_VERSION 12
 
 typedef enum ag_status {
   AG_OK = 0,
@@ -339,12 +339,16 @@ int ag_set_bidder_modes(ag_ctx *ctx, const int32_t *modes);
  *    inference 'policy', the policy fit (rsample noise as for DR, <= 16384 epochs);
  *  - PolicyLearningBidder (:364-431): imitation of the logging policy (first update), then
  *    the fit of its loss (no noise).
- * epochs host int32 [N][3] = (win-rate, imitation, policy fit); status host int32 [N]: 0
- * trained, 1 fallback (may be NULL); traces dev float32 [N][3][32768] (may be NULL).
- * AG_ERR_INVALID where the reference fails (no logs; a NaN loss, where it exits).
- * Synchronises. Arithmetic: oracle/ag_oracle_dr.c ora_dr_update / ora_vl_update /
- * ora_pl_update. */
-int ag_bidder_update(ag_ctx *ctx, const ag_shading_samples *samples, const float *noise,
+ * agents: host int32 [N], nonzero = update this agent (NULL: every learning bidder; the
+ * reference updates agents one by one, src/main.py:127-128, and the torch draws of one
+ * agent's update depend on the epochs the previous one ran). epochs host int32 [N][3] =
+ * (win-rate, imitation, policy fit); status host int32 [N] (may be NULL): 0 trained, 1
+ * fallback, -3 a noise-driven fit used all noise_epochs without stopping -- that agent's
+ * state is left unchanged, call again with more noise epochs; traces dev float32
+ * [N][3][32768] (may be NULL). AG_ERR_INVALID where the reference fails (no logs; a NaN
+ * loss, where it exits). Synchronises. Arithmetic: oracle/ag_oracle_dr.c ora_dr_update /
+ * ora_vl_update / ora_pl_update. */
+int ag_bidder_update(ag_ctx *ctx, const ag_shading_samples *samples, const int32_t *agents, const float *noise,
                      const int64_t *noise_offsets, int32_t noise_epochs, int32_t *epochs, int32_t *status,
                      float *traces, void *stream);
 

@@ -596,6 +596,76 @@ def learner_update_kat(cfg_name, out_name, rounds=2048):
     np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
 
 
+def learner_driver_kat(cfg_name, out_name, rounds, iters, torch_seed=0):
+    """The reference's driver loop (src/main.py:113-155) on a learning-bidder config for
+    `iters` iterations of `rounds` rounds (torch seeded with torch_seed before the agents
+    are built), recording per iteration the revenue, net and gross utilities, and after
+    every agent's update its bidder's parameters, the scheduled fits' epochs, the
+    imitation's epochs and the torch generator state; plus the numpy Generator state after
+    each iteration's rounds."""
+    import torch
+    import main as M
+    cfg = load_cfg(cfg_name, num_runs=1, num_iter=iters, rounds_per_iter=rounds)
+    path = write_cfg(cfg)
+    (rng, config, agent_configs, agents2items, agents2item_values, num_runs, max_slots,
+     E, var, OE) = M.parse_config(path)
+    os.unlink(path)
+    torch.manual_seed(torch_seed)
+    agents = M.instantiate_agents(rng, agent_configs, agents2item_values, agents2items)
+    auction, num_iter, rpi, _ = M.instantiate_auction(rng, config, agents2items, agents2item_values,
+                                                      agents, max_slots, E, var, OE)
+    recs, mse_n = [], [0]
+
+    class RecRP(torch.optim.lr_scheduler.ReduceLROnPlateau):
+        def __init__(self, *a, verbose=None, **k):
+            super().__init__(*a, **k)
+            self.n = 0
+            recs.append(self)
+
+        def step(self, metrics, *a, **k):
+            self.n += 1
+            return super().step(metrics, *a, **k)
+
+    class RecMSE(torch.nn.MSELoss):
+        def forward(self, a, b):
+            mse_n[0] += 1
+            return super().forward(a, b)
+
+    saved, saved_mse = torch.optim.lr_scheduler.ReduceLROnPlateau, torch.nn.MSELoss
+    torch.optim.lr_scheduler.ReduceLROnPlateau, torch.nn.MSELoss = RecRP, RecMSE
+    out = {"cfg": np.array(json.dumps(cfg))}
+    try:
+        for it in range(num_iter):
+            for _ in range(rpi):
+                auction.simulate_opportunity()
+            out[f"it{it}_revenue"] = np.array(auction.revenue)
+            out[f"it{it}_net"] = np.array([a.net_utility for a in agents])
+            out[f"it{it}_gross"] = np.array([a.gross_utility for a in agents])
+            out[f"it{it}_np_state"] = np.array(json.dumps(rng.bit_generator.state))
+            for i, a in enumerate(agents):
+                recs.clear()
+                mse_n[0] = 0
+                a.update(iteration=it)
+                b = a.bidder
+                out[f"it{it}_a{i}_fits"] = np.array([r.n for r in recs[1:]])  # recs[0]: LR-TS
+                out[f"it{it}_a{i}_imitation"] = np.array(mse_n[0] // 2)
+                for name in ("winrate_model", "bidding_policy", "model"):
+                    mod = getattr(b, name, None)
+                    if mod is not None:
+                        out[f"it{it}_a{i}_{name}"] = np.concatenate(
+                            [p.detach().numpy().ravel() for p in mod.parameters()])
+                out[f"it{it}_a{i}_init"] = np.array(bool(b.model_initialised))
+                out[f"it{it}_a{i}_torch_state"] = torch.get_rng_state().numpy()
+                a.clear_utility()
+                a.clear_logs()
+            auction.clear_revenue()
+            print(cfg_name, "iteration", it, "revenue", out[f"it{it}_revenue"],
+                  [list(out[f"it{it}_a{i}_fits"]) for i in range(len(agents))], flush=True)
+    finally:
+        torch.optim.lr_scheduler.ReduceLROnPlateau, torch.nn.MSELoss = saved, saved_mse
+    np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
+
+
 def sigmoid_kats():
     """Reference sigmoid (numba-faithful shim) on OracleAllocator-shaped dots."""
     import Models
@@ -740,8 +810,8 @@ def csv_outputs(runs=2, iters=3, rounds=2000):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also run SP_Oracle as shipped (3x20x10k rounds, ~1 min)")
-    ap.add_argument("--which", choices=["dm", "ips"], help="with --only learners: one config")
-    ap.add_argument("--only", choices=["empirical", "csv", "dr", "learners"], help="regenerate one fixture family only")
+    ap.add_argument("--which", choices=["dm", "ips", "dr"], help="with --only learners/drivers: one config")
+    ap.add_argument("--only", choices=["empirical", "csv", "dr", "learners", "drivers"], help="regenerate one fixture family only")
     args = ap.parse_args()
     install_shims()
     if args.only == "empirical":
@@ -752,6 +822,11 @@ def main():
         return
     if args.only == "dr":
         dr_update_kat()
+    if args.only == "drivers":
+        for cfg_name, tag in (("FP_DR_TS.json", "dr"), ("FP_DM_TS.json", "dm"), ("FP_IPS_TS.json", "ips")):
+            if args.which in (None, tag):
+                learner_driver_kat(cfg_name, f"{tag}_driver_kat", rounds=1000, iters=3)
+        return
     if args.only == "learners":
         if args.which in (None, "dm"):
             learner_update_kat("FP_DM_TS.json", "dm_update_kat")
