@@ -141,23 +141,21 @@ class Auction:
         if not (self._shading.any() or (self._lrts.any() and self._ts)):
             ctx, part, u = draw_round(self.rng, N, P, self.embedding_size, self.embedding_var,
                                       self.max_slots)
-            self._pending.append((ctx, part, u, None, None, None))
+            self._pending.append((ctx, part, u, None, None, None, None))
             return
         shading = [(a.bidder.prev_gamma, a.bidder.gamma_sigma) if self._shading[i] else None
                    for i, a in enumerate(self.agents)]
         models = [a.allocator.response_model if (self._lrts[i] and self._ts) else None
                   for i, a in enumerate(self.agents)]
-        policy = None
+        policy = search = None
         if self._learning.any():
             ls = [a.bidder._learner_state() if self._learning[i] else 0 for i, a in enumerate(self.agents)]
-            if _lib.LEARNER_SEARCH in ls:
-                raise NotImplementedError("ValueLearningBidder 'search' bids (src/Bidder.py:180-196) "
-                                          "are not on the GPU path yet")
             policy = [x == _lib.LEARNER_POLICY for x in ls]
-        ctx, part, g, u, noise, eps = draw_round_population(
+            search = [x == _lib.LEARNER_SEARCH for x in ls]
+        ctx, part, g, u, noise, eps, grid = draw_round_population(
             self.rng, N, P, self.embedding_size, self.embedding_var, shading, models, self.max_slots,
-            policy)
-        self._pending.append((ctx, part, u, g, noise, eps))
+            policy, search)
+        self._pending.append((ctx, part, u, g, noise, eps, grid))
 
     def _flush_limit(self):
         return self.FLUSH_ROUNDS_TS if (self._lrts.any() and self._ts) else self.FLUSH_ROUNDS
@@ -184,6 +182,8 @@ class Auction:
         eng.generate(seed, first_auction, inp)
         if "gamma_raw" in inp or "ts_noise" in inp:
             eng.generate_noise(seed, first_auction, inp)
+        if "gamma_grid" in inp:
+            eng.generate_search_grid(seed, first_auction, inp)
         self._run(inp)
 
     # ------------------------------------------------------------------ engine
@@ -196,7 +196,7 @@ class Auction:
         ctx = np.empty((self.embedding_size, B))
         part = np.empty((P, B), np.int32)
         u = np.empty(B)
-        for r, (c, p, uu, _, _, _) in enumerate(rows):
+        for r, (c, p, uu, _, _, _, _) in enumerate(rows):
             ctx[:, r], part[:, r], u[r] = c, p, uu
         inp = {"ctx": torch.from_numpy(ctx).to(d), "part": torch.from_numpy(part).to(d),
                "u": torch.from_numpy(u).to(d)}
@@ -209,6 +209,12 @@ class Auction:
                 if row[5] is not None:
                     e[:, r] = row[5]
             inp["policy_eps"] = torch.from_numpy(e).to(d)
+            if any(row[6] is not None for row in rows):
+                gg = np.zeros((P, 128, B))
+                for r, row in enumerate(rows):
+                    if row[6] is not None:
+                        gg[:, :, r] = row[6]
+                inp["gamma_grid"] = torch.from_numpy(gg).to(d)
         if self._lrts.any() and self._ts:
             KDo = self._engine.K * (self.obs_embedding_size + 1)
             z = np.zeros((B, P, KDo), np.float32)

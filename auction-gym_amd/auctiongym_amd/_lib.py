@@ -32,8 +32,9 @@ EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params
            "ag_generate_noise", "ag_lrts_collect", "ag_lrts_update", "ag_lrts_read",
            "ag_shading_collect", "ag_empirical_update", "ag_set_dr_state", "ag_get_dr_state",
            "ag_shading_counts", "ag_dr_update", "ag_set_bidder_modes", "ag_bidder_update",
+           "ag_generate_search_grid",
            "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_last_error", "ag_abi_version")
-ABI_VERSION = 12
+ABI_VERSION = 13
 LEARNER_UNINITIALISED, LEARNER_POLICY, LEARNER_SEARCH = 0, 1, 2
 VL_SEARCH, VL_POLICY = 0, 1
 PL_LOSSES = {"REINFORCE": 0, "REINFORCE_offpolicy": 1, "TRPO": 2, "PPO": 3}
@@ -52,7 +53,7 @@ class AgShape(ctypes.Structure):
 class AgBatchIn(ctypes.Structure):
     _fields_ = [("ctx", ctypes.c_void_p), ("part", ctypes.c_void_p), ("u", ctypes.c_void_p),
                 ("gamma_raw", ctypes.c_void_p), ("ts_noise", ctypes.c_void_p),
-                ("policy_eps", ctypes.c_void_p)]
+                ("policy_eps", ctypes.c_void_p), ("gamma_grid", ctypes.c_void_p)]
 
 
 class AgBatchOut(ctypes.Structure):
@@ -117,6 +118,7 @@ def load(path=None):
         "ag_set_bidder_modes": (ctypes.c_int, [vp, vp]),
         "ag_bidder_update": (ctypes.c_int, [vp, ctypes.POINTER(AgShadingSamples), vp, vp, vp, i32, vp, vp, vp, vp]),
         "ag_generate_noise": (ctypes.c_int, [vp, u64, u64, i64, vp, vp, vp, vp, vp]),
+        "ag_generate_search_grid": (ctypes.c_int, [vp, u64, u64, i64, vp, vp]),
         "ag_allocate": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, vp]),
         "ag_simulate": (ctypes.c_int, [vp, i64, ctypes.POINTER(AgBatchIn),
                                        ctypes.POINTER(AgBatchOut), vp, vp]),

@@ -30,6 +30,11 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+def _batch_in(inputs):
+    return AgBatchIn(*[_ptr(inputs.get(k)).value for k in ("ctx", "part", "u", "gamma_raw", "ts_noise",
+                                                           "policy_eps", "gamma_grid")])
+
+
 def require_gpu():
     if not torch.cuda.is_available():
         raise RuntimeError("auctiongym_amd needs a ROCm GPU (MI355X); none is visible. "
@@ -85,6 +90,7 @@ class AuctionEngine:
         pg = None if prev_gamma is None else np.ascontiguousarray(prev_gamma, np.float64)
         gs = None if gamma_sigma is None else np.ascontiguousarray(gamma_sigma, np.float64)
         self.shading = bool((b != _lib.BIDDER_TRUTHFUL).any())
+        self._bkind = b.copy()
         self.dr = bool(np.isin(b, (_lib.BIDDER_VALUE_LEARNING, _lib.BIDDER_POLICY_LEARNING,
                                    _lib.BIDDER_DOUBLY_ROBUST)).any())  # learning bidders
         self.lrts = bool((a == _lib.ALLOCATOR_LRTS).any())
@@ -131,9 +137,7 @@ class AuctionEngine:
     def lrts_collect(self, inputs, outputs, store):
         """Append the won LR-TS samples of a simulated batch (ag_lrts_collect)."""
         B = inputs["u"].shape[0]
-        bi = AgBatchIn(_ptr(inputs["ctx"]).value, _ptr(inputs["part"]).value, _ptr(inputs["u"]).value,
-                       _ptr(inputs.get("gamma_raw")).value, _ptr(inputs.get("ts_noise")).value,
-                       _ptr(inputs.get("policy_eps")).value)
+        bi = _batch_in(inputs)
         bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
         st = self._samples(store)
         self._check(self.L.ag_lrts_collect(self._h, B, ctypes.byref(bi), ctypes.byref(bo),
@@ -190,6 +194,8 @@ class AuctionEngine:
             inp["gamma_raw"] = torch.empty((self.P, B), dtype=torch.float64, device=d)
         if getattr(self, "dr", False):
             inp["policy_eps"] = torch.empty((self.P, B), dtype=torch.float32, device=d)
+        if getattr(self, "vl_search", False):
+            inp["gamma_grid"] = torch.empty((self.P, 128, B), dtype=torch.float64, device=d)
         if getattr(self, "lrts", False) and getattr(self, "ts_sample", True):
             inp["ts_noise"] = torch.empty((self.P, (B + 63) // 64, self.K * (self.OE + 1), 64),
                                           dtype=torch.float32, device=d)
@@ -237,9 +243,7 @@ class AuctionEngine:
                 raise ValueError(f"input {k} must be a contiguous tensor on {self.device}")
         if inputs["ctx"].shape != (self.E, B) or inputs["part"].shape != (self.P, B):
             raise ValueError("inputs must be SoA: ctx [E][B], part [P][B], u [B]")
-        bi = AgBatchIn(_ptr(inputs["ctx"]).value, _ptr(inputs["part"]).value, _ptr(inputs["u"]).value,
-                       _ptr(inputs.get("gamma_raw")).value, _ptr(inputs.get("ts_noise")).value,
-                       _ptr(inputs.get("policy_eps")).value)
+        bi = _batch_in(inputs)
         bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
         self._check(self.L.ag_simulate(self._h, B, ctypes.byref(bi), ctypes.byref(bo),
                                  _ptr(counters), _stream()), "ag_simulate")
@@ -248,6 +252,12 @@ class AuctionEngine:
         B = inputs["u"].shape[0]
         self._check(self.L.ag_generate(self._h, int(seed), int(first_auction), B, _ptr(inputs["ctx"]),
                                  _ptr(inputs["part"]), _ptr(inputs["u"]), _stream()), "ag_generate")
+
+    def generate_search_grid(self, seed, first_auction, inputs):
+        """Synthetic ValueLearningBidder search grids into inputs["gamma_grid"] (ag_generate_search_grid)."""
+        B = inputs["u"].shape[0]
+        self._check(self.L.ag_generate_search_grid(self._h, int(seed), int(first_auction), B,
+                                                   _ptr(inputs["gamma_grid"]), _stream()), "ag_generate_search_grid")
 
     def generate_noise(self, seed, first_auction, inputs):
         """Synthetic gamma_raw / ts_noise for the participants already in inputs["part"]."""
@@ -332,6 +342,7 @@ class AuctionEngine:
         (PL_LOSSES) per agent, int32 [N] (ag_set_bidder_modes)."""
         m = np.ascontiguousarray(modes, np.int32).reshape(self.N)
         self._check(self.L.ag_set_bidder_modes(self._h, m.ctypes.data), "ag_set_bidder_modes")
+        self.vl_search = bool(((self._bkind == _lib.BIDDER_VALUE_LEARNING) & (m == _lib.VL_SEARCH)).any())
 
     def bidder_update(self, store, noise=None, noise_offsets=None, noise_epochs=0, trace=False, agents=None):
         """Bidder.update of the learning bidders (ag_bidder_update; agents: [N] mask, None =
@@ -354,9 +365,7 @@ class AuctionEngine:
         """Append the shading-bidder records of a simulated batch of auctions
         [first_auction, first_auction + B) (ag_shading_collect)."""
         B = inputs["u"].shape[0]
-        bi = AgBatchIn(_ptr(inputs["ctx"]).value, _ptr(inputs["part"]).value, _ptr(inputs["u"]).value,
-                       _ptr(inputs.get("gamma_raw")).value, _ptr(inputs.get("ts_noise")).value,
-                       _ptr(inputs.get("policy_eps")).value)
+        bi = _batch_in(inputs)
         bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
         st = self._shading(store)
         self._check(self.L.ag_shading_collect(self._h, int(first_auction), B, ctypes.byref(bi), ctypes.byref(bo),

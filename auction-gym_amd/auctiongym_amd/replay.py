@@ -45,20 +45,24 @@ def draw_rounds(rng, B, num_agents, num_participants, embedding_size, embedding_
 
 
 def draw_round_population(rng, num_agents, num_participants, embedding_size, embedding_var,
-                          shading, ts_models, max_slots=1, policy=None):
+                          shading, ts_models, max_slots=1, policy=None, search=None):
     """One round of a general population. shading[a] = (prev_gamma, gamma_sigma) of a shading
     bidder in its uninitialised state (else None); ts_models[a] = the LR-TS model whose
     Thompson draw the round makes (else None); policy[a] = True for a learning bidder bidding
     from its fitted policy, whose rsample draws one standard normal from torch's generator
-    (src/Models.py:87-88 / :160-161, via torch.distributions.Normal.rsample). Returns ctx [E],
-    part [P], gamma_raw [P] (NaN where nothing is drawn), u, ts_noise [P][K*Do] float32 or
-    None, policy_eps [P] float32 (0 where nothing is drawn) or None."""
+    (src/Models.py:87-88 / :160-161, via torch.distributions.Normal.rsample); search[a] = True
+    for a ValueLearningBidder bidding by search, which draws rng.uniform(0.1, 1.0, 128) and
+    sorts it (src/Bidder.py:184-186). Returns ctx [E], part [P], gamma_raw [P] (NaN where
+    nothing is drawn), u, ts_noise [P][K*Do] float32 or None, policy_eps [P] float32 (0
+    where nothing is drawn) or None, gamma_grid [P][128] (0 where nothing is drawn) or
+    None."""
     rng.integers(1, max_slots + 1)
     ctx = rng.normal(0, embedding_var, size=embedding_size)
     part = rng.choice(num_agents, num_participants, replace=False)
     gamma_raw = np.full(num_participants, np.nan)
     noise = None
     eps = None
+    grid = None
     for s, a in enumerate(part):
         m = ts_models[a]
         if m is not None:  # Agent.select_item: the allocator's Thompson draw first
@@ -71,8 +75,15 @@ def draw_round_population(rng, num_agents, num_participants, embedding_size, emb
                 eps = np.zeros(num_participants, np.float32)
             eps[s] = torch.empty(1).normal_().item()
             continue
+        if search is not None and search[a]:
+            if grid is None:
+                grid = np.zeros((num_participants, 128))
+            gg = rng.uniform(0.1, 1.0, size=128)
+            gg.sort()
+            grid[s] = gg
+            continue
         sh = shading[a]
         if sh is not None:
             gamma_raw[s] = rng.normal(sh[0], sh[1])
     u = rng.random()
-    return ctx, part, gamma_raw, u, noise, eps
+    return ctx, part, gamma_raw, u, noise, eps, grid

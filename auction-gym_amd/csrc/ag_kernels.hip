@@ -290,6 +290,26 @@ __global__ __launch_bounds__(kThreads) void k_generate_noise(uint64_t seed, uint
   }
 }
 
+// Synthetic search grids: U(0.1, 1) with 53-bit uniforms, streams 32 + slot (two per
+// Philox block), grid point j of slot s of auction i at (s*128 + j)*B + i.
+__global__ __launch_bounds__(kThreads) void k_generate_grid(uint64_t seed, uint64_t first, int64_t B, int P,
+                                                           double *grid) {
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < B; i += (int64_t)gridDim.x * kThreads) {
+    const uint64_t idx = first + (uint64_t)i;
+    const uint32_t c0 = (uint32_t)idx, c1 = (uint32_t)(idx >> 32);
+    for (int s = 0; s < P; ++s)
+      for (int j = 0; j < 128; j += 2) {
+        uint32_t w[4];
+        philox(c0, c1, (uint32_t)(j >> 1), 32 + (uint32_t)s, k0, k1, w);
+        const double u0 = (double)((((uint64_t)w[0] << 32) | w[1]) >> 11) * 0x1p-53;
+        const double u1 = (double)((((uint64_t)w[2] << 32) | w[3]) >> 11) * 0x1p-53;
+        grid[((int64_t)s * 128 + j) * B + i] = 0.1 + 0.9 * u0;
+        grid[((int64_t)s * 128 + j + 1) * B + i] = 0.1 + 0.9 * u1;
+      }
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // known-answer kernels
 // ------------------------------------------------------------------------------------
@@ -581,9 +601,8 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
     return ag_set_error(AG_ERR_INVALID, "ag_simulate: shading bidders need gamma_raw");
   if (c->dr_any_init && !in->policy_eps)
     return ag_set_error(AG_ERR_INVALID, "ag_simulate: learning bidders with a fitted policy need policy_eps");
-  if (c->vl_any_search)
-    return ag_set_error(AG_ERR_UNSUPPORTED,
-                        "ag_simulate: ValueLearningBidder 'search' bids (src/Bidder.py:180-196) are not built");
+  if (c->vl_any_search && !in->gamma_grid)
+    return ag_set_error(AG_ERR_INVALID, "ag_simulate: ValueLearningBidders bidding by search need gamma_grid");
   SimParams prm;
   prm.B = B;
   prm.N = s.num_agents;
@@ -660,6 +679,18 @@ int ag_generate(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, double *ctx
   hipLaunchKernelGGL(k_generate, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, seed, first, B,
                      c->shape.num_agents, c->shape.num_participants, c->shape.embedding_size,
                      c->shape.embedding_var, ctx_out, part_out, u_out);
+  AG_HIP(hipGetLastError());
+  return AG_OK;
+}
+
+int ag_generate_search_grid(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, double *grid, void *stream) {
+  if (!c || !grid) return ag_set_error(AG_ERR_INVALID, "ag_generate_search_grid: null argument");
+  if (B < 0) return ag_set_error(AG_ERR_INVALID, "ag_generate_search_grid: B < 0");
+  if (B == 0) return AG_OK;
+  AgDeviceGuard g(c->device);
+  const int grid_n = grid_for(B, (int64_t)1 << 40);
+  hipLaunchKernelGGL(k_generate_grid, dim3(grid_n), dim3(kThreads), 0, (hipStream_t)stream, seed, first, B,
+                     c->shape.num_participants, grid);
   AG_HIP(hipGetLastError());
   return AG_OK;
 }

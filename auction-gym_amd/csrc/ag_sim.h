@@ -446,6 +446,33 @@ __device__ __forceinline__ void policy_bid(const float *p, double ctr, double va
   gamma = raw < 0.0f ? 0.0 : (raw > 1.0f ? 1.0 : (double)raw);
 }
 
+// ValueLearningBidder 'search' bid (src/Bidder.py:180-196): the shading factor maximising
+// the win-rate model's predicted utility W(ctr, value, g) (ev - ev g), ev = value * ctr,
+// over the agent's 128 grid draws (dev [128] with stride B). W in float32 as the
+// reference's torch model: z = ((c w0 + v w1) + g w2) + b without FMAs, W = sigmoid(z)
+// via the glibc-identical double exp, rounded to float32 (torch's vectorised sigmoid may
+// differ by an ulp: the argmax flips only where two grid points' utilities are that close).
+// The first maximum in sorted-grid order = the smallest gamma among tied maxima, so the
+// grid may arrive unsorted. oracle/ag_oracle.c ora_search_gamma is this, bit for bit.
+__device__ __forceinline__ double search_gamma(const float *wr, double ctr, double value, const double *grid,
+                                               uint32_t stride, const uint64_t *tab) {
+  const float c = (float)ctr, v = (float)value;
+  const float cv = c * wr[0] + v * wr[1];
+  const double ev = value * ctr;
+  double best_u = -INFINITY, best_g = 0.0;
+  for (int j = 0; j < 128; ++j) {
+    const double g = grid[(size_t)j * stride];
+    const float z = cv + (float)g * wr[2] + wr[3];
+    const float pw = (float)(1.0 / (1.0 + agexp::exp(-(double)z, tab)));
+    const double ut = (double)pw * (ev - ev * g);
+    if (ut > best_u || (ut == best_u && g < best_g)) {
+      best_u = ut;
+      best_g = g;
+    }
+  }
+  return best_g;
+}
+
 // Gaussian density of a shading factor (src/Bidder.py:178, :355, :462).
 __device__ __forceinline__ double shading_propensity(double pg, double sigma, double g,
                                                      const uint64_t *tab) {
@@ -500,6 +527,10 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
       const int bk = T.bkind[a];
       if (bk >= AG_BIDDER_VALUE_LEARNING && T.drs && T.dri[a] == AG_LEARNER_POLICY) {  // the fitted policy
         policy_bid(T.drs + a * 16 + 4, est, v, in.policy_eps[s * B + i], T.tab, g, prop);
+        b = b * g;
+      } else if (bk == AG_BIDDER_VALUE_LEARNING && T.drs && T.dri[a] == AG_LEARNER_SEARCH) {
+        g = search_gamma(T.drs + a * 16, est, v, in.gamma_grid + (size_t)s * 128 * B + i, B, T.tab);
+        prop = 1.0;  // src/Bidder.py:196
         b = b * g;
       } else if (bk != AG_BIDDER_TRUTHFUL) {
         g = in.gamma_raw[s * B + i];

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define AG_ABI_VERSION 12
+#define AG_ABI_VERSION 13
 
 typedef enum ag_status {
   AG_OK = 0,
@@ -136,8 +136,11 @@ typedef struct ag_batch_in {
                               coefficient of its 64 auctions as one 256-B row and a tile's
                               rows are contiguous; NULL if none / no sampling */
   const float *policy_eps; /* [P][B] the rsample draw (torch, standard normal) of a
-                              DoublyRobustBidder bidding from its fitted policy
-                              (src/Bidder.py:466-470); NULL if none */
+                              learning bidder bidding from its fitted policy
+                              (src/Bidder.py:198-203, :358-362, :466-470); NULL if none */
+  const double *gamma_grid; /* [P][128][B] the rng.uniform(0.1, 1.0, 128) grid of a
+                              ValueLearningBidder bidding by search (src/Bidder.py:184-186),
+                              any order; NULL if none */
 } ag_batch_in;
 
 /* Outputs of B auctions (dev). Any pointer may be NULL to skip that array. */
@@ -228,6 +231,11 @@ int ag_generate(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B, d
  * shading bidders (NaN otherwise), ts_noise (tiled as in ag_batch_in) = z / sqrt(q) for
  * LR-TS agents (0 otherwise), policy_eps [P][B] = z for every slot; any output may be NULL.
  * Same Philox key / counter scheme. */
+/* Synthetic search grids gamma_grid [P][128][B] (U(0.1, 1), Philox as ag_generate_noise,
+ * unsorted: the search takes the smallest gamma among tied maxima) for every slot. */
+int ag_generate_search_grid(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B, double *gamma_grid,
+                            void *stream);
+
 int ag_generate_noise(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B,
                       const int32_t *part, double *gamma_raw, float *ts_noise, float *policy_eps,
                       void *stream);

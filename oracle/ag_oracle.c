@@ -223,6 +223,10 @@ static void simulate_range(const ora_pop *pp, const double *items, const double 
       if (bk >= ORA_BIDDER_VALUE_LEARNING && pp->dr_init && pp->dr_init[a] == 1) { /* fitted policy */
         ora_policy_bid(pp->dr_state + (int64_t)a * 16 + 4, est, v, in->policy_eps[o], &g, &prop);
         b = b * g;
+      } else if (bk == ORA_BIDDER_VALUE_LEARNING && pp->dr_init && pp->dr_init[a] == 2) { /* search */
+        g = ora_search_gamma(pp->dr_state + (int64_t)a * 16, est, v, in->gamma_grid + (int64_t)o * 128, 1);
+        prop = 1.0;
+        b = b * g;
       } else if (bk != ORA_BIDDER_TRUTHFUL) {
         g = shading_gamma(bk, in->gamma_raw[o]);
         if (bk != ORA_BIDDER_EMPIRICAL) prop = ora_propensity(pp->prev_gamma[a], pp->gamma_sigma[a], g);
@@ -330,7 +334,7 @@ void ora_simulate(const ora_shape *s, const double *items, const double *values,
   int32_t *ak = (int32_t *)calloc((size_t)s->N, sizeof(int32_t));
   int32_t *bk = (int32_t *)calloc((size_t)s->N, sizeof(int32_t));
   ora_pop pp = {s->N, s->P, s->K, s->E, s->E, s->mech, ak, bk, NULL, NULL, NULL, 0, NULL, NULL};
-  ora_in in = {ctx, part, u, NULL, NULL, NULL};
+  ora_in in = {ctx, part, u, NULL, NULL, NULL, NULL};
   ora_out out = {winner, price, second_price, outcome, item, value, bid, est_ctr, true_ctr,
                  best_ev, NULL, NULL};
   ora_simulate_pop(&pp, items, values, B, &in, &out, counters, counters_fx, nthreads);

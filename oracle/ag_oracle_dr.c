@@ -414,6 +414,30 @@ int32_t ora_dr_update(int64_t n, const double *ctr, const double *value, const d
   return 0;
 }
 
+/* ValueLearningBidder 'search' bid (src/Bidder.py:180-196): x = float32 [ctr, value, g] for
+ * the 128 grid gammas, W = sigmoid(((c w0 + v w1) + g w2) + b) in float32 (no FMAs; the
+ * sigmoid through libm exp in double, rounded once), utility W (ev - ev g) in double with ev
+ * = value * ctr, the first maximum of the sorted grid = the smallest gamma among ties. torch
+ * evaluates W with its own float32 kernels (an ulp apart at most): the argmax agrees except
+ * where two grid points' utilities are that close. */
+double ora_search_gamma(const float *wr, double ctr, double value, const double *grid, int64_t stride) {
+  const float c = (float)ctr, v = (float)value;
+  const float cv = c * wr[0] + v * wr[1];
+  const double ev = value * ctr;
+  double best_u = -INFINITY, best_g = 0.0;
+  for (int j = 0; j < 128; ++j) {
+    const double g = grid[(int64_t)j * stride];
+    const float z = cv + (float)g * wr[2] + wr[3];
+    const float pw = (float)(1.0 / (1.0 + exp(-(double)z)));
+    const double ut = (double)pw * (ev - ev * g);
+    if (ut > best_u || (ut == best_u && g < best_g)) {
+      best_u = ut;
+      best_g = g;
+    }
+  }
+  return best_g;
+}
+
 /* DoublyRobustBidder.bid with a fitted policy (src/Bidder.py:466-470, src/Models.py:155-164):
  * x = float32 [estimated CTR, value]; the policy's mu and sigma (double, as in the fit, then
  * rounded to float32 like torch's tensors), the rsample mu + sigma * eps in float32, its

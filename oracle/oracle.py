@@ -38,7 +38,8 @@ class _Pop(ctypes.Structure):
 
 
 class _In(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("ctx", "part", "u", "gamma_raw", "ts_noise", "policy_eps")]
+    _fields_ = [(n, ctypes.c_void_p) for n in ("ctx", "part", "u", "gamma_raw", "ts_noise", "policy_eps",
+                                              "gamma_grid")]
 
 
 class _Out(ctypes.Structure):
@@ -94,6 +95,8 @@ def lib():
         L.ora_pl_update.argtypes = [i64] + [vp] * 6 + [i32, i32] + [vp] * 3
         L.ora_pl_loss_grad.restype = ctypes.c_float
         L.ora_pl_loss_grad.argtypes = [i64] + [vp] * 6 + [i32, vp]
+        L.ora_search_gamma.restype = d
+        L.ora_search_gamma.argtypes = [vp, d, d, vp, i64]
         L.ora_log1p_restated.restype = d
         L.ora_log1p_restated.argtypes = [d]
         L.ora_lrts_update.restype = i32
@@ -149,7 +152,7 @@ def simulate(mech, items, values, ctx, part, u, nthreads=1):
 
 def simulate_pop(mech, items, values, ctx, part, u, alloc_kind, bid_kind, prev_gamma=None,
                  gamma_sigma=None, OE=None, ts_m=None, ts_noise=None, gamma_raw=None,
-                 ts_sample=True, dr_state=None, dr_init=None, policy_eps=None, nthreads=1):
+                 ts_sample=True, dr_state=None, dr_init=None, policy_eps=None, gamma_grid=None, nthreads=1):
     """General population (OracleAllocator / LR-TS allocators; truthful / shading bidders in
     their first iteration). Row-major replay inputs; returns outputs + counters."""
     items = np.ascontiguousarray(items, np.float64)
@@ -179,6 +182,7 @@ def simulate_pop(mech, items, values, ctx, part, u, alloc_kind, bid_kind, prev_g
     ds = arr(dr_state if dr_state is not None else np.zeros((N, 16)), np.float32)
     di = arr(dr_init if dr_init is not None else np.zeros(N), np.int32)
     pe = arr(policy_eps if policy_eps is not None else np.zeros((B, P)), np.float32)
+    gg = arr(gamma_grid if gamma_grid is not None else np.zeros((1, 1, 128)), np.float64)
     pop = _Pop(N, P, K, E, OE, int(mech), ak.ctypes.data, bk.ctypes.data, pg.ctypes.data,
                gs.ctypes.data, tm.ctypes.data, int(bool(ts_sample)), ds.ctypes.data, di.ctypes.data)
     out = dict(winner=np.empty(B, np.int32), price=np.empty(B), second_price=np.empty(B),
@@ -188,7 +192,7 @@ def simulate_pop(mech, items, values, ctx, part, u, alloc_kind, bid_kind, prev_g
                propensity=np.empty((B, P)), counters=np.zeros((N, NUM_COUNTERS)),
                counters_fx=np.zeros((N, NUM_COUNTERS, 3), np.int64))
     cin = _In(ctx.ctypes.data, part.ctypes.data, u.ctypes.data, gr.ctypes.data, tn.ctypes.data,
-              pe.ctypes.data)
+              pe.ctypes.data, gg.ctypes.data)
     cout = _Out(*[out[k].ctypes.data for k in ("winner", "price", "second_price", "outcome", "item",
                                                "value", "bid", "est_ctr", "true_ctr", "best_ev",
                                                "gamma", "propensity")])
@@ -344,3 +348,10 @@ def pl_loss_grad(ctr, value, gamma, prop, util, pol, loss="PPO"):
     g = np.zeros(12, np.float32)
     loss_v = lib().ora_pl_loss_grad(n, *[_p(v) for v in a], _p(pol), PL_LOSSES[loss], _p(g))
     return float(loss_v), g
+
+
+def search_gamma(wr, ctr, value, grid):
+    """ValueLearningBidder 'search' (src/Bidder.py:180-196) for one bid over grid [128]."""
+    wr = np.ascontiguousarray(wr, np.float32)
+    grid = np.ascontiguousarray(grid, np.float64)
+    return float(lib().ora_search_gamma(_p(wr), float(ctr), float(value), _p(grid), 1))

@@ -666,6 +666,46 @@ def learner_driver_kat(cfg_name, out_name, rounds, iters, torch_seed=0):
     np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
 
 
+def search_bid_kat(out_name="search_bid_kat", rounds=1000, bids=4000):
+    """ValueLearningBidder 'search' bids (src/Bidder.py:180-196) of FP_DM_Oracle's agents after
+    their first update, through the reference's own bid(): per call the (value, estimated
+    CTR) given, the 128-point grid it drew (the same draws from a clone of its Generator) and
+    the gamma it chose, with the agent's win-rate parameters."""
+    import torch
+    import main as M
+    cfg = load_cfg("FP_DM_Oracle.json", num_runs=1, num_iter=1, rounds_per_iter=rounds)
+    path = write_cfg(cfg)
+    (rng, config, agent_configs, agents2items, agents2item_values, num_runs, max_slots,
+     E, var, OE) = M.parse_config(path)
+    os.unlink(path)
+    torch.manual_seed(0)
+    agents = M.instantiate_agents(rng, agent_configs, agents2item_values, agents2items)
+    auction, _, rpi, _ = M.instantiate_auction(rng, config, agents2items, agents2item_values,
+                                               agents, max_slots, E, var, OE)
+    for _ in range(rpi):
+        auction.simulate_opportunity()
+    out = {}
+    g = np.random.default_rng(11)
+    for i, a in enumerate(agents):
+        a.update(iteration=0)
+        b = a.bidder
+        assert b.model_initialised
+        out[f"a{i}_wr"] = np.concatenate([p.detach().numpy().ravel() for p in b.winrate_model.parameters()])
+        vals = g.lognormal(0.1, 0.2, bids)
+        ctrs = 1.0 / (1.0 + np.exp(-g.normal(-3.0, 1.0, bids)))
+        gammas, out_bids = np.zeros(bids), np.zeros(bids)
+        # each bid draws exactly its 128 grid points from the shared Generator: the grids
+        # are regenerated from this state by the test
+        out[f"a{i}_rng_state"] = np.array(json.dumps(b.rng.bit_generator.state))
+        for j in range(bids):
+            out_bids[j] = b.bid(vals[j], None, ctrs[j])
+            gammas[j] = b.gammas[-1]
+        out[f"a{i}_value"], out[f"a{i}_ctr"] = vals, ctrs
+        out[f"a{i}_gamma"], out[f"a{i}_bid"] = gammas, out_bids
+        print("search bids agent", i, "gamma mean", gammas.mean(), flush=True)
+    np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
+
+
 def sigmoid_kats():
     """Reference sigmoid (numba-faithful shim) on OracleAllocator-shaped dots."""
     import Models
@@ -810,7 +850,7 @@ def csv_outputs(runs=2, iters=3, rounds=2000):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also run SP_Oracle as shipped (3x20x10k rounds, ~1 min)")
-    ap.add_argument("--which", choices=["dm", "ips", "dr"], help="with --only learners/drivers: one config")
+    ap.add_argument("--which", choices=["dm", "ips", "dr", "dmo", "search"], help="with --only learners/drivers: one config")
     ap.add_argument("--only", choices=["empirical", "csv", "dr", "learners", "drivers"], help="regenerate one fixture family only")
     args = ap.parse_args()
     install_shims()
@@ -823,7 +863,10 @@ def main():
     if args.only == "dr":
         dr_update_kat()
     if args.only == "drivers":
-        for cfg_name, tag in (("FP_DR_TS.json", "dr"), ("FP_DM_TS.json", "dm"), ("FP_IPS_TS.json", "ips")):
+        if args.which in (None, "search"):
+            search_bid_kat()
+        for cfg_name, tag in (("FP_DR_TS.json", "dr"), ("FP_DM_TS.json", "dm"), ("FP_IPS_TS.json", "ips"),
+                              ("FP_DM_Oracle.json", "dmo")):
             if args.which in (None, tag):
                 learner_driver_kat(cfg_name, f"{tag}_driver_kat", rounds=1000, iters=3)
         return

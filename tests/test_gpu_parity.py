@@ -1131,3 +1131,77 @@ def test_driver_fp_ips_ts(gpu, tmp_path):
             if it == 0:
                 assert agents[i].bidder.epochs[1] == int(k[f"it0_a{i}_imitation"])
     _run_driver_learners("ips", tmp_path, check)
+
+
+def test_search_bids_match_oracle(gpu, oracle):
+    """ValueLearningBidder 'search' bids (src/Bidder.py:180-196): the gamma maximising the
+    win-rate model's utility over the 128-point grid. Population of OracleAllocator +
+    ValueLearningBidders, half bidding by search (random win-rate models), the rest with
+    Gaussian shading; synthetic contexts, draws and (unsorted) grids; every output equal to
+    the oracle's on the same inputs."""
+    import torch
+    from auctiongym_amd import _lib
+    from auctiongym_amd.engine import AuctionEngine
+    N, P, K, E, OE, B = 8, 3, 12, 5, 4, 1 << 16
+    g = np.random.default_rng(44)
+    items = np.concatenate([g.normal(0, 1, (N, K, E)), -3.0 - g.random((N, K, 1))], axis=2)
+    values = g.lognormal(0.1, 0.2, (N, K))
+    ak = np.zeros(N, np.int32)
+    bk = np.full(N, 2, np.int32)
+    pg, gs = np.ones(N), np.full(N, 0.02)
+    state = g.normal(0, 2.0, (N, 16)).astype(np.float32)
+    init = np.array([2 if a % 2 == 0 else 0 for a in range(N)], np.int32)
+    eng = AuctionEngine(N, P, K, E, OE, 0, 1.0)
+    eng.set_agent_params(ak, bk, pg, gs)
+    eng.load_catalog(items, values)
+    eng.set_dr_state(state, init)
+    eng.set_bidder_modes(np.full(N, _lib.VL_SEARCH, np.int32))
+    inp = eng.alloc_inputs(B)
+    assert "gamma_grid" in inp
+    eng.generate(3, 0, inp)
+    eng.generate_noise(3, 0, inp)
+    eng.generate_search_grid(3, 0, inp)
+    out = eng.alloc_outputs(B)
+    cnt = eng.new_counters()
+    eng.simulate(inp, out, cnt)
+    torch.cuda.synchronize()
+    T = lambda t: np.ascontiguousarray(t.cpu().numpy().T)  # noqa: E731
+    grid = np.ascontiguousarray(inp["gamma_grid"].cpu().numpy().transpose(2, 0, 1))  # [B][P][128]
+    assert grid.min() >= 0.1 and grid.max() < 1.0
+    orc = oracle.simulate_pop(0, items, values, T(inp["ctx"]), T(inp["part"]), inp["u"].cpu().numpy(),
+                              ak, bk, pg, gs, OE=OE, gamma_raw=T(inp["gamma_raw"]), dr_state=state,
+                              dr_init=init, gamma_grid=grid, nthreads=16)
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    for k in ("item", "bid", "est_ctr", "true_ctr", "best_ev", "gamma", "propensity"):
+        assert np.array_equal(np.ascontiguousarray(got[k].T), orc[k], equal_nan=True), k
+    for k in ("winner", "price", "second_price", "outcome"):
+        assert np.array_equal(got[k], orc[k], equal_nan=True), k
+    assert np.array_equal(cnt.cpu().numpy(), orc["counters_fx"])
+    part = T(inp["part"])
+    searched = init[part] == 2
+    gam = np.ascontiguousarray(got["gamma"].T)
+    prop = np.ascontiguousarray(got["propensity"].T)
+    assert searched.any() and (prop[searched] == 1.0).all()
+    assert (gam[searched][:, None] == grid[searched]).any(axis=1).all()  # one of its grid points
+    # without a grid the launch is refused
+    del inp["gamma_grid"]
+    with pytest.raises(ValueError, match="gamma_grid"):
+        eng.simulate(inp, out, eng.new_counters())
+    eng.close()
+
+
+def test_driver_fp_dm_oracle(gpu, tmp_path):
+    """FP_DM_Oracle (OracleAllocator + ValueLearningBidder 'search') through the drop-in driver
+    vs the reference's own run, 3 iterations x 1000 rounds: the numpy draw order (128 grid
+    draws per searching participant) stays aligned; revenue within 1e-8 in iteration 0 and
+    1e-3 afterwards (measured 2.4e-5); the win-rate models after each update within 5e-2
+    (their fits stop by the chaotic 1e-6 rule: measured up to 4.7e-2 apart in iteration 2)."""
+    def check(k, it, auction, agents, rng, i):
+        if i is None:
+            assert json.dumps(rng.bit_generator.state) == str(k[f"it{it}_np_state"])
+            np.testing.assert_allclose(auction.revenue, float(k[f"it{it}_revenue"]), rtol=1e-8 if it == 0 else 1e-3)
+        else:
+            b = agents[i].bidder
+            assert b.model_initialised == bool(k[f"it{it}_a{i}_init"])
+            np.testing.assert_allclose(b._state16()[:4], k[f"it{it}_a{i}_winrate_model"], atol=5e-2)
+    _run_driver_learners("dmo", tmp_path, check)
