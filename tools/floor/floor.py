@@ -1,0 +1,81 @@
+"""Streaming floor of the SP_Oracle byte pattern (tools/floor/stream_floor.hip) next to
+ag_simulate on the same buffers: HIP events on the launch stream, isolated and back to back.
+Build: hipcc --offload-arch=gfx950 -O3 -shared -fPIC -o tools/floor/libfloor.so tools/floor/stream_floor.hip"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "auction-gym_amd"))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from auctiongym_amd import _lib  # noqa: E402
+from auctiongym_amd.engine import AuctionEngine  # noqa: E402
+
+
+class Ptrs(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("ctx", "part", "u", "winner", "item", "price", "bid", "est",
+                                              "tru", "bev", "outcome")]
+
+
+def main():
+    L = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libfloor.so"))
+    L.floor_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(Ptrs), ctypes.c_int64, ctypes.c_void_p]
+    B = 1 << 24
+    items, values = bench.catalogue()
+    eng = AuctionEngine(6, 2, 12, 5, 4, _lib.SECOND_PRICE, 1.0, device=0)
+    eng.load_catalog(items, values)
+    inp = eng.alloc_inputs(B)
+    eng.generate(0, 0, inp)
+    full = ("winner", "price", "outcome", "item", "bid", "est_ctr", "true_ctr", "best_ev")
+    out = eng.alloc_outputs(B, full)
+    cnt = eng.new_counters()
+    P = lambda t: t.data_ptr()  # noqa: E731
+    p = Ptrs(P(inp["ctx"]), P(inp["part"]), P(inp["u"]), P(out["winner"]), P(out["item"]), P(out["price"]),
+             P(out["bid"]), P(out["est_ctr"]), P(out["true_ctr"]), P(out["best_ev"]), P(out["outcome"]))
+    st = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    runs = {
+        "floor persistent 8 blocks/CU": lambda: L.floor_run(1, cus * 8, ctypes.byref(p), B, sp),
+        "floor persistent 4 blocks/CU": lambda: L.floor_run(1, cus * 4, ctypes.byref(p), B, sp),
+        "floor one tile per block": lambda: L.floor_run(0, 0, ctypes.byref(p), B, sp),
+        "ag_simulate (bench)": lambda: eng.simulate(inp, out, cnt),
+        "ag_simulate, no counters": lambda: eng.simulate(inp, out, None),
+        "torch copy+fill of the same bytes": None,
+    }
+    src = torch.empty(56 * B // 8, dtype=torch.float64, device="cuda")
+    dst = torch.empty(56 * B // 8, dtype=torch.float64, device="cuda")
+    fill = torch.empty(29 * B // 8, dtype=torch.float64, device="cuda")
+    runs["torch copy+fill of the same bytes"] = lambda: (dst.copy_(src), fill.fill_(1.0))
+    for _ in range(40):
+        for f in runs.values():
+            f()
+    torch.cuda.synchronize()
+    iso = {k: [] for k in runs}
+    sus = {k: [] for k in runs}
+    for r in range(12):
+        for k, f in runs.items():
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            f()
+            b.record(st)
+            torch.cuda.synchronize()
+            iso[k].append(a.elapsed_time(b))
+            a.record(st)
+            for _ in range(20):
+                f()
+            b.record(st)
+            torch.cuda.synchronize()
+            sus[k].append(a.elapsed_time(b) / 20)
+    for k in runs:
+        mi, ms = float(np.median(iso[k])), float(np.median(sus[k]))
+        print(f"{k:36s} isolated {mi:7.4f} ms ({141 * B / mi / 1e9:7.1f} GB/s)   back-to-back {ms:7.4f} ms "
+              f"({141 * B / ms / 1e9:7.1f} GB/s)")
+
+
+if __name__ == "__main__":
+    main()
