@@ -18,6 +18,8 @@ OPT_ITEM_SEARCH = 0
 OPT_LAUNCH_AUCTIONS = 2
 OPT_LRTS_BLOCK_SAMPLES = 3
 OPT_LANE_AUCTIONS = 1
+OPT_BIDDER_BLOCK_SAMPLES = 4
+OPT_FIT_NOISE_SEED = 5
 ITEM_SEARCH_AUTO, ITEM_SEARCH_EXACT = 0, 1
 
 COUNTERS = ("net", "gross", "allocation_regret", "estimation_regret", "overbid_regret",

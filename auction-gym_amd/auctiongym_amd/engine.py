@@ -171,6 +171,14 @@ class AuctionEngine:
         capacity); larger batches run as consecutive launches, same results."""
         self._check(self.L.ag_set_option(self._h, _lib.OPT_LAUNCH_AUCTIONS, int(n)), "ag_set_option")
 
+    def set_bidder_block_samples(self, n):
+        """Records per workgroup of the learning bidders' trainer (0: 8192)."""
+        self._check(self.L.ag_set_option(self._h, _lib.OPT_BIDDER_BLOCK_SAMPLES, int(n)), "ag_set_option")
+
+    def set_fit_noise_seed(self, seed):
+        """Seed of the synthetic rsample noise of bidder_update(noise=None)."""
+        self._check(self.L.ag_set_option(self._h, _lib.OPT_FIT_NOISE_SEED, int(seed)), "ag_set_option")
+
     def set_lrts_block_samples(self, n):
         """Samples per workgroup of the LR-TS training kernel (0: 4096); same results."""
         self._check(self.L.ag_set_option(self._h, _lib.OPT_LRTS_BLOCK_SAMPLES, int(n)), "ag_set_option")

@@ -23,11 +23,13 @@
 #include "ag_exp_table.h"
 #include "ag_host.h"
 #include "ag_log1p.h"
+#include "ag_philox.h"
 
 namespace {
 
 constexpr int kDrThreads = 256;
 constexpr int kWrEpochs = 32768, kInitEpochs = 16384, kDrEpochs = 32768;
+constexpr int64_t kBidderChunk = 8192;  // records per workgroup of k_bidder_train (default)
 constexpr double kGrid = 0x1p40, kInv = 0x1p-40;
 constexpr int64_t kLo24 = (int64_t(1) << 24) - 1;
 
@@ -170,7 +172,7 @@ struct DrRecords {
   const uint8_t *won;
 };
 
-// LDS of one agent's workgroup
+// LDS of one workgroup
 struct TrainLds {
   uint64_t tab[256];
   float wr[4], pol[12];
@@ -188,14 +190,62 @@ __device__ __forceinline__ void adam_reset(TrainLds &S) {
   __syncthreads();
 }
 
-// Fixed-order double sums (the policy-learning fits: importance weights are unbounded, so
-// their terms do not fit a fixed-point grid). Record i is added by thread i mod 256 in
-// record order; each wave combines by the butterfly v + shfl_xor(v, o), o = 32 .. 1 (the
-// same value on every lane); the wave totals are added to 0.0 in wave order. oracle/
-// ag_oracle_dr.c pl_lane_sums is this order exactly.
+// The workgroups training one agent: each owns a contiguous chunk of the agent's records and
+// exchanges its per-epoch partial sums through `part` ([2 parities][nblk][32] words) at an
+// agent barrier; afterwards every workgroup holds the same totals and runs the same Adam /
+// scheduler / early-stop step on its LDS copy of the parameters (the workgroups stay in
+// lockstep without a second barrier: an exchange's parity buffer is only rewritten two
+// exchanges later, after every workgroup has passed the barrier in between).
+struct Coop {
+  int rank, nblk;
+  int64_t *part;
+  unsigned *bar_count, *bar_gen;
+  int ph;  // exchanges so far (identical in every workgroup of the agent)
+};
+
+// Barrier of the workgroups of one agent (all co-resident: cooperative launch); agent-scope
+// release / acquire make the partials written before it visible on every XCD after it.
+__device__ __forceinline__ void agent_barrier(unsigned *count, unsigned *gen, int nblk) {
+  __syncthreads();
+  if (nblk > 1 && threadIdx.x == 0) {
+    const unsigned g = __hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (__hip_atomic_fetch_add(count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nblk - 1) {
+      __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      while (__hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+
+// exact totals of NV fixed-point sums over the agent's records (S.tot: hi, lo pairs)
 template <int NV>
-__device__ __forceinline__ void block_fsums(const double (&v)[NV], TrainLds &S) {
-  static_assert(NV <= 16, "block_fsums: at most 16 sums");
+__device__ __forceinline__ void exact_totals(const int64_t (&acc)[NV], TrainLds &S, Coop &C) {
+  block_sums<NV>(acc, S.w, S.tot);
+  if (C.nblk > 1) {
+    int64_t *pp = C.part + (size_t)(C.ph & 1) * C.nblk * 32;
+    if (threadIdx.x < 2 * NV) pp[C.rank * 32 + threadIdx.x] = S.tot[threadIdx.x];
+    agent_barrier(C.bar_count, C.bar_gen, C.nblk);
+    if (threadIdx.x < 2 * NV) {
+      int64_t t = 0;
+      for (int b = 0; b < C.nblk; ++b) t += pp[b * 32 + threadIdx.x];
+      S.tot[threadIdx.x] = t;
+    }
+    __syncthreads();
+    ++C.ph;
+  }
+}
+
+// Fixed-order double sums (the policy-learning fits: importance weights are unbounded, so
+// their terms do not fit a fixed-point grid). In each workgroup, record c0 + j is added by
+// thread j mod 256 in record order; each wave combines by the butterfly v + shfl_xor(v, o),
+// o = 32 .. 1 (the same value on every lane); the wave totals are added to 0.0 in wave
+// order; the workgroup totals are added to 0.0 in workgroup order. oracle/ag_oracle_dr.c
+// pl_epoch is this order exactly.
+template <int NV>
+__device__ __forceinline__ void float_totals(const double (&v)[NV], TrainLds &S, Coop &C) {
+  static_assert(NV <= 16, "float_totals: at most 16 sums");
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
@@ -204,10 +254,21 @@ __device__ __forceinline__ void block_fsums(const double (&v)[NV], TrainLds &S) 
     if (lane == 0) S.wf[wv][j] = x;
   }
   __syncthreads();
-  if (threadIdx.x < NV) {
-    double t = 0.0;
+  double t = 0.0;
+  if (threadIdx.x < NV)
     for (int w = 0; w < kDrThreads / 64; ++w) t += S.wf[w][threadIdx.x];
-    S.ftot[threadIdx.x] = t;
+  if (C.nblk > 1) {
+    double *pp = reinterpret_cast<double *>(C.part + (size_t)(C.ph & 1) * C.nblk * 32);
+    if (threadIdx.x < NV) pp[C.rank * 32 + threadIdx.x] = t;
+    agent_barrier(C.bar_count, C.bar_gen, C.nblk);
+    if (threadIdx.x < NV) {
+      double T = 0.0;
+      for (int b = 0; b < C.nblk; ++b) T += pp[b * 32 + threadIdx.x];
+      S.ftot[threadIdx.x] = T;
+    }
+    ++C.ph;
+  } else if (threadIdx.x < NV) {
+    S.ftot[threadIdx.x] = 0.0 + t;
   }
   __syncthreads();
 }
@@ -226,26 +287,57 @@ __device__ __forceinline__ void adam_step_block(TrainLds &S, float *par, int np,
   }
 }
 
+// The rsample noise of the DR / DM policy fits: the caller's draws (noise != NULL: agent's
+// record i of epoch e at noise[e * n + i]) or synthetic ones -- a standard normal by
+// Marsaglia's polar method on Philox4x32-10 (counter (i, e, attempt, agent), key = seed),
+// its log through the restated log1p, so the host (oracle/ag_oracle_dr.c ora_fit_noise)
+// draws the same bits.
+struct FitNoise {
+  const float *noise;  // agent's draws or NULL
+  int64_t n;           // agent's record count
+  uint64_t seed;
+  uint32_t agent;
+  int epochs;          // epochs available (synthetic: unlimited)
+};
+
+__device__ __forceinline__ double fit_eps(const FitNoise &F, int e, int64_t i) {
+  if (F.noise) return (double)F.noise[(int64_t)e * F.n + i];
+  for (uint32_t t = 0; t < 64; ++t) {
+    uint32_t w[4];
+    philox((uint32_t)i, (uint32_t)e, t, F.agent, (uint32_t)F.seed, (uint32_t)(F.seed >> 32), w);
+    const double u = (double)((((uint64_t)w[0] << 32) | w[1]) >> 11) * 0x1p-52 - 1.0;
+    const double v = (double)((((uint64_t)w[2] << 32) | w[3]) >> 11) * 0x1p-52 - 1.0;
+    const double s = u * u + v * v;
+    if (s > 0.0 && s < 1.0) return (double)(float)(u * __builtin_sqrt(-2.0 * aglog1p::log1p(s - 1.0) / s));
+  }
+  return 0.0;
+}
+
+// records of the workgroup: [c0, c0 + nb) of the agent's n
+struct Chunk {
+  int64_t c0, nb, n;
+};
+
 // PyTorchWinRateEstimator fit (src/Bidder.py:229-252 ValueLearningBidder, :500-530
 // DoublyRobustBidder): BCE (mean) over the logs plus the gamma = 0, y = 0 augmentation,
 // Adam(lr 3e-3, wd 1e-6, AMSGrad), ReduceLROnPlateau(patience, factor, min_lr 1e-7),
 // early stop after `wait` epochs without a 1e-6 improvement, <= 32768 epochs.
-__device__ int fit_winrate(const DrRecords &R, int64_t n, TrainLds &S, int patience, double factor, int wait,
-                           const double *adam_tab, float *tr) {
+__device__ int fit_winrate(const DrRecords &R, const Chunk &K, TrainLds &S, Coop &C, int patience, double factor,
+                           int wait, const double *adam_tab, float *tr) {
   const int tid = threadIdx.x;
   adam_reset(S);
   double lr = 3e-3;
   Plateau pl{INFINITY, 1e-4, factor, 1e-7, 0, patience};
   Stopper sp{INFINITY, -1, wait};
-  const double M = 2.0 * (double)n;
+  const double M = 2.0 * (double)K.n;
   int e = 0;
   for (; e < kWrEpochs; ++e) {
     int64_t acc[5] = {0, 0, 0, 0, 0};
-    for (int64_t r = tid; r < 2 * n; r += kDrThreads) {
-      const int64_t i = r < n ? r : r - n;
+    for (int64_t r = tid; r < 2 * K.nb; r += kDrThreads) {
+      const int64_t i = K.c0 + (r < K.nb ? r : r - K.nb);
       const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i];
-      const double g = r < n ? (double)(float)R.gamma[i] : 0.0;
-      const double y = r < n ? (double)R.won[i] : 0.0;
+      const double g = r < K.nb ? (double)(float)R.gamma[i] : 0.0;
+      const double y = r < K.nb ? (double)R.won[i] : 0.0;
       const double z = c * (double)S.wr[0] + v * (double)S.wr[1] + g * (double)S.wr[2] + (double)S.wr[3];
       const double pw = 1.0 / (1.0 + agexp::exp(-z, S.tab));
       const double t = y > 0.0 ? fmin(softplus(-z, S.tab), 100.0) : fmin(softplus(z, S.tab), 100.0);
@@ -256,7 +348,7 @@ __device__ int fit_winrate(const DrRecords &R, int64_t n, TrainLds &S, int patie
       acc[3] += fxr(gz * g);
       acc[4] += fxr(gz);
     }
-    block_sums<5>(acc, S.w, S.tot);
+    exact_totals<5>(acc, S, C);
     // every thread: the same loss; threads 0..3 step their parameter
     const float loss = (float)(fxv(S.tot[0], S.tot[1]) / M);
     const float g = tid < 4 ? (float)(fxv(S.tot[2 + 2 * tid], S.tot[3 + 2 * tid]) / M) : 0.0f;
@@ -273,16 +365,19 @@ __device__ int fit_winrate(const DrRecords &R, int64_t n, TrainLds &S, int patie
 // BidShadingContextualBandit.initialise_policy (src/Models.py:106-137): imitation of the
 // logging policy, MSE of mu to the logged gammas + MSE of softplus(sigma) (without
 // min_sigma) to 0.05; Adam(lr 1e-3, wd 1e-4, AMSGrad), early stop after 512 epochs.
-__device__ int fit_imitation(const DrRecords &R, int64_t n, TrainLds &S, const double *adam_tab, float *tr) {
+__device__ int fit_imitation(const DrRecords &R, const Chunk &K, TrainLds &S, Coop &C, const double *adam_tab,
+                             float *tr) {
   const int tid = threadIdx.x;
   adam_reset(S);
   Stopper sp{INFINITY, -1, 512};
+  const double n = (double)K.n;
   int e = 0;
   for (; e < kInitEpochs; ++e) {
     int64_t acc[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = 0;
-    for (int64_t i = tid; i < n; i += kDrThreads) {
+    for (int64_t j = tid; j < K.nb; j += kDrThreads) {
+      const int64_t i = K.c0 + j;
       const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i];
       PolF f;
       policy_fwd(S.pol, c, v, f, S.tab);
@@ -291,9 +386,9 @@ __device__ int fit_imitation(const DrRecords &R, int64_t n, TrainLds &S, const d
       acc[13] += fxr(dsg * dsg);
       policy_bwd(S.pol, c, v, f, 2.0 * dm, 2.0 * dsg, acc, 0, S.tab);
     }
-    block_sums<16>(acc, S.w, S.tot);
-    const float loss = (float)(fxv(S.tot[24], S.tot[25]) / (double)n + fxv(S.tot[26], S.tot[27]) / (double)n);
-    const float g = tid < 12 ? (float)(fxv(S.tot[2 * tid], S.tot[2 * tid + 1]) / (double)n) : 0.0f;
+    exact_totals<16>(acc, S, C);
+    const float loss = (float)(fxv(S.tot[24], S.tot[25]) / n + fxv(S.tot[26], S.tot[27]) / n);
+    const float g = tid < 12 ? (float)(fxv(S.tot[2 * tid], S.tot[2 * tid + 1]) / n) : 0.0f;
     adam_step_block(S, S.pol, 12, g, e, 1e-3, (float)1e-4, adam_tab);
     if (tid == 0 && tr) tr[e] = loss;
     const bool stop = stop_step(sp, e, loss);
@@ -307,21 +402,22 @@ __device__ int fit_imitation(const DrRecords &R, int64_t n, TrainLds &S, const d
 // -mean((u - u^) clip(pi / pi0, 1/50, 50) + W(ctr, value, g~) (V - V g~)), g~ = clip(mu +
 // sigma eps, 0, 1); Adam(lr 7e-3, wd 1e-4, AMSGrad), ReduceLROnPlateau(patience 100, factor
 // 0.2, min_lr 1e-8, threshold 5e-3), early stop after 512 epochs, <= 32768 epochs.
-__device__ int fit_dr(const DrRecords &R, const double *eu, int64_t n, TrainLds &S, const float *nz,
-                      int noise_epochs, const double *adam_tab, float *tr) {
+__device__ int fit_dr(const DrRecords &R, const double *eu, const Chunk &K, TrainLds &S, Coop &C,
+                      const FitNoise &F, const double *adam_tab, float *tr) {
   const int tid = threadIdx.x;
   adam_reset(S);
   double lr = 7e-3;
   Plateau pl{INFINITY, 5e-3, 0.2, 1e-8, 0, 100};
   Stopper sp{INFINITY, -1, 512};
   const double inv_sqrt2pi = 1.0 / __builtin_sqrt(2.0 * 3.141592653589793);
+  const double n = (double)K.n;
   int e = 0;
-  for (; e < kDrEpochs && e < noise_epochs; ++e) {
-    const float *eps = nz + (int64_t)e * n;
+  for (; e < kDrEpochs && e < F.epochs; ++e) {
     int64_t acc[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = 0;
-    for (int64_t i = tid; i < n; i += kDrThreads) {
+    for (int64_t j = tid; j < K.nb; j += kDrThreads) {
+      const int64_t i = K.c0 + j;
       const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i], g = (double)(float)R.gamma[i];
       PolF f;
       policy_fwd(S.pol, c, v, f, S.tab);
@@ -333,7 +429,7 @@ __device__ int fit_dr(const DrRecords &R, const double *eu, int64_t n, TrainLds 
       const double iw = pi / p0;
       const double iwc = iw < 1.0 / 50.0 ? 1.0 / 50.0 : (iw > 50.0 ? 50.0 : iw);
       const double du = (double)(float)R.util[i] - (double)(float)eu[i];
-      const double ep = (double)eps[i];
+      const double ep = fit_eps(F, e, i);
       const double raw = mu + sg * ep;
       const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
       const double zw = c * (double)S.wr[0] + v * (double)S.wr[1] + gs * (double)S.wr[2] + (double)S.wr[3];
@@ -350,9 +446,9 @@ __device__ int fit_dr(const DrRecords &R, const double *eu, int64_t n, TrainLds 
       if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)S.wr[2];
       policy_bwd(S.pol, c, v, f, -(dpi_dmu + ddm), -(dpi_dsg + ddm * ep), acc, 0, S.tab);
     }
-    block_sums<16>(acc, S.w, S.tot);
-    const float loss = (float)(fxv(S.tot[24], S.tot[25]) / (double)n);
-    const float g = tid < 12 ? (float)(fxv(S.tot[2 * tid], S.tot[2 * tid + 1]) / (double)n) : 0.0f;
+    exact_totals<16>(acc, S, C);
+    const float loss = (float)(fxv(S.tot[24], S.tot[25]) / n);
+    const float g = tid < 12 ? (float)(fxv(S.tot[2 * tid], S.tot[2 * tid + 1]) / n) : 0.0f;
     adam_step_block(S, S.pol, 12, g, e, lr, (float)1e-4, adam_tab);
     if (tid == 0 && tr) tr[e] = loss;
     plateau_step(pl, loss, lr);
@@ -369,24 +465,25 @@ __device__ int fit_dr(const DrRecords &R, const double *eu, int64_t n, TrainLds 
 // -mean(W(ctr, value, g~) (V - V g~)), g~ = clip(mu + sigma eps, 0, 1); Adam(lr 2e-3, wd
 // 1e-6, AMSGrad), ReduceLROnPlateau(patience 100, factor 0.1, min_lr 1e-7), early stop after
 // 256 epochs, <= 16384 epochs. Exact fixed-point sums (bounded terms).
-__device__ int fit_dm(const DrRecords &R, int64_t n, TrainLds &S, const float *nz, int noise_epochs,
+__device__ int fit_dm(const DrRecords &R, const Chunk &K, TrainLds &S, Coop &C, const FitNoise &F,
                       const double *adam_tab, float *tr) {
   const int tid = threadIdx.x;
   adam_reset(S);
   double lr = 2e-3;
   Plateau pl{INFINITY, 1e-4, 0.1, 1e-7, 0, 100};
   Stopper sp{INFINITY, -1, 256};
+  const double n = (double)K.n;
   int e = 0;
-  for (; e < kInitEpochs && e < noise_epochs; ++e) {
-    const float *eps = nz + (int64_t)e * n;
+  for (; e < kInitEpochs && e < F.epochs; ++e) {
     int64_t acc[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = 0;
-    for (int64_t i = tid; i < n; i += kDrThreads) {
+    for (int64_t j = tid; j < K.nb; j += kDrThreads) {
+      const int64_t i = K.c0 + j;
       const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i];
       PolF f;
       policy_fwd(S.pol, c, v, f, S.tab);
-      const double ep = (double)eps[i];
+      const double ep = fit_eps(F, e, i);
       const double raw = f.mu + f.sigma * ep;
       const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
       const double zw = c * (double)S.wr[0] + v * (double)S.wr[1] + gs * (double)S.wr[2] + (double)S.wr[3];
@@ -397,9 +494,9 @@ __device__ int fit_dm(const DrRecords &R, int64_t n, TrainLds &S, const float *n
       if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)S.wr[2];
       policy_bwd(S.pol, c, v, f, -ddm, -(ddm * ep), acc, 0, S.tab);
     }
-    block_sums<16>(acc, S.w, S.tot);
-    const float loss = (float)(fxv(S.tot[24], S.tot[25]) / (double)n);
-    const float g = tid < 12 ? (float)(fxv(S.tot[2 * tid], S.tot[2 * tid + 1]) / (double)n) : 0.0f;
+    exact_totals<16>(acc, S, C);
+    const float loss = (float)(fxv(S.tot[24], S.tot[25]) / n);
+    const float g = tid < 12 ? (float)(fxv(S.tot[2 * tid], S.tot[2 * tid + 1]) / n) : 0.0f;
     adam_step_block(S, S.pol, 12, g, e, lr, (float)1e-6, adam_tab);
     if (tid == 0 && tr) tr[e] = loss;
     plateau_step(pl, loss, lr);
@@ -437,19 +534,22 @@ __device__ __forceinline__ void policy_grad(const float *p, double c, double v, 
 // 174-199; AG_PL_LOSS_* kinds): Adam(lr 2e-3, wd 1e-4, AMSGrad), ReduceLROnPlateau
 // (patience 100, factor 0.2, min_lr 1e-8), early stop after 512 epochs, <= 16384 epochs.
 // oracle/ag_oracle_dr.c pl_epoch, term for term, with the same fixed-order sums.
-__device__ int fit_pl(const DrRecords &R, int64_t n, TrainLds &S, int kind, const double *adam_tab, float *tr) {
+__device__ int fit_pl(const DrRecords &R, const Chunk &K, TrainLds &S, Coop &C, int kind, const double *adam_tab,
+                      float *tr) {
   const int tid = threadIdx.x;
   adam_reset(S);
   double lr = 2e-3;
   Plateau pl{INFINITY, 1e-4, 0.2, 1e-8, 0, 100};
   Stopper sp{INFINITY, -1, 512};
   const double inv_sqrt2pi = 1.0 / __builtin_sqrt(2.0 * 3.141592653589793);
+  const double n = (double)K.n;
   int e = 0;
   for (; e < kInitEpochs; ++e) {
     double acc[14];
 #pragma unroll
     for (int j = 0; j < 14; ++j) acc[j] = 0.0;
-    for (int64_t i = tid; i < n; i += kDrThreads) {
+    for (int64_t j = tid; j < K.nb; j += kDrThreads) {
+      const int64_t i = K.c0 + j;
       const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i], g = (double)(float)R.gamma[i];
       PolF f;
       policy_fwd(S.pol, c, v, f, S.tab);
@@ -485,16 +585,16 @@ __device__ int fit_pl(const DrRecords &R, int64_t n, TrainLds &S, int kind, cons
       }
       double gr[14];
 #pragma unroll
-      for (int j = 0; j < 14; ++j) gr[j] = 0.0;
+      for (int q = 0; q < 14; ++q) gr[q] = 0.0;
       policy_grad(S.pol, c, v, f, dmu, dsg, gr, S.tab);
 #pragma unroll
-      for (int j = 0; j < 12; ++j) acc[j] += gr[j];
+      for (int q = 0; q < 12; ++q) acc[q] += gr[q];
       acc[12] += term;
       acc[13] += kl;
     }
-    block_fsums<14>(acc, S);
-    const float loss = (float)(S.ftot[12] / (double)n + (S.ftot[13] / (double)n) * 5e-2);
-    const float g = tid < 12 ? (float)(S.ftot[tid] / (double)n) : 0.0f;
+    float_totals<14>(acc, S, C);
+    const float loss = (float)(S.ftot[12] / n + (S.ftot[13] / n) * 5e-2);
+    const float g = tid < 12 ? (float)(S.ftot[tid] / n) : 0.0f;
     adam_step_block(S, S.pol, 12, g, e, lr, (float)1e-4, adam_tab);
     if (tid == 0 && tr) tr[e] = loss;
     plateau_step(pl, loss, lr);
@@ -506,27 +606,32 @@ __device__ int fit_pl(const DrRecords &R, int64_t n, TrainLds &S, int kind, cons
   return e;
 }
 
-// One workgroup per learning bidder (ValueLearning, PolicyLearning, DoublyRobust), the
-// fits of its update() in the reference's order. status: 0 trained, 1 ValueLearningBidder
-// fallback (no wins: nothing trained), -1 no logs, -2 NaN loss; epochs [3] = (win-rate,
-// imitation, policy fit); traces [3][32768].
+// The workgroups of the learning bidders (ValueLearning, PolicyLearning, DoublyRobust): block
+// b trains agent blk_agent[b] as workgroup blk_rank[b] of agent_nblk[agent] over the agent's
+// records, running its fits in the reference's order. status: 0 trained, 1
+// ValueLearningBidder fallback (no wins: nothing trained), -1 no logs, -2 NaN loss, -3 out
+// of noise epochs (state not written); epochs [3] = (win-rate, imitation, policy fit);
+// traces [3][32768] (workgroup 0).
 __global__ __launch_bounds__(kDrThreads) void k_bidder_train(
-    const int32_t *__restrict__ bkind, const int32_t *__restrict__ bmode, const int32_t *__restrict__ mask,
-    const int64_t *__restrict__ offsets,
-    DrRecords R0, double *__restrict__ eu_ws, float *__restrict__ state, const int32_t *__restrict__ initialised,
-    const float *__restrict__ noise, const int64_t *__restrict__ noise_off, int noise_epochs,
-    const double *__restrict__ adam_tab, int32_t *__restrict__ epochs_out, int32_t *__restrict__ status,
-    float *__restrict__ traces) {
-  const int a = blockIdx.x, tid = threadIdx.x;
+    const int32_t *__restrict__ bkind, const int32_t *__restrict__ bmode, const int32_t *__restrict__ blk_agent,
+    const int32_t *__restrict__ blk_rank, const int32_t *__restrict__ agent_nblk,
+    const int64_t *__restrict__ offsets, DrRecords R0, double *__restrict__ eu_ws, float *__restrict__ state,
+    const int32_t *__restrict__ initialised, const float *__restrict__ noise, const int64_t *__restrict__ noise_off,
+    int noise_epochs, uint64_t noise_seed, const double *__restrict__ adam_tab, int32_t *__restrict__ epochs_out,
+    int32_t *__restrict__ status, float *__restrict__ traces, int64_t *__restrict__ partials,
+    unsigned *__restrict__ barriers) {
+  const int a = blk_agent[blockIdx.x], rank = blk_rank[blockIdx.x], nblk = agent_nblk[a];
+  const int tid = threadIdx.x;
   const int bk = bkind[a];
-  const bool learner = (bk == AG_BIDDER_VALUE_LEARNING || bk == AG_BIDDER_POLICY_LEARNING ||
-                        bk == AG_BIDDER_DOUBLY_ROBUST) && (!mask || mask[a]);
   const int64_t s0 = offsets[a], n = offsets[a + 1] - s0;
-  if (tid == 0) epochs_out[3 * a] = epochs_out[3 * a + 1] = epochs_out[3 * a + 2] = 0;
-  if (!learner || n == 0) {
+  const bool lead = rank == 0;
+  if (n == 0) {
     // no logs: a ValueLearningBidder falls back (its won mask sums to 0, src/Bidder.py:206-
     // 211); the other learners fail in the reference
-    if (tid == 0) status[a] = !learner ? 0 : (bk == AG_BIDDER_VALUE_LEARNING ? 1 : -1);
+    if (lead && tid == 0) {
+      epochs_out[3 * a] = epochs_out[3 * a + 1] = epochs_out[3 * a + 2] = 0;
+      status[a] = bk == AG_BIDDER_VALUE_LEARNING ? 1 : -1;
+    }
     return;
   }
   __shared__ TrainLds S;
@@ -537,14 +642,22 @@ __global__ __launch_bounds__(kDrThreads) void k_bidder_train(
   if (tid == 0) S.stop = S.exhausted = 0;
   __syncthreads();
   DrRecords R{R0.ctr + s0, R0.value + s0, R0.gamma + s0, R0.prop + s0, R0.util + s0, R0.won + s0};
-  float *tr = traces ? traces + (size_t)a * 3 * kDrEpochs : nullptr;
+  const int64_t per = (n + nblk - 1) / nblk;
+  const int64_t c0 = (int64_t)rank * per < n ? (int64_t)rank * per : n;
+  const Chunk K{c0, (c0 + per < n ? c0 + per : n) - c0, n};
+  // the agent's exchange region [2][nblk][32] (its workgroups have consecutive block indices)
+  Coop C{rank, nblk, partials + (size_t)(blockIdx.x - rank) * 2 * 32, barriers + 2 * a, barriers + 2 * a + 1, 0};
+  const FitNoise F{noise ? noise + noise_off[a] : nullptr, n, noise_seed, (uint32_t)a,
+                   noise ? noise_epochs : 1 << 30};
+  float *tr = (traces && lead) ? traces + (size_t)a * 3 * kDrEpochs : nullptr;
   int ep[3] = {0, 0, 0};
   int stat = 0;
   if (bk == AG_BIDDER_DOUBLY_ROBUST) {
-    ep[0] = fit_winrate(R, n, S, 256, 0.2, 1024, adam_tab, tr);
-    // estimated utilities with the fitted model (src/Bidder.py:541-546)
+    ep[0] = fit_winrate(R, K, S, C, 256, 0.2, 1024, adam_tab, tr);
+    // estimated utilities of this workgroup's records with the fitted model (src/Bidder.py:541-546)
     double *eu = eu_ws + s0;
-    for (int64_t i = tid; i < n; i += kDrThreads) {
+    for (int64_t j = tid; j < K.nb; j += kDrThreads) {
+      const int64_t i = K.c0 + j;
       const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i], g = (double)(float)R.gamma[i];
       const double z = c * (double)S.wr[0] + v * (double)S.wr[1] + g * (double)S.wr[2] + (double)S.wr[3];
       const float W = (float)(1.0 / (1.0 + agexp::exp(-z, S.tab)));
@@ -552,27 +665,27 @@ __global__ __launch_bounds__(kDrThreads) void k_bidder_train(
       eu[i] = (double)W * (V - P);
     }
     __syncthreads();
-    if (!initialised[a]) ep[1] = fit_imitation(R, n, S, adam_tab, tr ? tr + kDrEpochs : nullptr);
-    ep[2] = fit_dr(R, eu, n, S, noise + noise_off[a], noise_epochs, adam_tab, tr ? tr + 2 * kDrEpochs : nullptr);
+    if (!initialised[a]) ep[1] = fit_imitation(R, K, S, C, adam_tab, tr ? tr + kDrEpochs : nullptr);
+    ep[2] = fit_dr(R, eu, K, S, C, F, adam_tab, tr ? tr + 2 * kDrEpochs : nullptr);
     stat = S.stop ? -2 : 0;
   } else if (bk == AG_BIDDER_VALUE_LEARNING) {
     int64_t acc[1] = {0};
-    for (int64_t i = tid; i < n; i += kDrThreads) acc[0] += R.won[i] ? 1 : 0;
-    block_sums<1>(acc, S.w, S.tot);
+    for (int64_t j = tid; j < K.nb; j += kDrThreads) acc[0] += R.won[K.c0 + j] ? 1 : 0;
+    exact_totals<1>(acc, S, C);
     if (S.tot[0] == 0 && S.tot[1] == 0) {
       stat = 1;  // src/Bidder.py:206-211: revert to Gaussian shading, nothing trained
     } else {
-      ep[0] = fit_winrate(R, n, S, 100, 0.1, 512, adam_tab, tr);
-      if (bmode[a] == AG_VL_POLICY)
-        ep[2] = fit_dm(R, n, S, noise + noise_off[a], noise_epochs, adam_tab, tr ? tr + 2 * kDrEpochs : nullptr);
+      ep[0] = fit_winrate(R, K, S, C, 100, 0.1, 512, adam_tab, tr);
+      if (bmode[a] == AG_VL_POLICY) ep[2] = fit_dm(R, K, S, C, F, adam_tab, tr ? tr + 2 * kDrEpochs : nullptr);
     }
   } else {  // PolicyLearningBidder
-    if (!initialised[a]) ep[1] = fit_imitation(R, n, S, adam_tab, tr ? tr + kDrEpochs : nullptr);
-    ep[2] = fit_pl(R, n, S, bmode[a], adam_tab, tr ? tr + 2 * kDrEpochs : nullptr);
+    if (!initialised[a]) ep[1] = fit_imitation(R, K, S, C, adam_tab, tr ? tr + kDrEpochs : nullptr);
+    ep[2] = fit_pl(R, K, S, C, bmode[a], adam_tab, tr ? tr + 2 * kDrEpochs : nullptr);
     stat = S.stop ? -2 : 0;
   }
   __syncthreads();
   if (S.exhausted) stat = -3;  // not applied: the caller supplies more noise epochs
+  if (!lead) return;
   if (tid == 0) {
     epochs_out[3 * a] = ep[0];
     epochs_out[3 * a + 1] = ep[1];
@@ -639,6 +752,7 @@ void ag_dr_release(ag_ctx *c) {
   (void)hipFree(w.init);
   (void)hipFree(w.mode);
   (void)hipFree(w.scratch);
+  (void)hipFree(w.coop);
   w = ag_dr_ws();
 }
 
@@ -739,8 +853,7 @@ int ag_shading_counts(ag_ctx *c, const ag_shading_samples *s, int64_t *counts, v
 int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agents, const float *noise,
                      const int64_t *noise_offsets, int32_t noise_epochs, int32_t *epochs, int32_t *status,
                      float *traces, void *stream) {
-  if (!c || !s || !noise_offsets || (!noise && noise_epochs > 0))
-    return ag_set_error(AG_ERR_INVALID, "ag_bidder_update: null argument");
+  if (!c || !s || !noise_offsets) return ag_set_error(AG_ERR_INVALID, "ag_bidder_update: null argument");
   if (!s->ctr || !s->value || !s->propensity || !s->won || !s->order)
     return ag_set_error(AG_ERR_INVALID, "ag_bidder_update: the store needs ctr, value, propensity, won, order");
   if (!c->dr_loaded) return ag_set_error(AG_ERR_STATE, "ag_bidder_update: ag_set_dr_state not called");
@@ -792,15 +905,82 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agen
     AG_HIP(hipGetLastError());
   }
   int64_t *d_noff = w.scratch;                       // [N] noise offsets
-  int32_t *d_epochs = (int32_t *)(w.scratch + N);     // [N][3] epochs, then [N] status, [N] mask
+  int32_t *d_epochs = (int32_t *)(w.scratch + N);     // [N][3] epochs, then [N] status
   int32_t *d_stat = d_epochs + 3 * (size_t)N;
-  int32_t *d_mask = agents ? d_stat + N : nullptr;
   AG_HIP(hipMemcpyAsync(d_noff, noise_offsets, sizeof(int64_t) * N, hipMemcpyHostToDevice, st));
-  if (agents) AG_HIP(hipMemcpyAsync(d_mask, agents, sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
-  DrRecords R{b_ctr, b_val, b_gam, b_prop, b_util, b_won};
-  hipLaunchKernelGGL(k_bidder_train, dim3(N), dim3(kDrThreads), 0, st, c->d_bkind, w.mode, d_mask, d_off, R, b_eu, w.state,
-                     w.init, noise, d_noff, noise_epochs, w.adam_tab, d_epochs, d_stat, traces);
-  AG_HIP(hipGetLastError());
+  AG_HIP(hipMemsetAsync(d_epochs, 0, sizeof(int32_t) * 4 * N, st));
+  // workgroups per learning bidder: one per `chunk` records, co-resident (cooperative
+  // launch) when an agent has several; capped to the resident grid
+  if (!w.coop_blocks) {
+    int per_cu = 0, cus = 0;
+    AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_bidder_train, kDrThreads, 0));
+    AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    w.coop_blocks = per_cu * cus > 0 ? per_cu * cus : 1;
+  }
+  const int64_t chunk = c->bidder_chunk > 0 ? c->bidder_chunk : kBidderChunk;
+  std::vector<int32_t> nblk(N, 0), blk_agent, blk_rank;
+  int64_t want = 0;
+  for (int a = 0; a < N; ++a) {
+    const int bk = c->h_bkind[a];
+    const bool learner = bk == AG_BIDDER_VALUE_LEARNING || bk == AG_BIDDER_POLICY_LEARNING ||
+                         bk == AG_BIDDER_DOUBLY_ROBUST;
+    if (!learner || (agents && !agents[a])) continue;
+    nblk[a] = cnt[a] > 0 ? (int32_t)((cnt[a] + chunk - 1) / chunk) : 1;
+    want += nblk[a];
+  }
+  if (want > w.coop_blocks) {  // share the resident grid out
+    const double f = (double)w.coop_blocks / (double)want;
+    for (int a = 0; a < N; ++a)
+      if (nblk[a] > 1) nblk[a] = (int32_t)(nblk[a] * f) > 1 ? (int32_t)(nblk[a] * f) : 1;
+  }
+  bool multi = false;
+  for (int a = 0; a < N; ++a) {
+    multi |= nblk[a] > 1;
+    for (int r = 0; r < nblk[a]; ++r) {
+      blk_agent.push_back(a);
+      blk_rank.push_back(r);
+    }
+  }
+  const int G = (int)blk_agent.size();
+  if (multi && G > w.coop_blocks)
+    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_bidder_update: %d learning bidders need more co-resident "
+                        "workgroups (%d) than the device holds (%d)", N, G, w.coop_blocks);
+  if (G > 0) {
+    // tables: blk_agent [G], blk_rank [G], agent_nblk [N] i32; barriers [N][2] u32;
+    // exchange partials [G][2][32] i64
+    const size_t tbytes = sizeof(int32_t) * (2 * (size_t)G + N) + sizeof(unsigned) * 2 * N;
+    const size_t pbytes = sizeof(int64_t) * 64 * (size_t)G;
+    if (tbytes + pbytes + 64 > w.coop_bytes) {
+      (void)hipFree(w.coop);
+      w.coop = nullptr;
+      w.coop_bytes = 0;
+      AG_HIP(hipMalloc(&w.coop, tbytes + pbytes + 64));
+      w.coop_bytes = tbytes + pbytes + 64;
+    }
+    int64_t *d_part = (int64_t *)w.coop;
+    int32_t *d_bagent = (int32_t *)(d_part + 64 * (size_t)G);
+    int32_t *d_brank = d_bagent + G;
+    int32_t *d_nblk = d_brank + G;
+    unsigned *d_bar = (unsigned *)(d_nblk + N);
+    AG_HIP(hipMemcpyAsync(d_bagent, blk_agent.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
+    AG_HIP(hipMemcpyAsync(d_brank, blk_rank.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
+    AG_HIP(hipMemcpyAsync(d_nblk, nblk.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
+    AG_HIP(hipMemsetAsync(d_bar, 0, sizeof(unsigned) * 2 * N, st));
+    DrRecords R{b_ctr, b_val, b_gam, b_prop, b_util, b_won};
+    const int32_t *cbk = c->d_bkind, *cmode = w.mode, *cinit = w.init;
+    const int64_t *coff = d_off, *cnoff = d_noff;
+    double *ceu = b_eu;
+    float *cstate = w.state, *ctr = traces;
+    int cne = noise_epochs;
+    uint64_t cseed = c->fit_noise_seed;
+    const double *ctab = w.adam_tab;
+    void *args[] = {&cbk, &cmode, &d_bagent, &d_brank, &d_nblk, &coff, &R, &ceu, &cstate, &cinit, &noise, &cnoff,
+                    &cne, &cseed, &ctab, &d_epochs, &d_stat, &ctr, &d_part, &d_bar};
+    if (multi)  // workgroups of one agent wait for each other: they must all be resident
+      AG_HIP(hipLaunchCooperativeKernel((const void *)k_bidder_train, dim3(G), dim3(kDrThreads), args, 0, st));
+    else
+      AG_HIP(hipLaunchKernel((const void *)k_bidder_train, dim3(G), dim3(kDrThreads), args, 0, st));
+  }
   std::vector<int32_t> h(4 * (size_t)N);
   AG_HIP(hipMemcpyAsync(h.data(), d_epochs, sizeof(int32_t) * 4 * N, hipMemcpyDeviceToHost, st));
   AG_HIP(hipStreamSynchronize(st));

@@ -42,6 +42,9 @@ struct ag_dr_ws {
   int32_t *init = nullptr;      // [N] AG_LEARNER_*: what the agent bids from
   int32_t *mode = nullptr;      // [N] ValueLearningBidder inference / PolicyLearningBidder loss
   int64_t *scratch = nullptr;   // [N] noise offsets + [N][4] epochs / status
+  void *coop = nullptr;         // trainer workgroup tables, barriers, exchange partials
+  size_t coop_bytes = 0;
+  int coop_blocks = 0;          // co-resident workgroups of k_bidder_train
 };
 
 struct ag_ctx {
@@ -66,6 +69,8 @@ struct ag_ctx {
   int32_t *h_bkind = nullptr;  // host copy of the bidder kinds [N]
   bool dr_loaded = false, dr_any_init = false;  // learner models loaded; some bid from a policy
   bool vl_any_search = false;                    // some ValueLearningBidder bids by search
+  int64_t bidder_chunk = 0;                      // AG_OPT_BIDDER_BLOCK_SAMPLES (0: default)
+  uint64_t fit_noise_seed = 0;                   // AG_OPT_FIT_NOISE_SEED
   ag_dr_ws dr;
   int32_t *d_akind = nullptr, *d_bkind = nullptr;
   double *d_pg = nullptr, *d_gs = nullptr;

@@ -26,6 +26,7 @@
 #include <string>
 
 #include "ag_host.h"
+#include "ag_philox.h"
 #include "ag_sim.h"
 
 // ------------------------------------------------------------------------------------
@@ -165,28 +166,6 @@ __global__ __launch_bounds__(kThreads) void k_allocate_wave(const double *__rest
 // ------------------------------------------------------------------------------------
 // synthetic batch generator (Philox4x32-10; oracle/ag_oracle.c restates the integer part)
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                       uint32_t k0, uint32_t k1, uint32_t (&o)[4]) {
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
-    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-    const uint32_t n1 = (uint32_t)p1;
-    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
-    const uint32_t n3 = (uint32_t)p0;
-    c0 = n0;
-    c1 = n1;
-    c2 = n2;
-    c3 = n3;
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
-  }
-  o[0] = c0;
-  o[1] = c1;
-  o[2] = c2;
-  o[3] = c3;
-}
 
 __global__ __launch_bounds__(kThreads) void k_generate(uint64_t seed, uint64_t first, int64_t B, int N, int P,
                                                       int E, double scale, double *ctx, int32_t *part,
@@ -533,6 +512,13 @@ int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
     case AG_OPT_LRTS_BLOCK_SAMPLES:
       if (value < 0) return ag_set_error(AG_ERR_INVALID, "ag_set_option: block samples must be >= 0");
       c->lrts_chunk = value;
+      return AG_OK;
+    case AG_OPT_BIDDER_BLOCK_SAMPLES:
+      if (value < 0) return ag_set_error(AG_ERR_INVALID, "ag_set_option: block samples must be >= 0");
+      c->bidder_chunk = value;
+      return AG_OK;
+    case AG_OPT_FIT_NOISE_SEED:
+      c->fit_noise_seed = (uint64_t)value;
       return AG_OK;
     default:
       return ag_set_error(AG_ERR_INVALID, "ag_set_option: unknown option %d", option);

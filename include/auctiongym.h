@@ -188,9 +188,14 @@ typedef enum ag_option {
   AG_OPT_LAUNCH_AUCTIONS = 2, /* value: cap on auctions per k_simulate launch (0 = the exact-
                                  counter capacity of the resident grid); larger batches run
                                  as consecutive launches with identical results */
-  AG_OPT_LRTS_BLOCK_SAMPLES = 3 /* value: samples per workgroup of the LR-TS training kernel
+  AG_OPT_LRTS_BLOCK_SAMPLES = 3, /* value: samples per workgroup of the LR-TS training kernel
                                    (0 = 16 per lane = 4096); fewer spreads an agent over more
                                    workgroups -- identical results (exact sums) */
+  AG_OPT_BIDDER_BLOCK_SAMPLES = 4, /* value: records per workgroup of the learning bidders'
+                                   trainer (0 = 8192); identical results for the exact-sum fits,
+                                   the policy-learning fits' fixed-order sums follow the split */
+  AG_OPT_FIT_NOISE_SEED = 5       /* value: seed of the synthetic rsample noise of ag_bidder_update
+                                   called with noise == NULL (default 0) */
 } ag_option;
 
 typedef enum ag_item_search {

@@ -414,6 +414,33 @@ int32_t ora_dr_update(int64_t n, const double *ctr, const double *value, const d
   return 0;
 }
 
+/* Philox4x32-10 (ag_oracle.c) */
+void ora_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
+/* Synthetic rsample noise of the DR / DM fits (ag_bidder_update with noise == NULL): record
+ * i of epoch e of agent a ~ N(0, 1) by Marsaglia's polar method on Philox4x32-10 (counter (i,
+ * e, attempt, a), key = seed), log through the restated log1p, rounded to float32. */
+void ora_fit_noise(uint64_t seed, uint32_t agent, int32_t epochs, int64_t n, float *out) {
+  const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  for (int32_t e = 0; e < epochs; ++e)
+    for (int64_t i = 0; i < n; ++i) {
+      float z = 0.0f;
+      for (uint32_t t = 0; t < 64; ++t) {
+        const uint32_t ctr[4] = {(uint32_t)i, (uint32_t)e, t, agent};
+        uint32_t w[4];
+        ora_philox4x32_10(ctr, key, w);
+        const double u = (double)((((uint64_t)w[0] << 32) | w[1]) >> 11) * 0x1p-52 - 1.0;
+        const double v = (double)((((uint64_t)w[2] << 32) | w[3]) >> 11) * 0x1p-52 - 1.0;
+        const double s = u * u + v * v;
+        if (s > 0.0 && s < 1.0) {
+          z = (float)(u * sqrt(-2.0 * fl_log1p(s - 1.0) / s));
+          break;
+        }
+      }
+      out[(int64_t)e * n + i] = z;
+    }
+}
+
 /* ValueLearningBidder 'search' bid (src/Bidder.py:180-196): x = float32 [ctr, value, g] for
  * the 128 grid gammas, W = sigmoid(((c w0 + v w1) + g w2) + b) in float32 (no FMAs; the
  * sigmoid through libm exp in double, rounded once), utility W (ev - ev g) in double with ev
@@ -579,54 +606,62 @@ static void policy_grad(const float *p, double c, double v, const polf_t *f, dou
  * [3] = (0, imitation, policy). */
 /* one epoch of a policy-learning loss: the float32 loss and gradient (mean over the n
  * records) at pol */
-static float pl_epoch(int64_t n, const float *cf, const float *vf, const float *gf, const double *prop,
-                      const double *util, const float *pol, int32_t loss_kind, double (*acc)[PL_NV],
-                      float *grad) {
+static float pl_epoch(int64_t n, int32_t nblk, const float *cf, const float *vf, const float *gf,
+                      const double *prop, const double *util, const float *pol, int32_t loss_kind,
+                      double (*acc)[PL_NV], float *grad) {
   const double inv_sqrt2pi = 1.0 / sqrt(2.0 * 3.141592653589793);
-  memset(acc, 0, sizeof(double[PL_LANES][PL_NV]));
-  for (int64_t i = 0; i < n; ++i) {
-    polf_t f;
-    const double c = cf[i], v = vf[i], g = (double)gf[i];
-    policy_fwd(pol, c, v, &f);
-    const double mu = f.mu, sg = f.sigma;
-    const double zz = (mu - g) / sg;
-    const double pdf_raw = exp(-(zz * zz) / 2.0) / sg * inv_sqrt2pi;
-    const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
-    const double p0 = (double)fmaxf((float)prop[i], 1e-15f);
-    const double u = (double)(float)util[i];
-    double term = 0.0, kl = 0.0, dpi = 0.0, dmu = 0.0, dsg = 0.0;
-    if (loss_kind == 0) {
-      term = -(pi * u);
-      dpi = -u;
-    } else if (loss_kind == 1 || loss_kind == 2) {
-      term = -((pi / p0) * u);
-      dpi = -u / p0;
-      if (loss_kind == 2) {
-        kl = (sg * sg + (mu - g) * (mu - g)) / (2.0 * sg * sg) - 0.5;
-        dmu = 5e-2 * ((mu - g) / (sg * sg));
-        dsg = 5e-2 * (-((mu - g) * (mu - g)) / (sg * sg * sg));
-      }
-    } else {
-      const double iw = pi / p0;
-      const int in_range = iw >= 1.0 / 50.0 && iw <= 50.0;
-      const double iwc = iw < 1.0 / 50.0 ? 1.0 / 50.0 : (iw > 50.0 ? 50.0 : iw);
-      const double A = iw * u, Bc = iwc * u;
-      term = -(A < Bc ? A : Bc);
-      dpi = (in_range || A < Bc) ? -u / p0 : 0.0;
-    }
-    if (pdf_raw >= 1e-30 && dpi != 0.0) {
-      dmu += dpi * pdf_raw * (g - mu) / (sg * sg);
-      dsg += dpi * pdf_raw * ((g - mu) * (g - mu) / (sg * sg * sg) - 1.0 / sg);
-    }
-    double gr[12];
-    policy_grad(pol, c, v, &f, dmu, dsg, gr);
-    double *a = acc[i % PL_LANES];
-    for (int j = 0; j < 12; ++j) a[j] += gr[j];
-    a[12] += term;
-    a[13] += kl;
-  }
+  const int64_t per = (n + nblk - 1) / nblk;
   double tot[PL_NV];
-  pl_lane_sums(acc, tot);
+  for (int j = 0; j < PL_NV; ++j) tot[j] = 0.0;
+  for (int32_t b = 0; b < nblk; ++b) { /* the device's workgroups, in order */
+    const int64_t c0 = (int64_t)b * per < n ? (int64_t)b * per : n;
+    const int64_t c1 = c0 + per < n ? c0 + per : n;
+    memset(acc, 0, sizeof(double[PL_LANES][PL_NV]));
+    for (int64_t i = c0; i < c1; ++i) {
+      polf_t f;
+      const double c = cf[i], v = vf[i], g = (double)gf[i];
+      policy_fwd(pol, c, v, &f);
+      const double mu = f.mu, sg = f.sigma;
+      const double zz = (mu - g) / sg;
+      const double pdf_raw = exp(-(zz * zz) / 2.0) / sg * inv_sqrt2pi;
+      const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
+      const double p0 = (double)fmaxf((float)prop[i], 1e-15f);
+      const double u = (double)(float)util[i];
+      double term = 0.0, kl = 0.0, dpi = 0.0, dmu = 0.0, dsg = 0.0;
+      if (loss_kind == 0) {
+        term = -(pi * u);
+        dpi = -u;
+      } else if (loss_kind == 1 || loss_kind == 2) {
+        term = -((pi / p0) * u);
+        dpi = -u / p0;
+        if (loss_kind == 2) {
+          kl = (sg * sg + (mu - g) * (mu - g)) / (2.0 * sg * sg) - 0.5;
+          dmu = 5e-2 * ((mu - g) / (sg * sg));
+          dsg = 5e-2 * (-((mu - g) * (mu - g)) / (sg * sg * sg));
+        }
+      } else {
+        const double iw = pi / p0;
+        const int in_range = iw >= 1.0 / 50.0 && iw <= 50.0;
+        const double iwc = iw < 1.0 / 50.0 ? 1.0 / 50.0 : (iw > 50.0 ? 50.0 : iw);
+        const double A = iw * u, Bc = iwc * u;
+        term = -(A < Bc ? A : Bc);
+        dpi = (in_range || A < Bc) ? -u / p0 : 0.0;
+      }
+      if (pdf_raw >= 1e-30 && dpi != 0.0) {
+        dmu += dpi * pdf_raw * (g - mu) / (sg * sg);
+        dsg += dpi * pdf_raw * ((g - mu) * (g - mu) / (sg * sg * sg) - 1.0 / sg);
+      }
+      double gr[12];
+      policy_grad(pol, c, v, &f, dmu, dsg, gr);
+      double *a = acc[(i - c0) % PL_LANES];
+      for (int j = 0; j < 12; ++j) a[j] += gr[j];
+      a[12] += term;
+      a[13] += kl;
+    }
+    double bt[PL_NV];
+    pl_lane_sums(acc, bt);
+    for (int j = 0; j < PL_NV; ++j) tot[j] += bt[j];
+  }
   for (int j = 0; j < 12; ++j) grad[j] = (float)(tot[j] / (double)n);
   return (float)(tot[12] / (double)n + (tot[13] / (double)n) * 5e-2);
 }
@@ -642,7 +677,7 @@ float ora_pl_loss_grad(int64_t n, const double *ctr, const double *value, const 
                        float *grad) {
   float *cf = to_f32(n, ctr), *vf = to_f32(n, value), *gf = to_f32(n, gamma);
   double (*acc)[PL_NV] = malloc(sizeof(double[PL_LANES][PL_NV]));
-  const float loss = pl_epoch(n, cf, vf, gf, prop, util, pol, loss_kind, acc, grad);
+  const float loss = pl_epoch(n, 1, cf, vf, gf, prop, util, pol, loss_kind, acc, grad);
   free(acc);
   free(cf);
   free(vf);
@@ -652,7 +687,7 @@ float ora_pl_loss_grad(int64_t n, const double *ctr, const double *value, const 
 
 int32_t ora_pl_update(int64_t n, const double *ctr, const double *value, const double *gamma,
                       const double *prop, const double *util, float *pol, int32_t initialised,
-                      int32_t loss_kind, int32_t *epochs, float *init_trace, float *pl_trace) {
+                      int32_t loss_kind, int32_t nblk, int32_t *epochs, float *init_trace, float *pl_trace) {
   epochs[0] = epochs[1] = epochs[2] = 0;
   if (n < 1) return -1;
   float *cf = to_f32(n, ctr), *vf = to_f32(n, value), *gf = to_f32(n, gamma);
@@ -666,7 +701,7 @@ int32_t ora_pl_update(int64_t n, const double *ctr, const double *value, const d
   int32_t e = 0, rc = 0;
   for (; e < 16384; ++e) {
     float grad[12];
-    const float loss = pl_epoch(n, cf, vf, gf, prop, util, pol, loss_kind, acc, grad);
+    const float loss = pl_epoch(n, nblk < 1 ? 1 : nblk, cf, vf, gf, prop, util, pol, loss_kind, acc, grad);
     adam_step(&ad, pol, grad);
     if (pl_trace) pl_trace[e] = loss;
     plateau_step(&pl, loss, &ad.lr);

@@ -92,7 +92,9 @@ def lib():
         L.ora_vl_update.restype = i32
         L.ora_vl_update.argtypes = [i64] + [vp] * 6 + [i32, vp, i64] + [vp] * 3
         L.ora_pl_update.restype = i32
-        L.ora_pl_update.argtypes = [i64] + [vp] * 6 + [i32, i32] + [vp] * 3
+        L.ora_pl_update.argtypes = [i64] + [vp] * 6 + [i32, i32, i32] + [vp] * 3
+        L.ora_fit_noise.restype = None
+        L.ora_fit_noise.argtypes = [u64, ctypes.c_uint32, i32, i64, vp]
         L.ora_pl_loss_grad.restype = ctypes.c_float
         L.ora_pl_loss_grad.argtypes = [i64] + [vp] * 6 + [i32, vp]
         L.ora_search_gamma.restype = d
@@ -324,15 +326,17 @@ def vl_update(ctr, value, gamma, won, wr, pol, policy, noise, trace=True):
             "wr_losses": tr[0][:ep[0]].astype(np.float64), "pol_losses": tr[1][:ep[2]].astype(np.float64)}
 
 
-def pl_update(ctr, value, gamma, prop, util, pol, initialised, loss="PPO", trace=True):
-    """PolicyLearningBidder.update (src/Bidder.py:364-431) of one agent. Returns dict(pol,
-    epochs, init_losses, pl_losses, nan)."""
+def pl_update(ctr, value, gamma, prop, util, pol, initialised, loss="PPO", trace=True, nblk=1):
+    """PolicyLearningBidder.update (src/Bidder.py:364-431) of one agent, its policy-fit sums in
+    the order of `nblk` device workgroups. Returns dict(pol, epochs, init_losses, pl_losses,
+    nan)."""
     n = len(ctr)
     a = [np.ascontiguousarray(v, np.float64) for v in (ctr, value, gamma, prop, util)]
     pol = np.array(pol, np.float32).ravel().copy()
     ep = np.zeros(3, np.int32)
     tr = [np.zeros(16384, np.float32), np.zeros(16384, np.float32)]
-    rc = lib().ora_pl_update(n, *[_p(v) for v in a], _p(pol), int(bool(initialised)), PL_LOSSES[loss], _p(ep),
+    rc = lib().ora_pl_update(n, *[_p(v) for v in a], _p(pol), int(bool(initialised)), PL_LOSSES[loss], int(nblk),
+                             _p(ep),
                              *[(_p(t) if trace else None) for t in tr])
     if rc == -1:
         raise ValueError("PolicyLearningBidder.update without logs")
@@ -355,3 +359,10 @@ def search_gamma(wr, ctr, value, grid):
     wr = np.ascontiguousarray(wr, np.float32)
     grid = np.ascontiguousarray(grid, np.float64)
     return float(lib().ora_search_gamma(_p(wr), float(ctr), float(value), _p(grid), 1))
+
+
+def fit_noise(seed, agent, epochs, n):
+    """The synthetic rsample noise of ag_bidder_update(noise=NULL): float32 [epochs][n]."""
+    out = np.zeros((epochs, n), np.float32)
+    lib().ora_fit_noise(int(seed), int(agent), int(epochs), int(n), _p(out))
+    return out

@@ -1205,3 +1205,134 @@ def test_driver_fp_dm_oracle(gpu, tmp_path):
             assert b.model_initialised == bool(k[f"it{it}_a{i}_init"])
             np.testing.assert_allclose(b._state16()[:4], k[f"it{it}_a{i}_winrate_model"], atol=5e-2)
     _run_driver_learners("dmo", tmp_path, check)
+
+
+def _learner_store(eng, recs):
+    import torch
+    n_tot = sum(len(v) for v in recs["agent"])
+    st = eng.new_shading_samples(n_tot, learning=True)
+    perm = np.random.default_rng(9).permutation(n_tot)
+    dt = {"agent": np.int32, "won": np.uint8, "order": np.int64}
+    for f, parts in recs.items():
+        v = np.concatenate(parts).astype(dt.get(f, np.float64))[perm]
+        st[f][:n_tot] = torch.from_numpy(v).to(eng.device)
+    st["count"][0] = n_tot
+    return st
+
+
+def _kat_learners(specs):
+    """specs: [(kind, kat file, kat agent)] -> engine inputs: bidder kinds, modes, state0 [N][16],
+    records {field: [per agent]}, per-agent data dicts."""
+    from auctiongym_amd import _lib
+    N = len(specs)
+    bk = np.array([{"dm": 2, "ips": 3, "dr": 4}[s[0]] for s in specs], np.int32)
+    modes = np.array([_lib.VL_POLICY if s[0] == "dm" else (_lib.PL_LOSSES["PPO"] if s[0] == "ips" else 0)
+                      for s in specs], np.int32)
+    state0 = np.zeros((N, 16), np.float32)
+    recs = {f: [] for f in ("agent", "gamma", "utility", "ctr", "value", "propensity", "won", "order")}
+    data = []
+    for a, (kind, fname, j) in enumerate(specs):
+        kat = np.load(os.path.join(GOLDEN, fname))
+        k = lambda s, kat=kat, j=j: kat[f"a{j}_{s}"]  # noqa: E731
+        n = len(k("est_ctr"))
+        if kind == "ips":
+            state0[a, 4:] = np.concatenate([k(f"pol0_{i}").ravel() for i in range(6)])
+        else:
+            state0[a, :4] = np.concatenate([k("wr0_0").ravel(), k("wr0_1").ravel()])
+            idx = (0, 1, 4, 5, 8, 9) if kind == "dm" else range(6)
+            state0[a, 4:] = np.concatenate([k(f"pol0_{i}").ravel() for i in idx])
+        for f, v in (("agent", np.full(n, a)), ("gamma", k("gamma")), ("utility", k("util")),
+                     ("ctr", k("est_ctr")), ("value", k("value")), ("propensity", k("propensity")),
+                     ("won", k("won")), ("order", N * np.arange(n) + a)):
+            recs[f].append(v)
+        data.append(k)
+    return bk, modes, state0, recs, data
+
+
+def test_bidder_update_multi_workgroup(gpu, oracle):
+    """The learning bidders' trainer with every agent split over several cooperating
+    workgroups (200 records each): DM and DR fits (exact sums) give the single-workgroup
+    oracle's results bit for bit; the PPO fit's fixed-order sums follow the split, equal to
+    the oracle run with the same number of workgroups."""
+    import torch
+    from auctiongym_amd.engine import AuctionEngine
+    specs = [("dm", "dm_update_kat.npz", 2), ("ips", "ips_update_kat.npz", 0), ("ips", "ips_update_kat.npz", 1),
+             ("dr", "dr_update_kat.npz", 0)]
+    bk, modes, state0, recs, data = _kat_learners(specs)
+    N = len(specs)
+    eng = AuctionEngine(N, 2, 12, 5, 4, 0, 1.0)
+    eng.set_agent_params(np.ones(N, np.int32), bk, np.ones(N), np.full(N, 0.02))
+    eng.set_dr_state(state0, np.zeros(N, np.int32))
+    eng.set_bidder_modes(modes)
+    eng.set_bidder_block_samples(200)
+    E = 10300
+    noises, offs, off, orc = [], [], 0, []
+    for a, (kind, _, _) in enumerate(specs):
+        k = data[a]
+        n = len(k("est_ctr"))
+        nblk = (n + 199) // 200
+        if kind == "dm":
+            z = _dr_noise(k("fit1_rng"), n, E)
+            orc.append(oracle.vl_update(k("est_ctr"), k("value"), k("gamma"), k("won"), state0[a, :4], state0[a, 4:],
+                                        True, z[:3800]))
+        elif kind == "dr":
+            z = _dr_noise(k("dr_rng_state"), n, E)
+            orc.append(oracle.dr_update(k("est_ctr"), k("value"), k("gamma"), k("propensity"), k("won"), k("util"),
+                                        state0[a, :4], state0[a, 4:], False, z))
+        else:
+            z = np.zeros((0, n), np.float32)
+            orc.append(oracle.pl_update(k("est_ctr"), k("value"), k("gamma"), k("propensity"), k("util"),
+                                        state0[a, 4:], False, "PPO", nblk=nblk))
+        noises.append(z.ravel())
+        offs.append(off)
+        off += z.size
+    st = _learner_store(eng, recs)
+    noise = torch.from_numpy(np.concatenate(noises)).to(eng.device)
+    ep, stat, tr = eng.bidder_update(st, noise, offs, E, trace=True)
+    state, ini = eng.dr_state()
+    tr = tr.cpu().numpy()
+    assert list(stat) == [0] * N and list(ini) == [1] * N
+    for a, (kind, _, _) in enumerate(specs):
+        r = orc[a]
+        assert list(ep[a]) == list(r["epochs"]), (a, ep[a], r["epochs"])
+        for slot, key in ((0, "wr_losses"), (1, "init_losses"), (2, {"dm": "pol_losses", "dr": "dr_losses",
+                                                                    "ips": "pl_losses"}[kind])):
+            if key in r:
+                assert np.array_equal(tr[a, slot, :ep[a, slot]], r[key].astype(np.float32)), (a, key)
+        assert np.array_equal(state[a, 4:], r["pol"]), a
+        if kind != "ips":
+            assert np.array_equal(state[a, :4], r["wr"]), a
+    eng.close()
+
+
+def test_bidder_update_synthetic_noise(gpu, oracle):
+    """ag_bidder_update without caller noise: the DR and DM fits draw their rsample noise on
+    the device (Philox4x32-10 + polar method, keyed by the fit-noise seed); equal bit for bit
+    to the oracle fed ora_fit_noise's draws of the same seed."""
+    from auctiongym_amd.engine import AuctionEngine
+    specs = [("dm", "dm_update_kat.npz", 1), ("dr", "dr_update_kat.npz", 1)]
+    bk, modes, state0, recs, data = _kat_learners(specs)
+    N = len(specs)
+    eng = AuctionEngine(N, 2, 12, 5, 4, 0, 1.0)
+    eng.set_agent_params(np.ones(N, np.int32), bk, np.ones(N), np.full(N, 0.02))
+    eng.set_dr_state(state0, np.zeros(N, np.int32))
+    eng.set_bidder_modes(modes)
+    eng.set_fit_noise_seed(77)
+    st = _learner_store(eng, recs)
+    ep, stat, tr = eng.bidder_update(st, None, np.zeros(N, np.int64), 0, trace=True)
+    state, _ = eng.dr_state()
+    tr = tr.cpu().numpy()
+    assert list(stat) == [0, 0]
+    k0, k1 = data
+    n0, n1 = len(k0("est_ctr")), len(k1("est_ctr"))
+    r0 = oracle.vl_update(k0("est_ctr"), k0("value"), k0("gamma"), k0("won"), state0[0, :4], state0[0, 4:], True,
+                          oracle.fit_noise(77, 0, int(ep[0, 2]) + 1, n0))
+    r1 = oracle.dr_update(k1("est_ctr"), k1("value"), k1("gamma"), k1("propensity"), k1("won"), k1("util"),
+                          state0[1, :4], state0[1, 4:], False, oracle.fit_noise(77, 1, int(ep[1, 2]) + 1, n1))
+    assert list(ep[0]) == list(r0["epochs"]) and list(ep[1]) == list(r1["epochs"])
+    assert np.array_equal(tr[0, 2, :ep[0, 2]], r0["pol_losses"].astype(np.float32))
+    assert np.array_equal(tr[1, 2, :ep[1, 2]], r1["dr_losses"].astype(np.float32))
+    assert np.array_equal(state[0, 4:], r0["pol"]) and np.array_equal(state[1, 4:], r1["pol"])
+    z = oracle.fit_noise(77, 0, 3, n0)
+    assert abs(z.mean()) < 0.05 and abs(z.std() - 1) < 0.05
+    eng.close()
