@@ -69,9 +69,10 @@ def catalogue(cfg=None):
     return np.stack([a2i[n] for n in names]), np.stack([a2v[n] for n in names])
 
 
-def cpu_baseline(items, values, inp, sample, threads):
+def cpu_baseline(items, values, inp, sample, threads, min_seconds=10.0, max_passes=40):
     """Time the oracle (C restatement of the reference path) on `sample` auctions of the
-    same inputs; also check its outputs equal the GPU's on that sample."""
+    same inputs, repeated until at least `min_seconds` of CPU work; also check its outputs
+    equal the GPU's on that sample. Returns (auctions/s, seconds, passes, outputs)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     O.build()
@@ -81,8 +82,12 @@ def cpu_baseline(items, values, inp, sample, threads):
     O.simulate(1, items, values, ctx[:1000], part[:1000], u[:1000], nthreads=threads)  # warm
     t0 = time.perf_counter()
     o = O.simulate(1, items, values, ctx, part, u, nthreads=threads)
+    passes = 1
+    while time.perf_counter() - t0 < min_seconds and passes < max_passes:
+        O.simulate(1, items, values, ctx, part, u, nthreads=threads)
+        passes += 1
     dt = time.perf_counter() - t0
-    return sample / dt, dt, o
+    return sample * passes / dt, dt, passes, o
 
 
 SP_TS = dict(SP_ORACLE, agents=[{"name": "Truthful TS", "num_copies": 8, "num_items": 12,
@@ -205,6 +210,158 @@ def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True):
     return res
 
 
+def _agents_cfg(groups, base):
+    """A config dict whose agents are `groups`: [(name, copies, allocator type, bidder type,
+    bidder kwargs)] (the reference config schema)."""
+    ag = []
+    for name, copies, alloc, bidder, kw in groups:
+        akw = {"embedding_size": 4, "num_items": 12} if alloc == "PyTorchLogisticRegressionAllocator" else {}
+        ag.append({"name": name, "num_copies": copies, "num_items": 12,
+                   "allocator": {"type": alloc, "kwargs": akw}, "bidder": {"type": bidder, "kwargs": kw}})
+    return dict(base, agents=ag)
+
+
+LRTS, ORACLE_A = "PyTorchLogisticRegressionAllocator", "OracleAllocator"
+POPULATIONS = {
+    # BASELINE.json configs[2..4] (SURVEY §8d)
+    "configs_2": ("FP_DM_TS (configs[2]): 3 LR-TS allocators + ValueLearningBidder('policy'), FirstPrice",
+                  [("DM (policy)", 3, LRTS, "ValueLearningBidder",
+                    {"gamma_sigma": 0.02, "init_gamma": 1.0, "inference": "policy"})], 1 << 20, "dm"),
+    "configs_3": ("FP_DR_TS (configs[3]): 3 LR-TS allocators + DoublyRobustBidder, FirstPrice; 4M auctions "
+                  "over 8 GPUs = 512k per GPU",
+                  [("DR", 3, LRTS, "DoublyRobustBidder", {"gamma_sigma": 0.02, "init_gamma": 1.0})], 1 << 19, "dr"),
+    "configs_4": ("Mixed population (configs[4]): 32 bidders = 11 Oracle+Truthful, 11 LR-TS+Truthful, "
+                  "10 LR-TS+DoublyRobust, FirstPrice; 16M auctions over 8 GPUs = 2M per GPU",
+                  [("Oracle", 11, ORACLE_A, "TruthfulBidder", {}), ("TS", 11, LRTS, "TruthfulBidder", {}),
+                   ("DR", 10, LRTS, "DoublyRobustBidder", {"gamma_sigma": 0.02, "init_gamma": 1.0})],
+                  1 << 21, "mixed"),
+}
+
+
+def algorithmic_bytes_population(E, P, K, Do, ak, bk, init):
+    """Expected bytes per auction of a general population with bids from fitted policies:
+    reads ctx, part, u and, per participant (uniform over agents), its Thompson noise (LR-TS),
+    its rsample draw (fitted policy) or shading draw (uninitialised shading); writes winner,
+    price, second price, outcome and per participant item, bid, est / true CTR, best EV,
+    gamma, propensity."""
+    per_slot = []
+    for a in range(len(ak)):
+        b = K * Do * 4 if ak[a] == 1 else 0
+        if bk[a] != 0:
+            b += 4 if init[a] == 1 else 8
+        per_slot.append(b)
+    reads = 8 * E + 4 * P + 8 + P * float(np.mean(per_slot))
+    writes = 4 + 8 + 8 + 1 + P * (4 + 8 * 6)
+    return reads + writes
+
+
+def run_population(key, steps, warmup, world, rank, local, batch=None, with_update=True):
+    """A BASELINE config population on the GPU at its per-GPU shard size: iteration 0 with
+    Gaussian shading (uninitialised learners), the update of every learner (LR-TS allocators
+    and learning bidders, on the GPU, synthetic rsample noise; records all-gathered when N > 1)
+    timed, then the timed steps with bids from the fitted policies. Inputs Philox-generated
+    and resident in HBM."""
+    from auctiongym_amd import _lib
+    from auctiongym_amd.engine import AuctionEngine
+    from auctiongym_amd.sharding import allreduce_counters, gather_records, shard_range
+    what, groups, B0, tag = POPULATIONS[key]
+    B = int(batch or B0)
+    cfg = _agents_cfg(groups, dict(SP_ORACLE, allocation="FirstPrice"))
+    items, values = catalogue(cfg)
+    N, K, D = items.shape
+    E, P, OE = D - 1, 2, 4
+    Do = OE + 1
+    ak, bk, modes = [], [], []
+    kinds = {"TruthfulBidder": 0, "ValueLearningBidder": 2, "DoublyRobustBidder": 4}
+    for _, copies, alloc, bidder, kw in groups:
+        for _ in range(copies):
+            ak.append(1 if alloc == LRTS else 0)
+            bk.append(kinds[bidder])
+            modes.append(_lib.VL_POLICY if kw.get("inference") == "policy" else 0)
+    ak, bk, modes = np.array(ak, np.int32), np.array(bk, np.int32), np.array(modes, np.int32)
+    dev = torch.device("cuda", local)
+    eng = AuctionEngine(N, P, K, E, OE, _lib.FIRST_PRICE, 1.0, device=local)
+    eng.set_agent_params(ak, bk, np.ones(N), np.full(N, 0.02))
+    eng.load_catalog(items, values)
+    g = torch.Generator().manual_seed(0)
+    m = torch.empty(N, K, Do)
+    for a in range(N):
+        m[a].normal_(0.0, 1.0, generator=g)
+    eng.load_lrts(m.numpy(), np.ones((N, K, Do), np.float32), thompson_sampling=True)
+    st16 = np.zeros((N, 16), np.float32)
+    torch.manual_seed(0)
+    for a in range(N):  # win-rate models and policies as the constructors draw them (torch.nn.Linear)
+        lins = [torch.nn.Linear(3, 1), torch.nn.Linear(2, 2), torch.nn.Linear(2, 1), torch.nn.Linear(2, 1)]
+        st16[a] = np.concatenate([p.detach().numpy().ravel() for lin in lins for p in lin.parameters()])
+    eng.set_dr_state(st16, np.zeros(N, np.int32))
+    eng.set_bidder_modes(modes)
+    lo, _ = shard_range(B * world, rank, world)
+    inp = eng.alloc_inputs(B)
+    eng.generate(0, lo, inp)
+    eng.generate_noise(0, lo, inp)
+    out = eng.alloc_outputs(B)
+    cnt = eng.new_counters()
+    res = {"workload": what, "auctions_per_gpu_per_step": B}
+    # iteration 0 (uninitialised learners) and the update of every learner
+    eng.simulate(inp, out, cnt)
+    torch.cuda.synchronize()
+    if with_update:
+        lst = eng.new_lrts_samples(B)
+        sst = eng.new_shading_samples(B * P, learning=True)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        eng.lrts_collect(inp, out, lst)
+        eng.shading_collect(inp, out, sst, first_auction=lo)
+        if world > 1:
+            lst, sst = gather_records(lst), gather_records(sst)
+        lep = eng.lrts_update(lst)
+        t1 = time.perf_counter()
+        ep, stat = eng.bidder_update(sst, None, np.zeros(N, np.int64), 0)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        ms = [(t1 - t0) * 1e3, (t2 - t1) * 1e3]
+        if world > 1:
+            t = torch.tensor(ms, dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ms = [float(x) for x in t]
+        learners = np.nonzero(bk >= 2)[0]
+        res["agent_update"] = {
+            "ms": ms[0] + ms[1], "lrts_ms": ms[0], "bidders_ms": ms[1],
+            "records_per_bidder": int(sst["count"][0]) // max(1, N),
+            "bidder_epochs": [[int(x) for x in ep[a]] for a in learners[:4]],
+            "what": "Agent.update of every learner: LR-TS allocators (ag_lrts_update) + learning bidders "
+                    "(ag_bidder_update: win-rate fit, imitation, policy fit; synthetic on-device rsample noise)"
+                    + (" on the all-gathered records" if world > 1 else "")}
+        _, init = eng.dr_state()
+    else:
+        init = np.where(bk >= 2, 1, 0).astype(np.int32)
+        eng.set_dr_state(st16, init)
+    inp = eng.alloc_inputs(B)  # the fitted policies' rsample draws now
+    eng.generate(1, lo, inp)
+    eng.generate_noise(1, lo, inp)
+    stream = torch.cuda.current_stream()
+
+    def step(ev):
+        cnt.zero_()
+        if ev is not None:
+            ev[0].record(stream)
+        eng.simulate(inp, out, cnt)
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:
+            allreduce_counters(cnt)
+
+    elapsed, kern_ms = timed_steps(step, steps, warmup, world, stream)
+    bpa = algorithmic_bytes_population(E, P, K, Do, ak, bk, init)
+    res.update({"value": B * world * steps / elapsed, "unit": "auctions/s", "ms_per_step": elapsed / steps * 1e3,
+                "kernel_ms": kern_ms, "algorithmic_bytes_per_auction": bpa,
+                "roofline": {"bound": "hbm", "achieved": bpa * B / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": bpa * B / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}})
+    eng.close()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -212,12 +369,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=60,
                     help="untimed steps first (lets the clocks settle under sustained load)")
     ap.add_argument("--batch", type=int, default=1 << 24, help="auctions per GPU per step")
-    ap.add_argument("--cpu-sample", type=int, default=1 << 23)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 24)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu_count)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ts-batch", type=int, default=1 << 20, help="SP_Truthful_TS auctions per GPU per step")
     ap.add_argument("--no-ts", action="store_true", help="skip the SP_Truthful_TS (configs[1]) line")
-    ap.add_argument("--no-update", action="store_true", help="skip timing the LR-TS Agent.update")
+    ap.add_argument("--no-update", action="store_true", help="skip timing the Agent.update of learners")
+    ap.add_argument("--no-populations", action="store_true",
+                    help="skip the configs[2..4] lines (FP_DM_TS, FP_DR_TS, mixed population)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -329,17 +488,23 @@ def main():
         result["configs_1"] = run_sp_ts(args.ts_batch, args.steps, args.warmup, world, rank, local,
                                         with_update=not args.no_update)
 
+    if not args.no_populations:
+        for key in POPULATIONS:
+            result[key] = run_population(key, max(5, args.steps // 5), max(5, args.warmup // 5), world, rank, local,
+                                         with_update=not args.no_update)
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         sample = min(args.cpu_sample, B)
-        cps, dt, o = cpu_baseline(items, values, inp, sample, threads)
+        cps, dt, passes, o = cpu_baseline(items, values, inp, sample, threads)
         gpu_bid = out["bid"][:, :sample].cpu().numpy().T
         same = bool(np.array_equal(gpu_bid, o["bid"]) and
                     np.array_equal(out["winner"][:sample].cpu().numpy(), o["winner"]))
         result["cpu_baseline"] = {
             "value": cps, "unit": "auctions/s", "cores": threads, "kind": "port",
-            "sample": f"{sample} auctions of the same synthetic batch, oracle/ag_oracle.c "
-                      f"(OpenMP, {threads} threads), {dt:.2f} s; outputs identical to GPU: {same}"}
+            "sample": f"{passes} passes over {sample} auctions of the same synthetic batch, "
+                      f"oracle/ag_oracle.c (OpenMP, {threads} threads), {dt:.1f} s; "
+                      f"outputs identical to GPU: {same}"}
     if rank == 0:
         print(json.dumps(result))
     if world > 1:
