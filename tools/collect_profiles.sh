@@ -9,8 +9,8 @@ TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-HEAD="python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-ts"
-TS="python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-update"
+HEAD="python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-ts --no-populations"
+TS="python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-update --no-populations"
 HK='k_simulate<2, 6, true, 1, false>'
 TK='k_simulate<2, 6, true, 1, true>'
 step() { local name=$1; shift; echo "== $name"; timeout -k 10 400 "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "rc=$rc"; if [ $rc -ge 124 ]; then exit $rc; fi; }
