@@ -23,7 +23,7 @@ run() {  # name, seconds, command...
 rocm-smi --showproductname > "$OUT/gpu.txt" 2>&1 || true
 nproc > "$OUT/host.txt"; lscpu | grep "Model name" >> "$OUT/host.txt"
 run smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
-run pytest_gpu 900 python -m pytest tests -q -m gpu -x
+run pytest_gpu 900 python -u -m pytest tests -v -m gpu -x --timeout 300 --timeout-method thread
 run bench 600 python bench.py
 run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline
 echo "== done" | tee -a "$OUT/session.log"
