@@ -20,6 +20,7 @@ OPT_LRTS_BLOCK_SAMPLES = 3
 OPT_LANE_AUCTIONS = 1
 OPT_BIDDER_BLOCK_SAMPLES = 4
 OPT_FIT_NOISE_SEED = 5
+OPT_BIDDER_RECORD_CACHE = 6
 ITEM_SEARCH_AUTO, ITEM_SEARCH_EXACT = 0, 1
 
 COUNTERS = ("net", "gross", "allocation_regret", "estimation_regret", "overbid_regret",
@@ -36,7 +37,7 @@ EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params
            "ag_shading_counts", "ag_dr_update", "ag_set_bidder_modes", "ag_bidder_update",
            "ag_generate_search_grid",
            "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_last_error", "ag_abi_version")
-ABI_VERSION = 13
+ABI_VERSION = 14
 LEARNER_UNINITIALISED, LEARNER_POLICY, LEARNER_SEARCH = 0, 1, 2
 VL_SEARCH, VL_POLICY = 0, 1
 PL_LOSSES = {"REINFORCE": 0, "REINFORCE_offpolicy": 1, "TRPO": 2, "PPO": 3}

@@ -172,8 +172,13 @@ class AuctionEngine:
         self._check(self.L.ag_set_option(self._h, _lib.OPT_LAUNCH_AUCTIONS, int(n)), "ag_set_option")
 
     def set_bidder_block_samples(self, n):
-        """Records per workgroup of the learning bidders' trainer (0: 8192)."""
+        """Records per workgroup of the learning bidders' trainer (0: the default split)."""
         self._check(self.L.ag_set_option(self._h, _lib.OPT_BIDDER_BLOCK_SAMPLES, int(n)), "ag_set_option")
+
+    def set_bidder_record_cache(self, n):
+        """Most records per workgroup the learning bidders' trainer keeps in LDS (-1: as many
+        as fit, 0: none); results are identical."""
+        self._check(self.L.ag_set_option(self._h, _lib.OPT_BIDDER_RECORD_CACHE, int(n)), "ag_set_option")
 
     def set_fit_noise_seed(self, seed):
         """Seed of the synthetic rsample noise of bidder_update(noise=None)."""

@@ -29,11 +29,22 @@ namespace {
 
 constexpr int kDrThreads = 256;
 constexpr int kWrEpochs = 32768, kInitEpochs = 16384, kDrEpochs = 32768;
-constexpr int64_t kBidderChunk = 8192;  // records per workgroup of k_bidder_train (default)
+constexpr int64_t kBidderChunk = 8192;  // records per workgroup of a PolicyLearningBidder (default)
+constexpr int64_t kMinChunk = 1024;     // fewest records per workgroup of an exact-sum learner's split
+constexpr size_t kRecLdsBytes0 = 32 * 1024;  // record cache per workgroup, win-rate phase (4 per CU)
+constexpr size_t kRecLdsBytes = 72 * 1024;   // record cache per workgroup, later fits (2 per CU)
 constexpr double kGrid = 0x1p40, kInv = 0x1p-40;
 constexpr int64_t kLo24 = (int64_t(1) << 24) - 1;
 
-__device__ __forceinline__ int64_t fxr(double v) { return (int64_t)__builtin_rint(v * kGrid); }
+// (int64)rint(v * 2^40). For |v * 2^40| < 2^51 (every term in practice) adding 1.5 * 2^52
+// rounds to the integer (nearest, ties to even, as rint) and leaves it in the low mantissa
+// bits: 1 add + 1 integer subtract instead of the long double -> int64 conversion.
+__device__ __forceinline__ int64_t fxr(double v) {
+  const double x = v * kGrid;
+  if (__builtin_expect(__builtin_fabs(x) < 0x1p51, 1))
+    return (int64_t)(agexp::asu64(x + 0x1.8p52) - agexp::asu64(0x1.8p52));
+  return (int64_t)__builtin_rint(x);
+}
 
 __device__ __forceinline__ double fxv(int64_t hi, int64_t lo) {
   hi += lo >> 24;
@@ -41,14 +52,10 @@ __device__ __forceinline__ double fxv(int64_t hi, int64_t lo) {
   return ((double)hi * 0x1p24 + (double)lo) * kInv;
 }
 
-__device__ __forceinline__ double softplus(double u, const uint64_t *tab) {
-  return u > 20.0 ? u : aglog1p::log1p(agexp::exp(u, tab));
-}
-__device__ __forceinline__ double dsoftplus(double u, const uint64_t *tab) {
-  if (u > 20.0) return 1.0;
-  const double e = agexp::exp(u, tab);
-  return e / (e + 1.0);
-}
+// softplus(u) = u > 20 ? u : log1p(exp(u)) and its derivative exp(u) / (exp(u) + 1), from
+// e = exp(u) (the forward pass keeps it for the backward pass)
+__device__ __forceinline__ double softplus_e(double u, double e) { return u > 20.0 ? u : aglog1p::log1p(e); }
+__device__ __forceinline__ double dsoftplus_e(double u, double e) { return u > 20.0 ? 1.0 : e / (e + 1.0); }
 
 // Exact block sum of NV per-lane int64 accumulators (each split at bit 24 so nothing can
 // overflow): every thread gets the totals as (hi, lo) pairs in s_out.
@@ -124,24 +131,29 @@ __device__ __forceinline__ bool stop_step(Stopper &s, int epoch, float loss) {
   return epoch - s.best_epoch > s.wait;
 }
 
+// forward values of the policy; eh / eam / eas = exp of h / am / as, kept for the backward
+// pass's softplus derivatives
 struct PolF {
-  double h[2], s[2], am, as, mu, sp_sigma, sigma;
+  double h[2], s[2], am, as, mu, sp_sigma, sigma, eh[2], eam, eas;
 };
 __device__ __forceinline__ void policy_fwd(const float *p, double c, double v, PolF &f, const uint64_t *tab) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     f.h[j] = c * (double)p[2 * j] + v * (double)p[2 * j + 1] + (double)p[4 + j];
-    f.s[j] = softplus(f.h[j], tab);
+    f.eh[j] = agexp::exp(f.h[j], tab);
+    f.s[j] = softplus_e(f.h[j], f.eh[j]);
   }
   f.am = f.s[0] * (double)p[6] + f.s[1] * (double)p[7] + (double)p[8];
   f.as = f.s[0] * (double)p[9] + f.s[1] * (double)p[10] + (double)p[11];
-  f.mu = softplus(f.am, tab);
-  f.sp_sigma = softplus(f.as, tab);
+  f.eam = agexp::exp(f.am, tab);
+  f.eas = agexp::exp(f.as, tab);
+  f.mu = softplus_e(f.am, f.eam);
+  f.sp_sigma = softplus_e(f.as, f.eas);
   f.sigma = f.sp_sigma + 0.01;  // min_sigma (src/Models.py:104)
 }
 __device__ __forceinline__ void policy_bwd(const float *p, double c, double v, const PolF &f, double dmu,
                                            double dsigma, int64_t (&G)[16], int off, const uint64_t *tab) {
-  const double dam = dmu * dsoftplus(f.am, tab), das = dsigma * dsoftplus(f.as, tab);
+  const double dam = dmu * dsoftplus_e(f.am, f.eam), das = dsigma * dsoftplus_e(f.as, f.eas);
   double ds[2];
   ds[0] = dam * (double)p[6] + das * (double)p[9];
   ds[1] = dam * (double)p[7] + das * (double)p[10];
@@ -153,7 +165,7 @@ __device__ __forceinline__ void policy_bwd(const float *p, double c, double v, c
   G[off + 11] += fxr(das);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const double dh = ds[j] * dsoftplus(f.h[j], tab);
+    const double dh = ds[j] * dsoftplus_e(f.h[j], f.eh[j]);
     G[off + 2 * j] += fxr(dh * c);
     G[off + 2 * j + 1] += fxr(dh * v);
     G[off + 4 + j] += fxr(dh);
@@ -199,21 +211,65 @@ __device__ __forceinline__ void adam_reset(TrainLds &S) {
 struct Coop {
   int rank, nblk;
   int64_t *part;
-  unsigned *bar_count, *bar_gen;
-  int ph;  // exchanges so far (identical in every workgroup of the agent)
+  unsigned *bar;  // the agent's barrier lines (bar_lines)
+  int ph;         // exchanges so far (identical in every workgroup of the agent)
 };
 
-// Barrier of the workgroups of one agent (all co-resident: cooperative launch); agent-scope
-// release / acquire make the partials written before it visible on every XCD after it.
-__device__ __forceinline__ void agent_barrier(unsigned *count, unsigned *gen, int nblk) {
+// Agent barrier: a combining tree of arrival counters (fan-in kBarFanIn; the last arriver at
+// a node goes up a level) and a generation word the root's last arriver bumps, every word on
+// its own 128-B line -- same-address atomics serialise at the memory side, so one counter for
+// hundreds of workgroups (plus their polling of a word on the same line) cost ~0.3 us per
+// workgroup. Lines: [0] generation, then level 0's ceil(nblk / F) nodes, level 1's, ...
+#ifndef AG_BAR_SLEEP
+#define AG_BAR_SLEEP 2  // s_sleep units (64 cycles) between polls of the generation word
+#endif
+#ifndef AG_BAR_FANIN
+#define AG_BAR_FANIN 16
+#endif
+constexpr int kBarFanIn = AG_BAR_FANIN, kBarLineWords = 32;
+__host__ __device__ inline int bar_lines(int nblk) {
+  if (nblk <= 1) return 0;
+  int lines = 1;
+  for (int m = nblk; m > 1; m = (m + kBarFanIn - 1) / kBarFanIn) lines += (m + kBarFanIn - 1) / kBarFanIn;
+  return lines;
+}
+
+// Barrier of the workgroups of one agent (all co-resident: cooperative launch). Arrivals are
+// release read-modify-writes and the waiting is relaxed polling followed by ONE acquire fence:
+// on gfx950 an agent-scope acquire invalidates the XCD's L2 and a release writes it back, so
+// acquire polling (an invalidation per poll, from hundreds of workgroups) stalls every XCD.
+// The partials written before the barrier are visible on every XCD after it: every arrival
+// RMW extends the release sequences of the earlier ones, each level's last arriver takes an
+// acquire fence before it arrives one level up, and the root's release of the generation
+// word is acquired by every waiter's fence.
+__device__ __forceinline__ void agent_barrier(unsigned *bar, int rank, int nblk) {
   __syncthreads();
   if (nblk > 1 && threadIdx.x == 0) {
-    const unsigned g = __hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    if (__hip_atomic_fetch_add(count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nblk - 1) {
-      __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned *gen = bar;
+    const unsigned g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int idx = rank, members_prev = nblk, base = 1;
+    bool last = true;
+    for (;;) {
+      const int nodes = (members_prev + kBarFanIn - 1) / kBarFanIn, q = idx / kBarFanIn;
+      const int members = members_prev - q * kBarFanIn < kBarFanIn ? members_prev - q * kBarFanIn : kBarFanIn;
+      unsigned *cnt = bar + (size_t)(base + q) * kBarLineWords;
+      if (__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) != (unsigned)members - 1) {
+        last = false;
+        break;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (nodes == 1) break;
+      base += nodes;
+      idx = q;
+      members_prev = nodes;
+    }
+    if (last) {
       __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      while (__hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) __builtin_amdgcn_s_sleep(2);
+      while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g)
+        __builtin_amdgcn_s_sleep(AG_BAR_SLEEP);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
   }
   __syncthreads();
@@ -226,11 +282,15 @@ __device__ __forceinline__ void exact_totals(const int64_t (&acc)[NV], TrainLds 
   if (C.nblk > 1) {
     int64_t *pp = C.part + (size_t)(C.ph & 1) * C.nblk * 32;
     if (threadIdx.x < 2 * NV) pp[C.rank * 32 + threadIdx.x] = S.tot[threadIdx.x];
-    agent_barrier(C.bar_count, C.bar_gen, C.nblk);
-    if (threadIdx.x < 2 * NV) {
+    agent_barrier(C.bar, C.rank, C.nblk);
+    // wave w adds words j = w, w + 4, ...: lane l the workgroups l, l + 64, ..., then a
+    // butterfly (integer sums: any order gives the same totals)
+    const int lane = threadIdx.x & 63;
+    for (int j = threadIdx.x >> 6; j < 2 * NV; j += kDrThreads / 64) {
       int64_t t = 0;
-      for (int b = 0; b < C.nblk; ++b) t += pp[b * 32 + threadIdx.x];
-      S.tot[threadIdx.x] = t;
+      for (int b = lane; b < C.nblk; b += 64) t += pp[b * 32 + j];
+      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+      if (lane == 0) S.tot[j] = t;
     }
     __syncthreads();
     ++C.ph;
@@ -260,7 +320,7 @@ __device__ __forceinline__ void float_totals(const double (&v)[NV], TrainLds &S,
   if (C.nblk > 1) {
     double *pp = reinterpret_cast<double *>(C.part + (size_t)(C.ph & 1) * C.nblk * 32);
     if (threadIdx.x < NV) pp[C.rank * 32 + threadIdx.x] = t;
-    agent_barrier(C.bar_count, C.bar_gen, C.nblk);
+    agent_barrier(C.bar, C.rank, C.nblk);
     if (threadIdx.x < NV) {
       double T = 0.0;
       for (int b = 0; b < C.nblk; ++b) T += pp[b * 32 + threadIdx.x];
@@ -318,11 +378,38 @@ struct Chunk {
   int64_t c0, nb, n;
 };
 
+// The workgroup's records as the fits read them, every epoch: the first `cap` of its chunk
+// staged once in LDS as float32 fields (every fit consumes them through a float32 rounding,
+// so the staged values are the ones it would compute: (float)ctr, (float)value, ...), the rest
+// read from the global store. Local index j = record c0 + j of the agent. Fields [nf][cap]
+// floats: ctr, value, gamma, propensity, utility, estimated utility; then won [cap] bytes.
+enum { kFCtr = 0, kFVal, kFGam, kFProp, kFUtil, kFEu };
+struct RecView {
+  DrRecords R;       // the agent's records (global)
+  const double *eu;  // the agent's estimated utilities (global, DoublyRobustBidder)
+  int64_t c0;
+  const float *lf;  // LDS fields
+  const uint8_t *lw;
+  int64_t cap;      // staged records (a multiple of kDrThreads, so j < cap is block-uniform)
+  __device__ __forceinline__ double f(int fld, const double *g, int64_t j) const {
+    return j < cap ? (double)lf[(int64_t)fld * cap + j] : (double)(float)g[c0 + j];
+  }
+  __device__ __forceinline__ double ctr(int64_t j) const { return f(kFCtr, R.ctr, j); }
+  __device__ __forceinline__ double val(int64_t j) const { return f(kFVal, R.value, j); }
+  __device__ __forceinline__ double gam(int64_t j) const { return f(kFGam, R.gamma, j); }
+  __device__ __forceinline__ float prop(int64_t j) const {
+    return j < cap ? lf[(int64_t)kFProp * cap + j] : (float)R.prop[c0 + j];
+  }
+  __device__ __forceinline__ double util(int64_t j) const { return f(kFUtil, R.util, j); }
+  __device__ __forceinline__ double eut(int64_t j) const { return f(kFEu, eu, j); }
+  __device__ __forceinline__ double won(int64_t j) const { return (double)(j < cap ? lw[j] : R.won[c0 + j]); }
+};
+
 // PyTorchWinRateEstimator fit (src/Bidder.py:229-252 ValueLearningBidder, :500-530
 // DoublyRobustBidder): BCE (mean) over the logs plus the gamma = 0, y = 0 augmentation,
 // Adam(lr 3e-3, wd 1e-6, AMSGrad), ReduceLROnPlateau(patience, factor, min_lr 1e-7),
 // early stop after `wait` epochs without a 1e-6 improvement, <= 32768 epochs.
-__device__ int fit_winrate(const DrRecords &R, const Chunk &K, TrainLds &S, Coop &C, int patience, double factor,
+__device__ int fit_winrate(const RecView &V, const Chunk &K, TrainLds &S, Coop &C, int patience, double factor,
                            int wait, const double *adam_tab, float *tr) {
   const int tid = threadIdx.x;
   adam_reset(S);
@@ -333,20 +420,30 @@ __device__ int fit_winrate(const DrRecords &R, const Chunk &K, TrainLds &S, Coop
   int e = 0;
   for (; e < kWrEpochs; ++e) {
     int64_t acc[5] = {0, 0, 0, 0, 0};
-    for (int64_t r = tid; r < 2 * K.nb; r += kDrThreads) {
-      const int64_t i = K.c0 + (r < K.nb ? r : r - K.nb);
-      const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i];
-      const double g = r < K.nb ? (double)(float)R.gamma[i] : 0.0;
-      const double y = r < K.nb ? (double)R.won[i] : 0.0;
-      const double z = c * (double)S.wr[0] + v * (double)S.wr[1] + g * (double)S.wr[2] + (double)S.wr[3];
-      const double pw = 1.0 / (1.0 + agexp::exp(-z, S.tab));
-      const double t = y > 0.0 ? fmin(softplus(-z, S.tab), 100.0) : fmin(softplus(z, S.tab), 100.0);
+    const double w0 = (double)S.wr[0], w1 = (double)S.wr[1], w2 = (double)S.wr[2], w3 = (double)S.wr[3];
+    // one BCE row: its loss and gradient terms
+    auto row = [&](double c, double v, double g, double y) {
+      const double z = c * w0 + v * w1 + g * w2 + w3;
+      // -log(p) = softplus(-z) for a win, -log(1 - p) = softplus(z) otherwise: one exp(+-z)
+      // besides the sigmoid's exp(-z), one log1p
+      const double em = agexp::exp(-z, S.tab);
+      const double pw = 1.0 / (1.0 + em);
+      const double u = y > 0.0 ? -z : z;
+      const double eu = y > 0.0 ? em : agexp::exp(z, S.tab);
+      const double t = fmin(softplus_e(u, eu), 100.0);
       acc[0] += fxr(t);
       const double gz = pw - y;
       acc[1] += fxr(gz * c);
       acc[2] += fxr(gz * v);
       acc[3] += fxr(gz * g);
       acc[4] += fxr(gz);
+    };
+    // record j's logged row and its gamma = 0, y = 0 augmentation row together (two
+    // independent chains for the scheduler; the sums are exact, so any order)
+    for (int64_t j = tid; j < K.nb; j += kDrThreads) {
+      const double c = V.ctr(j), v = V.val(j);
+      row(c, v, V.gam(j), V.won(j));
+      row(c, v, 0.0, 0.0);
     }
     exact_totals<5>(acc, S, C);
     // every thread: the same loss; threads 0..3 step their parameter
@@ -365,7 +462,7 @@ __device__ int fit_winrate(const DrRecords &R, const Chunk &K, TrainLds &S, Coop
 // BidShadingContextualBandit.initialise_policy (src/Models.py:106-137): imitation of the
 // logging policy, MSE of mu to the logged gammas + MSE of softplus(sigma) (without
 // min_sigma) to 0.05; Adam(lr 1e-3, wd 1e-4, AMSGrad), early stop after 512 epochs.
-__device__ int fit_imitation(const DrRecords &R, const Chunk &K, TrainLds &S, Coop &C, const double *adam_tab,
+__device__ int fit_imitation(const RecView &V, const Chunk &K, TrainLds &S, Coop &C, const double *adam_tab,
                              float *tr) {
   const int tid = threadIdx.x;
   adam_reset(S);
@@ -377,11 +474,10 @@ __device__ int fit_imitation(const DrRecords &R, const Chunk &K, TrainLds &S, Co
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = 0;
     for (int64_t j = tid; j < K.nb; j += kDrThreads) {
-      const int64_t i = K.c0 + j;
-      const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i];
+      const double c = V.ctr(j), v = V.val(j);
       PolF f;
       policy_fwd(S.pol, c, v, f, S.tab);
-      const double dm = f.mu - (double)(float)R.gamma[i], dsg = f.sp_sigma - 0.05;
+      const double dm = f.mu - V.gam(j), dsg = f.sp_sigma - 0.05;
       acc[12] += fxr(dm * dm);
       acc[13] += fxr(dsg * dsg);
       policy_bwd(S.pol, c, v, f, 2.0 * dm, 2.0 * dsg, acc, 0, S.tab);
@@ -402,7 +498,7 @@ __device__ int fit_imitation(const DrRecords &R, const Chunk &K, TrainLds &S, Co
 // -mean((u - u^) clip(pi / pi0, 1/50, 50) + W(ctr, value, g~) (V - V g~)), g~ = clip(mu +
 // sigma eps, 0, 1); Adam(lr 7e-3, wd 1e-4, AMSGrad), ReduceLROnPlateau(patience 100, factor
 // 0.2, min_lr 1e-8, threshold 5e-3), early stop after 512 epochs, <= 32768 epochs.
-__device__ int fit_dr(const DrRecords &R, const double *eu, const Chunk &K, TrainLds &S, Coop &C,
+__device__ int fit_dr(const RecView &V, const Chunk &K, TrainLds &S, Coop &C,
                       const FitNoise &F, const double *adam_tab, float *tr) {
   const int tid = threadIdx.x;
   adam_reset(S);
@@ -418,17 +514,17 @@ __device__ int fit_dr(const DrRecords &R, const double *eu, const Chunk &K, Trai
     for (int j = 0; j < 16; ++j) acc[j] = 0;
     for (int64_t j = tid; j < K.nb; j += kDrThreads) {
       const int64_t i = K.c0 + j;
-      const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i], g = (double)(float)R.gamma[i];
+      const double c = V.ctr(j), v = V.val(j), g = V.gam(j);
       PolF f;
       policy_fwd(S.pol, c, v, f, S.tab);
       const double mu = f.mu, sg = f.sigma;
       const double zz = (mu - g) / sg;
       const double pdf_raw = agexp::exp(-(zz * zz) / 2.0, S.tab) / sg * inv_sqrt2pi;
       const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
-      const double p0 = (double)fmaxf((float)R.prop[i], 1e-15f);
+      const double p0 = (double)fmaxf(V.prop(j), 1e-15f);
       const double iw = pi / p0;
       const double iwc = iw < 1.0 / 50.0 ? 1.0 / 50.0 : (iw > 50.0 ? 50.0 : iw);
-      const double du = (double)(float)R.util[i] - (double)(float)eu[i];
+      const double du = V.util(j) - V.eut(j);
       const double ep = fit_eps(F, e, i);
       const double raw = mu + sg * ep;
       const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
@@ -465,7 +561,7 @@ __device__ int fit_dr(const DrRecords &R, const double *eu, const Chunk &K, Trai
 // -mean(W(ctr, value, g~) (V - V g~)), g~ = clip(mu + sigma eps, 0, 1); Adam(lr 2e-3, wd
 // 1e-6, AMSGrad), ReduceLROnPlateau(patience 100, factor 0.1, min_lr 1e-7), early stop after
 // 256 epochs, <= 16384 epochs. Exact fixed-point sums (bounded terms).
-__device__ int fit_dm(const DrRecords &R, const Chunk &K, TrainLds &S, Coop &C, const FitNoise &F,
+__device__ int fit_dm(const RecView &V, const Chunk &K, TrainLds &S, Coop &C, const FitNoise &F,
                       const double *adam_tab, float *tr) {
   const int tid = threadIdx.x;
   adam_reset(S);
@@ -480,7 +576,7 @@ __device__ int fit_dm(const DrRecords &R, const Chunk &K, TrainLds &S, Coop &C, 
     for (int j = 0; j < 16; ++j) acc[j] = 0;
     for (int64_t j = tid; j < K.nb; j += kDrThreads) {
       const int64_t i = K.c0 + j;
-      const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i];
+      const double c = V.ctr(j), v = V.val(j);
       PolF f;
       policy_fwd(S.pol, c, v, f, S.tab);
       const double ep = fit_eps(F, e, i);
@@ -511,7 +607,7 @@ __device__ int fit_dm(const DrRecords &R, const Chunk &K, TrainLds &S, Coop &C, 
 // per-record gradient of a policy loss term from d/dmu and d/dsigma (policy_bwd's order)
 __device__ __forceinline__ void policy_grad(const float *p, double c, double v, const PolF &f, double dmu,
                                             double dsigma, double (&G)[14], const uint64_t *tab) {
-  const double dam = dmu * dsoftplus(f.am, tab), das = dsigma * dsoftplus(f.as, tab);
+  const double dam = dmu * dsoftplus_e(f.am, f.eam), das = dsigma * dsoftplus_e(f.as, f.eas);
   double ds[2];
   ds[0] = dam * (double)p[6] + das * (double)p[9];
   ds[1] = dam * (double)p[7] + das * (double)p[10];
@@ -523,7 +619,7 @@ __device__ __forceinline__ void policy_grad(const float *p, double c, double v, 
   G[11] += das;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const double dh = ds[j] * dsoftplus(f.h[j], tab);
+    const double dh = ds[j] * dsoftplus_e(f.h[j], f.eh[j]);
     G[2 * j] += dh * c;
     G[2 * j + 1] += dh * v;
     G[4 + j] += dh;
@@ -534,7 +630,7 @@ __device__ __forceinline__ void policy_grad(const float *p, double c, double v, 
 // 174-199; AG_PL_LOSS_* kinds): Adam(lr 2e-3, wd 1e-4, AMSGrad), ReduceLROnPlateau
 // (patience 100, factor 0.2, min_lr 1e-8), early stop after 512 epochs, <= 16384 epochs.
 // oracle/ag_oracle_dr.c pl_epoch, term for term, with the same fixed-order sums.
-__device__ int fit_pl(const DrRecords &R, const Chunk &K, TrainLds &S, Coop &C, int kind, const double *adam_tab,
+__device__ int fit_pl(const RecView &V, const Chunk &K, TrainLds &S, Coop &C, int kind, const double *adam_tab,
                       float *tr) {
   const int tid = threadIdx.x;
   adam_reset(S);
@@ -549,16 +645,15 @@ __device__ int fit_pl(const DrRecords &R, const Chunk &K, TrainLds &S, Coop &C, 
 #pragma unroll
     for (int j = 0; j < 14; ++j) acc[j] = 0.0;
     for (int64_t j = tid; j < K.nb; j += kDrThreads) {
-      const int64_t i = K.c0 + j;
-      const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i], g = (double)(float)R.gamma[i];
+      const double c = V.ctr(j), v = V.val(j), g = V.gam(j);
       PolF f;
       policy_fwd(S.pol, c, v, f, S.tab);
       const double mu = f.mu, sg = f.sigma;
       const double zz = (mu - g) / sg;
       const double pdf_raw = agexp::exp(-(zz * zz) / 2.0, S.tab) / sg * inv_sqrt2pi;
       const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
-      const double p0 = (double)fmaxf((float)R.prop[i], 1e-15f);
-      const double u = (double)(float)R.util[i];
+      const double p0 = (double)fmaxf(V.prop(j), 1e-15f);
+      const double u = V.util(j);
       double term = 0.0, kl = 0.0, dpi = 0.0, dmu = 0.0, dsg = 0.0;
       if (kind == AG_PL_LOSS_REINFORCE) {
         term = -(pi * u);
@@ -608,36 +703,45 @@ __device__ int fit_pl(const DrRecords &R, const Chunk &K, TrainLds &S, Coop &C, 
 
 // The workgroups of the learning bidders (ValueLearning, PolicyLearning, DoublyRobust): block
 // b trains agent blk_agent[b] as workgroup blk_rank[b] of agent_nblk[agent] over the agent's
-// records, running its fits in the reference's order. status: 0 trained, 1
-// ValueLearningBidder fallback (no wins: nothing trained), -1 no logs, -2 NaN loss, -3 out
-// of noise epochs (state not written); epochs [3] = (win-rate, imitation, policy fit);
-// traces [3][32768] (workgroup 0).
-__global__ __launch_bounds__(kDrThreads) void k_bidder_train(
+// records, running its fits in the reference's order, in two launches:
+//   PH = 0: the win-rate fits (ValueLearning, DoublyRobust; a ValueLearningBidder without
+//           wins falls back, status 1) -> wr_ws, epochs [a][0]; a register-lean loop, 4 waves
+//           per SIMD;
+//   PH = 1: everything after (estimated utilities, imitation, the policy fits) from wr_ws,
+//           then the agent's state.
+// status: 0 trained, 1 ValueLearningBidder fallback (no wins: nothing trained), -1 no logs,
+// -2 NaN loss, -3 out of noise epochs (state not written); epochs [3] = (win-rate,
+// imitation, policy fit); traces [3][32768] (workgroup 0).
+template <int PH>
+__global__ __launch_bounds__(kDrThreads, PH == 0 ? 4 : 1) void k_bidder_train(
     const int32_t *__restrict__ bkind, const int32_t *__restrict__ bmode, const int32_t *__restrict__ blk_agent,
     const int32_t *__restrict__ blk_rank, const int32_t *__restrict__ agent_nblk,
     const int64_t *__restrict__ offsets, DrRecords R0, double *__restrict__ eu_ws, float *__restrict__ state,
-    const int32_t *__restrict__ initialised, const float *__restrict__ noise, const int64_t *__restrict__ noise_off,
-    int noise_epochs, uint64_t noise_seed, const double *__restrict__ adam_tab, int32_t *__restrict__ epochs_out,
-    int32_t *__restrict__ status, float *__restrict__ traces, int64_t *__restrict__ partials,
-    unsigned *__restrict__ barriers) {
+    float *__restrict__ wr_ws, const int32_t *__restrict__ initialised, const float *__restrict__ noise,
+    const int64_t *__restrict__ noise_off, int noise_epochs, uint64_t noise_seed, const double *__restrict__ adam_tab,
+    int32_t *__restrict__ epochs_out, int32_t *__restrict__ status, float *__restrict__ traces,
+    int64_t *__restrict__ partials, unsigned *__restrict__ barriers, const int32_t *__restrict__ bar_off, int nf,
+    int64_t cap) {
   const int a = blk_agent[blockIdx.x], rank = blk_rank[blockIdx.x], nblk = agent_nblk[a];
   const int tid = threadIdx.x;
   const int bk = bkind[a];
   const int64_t s0 = offsets[a], n = offsets[a + 1] - s0;
   const bool lead = rank == 0;
+  const bool has_wr = bk == AG_BIDDER_DOUBLY_ROBUST || bk == AG_BIDDER_VALUE_LEARNING;
   if (n == 0) {
     // no logs: a ValueLearningBidder falls back (its won mask sums to 0, src/Bidder.py:206-
     // 211); the other learners fail in the reference
-    if (lead && tid == 0) {
+    if (PH == 1 && lead && tid == 0) {
       epochs_out[3 * a] = epochs_out[3 * a + 1] = epochs_out[3 * a + 2] = 0;
       status[a] = bk == AG_BIDDER_VALUE_LEARNING ? 1 : -1;
     }
     return;
   }
+  if (PH == 1 && bk == AG_BIDDER_VALUE_LEARNING && status[a] == 1) return;  // fallback: state unchanged
   __shared__ TrainLds S;
   for (int i = tid; i < 256; i += kDrThreads) S.tab[i] = ag_exp_tab[i];
   float *st = state + (size_t)a * 16;
-  if (tid < 4) S.wr[tid] = st[tid];
+  if (tid < 4) S.wr[tid] = (PH == 1 && has_wr) ? wr_ws[(size_t)a * 4 + tid] : st[tid];
   if (tid < 12) S.pol[tid] = st[4 + tid];
   if (tid == 0) S.stop = S.exhausted = 0;
   __syncthreads();
@@ -646,58 +750,91 @@ __global__ __launch_bounds__(kDrThreads) void k_bidder_train(
   const int64_t c0 = (int64_t)rank * per < n ? (int64_t)rank * per : n;
   const Chunk K{c0, (c0 + per < n ? c0 + per : n) - c0, n};
   // the agent's exchange region [2][nblk][32] (its workgroups have consecutive block indices)
-  Coop C{rank, nblk, partials + (size_t)(blockIdx.x - rank) * 2 * 32, barriers + 2 * a, barriers + 2 * a + 1, 0};
-  const FitNoise F{noise ? noise + noise_off[a] : nullptr, n, noise_seed, (uint32_t)a,
-                   noise ? noise_epochs : 1 << 30};
-  float *tr = (traces && lead) ? traces + (size_t)a * 3 * kDrEpochs : nullptr;
-  int ep[3] = {0, 0, 0};
-  int stat = 0;
-  if (bk == AG_BIDDER_DOUBLY_ROBUST) {
-    ep[0] = fit_winrate(R, K, S, C, 256, 0.2, 1024, adam_tab, tr);
-    // estimated utilities of this workgroup's records with the fitted model (src/Bidder.py:541-546)
-    double *eu = eu_ws + s0;
-    for (int64_t j = tid; j < K.nb; j += kDrThreads) {
+  Coop C{rank, nblk, partials + (size_t)(blockIdx.x - rank) * 2 * 32, barriers + (size_t)bar_off[a] * kBarLineWords, 0};
+  // stage the chunk's first `cap` records in LDS (the fields this phase's fits read)
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+  float *lf = reinterpret_cast<float *>(s_dyn);
+  uint8_t *lw = reinterpret_cast<uint8_t *>(lf + (size_t)nf * cap);
+  {
+    const int64_t ns = K.nb < cap ? K.nb : cap;
+    const bool full = PH == 1 && bk != AG_BIDDER_VALUE_LEARNING;  // propensity, utility
+    const bool won = PH == 0 || bk == AG_BIDDER_DOUBLY_ROBUST;
+    for (int64_t j = tid; j < ns; j += kDrThreads) {
       const int64_t i = K.c0 + j;
-      const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i], g = (double)(float)R.gamma[i];
-      const double z = c * (double)S.wr[0] + v * (double)S.wr[1] + g * (double)S.wr[2] + (double)S.wr[3];
-      const float W = (float)(1.0 / (1.0 + agexp::exp(-z, S.tab)));
-      const double V = R.ctr[i] * R.value[i], P = R.ctr[i] * R.value[i] * R.gamma[i];
-      eu[i] = (double)W * (V - P);
+      lf[kFCtr * cap + j] = (float)R.ctr[i];
+      lf[kFVal * cap + j] = (float)R.value[i];
+      lf[kFGam * cap + j] = (float)R.gamma[i];
+      if (full) {
+        lf[kFProp * cap + j] = (float)R.prop[i];
+        lf[kFUtil * cap + j] = (float)R.util[i];
+      }
+      if (won) lw[j] = R.won[i];
     }
     __syncthreads();
-    if (!initialised[a]) ep[1] = fit_imitation(R, K, S, C, adam_tab, tr ? tr + kDrEpochs : nullptr);
-    ep[2] = fit_dr(R, eu, K, S, C, F, adam_tab, tr ? tr + 2 * kDrEpochs : nullptr);
-    stat = S.stop ? -2 : 0;
-  } else if (bk == AG_BIDDER_VALUE_LEARNING) {
-    int64_t acc[1] = {0};
-    for (int64_t j = tid; j < K.nb; j += kDrThreads) acc[0] += R.won[K.c0 + j] ? 1 : 0;
-    exact_totals<1>(acc, S, C);
-    if (S.tot[0] == 0 && S.tot[1] == 0) {
-      stat = 1;  // src/Bidder.py:206-211: revert to Gaussian shading, nothing trained
-    } else {
-      ep[0] = fit_winrate(R, K, S, C, 100, 0.1, 512, adam_tab, tr);
-      if (bmode[a] == AG_VL_POLICY) ep[2] = fit_dm(R, K, S, C, F, adam_tab, tr ? tr + 2 * kDrEpochs : nullptr);
+  }
+  const RecView V{R, eu_ws + s0, K.c0, lf, lw, cap};
+  float *tr = (traces && lead) ? traces + (size_t)a * 3 * kDrEpochs : nullptr;
+  if constexpr (PH == 0) {
+    int ep0 = 0, stat = 0;
+    if (bk == AG_BIDDER_DOUBLY_ROBUST) {
+      ep0 = fit_winrate(V, K, S, C, 256, 0.2, 1024, adam_tab, tr);
+    } else {  // ValueLearningBidder
+      int64_t acc[1] = {0};
+      for (int64_t j = tid; j < K.nb; j += kDrThreads) acc[0] += V.won(j) != 0.0 ? 1 : 0;
+      exact_totals<1>(acc, S, C);
+      if (S.tot[0] == 0 && S.tot[1] == 0)
+        stat = 1;  // src/Bidder.py:206-211: revert to Gaussian shading, nothing trained
+      else
+        ep0 = fit_winrate(V, K, S, C, 100, 0.1, 512, adam_tab, tr);
     }
-  } else {  // PolicyLearningBidder
-    if (!initialised[a]) ep[1] = fit_imitation(R, K, S, C, adam_tab, tr ? tr + kDrEpochs : nullptr);
-    ep[2] = fit_pl(R, K, S, C, bmode[a], adam_tab, tr ? tr + 2 * kDrEpochs : nullptr);
-    stat = S.stop ? -2 : 0;
+    if (!lead) return;
+    if (tid == 0) {
+      epochs_out[3 * a] = ep0;
+      status[a] = stat;
+    }
+    if (tid < 4) wr_ws[(size_t)a * 4 + tid] = S.wr[tid];
+  } else {
+    const FitNoise F{noise ? noise + noise_off[a] : nullptr, n, noise_seed, (uint32_t)a,
+                     noise ? noise_epochs : 1 << 30};
+    int ep1 = 0, ep2 = 0;
+    int stat = 0;
+    if (bk == AG_BIDDER_DOUBLY_ROBUST) {
+      // estimated utilities of this workgroup's records with the fitted model (src/Bidder.py:541-546)
+      double *eu = eu_ws + s0;
+      for (int64_t j = tid; j < K.nb; j += kDrThreads) {
+        const int64_t i = K.c0 + j;
+        const double c = (double)(float)R.ctr[i], v = (double)(float)R.value[i], g = (double)(float)R.gamma[i];
+        const double z = c * (double)S.wr[0] + v * (double)S.wr[1] + g * (double)S.wr[2] + (double)S.wr[3];
+        const float W = (float)(1.0 / (1.0 + agexp::exp(-z, S.tab)));
+        const double Vv = R.ctr[i] * R.value[i], P = R.ctr[i] * R.value[i] * R.gamma[i];
+        eu[i] = (double)W * (Vv - P);
+        if (j < cap) lf[kFEu * cap + j] = (float)eu[i];
+      }
+      __syncthreads();
+      if (!initialised[a]) ep1 = fit_imitation(V, K, S, C, adam_tab, tr ? tr + kDrEpochs : nullptr);
+      ep2 = fit_dr(V, K, S, C, F, adam_tab, tr ? tr + 2 * kDrEpochs : nullptr);
+      stat = S.stop ? -2 : 0;
+    } else if (bk == AG_BIDDER_VALUE_LEARNING) {
+      if (bmode[a] == AG_VL_POLICY) ep2 = fit_dm(V, K, S, C, F, adam_tab, tr ? tr + 2 * kDrEpochs : nullptr);
+    } else {  // PolicyLearningBidder
+      if (!initialised[a]) ep1 = fit_imitation(V, K, S, C, adam_tab, tr ? tr + kDrEpochs : nullptr);
+      ep2 = fit_pl(V, K, S, C, bmode[a], adam_tab, tr ? tr + 2 * kDrEpochs : nullptr);
+      stat = S.stop ? -2 : 0;
+    }
+    __syncthreads();
+    if (S.exhausted) stat = -3;  // not applied: the caller supplies more noise epochs
+    if (!lead) return;
+    if (tid == 0) {
+      epochs_out[3 * a + 1] = ep1;
+      epochs_out[3 * a + 2] = ep2;
+      status[a] = stat;
+    }
+    if (stat == -3) return;
+    if (tid < 4) st[tid] = S.wr[tid];
+    if (tid < 12) st[4 + tid] = S.pol[tid];
   }
-  __syncthreads();
-  if (S.exhausted) stat = -3;  // not applied: the caller supplies more noise epochs
-  if (!lead) return;
-  if (tid == 0) {
-    epochs_out[3 * a] = ep[0];
-    epochs_out[3 * a + 1] = ep[1];
-    epochs_out[3 * a + 2] = ep[2];
-    status[a] = stat;
-  }
-  if (stat == -3) return;
-  if (tid < 4) st[tid] = S.wr[tid];
-  if (tid < 12) st[4 + tid] = S.pol[tid];
 }
 
-// bucket the shading store by agent: histogram, scan, scatter of every record field
 __global__ __launch_bounds__(kDrThreads) void k_sh_hist(const int32_t *__restrict__ agent, int64_t n, int N,
                                                         int64_t *__restrict__ counts) {
   extern __shared__ unsigned int s_hist[];
@@ -909,78 +1046,142 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agen
   int32_t *d_stat = d_epochs + 3 * (size_t)N;
   AG_HIP(hipMemcpyAsync(d_noff, noise_offsets, sizeof(int64_t) * N, hipMemcpyHostToDevice, st));
   AG_HIP(hipMemsetAsync(d_epochs, 0, sizeof(int32_t) * 4 * N, st));
-  // workgroups per learning bidder: one per `chunk` records, co-resident (cooperative
-  // launch) when an agent has several; capped to the resident grid
-  if (!w.coop_blocks) {
-    int per_cu = 0, cus = 0;
-    AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_bidder_train, kDrThreads, 0));
-    AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-    w.coop_blocks = per_cu * cus > 0 ? per_cu * cus : 1;
-  }
-  const int64_t chunk = c->bidder_chunk > 0 ? c->bidder_chunk : kBidderChunk;
-  std::vector<int32_t> nblk(N, 0), blk_agent, blk_rank;
-  int64_t want = 0;
-  for (int a = 0; a < N; ++a) {
+  // Workgroups per learning bidder, co-resident (cooperative launch) when an agent has
+  // several; capped to the resident grid (occupancy with the phase's largest record cache).
+  // With AG_OPT_BIDDER_BLOCK_SAMPLES set: one per that many records. By default the
+  // exact-sum learners (ValueLearning, DoublyRobust: results independent of the split)
+  // share the resident grid in proportion to their records, >= kMinChunk records per
+  // workgroup; a PolicyLearningBidder (fixed-order float sums: its result follows the split)
+  // keeps one workgroup per kBidderChunk records. Both phases use the same rule with their
+  // own grid.
+  auto is_learner = [&](int a) {
     const int bk = c->h_bkind[a];
-    const bool learner = bk == AG_BIDDER_VALUE_LEARNING || bk == AG_BIDDER_POLICY_LEARNING ||
-                         bk == AG_BIDDER_DOUBLY_ROBUST;
-    if (!learner || (agents && !agents[a])) continue;
-    nblk[a] = cnt[a] > 0 ? (int32_t)((cnt[a] + chunk - 1) / chunk) : 1;
-    want += nblk[a];
-  }
-  if (want > w.coop_blocks) {  // share the resident grid out
-    const double f = (double)w.coop_blocks / (double)want;
-    for (int a = 0; a < N; ++a)
-      if (nblk[a] > 1) nblk[a] = (int32_t)(nblk[a] * f) > 1 ? (int32_t)(nblk[a] * f) : 1;
-  }
-  bool multi = false;
-  for (int a = 0; a < N; ++a) {
-    multi |= nblk[a] > 1;
-    for (int r = 0; r < nblk[a]; ++r) {
-      blk_agent.push_back(a);
-      blk_rank.push_back(r);
+    return (bk == AG_BIDDER_VALUE_LEARNING || bk == AG_BIDDER_POLICY_LEARNING || bk == AG_BIDDER_DOUBLY_ROBUST) &&
+           !(agents && !agents[a]);
+  };
+  struct Plan {
+    const void *fn = nullptr;
+    std::vector<int32_t> nblk, blk_agent, blk_rank, bar_off;
+    int G = 0, lines = 0, nf = 0;
+    bool multi = false;
+    int64_t rcap = 0;
+    size_t dyn = 0;
+  };
+  auto plan = [&](int ph, Plan &P) -> int {
+    P.fn = ph == 0 ? (const void *)k_bidder_train<0> : (const void *)k_bidder_train<1>;
+    const size_t lds_budget = ph == 0 ? kRecLdsBytes0 : kRecLdsBytes;
+    int &coop_blocks = ph == 0 ? w.coop_blocks0 : w.coop_blocks;
+    if (!coop_blocks) {
+      int per_cu = 0, cus = 0;
+      AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, P.fn, kDrThreads, lds_budget));
+      AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+      coop_blocks = per_cu * cus > 0 ? per_cu * cus : 1;
     }
-  }
-  const int G = (int)blk_agent.size();
-  if (multi && G > w.coop_blocks)
-    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_bidder_update: %d learning bidders need more co-resident "
-                        "workgroups (%d) than the device holds (%d)", N, G, w.coop_blocks);
-  if (G > 0) {
-    // tables: blk_agent [G], blk_rank [G], agent_nblk [N] i32; barriers [N][2] u32;
-    // exchange partials [G][2][32] i64
-    const size_t tbytes = sizeof(int32_t) * (2 * (size_t)G + N) + sizeof(unsigned) * 2 * N;
-    const size_t pbytes = sizeof(int64_t) * 64 * (size_t)G;
-    if (tbytes + pbytes + 64 > w.coop_bytes) {
-      (void)hipFree(w.coop);
-      w.coop = nullptr;
-      w.coop_bytes = 0;
-      AG_HIP(hipMalloc(&w.coop, tbytes + pbytes + 64));
-      w.coop_bytes = tbytes + pbytes + 64;
+    std::vector<int32_t> &nblk = P.nblk;
+    nblk.assign(N, 0);
+    int64_t want = 0, exact_recs = 0, fixed_blocks = 0;
+    int nf = 0;  // float fields of the record cache: 3 (win-rate, ValueLearning), 5 (PolicyLearning), 6 (DR)
+    for (int a = 0; a < N; ++a) {
+      const int bk = c->h_bkind[a];
+      if (!is_learner(a) || (ph == 0 && bk == AG_BIDDER_POLICY_LEARNING)) continue;
+      nf = std::max(nf, ph == 0 ? 3 : (bk == AG_BIDDER_DOUBLY_ROBUST ? 6 : (bk == AG_BIDDER_POLICY_LEARNING ? 5 : 3)));
+      if (c->bidder_chunk > 0 || bk == AG_BIDDER_POLICY_LEARNING) {
+        const int64_t chunk = c->bidder_chunk > 0 ? c->bidder_chunk : kBidderChunk;
+        nblk[a] = cnt[a] > 0 ? (int32_t)((cnt[a] + chunk - 1) / chunk) : 1;
+        fixed_blocks += nblk[a];
+      } else {
+        exact_recs += cnt[a];
+        nblk[a] = -1;
+      }
     }
-    int64_t *d_part = (int64_t *)w.coop;
-    int32_t *d_bagent = (int32_t *)(d_part + 64 * (size_t)G);
-    int32_t *d_brank = d_bagent + G;
-    int32_t *d_nblk = d_brank + G;
-    unsigned *d_bar = (unsigned *)(d_nblk + N);
-    AG_HIP(hipMemcpyAsync(d_bagent, blk_agent.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
-    AG_HIP(hipMemcpyAsync(d_brank, blk_rank.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
-    AG_HIP(hipMemcpyAsync(d_nblk, nblk.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
-    AG_HIP(hipMemsetAsync(d_bar, 0, sizeof(unsigned) * 2 * N, st));
+    for (int a = 0; a < N; ++a) {
+      if (nblk[a] < 0) {
+        const int64_t avail = std::max<int64_t>(1, coop_blocks - fixed_blocks);
+        const int64_t share = exact_recs > 0 ? (int64_t)((double)avail * (double)cnt[a] / (double)exact_recs) : 1;
+        nblk[a] = (int32_t)std::max<int64_t>(1, std::min<int64_t>((cnt[a] + kMinChunk - 1) / kMinChunk, share));
+      }
+      want += nblk[a];
+    }
+    if (want > coop_blocks) {  // share the resident grid out
+      const double f = (double)coop_blocks / (double)want;
+      for (int a = 0; a < N; ++a)
+        if (nblk[a] > 1) nblk[a] = (int32_t)(nblk[a] * f) > 1 ? (int32_t)(nblk[a] * f) : 1;
+    }
+    int64_t most = 0;  // records of the largest workgroup chunk
+    P.bar_off.assign(N, 0);
+    for (int a = 0; a < N; ++a) {
+      P.multi |= nblk[a] > 1;
+      if (nblk[a]) most = std::max<int64_t>(most, (cnt[a] + nblk[a] - 1) / nblk[a]);
+      P.bar_off[a] = P.lines;
+      P.lines += bar_lines(nblk[a]);
+      for (int r = 0; r < nblk[a]; ++r) {
+        P.blk_agent.push_back(a);
+        P.blk_rank.push_back(r);
+      }
+    }
+    P.G = (int)P.blk_agent.size();
+    if (P.multi && P.G > coop_blocks)
+      return ag_set_error(AG_ERR_UNSUPPORTED, "ag_bidder_update: %d learning bidders need more co-resident "
+                          "workgroups (%d) than the device holds (%d)", N, P.G, coop_blocks);
+    // record cache: [nf][cap] floats + [cap] bytes, cap a multiple of the block size
+    const int64_t rcap_fit = nf ? (int64_t)lds_budget / (4 * nf + 1) / kDrThreads * kDrThreads : 0;
+    P.rcap = std::min<int64_t>(rcap_fit, (most + kDrThreads - 1) / kDrThreads * kDrThreads);
+    if (c->bidder_cache >= 0) P.rcap = std::min<int64_t>(P.rcap, c->bidder_cache / kDrThreads * kDrThreads);
+    P.nf = nf;
+    P.dyn = ((size_t)P.rcap * (4 * nf + 1) + 15) / 16 * 16;
+    return AG_OK;
+  };
+  Plan P0, P1;
+  if (int rc = plan(0, P0)) return rc;
+  if (int rc = plan(1, P1)) return rc;
+  // device tables (shared by the two launches, rewritten in stream order): exchange
+  // partials [G][2][32] i64; barrier lines [lines][32] u32; blk_agent [G], blk_rank [G],
+  // agent_nblk [N], bar_off [N] i32; win-rate models [N][4] f32 (phase 0 -> phase 1)
+  const size_t gmax = (size_t)std::max(P0.G, P1.G), lmax = (size_t)std::max(P0.lines, P1.lines);
+  const size_t need_coop = sizeof(int64_t) * 64 * gmax + sizeof(unsigned) * kBarLineWords * lmax +
+                           sizeof(int32_t) * (2 * gmax + 2 * (size_t)N) + sizeof(float) * 4 * N + 64;
+  if (need_coop > w.coop_bytes) {
+    (void)hipFree(w.coop);
+    w.coop = nullptr;
+    w.coop_bytes = 0;
+    AG_HIP(hipMalloc(&w.coop, need_coop));
+    w.coop_bytes = need_coop;
+  }
+  int64_t *d_part = (int64_t *)w.coop;
+  unsigned *d_bar = (unsigned *)(d_part + 64 * gmax);
+  int32_t *d_bagent = (int32_t *)(d_bar + kBarLineWords * lmax);
+  int32_t *d_brank = d_bagent + gmax;
+  int32_t *d_nblk = d_brank + gmax;
+  int32_t *d_baroff = d_nblk + N;
+  float *d_wr = (float *)(d_baroff + N);
+  auto launch = [&](const Plan &P) -> int {
+    if (P.G == 0) return AG_OK;
+    AG_HIP(hipMemcpyAsync(d_bagent, P.blk_agent.data(), sizeof(int32_t) * P.G, hipMemcpyHostToDevice, st));
+    AG_HIP(hipMemcpyAsync(d_brank, P.blk_rank.data(), sizeof(int32_t) * P.G, hipMemcpyHostToDevice, st));
+    AG_HIP(hipMemcpyAsync(d_nblk, P.nblk.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
+    AG_HIP(hipMemcpyAsync(d_baroff, P.bar_off.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
+    if (P.lines) AG_HIP(hipMemsetAsync(d_bar, 0, sizeof(unsigned) * kBarLineWords * P.lines, st));
     DrRecords R{b_ctr, b_val, b_gam, b_prop, b_util, b_won};
-    const int32_t *cbk = c->d_bkind, *cmode = w.mode, *cinit = w.init;
+    const int32_t *cbk = c->d_bkind, *cmode = w.mode, *cinit = w.init, *cbo = d_baroff;
     const int64_t *coff = d_off, *cnoff = d_noff;
     double *ceu = b_eu;
-    float *cstate = w.state, *ctr = traces;
+    float *cstate = w.state, *ctr = traces, *cwr = d_wr;
     int cne = noise_epochs;
     uint64_t cseed = c->fit_noise_seed;
     const double *ctab = w.adam_tab;
-    void *args[] = {&cbk, &cmode, &d_bagent, &d_brank, &d_nblk, &coff, &R, &ceu, &cstate, &cinit, &noise, &cnoff,
-                    &cne, &cseed, &ctab, &d_epochs, &d_stat, &ctr, &d_part, &d_bar};
-    if (multi)  // workgroups of one agent wait for each other: they must all be resident
-      AG_HIP(hipLaunchCooperativeKernel((const void *)k_bidder_train, dim3(G), dim3(kDrThreads), args, 0, st));
+    int cnf = P.nf;
+    int64_t ccap = P.rcap;
+    void *args[] = {&cbk,  &cmode,  &d_bagent, &d_brank, &d_nblk, &coff,  &R,        &ceu,
+                    &cstate, &cwr,  &cinit,    &noise,   &cnoff,  &cne,   &cseed,    &ctab,
+                    &d_epochs, &d_stat, &ctr,  &d_part,  &d_bar,  &cbo,   &cnf,      &ccap};
+    if (P.multi)  // workgroups of one agent wait for each other: they must all be resident
+      AG_HIP(hipLaunchCooperativeKernel(P.fn, dim3(P.G), dim3(kDrThreads), args, P.dyn, st));
     else
-      AG_HIP(hipLaunchKernel((const void *)k_bidder_train, dim3(G), dim3(kDrThreads), args, 0, st));
-  }
+      AG_HIP(hipLaunchKernel(P.fn, dim3(P.G), dim3(kDrThreads), args, P.dyn, st));
+    return AG_OK;
+  };
+  if (int rc = launch(P0)) return rc;
+  if (int rc = launch(P1)) return rc;
   std::vector<int32_t> h(4 * (size_t)N);
   AG_HIP(hipMemcpyAsync(h.data(), d_epochs, sizeof(int32_t) * 4 * N, hipMemcpyDeviceToHost, st));
   AG_HIP(hipStreamSynchronize(st));

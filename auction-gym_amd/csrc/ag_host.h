@@ -44,7 +44,8 @@ struct ag_dr_ws {
   int64_t *scratch = nullptr;   // [N] noise offsets + [N][4] epochs / status
   void *coop = nullptr;         // trainer workgroup tables, barriers, exchange partials
   size_t coop_bytes = 0;
-  int coop_blocks = 0;          // co-resident workgroups of k_bidder_train
+  int coop_blocks = 0;          // co-resident workgroups of k_bidder_train<1>
+  int coop_blocks0 = 0;         // co-resident workgroups of k_bidder_train<0>
 };
 
 struct ag_ctx {
@@ -70,6 +71,7 @@ struct ag_ctx {
   bool dr_loaded = false, dr_any_init = false;  // learner models loaded; some bid from a policy
   bool vl_any_search = false;                    // some ValueLearningBidder bids by search
   int64_t bidder_chunk = 0;                      // AG_OPT_BIDDER_BLOCK_SAMPLES (0: default)
+  int64_t bidder_cache = -1;                     // AG_OPT_BIDDER_RECORD_CACHE (-1: default)
   uint64_t fit_noise_seed = 0;                   // AG_OPT_FIT_NOISE_SEED
   ag_dr_ws dr;
   int32_t *d_akind = nullptr, *d_bkind = nullptr;

@@ -520,6 +520,9 @@ int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
     case AG_OPT_FIT_NOISE_SEED:
       c->fit_noise_seed = (uint64_t)value;
       return AG_OK;
+    case AG_OPT_BIDDER_RECORD_CACHE:
+      c->bidder_cache = value;
+      return AG_OK;
     default:
       return ag_set_error(AG_ERR_INVALID, "ag_set_option: unknown option %d", option);
   }

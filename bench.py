@@ -255,17 +255,12 @@ def algorithmic_bytes_population(E, P, K, Do, ak, bk, init):
     return reads + writes
 
 
-def run_population(key, steps, warmup, world, rank, local, batch=None, with_update=True):
-    """A BASELINE config population on the GPU at its per-GPU shard size: iteration 0 with
-    Gaussian shading (uninitialised learners), the update of every learner (LR-TS allocators
-    and learning bidders, on the GPU, synthetic rsample noise; records all-gathered when N > 1)
-    timed, then the timed steps with bids from the fitted policies. Inputs Philox-generated
-    and resident in HBM."""
+def build_population(key, local):
+    """Engine for a BASELINE config population: catalogue as src/main.py:60-72, LR-TS posteriors
+    and learning bidders' models as the reference constructors draw them (seeded torch)."""
     from auctiongym_amd import _lib
     from auctiongym_amd.engine import AuctionEngine
-    from auctiongym_amd.sharding import allreduce_counters, gather_records, shard_range
     what, groups, B0, tag = POPULATIONS[key]
-    B = int(batch or B0)
     cfg = _agents_cfg(groups, dict(SP_ORACLE, allocation="FirstPrice"))
     items, values = catalogue(cfg)
     N, K, D = items.shape
@@ -279,7 +274,6 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
             bk.append(kinds[bidder])
             modes.append(_lib.VL_POLICY if kw.get("inference") == "policy" else 0)
     ak, bk, modes = np.array(ak, np.int32), np.array(bk, np.int32), np.array(modes, np.int32)
-    dev = torch.device("cuda", local)
     eng = AuctionEngine(N, P, K, E, OE, _lib.FIRST_PRICE, 1.0, device=local)
     eng.set_agent_params(ak, bk, np.ones(N), np.full(N, 0.02))
     eng.load_catalog(items, values)
@@ -295,6 +289,21 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
         st16[a] = np.concatenate([p.detach().numpy().ravel() for lin in lins for p in lin.parameters()])
     eng.set_dr_state(st16, np.zeros(N, np.int32))
     eng.set_bidder_modes(modes)
+    dims = dict(N=N, K=K, E=E, P=P, Do=Do)
+    return eng, what, B0, ak, bk, st16, dims
+
+
+def run_population(key, steps, warmup, world, rank, local, batch=None, with_update=True):
+    """A BASELINE config population on the GPU at its per-GPU shard size: iteration 0 with
+    Gaussian shading (uninitialised learners), the update of every learner (LR-TS allocators
+    and learning bidders, on the GPU, synthetic rsample noise; records all-gathered when N > 1)
+    timed, then the timed steps with bids from the fitted policies. Inputs Philox-generated
+    and resident in HBM."""
+    from auctiongym_amd.sharding import allreduce_counters, gather_records, shard_range
+    eng, what, B0, ak, bk, st16, dims = build_population(key, local)
+    B = int(batch or B0)
+    N, K, E, P, Do = (dims[k] for k in ("N", "K", "E", "P", "Do"))
+    dev = torch.device("cuda", local)
     lo, _ = shard_range(B * world, rank, world)
     inp = eng.alloc_inputs(B)
     eng.generate(0, lo, inp)

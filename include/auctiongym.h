@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define AG_ABI_VERSION 13
+#define AG_ABI_VERSION 14
 
 typedef enum ag_status {
   AG_OK = 0,
@@ -192,10 +192,15 @@ typedef enum ag_option {
                                    (0 = 16 per lane = 4096); fewer spreads an agent over more
                                    workgroups -- identical results (exact sums) */
   AG_OPT_BIDDER_BLOCK_SAMPLES = 4, /* value: records per workgroup of the learning bidders'
-                                   trainer (0 = 8192); identical results for the exact-sum fits,
-                                   the policy-learning fits' fixed-order sums follow the split */
-  AG_OPT_FIT_NOISE_SEED = 5       /* value: seed of the synthetic rsample noise of ag_bidder_update
+                                   trainer (0 = default: the exact-sum learners share the resident
+                                   grid, >= 1024 records per workgroup; PolicyLearningBidder 8192);
+                                   identical results for the exact-sum fits, the policy-learning
+                                   fits' fixed-order sums follow the split */
+  AG_OPT_FIT_NOISE_SEED = 5,      /* value: seed of the synthetic rsample noise of ag_bidder_update
                                    called with noise == NULL (default 0) */
+  AG_OPT_BIDDER_RECORD_CACHE = 6  /* value: most records per workgroup the learning bidders'
+                                   trainer stages in LDS (-1 = default: as many as fit; 0 = none,
+                                   every epoch reads the store); identical results */
 } ag_option;
 
 typedef enum ag_item_search {

@@ -1254,6 +1254,18 @@ def test_bidder_update_multi_workgroup(gpu, oracle):
     workgroups (200 records each): DM and DR fits (exact sums) give the single-workgroup
     oracle's results bit for bit; the PPO fit's fixed-order sums follow the split, equal to
     the oracle run with the same number of workgroups."""
+    _learners_vs_oracle(oracle, 200, -1)
+
+
+@pytest.mark.parametrize("cache", [0, 512])
+def test_bidder_update_record_cache(gpu, oracle, cache):
+    """One workgroup per learning bidder with its record cache in LDS capped (512 records:
+    the rest of each epoch read from the store; 0: every record from the store): the same
+    bits as the oracle."""
+    _learners_vs_oracle(oracle, 1 << 30, cache)
+
+
+def _learners_vs_oracle(oracle, block, cache):
     import torch
     from auctiongym_amd.engine import AuctionEngine
     specs = [("dm", "dm_update_kat.npz", 2), ("ips", "ips_update_kat.npz", 0), ("ips", "ips_update_kat.npz", 1),
@@ -1264,13 +1276,14 @@ def test_bidder_update_multi_workgroup(gpu, oracle):
     eng.set_agent_params(np.ones(N, np.int32), bk, np.ones(N), np.full(N, 0.02))
     eng.set_dr_state(state0, np.zeros(N, np.int32))
     eng.set_bidder_modes(modes)
-    eng.set_bidder_block_samples(200)
+    eng.set_bidder_block_samples(block)
+    eng.set_bidder_record_cache(cache)
     E = 10300
     noises, offs, off, orc = [], [], 0, []
     for a, (kind, _, _) in enumerate(specs):
         k = data[a]
         n = len(k("est_ctr"))
-        nblk = (n + 199) // 200
+        nblk = (n + block - 1) // block
         if kind == "dm":
             z = _dr_noise(k("fit1_rng"), n, E)
             orc.append(oracle.vl_update(k("est_ctr"), k("value"), k("gamma"), k("won"), state0[a, :4], state0[a, 4:],

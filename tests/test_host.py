@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 def test_library_loads_without_gpu_and_reports_abi():
     from auctiongym_amd import _lib
     L = _lib.load()
-    assert L.ag_abi_version() == _lib.ABI_VERSION == 13
+    assert L.ag_abi_version() == _lib.ABI_VERSION == 14
 
 
 def test_counters_to_double_host_helper():
