@@ -26,7 +26,7 @@ struct ag_lrts_ws {
   int32_t *epochs = nullptr;  // [N]
   void *tables = nullptr;     // workgroup -> (agent, rank) tables + per-agent barriers
   int64_t *partials = nullptr;  // per-workgroup exact partial sums, 2 epoch parities
-  size_t tab_cap = 0, part_cap = 0;
+  size_t tab_cap = 0, part_cap = 0, bar_cap = 0;
   int coop_blocks = 0;        // co-resident workgroups of the training kernel
   int32_t *status = nullptr;  // [1] device-side error flags
 };

@@ -26,6 +26,7 @@
 #include "ag_exp.h"
 #include "ag_exp_table.h"
 #include "ag_host.h"
+#include "ag_coop.h"
 
 namespace {
 
@@ -204,24 +205,6 @@ __device__ __forceinline__ void lr_laplace_sample(const LrSample &s, const float
     acc[(s.item * DO + d) * kAccStride] += fx_round((double)w * (double)(s.x[d] * s.x[d]), kGradScale);
 }
 
-// Barrier of the `nblk` workgroups training one agent (all co-resident: cooperative
-// launch). Thread 0 reads the generation, arrives, and the last arrival opens the next
-// generation; agent-scope release / acquire make the partials written before the barrier
-// (by any workgroup, on any XCD) visible to every workgroup after it.
-__device__ __forceinline__ void agent_barrier(unsigned *count, unsigned *gen, int nblk) {
-  __syncthreads();
-  if (nblk > 1 && threadIdx.x == 0) {
-    const unsigned g = __hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    if (__hip_atomic_fetch_add(count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nblk - 1) {
-      __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      while (__hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-}
-
 // Per-block column sums of the lane accumulator tile (thread = column c, row group r;
 // each value split at bit 24 so no partial can overflow) into the block's slot of the
 // agent's partials [rank][KD + 1][2] (column KD: the loss); the tile is zeroed for reuse.
@@ -270,14 +253,14 @@ __global__ __launch_bounds__(kLrThreads) void k_lrts_train(
     const int64_t *__restrict__ offsets, const uint32_t *__restrict__ key, const float *__restrict__ xs,
     int64_t cap, float *__restrict__ gm, float *__restrict__ gq, float *__restrict__ gpm,
     const double *__restrict__ adam_tab, int32_t *__restrict__ epochs_out, float *__restrict__ loss_trace,
-    int64_t *__restrict__ partials, unsigned *__restrict__ barriers) {
+    int64_t *__restrict__ partials, unsigned *__restrict__ barriers, const int32_t *__restrict__ bar_off) {
   const int a = blk_agent[blockIdx.x], rank = blk_rank[blockIdx.x], nblk = agent_nblk[a];
   const int tid = threadIdx.x;
   const int64_t s0 = offsets[a], n = offsets[a + 1] - s0;
   const int KD = K * DO;
   const int PW = 2 * (KD + 1);  // int64 per partial record
   int64_t *pbase = partials + agent_pbase[a];  // [2 parities][nblk][KD + 1][2]
-  unsigned *bar_count = barriers + 2 * a, *bar_gen = bar_count + 1;
+  unsigned *bar = barriers + (size_t)bar_off[a] * agcoop::kBarLineWords;
   // this workgroup's samples: [c0, c1) of the agent's n
   const int64_t per = (n + nblk - 1) / nblk;
   const int64_t c0 = (int64_t)rank * per, c1 = c0 + per < n ? c0 + per : n;
@@ -338,7 +321,7 @@ __global__ __launch_bounds__(kLrThreads) void k_lrts_train(
     // ---- B: this workgroup's exact partials -> global (parity buffer), agent barrier
     int64_t *pp = pbase + (size_t)(epoch & 1) * nblk * PW;
     lr_block_partials(s_acc, KD, lsum >> 24, lsum & kLo24, s_hi, s_lo, pp + (size_t)rank * PW);
-    agent_barrier(bar_count, bar_gen, nblk);
+    agcoop::agent_barrier(bar, rank, nblk);
     // ---- C: totals (identical in every workgroup), loss, Adam; scheduler on thread 0
     if (tid == 0) {
       int64_t h = 0, l = 0;
@@ -411,7 +394,7 @@ __global__ __launch_bounds__(kLrThreads) void k_lrts_train(
   __syncthreads();
   int64_t *pp = pbase + (size_t)(epoch & 1) * nblk * PW;
   lr_block_partials(s_acc, KD, 0, 0, s_hi, s_lo, pp + (size_t)rank * PW);
-  agent_barrier(bar_count, bar_gen, nblk);
+  agcoop::agent_barrier(bar, rank, nblk);
   if (rank == 0) {
     if (tid < KD) {
       const int c = tid;
@@ -430,7 +413,7 @@ __global__ __launch_bounds__(kLrThreads) void k_lrts_train(
 
 using TrainKernel = void (*)(int, const int32_t *, const int32_t *, const int32_t *, const int64_t *,
                              const int64_t *, const uint32_t *, const float *, int64_t, float *, float *,
-                             float *, const double *, int32_t *, float *, int64_t *, unsigned *);
+                             float *, const double *, int32_t *, float *, int64_t *, unsigned *, const int32_t *);
 
 TrainKernel pick_train(int Do) {
   switch (Do) {
@@ -598,8 +581,12 @@ int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *
       }
   }
   int64_t pwords = 0;
+  int lines = 0;
+  std::vector<int32_t> bar_off(N, 0);
   bool multi = false;
   for (int a = 0; a < N; ++a) {
+    bar_off[a] = lines;
+    lines += agcoop::bar_lines(nblk[a]);
     pbase[a] = pwords;
     pwords += 2 * (int64_t)nblk[a] * 2 * (K * Do + 1);
     multi |= nblk[a] > 1;
@@ -614,34 +601,37 @@ int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *
     if (multi && G > w.coop_blocks)
       return ag_set_error(AG_ERR_UNSUPPORTED, "ag_lrts_update: %d agents need more co-resident workgroups "
                                               "(%d) than the device holds (%d)", agents, G, w.coop_blocks);
-    if ((size_t)G > w.tab_cap || (size_t)pwords > w.part_cap) {
+    if ((size_t)G > w.tab_cap || (size_t)pwords > w.part_cap || (size_t)lines > w.bar_cap) {
       (void)hipFree(w.tables);
       (void)hipFree(w.partials);
       w.tables = nullptr;
       w.partials = nullptr;
       w.tab_cap = (size_t)G + 256;
       w.part_cap = (size_t)pwords + 4096;
-      hipError_t e2 = hipMalloc(&w.tables, sizeof(int64_t) * (w.tab_cap + 2 * (size_t)N) +
-                                               sizeof(unsigned) * 2 * (size_t)N);
+      w.bar_cap = (size_t)lines + 64;
+      hipError_t e2 = hipMalloc(&w.tables, sizeof(int64_t) * (w.tab_cap + 2 * (size_t)N) + sizeof(int32_t) * N +
+                                               sizeof(unsigned) * agcoop::kBarLineWords * w.bar_cap);
       if (e2 == hipSuccess) e2 = hipMalloc(&w.partials, sizeof(int64_t) * w.part_cap);
       if (e2 != hipSuccess) {
-        w.tab_cap = w.part_cap = 0;
+        w.tab_cap = w.part_cap = w.bar_cap = 0;
         return ag_set_error(AG_ERR_HIP, "ag_lrts_update: tables: %s", hipGetErrorString(e2));
       }
     }
     // tables: blk_agent [G] i32, blk_rank [G] i32, agent_nblk [N] i32, agent_pbase [N] i64,
-    // barriers [N][2] u32 (all inside w.tables)
+    // bar_off [N] i32, barrier lines [lines][32] u32 (all inside w.tables)
     char *tb = (char *)w.tables;
     int32_t *d_bagent = (int32_t *)tb;
     int32_t *d_brank = d_bagent + w.tab_cap;
     int32_t *d_nblk = d_brank + w.tab_cap;
     int64_t *d_pbase = (int64_t *)(d_nblk + 2 * (size_t)N);  // 8-B aligned (even count of i32 before)
-    unsigned *d_bar = (unsigned *)(d_pbase + N);
+    int32_t *d_baroff = (int32_t *)(d_pbase + N);
+    unsigned *d_bar = (unsigned *)(d_baroff + N);
     AG_HIP(hipMemcpyAsync(d_bagent, blk_agent.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
     AG_HIP(hipMemcpyAsync(d_brank, blk_rank.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
     AG_HIP(hipMemcpyAsync(d_nblk, nblk.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
     AG_HIP(hipMemcpyAsync(d_pbase, pbase.data(), sizeof(int64_t) * N, hipMemcpyHostToDevice, st));
-    AG_HIP(hipMemsetAsync(d_bar, 0, sizeof(unsigned) * 2 * N, st));
+    AG_HIP(hipMemcpyAsync(d_baroff, bar_off.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
+    if (lines) AG_HIP(hipMemsetAsync(d_bar, 0, sizeof(unsigned) * agcoop::kBarLineWords * lines, st));
     int Kv = K;
     const int32_t *cbagent = d_bagent, *cbrank = d_brank, *cnblk = d_nblk;
     const int64_t *cpbase = d_pbase, *coffsets = w.offsets;
@@ -654,8 +644,9 @@ int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *
     float *ctr = loss_trace;
     int64_t *cpart = w.partials;
     unsigned *cbar = d_bar;
+    const int32_t *cbaroff = d_baroff;
     void *args[] = {&Kv, &cbagent, &cbrank, &cnblk, &cpbase, &coffsets, &ckey, &cx, &ccap, &gm, &gq, &gpm,
-                    &ctab, &cep, &ctr, &cpart, &cbar};
+                    &ctab, &cep, &ctr, &cpart, &cbar, &cbaroff};
     if (multi)  // workgroups of one agent wait for each other: they must all be resident
       AG_HIP(hipLaunchCooperativeKernel((const void *)train, dim3(G), dim3(kLrThreads), args, (unsigned)lds, st));
     else
