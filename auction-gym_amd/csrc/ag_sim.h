@@ -19,6 +19,12 @@ namespace ag {
 #ifndef AG_PREFETCH
 #define AG_PREFETCH 0
 #endif
+#ifndef AG_GEN_MIN_WAVES
+#define AG_GEN_MIN_WAVES 3  // the general kernel: <= 168 VGPRs
+#endif
+#ifndef AG_TS_SCREEN
+#define AG_TS_SCREEN 1  // screened Thompson item choice (ts_select)
+#endif
 #ifndef AG_MIN_WAVES
 #define AG_MIN_WAVES 1
 #endif
@@ -390,13 +396,101 @@ __device__ __forceinline__ float ts_ctr_k(const float *w, const float (&x)[DW], 
   return 1.0f / (1.0f + e);
 }
 
+// float32 logit of item k: the products rounded separately and summed in order (ts_ctr_k's)
+template <int DW>
+__device__ __forceinline__ float ts_logit(const float *w, const float (&x)[DW], const float (&nzv)[DW], bool noisy,
+                                          int Do) {
+  float z = 0.0f;
+#pragma unroll
+  for (int d = 0; d < DW; ++d) {
+    if (d < Do) {
+      const float wd = noisy ? w[d] + nzv[d] : w[d];
+      const float t = wd * x[d];
+      z = d == 0 ? t : z + t;
+    }
+  }
+  return z;
+}
+__device__ __forceinline__ float ts_ctr_of(float z, const uint64_t *tab) {
+  const float e = (float)agexp::exp(-(double)z, tab);
+  return 1.0f / (1.0f + e);
+}
+
 // Thompson-sampling item choice of an LR-TS agent (src/Agent.py:29-42): first argmax of
 // sampled CTR * value. The noise of kTsGroup items is loaded together (one memory latency
 // per group instead of one per item), then the group is scored.
+//
+// Screened (K <= kTsScreenK): every item's logit is exact (float32, as ts_ctr's), its score
+// first estimated with the hardware exp2 / reciprocal -- relative error < 2^-16 for |z| <
+// 64 and value > 0 (argument rounding |z| log2 e 2^-23 <= 2^-16.5, v_exp_f32 / v_rcp_f32
+// 1 ulp each, float value and product 2^-24 each) -- then only the items within 2^-13 of
+// the best estimate (and any item outside those bounds) are scored exactly, in increasing
+// k: the exact first argmax is always among them (its estimate is >= best * (1 - 2^-15)),
+// so the choice is the plain loop's bit for bit.
 constexpr int kTsGroup = 4;
+constexpr int kTsScreenK = 12;
 template <int DW>
 __device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], const float *nz, int K, int Do,
                                          const double *vals, const uint64_t *tab) {
+  if (AG_TS_SCREEN && K <= kTsScreenK) {
+    float zk[kTsScreenK], ek[kTsScreenK];  // logits; score estimates (-1: score exactly)
+    float best_est = 0.0f;
+#pragma unroll
+    for (int k0 = 0; k0 < kTsScreenK; k0 += kTsGroup) {
+      if (k0 < K) {
+        float nzv[kTsGroup][DW];
+#pragma unroll
+        for (int g = 0; g < kTsGroup; ++g)
+#pragma unroll
+          for (int d = 0; d < DW; ++d)
+            nzv[g][d] = (nz && k0 + g < K && d < Do) ? nz[(size_t)((k0 + g) * Do + d) * 64] : 0.0f;
+#pragma unroll
+        for (int g = 0; g < kTsGroup; ++g) {
+          const int k = k0 + g;
+          zk[k] = 0.0f;
+          ek[k] = -1.0f;
+          if (k < K) {
+            const float z = ts_logit<DW>(m + k * Do, xo, nzv[g], nz != nullptr, Do);
+            const float v = (float)vals[k];
+            const bool ok = __builtin_fabsf(z) < 64.0f && v > 0.0f;
+            const float e = __builtin_amdgcn_exp2f(-z * 1.44269504f);
+            const float est = ok ? __builtin_amdgcn_rcpf(1.0f + e) * v : -1.0f;
+            zk[k] = z;
+            ek[k] = est;
+            best_est = est > best_est ? est : best_est;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int g = 0; g < kTsGroup; ++g) {
+          zk[k0 + g] = 0.0f;
+          ek[k0 + g] = -1.0f;
+        }
+      }
+    }
+    const float thr = best_est * (1.0f - 0x1p-13f);
+    uint32_t cand = 0;
+#pragma unroll
+    for (int k = 0; k < kTsScreenK; ++k)
+      if (k < K && (ek[k] < 0.0f || ek[k] >= thr)) cand |= 1u << k;
+    // exact scores of the candidates in increasing k (one exp in the code: a loop over the
+    // mask, the logit picked out of the register row by selects)
+    double best_sc = 0.0;
+    int best = -1;
+    while (cand) {
+      const int k = __builtin_ctz(cand);
+      cand &= cand - 1;
+      float z = zk[0];
+#pragma unroll
+      for (int kk = 1; kk < kTsScreenK; ++kk) z = k == kk ? zk[kk] : z;
+      const double sc = (double)ts_ctr_of(z, tab) * vals[k];
+      if (best < 0 || sc > best_sc) {
+        best_sc = sc;
+        best = k;
+      }
+    }
+    return best;
+  }
   double best_sc = 0.0;
   int best = 0;
   for (int k0 = 0; k0 < K; k0 += kTsGroup) {
@@ -575,7 +669,7 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
 }
 
 template <int P, int D, bool PRUNE, int W, bool GENERAL>
-__global__ __launch_bounds__(kThreads, AG_MIN_WAVES) void k_simulate(SimParams prm) {
+__global__ __launch_bounds__(kThreads, GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES) void k_simulate(SimParams prm) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = prm.N, K = prm.K;
   const uint32_t B = (uint32_t)prm.B;  // SoA leading dimension (auctions in the batch)

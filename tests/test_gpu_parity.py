@@ -449,6 +449,57 @@ def test_mixed_population_full_size(gpu, oracle):
     eng.close()
 
 
+@pytest.mark.parametrize("case", ["ties", "large_logits", "tiny_values"])
+def test_thompson_screen_adversarial(gpu, oracle, case):
+    """The screened Thompson item choice (hardware exp2 / rcp estimates, exact scores of the
+    near-best items) against the oracle's plain loop: exactly tied items (duplicate model rows
+    and values, noise ~1e-15 so the tie survives: first argmax), values 1 ulp apart, logits
+    beyond the screen's |z| < 64 bound, and values spanning 1e-30..1e30."""
+    import torch
+    from auctiongym_amd.engine import AuctionEngine
+    N, P, K, E, OE, B = 8, 2, 12, 5, 4, 1 << 18
+    g = np.random.default_rng(31)
+    items = np.concatenate([g.normal(0, 1, (N, K, E)), -3.0 - g.random((N, K, 1))], axis=2)
+    values = g.lognormal(0.1, 0.2, (N, K))
+    m = g.normal(0, 1, (N, K, OE + 1)).astype(np.float32)
+    q = np.ones_like(m)
+    if case == "ties":
+        m[:, 5] = m[:, 2]; values[:, 5] = values[:, 2]
+        m[:, 7] = m[:, 1]; values[:, 7] = np.nextafter(values[:, 1], 10)
+        m[:, 9] = m[:, 3]; values[:, 9] = np.nextafter(values[:, 3], -10)
+        q[:] = 1e30
+    elif case == "large_logits":
+        m *= 40.0
+    else:
+        values = values * 10.0 ** g.integers(-30, 31, (N, K))
+    eng = AuctionEngine(N, P, K, E, OE, 1, 1.0)
+    eng.set_agent_params(np.ones(N, np.int32), np.zeros(N, np.int32))
+    eng.load_catalog(items, values)
+    eng.load_lrts(m, q, thompson_sampling=True)
+    inp = eng.alloc_inputs(B)
+    eng.generate(3, 0, inp)
+    eng.generate_noise(3, 0, inp)
+    out = eng.alloc_outputs(B)
+    cnt = eng.new_counters()
+    eng.simulate(inp, out, cnt)
+    torch.cuda.synchronize()
+    ctx = np.ascontiguousarray(inp["ctx"].cpu().numpy().T)
+    part = np.ascontiguousarray(inp["part"].cpu().numpy().T)
+    u = inp["u"].cpu().numpy()
+    tn = eng.untile_ts_noise(inp["ts_noise"], B).reshape(B, P, K, OE + 1)
+    orc = oracle.simulate_pop(1, items, values, ctx, part, u, np.ones(N, np.int32), np.zeros(N, np.int32),
+                              np.ones(N), np.full(N, 0.02), OE=OE, ts_m=m, ts_noise=tn, nthreads=16)
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    for k in ("item", "bid", "est_ctr", "true_ctr", "best_ev"):
+        assert np.array_equal(np.ascontiguousarray(got[k].T), orc[k], equal_nan=True), k
+    for k in ("winner", "price", "second_price", "outcome"):
+        assert np.array_equal(got[k], orc[k], equal_nan=True), k
+    assert np.array_equal(cnt.cpu().numpy(), orc["counters_fx"])
+    if case == "ties":  # the tie is real: item 5 never beats item 2 for the same draw
+        assert (got["item"] != 5).any()
+    eng.close()
+
+
 def test_fitted_policy_bids_match_oracle(gpu, oracle):
     """Learning bidders bidding from a fitted policy (src/Bidder.py:198-203 ValueLearningBidder
     'policy', :358-362 PolicyLearningBidder, :466-470 DoublyRobustBidder): the gamma is the
