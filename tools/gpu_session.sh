@@ -25,5 +25,10 @@ nproc > "$OUT/host.txt"; lscpu | grep "Model name" >> "$OUT/host.txt"
 run smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
 run pytest_gpu 900 python -u -m pytest tests -v -m gpu -x --timeout 300 --timeout-method thread
 run bench 600 python bench.py
-run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline
+# last: rocprofv3 7.2 crashes in its exit handler after a cooperative launch (the learner
+# updates), after writing its results -- tools/gpu_round.sh skips this and profiles in
+# tools/collect_profiles.sh instead (PMC passes first, that command last)
+if [ -z "${NO_ROCPROF:-}" ]; then
+  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline
+fi
 echo "== done" | tee -a "$OUT/session.log"
