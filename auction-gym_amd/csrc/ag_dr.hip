@@ -43,6 +43,9 @@ constexpr int64_t kLo24 = (int64_t(1) << 24) - 1;
 // (int64)rint(v * 2^40). For |v * 2^40| < 2^51 (every term in practice) adding 1.5 * 2^52
 // rounds to the integer (nearest, ties to even, as rint) and leaves it in the low mantissa
 // bits: 1 add + 1 integer subtract instead of the long double -> int64 conversion.
+__device__ __forceinline__ int64_t fxr_fast(double v) {  // |v| <= 2^10 guaranteed by the caller
+  return (int64_t)(agexp::asu64(v * kGrid + 0x1.8p52) - agexp::asu64(0x1.8p52));
+}
 __device__ __forceinline__ int64_t fxr(double v) {
   const double x = v * kGrid;
   if (__builtin_expect(__builtin_fabs(x) < 0x1p51, 1))
@@ -58,8 +61,25 @@ __device__ __forceinline__ double fxv(int64_t hi, int64_t lo) {
 
 // softplus(u) = u > 20 ? u : log1p(exp(u)) and its derivative exp(u) / (exp(u) + 1), from
 // e = exp(u) (the forward pass keeps it for the backward pass)
-__device__ __forceinline__ double softplus_e(double u, double e) { return u > 20.0 ? u : aglog1p::log1p(e); }
 __device__ __forceinline__ double dsoftplus_e(double u, double e) { return u > 20.0 ? 1.0 : e / (e + 1.0); }
+// exp(x) and softplus from the branch-free main paths (the same bits), the rare inputs
+// outside them patched with the full functions
+__device__ __forceinline__ double exp_fast(double x, const uint64_t *tab) {
+  double e = agexp::exp_main(x, tab);
+  if (__builtin_expect(!agexp::exp_in_main(x), 0)) e = agexp::exp(x, tab);
+  return e;
+}
+// e = exp(u); returns softplus(u)
+__device__ __forceinline__ double softplus_fast(double u, double &e, const uint64_t *tab) {
+  e = agexp::exp_main(u, tab);
+  bool lok;
+  double l = aglog1p::log1p_main(e, lok);
+  if (__builtin_expect(!(agexp::exp_in_main(u) && (lok || u > 20.0)), 0)) {
+    e = agexp::exp(u, tab);
+    l = aglog1p::log1p(e);
+  }
+  return u > 20.0 ? u : l;
+}
 
 // Exact block sum of NV per-lane int64 accumulators (each split at bit 24 so nothing can
 // overflow): every thread gets the totals as (hi, lo) pairs in s_out.
@@ -144,15 +164,12 @@ __device__ __forceinline__ void policy_fwd(const float *p, double c, double v, P
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     f.h[j] = c * (double)p[2 * j] + v * (double)p[2 * j + 1] + (double)p[4 + j];
-    f.eh[j] = agexp::exp(f.h[j], tab);
-    f.s[j] = softplus_e(f.h[j], f.eh[j]);
+    f.s[j] = softplus_fast(f.h[j], f.eh[j], tab);
   }
   f.am = f.s[0] * (double)p[6] + f.s[1] * (double)p[7] + (double)p[8];
   f.as = f.s[0] * (double)p[9] + f.s[1] * (double)p[10] + (double)p[11];
-  f.eam = agexp::exp(f.am, tab);
-  f.eas = agexp::exp(f.as, tab);
-  f.mu = softplus_e(f.am, f.eam);
-  f.sp_sigma = softplus_e(f.as, f.eas);
+  f.mu = softplus_fast(f.am, f.eam, tab);
+  f.sp_sigma = softplus_fast(f.as, f.eas, tab);
   f.sigma = f.sp_sigma + 0.01;  // min_sigma (src/Models.py:104)
 }
 __device__ __forceinline__ void policy_bwd(const float *p, double c, double v, const PolF &f, double dmu,
@@ -368,19 +385,28 @@ __device__ int fit_winrate(const RecView &V, const Chunk &K, TrainLds &S, Coop &
     // one BCE row: its loss and gradient terms
     auto row = [&](double c, double v, double g, double y) {
       const double z = c * w0 + v * w1 + g * w2 + w3;
-      // -log(p) = softplus(-z) for a win, -log(1 - p) = softplus(z) otherwise: one exp(+-z)
-      // besides the sigmoid's exp(-z), one log1p
-      const double em = agexp::exp(-z, S.tab);
-      const double pw = 1.0 / (1.0 + em);
+      // -log(p) = softplus(-z) for a win, -log(1 - p) = softplus(z) otherwise. Branch-free
+      // main paths of exp(-z), exp(z) and log1p (the same bits), the rare inputs outside
+      // them patched with the full functions afterwards
+      double em = agexp::exp_main(-z, S.tab), ep = agexp::exp_main(z, S.tab);
       const double u = y > 0.0 ? -z : z;
-      const double eu = y > 0.0 ? em : agexp::exp(z, S.tab);
-      const double t = fmin(softplus_e(u, eu), 100.0);
-      acc[0] += fxr(t);
+      double eu = y > 0.0 ? em : ep;
+      bool lok;
+      double l = aglog1p::log1p_main(eu, lok);
+      if (__builtin_expect(!(agexp::exp_in_main(z) && (lok || u > 20.0)), 0)) {
+        em = agexp::exp(-z, S.tab);
+        eu = y > 0.0 ? em : agexp::exp(z, S.tab);
+        l = aglog1p::log1p(eu);
+      }
+      const double pw = 1.0 / (1.0 + em);
+      const double t = fmin(u > 20.0 ? u : l, 100.0);
+      // |t| <= 100, |pw - y| <= 1, ctr in [0, 1]: these terms are far inside fxr's fast range
+      acc[0] += fxr_fast(t);
       const double gz = pw - y;
-      acc[1] += fxr(gz * c);
+      acc[1] += fxr_fast(gz * c);
       acc[2] += fxr(gz * v);
       acc[3] += fxr(gz * g);
-      acc[4] += fxr(gz);
+      acc[4] += fxr_fast(gz);
     };
     // record j's logged row and its gamma = 0, y = 0 augmentation row together (two
     // independent chains for the scheduler; the sums are exact, so any order)
@@ -463,7 +489,7 @@ __device__ int fit_dr(const RecView &V, const Chunk &K, TrainLds &S, Coop &C,
       policy_fwd(S.pol, c, v, f, S.tab);
       const double mu = f.mu, sg = f.sigma;
       const double zz = (mu - g) / sg;
-      const double pdf_raw = agexp::exp(-(zz * zz) / 2.0, S.tab) / sg * inv_sqrt2pi;
+      const double pdf_raw = exp_fast(-(zz * zz) / 2.0, S.tab) / sg * inv_sqrt2pi;
       const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
       const double p0 = (double)fmaxf(V.prop(j), 1e-15f);
       const double iw = pi / p0;
@@ -473,7 +499,7 @@ __device__ int fit_dr(const RecView &V, const Chunk &K, TrainLds &S, Coop &C,
       const double raw = mu + sg * ep;
       const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
       const double zw = c * (double)S.wr[0] + v * (double)S.wr[1] + gs * (double)S.wr[2] + (double)S.wr[3];
-      const double Wv = 1.0 / (1.0 + agexp::exp(-zw, S.tab));
+      const double Wv = 1.0 / (1.0 + exp_fast(-zw, S.tab));
       const double V = c * v;
       acc[12] += fxr(-(du * iwc + Wv * (V - V * gs)));
       double dpi_dmu = 0.0, dpi_dsg = 0.0;
@@ -527,7 +553,7 @@ __device__ int fit_dm(const RecView &V, const Chunk &K, TrainLds &S, Coop &C, co
       const double raw = f.mu + f.sigma * ep;
       const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
       const double zw = c * (double)S.wr[0] + v * (double)S.wr[1] + gs * (double)S.wr[2] + (double)S.wr[3];
-      const double Wv = 1.0 / (1.0 + agexp::exp(-zw, S.tab));
+      const double Wv = 1.0 / (1.0 + exp_fast(-zw, S.tab));
       const double V = c * v;
       acc[12] += fxr(-(Wv * (V - V * gs)));
       double ddm = 0.0;
@@ -594,7 +620,7 @@ __device__ int fit_pl(const RecView &V, const Chunk &K, TrainLds &S, Coop &C, in
       policy_fwd(S.pol, c, v, f, S.tab);
       const double mu = f.mu, sg = f.sigma;
       const double zz = (mu - g) / sg;
-      const double pdf_raw = agexp::exp(-(zz * zz) / 2.0, S.tab) / sg * inv_sqrt2pi;
+      const double pdf_raw = exp_fast(-(zz * zz) / 2.0, S.tab) / sg * inv_sqrt2pi;
       const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
       const double p0 = (double)fmaxf(V.prop(j), 1e-15f);
       const double u = V.util(j);

@@ -97,6 +97,29 @@ AG_HD double exp(double x, const uint64_t *tab) {
   return fma(scale, tmp, scale);
 }
 
+// The main path of exp above alone, without its range checks: equal to exp(x) whenever
+// exp_in_main(x) (2^-54 <= |x| < 512, where exp takes exactly this path). Branch-free, so
+// independent calls interleave; callers patch the rare other inputs with exp().
+AG_HD bool exp_in_main(double x) {
+  const uint32_t abstop = (uint32_t)(asu64(x) >> 52) & 0x7ff;
+  return abstop - 0x3c9u < 0x408u - 0x3c9u;
+}
+AG_HD double exp_main(double x, const uint64_t *tab) {
+  double z = kInvLn2N * x;
+  double kd = z + kShift;
+  uint64_t ki = asu64(kd);
+  kd -= kShift;
+  double r = fma(kd, kNegLn2LoN, fma(kd, kNegLn2HiN, x));
+  uint64_t idx = 2 * (ki & 127);
+  uint64_t top = ki << 45;
+  double tail = asf64(tab[idx]);
+  uint64_t sbits = tab[idx + 1] + top;
+  double r2 = r * r;
+  double tmp = fma(r2 * r2, fma(r, kC5, kC4), fma(r2, fma(r, kC3, kC2), tail + r));
+  double scale = asf64(sbits);
+  return fma(scale, tmp, scale);
+}
+
 // src/Models.py:10-12  sigmoid(x) = 1.0 / (1.0 + np.exp(-x))  (IEEE division).
 AG_HD double sigmoid(double z, const uint64_t *tab) { return 1.0 / (1.0 + exp(-z, tab)); }
 

@@ -94,4 +94,42 @@ AG_L1P_HD double log1p(double x) {
   return k * ln2_hi - ((hfsq - (s * (hfsq + R) + (k * ln2_lo + c))) - f);
 }
 
+// log1p(x) for 2^-29 <= x < 2^53 without branches: both of log1p's paths for a positive x
+// (f = x, k = 0 below sqrt(2) - 1; 1 + x = 2^k (1 + f) with the rounding correction c
+// above) computed and selected, then the shared tail -- for k = 0 the general tail
+// k ln2_hi - ((hfsq - (s (hfsq + R) + (k ln2_lo + c))) - f) equals f - (hfsq - s (hfsq + R))
+// bit for bit (IEEE subtraction is antisymmetric, adding +0 is exact). ok = false outside
+// that range and on log1p's hu == 0 special case (f on a power-of-two boundary): the caller
+// then takes log1p(x).
+AG_L1P_HD double log1p_main(double x, bool &ok) {
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double Lp1 = 6.666666666666735130e-01, Lp2 = 3.999999999940941908e-01,
+               Lp3 = 2.857142874366239149e-01, Lp4 = 2.222219843214978396e-01,
+               Lp5 = 1.818357216161805012e-01, Lp6 = 1.531383769920937332e-01,
+               Lp7 = 1.479819860511658591e-01;
+  const int32_t hx = (int32_t)(bits(x) >> 32);
+  const bool small = hx < 0x3FDA827A;  // k = 0: f = x
+  double u = 1.0 + x;
+  int32_t hu = (int32_t)(bits(u) >> 32);
+  int32_t k = (hu >> 20) - 1023;
+  double c = (k > 0) ? 1.0 - (u - x) : x - (u - 1.0);
+  c /= u;
+  hu &= 0x000fffff;
+  const uint64_t lo = bits(u) & 0xffffffffull;
+  const bool low = hu < 0x6a09e;
+  u = from_bits(((uint64_t)(uint32_t)(hu | (low ? 0x3ff00000 : 0x3fe00000)) << 32) | lo);
+  k += low ? 0 : 1;
+  hu = low ? hu : (0x00100000 - hu) >> 2;
+  double f = u - 1.0;
+  f = small ? x : f;
+  k = small ? 0 : k;
+  c = small ? 0.0 : c;
+  hu = small ? 1 : hu;
+  ok = hx >= 0x3e200000 && hx < 0x43400000 && hu != 0;
+  const double hfsq = 0.5 * f * f;
+  const double s = f / (2.0 + f), z = s * s;
+  const double R = z * (Lp1 + z * (Lp2 + z * (Lp3 + z * (Lp4 + z * (Lp5 + z * (Lp6 + z * Lp7))))));
+  return k * ln2_hi - ((hfsq - (s * (hfsq + R) + (k * ln2_lo + c))) - f);
+}
+
 }  // namespace aglog1p

@@ -66,3 +66,57 @@ def test_log1p_restatement_accuracy():
         if a != b:
             worst = max(worst, abs(a - b) / abs(b))
     assert worst < 2.3e-16
+
+
+MAIN_SRC = r'''
+#include <stdio.h>
+#include <stdlib.h>
+#include <math.h>
+#include "ag_exp.h"
+#include "ag_exp_table.h"
+#include "ag_log1p.h"
+static unsigned long long s = 88172645463325252ull;
+static inline unsigned long long xr(void) { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; }
+int main(int argc, char **argv) {
+  long n = atol(argv[1]), ebad = 0, lbad = 0, eok = 0, lok = 0;
+  for (long i = 0; i < n; ++i) {
+    double x; int m = i % 6;
+    if (m == 0) x = (double)(xr() >> 11) * 0x1p-53 * 100 - 50;
+    else if (m == 1) x = (double)(xr() >> 11) * 0x1p-53 * 1460 - 750;
+    else if (m == 2) x = (double)(xr() >> 11) * 0x1p-53 * 16 - 8;
+    else if (m == 3) x = ldexp((double)(xr() >> 11) * 0x1p-53 + 0.5, (int)(xr() % 120) - 60);
+    else if (m == 4) x = (double)(xr() >> 11) * 0x1p-53 * 3;
+    else { unsigned long long u = xr(); __builtin_memcpy(&x, &u, 8); }
+    if (x != x) continue;
+    if (agexp::exp_in_main(x)) {
+      ++eok;
+      double a = agexp::exp(x, ag_exp_tab), b = agexp::exp_main(x, ag_exp_tab);
+      if (__builtin_memcmp(&a, &b, 8)) { if (ebad < 5) printf("exp x=%a %a %a\n", x, a, b); ebad++; }
+    }
+    double y = fabs(x);
+    bool ok;
+    double lb = aglog1p::log1p_main(y, ok);
+    if (ok) {
+      ++lok;
+      double la = aglog1p::log1p(y);
+      if (__builtin_memcmp(&la, &lb, 8)) { if (lbad < 5) printf("log1p x=%a %a %a\n", y, la, lb); lbad++; }
+    }
+  }
+  printf("exp bad %ld of %ld; log1p bad %ld of %ld\n", ebad, eok, lbad, lok);
+  return ebad || lbad;
+}
+'''
+
+
+def test_branch_free_main_paths_match(tmp_path):
+    """agexp::exp_main / aglog1p::log1p_main (the trainer's branch-free fast paths) equal
+    agexp::exp / aglog1p::log1p bit for bit wherever they report themselves valid, over
+    3e7 inputs (whole double range, the softplus range, powers of two 2^-60..2^60)."""
+    c = tmp_path / "m.cpp"
+    c.write_text(MAIN_SRC)
+    exe = tmp_path / "m"
+    inc = os.path.join(ROOT, "auction-gym_amd", "csrc")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", inc, str(c), "-o", str(exe),
+                    "-lm"], check=True)
+    r = subprocess.run([str(exe), "30000000"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout
