@@ -64,11 +64,7 @@ __device__ __forceinline__ double fxv(int64_t hi, int64_t lo) {
 __device__ __forceinline__ double dsoftplus_e(double u, double e) { return u > 20.0 ? 1.0 : e / (e + 1.0); }
 // exp(x) and softplus from the branch-free main paths (the same bits), the rare inputs
 // outside them patched with the full functions
-__device__ __forceinline__ double exp_fast(double x, const uint64_t *tab) {
-  double e = agexp::exp_main(x, tab);
-  if (__builtin_expect(!agexp::exp_in_main(x), 0)) e = agexp::exp(x, tab);
-  return e;
-}
+using agexp::exp_fast;
 // e = exp(u); returns softplus(u)
 __device__ __forceinline__ double softplus_fast(double u, double &e, const uint64_t *tab) {
   e = agexp::exp_main(u, tab);

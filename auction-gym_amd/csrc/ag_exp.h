@@ -120,7 +120,23 @@ AG_HD double exp_main(double x, const uint64_t *tab) {
   return fma(scale, tmp, scale);
 }
 
+// exp(x) through the branch-free main path, the inputs outside it patched with exp(): the
+// same bits as exp(), cheaper in divergent code (AG_EXP_FAST=0: plain exp, for A/B).
+#ifndef AG_EXP_FAST
+#define AG_EXP_FAST 1
+#endif
+AG_HD double exp_fast(double x, const uint64_t *tab) {
+#if AG_EXP_FAST
+  double e = exp_main(x, tab);
+  if (__builtin_expect(!exp_in_main(x), 0)) e = exp(x, tab);
+  return e;
+#else
+  return exp(x, tab);
+#endif
+}
+
 // src/Models.py:10-12  sigmoid(x) = 1.0 / (1.0 + np.exp(-x))  (IEEE division).
 AG_HD double sigmoid(double z, const uint64_t *tab) { return 1.0 / (1.0 + exp(-z, tab)); }
+AG_HD double sigmoid_fast(double z, const uint64_t *tab) { return 1.0 / (1.0 + exp_fast(-z, tab)); }
 
 }  // namespace agexp

@@ -219,7 +219,7 @@ __device__ __forceinline__ int select_item(const double *__restrict__ itm, const
   int best = -1;
   double best_s = 0.0, best_c = 0.0;
   auto exact = [&](int k) {
-    const double c = agexp::sigmoid(dot_ref<D>(itm + k * D, x), tab);
+    const double c = agexp::sigmoid_fast(dot_ref<D>(itm + k * D, x), tab);
     const double sc = c * vv[k];
     if (best < 0 || sc > best_s || (sc == best_s && k < best)) {
       best = k;
@@ -373,7 +373,7 @@ __device__ __forceinline__ float ts_ctr(const float *w, const float *x, int Do, 
     const float t = wd * x[d];
     z = d == 0 ? t : z + t;
   }
-  const float e = (float)agexp::exp(-(double)z, tab);
+  const float e = (float)agexp::exp_fast(-(double)z, tab);
   return 1.0f / (1.0f + e);
 }
 
@@ -392,7 +392,7 @@ __device__ __forceinline__ float ts_ctr_k(const float *w, const float (&x)[DW], 
       z = d == 0 ? t : z + t;
     }
   }
-  const float e = (float)agexp::exp(-(double)z, tab);
+  const float e = (float)agexp::exp_fast(-(double)z, tab);
   return 1.0f / (1.0f + e);
 }
 
@@ -412,7 +412,7 @@ __device__ __forceinline__ float ts_logit(const float *w, const float (&x)[DW], 
   return z;
 }
 __device__ __forceinline__ float ts_ctr_of(float z, const uint64_t *tab) {
-  const float e = (float)agexp::exp(-(double)z, tab);
+  const float e = (float)agexp::exp_fast(-(double)z, tab);
   return 1.0f / (1.0f + e);
 }
 
@@ -523,7 +523,10 @@ __device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], 
 // (softplus = log1p(exp), the restated log1p), mu / sigma rounded to float32, the rsample
 // mu + sigma * eps in float32, exp(log_prob) rounded to float32, gamma = clip(sample, 0, 1).
 __device__ __forceinline__ double policy_softplus(double u, const uint64_t *tab) {
-  return u > 20.0 ? u : aglog1p::log1p(agexp::exp(u, tab));
+  const double e = agexp::exp_fast(u, tab);
+  bool lok;
+  const double l = aglog1p::log1p_main(e, lok);
+  return u > 20.0 ? u : (__builtin_expect(lok, 1) ? l : aglog1p::log1p(e));
 }
 __device__ __forceinline__ void policy_bid(const float *p, double ctr, double value, float eps,
                                            const uint64_t *tab, double &gamma, double &prop) {
@@ -538,7 +541,7 @@ __device__ __forceinline__ void policy_bid(const float *p, double ctr, double va
   const float raw = mu + sg * eps;
   const double z = ((double)raw - (double)mu) / (double)sg;
   const double logp = -(z * z) / 2.0 - aglog1p::log1p((double)sg - 1.0) - 0.91893853320467274178;
-  prop = (double)(float)agexp::exp(logp, tab);
+  prop = (double)(float)agexp::exp_fast(logp, tab);
   gamma = raw < 0.0f ? 0.0 : (raw > 1.0f ? 1.0 : (double)raw);
 }
 
@@ -559,7 +562,7 @@ __device__ __forceinline__ double search_gamma(const float *wr, double ctr, doub
   for (int j = 0; j < 128; ++j) {
     const double g = grid[(size_t)j * stride];
     const float z = cv + (float)g * wr[2] + wr[3];
-    const float pw = (float)(1.0 / (1.0 + agexp::exp(-(double)z, tab)));
+    const float pw = (float)(1.0 / (1.0 + agexp::exp_fast(-(double)z, tab)));
     const double ut = (double)pw * (ev - ev * g);
     if (ut > best_u || (ut == best_u && g < best_g)) {
       best_u = ut;
@@ -573,7 +576,7 @@ __device__ __forceinline__ double search_gamma(const float *wr, double ctr, doub
 __device__ __forceinline__ double shading_propensity(double pg, double sigma, double g,
                                                      const uint64_t *tab) {
   const double t = (pg - g) / sigma;
-  return agexp::exp(-(t * t) / 2.0, tab) / (sigma * 2.5066282746310002);  // sqrt(2 pi)
+  return agexp::exp_fast(-(t * t) / 2.0, tab) / (sigma * 2.5066282746310002);  // sqrt(2 pi)
 }
 
 template <int P, int D, bool PRUNE, bool GENERAL>
@@ -614,7 +617,7 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
         for (int d = 0; d < D; ++d) xo[d] = d < Do - 1 ? (float)x[d] : (d == Do - 1 ? 1.0f : 0.0f);
         best = ts_select<D>(m, xo, nz, K, Do, T.vals + a * T.values_stride, T.tab);
         est = (double)ts_ctr_k<D>(m + best * Do, xo, xo, false, Do, T.tab);
-        tru = best == best_t ? c : agexp::sigmoid(dot_ref<D>(itm + best * D, x), T.tab);
+        tru = best == best_t ? c : agexp::sigmoid_fast(dot_ref<D>(itm + best * D, x), T.tab);
       }
     }
     const double v = T.vals[a * T.values_stride + best];
