@@ -186,7 +186,7 @@ template <int DO>
 __device__ __forceinline__ int64_t lr_epoch_sample(const LrSample &s, const float *__restrict__ sm,
                                                    int64_t *__restrict__ acc, const uint64_t *tab) {
   const float z = lr_logit<DO>(sm + s.item * DO, s.x);
-  const float p = 1.0f / (1.0f + (float)agexp::exp(-(double)z, tab));
+  const float p = 1.0f / (1.0f + (float)agexp::exp_fast(-(double)z, tab));
   const double t = s.y ? -fmax(log((double)p), -100.0) : -fmax(log1p(-(double)p), -100.0);
   const double gz = (double)p - (double)s.y;
 #pragma unroll
@@ -198,7 +198,7 @@ template <int DO>
 __device__ __forceinline__ void lr_laplace_sample(const LrSample &s, const float *__restrict__ sm,
                                                   int64_t *__restrict__ acc, const uint64_t *tab) {
   const float z = lr_logit<DO>(sm + s.item * DO, s.x);
-  const float P = 1.0f / (1.0f + (float)agexp::exp((double)(1.0f - z), tab));
+  const float P = 1.0f / (1.0f + (float)agexp::exp_fast((double)(1.0f - z), tab));
   const float w = P * (1.0f - P);
 #pragma unroll
   for (int d = 0; d < DO; ++d)
