@@ -349,8 +349,9 @@ int ag_dr_update(ag_ctx *ctx, const ag_shading_samples *samples, const float *no
  * (src/Bidder.py:159-167, :339-346). Defaults: 'search', 'PPO'. */
 int ag_set_bidder_modes(ag_ctx *ctx, const int32_t *modes);
 
-/* Agent.update -> Bidder.update of EVERY learning bidder from the store, one workgroup per
- * agent running its fits in the reference's order (src/Agent.py:79-94):
+/* Agent.update -> Bidder.update of EVERY learning bidder from the store, each agent on one
+ * or more cooperating workgroups (AG_OPT_BIDDER_BLOCK_SAMPLES) running its fits in the
+ * reference's order (src/Agent.py:79-94), in two launches (win-rate fits, then the rest):
  *  - DoublyRobustBidder (src/Bidder.py:473-615): as ag_dr_update;
  *  - ValueLearningBidder (:204-325): no won record -> the reference's fallback (nothing
  *    trained, status 1, bids revert to Gaussian shading); else the win-rate fit and, with
