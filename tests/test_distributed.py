@@ -124,3 +124,56 @@ def test_lrts_update_on_gathered_samples_is_rank_independent(tmp_path, oracle, w
     want = np.concatenate([m.ravel(), q.ravel(), [ep]])
     for g in got:
         assert np.array_equal(g, want)
+
+
+def _bidder_worker(rank, world, port, out_path):
+    import sys
+    for p in (os.path.join(ROOT, "auction-gym_amd"), os.path.join(ROOT, "oracle")):
+        sys.path.insert(0, p)
+    import oracle as O
+    from auctiongym_amd.sharding import gather_records, shard_range
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    kat = np.load(os.path.join(ROOT, "tests", "golden", "dm_update_kat.npz"))
+    k = lambda s: kat[f"a2_{s}"]  # noqa: E731
+    n = len(k("est_ctr"))
+    lo, hi = shard_range(n, rank, world)  # this rank's auctions' records, in log order
+    cap = hi - lo + 5
+    st = {"agent": torch.zeros(cap, dtype=torch.int32), "order": torch.zeros(cap, dtype=torch.int64)}
+    for f in ("gamma", "utility", "ctr", "value", "propensity"):
+        st[f] = torch.zeros(cap, dtype=torch.float64)
+    st["won"] = torch.zeros(cap, dtype=torch.uint8)
+    st["count"] = torch.tensor([hi - lo], dtype=torch.int64)
+    for f, v in (("gamma", k("gamma")), ("utility", k("util")), ("ctr", k("est_ctr")), ("value", k("value")),
+                 ("propensity", k("propensity")), ("won", k("won").astype(np.uint8)),
+                 ("order", np.arange(n, dtype=np.int64))):
+        st[f][:hi - lo] = torch.from_numpy(np.ascontiguousarray(v[lo:hi]))
+    g = gather_records(st)
+    m = int(g["count"][0])
+    idx = np.argsort(g["order"][:m].numpy(), kind="stable")  # the device's (agent, log order) sort
+    col = {f: g[f][:m].numpy()[idx] for f in ("ctr", "value", "gamma", "won")}
+    wr0 = np.concatenate([k("wr0_0").ravel(), k("wr0_1").ravel()])
+    pol0 = np.concatenate([k(f"pol0_{i}").ravel() for i in (0, 1, 4, 5, 8, 9)])
+    r = O.vl_update(col["ctr"], col["value"], col["gamma"], col["won"], wr0, pol0, False, None)
+    np.save(out_path + f".{rank}.npy", np.concatenate([r["wr"], r["epochs"].astype(np.float32)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bidder_update_on_gathered_records_is_rank_independent(tmp_path, oracle, world):
+    """Learning-bidder records (the store ag_bidder_update reads: ctr, value, gamma, won, log
+    order, ...) sharded by auction over ranks and all-gathered: restored to log order, every
+    rank fits the same ValueLearningBidder win-rate model, equal to one process on all the
+    reference's records (FP_DM_TS KAT agent 2)."""
+    out = str(tmp_path / "vl")
+    mp.spawn(_bidder_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    got = [np.load(out + f".{r}.npy") for r in range(world)]
+    kat = np.load(os.path.join(ROOT, "tests", "golden", "dm_update_kat.npz"))
+    k = lambda s: kat[f"a2_{s}"]  # noqa: E731
+    wr0 = np.concatenate([k("wr0_0").ravel(), k("wr0_1").ravel()])
+    pol0 = np.concatenate([k(f"pol0_{i}").ravel() for i in (0, 1, 4, 5, 8, 9)])
+    r = oracle.vl_update(k("est_ctr"), k("value"), k("gamma"), k("won"), wr0, pol0, False, None)
+    want = np.concatenate([r["wr"], r["epochs"].astype(np.float32)])
+    for g in got:
+        assert np.array_equal(g, want)
