@@ -319,15 +319,24 @@ struct FitNoise {
 
 __device__ __forceinline__ double fit_eps(const FitNoise &F, int e, int64_t i) {
   if (F.noise) return (double)F.noise[(int64_t)e * F.n + i];
-  for (uint32_t t = 0; t < 64; ++t) {
+  // the rejection loop only finds the first accepted (u, s); the transform runs once after
+  // it for every lane together (a wave's lanes accept at different attempts)
+  double u = 0.0, s = 0.0;
+  bool found = false;
+  for (uint32_t t = 0; t < 64 && !found; ++t) {
     uint32_t w[4];
     philox((uint32_t)i, (uint32_t)e, t, F.agent, (uint32_t)F.seed, (uint32_t)(F.seed >> 32), w);
-    const double u = (double)((((uint64_t)w[0] << 32) | w[1]) >> 11) * 0x1p-52 - 1.0;
-    const double v = (double)((((uint64_t)w[2] << 32) | w[3]) >> 11) * 0x1p-52 - 1.0;
-    const double s = u * u + v * v;
-    if (s > 0.0 && s < 1.0) return (double)(float)(u * __builtin_sqrt(-2.0 * aglog1p::log1p(s - 1.0) / s));
+    const double uu = (double)((((uint64_t)w[0] << 32) | w[1]) >> 11) * 0x1p-52 - 1.0;
+    const double vv = (double)((((uint64_t)w[2] << 32) | w[3]) >> 11) * 0x1p-52 - 1.0;
+    const double ss = uu * uu + vv * vv;
+    if (ss > 0.0 && ss < 1.0) {
+      u = uu;
+      s = ss;
+      found = true;
+    }
   }
-  return 0.0;
+  if (!found) return 0.0;
+  return (double)(float)(u * __builtin_sqrt(-2.0 * aglog1p::log1p(s - 1.0) / s));
 }
 
 // records of the workgroup: [c0, c0 + nb) of the agent's n
