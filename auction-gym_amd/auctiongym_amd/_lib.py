@@ -21,6 +21,8 @@ OPT_LANE_AUCTIONS = 1
 OPT_BIDDER_BLOCK_SAMPLES = 4
 OPT_FIT_NOISE_SEED = 5
 OPT_BIDDER_RECORD_CACHE = 6
+OPT_SIMULATE_KERNEL = 7
+SIM_KERNEL_AUTO, SIM_KERNEL_GENERIC = 0, 1
 ITEM_SEARCH_AUTO, ITEM_SEARCH_EXACT = 0, 1
 
 COUNTERS = ("net", "gross", "allocation_regret", "estimation_regret", "overbid_regret",
@@ -35,9 +37,9 @@ EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params
            "ag_generate_noise", "ag_lrts_collect", "ag_lrts_update", "ag_lrts_read",
            "ag_shading_collect", "ag_empirical_update", "ag_set_dr_state", "ag_get_dr_state",
            "ag_shading_counts", "ag_dr_update", "ag_set_bidder_modes", "ag_bidder_update",
-           "ag_generate_search_grid",
+           "ag_generate_search_grid", "ag_simulate_generated",
            "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_last_error", "ag_abi_version")
-ABI_VERSION = 14
+ABI_VERSION = 15
 LEARNER_UNINITIALISED, LEARNER_POLICY, LEARNER_SEARCH = 0, 1, 2
 VL_SEARCH, VL_POLICY = 0, 1
 PL_LOSSES = {"REINFORCE": 0, "REINFORCE_offpolicy": 1, "TRPO": 2, "PPO": 3}
@@ -53,27 +55,35 @@ class AgShape(ctypes.Structure):
                 ("embedding_var", ctypes.c_double)]
 
 
-class AgBatchIn(ctypes.Structure):
-    _fields_ = [("ctx", ctypes.c_void_p), ("part", ctypes.c_void_p), ("u", ctypes.c_void_p),
+class _Sized(ctypes.Structure):
+    """ABI structs passed by pointer start with struct_size = sizeof(struct) (ABI 15): set
+    here, so positional arguments start at the second field."""
+
+    def __init__(self, *args, **kw):
+        super().__init__(ctypes.sizeof(type(self)), *args, **kw)
+
+
+class AgBatchIn(_Sized):
+    _fields_ = [("struct_size", ctypes.c_uint64), ("ctx", ctypes.c_void_p), ("part", ctypes.c_void_p), ("u", ctypes.c_void_p),
                 ("gamma_raw", ctypes.c_void_p), ("ts_noise", ctypes.c_void_p),
                 ("policy_eps", ctypes.c_void_p), ("gamma_grid", ctypes.c_void_p)]
 
 
-class AgBatchOut(ctypes.Structure):
-    _fields_ = [("winner", ctypes.c_void_p), ("price", ctypes.c_void_p),
+class AgBatchOut(_Sized):
+    _fields_ = [("struct_size", ctypes.c_uint64), ("winner", ctypes.c_void_p), ("price", ctypes.c_void_p),
                 ("second_price", ctypes.c_void_p), ("outcome", ctypes.c_void_p),
                 ("item", ctypes.c_void_p), ("bid", ctypes.c_void_p), ("est_ctr", ctypes.c_void_p),
                 ("true_ctr", ctypes.c_void_p), ("best_ev", ctypes.c_void_p),
                 ("gamma", ctypes.c_void_p), ("propensity", ctypes.c_void_p)]
 
 
-class AgLrtsSamples(ctypes.Structure):
-    _fields_ = [("key", ctypes.c_void_p), ("x", ctypes.c_void_p), ("capacity", ctypes.c_int64),
+class AgLrtsSamples(_Sized):
+    _fields_ = [("struct_size", ctypes.c_uint64), ("key", ctypes.c_void_p), ("x", ctypes.c_void_p), ("capacity", ctypes.c_int64),
                 ("count", ctypes.c_void_p)]
 
 
-class AgShadingSamples(ctypes.Structure):
-    _fields_ = [("agent", ctypes.c_void_p), ("gamma", ctypes.c_void_p), ("utility", ctypes.c_void_p),
+class AgShadingSamples(_Sized):
+    _fields_ = [("struct_size", ctypes.c_uint64), ("agent", ctypes.c_void_p), ("gamma", ctypes.c_void_p), ("utility", ctypes.c_void_p),
                 ("capacity", ctypes.c_int64), ("count", ctypes.c_void_p), ("ctr", ctypes.c_void_p),
                 ("value", ctypes.c_void_p), ("propensity", ctypes.c_void_p), ("won", ctypes.c_void_p),
                 ("order", ctypes.c_void_p)]
@@ -126,6 +136,7 @@ def load(path=None):
         "ag_simulate": (ctypes.c_int, [vp, i64, ctypes.POINTER(AgBatchIn),
                                        ctypes.POINTER(AgBatchOut), vp, vp]),
         "ag_generate": (ctypes.c_int, [vp, u64, u64, i64, vp, vp, vp, vp]),
+        "ag_simulate_generated": (ctypes.c_int, [vp, u64, u64, i64, ctypes.POINTER(AgBatchOut), vp, vp]),
         "ag_counters_to_double": (ctypes.c_int, [vp, i64, vp]),
         "ag_sigmoid": (ctypes.c_int, [vp, vp, i64, vp]),
         "ag_exp": (ctypes.c_int, [vp, vp, i64, vp]),

@@ -161,6 +161,12 @@ class AuctionEngine:
         mode = _lib.ITEM_SEARCH_EXACT if exact else _lib.ITEM_SEARCH_AUTO
         self._check(self.L.ag_set_option(self._h, _lib.OPT_ITEM_SEARCH, mode), "ag_set_option")
 
+    def set_simulate_kernel(self, generic):
+        """generic=True: always the general simulate kernel; False (default): the dedicated
+        Oracle kernel for OracleAllocator + TruthfulBidder populations -- identical results."""
+        mode = _lib.SIM_KERNEL_GENERIC if generic else _lib.SIM_KERNEL_AUTO
+        self._check(self.L.ag_set_option(self._h, _lib.OPT_SIMULATE_KERNEL, mode), "ag_set_option")
+
     def set_lane_auctions(self, n):
         """Auctions per lane in the screened kernel: 1 (default) or 2 (16-B SoA accesses when
         B is even; lower occupancy, slower under sustained load). Same results either way."""
@@ -260,6 +266,15 @@ class AuctionEngine:
         bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
         self._check(self.L.ag_simulate(self._h, B, ctypes.byref(bi), ctypes.byref(bo),
                                  _ptr(counters), _stream()), "ag_simulate")
+
+    def simulate_generated(self, seed, first_auction, outputs, counters=None):
+        """Generate mode (ag_simulate_generated): B = outputs["winner"].shape[0] rounds whose
+        inputs are drawn inside the kernel -- the same bits generate(seed, first_auction)
+        writes -- so only the outputs touch HBM."""
+        B = outputs["winner"].shape[0]
+        bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
+        self._check(self.L.ag_simulate_generated(self._h, int(seed), int(first_auction), B, ctypes.byref(bo),
+                                                 _ptr(counters), _stream()), "ag_simulate_generated")
 
     def generate(self, seed, first_auction, inputs):
         B = inputs["u"].shape[0]

@@ -939,6 +939,7 @@ int ag_get_dr_state(ag_ctx *c, float *state, int32_t *initialised) {
 
 int ag_shading_counts(ag_ctx *c, const ag_shading_samples *s, int64_t *counts, void *stream) {
   if (!c || !s || !counts) return ag_set_error(AG_ERR_INVALID, "ag_shading_counts: null argument");
+  AG_CHECK_STRUCT(s, "ag_shading_counts", "ag_shading_samples");
   AgDeviceGuard g(c->device);
   if (int rc = dr_ws_ready(c)) return rc;
   const int N = c->shape.num_agents;
@@ -966,6 +967,7 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agen
                      const int64_t *noise_offsets, int32_t noise_epochs, int32_t *epochs, int32_t *status,
                      float *traces, void *stream) {
   if (!c || !s || !noise_offsets) return ag_set_error(AG_ERR_INVALID, "ag_bidder_update: null argument");
+  AG_CHECK_STRUCT(s, "ag_bidder_update", "ag_shading_samples");
   if (!s->ctr || !s->value || !s->propensity || !s->won || !s->order)
     return ag_set_error(AG_ERR_INVALID, "ag_bidder_update: the store needs ctr, value, propensity, won, order");
   if (!c->dr_loaded) return ag_set_error(AG_ERR_STATE, "ag_bidder_update: ag_set_dr_state not called");

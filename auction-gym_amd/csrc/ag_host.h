@@ -16,6 +16,23 @@ int ag_set_error(int code, const char *fmt, ...) __attribute__((format(printf, 2
                           __FILE__, __LINE__);                                          \
   } while (0)
 
+// ABI structs passed by pointer start with their size (include/auctiongym.h): a binding
+// compiled against another layout is refused before any other field is read.
+template <typename T>
+inline int ag_check_struct(const T *p, const char *who, const char *type) {
+  if (p && p->struct_size != (uint64_t)sizeof(T))
+    return ag_set_error(AG_ERR_INVALID,
+                        "%s: %s.struct_size is %llu, this library (ABI %d) expects %llu -- the caller's "
+                        "binding declares another layout of include/auctiongym.h",
+                        who, type, (unsigned long long)p->struct_size, AG_ABI_VERSION,
+                        (unsigned long long)sizeof(T));
+  return AG_OK;
+}
+#define AG_CHECK_STRUCT(p, who, type) \
+  do {                                \
+    if (int rc_ = ag_check_struct(p, who, type)) return rc_; \
+  } while (0)
+
 // LR-TS training workspace (ag_lrts.hip), grown on demand by ag_lrts_update.
 struct ag_lrts_ws {
   int64_t cap = 0;            // samples the bucket arrays hold
@@ -63,6 +80,10 @@ struct ag_ctx {
   int64_t lrts_chunk = 0;  // AG_OPT_LRTS_BLOCK_SAMPLES
   bool wide = false;  // 1 auction per lane by default: higher occupancy, faster when sustained
   bool catalog = false;
+  bool values_positive = false;  // every catalogue value > 0: the f32 item screens apply
+  bool ora_catalog = false;  // catalogue within k_oracle's bounds (ag_sim_oracle.h)
+  int32_t sim_kernel = AG_SIM_KERNEL_AUTO;  // AG_OPT_SIMULATE_KERNEL
+  int32_t resident_ora[4] = {};             // resident blocks of k_oracle [generate][counters]
   // general populations (anything beyond OracleAllocator + TruthfulBidder)
   bool general = false, has_lrts = false, has_shading = false, lrts_loaded = false;
   int32_t ts_sample = 1;

@@ -28,6 +28,7 @@
 #include "ag_host.h"
 #include "ag_philox.h"
 #include "ag_sim.h"
+#include "ag_sim_oracle.h"
 
 // ------------------------------------------------------------------------------------
 // error plumbing (declared in ag_host.h)
@@ -167,43 +168,20 @@ __global__ __launch_bounds__(kThreads) void k_allocate_wave(const double *__rest
 // synthetic batch generator (Philox4x32-10; oracle/ag_oracle.c restates the integer part)
 // ------------------------------------------------------------------------------------
 
+constexpr int kMaxGenE = 16;  // ag_generate: E <= 16 (the simulate kernels take E + 1 <= 16)
+
 __global__ __launch_bounds__(kThreads) void k_generate(uint64_t seed, uint64_t first, int64_t B, int N, int P,
                                                       int E, double scale, double *ctx, int32_t *part,
                                                       double *u) {
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < B;
        i += (int64_t)gridDim.x * kThreads) {
-    const uint64_t idx = first + (uint64_t)i;
-    const uint32_t c0 = (uint32_t)idx, c1 = (uint32_t)(idx >> 32);
-    uint32_t w[4];
-    philox(c0, c1, 0, 0, k0, k1, w);
-    u[i] = (double)((((uint64_t)w[0] << 32) | w[1]) >> 11) * 0x1p-53;
-    // participants: Floyd's algorithm, slot order = insertion order (stream 1)
+    double x[kMaxGenE], uu;
     int picked[64];
-    int n = 0;
-    for (int j = N - P; j < N; ++j) {
-      const int step = j - (N - P);
-      if ((step & 3) == 0) philox(c0, c1, (uint32_t)(step >> 2), 1, k0, k1, w);
-      int pick = (int)(((uint64_t)w[step & 3] * (uint64_t)(j + 1)) >> 32);
-      for (int q = 0; q < n; ++q)
-        if (picked[q] == pick) {
-          pick = j;
-          break;
-        }
-      picked[n++] = pick;
-      part[(int64_t)step * B + i] = pick;
-    }
-    // context: Box-Muller pairs (stream 2), ctx = 0 + scale * z (numpy normal(0, scale))
-    for (int m = 0; 2 * m < E; ++m) {
-      philox(c0, c1, (uint32_t)m, 2, k0, k1, w);
-      const double u1 = (double)(((((uint64_t)w[0] << 32) | w[1]) >> 11) + 1) * 0x1p-53;
-      const double u2 = (double)((((uint64_t)w[2] << 32) | w[3]) >> 11) * 0x1p-53;
-      const double r = sqrt(-2.0 * log(u1));
-      double sn, cs;
-      sincospi(2.0 * u2, &sn, &cs);
-      ctx[(int64_t)(2 * m) * B + i] = 0.0 + scale * (r * cs);
-      if (2 * m + 1 < E) ctx[(int64_t)(2 * m + 1) * B + i] = 0.0 + scale * (r * sn);
-    }
+    gen_auction<64, kMaxGenE>(k0, k1, first + (uint64_t)i, N, P, E, scale, x, picked, uu);
+    u[i] = uu;
+    for (int s = 0; s < P; ++s) part[(int64_t)s * B + i] = picked[s];
+    for (int e = 0; e < E; ++e) ctx[(int64_t)e * B + i] = x[e];
   }
 }
 
@@ -315,6 +293,92 @@ SimKernel pick_kernel(int P, int D, bool prune, int W, bool general) {
     case 8: return pick_kernel_for<8>(D, prune, W, general);
     default: return nullptr;
   }
+}
+
+OraKernel pick_oracle(int P, int D, bool gen) {
+  switch (P) {
+    case 1: return pick_oracle_for<1>(D, gen);
+    case 2: return pick_oracle_for<2>(D, gen);
+    case 3: return pick_oracle_for<3>(D, gen);
+    case 4: return pick_oracle_for<4>(D, gen);
+    case 5: return pick_oracle_for<5>(D, gen);
+    case 6: return pick_oracle_for<6>(D, gen);
+    case 7: return pick_oracle_for<7>(D, gen);
+    case 8: return pick_oracle_for<8>(D, gen);
+    default: return nullptr;
+  }
+}
+
+// Resident blocks of a kernel (grid of the persistent launches), capped by the partials
+// workspace.
+int resident_blocks(const ag_ctx *c, const void *k, size_t lds, int *out) {
+  int per_cu = 0, cus = 0;
+  AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, lds));
+  AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+  int res = per_cu * cus;
+  if (res < 1) res = 1;
+  if (res > c->partial_blocks) res = c->partial_blocks;
+  *out = res;
+  return AG_OK;
+}
+
+// ag_simulate for OracleAllocator + TruthfulBidder populations: k_oracle (ag_sim_oracle.h).
+int simulate_oracle(ag_ctx *c, OraKernel k, int64_t B, const ag_batch_in *in, const ag_batch_out *out,
+                    int64_t *counters_fx, hipStream_t st, uint64_t seed = 0, uint64_t first = 0) {
+  const ag_shape &s = c->shape;
+  OraParams prm;
+  prm.B = (int32_t)B;
+  prm.N = s.num_agents;
+  prm.K = s.num_items;
+  prm.mech = s.mechanism;
+  prm.want_counters = counters_fx != nullptr;
+  prm.L = make_ora_layout(s.num_agents, s.num_items, c->D, prm.want_counters);
+  prm.items = c->d_items;
+  prm.values = c->d_values;
+  prm.ctx = in ? in->ctx : nullptr;
+  prm.part = in ? in->part : nullptr;
+  prm.u = in ? in->u : nullptr;
+  prm.seed = seed;
+  prm.first = first;
+  prm.scale = s.embedding_var;
+  prm.winner = out->winner;
+  prm.price = out->price;
+  prm.second_price = out->second_price;
+  prm.outcome = out->outcome;
+  prm.item = out->item;
+  prm.bid = out->bid;
+  prm.est_ctr = out->est_ctr;
+  prm.true_ctr = out->true_ctr;
+  prm.best_ev = out->best_ev;
+  prm.partials = c->d_partials;
+  const size_t lds = (size_t)prm.L.total;
+  if (lds > 160 * 1024)
+    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
+  if (lds > 64 * 1024)
+    AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  int &res = c->resident_ora[(prm.want_counters ? 1 : 0) + (in ? 0 : 2)];
+  if (res == 0)
+    if (int rc = resident_blocks(c, (const void *)k, lds, &res)) return rc;
+  // a lane resolves at most kOraPerLane auctions per launch (8-bit packed counts, replica
+  // sums in range): larger batches run as consecutive launches
+  int64_t chunk_max = (int64_t)res * kThreads * kOraPerLane;
+  if (c->launch_cap > 0 && c->launch_cap < chunk_max) chunk_max = c->launch_cap;
+  if (chunk_max < 1) chunk_max = 1;
+  const int nc = s.num_agents * kC;
+  for (int64_t lo = 0; lo < B; lo += chunk_max) {
+    const int64_t hi = lo + chunk_max < B ? lo + chunk_max : B;
+    const int64_t tiles = (hi - lo + kThreads - 1) / kThreads;
+    const int grid = (int)(tiles < res ? tiles : res);
+    prm.lo = (int32_t)lo;
+    prm.hi = (int32_t)hi;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), lds, st, prm);  // generate mode: same lo/hi
+    AG_HIP(hipGetLastError());
+    if (counters_fx) {
+      hipLaunchKernelGGL(k_reduce_counters, dim3(nc), dim3(kThreads), 0, st, c->d_partials, grid, nc, counters_fx);
+      AG_HIP(hipGetLastError());
+    }
+  }
+  return AG_OK;
 }
 
 int grid_for(int64_t B, int64_t per_block_cap) {
@@ -523,6 +587,11 @@ int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
     case AG_OPT_BIDDER_RECORD_CACHE:
       c->bidder_cache = value;
       return AG_OK;
+    case AG_OPT_SIMULATE_KERNEL:
+      if (value != AG_SIM_KERNEL_AUTO && value != AG_SIM_KERNEL_GENERIC)
+        return ag_set_error(AG_ERR_INVALID, "ag_set_option: bad simulate kernel %lld", (long long)value);
+      c->sim_kernel = (int32_t)value;
+      return AG_OK;
     default:
       return ag_set_error(AG_ERR_INVALID, "ag_set_option: unknown option %d", option);
   }
@@ -535,6 +604,16 @@ int ag_load_catalog(ag_ctx *c, const double *item_emb, const double *item_val) {
   AG_HIP(hipMemcpy(c->d_items, item_emb, n * c->D * sizeof(double), hipMemcpyHostToDevice));
   AG_HIP(hipMemcpy(c->d_values, item_val, n * sizeof(double), hipMemcpyHostToDevice));
   c->catalog = true;
+  // k_oracle's bounds (ag_sim_oracle.h): finite embeddings, every value in (0, kOraMaxValue)
+  // the f32 screens rank items by 1 / (CTR * value): valid when every value is positive
+  bool pos = true, ok = true;
+  for (size_t j = 0; j < n; ++j) {
+    pos = pos && item_val[j] > 0.0 && isfinite(item_val[j]);
+    ok = ok && item_val[j] > 0.0 && item_val[j] < kOraMaxValue;
+  }
+  for (size_t j = 0; j < n * c->D && ok; ++j) ok = isfinite(item_emb[j]);
+  c->values_positive = pos;
+  c->ora_catalog = ok;
   return AG_OK;
 }
 
@@ -565,6 +644,8 @@ int ag_allocate(ag_ctx *c, const double *bids, int64_t B, int32_t *winner, doubl
 int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, int64_t *counters_fx,
                 void *stream) {
   if (!c || !in || !out) return ag_set_error(AG_ERR_INVALID, "ag_simulate: null argument");
+  AG_CHECK_STRUCT(in, "ag_simulate", "ag_batch_in");
+  AG_CHECK_STRUCT(out, "ag_simulate", "ag_batch_out");
   if (!c->can_simulate)
     return ag_set_error(AG_ERR_UNSUPPORTED,
                      "ag_simulate: supports P in [1,%d], E+1 in {2..9,11,13,16} and a catalogue "
@@ -581,7 +662,8 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   const ag_shape &s = c->shape;
   const int nc = s.num_agents * kC;
   const int D = c->D;
-  const bool prune = c->item_search == AG_ITEM_SEARCH_AUTO && D <= 8 && s.num_items <= 2 * kMaxKPairs;
+  const bool prune = c->item_search == AG_ITEM_SEARCH_AUTO && D <= 8 && s.num_items <= 2 * kMaxKPairs &&
+                     c->values_positive;
   if (c->has_lrts && !c->lrts_loaded)
     return ag_set_error(AG_ERR_STATE, "ag_simulate: LR-TS agents need ag_load_lrts");
   if (c->has_lrts && c->ts_sample && !in->ts_noise)
@@ -613,6 +695,9 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   prm.in = *in;
   prm.out = *out;
   prm.partials = c->d_partials;
+  if (prune && !c->general && c->ora_catalog && c->sim_kernel == AG_SIM_KERNEL_AUTO && !c->wide)
+    if (OraKernel ok = pick_oracle(s.num_participants, D, false))
+      return simulate_oracle(c, ok, B, in, out, counters_fx, (hipStream_t)stream);
   const int W = (prune && (B % 2) == 0 && c->wide && !c->general) ? 2 : 1;
   SimKernel k = pick_kernel(s.num_participants, D, prune, W, c->general);
   if (!k) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: no kernel for P=%d D=%d", s.num_participants, D);
@@ -646,7 +731,7 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
     const int grid = (int)(tiles < res ? tiles : res);
     prm.lo = (int32_t)lo;
     prm.hi = (int32_t)hi;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), lds, st, prm);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), lds, st, prm);  // generate mode: same lo/hi
     AG_HIP(hipGetLastError());
     if (counters_fx) {
       hipLaunchKernelGGL(k_reduce_counters, dim3(nc), dim3(kThreads), 0, st, c->d_partials, grid, nc,
@@ -657,12 +742,36 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   return AG_OK;
 }
 
+int ag_simulate_generated(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, ag_batch_out *out,
+                          int64_t *counters_fx, void *stream) {
+  if (!c || !out) return ag_set_error(AG_ERR_INVALID, "ag_simulate_generated: null argument");
+  AG_CHECK_STRUCT(out, "ag_simulate_generated", "ag_batch_out");
+  if (!c->catalog) return ag_set_error(AG_ERR_STATE, "ag_simulate_generated: ag_load_catalog not called");
+  if (B < 0) return ag_set_error(AG_ERR_INVALID, "ag_simulate_generated: B < 0");
+  if (B == 0) return AG_OK;
+  const ag_shape &s = c->shape;
+  if (B * s.num_participants > INT32_MAX)
+    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate_generated: B * P must be < 2^31; split the batch");
+  OraKernel k = (!c->general && c->ora_catalog && s.num_items <= 2 * kMaxKPairs)
+                    ? pick_oracle(s.num_participants, c->D, true) : nullptr;
+  if (!k)
+    return ag_set_error(AG_ERR_UNSUPPORTED,
+                        "ag_simulate_generated: OracleAllocator + TruthfulBidder populations with P <= %d, "
+                        "E + 1 <= 8, K <= %d and catalogue values in (0, %g) only",
+                        kMaxP, 2 * kMaxKPairs, kOraMaxValue);
+  AgDeviceGuard g(c->device);
+  // a launch covers auctions [lo, hi) of the batch: their global indices are first + lo ...
+  return simulate_oracle(c, k, B, nullptr, out, counters_fx, (hipStream_t)stream, seed, first);
+}
+
 int ag_generate(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, double *ctx_out, int32_t *part_out,
                 double *u_out, void *stream) {
   if (!c || !ctx_out || !part_out || !u_out) return ag_set_error(AG_ERR_INVALID, "ag_generate: null argument");
   if (B < 0) return ag_set_error(AG_ERR_INVALID, "ag_generate: B < 0");
   if (B == 0) return AG_OK;
   if (c->shape.num_participants > 64) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_generate: P > 64");
+  if (c->shape.embedding_size > kMaxGenE)
+    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_generate: E > %d", kMaxGenE);
   AgDeviceGuard g(c->device);
   const int grid = grid_for(B, (int64_t)1 << 40);
   hipLaunchKernelGGL(k_generate, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, seed, first, B,

@@ -437,6 +437,7 @@ int grid_over(int64_t n) {
 
 int check_store(const ag_ctx *c, const ag_lrts_samples *s, const char *who) {
   if (!c || !s) return ag_set_error(AG_ERR_INVALID, "%s: null argument", who);
+  AG_CHECK_STRUCT(s, who, "ag_lrts_samples");
   if (!s->key || !s->x || !s->count || s->capacity < 0)
     return ag_set_error(AG_ERR_INVALID, "%s: sample store needs key, x, count and capacity >= 0", who);
   return AG_OK;
@@ -462,6 +463,8 @@ int ag_lrts_collect(ag_ctx *c, int64_t B, const ag_batch_in *in, const ag_batch_
                     const ag_lrts_samples *s, void *stream) {
   if (int rc = check_store(c, s, "ag_lrts_collect")) return rc;
   if (!in || !out) return ag_set_error(AG_ERR_INVALID, "ag_lrts_collect: null argument");
+  AG_CHECK_STRUCT(in, "ag_lrts_collect", "ag_batch_in");
+  AG_CHECK_STRUCT(out, "ag_lrts_collect", "ag_batch_out");
   if (B < 0) return ag_set_error(AG_ERR_INVALID, "ag_lrts_collect: B < 0");
   if (B == 0 || !c->has_lrts) return AG_OK;
   if (c->shape.num_agents > 65536 || c->shape.num_items > 32768)

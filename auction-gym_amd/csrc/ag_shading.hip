@@ -226,6 +226,7 @@ int grid_over(int64_t n) {
 
 int check_store(const ag_ctx *c, const ag_shading_samples *s, const char *who) {
   if (!c || !s) return ag_set_error(AG_ERR_INVALID, "%s: null argument", who);
+  AG_CHECK_STRUCT(s, who, "ag_shading_samples");
   if (!s->agent || !s->gamma || !s->utility || !s->count || s->capacity < 0)
     return ag_set_error(AG_ERR_INVALID, "%s: sample store needs agent, gamma, utility, count, capacity", who);
   return AG_OK;
@@ -239,6 +240,8 @@ int ag_shading_collect(ag_ctx *c, int64_t first, int64_t B, const ag_batch_in *i
                        const ag_shading_samples *s, void *stream) {
   if (int rc = check_store(c, s, "ag_shading_collect")) return rc;
   if (!in || !out) return ag_set_error(AG_ERR_INVALID, "ag_shading_collect: null argument");
+  AG_CHECK_STRUCT(in, "ag_shading_collect", "ag_batch_in");
+  AG_CHECK_STRUCT(out, "ag_shading_collect", "ag_batch_out");
   if (B < 0) return ag_set_error(AG_ERR_INVALID, "ag_shading_collect: B < 0");
   if (B == 0 || !c->has_shading) return AG_OK;
   if (!in->part || !out->winner || !out->item || !out->outcome || !out->price || !out->gamma)

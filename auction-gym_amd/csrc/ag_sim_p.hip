@@ -1,6 +1,7 @@
 // ag_sim_p.hip -- k_simulate instantiations for one participant count AG_P (the Makefile
 // compiles this file once per P = 1..8, in parallel).
 #include "ag_sim.h"
+#include "ag_sim_oracle.h"
 
 #ifndef AG_P
 #error "compile with -DAG_P=<participants>"
@@ -42,6 +43,21 @@ SimKernel pick_kernel_for<AG_P>(int D, bool prune, int W, bool general) {
     case 11: return k_simulate<P, 11, false, 1, false>;
     case 13: return k_simulate<P, 13, false, 1, false>;
     case 16: return k_simulate<P, 16, false, 1, false>;
+    default: return nullptr;
+  }
+}
+
+template <>
+OraKernel pick_oracle_for<AG_P>(int D, bool gen) {
+  constexpr int P = AG_P;
+  switch (D) {
+    case 2: return gen ? k_oracle<P, 2, true> : k_oracle<P, 2, false>;
+    case 3: return gen ? k_oracle<P, 3, true> : k_oracle<P, 3, false>;
+    case 4: return gen ? k_oracle<P, 4, true> : k_oracle<P, 4, false>;
+    case 5: return gen ? k_oracle<P, 5, true> : k_oracle<P, 5, false>;
+    case 6: return gen ? k_oracle<P, 6, true> : k_oracle<P, 6, false>;
+    case 7: return gen ? k_oracle<P, 7, true> : k_oracle<P, 7, false>;
+    case 8: return gen ? k_oracle<P, 8, true> : k_oracle<P, 8, false>;
     default: return nullptr;
   }
 }

@@ -17,6 +17,10 @@
  *    synchronise and are stream-ordered on `stream` (a hipStream_t, NULL = default):
  *    they may be captured into a hipGraph.
  *  - One ag_ctx per process and device; a ctx is not thread-safe.
+ *  - Every struct passed by pointer (ag_batch_in, ag_batch_out, ag_lrts_samples,
+ *    ag_shading_samples) starts with `struct_size` = sizeof(struct) as the caller compiled
+ *    it. A binding written against another layout is refused with AG_ERR_INVALID before
+ *    any other field is read (AG_STRUCT_INIT sets it in C).
  */
 #ifndef AUCTIONGYM_H
 #define AUCTIONGYM_H
@@ -27,7 +31,7 @@
 extern "C" {
 #endif
 
-#define AG_ABI_VERSION 14
+#define AG_ABI_VERSION 15
 
 typedef enum ag_status {
   AG_OK = 0,
@@ -121,9 +125,13 @@ typedef struct ag_shape {
 
 typedef struct ag_ctx ag_ctx;
 
+/* C initialiser of the struct_size field: ag_batch_in in = {AG_STRUCT_INIT(ag_batch_in), ...}; */
+#define AG_STRUCT_INIT(type) ((uint64_t)sizeof(type))
+
 /* Replay inputs of B auctions (dev). The reference draws these from its numpy Generator
  * in the order src/Auction.py:33 (normal), :42 (choice), :65 (binomial's next_double). */
 typedef struct ag_batch_in {
+  uint64_t struct_size; /* sizeof(ag_batch_in) (ABI 15)                                   */
   const double *ctx;   /* [E][B] true context without the intercept                      */
   const int32_t *part; /* [P][B] participating agent index per slot, P distinct of N     */
   const double *u;     /* [B]    uniform in [0,1) consumed by binomial(1, CTR[winner])   */
@@ -145,6 +153,7 @@ typedef struct ag_batch_in {
 
 /* Outputs of B auctions (dev). Any pointer may be NULL to skip that array. */
 typedef struct ag_batch_out {
+  uint64_t struct_size;  /* sizeof(ag_batch_out) (ABI 15)                                */
   int32_t *winner;       /* [B] winning slot (argsort(-bids)[0]; ties -> lowest slot)    */
   double *price;         /* [B] price charged (NaN when P == 1: nobody charged)          */
   double *second_price;  /* [B] second highest bid (NaN when P == 1)                     */
@@ -198,10 +207,18 @@ typedef enum ag_option {
                                    fits' fixed-order sums follow the split */
   AG_OPT_FIT_NOISE_SEED = 5,      /* value: seed of the synthetic rsample noise of ag_bidder_update
                                    called with noise == NULL (default 0) */
-  AG_OPT_BIDDER_RECORD_CACHE = 6  /* value: most records per workgroup the learning bidders'
+  AG_OPT_BIDDER_RECORD_CACHE = 6, /* value: most records per workgroup the learning bidders'
                                    trainer stages in LDS (-1 = default: as many as fit; 0 = none,
                                    every epoch reads the store); identical results */
+  AG_OPT_SIMULATE_KERNEL = 7      /* value: ag_sim_kernel; identical results */
 } ag_option;
+
+typedef enum ag_sim_kernel {
+  AG_SIM_KERNEL_AUTO = 0,   /* OracleAllocator + TruthfulBidder populations whose catalogue
+                               values lie in (0, 1024): the dedicated Oracle kernel; else the
+                               general one */
+  AG_SIM_KERNEL_GENERIC = 1 /* always the general simulate kernel (A/B and parity tests) */
+} ag_sim_kernel;
 
 typedef enum ag_item_search {
   AG_ITEM_SEARCH_AUTO = 0,  /* f32 screen of all K items, exact FP64 re-score of the items
@@ -228,6 +245,14 @@ int ag_allocate(ag_ctx *ctx, const double *bids, int64_t B, int32_t *winner, dou
  * start of an iteration, like Agent.clear_utility); may be NULL. */
 int ag_simulate(ag_ctx *ctx, int64_t B, const ag_batch_in *in, ag_batch_out *out,
                 int64_t *counters_fx, void *stream);
+
+/* Generate mode: B rounds of Auction.simulate_opportunity whose inputs are drawn on the chip
+ * inside the simulate kernel, the same bits ag_generate(seed, first_auction, B) writes (so
+ * the outputs equal ag_generate followed by ag_simulate); nothing but the catalogue is read
+ * from HBM. OracleAllocator + TruthfulBidder populations whose catalogue values lie in
+ * (0, 1024), P <= 8, E + 1 <= 8, K <= 16; otherwise AG_ERR_UNSUPPORTED. */
+int ag_simulate_generated(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B, ag_batch_out *out,
+                          int64_t *counters_fx, void *stream);
 
 /* Synthetic replay inputs for auctions [first_auction, first_auction + B) (dev, SoA):
  * Philox4x32-10 keyed by seed and the GLOBAL auction index, so a sharded batch is
@@ -260,6 +285,7 @@ int ag_generate_noise(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_
 #define AG_LRTS_MAX_DO 8         /* OE + 1 <= 8; K * (OE + 1) <= 64 */
 
 typedef struct ag_lrts_samples {
+  uint64_t struct_size; /* sizeof(ag_lrts_samples) (ABI 15)                               */
   uint32_t *key;     /* dev [capacity]: agent << 16 | item << 1 | outcome               */
   float *x;          /* dev [OE+1][capacity]: float32(observed context), 1.0             */
   int64_t capacity;
@@ -290,6 +316,7 @@ int ag_lrts_read(ag_ctx *ctx, float *m, float *q, float *prev_m);
  * derives from the logs, src/Bidder.py:62-63) accumulates in a caller-owned store;
  * reset *count where the reference calls Agent.clear_logs. Records are unordered. */
 typedef struct ag_shading_samples {
+  uint64_t struct_size; /* sizeof(ag_shading_samples) (ABI 15)                           */
   int32_t *agent;    /* dev [capacity]                                                   */
   double *gamma;     /* dev [capacity]: the shading factor of the bid                    */
   double *utility;   /* dev [capacity]: value * outcome - price if won, else 0           */

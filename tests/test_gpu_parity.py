@@ -186,19 +186,30 @@ def test_full_size_synthetic_batch_bit_exact(gpu, oracle):
     assert np.array_equal(cnt.cpu().numpy(), orc["counters_fx"])
     # the exact item scan, two auctions per lane, and a batch run as several launches
     # (odd-sized auction ranges) give the same bits
-    for exact, lanes, cap in ((True, 1, 0), (False, 2, 0), (False, 1, 1000002), (False, 2, 777778)):
+    # (the default is the dedicated Oracle kernel, k_oracle; the general kernel must agree)
+    for exact, lanes, cap, generic in ((True, 1, 0, False), (False, 2, 0, False), (False, 1, 1000002, False),
+                                       (False, 2, 777778, False), (False, 1, 0, True), (False, 1, 777777, True),
+                                       (False, 1, 333333, False)):
         eng.set_item_search(exact)
         eng.set_lane_auctions(lanes)
         eng.set_launch_auctions(cap)
+        eng.set_simulate_kernel(generic)
         out_x = eng.alloc_outputs(B)
         cnt_x = eng.new_counters()
         eng.simulate(inp, out_x, cnt_x)
         for k in out:
-            assert torch.equal(out[k], out_x[k]), (k, exact, lanes, cap)
+            assert torch.equal(out[k], out_x[k]), (k, exact, lanes, cap, generic)
         assert torch.equal(cnt, cnt_x)
     eng.set_item_search(False)
     eng.set_lane_auctions(1)
     eng.set_launch_auctions(0)
+    eng.set_simulate_kernel(False)
+    # the bench's output set (no second_price) and no counters: same arrays
+    sub = ("winner", "price", "outcome", "item", "bid", "est_ctr", "true_ctr", "best_ev")
+    out_s = eng.alloc_outputs(B, sub)
+    eng.simulate(inp, out_s, None)
+    for k in sub:
+        assert torch.equal(out[k], out_s[k]), k
     # batch split invariance: two halves accumulate to the same exact counters
     cnt2 = eng.new_counters()
     for lo, hi in ((0, B // 3), (B // 3, B)):
@@ -298,6 +309,74 @@ def test_empty_batch(gpu):
     eng.close()
 
 
+def test_generate_mode_equals_hbm_inputs(gpu):
+    """ag_simulate_generated (inputs drawn inside k_oracle) == ag_generate + ag_simulate, bit
+    for bit: every output and the exact counters, for a batch run as several launches with a
+    nonzero first auction index, P in {1, 2, 5}, both mechanisms."""
+    import torch
+    from auctiongym_amd.engine import AuctionEngine
+    g = np.random.default_rng(5)
+    for N, P, mech, B, cap in ((6, 2, 1, 1 << 20, 0), (6, 2, 0, 300001, 65537), (9, 5, 0, 100000, 0),
+                               (3, 1, 1, 50000, 7777)):
+        items = np.concatenate([g.normal(0, 1, (N, 12, 5)), -3.0 - g.random((N, 12, 1))], axis=2)
+        values = g.lognormal(0.1, 0.2, (N, 12))
+        eng = AuctionEngine(N, P, 12, 5, 4, mech, 1.3)
+        eng.load_catalog(items, values)
+        eng.set_launch_auctions(cap)
+        first = 123456789012
+        inp = eng.alloc_inputs(B)
+        eng.generate(42, first, inp)
+        out, cnt = eng.alloc_outputs(B), eng.new_counters()
+        eng.simulate(inp, out, cnt)
+        out_g, cnt_g = eng.alloc_outputs(B), eng.new_counters()
+        eng.simulate_generated(42, first, out_g, cnt_g)
+        torch.cuda.synchronize()
+        for k in out:
+            assert torch.equal(out[k], out_g[k]) or (torch.isnan(out[k]).all() and torch.isnan(out_g[k]).all()), k
+        assert torch.equal(cnt, cnt_g)
+        eng.close()
+    eng = AuctionEngine(4, 2, 12, 5, 4, 1)  # outside k_oracle's bounds: refused, loudly
+    items = np.concatenate([g.normal(0, 1, (4, 12, 5)), -3.0 - g.random((4, 12, 1))], axis=2)
+    eng.load_catalog(items, np.full((4, 12), 5000.0))
+    with pytest.raises(NotImplementedError, match="ag_simulate_generated"):
+        eng.simulate_generated(0, 0, eng.alloc_outputs(64))
+    eng.close()
+
+
+def test_stale_binding_is_refused(gpu):
+    """A caller compiled against another layout of the ABI structs (here the 3-field
+    ag_batch_in of ABI 14) is refused with AG_ERR_INVALID before any field is used."""
+    import ctypes
+    import torch
+    from auctiongym_amd import _lib
+    from auctiongym_amd.engine import AuctionEngine
+    eng = AuctionEngine(6, 2, 12, 5, 4, 1)
+    g = np.random.default_rng(0)
+    eng.load_catalog(np.concatenate([g.normal(0, 1, (6, 12, 5)), -3.0 - g.random((6, 12, 1))], axis=2),
+                     g.lognormal(0.1, 0.2, (6, 12)))
+
+    class OldIn(ctypes.Structure):
+        _fields_ = [("ctx", ctypes.c_void_p), ("part", ctypes.c_void_p), ("u", ctypes.c_void_p)]
+    inp = eng.alloc_inputs(64)
+    eng.generate(0, 0, inp)
+    out = eng.alloc_outputs(64)
+    old = OldIn(inp["ctx"].data_ptr(), inp["part"].data_ptr(), inp["u"].data_ptr())
+    bo = _lib.AgBatchOut(*[out[k].data_ptr() if k in out else None for k in
+                           ("winner", "price", "second_price", "outcome", "item", "bid", "est_ctr",
+                            "true_ctr", "best_ev", "gamma", "propensity")])
+    L = eng.L
+    rc = L.ag_simulate(eng._h, 64, ctypes.cast(ctypes.pointer(old), ctypes.POINTER(_lib.AgBatchIn)),
+                       ctypes.byref(bo), None, None)
+    assert rc == _lib.AG_ERR_INVALID
+    assert b"struct_size" in L.ag_last_error()
+    bo.struct_size = 12345
+    rc = L.ag_simulate(eng._h, 64, ctypes.byref(_lib.AgBatchIn(inp["ctx"].data_ptr(), inp["part"].data_ptr(),
+                                                                inp["u"].data_ptr())), ctypes.byref(bo), None, None)
+    assert rc == _lib.AG_ERR_INVALID
+    torch.cuda.synchronize()
+    eng.close()
+
+
 def test_screened_search_adversarial_catalogues(gpu, oracle):
     """Catalogues built to stress the f32 screen: exact duplicate items (ties -> first max),
     near-ties 1 ulp apart, huge embeddings (guard -> exact scan), intercepts so negative
@@ -319,24 +398,32 @@ def test_screened_search_adversarial_catalogues(gpu, oracle):
     cats.append((c, values))
     c = base.copy(); c[:, :, :E] *= 1e-9                         # all items ~ equal z
     cats.append((c, values * (1 + 1e-15 * g.random((N, K)))))
+    c = base.copy(); v = values.copy(); v[0, 3] = 2000.0            # a value beyond k_oracle's
+    cats.append((c, v))                                              # bound: general kernel
+    c = base.copy(); v = values.copy(); v[1, 4] = -0.5               # negative value: general kernel
+    cats.append((c, v))
     for items, vals in cats:
-        eng = AuctionEngine(N, P, K, E, 4, 0, 1.0)
-        eng.load_catalog(items, vals)
-        inp = eng.alloc_inputs(B)
-        eng.generate(7, 0, inp)
-        out = eng.alloc_outputs(B)
-        cnt = eng.new_counters()
-        eng.simulate(inp, out, cnt)
-        ctx = np.ascontiguousarray(inp["ctx"].cpu().numpy().T)
-        part = np.ascontiguousarray(inp["part"].cpu().numpy().T)
-        u = inp["u"].cpu().numpy()
-        orc = oracle.simulate(0, items, vals, ctx, part, u, nthreads=16)
-        assert np.array_equal(out["item"].cpu().numpy().T, orc["item"])
-        assert np.array_equal(out["bid"].cpu().numpy().T, orc["bid"])
-        assert np.array_equal(out["best_ev"].cpu().numpy().T, orc["best_ev"])
-        assert np.array_equal(out["price"].cpu().numpy(), orc["price"])
-        assert np.array_equal(cnt.cpu().numpy(), orc["counters_fx"])
-        eng.close()
+        for generic in (False, True):  # the dedicated Oracle kernel and the general one
+            eng = AuctionEngine(N, P, K, E, 4, 0, 1.0)
+            eng.load_catalog(items, vals)
+            eng.set_simulate_kernel(generic)
+            inp = eng.alloc_inputs(B)
+            eng.generate(7, 0, inp)
+            out = eng.alloc_outputs(B)
+            cnt = eng.new_counters()
+            eng.simulate(inp, out, cnt)
+            ctx = np.ascontiguousarray(inp["ctx"].cpu().numpy().T)
+            part = np.ascontiguousarray(inp["part"].cpu().numpy().T)
+            u = inp["u"].cpu().numpy()
+            orc = oracle.simulate(0, items, vals, ctx, part, u, nthreads=16)
+            assert np.array_equal(out["item"].cpu().numpy().T, orc["item"])
+            assert np.array_equal(out["bid"].cpu().numpy().T, orc["bid"])
+            assert np.array_equal(out["best_ev"].cpu().numpy().T, orc["best_ev"])
+            assert np.array_equal(out["price"].cpu().numpy(), orc["price"])
+            assert np.array_equal(out["second_price"].cpu().numpy(), orc["second_price"])
+            assert np.array_equal(out["outcome"].cpu().numpy(), orc["outcome"])
+            assert np.array_equal(cnt.cpu().numpy(), orc["counters_fx"])
+            eng.close()
 
 
 # ---- general populations: LR-TS allocators, shading bidders (first iteration) ----

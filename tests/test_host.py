@@ -33,7 +33,34 @@ def test_library_exports_every_declared_symbol():
 def test_library_loads_without_gpu_and_reports_abi():
     from auctiongym_amd import _lib
     L = _lib.load()
-    assert L.ag_abi_version() == _lib.ABI_VERSION == 14
+    assert L.ag_abi_version() == _lib.ABI_VERSION == 15
+
+
+def test_ctypes_structs_match_the_c_header(tmp_path):
+    """The ctypes mirrors of the ABI structs (auctiongym_amd/_lib.py) have the sizes and
+    field offsets a C compiler gives include/auctiongym.h, and set struct_size themselves."""
+    import ctypes
+    from auctiongym_amd import _lib
+    structs = {"ag_shape": _lib.AgShape, "ag_batch_in": _lib.AgBatchIn, "ag_batch_out": _lib.AgBatchOut,
+               "ag_lrts_samples": _lib.AgLrtsSamples, "ag_shading_samples": _lib.AgShadingSamples}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "auctiongym.h"', "int main(void) {"]
+    for cname, cls in structs.items():
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in cls._fields_:
+            lines.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
+    got = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                        check=True).stdout.splitlines())
+    for cname, cls in structs.items():
+        assert int(got[cname]) == ctypes.sizeof(cls), cname
+        for f, _ in cls._fields_:
+            assert int(got[f"{cname}.{f}"]) == getattr(cls, f).offset, (cname, f)
+    for cls in list(structs.values())[1:]:
+        assert cls().struct_size == ctypes.sizeof(cls)
 
 
 def test_counters_to_double_host_helper():

@@ -15,28 +15,39 @@ struct Ptrs {
   uint8_t *outcome;
 };
 
+template <bool NT, typename T> __device__ __forceinline__ T L(const T *q) {
+  if constexpr (NT) return __builtin_nontemporal_load(q); else return *q;
+}
+template <bool NT, typename T> __device__ __forceinline__ void S(T *q, T v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, q); else *q = v;
+}
+template <bool NT = false>
 __device__ __forceinline__ void one(const Ptrs &p, int64_t B, int64_t i) {
-  double x0 = p.ctx[i], x1 = p.ctx[B + i], x2 = p.ctx[2 * B + i], x3 = p.ctx[3 * B + i], x4 = p.ctx[4 * B + i];
-  int a0 = p.part[i], a1 = p.part[B + i];
-  double u = p.u[i];
+  double x0 = L<NT>(p.ctx + i), x1 = L<NT>(p.ctx + B + i), x2 = L<NT>(p.ctx + 2 * B + i),
+         x3 = L<NT>(p.ctx + 3 * B + i), x4 = L<NT>(p.ctx + 4 * B + i);
+  int a0 = L<NT>(p.part + i), a1 = L<NT>(p.part + B + i);
+  double u = L<NT>(p.u + i);
   double s = x0 + x1 + x2 + x3 + x4;
-  p.winner[i] = a0 > a1;
-  p.price[i] = s * u;
-  p.outcome[i] = (uint8_t)(u > 0.5);
-  p.item[i] = a0;
-  p.item[B + i] = a1;
-  p.bid[i] = s;
-  p.bid[B + i] = s + u;
-  p.est[i] = x0;
-  p.est[B + i] = x1;
-  p.tru[i] = x2;
-  p.tru[B + i] = x3;
-  p.bev[i] = x4;
-  p.bev[B + i] = u;
+  S<NT>(p.winner + i, (int32_t)(a0 > a1));
+  S<NT>(p.price + i, s * u);
+  S<NT>(p.outcome + i, (uint8_t)(u > 0.5));
+  S<NT>(p.item + i, (int32_t)a0);
+  S<NT>(p.item + B + i, (int32_t)a1);
+  S<NT>(p.bid + i, s);
+  S<NT>(p.bid + B + i, s + u);
+  S<NT>(p.est + i, x0);
+  S<NT>(p.est + B + i, x1);
+  S<NT>(p.tru + i, x2);
+  S<NT>(p.tru + B + i, x3);
+  S<NT>(p.bev + i, x4);
+  S<NT>(p.bev + B + i, u);
 }
 
 __global__ __launch_bounds__(256) void k_floor_persistent(Ptrs p, int64_t B) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < B; i += (int64_t)gridDim.x * 256) one(p, B, i);
+}
+__global__ __launch_bounds__(256) void k_floor_persistent_nt(Ptrs p, int64_t B) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < B; i += (int64_t)gridDim.x * 256) one<true>(p, B, i);
 }
 __global__ __launch_bounds__(256) void k_floor_tiles(Ptrs p, int64_t B) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -44,7 +55,9 @@ __global__ __launch_bounds__(256) void k_floor_tiles(Ptrs p, int64_t B) {
 }
 
 extern "C" int floor_run(int persistent, int grid, const Ptrs *p, int64_t B, void *stream) {
-  if (persistent)
+  if (persistent == 2)
+    hipLaunchKernelGGL(k_floor_persistent_nt, dim3(grid), dim3(256), 0, (hipStream_t)stream, *p, B);
+  else if (persistent)
     hipLaunchKernelGGL(k_floor_persistent, dim3(grid), dim3(256), 0, (hipStream_t)stream, *p, B);
   else
     hipLaunchKernelGGL(k_floor_tiles, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, *p, B);
