@@ -167,6 +167,11 @@ class AuctionEngine:
         mode = _lib.SIM_KERNEL_GENERIC if generic else _lib.SIM_KERNEL_AUTO
         self._check(self.L.ag_set_option(self._h, _lib.OPT_SIMULATE_KERNEL, mode), "ag_set_option")
 
+    def set_blocks_per_cu(self, n):
+        """Resident workgroups per CU of the Oracle kernel's persistent grid (0: as many as
+        fit); same results."""
+        self._check(self.L.ag_set_option(self._h, _lib.OPT_SIM_BLOCKS_PER_CU, int(n)), "ag_set_option")
+
     def set_lane_auctions(self, n):
         """Auctions per lane in the screened kernel: 1 (default) or 2 (16-B SoA accesses when
         B is even; lower occupancy, slower under sustained load). Same results either way."""
@@ -430,3 +435,14 @@ def device_exp(x, sigmoid=False):
     f = L.ag_sigmoid if sigmoid else L.ag_exp
     _check(f(_ptr(x), _ptr(y), x.numel(), _stream()), "ag_exp")
     return y
+
+
+def stream_copy(src, dst):
+    """ag_stream_copy of src into dst (contiguous device tensors of the same byte size):
+    the measured HBM peak of bench.py's roofline."""
+    require_gpu()
+    L = _lib.load()
+    n = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() != n or not (src.is_contiguous() and dst.is_contiguous()):
+        raise ValueError("stream_copy: contiguous tensors of equal byte size")
+    _check(L.ag_stream_copy(_ptr(src), _ptr(dst), n, _stream()), "ag_stream_copy")

@@ -83,6 +83,7 @@ struct ag_ctx {
   bool values_positive = false;  // every catalogue value > 0: the f32 item screens apply
   bool ora_catalog = false;  // catalogue within k_oracle's bounds (ag_sim_oracle.h)
   int32_t sim_kernel = AG_SIM_KERNEL_AUTO;  // AG_OPT_SIMULATE_KERNEL
+  int32_t grid_per_cu = 0;                  // AG_OPT_SIM_BLOCKS_PER_CU (0: as many as fit)
   int32_t resident_ora[4] = {};             // resident blocks of k_oracle [generate][counters]
   // general populations (anything beyond OracleAllocator + TruthfulBidder)
   bool general = false, has_lrts = false, has_shading = false, lrts_loaded = false;

@@ -278,6 +278,23 @@ __global__ __launch_bounds__(kThreads) void k_exp_kat(const double *x, double *y
     y[i] = sig ? agexp::sigmoid(x[i], s_tab) : agexp::exp(x[i], s_tab);
 }
 
+// Streaming copy, 16 B per lane, non-temporal both ways (bench.py's measured HBM peak):
+// 4 independent 16-B loads in flight per lane per step.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(kThreads) void k_stream_copy(const u32x4 *__restrict__ src, u32x4 *__restrict__ dst,
+                                                          int64_t n16) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = __builtin_nontemporal_load(src + i + q * stride);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(v[q], dst + i + q * stride);
+  }
+  for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
 // ------------------------------------------------------------------------------------
 // dispatch
 // ------------------------------------------------------------------------------------
@@ -356,12 +373,24 @@ int simulate_oracle(ag_ctx *c, OraKernel k, int64_t B, const ag_batch_in *in, co
     return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
   if (lds > 64 * 1024)
     AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  int &res = c->resident_ora[(prm.want_counters ? 1 : 0) + (in ? 0 : 2)];
-  if (res == 0)
-    if (int rc = resident_blocks(c, (const void *)k, lds, &res)) return rc;
-  // a lane resolves at most kOraPerLane auctions per launch (8-bit packed counts, replica
-  // sums in range): larger batches run as consecutive launches
-  int64_t chunk_max = (int64_t)res * kThreads * kOraPerLane;
+  int &res_max = c->resident_ora[(prm.want_counters ? 1 : 0) + (in ? 0 : 2)];
+  if (res_max == 0)
+    if (int rc = resident_blocks(c, (const void *)k, lds, &res_max)) return rc;
+  // Persistent grid of kOraBlocksPerCu workgroups per CU (AG_OPT_SIM_BLOCKS_PER_CU overrides):
+  // fewer than the 5 the registers allow streams better (tools/ab_oracle.py: 4 per CU 0.473 ms
+  // vs 5 per CU 0.503 ms on one box, equal on another; a 16-B copy likewise runs faster on
+  // 4 persistent workgroups per CU than on 8 or 16, tools/floor/copy_peak.py)
+  int res = res_max;
+  {
+    const int per_cu = c->grid_per_cu > 0 ? c->grid_per_cu : kOraBlocksPerCu;
+    int cus = 0;
+    AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    if ((int64_t)per_cu * cus < res) res = per_cu * cus;
+  }
+  // a lane resolves at most ora_lane_cap(R) auctions per launch (replica sums in range):
+  // larger batches run as consecutive launches
+  int64_t chunk_max = (int64_t)res * kThreads * ora_lane_cap(prm.L.replicas);
+  if (chunk_max > INT32_MAX) chunk_max = INT32_MAX;
   if (c->launch_cap > 0 && c->launch_cap < chunk_max) chunk_max = c->launch_cap;
   if (chunk_max < 1) chunk_max = 1;
   const int nc = s.num_agents * kC;
@@ -586,6 +615,10 @@ int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
       return AG_OK;
     case AG_OPT_BIDDER_RECORD_CACHE:
       c->bidder_cache = value;
+      return AG_OK;
+    case AG_OPT_SIM_BLOCKS_PER_CU:
+      if (value < 0 || value > 64) return ag_set_error(AG_ERR_INVALID, "ag_set_option: blocks per CU in [0, 64]");
+      c->grid_per_cu = (int32_t)value;
       return AG_OK;
     case AG_OPT_SIMULATE_KERNEL:
       if (value != AG_SIM_KERNEL_AUTO && value != AG_SIM_KERNEL_GENERIC)
@@ -825,6 +858,23 @@ int ag_sigmoid(const double *z, double *o, int64_t n, void *stream) {
   if (n <= 0) return AG_OK;
   const int grid = grid_for(n, (int64_t)1 << 40);
   hipLaunchKernelGGL(k_exp_kat, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, z, o, n, 1);
+  AG_HIP(hipGetLastError());
+  return AG_OK;
+}
+
+int ag_stream_copy(const void *src, void *dst, int64_t nbytes, void *stream) {
+  if ((!src || !dst) && nbytes > 0) return ag_set_error(AG_ERR_INVALID, "ag_stream_copy: null argument");
+  if (nbytes < 0 || nbytes % 16 || ((uintptr_t)src | (uintptr_t)dst) % 16)
+    return ag_set_error(AG_ERR_INVALID, "ag_stream_copy: nbytes and both pointers must be multiples of 16");
+  if (nbytes == 0) return AG_OK;
+  int dev = 0, cus = 0;
+  AG_HIP(hipGetDevice(&dev));
+  AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int64_t n16 = nbytes / 16;
+  const int64_t tiles = (n16 + kThreads - 1) / kThreads;
+  const int grid = (int)(tiles < (int64_t)cus * 8 ? tiles : (int64_t)cus * 8);
+  hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, (const u32x4 *)src,
+                     (u32x4 *)dst, n16);
   AG_HIP(hipGetLastError());
   return AG_OK;
 }

@@ -35,11 +35,19 @@ namespace ag {
 constexpr int kOraSlotGross = 0, kOraSlotPaid = 1, kOraSlotUnderbid1 = 1, kOraSlotOverbid = 2,
               kOraSlotBestEv = 3, kOraSlotCounts = 4;  // counts only when N > 8 (else registers)
 constexpr int kOraStride = 5;      // qwords per (agent, replica): odd -> lanes spread over banks
-constexpr int kOraPerLane = 255;   // auctions a lane resolves per launch (8-bit packed counts)
 // Catalogue values must lie in (0, kOraMaxValue): then every counter term is < 2^10 (bids,
-// prices, best EVs and clicked values are <= max value), its fixed-point image < 2^46, and
-// a replica sums at most kOraPerLane * 256 terms per slot: < 2^62, no int64 overflow.
+// prices, best EVs and clicked values are <= max value) and its fixed-point image < 2^46.
+// A replica column is shared by 256 / R lanes, each adding at most one term per slot per
+// auction, so with at most ora_lane_cap(R) = 512 R auctions per lane per launch a replica
+// sums fewer than 2^17 terms: |sum| < 2^63, no int64 overflow. Participation counts are
+// 8-bit fields in registers, flushed to LDS every kOraFlush auctions.
 constexpr double kOraMaxValue = 1024.0;
+#ifndef AG_ORA_PREFETCH
+#define AG_ORA_PREFETCH 0  // software-pipelined input loads (A/B: make variant VFLAGS=-DAG_ORA_PREFETCH=1)
+#endif
+constexpr int kOraFlush = 255;
+constexpr int kOraBlocksPerCu = 4;  // default persistent grid (ag_kernels.hip simulate_oracle)
+__host__ inline int64_t ora_lane_cap(int R) { return 512 * (int64_t)R; }
 
 struct OraLayout {
   int32_t tab, items, values, scr, scr_val, amax, cnt, total;
@@ -196,11 +204,35 @@ __global__ __launch_bounds__(kThreads) void k_oracle(OraParams prm) {
   const uint32_t agent_bytes = (uint32_t)R * kOraStride * 8;
   const uint32_t lane_off = (uint32_t)(tid & (R - 1)) * kOraStride * 8;
   uint64_t n_logs_packed = 0, n_won_packed = 0;
+  int since_flush = 0;
   auto cadd = [&](uint32_t addr, int slot, unsigned long long v) {
     atomicAdd(reinterpret_cast<unsigned long long *>(s_cnt + addr + slot * 8), v);
   };
+  auto flush_counts = [&]() {  // the 8-bit per-agent fields -> the LDS count slot
+    for (int a = 0; a < N; ++a) {
+      const uint64_t v = ((n_logs_packed >> (8 * a)) & 255ull) | (((n_won_packed >> (8 * a)) & 255ull) << 32);
+      if (v) cadd((uint32_t)a * agent_bytes + lane_off, kOraSlotCounts, (unsigned long long)v);
+    }
+    n_logs_packed = 0;
+    n_won_packed = 0;
+    since_flush = 0;
+  };
 
-  for (uint32_t i = lo + blockIdx.x * kThreads + tid; i < hi; i += gridDim.x * kThreads) {
+  const uint32_t stride = gridDim.x * kThreads;
+#if AG_ORA_PREFETCH
+  // the next auction's inputs are in flight while this one resolves
+  double xn[kMaxD], un = 0.0;
+  int an[P];
+  if (!GEN && lo + blockIdx.x * kThreads + tid < hi) {
+    const uint32_t i0 = lo + blockIdx.x * kThreads + tid;
+#pragma unroll
+    for (int e = 0; e < D - 1; ++e) xn[e] = ldg(prm.ctx + e * B + i0);
+#pragma unroll
+    for (int s = 0; s < P; ++s) an[s] = ldg(prm.part + s * B + i0);
+    un = ldg(prm.u + i0);
+  }
+#endif
+  for (uint32_t i = lo + blockIdx.x * kThreads + tid; i < hi; i += stride) {
     double x[kMaxD];
     float xf[kMaxD];
     float xabs = 1.0f;
@@ -210,11 +242,26 @@ __global__ __launch_bounds__(kThreads) void k_oracle(OraParams prm) {
       gen_auction<P, kMaxD>((uint32_t)prm.seed, (uint32_t)(prm.seed >> 32), prm.first + i, N, P, D - 1,
                             prm.scale, x, ag, u);
     } else {
+#if AG_ORA_PREFETCH
+#pragma unroll
+      for (int e = 0; e < D - 1; ++e) x[e] = xn[e];
+#pragma unroll
+      for (int s = 0; s < P; ++s) ag[s] = an[s];
+      u = un;
+      if (i + stride < hi) {
+#pragma unroll
+        for (int e = 0; e < D - 1; ++e) xn[e] = ldg(prm.ctx + e * B + i + stride);
+#pragma unroll
+        for (int s = 0; s < P; ++s) an[s] = ldg(prm.part + s * B + i + stride);
+        un = ldg(prm.u + i + stride);
+      }
+#else
 #pragma unroll
       for (int e = 0; e < D - 1; ++e) x[e] = ldg(prm.ctx + e * B + i);
 #pragma unroll
       for (int s = 0; s < P; ++s) ag[s] = ldg(prm.part + s * B + i);
       u = ldg(prm.u + i);
+#endif
     }
 #pragma unroll
     for (int e = 0; e < D - 1; ++e) {
@@ -316,17 +363,12 @@ __global__ __launch_bounds__(kThreads) void k_oracle(OraParams prm) {
           cadd(addr, kOraSlotCounts, won ? 0x100000001ull : 1ull);
         }
       }
+      if (packed && ++since_flush == kOraFlush) flush_counts();
     }
   }
 
   if (!prm.want_counters) return;
-  if (packed) {
-    const uint32_t lane_addr = lane_off;
-    for (int a = 0; a < N; ++a) {
-      const uint64_t v = ((n_logs_packed >> (8 * a)) & 255ull) | (((n_won_packed >> (8 * a)) & 255ull) << 32);
-      if (v) cadd((uint32_t)a * agent_bytes + lane_addr, kOraSlotCounts, (unsigned long long)v);
-    }
-  }
+  if (packed) flush_counts();
   __syncthreads();
   // per (agent, slot): the replicas summed as two limbs (value = lo + hi * 2^42; counts:
   // logs in lo, wins in hi), then the block's partials in k_simulate's format

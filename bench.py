@@ -44,7 +44,8 @@ SP_ORACLE = {"random_seed": 0, "num_runs": 3, "num_iter": 20, "rounds_per_iter":
                          "bidder": {"type": "TruthfulBidder", "kwargs": {}}}],
              "output_dir": "results/SP_Oracle/"}
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured copy ~6290
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); the measured copy peak is
+#                        measured live (measured_copy_peak) and reported beside it
 
 
 def algorithmic_bytes_per_auction(E, P, first_price):
@@ -67,6 +68,38 @@ def catalogue(cfg=None):
         os.unlink(f.name)
     names = [c["name"] for c in agent_configs]
     return np.stack([a2i[n] for n in names]), np.stack([a2v[n] for n in names])
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def measured_copy_peak(nbytes=1 << 32, reps=20):
+    """HBM bandwidth of a 16-B non-temporal streaming copy (ag_stream_copy) of nbytes:
+    (read + write bytes) / time, HIP events on the launch stream."""
+    from auctiongym_amd.engine import stream_copy
+    src = torch.empty(nbytes // 8, dtype=torch.float64, device="cuda")
+    dst = torch.empty_like(src)
+    src.fill_(1.0)
+    for _ in range(10):
+        stream_copy(src, dst)
+    st = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    for _ in range(reps):
+        stream_copy(src, dst)
+    b.record(st)
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / reps
+    del src, dst
+    return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
 def cpu_baseline(items, values, inp, sample, threads, min_seconds=10.0, max_passes=40):
@@ -377,7 +410,11 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=60,
                     help="untimed steps first (lets the clocks settle under sustained load)")
-    ap.add_argument("--batch", type=int, default=1 << 24, help="auctions per GPU per step")
+    ap.add_argument("--batch", type=int, default=1 << 27,
+                    help="auctions per GPU per step (2^27: 19 GB of inputs + outputs resident in HBM; a "
+                         "step of ~3.5 ms keeps the driver's few warm-up steps past the clock ramp of a "
+                         "fresh process, DESIGN.md section 6)")
+    ap.add_argument("--no-generate", action="store_true", help="skip the generate-mode line")
     ap.add_argument("--cpu-sample", type=int, default=1 << 24)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu_count)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -457,6 +494,47 @@ def main():
     bpa = algorithmic_bytes_per_auction(E, P, first_price=False)
     achieved = bpa * B / (kern_ms * 1e-3) / 1e9
 
+    gen = None
+    if not args.no_generate:
+        # generate mode: the same workload with the inputs drawn inside the
+        # kernel (ag_simulate_generated: the bits ag_generate wrote), writes only
+        def gstep(i=None):
+            cnt.zero_()
+            if i is not None:
+                ev[i][0].record(stream)
+            eng.simulate_generated(0, lo, out, cnt)
+            if i is not None:
+                ev[i][1].record(stream)
+            if world > 1:
+                allreduce_counters(cnt)
+        for _ in range(args.warmup):
+            gstep()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        for i in range(args.steps):
+            gstep(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        gel = time.perf_counter() - g0
+        gk = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        if world > 1:
+            t = torch.tensor([gel, gk], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            gel, gk = float(t[0]), float(t[1])
+        wb = bpa - (8 * E + 4 * P + 8)  # the writes alone
+        gen = {"workload": "the headline workload in generate mode: contexts, participants and uniforms "
+                           "drawn on the chip (Philox4x32-10, the bits ag_generate writes); outputs identical",
+               "value": B * world * args.steps / gel, "unit": "auctions/s", "ms_per_step": gel / args.steps * 1e3,
+               "kernel_ms": gk, "algorithmic_bytes_per_auction": wb,
+               "roofline": {"bound": "hbm (writes) / FP64 VALU (Philox + Box-Muller)",
+                            "achieved": wb * B / (gk * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": wb * B / (gk * 1e-3) / 1e9 / HBM_PEAK_GBS}}
+    peak_meas = measured_copy_peak()
+
     traffic = None
     traffic_src = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -486,12 +564,19 @@ def main():
                    "auctions_per_gpu_per_step": B, "global_batch": B * world,
                    "parallelism": f"dp{world} (independent auction shards; int64 counter all-reduce)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "peak_measured": peak_meas, "frac_of_measured": achieved / peak_meas,
+                     "peak_measured_what": "ag_stream_copy: 4 GiB -> 4 GiB, 16-B non-temporal loads/stores, "
+                                           "(read + write bytes) / time",
+                     "traffic": traffic,
                      "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
                      "traffic_source": traffic_src,
-                     "kernel": "ag_simulate (k_simulate + k_reduce_counters)",
+                     "kernel": "ag_simulate (k_oracle + k_reduce_counters)",
                      "kernel_ms": kern_ms, "algorithmic_bytes_per_auction": bpa},
     }
+
+    if gen is not None:
+        result["generate_mode"] = gen
 
     if not args.no_ts:
         result["configs_1"] = run_sp_ts(args.ts_batch, args.steps, args.warmup, world, rank, local,
@@ -509,11 +594,19 @@ def main():
         gpu_bid = out["bid"][:, :sample].cpu().numpy().T
         same = bool(np.array_equal(gpu_bid, o["bid"]) and
                     np.array_equal(out["winner"][:sample].cpu().numpy(), o["winner"]))
+        s1 = min(1 << 22, sample)
+        cps1, dt1, passes1, _ = cpu_baseline(items, values, inp, s1, 1, min_seconds=5.0)
         result["cpu_baseline"] = {
             "value": cps, "unit": "auctions/s", "cores": threads, "kind": "port",
             "sample": f"{passes} passes over {sample} auctions of the same synthetic batch, "
                       f"oracle/ag_oracle.c (OpenMP, {threads} threads), {dt:.1f} s; "
-                      f"outputs identical to GPU: {same}"}
+                      f"outputs identical to GPU: {same}",
+            "one_core": {"value": cps1, "unit": "auctions/s", "cores": 1,
+                         "sample": f"{passes1} passes over {s1} auctions, 1 thread, {dt1:.1f} s"},
+            "nproc": os.cpu_count(), "threads_available": len(os.sched_getaffinity(0)),
+            "cpu_model": cpu_model(),
+            "reference_itself": "12.8k auctions/s on one core of the survey container (the reference's "
+                                "Python/numpy path, BASELINE.md section 2; it cannot run on the GPU box)"}
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

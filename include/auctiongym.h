@@ -210,7 +210,9 @@ typedef enum ag_option {
   AG_OPT_BIDDER_RECORD_CACHE = 6, /* value: most records per workgroup the learning bidders'
                                    trainer stages in LDS (-1 = default: as many as fit; 0 = none,
                                    every epoch reads the store); identical results */
-  AG_OPT_SIMULATE_KERNEL = 7      /* value: ag_sim_kernel; identical results */
+  AG_OPT_SIMULATE_KERNEL = 7,     /* value: ag_sim_kernel; identical results */
+  AG_OPT_SIM_BLOCKS_PER_CU = 8    /* value: workgroups per CU of the Oracle kernel's persistent
+                                     grid (0 = default 4, capped by what fits); identical results */
 } ag_option;
 
 typedef enum ag_sim_kernel {
@@ -406,6 +408,11 @@ int ag_counters_to_double(const int64_t *counters_fx, int64_t n, double *out);
  * src/Models.py:10-12 sigmoid with glibc-2.35-identical exp, and that exp alone. */
 int ag_sigmoid(const double *z, double *out, int64_t n, void *stream);
 int ag_exp(const double *x, double *out, int64_t n, void *stream);
+
+/* Measurement hook (bench.py's measured HBM peak beside the 8 TB/s spec): copy nbytes
+ * (multiple of 16, 16-B aligned dev pointers) with 16-B non-temporal loads and stores on the
+ * current device, stream-ordered. */
+int ag_stream_copy(const void *src, void *dst, int64_t nbytes, void *stream);
 
 /* Thread-local description of the last error. */
 const char *ag_last_error(void);

@@ -37,6 +37,7 @@ def main():
     for n, p in paths.items():
         e = AuctionEngine(6, 2, 12, 5, 4, _lib.SECOND_PRICE, 1.0, device=0, lib_path=p)
         e.load_catalog(items, values)
+        e.set_blocks_per_cu(int(os.environ.get("AG_BPC", "0")))
         engs[n] = e
     base = engs["base"]
     inp = base.alloc_inputs(B)

@@ -27,23 +27,30 @@ def main():
     inp = eng.alloc_inputs(B)
     eng.generate(0, 0, inp)
     fields = ("winner", "price", "outcome", "item", "bid", "est_ctr", "true_ctr", "best_ev")
-    out = {False: eng.alloc_outputs(B, fields), True: eng.alloc_outputs(B, fields)}
-    cnt = {False: eng.new_counters(), True: eng.new_counters()}
+    # variants: (generic kernel?, blocks per CU)
+    variants = [(False, 0), (True, 0), (False, 1), (False, 2), (False, 3), (False, 4)]
+    out = {v: eng.alloc_outputs(B, fields) for v in variants}
+    cnt = {v: eng.new_counters() for v in variants}
     st = torch.cuda.current_stream()
+    def use(v):
+        eng.set_simulate_kernel(v[0])
+        eng.set_blocks_per_cu(v[1])
     for _ in range(150):
-        eng.simulate(inp, out[False], cnt[False])
-    for g in (False, True):
-        eng.set_simulate_kernel(g)
+        eng.simulate(inp, out[variants[0]], cnt[variants[0]])
+    for g in variants:
+        use(g)
         cnt[g].zero_()
         eng.simulate(inp, out[g], cnt[g])
     torch.cuda.synchronize()
-    same = all(torch.equal(out[False][k], out[True][k]) for k in fields) and torch.equal(cnt[False], cnt[True])
+    v0 = variants[0]
+    same = all(all(torch.equal(out[v0][k], out[g][k]) for k in fields) and torch.equal(cnt[v0], cnt[g])
+               for g in variants)
     print("outputs and counters identical:", same, flush=True)
-    iso = {False: [], True: []}
-    sus = {False: [], True: []}
+    iso = {g: [] for g in variants}
+    sus = {g: [] for g in variants}
     for r in range(12):
-        for g in (False, True):
-            eng.set_simulate_kernel(g)
+        for g in variants:
+            use(g)
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(st)
             eng.simulate(inp, out[g], cnt[g])
@@ -58,7 +65,8 @@ def main():
             torch.cuda.synchronize()
             sus[g].append(a.elapsed_time(b) / 20)
     bpa = bench.algorithmic_bytes_per_auction(5, 2, False)
-    for g, name in ((False, "k_oracle"), (True, "k_simulate (general)")):
+    for g in variants:
+        name = ("k_simulate (general)" if g[0] else "k_oracle") + (f" {g[1]}/CU" if g[1] else "")
         mi, ms = float(np.median(iso[g])), float(np.median(sus[g]))
         print(f"{name:22s} isolated {mi:.4f} ms ({bpa * B / mi / 1e6:6.0f} GB/s)  "
               f"back-to-back (+counter zeroing) {ms:.4f} ms ({bpa * B / ms / 1e6:6.0f} GB/s)")

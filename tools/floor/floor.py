@@ -43,6 +43,8 @@ def main():
         "floor persistent 8 blocks/CU": lambda: L.floor_run(1, cus * 8, ctypes.byref(p), B, sp),
         "floor persistent 4 blocks/CU": lambda: L.floor_run(1, cus * 4, ctypes.byref(p), B, sp),
         "floor persistent nt 8 blocks/CU": lambda: L.floor_run(2, cus * 8, ctypes.byref(p), B, sp),
+        "floor w2 nt 8 blocks/CU": lambda: L.floor_run(3, cus * 8, ctypes.byref(p), B, sp),
+        "floor w2 nt 4 blocks/CU": lambda: L.floor_run(3, cus * 4, ctypes.byref(p), B, sp),
         "floor one tile per block": lambda: L.floor_run(0, 0, ctypes.byref(p), B, sp),
         "ag_simulate (bench)": lambda: eng.simulate(inp, out, cnt),
         "ag_simulate, no counters": lambda: eng.simulate(inp, out, None),
@@ -52,6 +54,10 @@ def main():
     dst = torch.empty(56 * B // 8, dtype=torch.float64, device="cuda")
     fill = torch.empty(29 * B // 8, dtype=torch.float64, device="cuda")
     runs["torch copy+fill of the same bytes"] = lambda: (dst.copy_(src), fill.fill_(1.0))
+    from auctiongym_amd.engine import stream_copy
+    big = torch.empty(141 * B // 16, dtype=torch.float64, device="cuda")  # 141 B per auction moved
+    big2 = torch.empty_like(big)
+    runs["ag_stream_copy of 141 B/auction (read+write)"] = lambda: stream_copy(big, big2)
     for _ in range(200):
         for f in runs.values():
             f()

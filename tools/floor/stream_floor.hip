@@ -43,6 +43,36 @@ __device__ __forceinline__ void one(const Ptrs &p, int64_t B, int64_t i) {
   S<NT>(p.bev + B + i, u);
 }
 
+// two consecutive auctions per lane: 16-B f64 accesses, 8-B int32 pairs, 2-B outcome pairs
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void two(const Ptrs &p, int64_t B, int64_t i) {
+  auto L2 = [&](const double *q) { return __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(q)); };
+  auto S2 = [&](double *q, f64x2 v) { __builtin_nontemporal_store(v, reinterpret_cast<f64x2 *>(q)); };
+  f64x2 x0 = L2(p.ctx + i), x1 = L2(p.ctx + B + i), x2 = L2(p.ctx + 2 * B + i), x3 = L2(p.ctx + 3 * B + i),
+        x4 = L2(p.ctx + 4 * B + i);
+  i32x2 a0 = __builtin_nontemporal_load(reinterpret_cast<const i32x2 *>(p.part + i));
+  i32x2 a1 = __builtin_nontemporal_load(reinterpret_cast<const i32x2 *>(p.part + B + i));
+  f64x2 u = L2(p.u + i);
+  f64x2 s = x0 + x1 + x2 + x3 + x4;
+  __builtin_nontemporal_store(i32x2{a0.x > a1.x, a0.y > a1.y}, reinterpret_cast<i32x2 *>(p.winner + i));
+  S2(p.price + i, s * u);
+  __builtin_nontemporal_store((uint16_t)((u.x > 0.5) | ((u.y > 0.5) << 8)), reinterpret_cast<uint16_t *>(p.outcome + i));
+  __builtin_nontemporal_store(a0, reinterpret_cast<i32x2 *>(p.item + i));
+  __builtin_nontemporal_store(a1, reinterpret_cast<i32x2 *>(p.item + B + i));
+  S2(p.bid + i, s);
+  S2(p.bid + B + i, s + u);
+  S2(p.est + i, x0);
+  S2(p.est + B + i, x1);
+  S2(p.tru + i, x2);
+  S2(p.tru + B + i, x3);
+  S2(p.bev + i, x4);
+  S2(p.bev + B + i, u);
+}
+__global__ __launch_bounds__(256) void k_floor_w2(Ptrs p, int64_t B) {
+  for (int64_t i = 2 * ((int64_t)blockIdx.x * 256 + threadIdx.x); i < B; i += 2 * (int64_t)gridDim.x * 256) two(p, B, i);
+}
+
 __global__ __launch_bounds__(256) void k_floor_persistent(Ptrs p, int64_t B) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < B; i += (int64_t)gridDim.x * 256) one(p, B, i);
 }
@@ -55,11 +85,44 @@ __global__ __launch_bounds__(256) void k_floor_tiles(Ptrs p, int64_t B) {
 }
 
 extern "C" int floor_run(int persistent, int grid, const Ptrs *p, int64_t B, void *stream) {
-  if (persistent == 2)
+  if (persistent == 3)
+    hipLaunchKernelGGL(k_floor_w2, dim3(grid), dim3(256), 0, (hipStream_t)stream, *p, B);
+  else if (persistent == 2)
     hipLaunchKernelGGL(k_floor_persistent_nt, dim3(grid), dim3(256), 0, (hipStream_t)stream, *p, B);
   else if (persistent)
     hipLaunchKernelGGL(k_floor_persistent, dim3(grid), dim3(256), 0, (hipStream_t)stream, *p, B);
   else
     hipLaunchKernelGGL(k_floor_tiles, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, *p, B);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// copy variants (the measured HBM peak): 16 B per lane
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__global__ __launch_bounds__(256) void k_copy_persist(const u32x4 *src, u32x4 *dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    if constexpr (NT) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+    else dst[i] = src[i];
+  }
+}
+template <bool NT>
+__global__ __launch_bounds__(256) void k_copy_tiles(const u32x4 *src, u32x4 *dst, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    if constexpr (NT) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+    else dst[i] = src[i];
+  }
+}
+extern "C" int copy_run(int variant, int grid, const void *src, void *dst, int64_t nbytes, void *stream) {
+  const int64_t n = nbytes / 16;
+  const u32x4 *s = (const u32x4 *)src;
+  u32x4 *d = (u32x4 *)dst;
+  hipStream_t st = (hipStream_t)stream;
+  switch (variant) {
+    case 0: hipLaunchKernelGGL(k_copy_persist<false>, dim3(grid), dim3(256), 0, st, s, d, n); break;
+    case 1: hipLaunchKernelGGL(k_copy_persist<true>, dim3(grid), dim3(256), 0, st, s, d, n); break;
+    case 2: hipLaunchKernelGGL(k_copy_tiles<false>, dim3((n + 255) / 256), dim3(256), 0, st, s, d, n); break;
+    case 3: hipLaunchKernelGGL(k_copy_tiles<true>, dim3((n + 255) / 256), dim3(256), 0, st, s, d, n); break;
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
