@@ -8,6 +8,8 @@ sees the same values.
 """
 import math
 
+import numpy as np
+
 from . import _lib
 from .Impression import ImpressionOpportunity
 
@@ -39,6 +41,7 @@ class Agent:
         self._index = None
         self._fx = [0] * _lib.NUM_COUNTERS
         self._log_start = 0
+        self._call_logs = []
 
     # engine plumbing --------------------------------------------------------
     def _attach(self, auction, index):
@@ -64,17 +67,40 @@ class Agent:
 
     @property
     def logs(self):
-        """Materialised ImpressionOpportunity records of the current iteration."""
+        """Materialised ImpressionOpportunity records of the current iteration: the auction's
+        rounds (from the device SoA outputs), then any per-call Agent.bid records."""
         self._sync()
-        if self._auction is None:
-            return []
-        return self._auction._materialise_logs(self._index, self._log_start)
+        recs = [] if self._auction is None else self._auction._materialise_logs(self._index, self._log_start)
+        return recs + self._call_logs
+
+    # the per-call surface (src/Agent.py:29-68): one request through the GPU plugins
+    def select_item(self, context):
+        """src/Agent.py:29-42: the allocator's CTR estimates (ag_estimate_ctr), the first
+        argmax of CTR * value, and for Thompson sampling the MAP CTR of that item."""
+        from .BidderAllocation import PyTorchLogisticRegressionAllocator
+        estim = self.allocator.estimate_CTR(context)
+        best = int(np.argmax(estim * self.item_values))
+        if type(self.allocator) is PyTorchLogisticRegressionAllocator and self.allocator.thompson_sampling:
+            return best, self.allocator.estimate_CTR(context, sample=False)[best]
+        return best, estim[best]
+
+    def bid(self, context):
+        """src/Agent.py:44-68: select_item, the bidder's bid (ag_bid for shading bidders), and
+        the log record (kept with this agent's logs until clear_logs)."""
+        best, ctr = self.select_item(context)
+        value = self.item_values[best]
+        b = self.bidder.bid(value, context, ctr)
+        self._call_logs.append(ImpressionOpportunity(
+            context=context, item=best, value=value, bid=b, best_expected_value=0.0, true_CTR=0.0,
+            estimated_CTR=ctr, price=0.0, second_price=0.0, outcome=False, won=False))
+        return b, best
 
     def update(self, iteration, plot=False, figsize=(8, 5), fontsize=14):
         """src/Agent.py:79-94. Oracle / Truthful updates are no-ops (src/BidderAllocation.py:
-        17-18, src/Bidder.py:21-22); the LR-TS allocator trains on the GPU over this agent's
-        won samples (Auction._update_agent); shading bidders' updates are not built yet and
-        raise NotImplementedError."""
+        17-18, src/Bidder.py:21-22); every learner trains on the GPU from the device record
+        stores of its rounds (Auction._update_agent): the LR-TS allocator on its won samples
+        (ag_lrts_update), EmpiricalShadedBidder (ag_empirical_update) and the learning bidders
+        (ag_bidder_update) on all of its records."""
         self._sync()
         if self._auction is not None:
             self._auction._update_agent(self._index, iteration)
@@ -122,14 +148,17 @@ class Agent:
         if self._auction is not None:
             self._log_start = self._auction._log_rounds()
             self._auction._cleared_logs(self._index)
+        self._call_logs = self._call_logs[-self.memory:] if self.memory else []
         self.bidder.clear_logs(memory=self.memory)
 
     def __repr__(self):
         return f"Agent({self.name!r})"
 
 
-def _records(part, out, agent, first_round, values):
-    """Build ImpressionOpportunity rows of `agent` from host copies of one batch."""
+def _records(part, out, ctx, agent, first_round, values, obs=None):
+    """Build ImpressionOpportunity rows of `agent` from host copies of one batch. ctx [E][B]:
+    the record's context is the true context + intercept, or (obs = OE) its first OE entries
+    + intercept (src/Auction.py:33-36)."""
     recs = []
     P, B = part.shape
     for r in range(B):
@@ -139,8 +168,10 @@ def _records(part, out, agent, first_round, values):
             charged = P >= 2
             won = charged and out["winner"][r] == s
             it = int(out["item"][s, r])
+            c = ctx[:, r] if obs is None else ctx[:obs, r]
             recs.append(ImpressionOpportunity(
-                context=None, item=it, value=float(values[agent][it]), bid=float(out["bid"][s, r]),
+                context=np.concatenate((c, [1.0])), item=it, value=float(values[agent][it]),
+                bid=float(out["bid"][s, r]),
                 best_expected_value=float(out["best_ev"][s, r]),
                 true_CTR=float(out["true_ctr"][s, r]), estimated_CTR=float(out["est_ctr"][s, r]),
                 price=float(out["price"][r]) if charged else 0.0,
@@ -149,19 +180,20 @@ def _records(part, out, agent, first_round, values):
     return recs
 
 
-def materialise(batches, agent, start_round, values):
+def materialise(batches, agent, start_round, values, obs=None):
     recs = []
     base = 0
-    for part, out in batches:
+    for part, out, ctx in batches:
         B = part.shape[1]
         if base + B > start_round:
             p = part.cpu().numpy()
+            c = ctx.cpu().numpy()
             o = {k: v.cpu().numpy() for k, v in out.items()}
             lo = max(0, start_round - base)
             if lo:
-                p = p[:, lo:]
+                p, c = p[:, lo:], c[:, lo:]
                 o = {k: (v[:, lo:] if v.ndim == 2 else v[lo:]) for k, v in o.items()}
-            recs.extend(_records(p, o, agent, base + lo, values))
+            recs.extend(_records(p, o, c, agent, base + lo, values, obs))
         base += B
     return recs
 

@@ -256,7 +256,7 @@ class Auction:
                     paid += v
         self._revenue_fx += paid
         if self.keep_logs:
-            self._log_batches.append((inp["part"], out))
+            self._log_batches.append((inp["part"], out, inp["ctx"]))
         self._logged_rounds += B
 
     # ------------------------------------------------------------------ Agent.update
@@ -348,45 +348,11 @@ class Auction:
             self._update_learner(index)
         self._claimed.add(index)
 
-    NOISE_EPOCHS0 = 2048
-
     def _update_learner(self, index):
-        """One learning bidder's update (ag_bidder_update with a one-agent mask). The DR and
-        ValueLearning 'policy' fits draw one rsample per record per epoch from torch's global
-        generator (src/Models.py:160, :87): the draws are made here, on the host, with the same
-        torch calls, for a growing epoch budget (the fit's length is only known after it ran;
-        a fit that exhausts its budget is re-run with twice as many epochs, same result), and
-        the generator is left exactly where the reference's is after the update (including the
-        rsample of every record after DR / PolicyLearning fits, src/Bidder.py:605, :423)."""
+        """One learning bidder's update (ag_bidder_update with a one-agent mask)."""
         eng = self._engine
-        b = self.agents[index].bidder
         st = self._stores.get("shading") or eng.new_shading_samples(1, learning=True)
-        n = int(eng.shading_counts(st)[index])
-        mask = np.zeros(len(self.agents), np.int32)
-        mask[index] = 1
-        offs = np.zeros(len(self.agents), np.int64)
-        noisy = b.kind == _lib.BIDDER_DOUBLY_ROBUST or (b.kind == _lib.BIDDER_VALUE_LEARNING
-                                                         and b.inference == "policy")
-        if noisy and n > 0:
-            max_ep = 32768 if b.kind == _lib.BIDDER_DOUBLY_ROBUST else 16384
-            stream = _TorchNoise(n, eng.device)
-            E = min(self.NOISE_EPOCHS0, max_ep)
-            while True:
-                ep, stat = eng.bidder_update(st, stream.upto(E), offs, E, agents=mask)
-                if stat[index] != -3 or E >= max_ep:
-                    break
-                E = min(2 * E, max_ep)
-            stream.rewind(int(ep[index, 2]))
-        else:
-            ep, stat = eng.bidder_update(st, None, offs, 0, agents=mask)
-        state, init = eng.dr_state()
-        b._load_state16(state[index])
-        b.model_initialised = bool(init[index] != _lib.LEARNER_UNINITIALISED)
-        b.epochs = ep[index].copy()
-        if stat[index] == 1:
-            print(f"! Fallback for {self.agents[index].name}")
-        if b.kind in (_lib.BIDDER_DOUBLY_ROBUST, _lib.BIDDER_POLICY_LEARNING) and n > 0:
-            torch.empty(n).normal_()  # pred_gammas = policy(X) after the fit
+        learner_update(eng, st, index, self.agents[index].bidder, self.agents[index].name)
 
     def _cleared_logs(self, index):
         if not self._learner[index]:
@@ -410,8 +376,11 @@ class Auction:
         return self._logged_rounds
 
     def _materialise_logs(self, agent_index, start_round):
+        # the context an agent bid on (src/Agent.py:55): the true context for an
+        # OracleAllocator agent, the observed one for the others (src/Auction.py:44-49)
+        oe = None if self.agents[agent_index].allocator.kind == _lib.ALLOCATOR_ORACLE else self.obs_embedding_size
         return _agent_mod.materialise(self._log_batches, agent_index,
-                                      start_round - self._log_base, self._values)
+                                      start_round - self._log_base, self._values, obs=oe)
 
     # ------------------------------------------------------------------ revenue
     @property
@@ -422,6 +391,49 @@ class Auction:
     def clear_revenue(self):
         self._flush()
         self._revenue_fx = 0
+
+
+NOISE_EPOCHS0 = 2048
+
+
+def learner_update(eng, store, index, bidder, name):
+    """Bidder.update of the learning bidder at engine slot `index` from the records of the
+    device store (ag_bidder_update with a one-agent mask), the bidder's host mirror refreshed
+    afterwards. The DR and ValueLearning 'policy' fits draw one rsample per record per epoch
+    from torch's global generator (src/Models.py:160, :87): the draws are made here, on the
+    host, with the same torch calls, for a growing epoch budget (the fit's length is only
+    known after it ran; a fit that exhausts its budget is re-run with twice as many epochs,
+    same result), and the generator is left exactly where the reference's is after the update
+    (including the rsample of every record after DR / PolicyLearning fits, src/Bidder.py:605,
+    :423). Returns the epochs [3] the fits ran."""
+    b = bidder
+    n = int(eng.shading_counts(store)[index])
+    mask = np.zeros(eng.N, np.int32)
+    mask[index] = 1
+    offs = np.zeros(eng.N, np.int64)
+    noisy = b.kind == _lib.BIDDER_DOUBLY_ROBUST or (b.kind == _lib.BIDDER_VALUE_LEARNING
+                                                     and b.inference == "policy")
+    if noisy and n > 0:
+        max_ep = 32768 if b.kind == _lib.BIDDER_DOUBLY_ROBUST else 16384
+        stream = _TorchNoise(n, eng.device)
+        E = min(NOISE_EPOCHS0, max_ep)
+        while True:
+            ep, stat = eng.bidder_update(store, stream.upto(E), offs, E, agents=mask)
+            if stat[index] != -3 or E >= max_ep:
+                break
+            E = min(2 * E, max_ep)
+        stream.rewind(int(ep[index, 2]))
+    else:
+        ep, stat = eng.bidder_update(store, None, offs, 0, agents=mask)
+    state, init = eng.dr_state()
+    b._load_state16(state[index])
+    b.model_initialised = bool(init[index] != _lib.LEARNER_UNINITIALISED)
+    b.epochs = ep[index].copy()
+    if stat[index] == 1:
+        print(f"! Fallback for {name}")
+    if b.kind in (_lib.BIDDER_DOUBLY_ROBUST, _lib.BIDDER_POLICY_LEARNING) and n > 0:
+        torch.empty(n).normal_()  # pred_gammas = policy(X) after the fit
+    return ep[index].copy()
 
 
 class _TorchNoise:
@@ -447,7 +459,9 @@ class _TorchNoise:
         return self.dev
 
     def rewind(self, e):
-        k = e // self.SNAP
+        # the nearest snapshot at or before epoch e (a fit that ran every epoch of the budget
+        # E returns e == E, one past the last snapshot taken), then replay forward to e
+        k = min(e // self.SNAP, len(self.snaps) - 1)
         torch.set_rng_state(self.snaps[k])
         for _ in range(e - k * self.SNAP):
             torch.empty(self.n).normal_()

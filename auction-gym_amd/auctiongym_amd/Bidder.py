@@ -25,8 +25,11 @@ class Bidder:
         self.truthful = False
 
     def update(self, contexts, values, bids, prices, outcomes, estimated_CTRs, won_mask, iteration,
-               plot, figsize, fontsize, name):
-        pass
+               plot=False, figsize=(8, 5), fontsize=14, name=""):
+        """The reference's base update is a no-op (src/Bidder.py:21-22); TruthfulBidder inherits
+        it. The shading and learning bidders override it (GPU updates)."""
+        if self.kind is None:
+            raise NotImplementedError(f"{type(self).__name__}.update: not a built plugin")
 
     def clear_logs(self, memory):
         pass
@@ -55,11 +58,28 @@ class _ShadingBidder(Bidder):
         self.kwargs = kw
         self.gammas = []
 
+    def bid(self, value, context, estimated_CTR):
+        """Bidder.bid (src/Bidder.py:47-58, :171-208, :348-367, :455-475) as one call: the draw
+        of the bidder's state on the host (numpy rng / torch generator, the reference's
+        calls), the bid rule on the GPU (ag_bid); gamma (and the propensity) are logged."""
+        from .plugin_gpu import shading_bid
+        return shading_bid(self, value, estimated_CTR)
+
 
 class EmpiricalShadedBidder(_ShadingBidder):
     """src/Bidder.py:38-153."""
 
     kind = _lib.BIDDER_EMPIRICAL_SHADED
+
+    def update(self, contexts, values, bids, prices, outcomes, estimated_CTRs, won_mask, iteration,
+               plot=False, figsize=(8, 5), fontsize=14, name=""):
+        """src/Bidder.py:60-147 called directly: the GPU update (ag_empirical_update) of the
+        logged gammas against these utilities; sets prev_gamma."""
+        from .plugin_gpu import empirical_update
+        empirical_update(self, values, prices, outcomes, won_mask)
+
+    def clear_logs(self, memory):
+        self.gammas = self.gammas[-memory:] if memory else []
 
 
 def _linear(n_in, n_out):
@@ -113,10 +133,20 @@ class _LearningBidder(_ShadingBidder):
             return _lib.LEARNER_UNINITIALISED
         return _lib.LEARNER_SEARCH if getattr(self, "inference", None) == "search" else _lib.LEARNER_POLICY
 
+    def update(self, contexts, values, bids, prices, outcomes, estimated_CTRs, won_mask, iteration,
+               plot=False, figsize=(8, 5), fontsize=14, name=""):
+        """The bidder's update (src/Bidder.py:204-325, :364-431, :473-615) called directly: the
+        GPU trainer (ag_bidder_update) on the logged gammas / propensities and these arrays."""
+        from .plugin_gpu import learner_update_call
+        learner_update_call(self, values, prices, outcomes, estimated_CTRs, won_mask, name)
+
     def clear_logs(self, memory):
         if not memory:
             self.gammas = []
             self.propensities = []
+        else:
+            self.gammas = self.gammas[-memory:]
+            self.propensities = self.propensities[-memory:]
 
 
 class ValueLearningBidder(_LearningBidder):

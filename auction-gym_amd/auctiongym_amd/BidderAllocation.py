@@ -21,7 +21,10 @@ class Allocator:
         self.rng = rng
 
     def update(self, contexts, items, outcomes, iteration, plot, figsize, fontsize, name):
-        pass
+        """The reference's base update is a no-op (src/BidderAllocation.py:17-18); OracleAllocator
+        inherits it. PyTorchLogisticRegressionAllocator overrides it (GPU trainer)."""
+        if self.kind is None:
+            raise NotImplementedError(f"{type(self).__name__}.update: not a built plugin")
 
 
 class OracleAllocator(Allocator):
@@ -35,6 +38,12 @@ class OracleAllocator(Allocator):
 
     def update_item_embeddings(self, item_embeddings):
         self.item_embeddings = item_embeddings
+
+    def estimate_CTR(self, context):
+        """sigmoid(item_embeddings @ context) (src/BidderAllocation.py:81-82) on the GPU, with
+        the simulate kernels' exact FP64 arithmetic (ag_estimate_ctr)."""
+        from .plugin_gpu import oracle_estimate_ctr
+        return oracle_estimate_ctr(self, context)
 
 
 class PyTorchLogisticRegression:
@@ -64,3 +73,16 @@ class PyTorchLogisticRegressionAllocator(Allocator):
         self.num_items = num_items
         self.epochs = None  # epochs run by the last update (None: not updated yet)
         super().__init__(rng)
+
+    def estimate_CTR(self, context, sample=True):
+        """src/BidderAllocation.py:67-68 on the GPU (ag_estimate_ctr): float32 CTRs [K] of the
+        observed context (with its intercept); with Thompson sampling (and sample=True) the
+        posterior draw is torch.normal(0, 1/sqrt(q)) from torch's global generator."""
+        from .plugin_gpu import lrts_estimate_ctr
+        return lrts_estimate_ctr(self, context, sample=sample)
+
+    def update(self, contexts, items, outcomes, iteration, plot=False, figsize=(8, 5), fontsize=14, name=""):
+        """src/BidderAllocation.py:29-65 called directly (outside an Auction, whose Agent.update
+        batches every LR-TS agent): the GPU trainer (ag_lrts_update) on these samples."""
+        from .plugin_gpu import lrts_update
+        lrts_update(self, contexts, items, outcomes)

@@ -38,7 +38,7 @@ EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params
            "ag_generate_noise", "ag_lrts_collect", "ag_lrts_update", "ag_lrts_read",
            "ag_shading_collect", "ag_empirical_update", "ag_set_dr_state", "ag_get_dr_state",
            "ag_shading_counts", "ag_dr_update", "ag_set_bidder_modes", "ag_bidder_update",
-           "ag_generate_search_grid", "ag_simulate_generated", "ag_stream_copy",
+           "ag_generate_search_grid", "ag_simulate_generated", "ag_stream_copy", "ag_estimate_ctr", "ag_bid",
            "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_last_error", "ag_abi_version")
 ABI_VERSION = 15
 LEARNER_UNINITIALISED, LEARNER_POLICY, LEARNER_SEARCH = 0, 1, 2
@@ -142,6 +142,8 @@ def load(path=None):
         "ag_sigmoid": (ctypes.c_int, [vp, vp, i64, vp]),
         "ag_exp": (ctypes.c_int, [vp, vp, i64, vp]),
         "ag_stream_copy": (ctypes.c_int, [vp, vp, i64, vp]),
+        "ag_estimate_ctr": (ctypes.c_int, [vp, i32, i64, vp, vp, vp, vp]),
+        "ag_bid": (ctypes.c_int, [vp, i32, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "ag_last_error": (ctypes.c_char_p, []),
         "ag_abi_version": (i32, []),
     }

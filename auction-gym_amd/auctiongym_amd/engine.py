@@ -301,6 +301,40 @@ class AuctionEngine:
                                              _stream()),
                     "ag_generate_noise")
 
+    # ---------------------------------------------------------------- per-call plugin surface
+    def _dev(self, a, dtype):
+        if a is None:
+            return None
+        t = a if torch.is_tensor(a) else torch.from_numpy(np.ascontiguousarray(a))
+        return t.to(device=self.device, dtype=dtype).contiguous()
+
+    def estimate_ctr(self, agent, contexts, noise=None):
+        """Allocator.estimate_CTR of `agent` for n contexts [n][E+1] (OracleAllocator: true
+        context with intercept) or [n][OE+1] (LR-TS: observed context with intercept); noise
+        [n][K][OE+1] float32 Thompson draws or None (MAP). Returns float64 [n][K] (device)."""
+        x = self._dev(contexts, torch.float64)
+        n = x.shape[0]
+        nz = self._dev(noise, torch.float32)
+        out = torch.empty((n, self.K), dtype=torch.float64, device=self.device)
+        self._check(self.L.ag_estimate_ctr(self._h, int(agent), n, _ptr(x), _ptr(nz), _ptr(out), _stream()),
+                    "ag_estimate_ctr")
+        return out
+
+    def bid(self, agent, values, ctrs, gamma_raw=None, policy_eps=None, gamma_grid=None):
+        """Bidder.bid of `agent` for n requests (ag_bid): values, estimated CTRs [n]; the
+        draws its state makes: gamma_raw [n], policy_eps [n], gamma_grid [n][128]. Returns
+        (bid, gamma, propensity) float64 [n] device tensors."""
+        v = self._dev(values, torch.float64).reshape(-1)
+        c = self._dev(ctrs, torch.float64).reshape(-1)
+        n = v.numel()
+        g = self._dev(gamma_raw, torch.float64)
+        e = self._dev(policy_eps, torch.float32)
+        gr = None if gamma_grid is None else self._dev(gamma_grid, torch.float64).reshape(n, 128).t().contiguous()
+        b, gm, pr = (torch.empty(n, dtype=torch.float64, device=self.device) for _ in range(3))
+        self._check(self.L.ag_bid(self._h, int(agent), n, _ptr(v), _ptr(c), _ptr(g), _ptr(e), _ptr(gr), _ptr(b),
+                                  _ptr(gm), _ptr(pr), _stream()), "ag_bid")
+        return b, gm, pr
+
     def allocate(self, bids):
         """Batched allocate: bids [P][B] (device, float64) -> winner, price, second_price."""
         if bids.dim() != 2 or bids.shape[0] != self.P or bids.dtype != torch.float64:

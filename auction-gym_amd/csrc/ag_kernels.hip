@@ -278,21 +278,14 @@ __global__ __launch_bounds__(kThreads) void k_exp_kat(const double *x, double *y
     y[i] = sig ? agexp::sigmoid(x[i], s_tab) : agexp::exp(x[i], s_tab);
 }
 
-// Streaming copy, 16 B per lane, non-temporal both ways (bench.py's measured HBM peak):
-// 4 independent 16-B loads in flight per lane per step.
+// Streaming copy, one 16-B element per lane, non-temporal both ways, one tile per workgroup
+// (bench.py's measured HBM peak: the fastest of the copy shapes tools/floor/copy_peak.py
+// measured -- 6.6 TB/s against 5.0-6.0 for persistent grid-stride copies).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(kThreads) void k_stream_copy(const u32x4 *__restrict__ src, u32x4 *__restrict__ dst,
                                                           int64_t n16) {
-  const int64_t stride = (int64_t)gridDim.x * kThreads;
-  int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  for (; i + 3 * stride < n16; i += 4 * stride) {
-    u32x4 v[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = __builtin_nontemporal_load(src + i + q * stride);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(v[q], dst + i + q * stride);
-  }
-  for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i < n16) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 
 // ------------------------------------------------------------------------------------
@@ -866,16 +859,13 @@ int ag_stream_copy(const void *src, void *dst, int64_t nbytes, void *stream) {
   if ((!src || !dst) && nbytes > 0) return ag_set_error(AG_ERR_INVALID, "ag_stream_copy: null argument");
   if (nbytes < 0 || nbytes % 16 || ((uintptr_t)src | (uintptr_t)dst) % 16)
     return ag_set_error(AG_ERR_INVALID, "ag_stream_copy: nbytes and both pointers must be multiples of 16");
-  if (nbytes == 0) return AG_OK;
-  int dev = 0, cus = 0;
-  AG_HIP(hipGetDevice(&dev));
-  AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const int64_t n16 = nbytes / 16;
-  const int64_t tiles = (n16 + kThreads - 1) / kThreads;
-  const int grid = (int)(tiles < (int64_t)cus * 8 ? tiles : (int64_t)cus * 8);
-  hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, (const u32x4 *)src,
-                     (u32x4 *)dst, n16);
-  AG_HIP(hipGetLastError());
+  for (int64_t lo = 0; lo < n16; lo += (int64_t)INT32_MAX * kThreads / 2) {  // grid.x < 2^31
+    const int64_t n = n16 - lo < (int64_t)INT32_MAX * kThreads / 2 ? n16 - lo : (int64_t)INT32_MAX * kThreads / 2;
+    hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                       (hipStream_t)stream, (const u32x4 *)src + lo, (u32x4 *)dst + lo, n);
+    AG_HIP(hipGetLastError());
+  }
   return AG_OK;
 }
 

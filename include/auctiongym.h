@@ -400,6 +400,29 @@ int ag_bidder_update(ag_ctx *ctx, const ag_shading_samples *samples, const int32
                      const int64_t *noise_offsets, int32_t noise_epochs, int32_t *epochs, int32_t *status,
                      float *traces, void *stream);
 
+/* ---- Per-call plugin surface (one agent, n requests; n = 1 is the reference's call) ----
+ * Allocator.estimate_CTR of agent `agent` for n contexts (dev), ctr dev [n][K]:
+ *  - OracleAllocator (src/BidderAllocation.py:81-82): context [n][E+1], the TRUE context with
+ *    its intercept; ctr = sigmoid(items @ context), FP64, the simulate kernels' arithmetic;
+ *  - PyTorchLogisticRegressionAllocator (src/BidderAllocation.py:67-68, src/Models.py:28-33):
+ *    context [n][OE+1], the OBSERVED context with its intercept; ctr = float32
+ *    sigmoid(x32 . (m + noise)) widened to double; noise dev float32 [n][K][OE+1] is the
+ *    Thompson draw torch.normal(0, 1/sqrt(q)) of each request (NULL: the MAP estimate,
+ *    estimate_CTR(context, sample=False)). */
+int ag_estimate_ctr(ag_ctx *ctx, int32_t agent, int64_t n, const double *context, const float *noise,
+                    double *ctr, void *stream);
+
+/* Bidder.bid of agent `agent` for n requests (dev [n] value and estimated CTR): bid [n], and
+ * gamma / propensity [n] (may be NULL) as ag_batch_out defines them, by the agent's bidder
+ * kind and state (src/Bidder.py:34-35, :47-58, :171-208, :348-367, :455-475). The draws the
+ * reference makes inside bid() are inputs, as in ag_batch_in: gamma_raw [n] (the
+ * rng.normal(prev_gamma, gamma_sigma) of a Gaussian-shading bid), policy_eps float32 [n] (the
+ * rsample draw of a fitted policy), gamma_grid [128][n] (the 'search' grid); pass NULL for
+ * what the agent's state does not draw. Synchronises for the agent's state. */
+int ag_bid(ag_ctx *ctx, int32_t agent, int64_t n, const double *value, const double *est_ctr,
+           const double *gamma_raw, const float *policy_eps, const double *gamma_grid, double *bid,
+           double *gamma, double *propensity, void *stream);
+
 /* Exact counters (host int64 [n][AG_FX_LIMBS], e.g. copied back or all-reduced)
  * -> doubles (host [n]), correctly rounded from the exact fixed-point sum. */
 int ag_counters_to_double(const int64_t *counters_fx, int64_t n, double *out);
@@ -410,8 +433,8 @@ int ag_sigmoid(const double *z, double *out, int64_t n, void *stream);
 int ag_exp(const double *x, double *out, int64_t n, void *stream);
 
 /* Measurement hook (bench.py's measured HBM peak beside the 8 TB/s spec): copy nbytes
- * (multiple of 16, 16-B aligned dev pointers) with 16-B non-temporal loads and stores on the
- * current device, stream-ordered. */
+ * (multiple of 16, 16-B aligned dev pointers) with one 16-B non-temporal load and store per
+ * lane, one 256-lane tile per workgroup, on the current device, stream-ordered. */
 int ag_stream_copy(const void *src, void *dst, int64_t nbytes, void *stream);
 
 /* Thread-local description of the last error. */

@@ -377,6 +377,51 @@ def test_stale_binding_is_refused(gpu):
     eng.close()
 
 
+def _integration_block():
+    """The python block of INTEGRATION.md section 2 (the reference-side ctypes stub)."""
+    text = open(os.path.join(os.path.dirname(GOLDEN), "..", "INTEGRATION.md")).read()
+    sec = text[text.index("## 2. Raw C-ABI"):text.index("## 3. ")]
+    return sec[sec.index("```python") + len("```python"):sec.index("```", sec.index("```python") + 9)]
+
+
+def test_integration_stub_runs_verbatim(gpu):
+    """INTEGRATION.md's ctypes stub, executed as published, on a stand-in for the reference's
+    Auction built exactly as src/main.py builds SP_Oracle (seed 0): the draws it makes are the
+    reference's, so its winners, prices, utilities and revenue equal the reference's own
+    capture (sp_oracle_r4096)."""
+    import ctypes
+    import types
+    import auctiongym_amd.main as M
+    from auctiongym_amd import _lib
+    d, meta, agg = load_capture("sp_oracle_r4096")
+    ns = {"AG_LIB": _lib.LIB_PATH, "__name__": "integration_stub"}
+    exec(compile(_integration_block(), "INTEGRATION.md#2", "exec"), ns)
+    with open(os.path.join(GOLDEN, "sp_oracle_full_run.json")) as f:
+        cfg = json.load(f)["config"]
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "ag_integration_sp_oracle.json")
+    with open(path, "w") as f:
+        json.dump(cfg, f)
+    rng, config, agent_configs, a2i, a2v, _, max_slots, E, var, OE = M.parse_config(path)
+    SecondPrice = type("SecondPrice", (), {})
+    auction = types.SimpleNamespace(
+        rng=rng, agents=[types.SimpleNamespace(name=c["name"], net_utility=0.0, gross_utility=0.0)
+                         for c in agent_configs],
+        num_participants_per_round=config["num_participants_per_round"], agents2item_values=a2v,
+        agent2items=a2i, embedding_size=E, obs_embedding_size=OE, embedding_var=var,
+        allocation=SecondPrice(), max_slots=max_slots, revenue=0.0)
+    path_ = ns["GPUAuctionPath"](auction)
+    B = 4096
+    path_.run_rounds(B)
+    w = np.empty(B, np.int32)
+    pr = np.empty(B)
+    ns["d2h"](w, ctypes.c_void_p(path_.last["winner"]))
+    ns["d2h"](pr, ctypes.c_void_p(path_.last["price"]))
+    assert np.array_equal(w, d["winner"])
+    assert np.array_equal(pr, d["price"])
+    np.testing.assert_allclose([a.net_utility for a in auction.agents], agg["net_utility"], rtol=1e-9)
+    np.testing.assert_allclose(auction.revenue, agg["revenue"], rtol=1e-9)
+
+
 def test_screened_search_adversarial_catalogues(gpu, oracle):
     """Catalogues built to stress the f32 screen: exact duplicate items (ties -> first max),
     near-ties 1 ulp apart, huge embeddings (guard -> exact scan), intercepts so negative
@@ -1487,3 +1532,132 @@ def test_bidder_update_synthetic_noise(gpu, oracle):
     z = oracle.fit_noise(77, 0, 3, n0)
     assert abs(z.mean()) < 0.05 and abs(z.std() - 1) < 0.05
     eng.close()
+
+
+# ---- the per-call plugin surface (src/BidderAllocation.py:67-82, src/Bidder.py bid / update,
+# src/Agent.py:29-68), outside a batched Auction ----
+def test_per_call_estimate_and_bid_match_reference(gpu, oracle):
+    """OracleAllocator.estimate_CTR, Agent.select_item and Agent.bid called one request at a
+    time (B = 1 calls into the kernels) reproduce the reference's own capture bit for bit:
+    items, estimated CTRs and bids of SP_Oracle's first 300 rounds; the shading bidders'
+    Gaussian-shading bids (the rng.normal draw patched to the recorded one) equal the
+    reference's bids, and their propensities the oracle's."""
+    import types
+    from auctiongym_amd.Agent import Agent
+    from auctiongym_amd.Bidder import DoublyRobustBidder, TruthfulBidder
+    from auctiongym_amd.BidderAllocation import OracleAllocator
+    d, meta, _ = load_capture("sp_oracle_r4096")
+    agents = []
+    for a in range(meta["N"]):
+        al = OracleAllocator(None)
+        al.update_item_embeddings(d["items"][a])
+        agents.append(Agent(None, f"A{a}", meta["K"], d["values"][a], al, TruthfulBidder(None)))
+    for r in range(300):
+        x = np.concatenate([d["ctx"][r], [1.0]])
+        for s_ in range(meta["P"]):
+            ag = agents[d["part"][r, s_]]
+            ctr = ag.allocator.estimate_CTR(x)
+            item, est = ag.select_item(x)
+            assert item == d["item"][r, s_] and est == d["slot_est_ctr"][r, s_] == ctr[item]
+            b, it2 = ag.bid(x)
+            assert it2 == item and b == d["slot_bid"][r, s_]
+    assert len(agents[0].logs) == sum((d["part"][:300] == 0).ravel())  # per-call records are logged
+    # Gaussian shading of an uninitialised DoublyRobustBidder (FP_DR_TS capture)
+    d, meta, _ = load_capture("fp_dr_ts_r1024")
+    kw = meta["bidder_kwargs"][0]
+    args = pop_args(d, meta)
+    orc = oracle.simulate_pop(0, d["items"], d["values"], d["ctx"], d["part"], d["u"], **args)
+    for r in range(200):
+        for s_ in range(meta["P"]):
+            bd = DoublyRobustBidder(None, **kw)
+            bd.rng = types.SimpleNamespace(normal=lambda loc, sc, g=d["gamma_raw"][r, s_]: g)
+            b = bd.bid(d["slot_value"][r, s_], None, d["slot_est_ctr"][r, s_])
+            assert b == d["slot_bid"][r, s_]
+            assert bd.gammas == [d["gamma_raw"][r, s_]]
+            assert bd.propensities[0] == orc["propensity"][r, s_]
+
+
+def test_per_call_lrts_estimate_matches_simulate(gpu, oracle):
+    """PyTorchLogisticRegressionAllocator.estimate_CTR (Thompson draw patched to the recorded
+    torch.normal noise) and Agent.select_item on SP_Truthful_TS's capture: the items the
+    reference chose and the MAP CTRs the oracle computes, bit for bit."""
+    from auctiongym_amd.Agent import Agent
+    from auctiongym_amd.Bidder import TruthfulBidder
+    from auctiongym_amd.BidderAllocation import PyTorchLogisticRegressionAllocator
+    import torch
+    d, meta, _ = load_capture("sp_ts_r2048")
+    args = pop_args(d, meta)
+    orc = oracle.simulate_pop(mech_code(meta), d["items"], d["values"], d["ctx"], d["part"], d["u"], **args)
+    OE, K = meta["OE"], meta["K"]
+    agents = []
+    for a in range(meta["N"]):
+        al = PyTorchLogisticRegressionAllocator(None, OE, K)
+        al.response_model.m = torch.from_numpy(np.ascontiguousarray(args["ts_m"][a], np.float32))
+        al.response_model.prev_iter_m = al.response_model.m.clone()
+        al.response_model.q = torch.ones(K, OE + 1)
+        agents.append(Agent(None, f"TS{a}", K, d["values"][a], al, TruthfulBidder(None)))
+    for r in range(200):
+        x = np.concatenate([d["ctx"][r, :OE], [1.0]])
+        for s_ in range(meta["P"]):
+            ag = agents[d["part"][r, s_]]
+            z = torch.from_numpy(np.ascontiguousarray(d["ts_noise"][r, s_].reshape(K, OE + 1), np.float32))
+            ag.allocator.response_model.sample_noise = lambda z=z: z
+            item, est = ag.select_item(x)
+            assert item == d["item"][r, s_] == orc["item"][r, s_]
+            assert est == np.float32(orc["est_ctr"][r, s_])
+
+
+def test_plugin_level_updates_match_oracle(gpu, oracle):
+    """The reference's plugin-level update(...) calls, made directly on a plugin: the LR-TS
+    allocator (sp_ts_update_kat), EmpiricalShadedBidder (empirical_update_kat) and a
+    DoublyRobustBidder (dr_update_kat, its torch rsample noise drawn from the recorded
+    generator state) train on the GPU and equal the oracle / the reference bit for bit."""
+    import torch
+    from auctiongym_amd.Bidder import DoublyRobustBidder, EmpiricalShadedBidder
+    from auctiongym_amd.BidderAllocation import PyTorchLogisticRegressionAllocator
+    kat = np.load(os.path.join(GOLDEN, "sp_ts_update_kat.npz"))
+    X, A, y = kat["a0_X"], kat["a0_A"], kat["a0_y"]
+    K, Do = kat["a0_m0"].shape
+    al = PyTorchLogisticRegressionAllocator(None, Do - 1, K)
+    rm = al.response_model
+    rm.m = torch.from_numpy(kat["a0_m0"].copy())
+    rm.prev_iter_m = torch.from_numpy(kat["a0_prevm0"].copy())
+    rm.q = torch.from_numpy(kat["a0_q0"].copy())
+    al.update(X, A, y, 0)
+    om, opm, oq, oep, _ = oracle.lrts_update(X, A, y, kat["a0_m0"], kat["a0_prevm0"], kat["a0_q0"])
+    assert al.epochs == oep
+    assert np.array_equal(rm.m.numpy(), om) and np.array_equal(rm.q.numpy(), oq)
+    assert np.array_equal(rm.prev_iter_m.numpy(), opm)
+    # EmpiricalShadedBidder
+    ek = np.load(os.path.join(GOLDEN, "empirical_update_kat.npz"))
+    for a in range(3):
+        g, u = ek[f"c0_it0_a{a}_gammas"], ek[f"c0_it0_a{a}_util"]
+        b = EmpiricalShadedBidder(None, gamma_sigma=0.05, init_gamma=float(ek[f"c0_it0_a{a}_pg0"]))
+        b.gammas = list(g)
+        n = len(g)  # utility = value * outcome - price on won records: value = u, outcome 1, price 0
+        b.update(None, u, None, np.zeros(n), np.ones(n), None, np.ones(n, bool), 0)
+        assert b.prev_gamma == float(ek[f"c0_it0_a{a}_pg1"])
+    # DoublyRobustBidder
+    dk = np.load(os.path.join(GOLDEN, "dr_update_kat.npz"))
+    k = lambda s: dk[f"a0_{s}"]  # noqa: E731
+    b = DoublyRobustBidder(None, gamma_sigma=0.02, init_gamma=1.0)
+    st0 = np.zeros(16, np.float32)
+    st0[:4] = np.concatenate([k("wr0_0").ravel(), k("wr0_1").ravel()])
+    st0[4:] = np.concatenate([k(f"pol0_{j}").ravel() for j in range(6)])
+    b._load_state16(st0)
+    b.gammas, b.propensities = list(k("gamma")), list(k("propensity"))
+    n = len(b.gammas)
+    torch.set_rng_state(torch.from_numpy(np.asarray(k("dr_rng_state"))))
+    b.update(None, k("value"), None, k("price"), k("outcome"), k("est_ctr"), k("won").astype(bool), 0)
+    after = torch.get_rng_state()
+    z = _dr_noise(k("dr_rng_state"), n, int(b.epochs[2]) + 1)
+    orc = oracle.dr_update(k("est_ctr"), k("value"), k("gamma"), k("propensity"), k("won"), k("util"),
+                           st0[:4], st0[4:], False, z[:-1])
+    assert list(b.epochs) == list(orc["epochs"])
+    assert np.array_equal(b._state16()[:4], orc["wr"]) and np.array_equal(b._state16()[4:], orc["pol"])
+    assert b.model_initialised
+    # the generator is where the reference leaves it: the fit's draws + one rsample of every record
+    torch.set_rng_state(torch.from_numpy(np.asarray(k("dr_rng_state"))))
+    for _ in range(int(b.epochs[2]) + 1):
+        torch.empty(n).normal_()
+    assert torch.equal(torch.get_rng_state(), after)

@@ -186,3 +186,24 @@ def test_ts_noise_tiling_roundtrip():
                 for c in (0, 17, 59):
                     assert flat[((s * T + i // 64) * 60 + c) * 64 + i % 64] == z[i, s].ravel()[c]
         assert np.array_equal(AuctionEngine.untile_ts_noise(t, B), z.reshape(B, 2, 60))
+
+
+@pytest.mark.parametrize("budget", [512, 2048])
+def test_torch_noise_rewind_at_every_epoch_boundary(budget):
+    """Auction._TorchNoise: rewind(e) leaves torch's generator exactly e epochs of draws past
+    its start for every e up to and including the budget E (a fit that uses every epoch of
+    its budget stops at e == E, one past the last snapshot)."""
+    import torch
+    from auctiongym_amd.Auction import _TorchNoise
+    n = 5
+    torch.manual_seed(1234)
+    start = torch.get_rng_state()
+    s = _TorchNoise(n, "cpu")
+    s.upto(budget)
+    for e in (0, 1, 255, 256, 257, budget - 1, budget):
+        s.rewind(e)
+        got = torch.empty(n).normal_()
+        torch.set_rng_state(start)
+        for _ in range(e):
+            torch.empty(n).normal_()
+        assert torch.equal(torch.empty(n).normal_(), got), e
