@@ -75,7 +75,7 @@ struct ag_ctx {
   double *d_values = nullptr;
   int64_t *d_partials = nullptr;
   int32_t partial_blocks = 0;
-  int32_t resident[16] = {};  // resident blocks [general][W][screened][counters]
+  int32_t resident[32] = {};  // resident blocks [1024 lanes][general][W][screened][counters]
   int64_t launch_cap = 0;  // AG_OPT_LAUNCH_AUCTIONS
   int64_t lrts_chunk = 0;  // AG_OPT_LRTS_BLOCK_SAMPLES
   bool wide = false;  // 1 auction per lane by default: higher occupancy, faster when sustained
@@ -84,6 +84,7 @@ struct ag_ctx {
   bool ora_catalog = false;  // catalogue within k_oracle's bounds (ag_sim_oracle.h)
   int32_t sim_kernel = AG_SIM_KERNEL_AUTO;  // AG_OPT_SIMULATE_KERNEL
   int32_t grid_per_cu = 0;                  // AG_OPT_SIM_BLOCKS_PER_CU (0: as many as fit)
+  int32_t block_threads = 0;                // AG_OPT_SIM_BLOCK_THREADS (0: auto)
   int32_t resident_ora[4] = {};             // resident blocks of k_oracle [generate][counters]
   // general populations (anything beyond OracleAllocator + TruthfulBidder)
   bool general = false, has_lrts = false, has_shading = false, lrts_loaded = false;

@@ -291,16 +291,16 @@ __global__ __launch_bounds__(kThreads) void k_stream_copy(const u32x4 *__restric
 // ------------------------------------------------------------------------------------
 // dispatch
 // ------------------------------------------------------------------------------------
-SimKernel pick_kernel(int P, int D, bool prune, int W, bool general) {
+SimKernel pick_kernel(int P, int D, bool prune, int W, bool general, int bt) {
   switch (P) {
-    case 1: return pick_kernel_for<1>(D, prune, W, general);
-    case 2: return pick_kernel_for<2>(D, prune, W, general);
-    case 3: return pick_kernel_for<3>(D, prune, W, general);
-    case 4: return pick_kernel_for<4>(D, prune, W, general);
-    case 5: return pick_kernel_for<5>(D, prune, W, general);
-    case 6: return pick_kernel_for<6>(D, prune, W, general);
-    case 7: return pick_kernel_for<7>(D, prune, W, general);
-    case 8: return pick_kernel_for<8>(D, prune, W, general);
+    case 1: return pick_kernel_for<1>(D, prune, W, general, bt);
+    case 2: return pick_kernel_for<2>(D, prune, W, general, bt);
+    case 3: return pick_kernel_for<3>(D, prune, W, general, bt);
+    case 4: return pick_kernel_for<4>(D, prune, W, general, bt);
+    case 5: return pick_kernel_for<5>(D, prune, W, general, bt);
+    case 6: return pick_kernel_for<6>(D, prune, W, general, bt);
+    case 7: return pick_kernel_for<7>(D, prune, W, general, bt);
+    case 8: return pick_kernel_for<8>(D, prune, W, general, bt);
     default: return nullptr;
   }
 }
@@ -448,7 +448,7 @@ int ag_create(int32_t device, const ag_shape *s, ag_ctx **out) {
   // simulate needs a kernel for (P, D) and the catalogue in LDS; allocate-only contexts
   // (any P) do not.
   const LdsLayout lay = make_layout(s->num_agents, s->num_items, D, true);
-  c->can_simulate = s->num_participants <= kMaxP && pick_kernel(s->num_participants, D, false, 1, false) &&
+  c->can_simulate = s->num_participants <= kMaxP && pick_kernel(s->num_participants, D, false, 1, false, kThreads) &&
                     lay.total <= 160 * 1024;
   AgDeviceGuard g(device);
   hipError_t e = hipMalloc(&c->d_items, sizeof(double) * s->num_agents * s->num_items * D);
@@ -613,6 +613,11 @@ int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
       if (value < 0 || value > 64) return ag_set_error(AG_ERR_INVALID, "ag_set_option: blocks per CU in [0, 64]");
       c->grid_per_cu = (int32_t)value;
       return AG_OK;
+    case AG_OPT_SIM_BLOCK_THREADS:
+      if (value != 0 && value != 256 && value != 1024)
+        return ag_set_error(AG_ERR_INVALID, "ag_set_option: block threads must be 0, 256 or 1024");
+      c->block_threads = (int32_t)value;
+      return AG_OK;
     case AG_OPT_SIMULATE_KERNEL:
       if (value != AG_SIM_KERNEL_AUTO && value != AG_SIM_KERNEL_GENERIC)
         return ag_set_error(AG_ERR_INVALID, "ag_set_option: bad simulate kernel %lld", (long long)value);
@@ -725,20 +730,31 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
     if (OraKernel ok = pick_oracle(s.num_participants, D, false))
       return simulate_oracle(c, ok, B, in, out, counters_fx, (hipStream_t)stream);
   const int W = (prune && (B % 2) == 0 && c->wide && !c->general) ? 2 : 1;
-  SimKernel k = pick_kernel(s.num_participants, D, prune, W, c->general);
-  if (!k) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: no kernel for P=%d D=%d", s.num_participants, D);
   const size_t lds = (size_t)prm.lds.total;
   if (lds > 160 * 1024)
     return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
+  // Lanes per workgroup: the LDS image (catalogue, screen, LR-TS means, counter replicas) is
+  // per workgroup, so a large population with 256-lane workgroups keeps few waves resident
+  // (N = 32: ~75 KB -> 2 workgroups = 2 waves per SIMD); 1024-lane workgroups share one
+  // image among 16 waves. Same results (the counters are exact sums).
+  int bt = c->block_threads;
+  if (bt == 0) bt = (c->general && prune && lds > 40 * 1024) ? 1024 : kThreads;
+  SimKernel k = pick_kernel(s.num_participants, D, prune, W, c->general, bt);
+  if (!k && bt != kThreads) {
+    bt = kThreads;
+    k = pick_kernel(s.num_participants, D, prune, W, c->general, bt);
+  }
+  if (!k) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: no kernel for P=%d D=%d", s.num_participants, D);
   hipStream_t st = (hipStream_t)stream;
   if (lds > 64 * 1024)
     AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   // Persistent grid: exactly the blocks the device keeps resident (no partial last round),
-  // each striding over 256-auction tiles.
-  int &res = c->resident[(c->general ? 8 : 0) + (W == 2 ? 4 : 0) + (prune ? 2 : 0) + (prm.want_counters ? 1 : 0)];
+  // each striding over bt-auction tiles.
+  int &res = c->resident[(bt == kThreads ? 0 : 16) + (c->general ? 8 : 0) + (W == 2 ? 4 : 0) + (prune ? 2 : 0) +
+                         (prm.want_counters ? 1 : 0)];
   if (res == 0) {
     int per_cu = 0, cus = 0;
-    AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k, kThreads, lds));
+    AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k, bt, lds));
     AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
     res = per_cu * cus;
     if (res < 1) res = 1;
@@ -753,11 +769,11 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   if (chunk_max < 2) chunk_max = 2;
   for (int64_t lo = 0; lo < B; lo += chunk_max) {
     const int64_t hi = lo + chunk_max < B ? lo + chunk_max : B;
-    const int64_t tiles = (hi - lo + kThreads * W - 1) / (kThreads * W);
+    const int64_t tiles = (hi - lo + bt * W - 1) / (bt * W);
     const int grid = (int)(tiles < res ? tiles : res);
     prm.lo = (int32_t)lo;
     prm.hi = (int32_t)hi;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), lds, st, prm);  // generate mode: same lo/hi
+    hipLaunchKernelGGL(k, dim3(grid), dim3(bt), lds, st, prm);  // generate mode: same lo/hi
     AG_HIP(hipGetLastError());
     if (counters_fx) {
       hipLaunchKernelGGL(k_reduce_counters, dim3(nc), dim3(kThreads), 0, st, c->d_partials, grid, nc,

@@ -671,8 +671,8 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
   r.oc = bernoulli(ctr_w, u);  // src/Auction.py:65 (true CTR of the winner's item)
 }
 
-template <int P, int D, bool PRUNE, int W, bool GENERAL>
-__global__ __launch_bounds__(kThreads, GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES) void k_simulate(SimParams prm) {
+template <int P, int D, bool PRUNE, int W, bool GENERAL, int BT = kThreads>
+__global__ __launch_bounds__(BT, GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES) void k_simulate(SimParams prm) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = prm.N, K = prm.K;
   const uint32_t B = (uint32_t)prm.B;  // SoA leading dimension (auctions in the batch)
@@ -695,41 +695,41 @@ __global__ __launch_bounds__(kThreads, GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES
 
   const int tid = threadIdx.x;
   if constexpr (GENERAL) {
-    for (int a = tid; a < N; a += kThreads) {
+    for (int a = tid; a < N; a += BT) {
       s_akind[a] = prm.akind[a];
       s_bkind[a] = prm.bkind[a];
       s_pg[a] = prm.pg[a];
       s_gs[a] = prm.gs[a];
     }
-    for (int j = tid; j < N * K * L.ts_do; j += kThreads) s_tsm[j] = prm.tsm[j];
+    for (int j = tid; j < N * K * L.ts_do; j += BT) s_tsm[j] = prm.tsm[j];
     if (prm.drs) {
-      for (int j = tid; j < N * 16; j += kThreads) s_drs[j] = prm.drs[j];
-      for (int a = tid; a < N; a += kThreads) s_dri[a] = prm.dri[a];
+      for (int j = tid; j < N * 16; j += BT) s_drs[j] = prm.drs[j];
+      for (int a = tid; a < N; a += BT) s_dri[a] = prm.dri[a];
     }
   }
-  for (int i = tid; i < 256; i += kThreads) s_tab[i] = ag_exp_tab[i];
-  for (int i = tid; i < N * K * D; i += kThreads) {
+  for (int i = tid; i < 256; i += BT) s_tab[i] = ag_exp_tab[i];
+  for (int i = tid; i < N * K * D; i += BT) {
     const int a = i / (K * D), r = i - a * (K * D);
     s_items[a * L.items_stride + r] = prm.items[i];
   }
-  for (int i = tid; i < N * K; i += kThreads) {
+  for (int i = tid; i < N * K; i += BT) {
     const int a = i / K, r = i - a * K;
     s_vals[a * L.values_stride + r] = prm.values[i];
   }
   if (PRUNE) {
     // screening rows: [pair p][dim d][item 2p, 2p+1], coefficients * -log2(e); padded
     // dims and the odd item's partner are 0
-    for (int i = tid; i < N * L.kpairs * 16; i += kThreads) {
+    for (int i = tid; i < N * L.kpairs * 16; i += BT) {
       const int a = i / (L.kpairs * 16), r = i - a * (L.kpairs * 16);
       const int p = r >> 4, d = (r >> 1) & 7, k = 2 * p + (r & 1);
       const float c = (d < D && k < K) ? (float)prm.items[((size_t)a * K + k) * D + d] : 0.0f;
       s_scr[a * L.scr_stride + r] = c * kNegLog2e;
     }
-    for (int i = tid; i < N * L.kpairs * 2; i += kThreads) {  // 1/v (padding items: +inf)
+    for (int i = tid; i < N * L.kpairs * 2; i += BT) {  // 1/v (padding items: +inf)
       const int a = i / (L.kpairs * 2), k = i - a * (L.kpairs * 2);
       s_scr_val[a * L.scr_val_stride + k] = k < K ? 1.0f / (float)prm.values[(size_t)a * K + k] : INFINITY;
     }
-    for (int a = tid; a < N; a += kThreads) {
+    for (int a = tid; a < N; a += BT) {
       float m = 0.0f;
       for (int r = 0; r < K * D; ++r) m = fmaxf(m, (float)fabs(prm.items[(size_t)a * K * D + r]));
       s_amax[a] = m * 1.001f;
@@ -737,7 +737,7 @@ __global__ __launch_bounds__(kThreads, GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES
   }
   const int R = L.replicas;
   if (prm.want_counters)
-    for (int i = tid; i < R * N * L.ncnt; i += kThreads) s_cnt[i] = 0ull;
+    for (int i = tid; i < R * N * L.ncnt; i += BT) s_cnt[i] = 0ull;
   __syncthreads();
 
   const Lds T{s_tab, s_items, s_vals, s_scr, s_scr_val, s_amax, L.items_stride, L.values_stride,
@@ -759,20 +759,20 @@ __global__ __launch_bounds__(kThreads, GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES
     for (int s = 0; s < P; ++s) ld_i32<W>(in.part + s * B + i, pv[s]);
     ld_f64<W>(in.u + i, uv);
   };
-  const uint32_t stride = gridDim.x * (kThreads * W);
-  // Participation / win counts: a lane resolves at most kAuctionsPerReplica * R / kThreads
+  const uint32_t stride = gridDim.x * (BT * W);
+  // Participation / win counts: a lane resolves at most kAuctionsPerReplica * R / BT
   // (<= 255) auctions per launch, so for N <= 8 agents its counts fit 8-bit fields of one
   // register each; flushed to the LDS counters once, after the loop.
-  const bool packed = N <= 8 && kAuctionsPerReplica * R / kThreads <= 255;
+  const bool packed = N <= 8 && kAuctionsPerReplica * R / BT <= 255;
   uint64_t n_logs_packed = 0, n_won_packed = 0;
 #if AG_PREFETCH
   // software pipelining: the next tile's loads are in flight while this tile computes
   double xn[kMaxD][W];
   int pn[P][W];
   double un[W];
-  if (lo + blockIdx.x * (kThreads * W) + tid * W < hi) load_tile(lo + blockIdx.x * (kThreads * W) + tid * W);
+  if (lo + blockIdx.x * (BT * W) + tid * W < hi) load_tile(lo + blockIdx.x * (BT * W) + tid * W);
 #endif
-  for (uint32_t base = lo + blockIdx.x * (kThreads * W); base < hi; base += stride) {
+  for (uint32_t base = lo + blockIdx.x * (BT * W); base < hi; base += stride) {
     const uint32_t i = base + tid * W;  // W consecutive auctions (even chunk bounds when W = 2)
 #if AG_PREFETCH
     if (i >= hi) continue;
@@ -930,7 +930,7 @@ __global__ __launch_bounds__(kThreads, GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES
     };
     const int pairs = L.ncnt * N;
     if (R >= 2) {
-      for (int pr = tid; pr < pairs; pr += kThreads) {
+      for (int pr = tid; pr < pairs; pr += BT) {
         long long slo = 0, shi = 0;
         for (int r = 0; r < R; ++r) {
           long long l, h;
@@ -943,7 +943,7 @@ __global__ __launch_bounds__(kThreads, GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES
       }
       __syncthreads();
     }
-    for (int a = tid; a < N; a += kThreads) {
+    for (int a = tid; a < N; a += BT) {
       long long lo[kGeneralSlots], hi[kGeneralSlots];
       unsigned long long nlogs = 0, nwon = 0;
       for (int j = 0; j < kGeneralSlots; ++j) {
@@ -996,14 +996,14 @@ typedef void (*SimKernel)(SimParams);
 // Defined per participant count P in ag_sim_p.hip (one translation unit per P, compiled
 // in parallel): the k_simulate instantiation for (D, screened search, auctions per lane).
 template <int P>
-SimKernel pick_kernel_for(int D, bool prune, int W, bool general);
-template <> SimKernel pick_kernel_for<1>(int, bool, int, bool);
-template <> SimKernel pick_kernel_for<2>(int, bool, int, bool);
-template <> SimKernel pick_kernel_for<3>(int, bool, int, bool);
-template <> SimKernel pick_kernel_for<4>(int, bool, int, bool);
-template <> SimKernel pick_kernel_for<5>(int, bool, int, bool);
-template <> SimKernel pick_kernel_for<6>(int, bool, int, bool);
-template <> SimKernel pick_kernel_for<7>(int, bool, int, bool);
-template <> SimKernel pick_kernel_for<8>(int, bool, int, bool);
+SimKernel pick_kernel_for(int D, bool prune, int W, bool general, int bt);
+template <> SimKernel pick_kernel_for<1>(int, bool, int, bool, int);
+template <> SimKernel pick_kernel_for<2>(int, bool, int, bool, int);
+template <> SimKernel pick_kernel_for<3>(int, bool, int, bool, int);
+template <> SimKernel pick_kernel_for<4>(int, bool, int, bool, int);
+template <> SimKernel pick_kernel_for<5>(int, bool, int, bool, int);
+template <> SimKernel pick_kernel_for<6>(int, bool, int, bool, int);
+template <> SimKernel pick_kernel_for<7>(int, bool, int, bool, int);
+template <> SimKernel pick_kernel_for<8>(int, bool, int, bool, int);
 
 }  // namespace ag

@@ -10,16 +10,16 @@
 namespace ag {
 namespace {
 
-template <int P, bool PRUNE, int W, bool G>
+template <int P, bool PRUNE, int W, bool G, int BT = kThreads>
 SimKernel pick_d(int D) {
   switch (D) {
-    case 2: return k_simulate<P, 2, PRUNE, W, G>;
-    case 3: return k_simulate<P, 3, PRUNE, W, G>;
-    case 4: return k_simulate<P, 4, PRUNE, W, G>;
-    case 5: return k_simulate<P, 5, PRUNE, W, G>;
-    case 6: return k_simulate<P, 6, PRUNE, W, G>;
-    case 7: return k_simulate<P, 7, PRUNE, W, G>;
-    case 8: return k_simulate<P, 8, PRUNE, W, G>;
+    case 2: return k_simulate<P, 2, PRUNE, W, G, BT>;
+    case 3: return k_simulate<P, 3, PRUNE, W, G, BT>;
+    case 4: return k_simulate<P, 4, PRUNE, W, G, BT>;
+    case 5: return k_simulate<P, 5, PRUNE, W, G, BT>;
+    case 6: return k_simulate<P, 6, PRUNE, W, G, BT>;
+    case 7: return k_simulate<P, 7, PRUNE, W, G, BT>;
+    case 8: return k_simulate<P, 8, PRUNE, W, G, BT>;
     default: return nullptr;
   }
 }
@@ -28,14 +28,18 @@ SimKernel pick_d(int D) {
 
 // prune: the f32-screened item search (D <= 8, K <= 2 kMaxKPairs), W auctions per lane
 // (2 when B is even: 16-B accesses); otherwise the exact scan, one auction per lane.
-// general: populations beyond OracleAllocator + TruthfulBidder (one auction per lane).
+// general: populations beyond OracleAllocator + TruthfulBidder (one auction per lane), in
+// 256-lane workgroups or, screened, 1024-lane ones (bt; large populations' LDS images).
 template <>
-SimKernel pick_kernel_for<AG_P>(int D, bool prune, int W, bool general) {
+SimKernel pick_kernel_for<AG_P>(int D, bool prune, int W, bool general, int bt) {
   constexpr int P = AG_P;
   if (general) {
     if (D > 8) return nullptr;
+    if (bt == 1024) return prune ? pick_d<P, true, 1, true, 1024>(D) : nullptr;
+    if (bt != kThreads) return nullptr;
     return prune ? pick_d<P, true, 1, true>(D) : pick_d<P, false, 1, true>(D);
   }
+  if (bt != kThreads) return nullptr;
   if (prune) return W == 2 ? pick_d<P, true, 2, false>(D) : pick_d<P, true, 1, false>(D);
   if (D <= 8) return pick_d<P, false, 1, false>(D);
   switch (D) {

@@ -423,6 +423,8 @@ def main():
     ap.add_argument("--no-update", action="store_true", help="skip timing the Agent.update of learners")
     ap.add_argument("--no-populations", action="store_true",
                     help="skip the configs[2..4] lines (FP_DM_TS, FP_DR_TS, mixed population)")
+    ap.add_argument("--populations", default=",".join(POPULATIONS),
+                    help="comma-separated subset of the configs[2..4] lines to run")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -583,7 +585,7 @@ def main():
                                         with_update=not args.no_update)
 
     if not args.no_populations:
-        for key in POPULATIONS:
+        for key in [k for k in args.populations.split(",") if k]:
             result[key] = run_population(key, max(5, args.steps // 5), max(5, args.warmup // 5), world, rank, local,
                                          with_update=not args.no_update)
 

@@ -5,6 +5,7 @@ and the mixed population (configs[4], 2M auctions, fitted policies), interleaved
 process; outputs checked identical to the base build.
 
     python tools/ab_ts.py name1 name2 ...
+    python tools/ab_ts.py bt256 bt1024     (base build, AG_OPT_SIM_BLOCK_THREADS forced)
 """
 import os
 import sys
@@ -65,10 +66,20 @@ def time_all(engs, inp, fields, reps=25):
 def main():
     vdir = os.path.join(ROOT, "auction-gym_amd", "build", "variants")
     paths = {"base": _lib.LIB_PATH}
+    opts = {}
     for n in sys.argv[1:]:
-        paths[n] = os.path.join(vdir, f"libauctiongym_hip_{n}.so")
+        if n.startswith("bt"):
+            paths[n] = _lib.LIB_PATH
+            opts[n] = int(n[2:])
+        else:
+            paths[n] = os.path.join(vdir, f"libauctiongym_hip_{n}.so")
+
+    def apply(n, e):
+        if n in opts:
+            e._check(e.L.ag_set_option(e._h, _lib.OPT_SIM_BLOCK_THREADS, opts[n]), "ag_set_option")
+        return e
     B = 1 << 20
-    engs = {n: ts_engine(p) for n, p in paths.items()}
+    engs = {n: apply(n, ts_engine(p)) for n, p in paths.items()}
     inp = engs["base"].alloc_inputs(B)
     engs["base"].generate(0, 0, inp)
     engs["base"].generate_noise(0, 0, inp)
@@ -84,7 +95,7 @@ def main():
         e, what, B4, ak, bk, st16, dims = bench.build_population("configs_4", 0)
         _lib.LIB_PATH = keep
         e.set_dr_state(st16, np.where(bk >= 2, 1, 0).astype(np.int32))
-        engs[n] = e
+        engs[n] = apply(n, e)
     inp = engs["base"].alloc_inputs(B4)
     engs["base"].generate(1, 0, inp)
     engs["base"].generate_noise(1, 0, inp)
