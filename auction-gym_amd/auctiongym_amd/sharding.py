@@ -3,10 +3,17 @@
 Auctions are independent given agent state, so a batch of B auctions
 is split into contiguous shards of global auction indices, one per rank; synthetic
 inputs are keyed by the global index (ag_generate), so every per-auction output is the
-same whatever the number of GPUs. The only exchange is the per-agent counter sums: exact
-int64 fixed-point limbs (include/auctiongym.h AG_FX_*), summed with an int64 all-reduce
-(RCCL over xGMI with backend "nccl", gloo on CPU) -- integer addition, so the totals are
-bit-identical for any world size and any reduction order.
+same whatever the number of GPUs. The only exchange of the simulation is the per-agent
+counter sums: exact int64 fixed-point limbs (include/auctiongym.h AG_FX_*), summed with an
+int64 all-reduce (RCCL over xGMI with backend "nccl", gloo on CPU) -- integer addition, so
+the totals are bit-identical for any world size and any reduction order.
+
+Learner updates (Agent.update, src/Agent.py:79-94, called per agent by src/main.py:127-128)
+are agent-parallel: each learning agent has an owner rank (round robin over the learners,
+`owners`), every record travels once to its agent's owner (`route_records`, one
+all-to-all), the owner trains its agents alone, and the trained states are exchanged
+(`take_owned_rows`, one all-gather of a few KB). A rank's update work is its own agents'
+records only -- not every agent's, as training on all-gathered records would be.
 """
 import numpy as np
 import torch
@@ -46,6 +53,45 @@ def normalize_limbs(limbs):
     return out.reshape(np.shape(limbs))
 
 
+def _world(group=None):
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1
+    return dist.get_world_size(group)
+
+
+def _store_shape(store):
+    """(count, capacity) of a record store (count read back from the device)."""
+    fields = [k for k in store if k != "count"]
+    return int(store["count"][0].item()), int(store[fields[0]].shape[-1])
+
+
+def _check_all(store, group=None):
+    """All ranks' (count, capacity), all-gathered; raises on EVERY rank if any rank's store
+    overflowed (count > capacity: records were dropped, the update would be wrong) -- so no
+    rank is left waiting in the next collective."""
+    n, cap = _store_shape(store)
+    dev = store["count"].device
+    mine = torch.tensor([n, cap], dtype=torch.int64, device=dev)
+    allc = [torch.zeros_like(mine) for _ in range(_world(group))]
+    dist.all_gather(allc, mine, group=group)
+    allc = [(int(t[0]), int(t[1])) for t in allc]
+    bad = [r for r, (c, k) in enumerate(allc) if c > k]
+    if bad:
+        raise ValueError(f"record store overflow on rank(s) {bad}: count > capacity {allc}")
+    return allc
+
+
+def _host_staged(store, group, fn):
+    """gloo has no device all-to-all: under gloo, device stores are staged through host
+    memory (the multi-process GPU tests run ranks that share one GPU over gloo); under RCCL
+    the collectives run on the device buffers directly."""
+    dev = store["count"].device
+    if _world(group) > 1 and dev.type == "cuda" and dist.get_backend(group) == "gloo":
+        out = fn({k: v.cpu() for k, v in store.items()})
+        return {k: v.to(dev) for k, v in out.items()}
+    return fn(store)
+
+
 def gather_records(store, group=None):
     """All-gather a record store across ranks (LR-TS won samples: key [cap], x [Do][cap],
     count [1]; or shading records: agent / gamma / utility [cap], count [1]) into one store
@@ -53,13 +99,14 @@ def gather_records(store, group=None):
     the gathered records gives bit-identical results on every rank and equals a single
     process training on the whole batch -- the update needs no per-epoch collective.
     One all-gather of the counts, one of each record array (padded to the largest count)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+    if _world(group) == 1:
         return store
-    world = dist.get_world_size(group)
-    n = store["count"].clone()
-    counts = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(counts, n, group=group)
-    counts = [int(c.item()) for c in counts]
+    return _host_staged(store, group, lambda st: _gather(st, group))
+
+
+def _gather(store, group):
+    world = _world(group)
+    counts = [c for c, _ in _check_all(store, group)]
     mx = max(max(counts), 1)
     total = sum(counts)
     fields = [k for k in store if k != "count"]
@@ -67,9 +114,11 @@ def gather_records(store, group=None):
     for k in fields:
         v = store[k]
         lead = v.shape[:-1]
-        if v.shape[-1] < mx:
-            raise ValueError(f"store field {k} holds {v.shape[-1]} < {mx} records")
-        part = v[..., :mx].contiguous()
+        if v.shape[-1] >= mx:
+            part = v[..., :mx].contiguous()
+        else:  # this rank's store is smaller than the largest count: pad (never read)
+            part = torch.zeros(lead + (mx,), dtype=v.dtype, device=v.device)
+            part[..., :v.shape[-1]] = v
         bufs = [torch.empty_like(part) for _ in range(world)]
         dist.all_gather(bufs, part, group=group)
         merged = torch.empty(lead + (max(total, 1),), dtype=v.dtype, device=v.device)
@@ -80,3 +129,139 @@ def gather_records(store, group=None):
         out[k] = merged
     out["count"] = torch.tensor([total], dtype=store["count"].dtype, device=store["count"].device)
     return out
+
+
+def owners(agents, world):
+    """Owner rank of each agent in `agents` (round robin in the given order), as a dict."""
+    return {int(a): i % world for i, a in enumerate(agents)}
+
+
+def record_agents(store):
+    """Agent of every record of a store ([count] int64, device): LR-TS won samples carry it
+    in key >> 16 (ag_lrts_samples), shading / learning-bidder records in `agent`."""
+    n = int(store["count"][0].item())
+    if "key" in store:
+        return (store["key"][:n].to(torch.int64) >> 16) & 0xFFFF
+    return store["agent"][:n].to(torch.int64)
+
+
+def route_records(store, owner, group=None):
+    """Send every record of a store to the rank that owns its agent (`owner`: agent ->
+    rank; records of agents without an owner are dropped). One all-to-all of the counts,
+    one per field. The result is a store (same fields) holding, on each rank, every rank's
+    records of the agents it owns. Record order within the store is not meaningful: the
+    updates' sums are exact (LR-TS) or the records carry their log order (learning
+    bidders, ag_shading_samples.order), so training on the routed store equals training on
+    all records."""
+    if _world(group) == 1:
+        return store
+    return _host_staged(store, group, lambda st: _route(st, owner, group))
+
+
+def _route(store, owner, group):
+    world = _world(group)
+    _check_all(store, group)
+    dev = store["count"].device
+    agent = record_agents(store)
+    N = int(max(owner) + 1) if owner else 1
+    if agent.numel():
+        N = max(N, int(agent.max().item()) + 1)
+    table = torch.full((N,), -1, dtype=torch.int64, device=dev)
+    for a, r in owner.items():
+        table[a] = r
+    dest = table[agent] if agent.numel() else agent
+    keep = dest >= 0
+    idx = torch.nonzero(keep).flatten()
+    dest = dest[idx]
+    order = torch.argsort(dest, stable=True)
+    idx = idx[order]
+    send = torch.bincount(dest, minlength=world).to(torch.int64)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    sl, rl = [int(x) for x in send.tolist()], [int(x) for x in recv.tolist()]
+    total = sum(rl)
+    out = {}
+    for k, v in store.items():
+        if k == "count":
+            continue
+        lead = v.shape[:-1]
+        rows = v[..., idx]                                   # [..., m] in destination order
+        rows = rows.reshape(-1, rows.shape[-1]).t().contiguous()   # [m][fields]
+        dst = torch.empty((total, rows.shape[1]), dtype=v.dtype, device=dev)
+        dist.all_to_all_single(dst, rows, output_split_sizes=rl, input_split_sizes=sl, group=group)
+        merged = torch.zeros(lead + (max(total, 1),), dtype=v.dtype, device=dev)
+        merged[..., :total] = dst.t().reshape(lead + (total,))
+        out[k] = merged
+    out["count"] = torch.tensor([total], dtype=store["count"].dtype, device=dev)
+    return out
+
+
+def take_owned_rows(local, owner, group=None, device=None):
+    """Per-agent state rows (array [N, ...]) trained by their owners: every rank sends its
+    whole array (one all-gather of a few KB) and takes agent a's row from rank owner[a]
+    (agents without an owner keep the local row). Returns a numpy array like `local`."""
+    world = _world(group)
+    if world == 1:
+        return np.array(local)
+    arr = np.ascontiguousarray(local)
+    t = torch.from_numpy(arr.copy())
+    if device is not None:
+        t = t.to(device)
+    bufs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(bufs, t, group=group)
+    bufs = [b.cpu().numpy() for b in bufs]
+    out = arr.copy()
+    for a, r in owner.items():
+        out[a] = bufs[r][a]
+    return out
+
+
+def _gather_device(eng, group=None):
+    """Where take_owned_rows' all-gather runs: the GPU under RCCL ("nccl"), host under gloo."""
+    return eng.device if dist.get_backend(group) == "nccl" else None
+
+
+def lrts_update_agent_parallel(eng, store, lrts_agents, group=None):
+    """Agent.update of every LR-TS allocator (src/Agent.py:79-91) across ranks: samples
+    routed to their agent's owner, each owner trains its agents (ag_lrts_update; agents
+    with < 2 samples -- here every agent it does not own -- are left unchanged), then every
+    rank loads the owners' posteriors. Bit-identical to one process training on all
+    samples (exact sums). Returns the epochs [N] (owners' values)."""
+    if _world(group) == 1:
+        return eng.lrts_update(store)
+    own = owners(lrts_agents, _world(group))
+    st = route_records(store, own, group)
+    ep = eng.lrts_update(st)
+    dev = _gather_device(eng, group)
+    m, q, pm = (take_owned_rows(x, own, group, dev) for x in eng.lrts_state())
+    eng.load_lrts(m, q, pm, thompson_sampling=eng.ts_sample)
+    return take_owned_rows(ep, own, group, dev)
+
+
+def bidder_update_agent_parallel(eng, store, learners, group=None):
+    """Agent.update of every learning bidder (src/Agent.py:79-94 -> Bidder.update) across
+    ranks: records routed to their agent's owner (they carry their log order, which the
+    trainer restores), each owner trains its own agents (ag_bidder_update with an agent
+    mask; synthetic rsample noise keyed by agent and log position, so the fit does not
+    depend on the rank), then every rank takes the owners' models. Returns (epochs [N][3],
+    status [N])."""
+    world = _world(group)
+    N = eng.N
+    if world == 1:
+        return eng.bidder_update(store, None, np.zeros(N, np.int64), 0)
+    rank = dist.get_rank(group)
+    own = owners(learners, world)
+    st = route_records(store, own, group)
+    mask = np.zeros(N, np.int32)
+    for a, r in own.items():
+        if r == rank:
+            mask[a] = 1
+    ep = np.zeros((N, 3), np.int32)
+    stat = np.zeros(N, np.int32)
+    if mask.any():
+        ep, stat = eng.bidder_update(st, None, np.zeros(N, np.int64), 0, agents=mask)
+    dev = _gather_device(eng, group)
+    state, init = eng.dr_state()
+    state, init = take_owned_rows(state, own, group, dev), take_owned_rows(init, own, group, dev)
+    eng.set_dr_state(state, init)
+    return take_owned_rows(ep, own, group, dev), take_owned_rows(stat, own, group, dev)

@@ -218,26 +218,27 @@ def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True):
                         "unit": "GB/s", "frac": bpa * B / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                         "traffic": traffic}}
     if with_update:
-        from auctiongym_amd.sharding import gather_records
+        from auctiongym_amd.sharding import lrts_update_agent_parallel
         st = eng.new_lrts_samples(B)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
         eng.lrts_collect(inp, out, st)
-        if world > 1:  # every rank trains on all ranks' samples: identical models everywhere
-            st = gather_records(st)
-        ep = eng.lrts_update(st)  # synchronises
+        # agent-parallel at N > 1: samples routed to their agent's owner rank, owners train,
+        # posteriors exchanged (sharding.lrts_update_agent_parallel)
+        ep = lrts_update_agent_parallel(eng, st, list(range(N)))  # synchronises
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3
         if world > 1:
             t = torch.tensor([ms], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             ms = float(t[0])
-        res["agent_update"] = {"ms": ms, "won_samples": int(st["count"][0]),
+        res["agent_update"] = {"ms": ms, "won_samples_rank0": int(st["count"][0]),
                                "epochs": [int(e) for e in ep],
                                "what": "Agent.update of all 8 LR-TS agents (ag_lrts_collect"
-                                       + (" + all-gather of the won samples over RCCL" if world > 1 else "")
+                                       + (" + won samples routed to their agent's owner rank, posteriors "
+                                          "exchanged over RCCL" if world > 1 else "")
                                        + " + ag_lrts_update: Adam, ReduceLROnPlateau, early stop, Laplace q)"}
     eng.close()
     return res
@@ -332,7 +333,8 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
     and learning bidders, on the GPU, synthetic rsample noise; records all-gathered when N > 1)
     timed, then the timed steps with bids from the fitted policies. Inputs Philox-generated
     and resident in HBM."""
-    from auctiongym_amd.sharding import allreduce_counters, gather_records, shard_range
+    from auctiongym_amd.sharding import (allreduce_counters, bidder_update_agent_parallel,
+                                         lrts_update_agent_parallel, shard_range)
     eng, what, B0, ak, bk, st16, dims = build_population(key, local)
     B = int(batch or B0)
     N, K, E, P, Do = (dims[k] for k in ("N", "K", "E", "P", "Do"))
@@ -355,11 +357,11 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
         t0 = time.perf_counter()
         eng.lrts_collect(inp, out, lst)
         eng.shading_collect(inp, out, sst, first_auction=lo)
-        if world > 1:
-            lst, sst = gather_records(lst), gather_records(sst)
-        lep = eng.lrts_update(lst)
+        # agent-parallel at N > 1 (each learner trained by one owner rank on every rank's
+        # records of it; sharding.*_agent_parallel); identical to one process
+        lep = lrts_update_agent_parallel(eng, lst, [a for a in range(N) if ak[a] == 1])
         t1 = time.perf_counter()
-        ep, stat = eng.bidder_update(sst, None, np.zeros(N, np.int64), 0)
+        ep, stat = bidder_update_agent_parallel(eng, sst, [a for a in range(N) if bk[a] >= 2])
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         ms = [(t1 - t0) * 1e3, (t2 - t1) * 1e3]
@@ -374,7 +376,8 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
             "bidder_epochs": [[int(x) for x in ep[a]] for a in learners[:4]],
             "what": "Agent.update of every learner: LR-TS allocators (ag_lrts_update) + learning bidders "
                     "(ag_bidder_update: win-rate fit, imitation, policy fit; synthetic on-device rsample noise)"
-                    + (" on the all-gathered records" if world > 1 else "")}
+                    + (f"; agent-parallel over {world} ranks: records routed to their agent's owner "
+                       "(all-to-all), owners train, models exchanged (all-gather)" if world > 1 else "")}
         _, init = eng.dr_state()
     else:
         init = np.where(bk >= 2, 1, 0).astype(np.int32)

@@ -177,3 +177,175 @@ def test_bidder_update_on_gathered_records_is_rank_independent(tmp_path, oracle,
     want = np.concatenate([r["wr"], r["epochs"].astype(np.float32)])
     for g in got:
         assert np.array_equal(g, want)
+
+
+# ---- agent-parallel learner updates (sharding.route_records / take_owned_rows: the path
+# bench.py and sharding.*_agent_parallel take at N > 1)
+
+def _lrts_agents_case():
+    """The reference's SP_Truthful_TS won samples (agent 2's KAT) relabelled over 3 agents."""
+    kat = np.load(os.path.join(ROOT, "tests", "golden", "sp_ts_update_kat.npz"))
+    X, A, y = kat["a2_X"], kat["a2_A"], kat["a2_y"]
+    agent = np.arange(len(y)) % 3
+    return kat, X, A, y, agent
+
+
+def _lrts_route_worker(rank, world, port, out_path):
+    import sys
+    for p in (os.path.join(ROOT, "auction-gym_amd"), os.path.join(ROOT, "oracle")):
+        sys.path.insert(0, p)
+    import oracle as O
+    from auctiongym_amd.sharding import owners, route_records, shard_range, take_owned_rows
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    kat, X, A, y, agent = _lrts_agents_case()
+    lo, hi = shard_range(len(y), rank, world)  # this rank's auctions' won samples
+    key = (agent[lo:hi].astype(np.int64) << 16) | (A[lo:hi].astype(np.int64) << 1) | (y[lo:hi] != 0)
+    cap = hi - lo + 3
+    st = {"key": torch.zeros(cap, dtype=torch.int32), "x": torch.zeros((5, cap), dtype=torch.float32),
+          "count": torch.tensor([hi - lo], dtype=torch.int64)}
+    st["key"][:hi - lo] = torch.from_numpy(key.astype(np.uint32).view(np.int32))
+    st["x"][:, :hi - lo] = torch.from_numpy(X[lo:hi].astype(np.float32).T)
+    own = owners([0, 1, 2], world)
+    r = route_records(st, own)
+    n = int(r["count"][0])
+    k = r["key"][:n].numpy().view(np.uint32)
+    xs = r["x"][:, :n].numpy().T
+    ag = k >> 16
+    assert set(ag.tolist()) <= {a for a, o in own.items() if o == rank}  # only owned agents arrive
+    m = np.zeros((3,) + kat["a2_m0"].shape, np.float32)
+    q = np.zeros_like(m)
+    ep = np.zeros(3, np.int64)
+    for a in range(3):
+        if own[a] == rank:
+            sel = ag == a
+            m[a], _, q[a], ep[a], _ = O.lrts_update(xs[sel], (k[sel] >> 1) & 0x7FFF, k[sel] & 1, kat["a2_m0"],
+                                                   kat["a2_prevm0"], kat["a2_q0"])
+    m, q, ep = (take_owned_rows(v, own) for v in (m, q, ep))
+    np.save(out_path + f".{rank}.npy", np.concatenate([m.ravel(), q.ravel(), ep.astype(np.float32)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_lrts_agent_parallel_update_equals_single_process(tmp_path, oracle, world):
+    """Won samples of 3 LR-TS agents sharded by auction over ranks; each is routed to its
+    agent's owner (all-to-all), owners train their agents, posteriors exchanged
+    (all-gather): every rank ends with the single-process models bit for bit, and no rank
+    trains an agent it does not own."""
+    out = str(tmp_path / "lrts_ap")
+    mp.spawn(_lrts_route_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    kat, X, A, y, agent = _lrts_agents_case()
+    m = np.zeros((3,) + kat["a2_m0"].shape, np.float32)
+    q = np.zeros_like(m)
+    ep = np.zeros(3, np.int64)
+    for a in range(3):
+        s = agent == a
+        m[a], _, q[a], ep[a], _ = oracle.lrts_update(X[s], A[s], y[s], kat["a2_m0"], kat["a2_prevm0"], kat["a2_q0"])
+    want = np.concatenate([m.ravel(), q.ravel(), ep.astype(np.float32)])
+    for r in range(world):
+        assert np.array_equal(np.load(out + f".{r}.npy"), want)
+
+
+def _dm_agents_case():
+    kat = np.load(os.path.join(ROOT, "tests", "golden", "dm_update_kat.npz"))
+    k = lambda s: kat[f"a2_{s}"]  # noqa: E731
+    n = len(k("est_ctr"))
+    agent = (np.arange(n) % 2).astype(np.int32)  # the reference's records split over 2 agents
+    wr0 = np.concatenate([k("wr0_0").ravel(), k("wr0_1").ravel()])
+    pol0 = np.concatenate([k(f"pol0_{i}").ravel() for i in (0, 1, 4, 5, 8, 9)])
+    return k, n, agent, wr0, pol0
+
+
+def _bidder_route_worker(rank, world, port, out_path):
+    import sys
+    for p in (os.path.join(ROOT, "auction-gym_amd"), os.path.join(ROOT, "oracle")):
+        sys.path.insert(0, p)
+    import oracle as O
+    from auctiongym_amd.sharding import owners, route_records, shard_range, take_owned_rows
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    k, n, agent, wr0, pol0 = _dm_agents_case()
+    lo, hi = shard_range(n, rank, world)
+    cap = hi - lo + 5
+    st = {"agent": torch.zeros(cap, dtype=torch.int32), "order": torch.zeros(cap, dtype=torch.int64)}
+    for f in ("gamma", "utility", "ctr", "value", "propensity"):
+        st[f] = torch.zeros(cap, dtype=torch.float64)
+    st["won"] = torch.zeros(cap, dtype=torch.uint8)
+    st["count"] = torch.tensor([hi - lo], dtype=torch.int64)
+    for f, v in (("agent", agent), ("gamma", k("gamma")), ("utility", k("util")), ("ctr", k("est_ctr")),
+                 ("value", k("value")), ("propensity", k("propensity")), ("won", k("won").astype(np.uint8)),
+                 ("order", np.arange(n, dtype=np.int64))):
+        st[f][:hi - lo] = torch.from_numpy(np.ascontiguousarray(v[lo:hi]))
+    own = owners([1, 0], world)  # owner order need not follow agent order
+    r = route_records(st, own)
+    m = int(r["count"][0])
+    ag = r["agent"][:m].numpy()
+    assert set(ag.tolist()) <= {a for a, o in own.items() if o == rank}
+    wr = np.zeros((2, 4), np.float32)
+    ep = np.zeros((2, 3), np.int32)
+    for a in range(2):
+        if own[a] != rank:
+            continue
+        sel = np.nonzero(ag == a)[0]
+        idx = sel[np.argsort(r["order"][:m].numpy()[sel], kind="stable")]  # the trainer's log-order sort
+        col = {f: r[f][:m].numpy()[idx] for f in ("ctr", "value", "gamma", "won")}
+        res = O.vl_update(col["ctr"], col["value"], col["gamma"], col["won"], wr0, pol0, False, None)
+        wr[a], ep[a] = res["wr"], res["epochs"]
+    wr, ep = take_owned_rows(wr, own), take_owned_rows(ep, own)
+    np.save(out_path + f".{rank}.npy", np.concatenate([wr.ravel(), ep.ravel().astype(np.float32)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bidder_agent_parallel_update_equals_single_process(tmp_path, oracle, world):
+    """Learning-bidder records of 2 agents sharded by auction; routed to their owners, who
+    restore log order and fit; models exchanged: every rank holds the single-process win-rate
+    models and epochs (FP_DM_TS KAT records). With world 3 one rank owns nothing."""
+    out = str(tmp_path / "vl_ap")
+    mp.spawn(_bidder_route_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    k, n, agent, wr0, pol0 = _dm_agents_case()
+    wr = np.zeros((2, 4), np.float32)
+    ep = np.zeros((2, 3), np.int32)
+    for a in range(2):
+        s = agent == a
+        res = oracle.vl_update(k("est_ctr")[s], k("value")[s], k("gamma")[s], k("won")[s], wr0, pol0, False, None)
+        wr[a], ep[a] = res["wr"], res["epochs"]
+    want = np.concatenate([wr.ravel(), ep.ravel().astype(np.float32)])
+    for r in range(world):
+        assert np.array_equal(np.load(out + f".{r}.npy"), want)
+
+
+def _overflow_worker(rank, world, port, out_path):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "auction-gym_amd"))
+    from auctiongym_amd.sharding import gather_records, owners, route_records
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cap = 4 + rank  # ranks hold different capacities
+    st = {"agent": torch.zeros(cap, dtype=torch.int32), "gamma": torch.zeros(cap, dtype=torch.float64),
+          "count": torch.tensor([cap + 2 if rank == 1 else 2], dtype=torch.int64)}  # rank 1 overflowed
+    res = []
+    for fn in (lambda: gather_records(st), lambda: route_records(st, owners([0], world))):
+        try:
+            fn()
+            res.append(0)
+        except ValueError:
+            res.append(1)
+    ok = {"agent": torch.zeros(cap, dtype=torch.int32), "count": torch.tensor([3 + rank], dtype=torch.int64)}
+    g = gather_records(ok)  # capacities below the largest count are padded, not refused
+    res.append(int(g["count"][0]))
+    np.save(out_path + f".{rank}.npy", np.array(res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_store_overflow_raises_on_every_rank(tmp_path):
+    """A rank whose record store overflowed makes gather_records / route_records raise on
+    EVERY rank (no rank left waiting in a collective); stores smaller than another rank's
+    count are padded."""
+    out = str(tmp_path / "ovf")
+    mp.spawn(_overflow_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        assert np.load(out + f".{r}.npy").tolist() == [1, 1, 7]
