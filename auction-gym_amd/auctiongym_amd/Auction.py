@@ -24,7 +24,7 @@ import torch
 from . import Agent as _agent_mod
 from . import _lib
 from .engine import AuctionEngine
-from .replay import draw_round, draw_round_population
+from .replay import draw_round, draw_round_population, draw_rounds_native
 
 C = _agent_mod.C
 
@@ -166,9 +166,43 @@ class Auction:
         if len(self._pending) >= self._flush_limit():
             self._flush()
 
+    def _native_draws(self):
+        """True when every draw of a round comes from the numpy generator (no torch Thompson
+        or rsample draws, no search grids): then ag_replay_draw makes them in C."""
+        if self._lrts.any() and self._ts:
+            return False
+        if self._learning.any():
+            for i, a in enumerate(self.agents):
+                if self._learning[i] and a.bidder._learner_state() != _lib.LEARNER_UNINITIALISED:
+                    return False
+        return isinstance(self.rng.bit_generator, np.random.PCG64)
+
     def simulate_batch(self, B):
-        """B rounds with the reference's draws, run as one batch."""
-        for _ in range(int(B)):
+        """B rounds with the reference's draws, run as one batch. Draws that all come from
+        the numpy generator are made in C for the whole batch (replay.draw_rounds_native:
+        the same numbers and generator state as the per-round loop)."""
+        B = int(B)
+        if self._native_draws():
+            self._flush()
+            N, P = len(self.agents), self.num_participants_per_round
+            shading = None
+            if self._shading.any():
+                shading = [(a.bidder.prev_gamma, a.bidder.gamma_sigma) if self._shading[i] else None
+                           for i, a in enumerate(self.agents)]
+            for lo in range(0, B, self.FLUSH_ROUNDS):
+                n = min(self.FLUSH_ROUNDS, B - lo)
+                ctx, part, u, g = draw_rounds_native(self.rng, n, N, P, self.embedding_size, self.embedding_var,
+                                                     self.max_slots, shading)
+                d = self._engine.device
+                inp = {"ctx": torch.from_numpy(ctx).to(d), "part": torch.from_numpy(part).to(d),
+                       "u": torch.from_numpy(u).to(d)}
+                if self._shading.any():
+                    inp["gamma_raw"] = torch.from_numpy(g).to(d)
+                if self._learning.any():
+                    inp["policy_eps"] = torch.zeros((P, n), dtype=torch.float32, device=d)
+                self._run(inp)
+            return
+        for _ in range(B):
             self._draw_round()
             if len(self._pending) >= self._flush_limit():
                 self._flush()

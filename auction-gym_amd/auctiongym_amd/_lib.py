@@ -40,7 +40,8 @@ EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params
            "ag_shading_collect", "ag_empirical_update", "ag_set_dr_state", "ag_get_dr_state",
            "ag_shading_counts", "ag_dr_update", "ag_set_bidder_modes", "ag_bidder_update",
            "ag_generate_search_grid", "ag_simulate_generated", "ag_stream_copy", "ag_estimate_ctr", "ag_bid",
-           "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_last_error", "ag_abi_version")
+           "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_replay_draw", "ag_last_error",
+           "ag_abi_version")
 ABI_VERSION = 15
 LEARNER_UNINITIALISED, LEARNER_POLICY, LEARNER_SEARCH = 0, 1, 2
 VL_SEARCH, VL_POLICY = 0, 1
@@ -89,6 +90,12 @@ class AgShadingSamples(_Sized):
                 ("capacity", ctypes.c_int64), ("count", ctypes.c_void_p), ("ctr", ctypes.c_void_p),
                 ("value", ctypes.c_void_p), ("propensity", ctypes.c_void_p), ("won", ctypes.c_void_p),
                 ("order", ctypes.c_void_p)]
+
+
+class AgPcg64State(_Sized):
+    _fields_ = [("struct_size", ctypes.c_uint64), ("state_hi", ctypes.c_uint64), ("state_lo", ctypes.c_uint64),
+                ("inc_hi", ctypes.c_uint64), ("inc_lo", ctypes.c_uint64), ("has_uint32", ctypes.c_int32),
+                ("uinteger", ctypes.c_uint32)]
 
 
 class AgError(RuntimeError):
@@ -145,6 +152,8 @@ def load(path=None):
         "ag_stream_copy": (ctypes.c_int, [vp, vp, i64, vp]),
         "ag_estimate_ctr": (ctypes.c_int, [vp, i32, i64, vp, vp, vp, vp]),
         "ag_bid": (ctypes.c_int, [vp, i32, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "ag_replay_draw": (ctypes.c_int, [ctypes.POINTER(AgPcg64State), i64, i32, i32, i32, ctypes.c_double, i32,
+                                          vp, vp, vp, vp, vp, vp, vp]),
         "ag_last_error": (ctypes.c_char_p, []),
         "ag_abi_version": (i32, []),
     }

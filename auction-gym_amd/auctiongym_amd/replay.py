@@ -44,6 +44,54 @@ def draw_rounds(rng, B, num_agents, num_participants, embedding_size, embedding_
     return ctx, part, u
 
 
+M128 = (1 << 128) - 1
+M64 = (1 << 64) - 1
+
+
+def draw_rounds_native(rng, B, num_agents, num_participants, embedding_size, embedding_var, max_slots=1,
+                       shading=None, out=None):
+    """B rounds of draw_round (and, with `shading` [N] of (prev_gamma, gamma_sigma) or None,
+    of draw_round_population's numpy-only draws: the shading bidders' Gaussian gammas) in C
+    (ag_replay_draw), the same numbers and the same generator state afterwards as the Python
+    loop. rng must be a numpy Generator on PCG64. Returns SoA host arrays ctx [E][B], part
+    [P][B] int32, u [B] and gamma_raw [P][B] (NaN where nothing is drawn; None without
+    shading). `out` may supply the arrays (e.g. pinned host tensors' numpy views)."""
+    import ctypes
+
+    from . import _lib
+    bg = rng.bit_generator
+    st = bg.state
+    if st.get("bit_generator") != "PCG64":
+        raise NotImplementedError("ag_replay_draw restates numpy's PCG64 only")
+    s, inc = int(st["state"]["state"]), int(st["state"]["inc"])
+    c = _lib.AgPcg64State(s >> 64, s & M64, inc >> 64, inc & M64, int(st["has_uint32"]), int(st["uinteger"]))
+    B, N, P, E = int(B), int(num_agents), int(num_participants), int(embedding_size)
+    o = out or {}
+    ctx = o.get("ctx") if o.get("ctx") is not None else np.empty((E, B))
+    part = o.get("part") if o.get("part") is not None else np.empty((P, B), np.int32)
+    u = o.get("u") if o.get("u") is not None else np.empty(B)
+    g = None
+    sh = pg = gs = None
+    if shading is not None:
+        g = o.get("gamma_raw") if o.get("gamma_raw") is not None else np.empty((P, B))
+        sh = np.array([x is not None for x in shading], np.uint8)
+        pg = np.array([x[0] if x is not None else 0.0 for x in shading], np.float64)
+        gs = np.array([x[1] if x is not None else 1.0 for x in shading], np.float64)
+    for a in (ctx, part, u) + ((g,) if g is not None else ()):
+        if not a.flags.c_contiguous:
+            raise ValueError("replay arrays must be C-contiguous")
+    ptr = lambda a: None if a is None else a.ctypes.data  # noqa: E731
+    L = _lib.load()
+    _lib.check(L.ag_replay_draw(ctypes.byref(c), B, N, P, E, float(embedding_var), int(max_slots), ptr(sh), ptr(pg),
+                                ptr(gs), ptr(ctx), ptr(part), ptr(g), ptr(u)), "ag_replay_draw", L)
+    st["state"]["state"] = (int(c.state_hi) << 64) | int(c.state_lo)
+    st["state"]["inc"] = (int(c.inc_hi) << 64) | int(c.inc_lo)
+    st["has_uint32"] = int(c.has_uint32)
+    st["uinteger"] = int(c.uinteger)
+    bg.state = st
+    return ctx, part, u, g
+
+
 def draw_round_population(rng, num_agents, num_participants, embedding_size, embedding_var,
                           shading, ts_models, max_slots=1, policy=None, search=None):
     """One round of a general population. shading[a] = (prev_gamma, gamma_sigma) of a shading

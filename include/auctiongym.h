@@ -281,6 +281,31 @@ int ag_generate_noise(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_
                       const int32_t *part, double *gamma_raw, float *ts_noise, float *policy_eps,
                       void *stream);
 
+/* ---- Replay-mode draws on the host (src/Auction.py:30-42, :65; src/main.py:29) -----------
+ * B rounds of the reference's numpy draws in its order, without a Python round trip per
+ * round: per round rng.integers(1, max_slots + 1) (nothing drawn for one slot),
+ * rng.normal(0, embedding_var, E), rng.choice(N, P, replace=False), for every slot whose
+ * agent is a shading bidder in its Gaussian state rng.normal(prev_gamma, gamma_sigma)
+ * (src/Bidder.py:51, 177, 354, 461), then the next_double rng.binomial(1, p) consumes.
+ * The generator is numpy's PCG64 bit generator: its state (bit_generator.state) goes in and
+ * comes back advanced past the B rounds; the distributions are numpy's own (libnpyrandom).
+ * Host arrays, SoA with leading dimension B (the ag_batch_in layout): ctx [E][B],
+ * part [P][B], gamma_raw [P][B] (NaN where nothing is drawn; may be NULL when shading is
+ * NULL), u [B]. shading: host uint8 [N] (NULL: none), prev_gamma / gamma_sigma host [N].
+ * Draws that come from torch's generator (Thompson noise, fitted-policy rsample) are not
+ * made here. AG_ERR_INVALID with numpy's message when P > N. */
+typedef struct ag_pcg64_state {
+  uint64_t struct_size; /* sizeof(ag_pcg64_state) (ABI 15)                                  */
+  uint64_t state_hi, state_lo; /* the 128-bit LCG state                                     */
+  uint64_t inc_hi, inc_lo;     /* the 128-bit increment                                     */
+  int32_t has_uint32;          /* numpy's buffered upper half of a 64-bit draw ...          */
+  uint32_t uinteger;           /* ... and its value                                         */
+} ag_pcg64_state;
+
+int ag_replay_draw(ag_pcg64_state *rng, int64_t B, int32_t N, int32_t P, int32_t E, double embedding_var,
+                   int32_t max_slots, const uint8_t *shading, const double *prev_gamma, const double *gamma_sigma,
+                   double *ctx, int32_t *part, double *gamma_raw, double *u);
+
 /* ---- LR-TS allocator update (Agent.update -> PyTorchLogisticRegressionAllocator.update,
  * src/Agent.py:79-91, src/BidderAllocation.py:29-65) ------------------------------------
  * The won samples of LR-TS agents (Agent.update's won_mask) accumulate in a caller-owned

@@ -112,7 +112,9 @@ int64_t ora_to_fx(double x) {
 }
 
 static void add_limbs(int64_t *L, __int128 v) {
-  __int128 t = ((__int128)L[2] << 84) + ((__int128)L[1] << 42) + (__int128)L[0] + v;
+  /* multiplications, not shifts: the top limb of a negative sum is negative (a left shift of
+   * a negative value is undefined; found by the UBSan build, tools/sanitize_oracle.sh) */
+  __int128 t = (__int128)L[2] * ((__int128)1 << 84) + (__int128)L[1] * ((__int128)1 << 42) + (__int128)L[0] + v;
   const int64_t mask = ((int64_t)1 << 42) - 1;
   L[0] = (int64_t)(t & mask);
   t >>= 42;

@@ -12,7 +12,9 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_SO = os.path.join(_HERE, "libag_oracle.so")
+# AG_ORACLE_LIB selects another build of the checker, e.g. the sanitizer build
+# (make -C oracle sanitize; tools/sanitize_oracle.sh runs the oracle tests under it)
+_SO = os.environ.get("AG_ORACLE_LIB") or os.path.join(_HERE, "libag_oracle.so")
 
 FIRST_PRICE, SECOND_PRICE = 0, 1
 COUNTERS = ("net", "gross", "allocation_regret", "estimation_regret", "overbid_regret",
@@ -49,7 +51,8 @@ class _Out(ctypes.Structure):
 
 
 def build():
-    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    if not os.environ.get("AG_ORACLE_LIB"):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
 
 
 def lib():

@@ -42,7 +42,8 @@ def test_ctypes_structs_match_the_c_header(tmp_path):
     import ctypes
     from auctiongym_amd import _lib
     structs = {"ag_shape": _lib.AgShape, "ag_batch_in": _lib.AgBatchIn, "ag_batch_out": _lib.AgBatchOut,
-               "ag_lrts_samples": _lib.AgLrtsSamples, "ag_shading_samples": _lib.AgShadingSamples}
+               "ag_lrts_samples": _lib.AgLrtsSamples, "ag_shading_samples": _lib.AgShadingSamples,
+               "ag_pcg64_state": _lib.AgPcg64State}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "auctiongym.h"', "int main(void) {"]
     for cname, cls in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
@@ -114,6 +115,66 @@ def test_replay_draws_reproduce_reference_inputs(tmp_path):
     ctx, part, u = draw_rounds(rng, 4096, meta["N"], meta["P"], meta["E"], meta["var"])
     assert np.array_equal(ctx.T, d["ctx"]) and np.array_equal(part.T, d["part"])
     assert np.array_equal(u, d["u"])
+
+
+def test_replay_draws_native_reproduce_reference_inputs(tmp_path):
+    """ag_replay_draw (C: PCG64 restated, numpy's own distributions) gives the reference's
+    captured SP_Oracle inputs and leaves the generator where the Python loop leaves it."""
+    import auctiongym_amd.main as M
+    from auctiongym_amd.replay import draw_rounds, draw_rounds_native
+    d, meta, _ = load_capture("sp_oracle_r4096")
+    rng, *_ = M.parse_config(_sp_config(tmp_path))
+    rng2, *_ = M.parse_config(_sp_config(tmp_path))
+    ctx, part, u, g = draw_rounds_native(rng, 4096, meta["N"], meta["P"], meta["E"], meta["var"])
+    assert g is None
+    assert np.array_equal(ctx.T, d["ctx"]) and np.array_equal(part.T, d["part"]) and np.array_equal(u, d["u"])
+    draw_rounds(rng2, 4096, meta["N"], meta["P"], meta["E"], meta["var"])
+    assert rng.bit_generator.state == rng2.bit_generator.state
+
+
+@pytest.mark.parametrize("N,P,E,var,slots,seed", [
+    (6, 2, 5, 1.0, 1, 0), (1, 1, 3, 0.5, 1, 1), (8, 8, 5, 2.0, 3, 2), (40, 7, 0, 1.0, 2, 3),
+    (33, 32, 6, 1.0, 1, 4), (3, 3, 5, 1.0, 5, 5),
+    (20000, 500, 2, 1.0, 1, 6),   # numpy's tail-shuffle choice branch (N > 10000, P > N // 50)
+    (20000, 3, 2, 1.0, 1, 7)])    # Floyd's branch at a large population
+def test_replay_draws_native_match_numpy(N, P, E, var, slots, seed):
+    """Round for round and state for state equal to the Python loop over numpy's Generator
+    (the reference's draws), including multi-slot integers draws, P == N, the 32-bit half
+    buffer the choice leaves behind, and a generator that starts with a buffered half."""
+    from auctiongym_amd.replay import draw_rounds, draw_rounds_native
+    B = 3000 if N < 10000 else 40
+    a, b = np.random.default_rng(seed), np.random.default_rng(seed)
+    a.integers(0, 5), b.integers(0, 5)      # a 32-bit draw: has_uint32 set on entry
+    a.random(), b.random()
+    x = draw_rounds_native(a, B, N, P, E, var, slots)
+    y = draw_rounds(b, B, N, P, E, var, slots)
+    for u, v in zip(x[:3], y):
+        assert np.array_equal(u, v)
+    assert a.bit_generator.state == b.bit_generator.state
+    assert a.random() == b.random()
+
+
+def test_replay_draws_native_shading_match_numpy():
+    """With shading bidders (Gaussian gammas, src/Bidder.py:51, 177, 354, 461) in slot order:
+    the same as draw_round_population with no torch draws."""
+    from auctiongym_amd.replay import draw_round_population, draw_rounds_native
+    N, P, E, B = 7, 3, 5, 2000
+    shading = [(1.0, 0.02), None, (0.7, 0.1), None, None, (0.9, 0.05), (1.2, 0.3)]
+    a, b = np.random.default_rng(11), np.random.default_rng(11)
+    ctx, part, u, g = draw_rounds_native(a, B, N, P, E, 1.0, 1, shading=shading)
+    for r in range(B):
+        c, p, gr, uu, *_ = draw_round_population(b, N, P, E, 1.0, shading, [None] * N)
+        assert np.array_equal(ctx[:, r], c) and np.array_equal(part[:, r], p) and uu == u[r]
+        assert np.array_equal(g[:, r], gr, equal_nan=True)
+    assert a.bit_generator.state == b.bit_generator.state
+
+
+def test_replay_draws_native_errors():
+    from auctiongym_amd.replay import draw_rounds_native
+    with pytest.raises(ValueError, match="larger sample than population"):
+        draw_rounds_native(np.random.default_rng(0), 4, 3, 4, 5, 1.0)
+    with pytest.raises(NotImplementedError):
+        draw_rounds_native(np.random.Generator(np.random.MT19937(0)), 4, 6, 2, 5, 1.0)
 
 
 def test_plugin_factory_semantics(tmp_path):
