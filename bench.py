@@ -399,10 +399,18 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
 
     elapsed, kern_ms = timed_steps(step, steps, warmup, world, stream)
     bpa = algorithmic_bytes_population(E, P, K, Do, ak, bk, init)
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            tj = json.load(f).get(key, {})
+        if tj.get("batch") == B:
+            traffic = tj.get("hbm_bytes_per_launch")
     res.update({"value": B * world * steps / elapsed, "unit": "auctions/s", "ms_per_step": elapsed / steps * 1e3,
                 "kernel_ms": kern_ms, "algorithmic_bytes_per_auction": bpa,
                 "roofline": {"bound": "hbm", "achieved": bpa * B / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                             "unit": "GB/s", "frac": bpa * B / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}})
+                             "unit": "GB/s", "frac": bpa * B / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                             "traffic": traffic}})
     eng.close()
     return res
 
