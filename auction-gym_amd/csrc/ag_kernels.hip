@@ -292,6 +292,7 @@ __global__ __launch_bounds__(kThreads) void k_stream_copy(const u32x4 *__restric
 // dispatch
 // ------------------------------------------------------------------------------------
 SimKernel pick_kernel(int P, int D, bool prune, int W, bool general, int bt) {
+  if (P > kMaxP) return pick_kernel_for<0>(D, prune, W, general, bt);  // runtime-P kernel
   switch (P) {
     case 1: return pick_kernel_for<1>(D, prune, W, general, bt);
     case 2: return pick_kernel_for<2>(D, prune, W, general, bt);
@@ -448,7 +449,7 @@ int ag_create(int32_t device, const ag_shape *s, ag_ctx **out) {
   // simulate needs a kernel for (P, D) and the catalogue in LDS; allocate-only contexts
   // (any P) do not.
   const LdsLayout lay = make_layout(s->num_agents, s->num_items, D, true);
-  c->can_simulate = s->num_participants <= kMaxP && pick_kernel(s->num_participants, D, false, 1, false, kThreads) &&
+  c->can_simulate = pick_kernel(s->num_participants, D, false, 1, false, kThreads) &&
                     lay.total <= 160 * 1024;
   AgDeviceGuard g(device);
   hipError_t e = hipMalloc(&c->d_items, sizeof(double) * s->num_agents * s->num_items * D);
@@ -679,7 +680,7 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   AG_CHECK_STRUCT(out, "ag_simulate", "ag_batch_out");
   if (!c->can_simulate)
     return ag_set_error(AG_ERR_UNSUPPORTED,
-                     "ag_simulate: supports P in [1,%d], E+1 in {2..9,11,13,16} and a catalogue "
+                     "ag_simulate: supports E+1 in {2..9,11,13,16} (E+1 <= 8 when P > %d) and a catalogue "
                      "that fits LDS (P=%d, D=%d, N=%d, K=%d)",
                      kMaxP, c->shape.num_participants, c->D, c->shape.num_agents, c->shape.num_items);
   if (!c->catalog) return ag_set_error(AG_ERR_STATE, "ag_simulate: ag_load_catalog not called");
@@ -726,10 +727,11 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   prm.in = *in;
   prm.out = *out;
   prm.partials = c->d_partials;
+  prm.P = s.num_participants;
   if (prune && !c->general && c->ora_catalog && c->sim_kernel == AG_SIM_KERNEL_AUTO && !c->wide)
     if (OraKernel ok = pick_oracle(s.num_participants, D, false))
       return simulate_oracle(c, ok, B, in, out, counters_fx, (hipStream_t)stream);
-  const int W = (prune && (B % 2) == 0 && c->wide && !c->general) ? 2 : 1;
+  const int W = (prune && (B % 2) == 0 && c->wide && !c->general && s.num_participants <= kMaxP) ? 2 : 1;
   const size_t lds = (size_t)prm.lds.total;
   if (lds > 160 * 1024)
     return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);

@@ -187,6 +187,7 @@ struct SimParams {
   ag_batch_in in;
   ag_batch_out out;
   int64_t *partials;      // [grid][N][AG_NUM_COUNTERS][2]
+  int32_t P;              // participants per round (read by the runtime-P kernel, P = 0)
 };
 
 // Screening margin. The screen ranks items by t_k = (1 + 2^(z'_k)) / v_k = 1 / (exact
@@ -579,6 +580,85 @@ __device__ __forceinline__ double shading_propensity(double pg, double sigma, do
   return agexp::exp_fast(-(t * t) / 2.0, tab) / (sigma * 2.5066282746310002);  // sqrt(2 pi)
 }
 
+// One participant (slot s, agent a) of a round: its item, bid and the values its log
+// record and counters need (src/Auction.py:44-53, src/Agent.py:29-68).
+struct SlotResult {
+  int item;
+  double val, bid, ctr, est, bev, gamma, prop;
+};
+
+template <int D, bool PRUNE, bool GENERAL>
+__device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const double (&x)[kMaxD],
+                                                   const float (&xf)[kMaxD], float xabs, int a, int s,
+                                                   const ag_batch_in &in, uint32_t B, uint32_t i, bool ts_sample) {
+  // true CTRs (src/Auction.py:52-53): exact search on the true context; for an Oracle
+  // agent this IS Agent.select_item (src/BidderAllocation.py:81-82)
+  double c, bs;
+  const double *itm = T.items + a * T.items_stride;
+  const int best_t = select_item<D, PRUNE>(itm, T.vals + a * T.values_stride,
+                                           T.scr + a * T.scr_stride, T.scr_val + a * T.scr_val_stride,
+                                           PRUNE ? T.amax[a] : 0.0f, K, T.kpairs, x, xf, xabs, T.tab, c, bs);
+  int best = best_t;
+  double est = c, tru = c;
+  double g = NAN, prop = NAN;
+  if constexpr (GENERAL) {
+    if (T.akind[a] == AG_ALLOCATOR_LRTS) {
+      // LR-TS (src/Agent.py:29-42): the sampled CTRs on the observed context pick the
+      // item by first argmax of CTR * value (float32 CTR widened to double), the MAP CTR
+      // of that item is the estimate
+      const int Do = T.ts_do;
+      const float *m = T.tsm + (size_t)a * K * Do;
+      // tiled noise: coefficient c of auction i at ((s*T + i/64)*K*Do + c)*64 + i%64
+      const float *nz = (ts_sample && in.ts_noise)
+                            ? in.ts_noise + ((size_t)(s * ((B + 63) >> 6) + (i >> 6)) * K * Do) * 64 + (i & 63)
+                            : nullptr;
+      // observed context (src/Auction.py:36) in a register row of width D >= Do
+      float xo[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) xo[d] = d < Do - 1 ? (float)x[d] : (d == Do - 1 ? 1.0f : 0.0f);
+      best = ts_select<D>(m, xo, nz, K, Do, T.vals + a * T.values_stride, T.tab);
+      est = (double)ts_ctr_k<D>(m + best * Do, xo, xo, false, Do, T.tab);
+      tru = best == best_t ? c : agexp::sigmoid_fast(dot_ref<D>(itm + best * D, x), T.tab);
+    }
+  }
+  const double v = T.vals[a * T.values_stride + best];
+  double b = v * est;  // Bidder.bid: value * estimated CTR (src/Bidder.py:35, :49, :173, ...)
+  if constexpr (GENERAL) {
+    const int bk = T.bkind[a];
+    if (bk >= AG_BIDDER_VALUE_LEARNING && T.drs && T.dri[a] == AG_LEARNER_POLICY) {  // the fitted policy
+      policy_bid(T.drs + a * 16 + 4, est, v, in.policy_eps[(size_t)s * B + i], T.tab, g, prop);
+      b = b * g;
+    } else if (bk == AG_BIDDER_VALUE_LEARNING && T.drs && T.dri[a] == AG_LEARNER_SEARCH) {
+      g = search_gamma(T.drs + a * 16, est, v, in.gamma_grid + (size_t)s * 128 * B + i, B, T.tab);
+      prop = 1.0;  // src/Bidder.py:196
+      b = b * g;
+    } else if (bk != AG_BIDDER_TRUTHFUL) {
+      g = in.gamma_raw[(size_t)s * B + i];
+      if (bk == AG_BIDDER_EMPIRICAL_SHADED) {  // clipped to [0, 1] (src/Bidder.py:52-55)
+        if (g < 0.0) g = 0.0;
+        if (g > 1.0) g = 1.0;
+      } else {
+        prop = shading_propensity(T.pg[a], T.gs[a], g, T.tab);
+      }
+      b = b * g;  // bid *= gamma
+    }
+  }
+  return SlotResult{best, v, b, tru, est, bs, g, prop};  // bev: max_k true_CTR_k * value_k (src/Auction.py:53)
+}
+
+// streaming top-2 of the bids in slot order, ties -> lowest slot (src/AuctionAllocation.py:19-34)
+__device__ __forceinline__ void top2_step(int s, double b, double &m1, double &m2, int &w) {
+  if (s == 0) {
+    m1 = b;
+  } else if (b > m1) {
+    m2 = m1;
+    m1 = b;
+    w = s;
+  } else if (b > m2) {
+    m2 = b;
+  }
+}
+
 template <int P, int D, bool PRUNE, bool GENERAL>
 __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const double (&x)[kMaxD],
                                         const float (&xf)[kMaxD], float xabs, const int (&ag)[P], double u,
@@ -590,76 +670,16 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
   for (int s = 0; s < P; ++s) {
     const int a = ag[s];
     r.ag[s] = a;
-    // true CTRs (src/Auction.py:52-53): exact search on the true context; for an Oracle
-    // agent this IS Agent.select_item (src/BidderAllocation.py:81-82)
-    double c, bs;
-    const double *itm = T.items + a * T.items_stride;
-    const int best_t = select_item<D, PRUNE>(itm, T.vals + a * T.values_stride,
-                                             T.scr + a * T.scr_stride, T.scr_val + a * T.scr_val_stride,
-                                             PRUNE ? T.amax[a] : 0.0f, K, T.kpairs, x, xf, xabs, T.tab, c, bs);
-    int best = best_t;
-    double est = c, tru = c;
-    double g = NAN, prop = NAN;
-    if constexpr (GENERAL) {
-      if (T.akind[a] == AG_ALLOCATOR_LRTS) {
-        // LR-TS (src/Agent.py:29-42): the sampled CTRs on the observed context pick the
-        // item by first argmax of CTR * value (float32 CTR widened to double), the MAP CTR
-        // of that item is the estimate
-        const int Do = T.ts_do;
-        const float *m = T.tsm + (size_t)a * K * Do;
-        // tiled noise: coefficient c of auction i at ((s*T + i/64)*K*Do + c)*64 + i%64
-        const float *nz = (ts_sample && in.ts_noise)
-                              ? in.ts_noise + ((size_t)(s * ((B + 63) >> 6) + (i >> 6)) * K * Do) * 64 + (i & 63)
-                              : nullptr;
-        // observed context (src/Auction.py:36) in a register row of width D >= Do
-        float xo[D];
-#pragma unroll
-        for (int d = 0; d < D; ++d) xo[d] = d < Do - 1 ? (float)x[d] : (d == Do - 1 ? 1.0f : 0.0f);
-        best = ts_select<D>(m, xo, nz, K, Do, T.vals + a * T.values_stride, T.tab);
-        est = (double)ts_ctr_k<D>(m + best * Do, xo, xo, false, Do, T.tab);
-        tru = best == best_t ? c : agexp::sigmoid_fast(dot_ref<D>(itm + best * D, x), T.tab);
-      }
-    }
-    const double v = T.vals[a * T.values_stride + best];
-    double b = v * est;  // Bidder.bid: value * estimated CTR (src/Bidder.py:35, :49, :173, ...)
-    if constexpr (GENERAL) {
-      const int bk = T.bkind[a];
-      if (bk >= AG_BIDDER_VALUE_LEARNING && T.drs && T.dri[a] == AG_LEARNER_POLICY) {  // the fitted policy
-        policy_bid(T.drs + a * 16 + 4, est, v, in.policy_eps[s * B + i], T.tab, g, prop);
-        b = b * g;
-      } else if (bk == AG_BIDDER_VALUE_LEARNING && T.drs && T.dri[a] == AG_LEARNER_SEARCH) {
-        g = search_gamma(T.drs + a * 16, est, v, in.gamma_grid + (size_t)s * 128 * B + i, B, T.tab);
-        prop = 1.0;  // src/Bidder.py:196
-        b = b * g;
-      } else if (bk != AG_BIDDER_TRUTHFUL) {
-        g = in.gamma_raw[s * B + i];
-        if (bk == AG_BIDDER_EMPIRICAL_SHADED) {  // clipped to [0, 1] (src/Bidder.py:52-55)
-          if (g < 0.0) g = 0.0;
-          if (g > 1.0) g = 1.0;
-        } else {
-          prop = shading_propensity(T.pg[a], T.gs[a], g, T.tab);
-        }
-        b = b * g;  // bid *= gamma
-      }
-    }
-    r.item[s] = best;
-    r.val[s] = v;
-    r.bid[s] = b;
-    r.ctr[s] = tru;
-    r.est[s] = est;
-    r.bev[s] = bs;  // max_k true_CTR_k * value_k (src/Auction.py:53)
-    r.gamma[s] = g;
-    r.prop[s] = prop;
-    // streaming top-2, ties -> lowest slot (src/AuctionAllocation.py:19-34)
-    if (s == 0) {
-      m1 = b;
-    } else if (b > m1) {
-      m2 = m1;
-      m1 = b;
-      w = s;
-    } else if (b > m2) {
-      m2 = b;
-    }
+    const SlotResult q = resolve_slot<D, PRUNE, GENERAL>(T, K, x, xf, xabs, a, s, in, B, i, ts_sample);
+    r.item[s] = q.item;
+    r.val[s] = q.val;
+    r.bid[s] = q.bid;
+    r.ctr[s] = q.ctr;
+    r.est[s] = q.est;
+    r.bev[s] = q.bev;
+    r.gamma[s] = q.gamma;
+    r.prop[s] = q.prop;
+    top2_step(s, q.bid, m1, m2, w);
   }
   r.w = w;
   r.price = mech == AG_FIRST_PRICE ? m1 : m2;
@@ -746,11 +766,15 @@ __global__ __launch_bounds__(BT, GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES) void
   const int rep = tid & (R - 1);
   const ag_batch_in in = prm.in;
   const ag_batch_out out = prm.out;
-  const bool charged = P >= 2;  // P == 1: empty price arrays, nobody charged (Auction.py:68)
+  // P == 0: the runtime-P kernel (more than kMaxP participants; slot results are not kept
+  // in registers -- see the wide path in the loop)
+  constexpr int PA = P > 0 ? P : 1;  // register array extent
+  static_assert(P > 0 || !AG_PREFETCH, "the runtime-P path has no software-pipelined loads");
+  const bool charged = P == 0 ? prm.P >= 2 : P >= 2;  // P == 1: nobody charged (Auction.py:68)
 
   // inputs of one tile: the context, participants and uniform of W consecutive auctions
   double xv[kMaxD][W];
-  int pv[P][W];
+  int pv[PA][W];
   double uv[W];
   auto load_tile = [&](uint32_t i) {
 #pragma unroll
@@ -763,12 +787,47 @@ __global__ __launch_bounds__(BT, GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES) void
   // Participation / win counts: a lane resolves at most kAuctionsPerReplica * R / BT
   // (<= 255) auctions per launch, so for N <= 8 agents its counts fit 8-bit fields of one
   // register each; flushed to the LDS counters once, after the loop.
-  const bool packed = N <= 8 && kAuctionsPerReplica * R / BT <= 255;
+  const bool packed = P > 0 && N <= 8 && kAuctionsPerReplica * R / BT <= 255;
   uint64_t n_logs_packed = 0, n_won_packed = 0;
+  // the counter terms of one participant (src/Agent.py:96-118, via the exact LDS replicas)
+  auto count_slot = [&](int a, bool won, double lp, double price, double second, double bid, double ctr,
+                        double val, double est, double bev, int oc) {
+    // [slot j][agent a][replica]: lane-private replicas, conflict-free 8-B atomics
+    auto add_raw = [&](int j, unsigned long long v) { atomicAdd(s_cnt + ((size_t)(j * N + a) * R + rep), v); };
+    // zero terms are skipped (a wave whose lanes all hold 0 issues no atomic): no clicks
+    // for GROSS, and under SecondPrice with P == 2 the loser's underbid term
+    // (price - bid) * [...] is exactly 0 because the price is its bid
+    auto add_nz = [&](int j, unsigned long long v) {
+      if (v != 0ull) add_raw(j, v);
+    };
+    const double tv = ctr * val;
+    if (won) {
+      add_nz(kSlotGross, to_fx(val * (double)oc));
+      add_raw(kSlotPaid, to_fx(price));
+      if (prm.mech == AG_FIRST_PRICE) add_nz(kSlotOverbid, to_fx(lp - second));
+    } else {
+      add_nz(kSlotUnderbid, to_fx((lp - bid) * (double)(lp < tv)));
+    }
+    add_raw(kSlotBestEv, to_fx(bev));
+    if (packed) {  // 8-bit per-agent fields in registers, flushed once per block
+      const uint64_t bit = 1ull << (8 * a);
+      n_logs_packed += bit;
+      if (won) n_won_packed += bit;
+    } else {
+      add_raw(kSlotCounts, won ? 0x100000001ull : 1ull);
+    }
+    if constexpr (GENERAL) {  // src/Agent.py:96-118 terms that vanish for Oracle agents
+      add_nz(kSlotAlloc, to_fx(bev - tv));
+      add_nz(kSlotEst, to_fx(est * val - tv));
+      const double dd = ctr - est;
+      add_nz(kSlotSqerr, to_fx(dd * dd));
+      if (won) add_raw(kSlotBias, to_fx(est / ctr));
+    }
+  };
 #if AG_PREFETCH
   // software pipelining: the next tile's loads are in flight while this tile computes
   double xn[kMaxD][W];
-  int pn[P][W];
+  int pn[PA][W];
   double un[W];
   if (lo + blockIdx.x * (BT * W) + tid * W < hi) load_tile(lo + blockIdx.x * (BT * W) + tid * W);
 #endif
@@ -792,13 +851,63 @@ __global__ __launch_bounds__(BT, GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES) void
 #define UV un
 #else
     if (i >= hi) continue;
+    if constexpr (P == 0) {
+      // more than kMaxP participants (runtime P): the slots are resolved in a loop, their
+      // outputs written as they come; the counter terms need the winner and price, so the
+      // slots are resolved once more (the same arithmetic: the same values) afterwards
+      const int Pn = prm.P;
+      double x[kMaxD];
+      float xf[kMaxD];
+      float xabs = 1.0f;
+#pragma unroll
+      for (int e = 0; e < D - 1; ++e) {
+        x[e] = ldg(in.ctx + e * B + i);
+        xf[e] = (float)x[e];
+        xabs += fabsf(xf[e]);
+      }
+      x[D - 1] = 1.0;  // intercept (src/Auction.py:33)
+      xf[D - 1] = 1.0f;
+      xabs *= 1.001f;
+      const double u = ldg(in.u + i);
+      double m1 = 0.0, m2 = -INFINITY, ctr_w = 0.0;
+      int w = 0;
+      for (int s = 0; s < Pn; ++s) {
+        const uint32_t o = (uint32_t)s * B + i;
+        const int a = ldg(in.part + o);
+        const SlotResult q = resolve_slot<D, PRUNE, GENERAL>(T, K, x, xf, xabs, a, s, in, B, i, prm.ts_sample != 0);
+        if (out.item) stg(out.item + o, (int32_t)q.item);
+        if (out.bid) stg(out.bid + o, q.bid);
+        if (out.est_ctr) stg(out.est_ctr + o, q.est);
+        if (out.true_ctr) stg(out.true_ctr + o, q.ctr);
+        if (out.best_ev) stg(out.best_ev + o, q.bev);
+        if (out.gamma) stg(out.gamma + o, q.gamma);
+        if (out.propensity) stg(out.propensity + o, q.prop);
+        top2_step(s, q.bid, m1, m2, w);
+        if (w == s) ctr_w = q.ctr;  // the current leader's true CTR
+      }
+      const double price = prm.mech == AG_FIRST_PRICE ? m1 : m2;
+      const int oc = bernoulli(ctr_w, u);  // src/Auction.py:65
+      if (out.winner) stg(out.winner + i, (int32_t)w);
+      if (out.price) stg(out.price + i, charged ? price : (double)NAN);
+      if (out.second_price) stg(out.second_price + i, charged ? m2 : (double)NAN);
+      if (out.outcome) stg(out.outcome + i, (uint8_t)oc);
+      if (prm.want_counters) {
+        for (int s = 0; s < Pn; ++s) {
+          const int a = ldg(in.part + (uint32_t)s * B + i);
+          const SlotResult q =
+              resolve_slot<D, PRUNE, GENERAL>(T, K, x, xf, xabs, a, s, in, B, i, prm.ts_sample != 0);
+          count_slot(a, charged && s == w, charged ? price : 0.0, price, m2, q.bid, q.ctr, q.val, q.est, q.bev, oc);
+        }
+      }
+      continue;
+    }
     load_tile(i);
 #define XV xv
 #define PV pv
 #define UV uv
 #endif
 
-    Resolved<P> r[W];
+    Resolved<PA> r[W];
 #pragma unroll
     for (int q = 0; q < W; ++q) {
       double x[kMaxD];
@@ -813,10 +922,10 @@ __global__ __launch_bounds__(BT, GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES) void
       x[D - 1] = 1.0;  // intercept (src/Auction.py:33)
       xf[D - 1] = 1.0f;
       xabs *= 1.001f;
-      int ag[P];
+      int ag[PA];
 #pragma unroll
       for (int s = 0; s < P; ++s) ag[s] = PV[s][q];
-      resolve<P, D, PRUNE, GENERAL>(T, K, prm.mech, x, xf, xabs, ag, UV[q], in, B, i + q,
+      resolve<PA, D, PRUNE, GENERAL>(T, K, prm.mech, x, xf, xabs, ag, UV[q], in, B, i + q,
                                     prm.ts_sample != 0, r[q]);
     }
 
@@ -861,47 +970,13 @@ __global__ __launch_bounds__(BT, GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES) void
     }
 
     if (prm.want_counters) {
-      // [slot j][agent a][replica]: lane-private replicas, conflict-free 8-B atomics
-      auto add_raw = [&](int j, int a, unsigned long long v) {
-        atomicAdd(s_cnt + ((size_t)(j * N + a) * R + rep), v);
-      };
-      // zero terms are skipped (a wave whose lanes all hold 0 issues no atomic): no clicks
-      // for GROSS, and under SecondPrice with P == 2 the loser's underbid term
-      // (price - bid) * [...] is exactly 0 because the price is its bid
-      auto add_nz = [&](int j, int a, unsigned long long v) {
-        if (v != 0ull) add_raw(j, a, v);
-      };
 #pragma unroll
       for (int q = 0; q < W; ++q) {
-        const Resolved<P> &rr = r[q];
+        const Resolved<PA> &rr = r[q];
 #pragma unroll
-        for (int s = 0; s < P; ++s) {
-          const bool won = charged && s == rr.w;
-          const double lp = charged ? rr.price : 0.0;
-          const double tv = rr.ctr[s] * rr.val[s];
-          if (won) {
-            add_nz(kSlotGross, rr.ag[s], to_fx(rr.val[s] * (double)rr.oc));
-            add_raw(kSlotPaid, rr.ag[s], to_fx(rr.price));
-            if (prm.mech == AG_FIRST_PRICE) add_nz(kSlotOverbid, rr.ag[s], to_fx(lp - rr.second));
-          } else {
-            add_nz(kSlotUnderbid, rr.ag[s], to_fx((lp - rr.bid[s]) * (double)(lp < tv)));
-          }
-          add_raw(kSlotBestEv, rr.ag[s], to_fx(rr.bev[s]));
-          if (packed) {  // 8-bit per-agent fields in registers, flushed once per block
-            const uint64_t bit = 1ull << (8 * rr.ag[s]);
-            n_logs_packed += bit;
-            if (won) n_won_packed += bit;
-          } else {
-            add_raw(kSlotCounts, rr.ag[s], won ? 0x100000001ull : 1ull);
-          }
-          if constexpr (GENERAL) {  // src/Agent.py:96-118 terms that vanish for Oracle agents
-            add_nz(kSlotAlloc, rr.ag[s], to_fx(rr.bev[s] - tv));
-            add_nz(kSlotEst, rr.ag[s], to_fx(rr.est[s] * rr.val[s] - tv));
-            const double dd = rr.ctr[s] - rr.est[s];
-            add_nz(kSlotSqerr, rr.ag[s], to_fx(dd * dd));
-            if (won) add_raw(kSlotBias, rr.ag[s], to_fx(rr.est[s] / rr.ctr[s]));
-          }
-        }
+        for (int s = 0; s < P; ++s)
+          count_slot(rr.ag[s], charged && s == rr.w, charged ? rr.price : 0.0, rr.price, rr.second, rr.bid[s],
+                     rr.ctr[s], rr.val[s], rr.est[s], rr.bev[s], rr.oc);
       }
     }
   }
@@ -997,6 +1072,7 @@ typedef void (*SimKernel)(SimParams);
 // in parallel): the k_simulate instantiation for (D, screened search, auctions per lane).
 template <int P>
 SimKernel pick_kernel_for(int D, bool prune, int W, bool general, int bt);
+template <> SimKernel pick_kernel_for<0>(int, bool, int, bool, int);
 template <> SimKernel pick_kernel_for<1>(int, bool, int, bool, int);
 template <> SimKernel pick_kernel_for<2>(int, bool, int, bool, int);
 template <> SimKernel pick_kernel_for<3>(int, bool, int, bool, int);

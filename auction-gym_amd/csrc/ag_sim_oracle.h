@@ -429,6 +429,7 @@ typedef void (*OraKernel)(OraParams);
 // Defined per P in ag_sim_p.hip: k_oracle<P, D, gen> for D in [2, 8].
 template <int P>
 OraKernel pick_oracle_for(int D, bool gen);
+template <> OraKernel pick_oracle_for<0>(int, bool);
 template <> OraKernel pick_oracle_for<1>(int, bool);
 template <> OraKernel pick_oracle_for<2>(int, bool);
 template <> OraKernel pick_oracle_for<3>(int, bool);

@@ -30,6 +30,18 @@ SimKernel pick_d(int D) {
 // (2 when B is even: 16-B accesses); otherwise the exact scan, one auction per lane.
 // general: populations beyond OracleAllocator + TruthfulBidder (one auction per lane), in
 // 256-lane workgroups or, screened, 1024-lane ones (bt; large populations' LDS images).
+#if AG_P == 0
+// P = 0: the runtime-P kernel (more than kMaxP participants), one auction per lane.
+template <>
+SimKernel pick_kernel_for<0>(int D, bool prune, int W, bool general, int bt) {
+  if (W != 1 || bt != kThreads || D > 8) return nullptr;
+  if (general) return prune ? pick_d<0, true, 1, true>(D) : pick_d<0, false, 1, true>(D);
+  return prune ? pick_d<0, true, 1, false>(D) : pick_d<0, false, 1, false>(D);
+}
+
+template <>
+OraKernel pick_oracle_for<0>(int, bool) { return nullptr; }
+#else
 template <>
 SimKernel pick_kernel_for<AG_P>(int D, bool prune, int W, bool general, int bt) {
   constexpr int P = AG_P;
@@ -65,5 +77,6 @@ OraKernel pick_oracle_for<AG_P>(int D, bool gen) {
     default: return nullptr;
   }
 }
+#endif
 
 }  // namespace ag

@@ -581,6 +581,56 @@ def test_mixed_population_full_size(gpu, oracle):
     eng.close()
 
 
+@pytest.mark.parametrize("P,mech,mixed", [(9, 1, False), (16, 0, True), (40, 1, True), (12, 0, False)])
+def test_wide_participants_match_oracle(gpu, oracle, P, mech, mixed):
+    """More than 8 participants per round (src/Auction.py:42 has no bound): the runtime-P
+    simulate kernel, every output and the exact counters equal to the oracle (Oracle-only
+    and mixed populations, both mechanisms, P up to N)."""
+    import torch
+    from auctiongym_amd.engine import AuctionEngine
+    N, K, E, OE = 40, 12, 5, 4
+    B = 1 << 16 if P < 32 else 1 << 14
+    g = np.random.default_rng(100 + P)
+    items = np.concatenate([g.normal(0, 1, (N, K, E)), -3.0 - g.random((N, K, 1))], axis=2)
+    values = g.lognormal(0.1, 0.2, (N, K))
+    ak = np.array([i % 2 for i in range(N)] if mixed else [0] * N, np.int32)
+    bk = np.array([(i // 2) % 5 for i in range(N)] if mixed else [0] * N, np.int32)
+    pg = 0.5 + 0.5 * g.random(N)
+    gs = 0.01 + 0.05 * g.random(N)
+    m = g.normal(0, 1, (N, K, OE + 1)).astype(np.float32)
+    q = (1.0 + 3.0 * g.random((N, K, OE + 1))).astype(np.float32)
+    eng = AuctionEngine(N, P, K, E, OE, mech, 1.0)
+    eng.set_agent_params(ak, bk, pg, gs)
+    eng.load_catalog(items, values)
+    if mixed:
+        eng.load_lrts(m, q, thompson_sampling=True)
+    inp = eng.alloc_inputs(B)
+    eng.generate(7, 0, inp)
+    if mixed:
+        eng.generate_noise(7, 0, inp)
+    out = eng.alloc_outputs(B, ("winner", "price", "second_price", "outcome", "item", "bid", "est_ctr",
+                                "true_ctr", "best_ev", "gamma", "propensity"))
+    cnt = eng.new_counters()
+    eng.simulate(inp, out, cnt)
+    torch.cuda.synchronize()
+    ctx = np.ascontiguousarray(inp["ctx"].cpu().numpy().T)
+    part = np.ascontiguousarray(inp["part"].cpu().numpy().T)
+    assert all(len(set(r)) == P for r in part[:100])  # distinct participants per round
+    u = inp["u"].cpu().numpy()
+    kw = {}
+    if mixed:
+        kw = dict(OE=OE, ts_m=m, ts_noise=eng.untile_ts_noise(inp["ts_noise"], B).reshape(B, P, K, OE + 1),
+                  gamma_raw=np.ascontiguousarray(inp["gamma_raw"].cpu().numpy().T))
+    orc = oracle.simulate_pop(mech, items, values, ctx, part, u, ak, bk, pg, gs, nthreads=16, **kw)
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    for k in ("item", "bid", "est_ctr", "true_ctr", "best_ev", "gamma", "propensity"):
+        assert np.array_equal(np.ascontiguousarray(got[k].T), orc[k], equal_nan=True), k
+    for k in ("winner", "price", "second_price", "outcome"):
+        assert np.array_equal(got[k], orc[k], equal_nan=True), k
+    assert np.array_equal(cnt.cpu().numpy(), orc["counters_fx"])
+    eng.close()
+
+
 @pytest.mark.parametrize("case", ["ties", "large_logits", "tiny_values"])
 def test_thompson_screen_adversarial(gpu, oracle, case):
     """The screened Thompson item choice (hardware exp2 / rcp estimates, exact scores of the
