@@ -33,10 +33,8 @@ class Agent:
         self.item_values = item_values
         self.allocator = allocator
         self.bidder = bidder
-        if memory:
-            raise NotImplementedError("Agent(memory>0): log memory across iterations is not "
-                                      "implemented on the GPU path yet")
-        self.memory = memory
+        self.memory = int(memory)
+        self._kept = None  # Agent(memory=M): columns of the M records kept by clear_logs
         self._auction = None
         self._index = None
         self._fx = [0] * _lib.NUM_COUNTERS
@@ -71,7 +69,8 @@ class Agent:
         rounds (from the device SoA outputs), then any per-call Agent.bid records."""
         self._sync()
         recs = [] if self._auction is None else self._auction._materialise_logs(self._index, self._log_start)
-        return recs + self._call_logs
+        kept = records_from_columns(self._kept) if self._kept is not None else []
+        return kept + recs + self._call_logs
 
     # the per-call surface (src/Agent.py:29-68): one request through the GPU plugins
     def select_item(self, context):
@@ -142,13 +141,26 @@ class Agent:
             self._fx[i] = 0
 
     def clear_logs(self):
+        """src/Agent.py:124-129: the logs are emptied, or with memory = M the last M records
+        are kept -- they stay in this agent's metrics (their exact counter terms, recomputed
+        on the host from the kept columns) and in the records its next update trains on (the
+        device record stores are rebuilt from them, Auction._cleared_logs)."""
         self._sync()
-        for i in _LOGS:
-            self._fx[i] = 0
+        if self.memory and self._auction is not None:
+            cols = self._auction._agent_columns(self._index, self._log_start)
+            if self._kept is not None:
+                cols = concat_columns(self._kept, cols)
+            self._kept = take_last(cols, self.memory)
+            terms = log_counter_terms(self._kept, self._auction._charged, self._auction._first_price)
+            for i in _LOGS:
+                self._fx[i] = terms.get(i, 0)
+        else:
+            for i in _LOGS:
+                self._fx[i] = 0
         if self._auction is not None:
             self._log_start = self._auction._log_rounds()
             self._auction._cleared_logs(self._index)
-        self._call_logs = self._call_logs[-self.memory:] if self.memory else []
+        self._call_logs = []
         self.bidder.clear_logs(memory=self.memory)
 
     def __repr__(self):
@@ -180,6 +192,108 @@ def _records(part, out, ctx, agent, first_round, values, obs=None):
     return recs
 
 
+# ---- Agent(memory=M): the kept records as columns ------------------------------------
+COLUMNS = ("context", "item", "value", "bid", "best_ev", "true_ctr", "est_ctr", "price", "second_price",
+           "outcome", "won", "gamma", "propensity", "order")
+
+
+def agent_columns(batches, agent, start_round, values, P, log_base, obs=None):
+    """Columns of `agent`'s records from round start_round on (log order: round, then slot):
+    the ImpressionOpportunity fields plus what the learners' record stores hold (gamma,
+    propensity; order = global round index * P + slot, ag_shading_samples.order)."""
+    parts = {k: [] for k in COLUMNS}
+    base = 0
+    for part, out, ctx in batches:
+        B = part.shape[1]
+        if base + B > start_round:
+            lo = max(0, start_round - base)
+            p = part[:, lo:].cpu().numpy()
+            r, s = np.nonzero(p.T == agent)  # row-major over [round][slot]: log order
+            if len(r):
+                o = {k: v.cpu().numpy() for k, v in out.items()}
+                rr = r + lo
+                charged = P >= 2
+                won = (o["winner"][rr] == s) if charged else np.zeros(len(r), bool)
+                c = ctx.cpu().numpy()[:, rr].T
+                c = c if obs is None else c[:, :obs]
+                item = o["item"][s, rr]
+                parts["context"].append(np.concatenate([c, np.ones((len(r), 1))], axis=1))
+                parts["item"].append(item.astype(np.int64))
+                parts["value"].append(np.asarray(values[agent], np.float64)[item])
+                parts["bid"].append(o["bid"][s, rr])
+                parts["best_ev"].append(o["best_ev"][s, rr])
+                parts["true_ctr"].append(o["true_ctr"][s, rr])
+                parts["est_ctr"].append(o["est_ctr"][s, rr])
+                parts["price"].append(o["price"][rr] if charged else np.zeros(len(r)))
+                parts["second_price"].append(np.where(won, o["second_price"][rr], 0.0) if charged
+                                             else np.zeros(len(r)))
+                parts["outcome"].append(np.where(won, o["outcome"][rr] != 0, False))
+                parts["won"].append(won)
+                nan = np.full(len(r), np.nan)
+                parts["gamma"].append(o["gamma"][s, rr] if "gamma" in o else nan)
+                parts["propensity"].append(o["propensity"][s, rr] if "propensity" in o else nan)
+                parts["order"].append(((log_base + base + rr).astype(np.int64)) * P + s)
+        base += B
+    return {k: (np.concatenate(v) if v else None) for k, v in parts.items()}
+
+
+def _ncols(cols):
+    return 0 if cols is None or cols["item"] is None else len(cols["item"])
+
+
+def concat_columns(a, b):
+    if _ncols(a) == 0:
+        return b
+    if _ncols(b) == 0:
+        return a
+    return {k: np.concatenate([a[k], b[k]]) for k in COLUMNS}
+
+
+def take_last(cols, m):
+    n = _ncols(cols)
+    if n == 0:
+        return None
+    return {k: v[max(0, n - m):] for k, v in cols.items()}
+
+
+def records_from_columns(cols):
+    n = _ncols(cols)
+    return [ImpressionOpportunity(
+        context=cols["context"][j].copy(), item=int(cols["item"][j]), value=float(cols["value"][j]),
+        bid=float(cols["bid"][j]), best_expected_value=float(cols["best_ev"][j]),
+        true_CTR=float(cols["true_ctr"][j]), estimated_CTR=float(cols["est_ctr"][j]),
+        price=float(cols["price"][j]), second_price=float(cols["second_price"][j]),
+        outcome=bool(cols["outcome"][j]), won=bool(cols["won"][j])) for j in range(n)]
+
+
+def _fx(x):
+    """The kernels' per-record rounding (ag_sim.h to_fx): x * 2^36 to nearest-even as an
+    integer, terms with |x| >= 2^26 (or non-finite) dropped."""
+    x = np.asarray(x, np.float64)
+    ok = np.abs(x) < 2.0 ** 26
+    r = np.rint(np.where(ok, x, 0.0) * 2.0 ** 36).astype(np.int64)
+    return sum(int(v) for v in r)
+
+
+def log_counter_terms(cols, charged, first_price):
+    """Exact fixed-point sums of the log counters (src/Agent.py:96-118 terms, as the simulate
+    kernels add them per record) over the kept records."""
+    n = _ncols(cols)
+    if n == 0:
+        return {}
+    won = cols["won"].astype(bool)
+    val, bid, tru, est, bev = (cols[k] for k in ("value", "bid", "true_ctr", "est_ctr", "best_ev"))
+    lp = cols["price"] if charged else np.zeros(n)
+    tv = tru * val
+    t = {C["allocation_regret"]: _fx(bev - tv), C["estimation_regret"]: _fx(est * val - tv),
+         C["underbid_regret"]: _fx(((lp - bid) * (lp < tv).astype(np.float64))[~won]),
+         C["ctr_sqerr"]: _fx((tru - est) * (tru - est)), C["best_ev_sum"]: _fx(bev),
+         C["ctr_bias_sum"]: _fx((est / np.where(won, tru, 1.0))[won]),
+         C["n_logs"]: n << _lib.FX_FRAC_BITS, C["n_won"]: int(won.sum()) << _lib.FX_FRAC_BITS,
+         C["overbid_regret"]: _fx((lp - cols["second_price"])[won]) if first_price else 0}
+    return t
+
+
 def materialise(batches, agent, start_round, values, obs=None):
     recs = []
     base = 0
@@ -198,4 +312,4 @@ def materialise(batches, agent, start_round, values, obs=None):
     return recs
 
 
-__all__ = ["Agent", "fx_to_float", "materialise"]
+__all__ = ["Agent", "fx_to_float", "materialise", "agent_columns"]

@@ -93,6 +93,8 @@ class Auction:
             self._load_learners()
         for i, a in enumerate(agents):
             a._attach(self, i)
+        self._charged = num_participants_per_round >= 2  # P == 1: nobody charged (src/Auction.py:68)
+        self._first_price = allocation.code == _lib.FIRST_PRICE
         self._revenue_fx = 0
         self._pending = []
         self._log_batches = []
@@ -397,8 +399,61 @@ class Auction:
             for st in self._stores.values():
                 st["count"].zero_()
             self._bounds = {"lrts": 0, "shading": 0}
+            self._restore_kept()
             self._trained = False
             self._claimed, self._cleared = set(), set()
+
+    def _restore_kept(self):
+        """Agent(memory=M): the records the learners kept (src/Agent.py:128) go back into the
+        emptied device stores, so the next update trains on them and the new rounds' records
+        -- as the reference's update reads the kept logs (src/Agent.py:81-94). LR-TS won
+        samples as ag_lrts_collect writes them; shading records with their log order."""
+        eng, d = self._engine, self._engine.device
+        lr, sh = [], []
+        for i, a in enumerate(self.agents):
+            cols = a._kept if self._learner[i] else None
+            if cols is None:
+                continue
+            if self._lrts[i]:
+                w = cols["won"].astype(bool)
+                if w.any():
+                    lr.append((i, {k: v[w] for k, v in cols.items()}))
+            if self._shading_rec[i]:
+                sh.append((i, cols))
+        if lr:
+            key = np.concatenate([(np.int64(i) << 16) | (c["item"] << 1) | c["outcome"].astype(np.int64)
+                                  for i, c in lr]).astype(np.uint32).view(np.int32)
+            x = np.concatenate([c["context"] for _, c in lr]).astype(np.float32).T
+            n = len(key)
+            st = self._grow("lrts", n, eng.new_lrts_samples)
+            st["key"][:n] = torch.from_numpy(key).to(d)
+            st["x"][:, :n] = torch.from_numpy(np.ascontiguousarray(x)).to(d)
+            st["count"][0] = n
+            self._bounds["lrts"] = n
+        if sh:
+            cols = {k: np.concatenate([c[k] for _, c in sh]) for k in sh[0][1]}
+            n = len(cols["item"])
+            won = cols["won"].astype(bool)
+            util = np.where(won, cols["value"] * cols["outcome"].astype(np.float64) - cols["price"], 0.0)
+            learning = bool(self._learning.any())
+            st = self._grow("shading", n, lambda cap: eng.new_shading_samples(cap, learning=learning))
+            fields = {"agent": np.concatenate([np.full(len(c["item"]), i, np.int32) for i, c in sh]),
+                      "gamma": cols["gamma"], "utility": util, "ctr": cols["est_ctr"], "value": cols["value"],
+                      "propensity": cols["propensity"], "won": won.astype(np.uint8), "order": cols["order"]}
+            for k, v in fields.items():
+                if k in st:
+                    st[k][:n] = torch.from_numpy(np.ascontiguousarray(v)).to(device=d, dtype=st[k].dtype)
+            st["count"][0] = n
+            self._bounds["shading"] = n
+
+    def _agent_columns(self, index, start_round):
+        """Agent(memory=M): columns of agent `index`'s records since start_round (host)."""
+        self._flush()
+        if not self.keep_logs:
+            raise NotImplementedError("Agent(memory>0) needs the auction's logs (keep_logs=True)")
+        oe = None if self.agents[index].allocator.kind == _lib.ALLOCATOR_ORACLE else self.obs_embedding_size
+        return _agent_mod.agent_columns(self._log_batches, index, start_round - self._log_base, self._values,
+                                        self.num_participants_per_round, self._log_base, obs=oe)
 
     # ------------------------------------------------------------------ logs
     def _log_rounds(self):

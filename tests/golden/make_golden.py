@@ -805,6 +805,64 @@ def empirical_update_kat(out_name="empirical_update_kat", iters=3):
     np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
 
 
+MEMORY_CASES = {
+    # name: (population, memory, rounds, iterations, allocation, seed)
+    "empirical": ("empirical", 300, 1000, 4, "FirstPrice", 31),
+    "lrts": ("lrts", 150, 1000, 3, "SecondPrice", 32),
+}
+
+
+def memory_driver_kat(out_name="memory_driver_kat"):
+    """Agent(memory=M) (src/Agent.py:124-129; 'memory' in an agent config, src/main.py:87)
+    through the reference's own driver loop (src/main.py:113-155): per iteration the revenue,
+    the utilities and, after every agent's update (before clear_logs), the metrics main.py
+    records over its logs -- which carry the last M records of the previous iteration -- the
+    log count and the learner's new state (prev_gamma / LR-TS m)."""
+    import torch
+    import main as M
+    out = {}
+    for name, (pop, mem, rounds, iters, alloc, seed) in MEMORY_CASES.items():
+        if pop == "empirical":
+            cfg = oracle_truthful_cfg(6, 12, 2, alloc, seed=seed)
+            cfg["agents"][0]["bidder"] = {"type": "EmpiricalShadedBidder",
+                                          "kwargs": {"gamma_sigma": 0.05, "init_gamma": 0.9}}
+        else:
+            cfg = load_cfg("SP_Truthful_TS.json", random_seed=seed, allocation=alloc)
+        cfg["agents"][0]["memory"] = mem
+        cfg["rounds_per_iter"], cfg["num_iter"], cfg["num_runs"] = rounds, iters, 1
+        out[f"{name}_cfg"] = np.array(json.dumps(cfg))
+        path = write_cfg(cfg)
+        (rng, config, agent_configs, a2i, a2v, _, max_slots, E, var, OE) = M.parse_config(path)
+        os.unlink(path)
+        torch.manual_seed(0)
+        agents = M.instantiate_agents(rng, agent_configs, a2v, a2i)
+        auction, _, _, _ = M.instantiate_auction(rng, config, a2i, a2v, agents, max_slots, E, var, OE)
+        for it in range(iters):
+            for _ in range(rounds):
+                auction.simulate_opportunity()
+            k = f"{name}_it{it}"
+            out[k + "_revenue"] = np.array(auction.revenue)
+            out[k + "_net"] = np.array([a.net_utility for a in agents])
+            out[k + "_gross"] = np.array([a.gross_utility for a in agents])
+            met = []
+            for i, a in enumerate(agents):
+                out[k + f"_a{i}_nlogs"] = np.array(len(a.logs))
+                a.update(iteration=it)
+                met.append([a.get_allocation_regret(), a.get_estimation_regret(), a.get_overbid_regret(),
+                            a.get_underbid_regret(), a.get_CTR_RMSE(), a.get_CTR_bias(),
+                            np.mean([o.best_expected_value for o in a.logs])])
+                if pop == "empirical":
+                    out[k + f"_a{i}_pg"] = np.array(float(a.bidder.prev_gamma))
+                else:
+                    out[k + f"_a{i}_m"] = a.allocator.response_model.m.detach().numpy().copy()
+                a.clear_utility()
+                a.clear_logs()
+            out[k + "_metrics"] = np.array(met, np.float64)
+            auction.clear_revenue()
+            print("memory", name, it, float(out[k + "_revenue"]), flush=True)
+    np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
+
+
 CSV_CASES = {
     # name: config overrides on oracle_truthful_cfg(...) (both populations run end to end on
     # the GPU path, so main.py's CSV files can be compared cell by cell)
@@ -851,9 +909,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also run SP_Oracle as shipped (3x20x10k rounds, ~1 min)")
     ap.add_argument("--which", choices=["dm", "ips", "dr", "dmo", "search"], help="with --only learners/drivers: one config")
-    ap.add_argument("--only", choices=["empirical", "csv", "dr", "learners", "drivers"], help="regenerate one fixture family only")
+    ap.add_argument("--only", choices=["empirical", "csv", "dr", "learners", "drivers", "memory"],
+                    help="regenerate one fixture family only")
     args = ap.parse_args()
     install_shims()
+    if args.only == "memory":
+        memory_driver_kat()
+        return
     if args.only == "empirical":
         empirical_update_kat()
         return
