@@ -345,7 +345,11 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
     eng.generate_noise(0, lo, inp)
     out = eng.alloc_outputs(B)
     cnt = eng.new_counters()
-    res = {"workload": what, "auctions_per_gpu_per_step": B}
+    res = {"workload": what, "auctions_per_gpu_per_step": B,
+           "parity": "simulate: bit-exact vs the oracle; learner updates: bit-exact vs the oracle, which tracks "
+                     "the reference's float32 torch fits -- after the first update their stopping epochs are "
+                     "chaotic, so later iterations match the reference within 7e-6 (FP_DM_TS) .. 2.6e-3 "
+                     "(FP_DR_TS) of revenue, not bit for bit (DESIGN.md section 5)"}
     # iteration 0 (uninitialised learners) and the update of every learner
     eng.simulate(inp, out, cnt)
     torch.cuda.synchronize()
