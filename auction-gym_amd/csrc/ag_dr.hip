@@ -230,25 +230,74 @@ struct Coop {
   int64_t *part;
   unsigned *bar;  // the agent's barrier lines (bar_lines)
   int ph;         // exchanges so far (identical in every workgroup of the agent)
+  int64_t *acc;   // exact_totals' accumulator rows [bar_lines][32] (row 0: the totals), zero
+                  // between exchanges
 };
 
-// exact totals of NV fixed-point sums over the agent's records (S.tot: hi, lo pairs)
+// exact totals of NV fixed-point sums over the agent's records (S.tot: hi, lo pairs), summed
+// up the agent barrier's combining tree with integer atomics: each workgroup adds its 2 NV
+// words to its level-0 node's accumulator row and arrives; the last arriver at a node moves
+// the node's row into its parent's (zeroing it) and arrives one level up; the root's last
+// arriver publishes the totals in row 0 and releases everyone, who read that one row.
+// Integer additions: the totals are exact whatever the order (round 1 had every workgroup
+// read every other workgroup's partials after the barrier: nblk lines from other XCDs per
+// workgroup per epoch).
 template <int NV>
 __device__ __forceinline__ void exact_totals(const int64_t (&acc)[NV], TrainLds &S, Coop &C) {
   block_sums<NV>(acc, S.w, S.tot);
   if (C.nblk > 1) {
-    int64_t *pp = C.part + (size_t)(C.ph & 1) * C.nblk * 32;
-    if (threadIdx.x < 2 * NV) pp[C.rank * 32 + threadIdx.x] = S.tot[threadIdx.x];
-    agent_barrier(C.bar, C.rank, C.nblk);
-    // wave w adds words j = w, w + 4, ...: lane l the workgroups l, l + 64, ..., then a
-    // butterfly (integer sums: any order gives the same totals)
-    const int lane = threadIdx.x & 63;
-    for (int j = threadIdx.x >> 6; j < 2 * NV; j += kDrThreads / 64) {
-      int64_t t = 0;
-      for (int b = lane; b < C.nblk; b += 64) t += pp[b * 32 + j];
-      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-      if (lane == 0) S.tot[j] = t;
+    constexpr int W = 2 * NV;
+    constexpr int F = agcoop::kBarFanIn;
+    int64_t *row0 = C.acc;
+    if (threadIdx.x < W)
+      __hip_atomic_fetch_add(row0 + (size_t)(1 + C.rank / F) * 32 + threadIdx.x, S.tot[threadIdx.x],
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned *gen = C.bar;
+      const unsigned g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int idx = C.rank, members_prev = C.nblk, base = 1;
+      bool last = true;
+      for (;;) {
+        const int nodes = (members_prev + F - 1) / F, q = idx / F;
+        const int members = members_prev - q * F < F ? members_prev - q * F : F;
+        unsigned *cnt = C.bar + (size_t)(base + q) * kBarLineWords;
+        if (__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) != (unsigned)members - 1) {
+          last = false;
+          break;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int64_t *node = row0 + (size_t)(base + q) * 32;
+        int64_t v[W];
+#pragma unroll
+        for (int j = 0; j < W; ++j) v[j] = __hip_atomic_load(node + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int j = 0; j < W; ++j) __hip_atomic_store(node + j, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (nodes == 1) {  // the root: publish
+#pragma unroll
+          for (int j = 0; j < W; ++j) __hip_atomic_store(row0 + j, v[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        const int pbase = base + nodes;
+        int64_t *parent = row0 + (size_t)(pbase + q / F) * 32;
+#pragma unroll
+        for (int j = 0; j < W; ++j)
+          __hip_atomic_fetch_add(parent + j, v[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        base = pbase;
+        idx = q;
+        members_prev = nodes;
+      }
+      if (last) {
+        __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g)
+          __builtin_amdgcn_s_sleep(AG_BAR_SLEEP);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
     }
+    __syncthreads();
+    if (threadIdx.x < W) S.tot[threadIdx.x] = __hip_atomic_load(row0 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     ++C.ph;
   }
@@ -725,7 +774,9 @@ __global__ __launch_bounds__(kDrThreads, PH == 0 ? 4 : 1) void k_bidder_train(
   const int64_t c0 = (int64_t)rank * per < n ? (int64_t)rank * per : n;
   const Chunk K{c0, (c0 + per < n ? c0 + per : n) - c0, n};
   // the agent's exchange region [2][nblk][32] (its workgroups have consecutive block indices)
-  Coop C{rank, nblk, partials + (size_t)(blockIdx.x - rank) * 2 * 32, barriers + (size_t)bar_off[a] * kBarLineWords, 0};
+  // the agent's exchange region: [2][nblk][32] parity buffers, then [nblk][32] accumulator rows
+  int64_t *preg = partials + (size_t)(blockIdx.x - rank) * 3 * 32;
+  Coop C{rank, nblk, preg, barriers + (size_t)bar_off[a] * kBarLineWords, 0, preg + (size_t)2 * nblk * 32};
   // stage the chunk's first `cap` records in LDS (the fields this phase's fits read)
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   float *lf = reinterpret_cast<float *>(s_dyn);
@@ -1115,7 +1166,7 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agen
   // partials [G][2][32] i64; barrier lines [lines][32] u32; blk_agent [G], blk_rank [G],
   // agent_nblk [N], bar_off [N] i32; win-rate models [N][4] f32 (phase 0 -> phase 1)
   const size_t gmax = (size_t)std::max(P0.G, P1.G), lmax = (size_t)std::max(P0.lines, P1.lines);
-  const size_t need_coop = sizeof(int64_t) * 64 * gmax + sizeof(unsigned) * kBarLineWords * lmax +
+  const size_t need_coop = sizeof(int64_t) * 96 * gmax + sizeof(unsigned) * kBarLineWords * lmax +
                            sizeof(int32_t) * (2 * gmax + 2 * (size_t)N) + sizeof(float) * 4 * N + 64;
   if (need_coop > w.coop_bytes) {
     (void)hipFree(w.coop);
@@ -1125,7 +1176,7 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agen
     w.coop_bytes = need_coop;
   }
   int64_t *d_part = (int64_t *)w.coop;
-  unsigned *d_bar = (unsigned *)(d_part + 64 * gmax);
+  unsigned *d_bar = (unsigned *)(d_part + 96 * gmax);
   int32_t *d_bagent = (int32_t *)(d_bar + kBarLineWords * lmax);
   int32_t *d_brank = d_bagent + gmax;
   int32_t *d_nblk = d_brank + gmax;
@@ -1138,6 +1189,7 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agen
     AG_HIP(hipMemcpyAsync(d_nblk, P.nblk.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
     AG_HIP(hipMemcpyAsync(d_baroff, P.bar_off.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
     if (P.lines) AG_HIP(hipMemsetAsync(d_bar, 0, sizeof(unsigned) * kBarLineWords * P.lines, st));
+    if (P.multi) AG_HIP(hipMemsetAsync(d_part, 0, sizeof(int64_t) * 96 * (size_t)P.G, st));  // accumulators
     DrRecords R{b_ctr, b_val, b_gam, b_prop, b_util, b_won};
     const int32_t *cbk = c->d_bkind, *cmode = w.mode, *cinit = w.init, *cbo = d_baroff;
     const int64_t *coff = d_off, *cnoff = d_noff;
