@@ -69,4 +69,81 @@ __device__ __forceinline__ void agent_barrier(unsigned *bar, int rank, int nblk)
   __syncthreads();
 }
 
+// Exact int64 all-reduce of W words over the workgroups of one agent, summed up the same
+// combining tree with integer atomics (exact in any order), every workgroup taking part:
+//  - each workgroup adds its words (LDS vals [W]) to its level-0 node's accumulator row;
+//  - the last arriver at a node (decided by thread 0, broadcast through LDS) moves the node's
+//    row into its parent's with all its threads, zeroing the node row, and arrives one level
+//    up; the root's last arriver writes the totals to row 0 and bumps the generation;
+//  - everyone then reads row 0 into LDS tot [W].
+// acc: the agent's rows [bar_lines(nblk)][stride] int64 (stride >= W), zero on entry and --
+// row 0 aside -- zero again on return, so the next call needs no clearing. Instead of every
+// workgroup reading every other workgroup's partials (nblk lines from other XCDs each), a
+// workgroup reads one row. Call with every thread; nblk <= 1 copies vals to tot.
+__device__ __forceinline__ void agent_allreduce_i64(unsigned *bar, int64_t *acc, int stride, int rank, int nblk,
+                                                    const int64_t *vals, int W, int64_t *tot, int *s_flag) {
+  const int t = threadIdx.x, nt = blockDim.x;
+  __syncthreads();
+  if (nblk <= 1) {
+    for (int j = t; j < W; j += nt) tot[j] = vals[j];
+    __syncthreads();
+    return;
+  }
+  for (int j = t; j < W; j += nt)
+    __hip_atomic_fetch_add(acc + (size_t)(1 + rank / kBarFanIn) * stride + j, vals[j], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  unsigned *gen = bar;
+  unsigned g = 0;
+  if (t == 0) g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int idx = rank, members_prev = nblk, base = 1;
+  bool root = false;
+  for (;;) {
+    const int nodes = (members_prev + kBarFanIn - 1) / kBarFanIn, q = idx / kBarFanIn;
+    const int members = members_prev - q * kBarFanIn < kBarFanIn ? members_prev - q * kBarFanIn : kBarFanIn;
+    __syncthreads();  // this workgroup's additions to the node are issued before it arrives
+    if (t == 0) {
+      unsigned *cnt = bar + (size_t)(base + q) * kBarLineWords;
+      const bool last =
+          __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)members - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      *s_flag = last;
+    }
+    __syncthreads();
+    if (!*s_flag) break;
+    int64_t *node = acc + (size_t)(base + q) * stride;
+    int64_t *dst = nodes == 1 ? acc : acc + (size_t)(base + nodes + q / kBarFanIn) * stride;
+    for (int j = t; j < W; j += nt) {
+      const int64_t v = __hip_atomic_load(node + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(node + j, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (nodes == 1)
+        __hip_atomic_store(dst + j, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        __hip_atomic_fetch_add(dst + j, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (nodes == 1) {
+      root = true;
+      break;
+    }
+    base += nodes;
+    idx = q;
+    members_prev = nodes;
+  }
+  __syncthreads();  // the root's totals are stored before the generation moves
+  if (t == 0) {
+    if (root) {
+      __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g)
+        __builtin_amdgcn_s_sleep(AG_BAR_SLEEP);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+  }
+  __syncthreads();
+  for (int j = t; j < W; j += nt) tot[j] = __hip_atomic_load(acc + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+}
+
 }  // namespace agcoop

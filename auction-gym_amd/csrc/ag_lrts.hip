@@ -33,6 +33,7 @@ namespace {
 constexpr int kLrThreads = 256;        // 4 waves; one sample per lane per pass
 constexpr int kLrEpochs = AG_LRTS_MAX_EPOCHS;
 constexpr int kLrMaxKD = 64;           // K * (OE + 1) columns of the accumulator tile
+constexpr int kLrAccStride = 144;      // int64 per accumulator row: 2 (KD + 1) <= 130, 128-B multiple
 constexpr int kLrCache = 16;           // samples per lane kept in registers (1 workgroup / CU)
 constexpr int kAccStride = kLrThreads + 1;  // [column][lane] int64 tile, padded: the column
                                             // reduction (lanes = columns) is conflict-free
@@ -259,7 +260,8 @@ __global__ __launch_bounds__(kLrThreads) void k_lrts_train(
   const int64_t s0 = offsets[a], n = offsets[a + 1] - s0;
   const int KD = K * DO;
   const int PW = 2 * (KD + 1);  // int64 per partial record
-  int64_t *pbase = partials + agent_pbase[a];  // [2 parities][nblk][KD + 1][2]
+  // the agent's accumulator rows [bar_lines(nblk)][kLrAccStride] (agcoop::agent_allreduce_i64)
+  int64_t *accrows = partials + agent_pbase[a];
   unsigned *bar = barriers + (size_t)bar_off[a] * agcoop::kBarLineWords;
   // this workgroup's samples: [c0, c1) of the agent's n
   const int64_t per = (n + nblk - 1) / nblk;
@@ -273,7 +275,8 @@ __global__ __launch_bounds__(kLrThreads) void k_lrts_train(
   __shared__ float s_hist[kHistory];
   __shared__ float s_loss, s_negstep, s_bc2;
   __shared__ double s_lr, s_best;
-  __shared__ int s_bad, s_stop;
+  __shared__ int s_bad, s_stop, s_flag;
+  __shared__ int64_t s_part[2 * (kLrMaxKD + 1)], s_tot[2 * (kLrMaxKD + 1)];
 
   for (int i = tid; i < 256; i += kLrThreads) s_tab[i] = ag_exp_tab[i];
   float *m_g = gm + (size_t)a * KD, *q_g = gq + (size_t)a * KD, *pm_g = gpm + (size_t)a * KD;
@@ -318,17 +321,13 @@ __global__ __launch_bounds__(kLrThreads) void k_lrts_train(
       lsum += lr_epoch_sample<DO>(sm, s_m, acc, s_tab);
     }
     __syncthreads();
-    // ---- B: this workgroup's exact partials -> global (parity buffer), agent barrier
-    int64_t *pp = pbase + (size_t)(epoch & 1) * nblk * PW;
-    lr_block_partials(s_acc, KD, lsum >> 24, lsum & kLo24, s_hi, s_lo, pp + (size_t)rank * PW);
-    agcoop::agent_barrier(bar, rank, nblk);
+    // ---- B: this workgroup's exact partials, summed over the agent's workgroups up the
+    // barrier tree (exact integer atomics; every workgroup gets the same totals)
+    lr_block_partials(s_acc, KD, lsum >> 24, lsum & kLo24, s_hi, s_lo, s_part);
+    agcoop::agent_allreduce_i64(bar, accrows, kLrAccStride, rank, nblk, s_part, PW, s_tot, &s_flag);
     // ---- C: totals (identical in every workgroup), loss, Adam; scheduler on thread 0
     if (tid == 0) {
-      int64_t h = 0, l = 0;
-      for (int b = 0; b < nblk; ++b) {
-        h += pp[(size_t)b * PW + 2 * KD];
-        l += pp[(size_t)b * PW + 2 * KD + 1];
-      }
+      const int64_t h = s_tot[2 * KD], l = s_tot[2 * KD + 1];
       double prior = 0.0;
       for (int k = 0; k < K; ++k)
         for (int d = 0; d < DO - 1; ++d) {
@@ -342,11 +341,7 @@ __global__ __launch_bounds__(kLrThreads) void k_lrts_train(
     __syncthreads();
     if (tid < KD) {
       const int c = tid;
-      int64_t h = 0, l = 0;
-      for (int b = 0; b < nblk; ++b) {
-        h += pp[(size_t)b * PW + 2 * c];
-        l += pp[(size_t)b * PW + 2 * c + 1];
-      }
+      const int64_t h = s_tot[2 * c], l = s_tot[2 * c + 1];
       const double gp = (c % DO) < DO - 1 ? -(double)s_q[c] * ((double)s_pm[c] - (double)s_m[c]) : 0.0;
       const float g = (float)(fx_read(h, l, 1.0 / kGradScale) + gp);
       const float ea = s_ea[c] + 0.1f * (g - s_ea[c]);
@@ -392,17 +387,12 @@ __global__ __launch_bounds__(kLrThreads) void k_lrts_train(
     lr_laplace_sample<DO>(sm, s_m, acc, s_tab);
   }
   __syncthreads();
-  int64_t *pp = pbase + (size_t)(epoch & 1) * nblk * PW;
-  lr_block_partials(s_acc, KD, 0, 0, s_hi, s_lo, pp + (size_t)rank * PW);
-  agcoop::agent_barrier(bar, rank, nblk);
+  lr_block_partials(s_acc, KD, 0, 0, s_hi, s_lo, s_part);
+  agcoop::agent_allreduce_i64(bar, accrows, kLrAccStride, rank, nblk, s_part, PW, s_tot, &s_flag);
   if (rank == 0) {
     if (tid < KD) {
       const int c = tid;
-      int64_t h = 0, l = 0;
-      for (int b = 0; b < nblk; ++b) {
-        h += pp[(size_t)b * PW + 2 * c];
-        l += pp[(size_t)b * PW + 2 * c + 1];
-      }
+      const int64_t h = s_tot[2 * c], l = s_tot[2 * c + 1];
       q_g[c] = s_q[c] + (float)fx_read(h, l, 1.0 / kGradScale);
       m_g[c] = s_m[c];
       pm_g[c] = s_m[c];
@@ -591,7 +581,7 @@ int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *
     bar_off[a] = lines;
     lines += agcoop::bar_lines(nblk[a]);
     pbase[a] = pwords;
-    pwords += 2 * (int64_t)nblk[a] * 2 * (K * Do + 1);
+    pwords += (int64_t)agcoop::bar_lines(nblk[a]) * kLrAccStride;
     multi |= nblk[a] > 1;
     for (int r = 0; r < nblk[a]; ++r) {
       blk_agent.push_back(a);
@@ -635,6 +625,7 @@ int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *
     AG_HIP(hipMemcpyAsync(d_pbase, pbase.data(), sizeof(int64_t) * N, hipMemcpyHostToDevice, st));
     AG_HIP(hipMemcpyAsync(d_baroff, bar_off.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
     if (lines) AG_HIP(hipMemsetAsync(d_bar, 0, sizeof(unsigned) * agcoop::kBarLineWords * lines, st));
+    if (pwords) AG_HIP(hipMemsetAsync(w.partials, 0, sizeof(int64_t) * pwords, st));  // accumulator rows
     int Kv = K;
     const int32_t *cbagent = d_bagent, *cbrank = d_brank, *cnblk = d_nblk;
     const int64_t *cpbase = d_pbase, *coffsets = w.offsets;
