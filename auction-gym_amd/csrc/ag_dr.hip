@@ -212,6 +212,7 @@ struct TrainLds {
   AdamState adam;
   int stop;       // a NaN loss
   int exhausted;  // a noise-driven fit ran out of noise epochs before it stopped
+  int flag;       // agent_allreduce_i64's broadcast
 };
 
 __device__ __forceinline__ void adam_reset(TrainLds &S) {
@@ -246,59 +247,7 @@ template <int NV>
 __device__ __forceinline__ void exact_totals(const int64_t (&acc)[NV], TrainLds &S, Coop &C) {
   block_sums<NV>(acc, S.w, S.tot);
   if (C.nblk > 1) {
-    constexpr int W = 2 * NV;
-    constexpr int F = agcoop::kBarFanIn;
-    int64_t *row0 = C.acc;
-    if (threadIdx.x < W)
-      __hip_atomic_fetch_add(row0 + (size_t)(1 + C.rank / F) * 32 + threadIdx.x, S.tot[threadIdx.x],
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned *gen = C.bar;
-      const unsigned g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int idx = C.rank, members_prev = C.nblk, base = 1;
-      bool last = true;
-      for (;;) {
-        const int nodes = (members_prev + F - 1) / F, q = idx / F;
-        const int members = members_prev - q * F < F ? members_prev - q * F : F;
-        unsigned *cnt = C.bar + (size_t)(base + q) * kBarLineWords;
-        if (__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) != (unsigned)members - 1) {
-          last = false;
-          break;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int64_t *node = row0 + (size_t)(base + q) * 32;
-        int64_t v[W];
-#pragma unroll
-        for (int j = 0; j < W; ++j) v[j] = __hip_atomic_load(node + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int j = 0; j < W; ++j) __hip_atomic_store(node + j, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (nodes == 1) {  // the root: publish
-#pragma unroll
-          for (int j = 0; j < W; ++j) __hip_atomic_store(row0 + j, v[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        const int pbase = base + nodes;
-        int64_t *parent = row0 + (size_t)(pbase + q / F) * 32;
-#pragma unroll
-        for (int j = 0; j < W; ++j)
-          __hip_atomic_fetch_add(parent + j, v[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        base = pbase;
-        idx = q;
-        members_prev = nodes;
-      }
-      if (last) {
-        __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g)
-          __builtin_amdgcn_s_sleep(AG_BAR_SLEEP);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x < W) S.tot[threadIdx.x] = __hip_atomic_load(row0 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
+    agcoop::agent_allreduce_i64(C.bar, C.acc, 32, C.rank, C.nblk, S.tot, 2 * NV, S.tot, &S.flag);
     ++C.ph;
   }
 }
