@@ -388,21 +388,22 @@ __device__ int fit_winrate(const RecView &V, const Chunk &K, TrainLds &S, Coop &
     // one BCE row: its loss and gradient terms
     auto row = [&](double c, double v, double g, double y) {
       const double z = c * w0 + v * w1 + g * w2 + w3;
-      // -log(p) = softplus(-z) for a win, -log(1 - p) = softplus(z) otherwise. Branch-free
-      // main paths of exp(-z), exp(z) and log1p (the same bits), the rare inputs outside
-      // them patched with the full functions afterwards
-      double em = agexp::exp_main(-z, S.tab), ep = agexp::exp_main(z, S.tab);
-      const double u = y > 0.0 ? -z : z;
-      double eu = y > 0.0 ? em : ep;
+      // one exp per row (oracle/ag_oracle_dr.c fit_winrate): e = exp(-|z|), L = log1p(e);
+      // p = (z >= 0 ? 1 : e) / (1 + e); -log(p) = softplus(-z) for a win, -log(1 - p) =
+      // softplus(z) otherwise, softplus(u) = L for u <= 0, |z| + L for u > 0 (u past 20: u).
+      // Branch-free main paths of exp and log1p (the same bits), the rare inputs outside them
+      // patched with the full functions afterwards
+      const double a = __builtin_fabs(z);
+      double e = agexp::exp_main(-a, S.tab);
       bool lok;
-      double l = aglog1p::log1p_main(eu, lok);
-      if (__builtin_expect(!(agexp::exp_in_main(z) && (lok || u > 20.0)), 0)) {
-        em = agexp::exp(-z, S.tab);
-        eu = y > 0.0 ? em : agexp::exp(z, S.tab);
-        l = aglog1p::log1p(eu);
+      double Lz = aglog1p::log1p_main(e, lok);
+      if (__builtin_expect(!(agexp::exp_in_main(a) && lok), 0)) {
+        e = agexp::exp(-a, S.tab);
+        Lz = aglog1p::log1p(e);
       }
-      const double pw = 1.0 / (1.0 + em);
-      const double t = fmin(u > 20.0 ? u : l, 100.0);
+      const double pw = (z >= 0.0 ? 1.0 : e) / (1.0 + e);
+      const double u = y > 0.0 ? -z : z;
+      const double t = fmin(u > 20.0 ? u : (u > 0.0 ? a + Lz : Lz), 100.0);
       // |t| <= 100, |pw - y| <= 1, ctr in [0, 1]: these terms are far inside fxr's fast range
       acc[0] += fxr_fast(t);
       const double gz = pw - y;

@@ -267,10 +267,14 @@ static int32_t fit_winrate(int64_t n, const float *cf, const float *vf, const fl
       const double c = cf[i], v = vf[i], g = r < n ? gf[i] : 0.0;
       const double y = r < n ? (double)won[i] : 0.0;
       const double z = c * (double)wr[0] + v * (double)wr[1] + g * (double)wr[2] + (double)wr[3];
-      const double pw = 1.0 / (1.0 + exp(-z));
-      /* BCE with torch's clamp of the logs at -100: -log(p) = softplus(-z), -log(1-p) =
-       * softplus(z) (exp + the restated log1p: the same bits on the device) */
-      const double t = y > 0.0 ? fmin(softplus(-z), 100.0) : fmin(softplus(z), 100.0);
+      /* one exp per row: e = exp(-|z|), L = log1p(e) (the restated log1p: the same bits on
+       * the device); p = sigmoid(z) = (z >= 0 ? 1 : e) / (1 + e); BCE with torch's clamp of
+       * the logs at -100: -log(p) = softplus(-z), -log(1-p) = softplus(z), where softplus(u)
+       * = u past torch's threshold 20, L for u <= 0 and |z| + L for u > 0 */
+      const double a = fabs(z), e = exp(-a), Lz = fl_log1p(e);
+      const double pw = (z >= 0.0 ? 1.0 : e) / (1.0 + e);
+      const double u = y > 0.0 ? -z : z;
+      const double t = fmin(u > 20.0 ? u : (u > 0.0 ? a + Lz : Lz), 100.0);
       L += fxr(t);
       const double gz = pw - y;
       G[0] += fxr(gz * c);
