@@ -615,8 +615,9 @@ int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
       c->grid_per_cu = (int32_t)value;
       return AG_OK;
     case AG_OPT_SIM_BLOCK_THREADS:
-      if (value != 0 && value != 256 && value != 1024)
-        return ag_set_error(AG_ERR_INVALID, "ag_set_option: block threads must be 0, 256 or 1024");
+      if (value != 0 && value != kThreads && value != kLargeThreads)
+        return ag_set_error(AG_ERR_INVALID, "ag_set_option: block threads must be 0, %d or %d", kThreads,
+                            kLargeThreads);
       c->block_threads = (int32_t)value;
       return AG_OK;
     case AG_OPT_SIMULATE_KERNEL:
@@ -740,7 +741,7 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   // (N = 32: ~75 KB -> 2 workgroups = 2 waves per SIMD); 1024-lane workgroups share one
   // image among 16 waves. Same results (the counters are exact sums).
   int bt = c->block_threads;
-  if (bt == 0) bt = (c->general && prune && lds > 40 * 1024) ? 1024 : kThreads;
+  if (bt == 0) bt = (c->general && prune && lds > 40 * 1024) ? kLargeThreads : kThreads;
   SimKernel k = pick_kernel(s.num_participants, D, prune, W, c->general, bt);
   if (!k && bt != kThreads) {
     bt = kThreads;

@@ -33,6 +33,10 @@ namespace ag {
 #endif
 
 constexpr int kThreads = 256;              // 4 waves of 64 lanes
+#ifndef AG_LARGE_BT
+#define AG_LARGE_BT 1024
+#endif
+constexpr int kLargeThreads = AG_LARGE_BT;  // the general kernel's workgroups for large LDS images
 constexpr int kC = AG_NUM_COUNTERS;
 // Auctions one block may resolve per launch: 1024 per counter replica keeps every replica's
 // int64 sum exact (<= 1024 * P terms of magnitude < 2^50, to_fx).

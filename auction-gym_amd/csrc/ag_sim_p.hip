@@ -47,7 +47,7 @@ SimKernel pick_kernel_for<AG_P>(int D, bool prune, int W, bool general, int bt) 
   constexpr int P = AG_P;
   if (general) {
     if (D > 8) return nullptr;
-    if (bt == 1024) return prune ? pick_d<P, true, 1, true, 1024>(D) : nullptr;
+    if (bt == kLargeThreads) return prune ? pick_d<P, true, 1, true, kLargeThreads>(D) : nullptr;
     if (bt != kThreads) return nullptr;
     return prune ? pick_d<P, true, 1, true>(D) : pick_d<P, false, 1, true>(D);
   }
