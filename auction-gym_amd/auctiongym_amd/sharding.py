@@ -35,7 +35,12 @@ def allreduce_counters(limbs, group=None):
     if limbs.dtype != torch.int64:
         raise TypeError("counter limbs are int64")
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(limbs, op=dist.ReduceOp.SUM, group=group)
+        if limbs.is_cuda and dist.get_backend(group) == "gloo":  # gloo rehearsal: via host memory
+            h = limbs.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+            limbs.copy_(h)
+        else:
+            dist.all_reduce(limbs, op=dist.ReduceOp.SUM, group=group)
     return limbs
 
 

@@ -48,6 +48,17 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); the measured c
 #                        measured live (measured_copy_peak) and reported beside it
 
 
+def all_reduce_max(t):
+    """MAX over ranks in place (RCCL on the device; a gloo rehearsal goes through host memory)."""
+    if dist.get_backend() == "gloo" and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.MAX)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t
+
+
 def algorithmic_bytes_per_auction(E, P, first_price):
     reads = 8 * E + 4 * P + 8                       # ctx, part, u
     writes = 4 + 8 + 1 + P * (4 + 8 + 8 + 8 + 8)    # winner, price, outcome; per slot
@@ -154,7 +165,7 @@ def timed_steps(step, steps, warmup, world, stream):
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=stream.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        all_reduce_max(t)
         elapsed, kern_ms = float(t[0]), float(t[1])
     return elapsed, kern_ms
 
@@ -232,7 +243,7 @@ def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True):
         ms = (time.perf_counter() - t0) * 1e3
         if world > 1:
             t = torch.tensor([ms], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            all_reduce_max(t)
             ms = float(t[0])
         res["agent_update"] = {"ms": ms, "won_samples_rank0": int(st["count"][0]),
                                "epochs": [int(e) for e in ep],
@@ -371,7 +382,7 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
         ms = [(t1 - t0) * 1e3, (t2 - t1) * 1e3]
         if world > 1:
             t = torch.tensor(ms, dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            all_reduce_max(t)
             ms = [float(x) for x in t]
         learners = np.nonzero(bk >= 2)[0]
         res["agent_update"] = {
@@ -440,6 +451,10 @@ def main():
                     help="skip the configs[2..4] lines (FP_DM_TS, FP_DR_TS, mixed population)")
     ap.add_argument("--populations", default=",".join(POPULATIONS),
                     help="comma-separated subset of the configs[2..4] lines to run")
+    ap.add_argument("--rehearse-on-one-gpu", action="store_true",
+                    help="N > 1 ranks sharing the visible GPU(s) over gloo: exercises the multi-GPU code path "
+                         "(shards, counter all-reduce, agent-parallel updates) where only one GPU is at hand; "
+                         "its timings mean nothing")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -447,10 +462,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    if args.rehearse_on_one_gpu:
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.rehearse_on_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from auctiongym_amd import _lib
     from auctiongym_amd.engine import AuctionEngine
@@ -503,7 +523,7 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        all_reduce_max(t)
         elapsed, kern_ms = float(t[0]), float(t[1])
 
     total_auctions = B * world * args.steps
@@ -540,7 +560,7 @@ def main():
         gk = float(np.mean([a.elapsed_time(b) for a, b in ev]))
         if world > 1:
             t = torch.tensor([gel, gk], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            all_reduce_max(t)
             gel, gk = float(t[0]), float(t[1])
         wb = bpa - (8 * E + 4 * P + 8)  # the writes alone
         gen = {"workload": "the headline workload in generate mode: contexts, participants and uniforms "

@@ -76,3 +76,25 @@ def test_agent_parallel_updates_equal_single_process(gpu, tmp_path):
         got = np.load(out + f".2.{r}.npz")
         for k in ("m", "q", "pm", "state", "init", "lep", "ep", "stat"):
             assert np.array_equal(got[k], ref[k]), (r, k)
+
+
+def test_bench_multi_rank_rehearsal(gpu, tmp_path):
+    """bench.py's N > 1 path end to end -- shards, the exact counter all-reduce, the
+    agent-parallel learner updates of configs[1..4] -- with 2 ranks sharing the box's GPU over
+    gloo (`--rehearse-on-one-gpu`; the driver's multi-GPU runs use RCCL on one GPU per rank).
+    Every rank must finish and rank 0 print one JSON line for 2 GPUs."""
+    import json
+    import subprocess
+    import sys
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", str(1 << 20), "--ts-batch", str(1 << 16),
+           "--no-cpu-baseline", "--no-generate", "--populations", "configs_4", "--rehearse-on-one-gpu"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert d["configs_1"]["agent_update"]["epochs"] and d["configs_4"]["agent_update"]["bidder_epochs"]
