@@ -550,24 +550,46 @@ __device__ __forceinline__ void policy_bid(const float *p, double ctr, double va
   gamma = raw < 0.0f ? 0.0 : (raw > 1.0f ? 1.0 : (double)raw);
 }
 
+// torch's float32 exp on the CPU as torch.sigmoid's vectorised path computes it (SLEEF's
+// expf_u10; oracle/ag_oracle_dr.c torch_expf bit for bit): q = round(x / ln 2), the reduced
+// argument in two fused steps, a degree-5 fused Horner polynomial, times 2^q in two steps.
+__device__ __forceinline__ float torch_expf(float d) {
+  const float q = __builtin_rintf(d * 1.442695040888963407359924681001892137426645954152985934135449406931f);
+  float s = __builtin_fmaf(q, -0.693145751953125f, d);
+  s = __builtin_fmaf(q, -1.428606765330187045e-06f, s);
+  float u = 0.000198527617612853646278381f;
+  u = __builtin_fmaf(u, s, 0.00139304355252534151077271f);
+  u = __builtin_fmaf(u, s, 0.00833336077630519866943359f);
+  u = __builtin_fmaf(u, s, 0.0416664853692054748535156f);
+  u = __builtin_fmaf(u, s, 0.166666671633720397949219f);
+  u = __builtin_fmaf(u, s, 0.5f);
+  u = 1.0f + __builtin_fmaf(s * s, u, s);
+  const int e = (int)q, e1 = e >> 1;
+  u = u * __builtin_ldexpf(1.0f, e1) * __builtin_ldexpf(1.0f, e - e1);
+  if (d < -104.0f) u = 0.0f;
+  if (d > 100.0f) u = INFINITY;
+  return u;
+}
+
 // ValueLearningBidder 'search' bid (src/Bidder.py:180-196): the shading factor maximising
 // the win-rate model's predicted utility W(ctr, value, g) (ev - ev g), ev = value * ctr,
-// over the agent's 128 grid draws (dev [128] with stride B). W in float32 as the
-// reference's torch model: z = ((c w0 + v w1) + g w2) + b without FMAs, W = sigmoid(z)
-// via the glibc-identical double exp, rounded to float32 (torch's vectorised sigmoid may
-// differ by an ulp: the argmax flips only where two grid points' utilities are that close).
-// The first maximum in sorted-grid order = the smallest gamma among tied maxima, so the
-// grid may arrive unsorted. oracle/ag_oracle.c ora_search_gamma is this, bit for bit.
+// over the agent's 128 grid draws (dev [128] with stride B). W in float32 as torch runs the
+// reference's model on the CPU: Linear(3, 1) summed as its BLAS kernel does,
+// z = (fma(v, w1, c w0) + g w2) + b, then torch.sigmoid's vectorised 1 / (1 + exp(-z))
+// (torch_expf). The first maximum in sorted-grid order = the smallest gamma among tied
+// maxima, so the grid may arrive unsorted. oracle/ag_oracle_dr.c ora_search_gamma is this,
+// bit for bit; it picks the reference's gamma in all 24000 bids of search_bid_kat.npz.
 __device__ __forceinline__ double search_gamma(const float *wr, double ctr, double value, const double *grid,
                                                uint32_t stride, const uint64_t *tab) {
+  (void)tab;
   const float c = (float)ctr, v = (float)value;
-  const float cv = c * wr[0] + v * wr[1];
+  const float cv = __builtin_fmaf(v, wr[1], c * wr[0]);
   const double ev = value * ctr;
   double best_u = -INFINITY, best_g = 0.0;
   for (int j = 0; j < 128; ++j) {
     const double g = grid[(size_t)j * stride];
-    const float z = cv + (float)g * wr[2] + wr[3];
-    const float pw = (float)(1.0 / (1.0 + agexp::exp_fast(-(double)z, tab)));
+    const float z = (cv + (float)g * wr[2]) + wr[3];
+    const float pw = 1.0f / (1.0f + torch_expf(-z));
     const double ut = (double)pw * (ev - ev * g);
     if (ut > best_u || (ut == best_u && g < best_g)) {
       best_u = ut;

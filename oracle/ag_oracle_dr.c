@@ -451,15 +451,46 @@ void ora_fit_noise(uint64_t seed, uint32_t agent, int32_t epochs, int64_t n, flo
  * = value * ctr, the first maximum of the sorted grid = the smallest gamma among ties. torch
  * evaluates W with its own float32 kernels (an ulp apart at most): the argmax agrees except
  * where two grid points' utilities are that close. */
+/* torch's float32 exp on the CPU, as torch.sigmoid's vectorised path computes it (ATen's
+ * sigmoid kernel: (1 + exp(-x)).reciprocal() with Vectorized<float>::exp = SLEEF's expf_u10):
+ * round(x / ln 2) = q, x - q ln 2 in two fused steps, a degree-5 polynomial by fused Horner,
+ * times 2^q in two power-of-two steps; 0 below -104, inf above 100. Pinned against
+ * torch.sigmoid in tests/golden (every search-bid grid point of search_bid_kat.npz). */
+static float torch_expf(float d) {
+  const float q = rintf(d * 1.442695040888963407359924681001892137426645954152985934135449406931f);
+  float s = fmaf(q, -0.693145751953125f, d);
+  s = fmaf(q, -1.428606765330187045e-06f, s);
+  float u = 0.000198527617612853646278381f;
+  u = fmaf(u, s, 0.00139304355252534151077271f);
+  u = fmaf(u, s, 0.00833336077630519866943359f);
+  u = fmaf(u, s, 0.0416664853692054748535156f);
+  u = fmaf(u, s, 0.166666671633720397949219f);
+  u = fmaf(u, s, 0.5f);
+  u = 1.0f + fmaf(s * s, u, s);
+  const int e = (int)q, e1 = e >> 1;
+  u = u * ldexpf(1.0f, e1) * ldexpf(1.0f, e - e1);
+  if (d < -104.0f) u = 0.0f;
+  if (d > 100.0f) u = INFINITY;
+  return u;
+}
+
+float ora_torch_sigmoidf(float z) { return 1.0f / (1.0f + torch_expf(-z)); }
+
+/* ValueLearningBidder 'search' (src/Bidder.py:180-196): prob_win of the 128 grid points is
+ * PyTorchWinRateEstimator on float32 rows [ctr, value, gamma] as torch runs it on the CPU --
+ * Linear(3, 1) as the BLAS kernel sums it, z = (fma(value, w1, ctr w0) + gamma w2) + b, then
+ * the vectorised sigmoid (torch_expf) -- and the utility prob_win (ev - ev gamma) in double;
+ * the first maximum in sorted-grid order (the smallest gamma among ties). Reproduces the
+ * reference's gamma in every one of the 24000 bids of search_bid_kat.npz. */
 double ora_search_gamma(const float *wr, double ctr, double value, const double *grid, int64_t stride) {
   const float c = (float)ctr, v = (float)value;
-  const float cv = c * wr[0] + v * wr[1];
+  const float cv = fmaf(v, wr[1], c * wr[0]);
   const double ev = value * ctr;
   double best_u = -INFINITY, best_g = 0.0;
   for (int j = 0; j < 128; ++j) {
     const double g = grid[(int64_t)j * stride];
-    const float z = cv + (float)g * wr[2] + wr[3];
-    const float pw = (float)(1.0 / (1.0 + exp(-(double)z)));
+    const float z = (cv + (float)g * wr[2]) + wr[3];
+    const float pw = ora_torch_sigmoidf(z);
     const double ut = (double)pw * (ev - ev * g);
     if (ut > best_u || (ut == best_u && g < best_g)) {
       best_u = ut;

@@ -104,6 +104,8 @@ def lib():
         L.ora_search_gamma.argtypes = [vp, d, d, vp, i64]
         L.ora_log1p_restated.restype = d
         L.ora_log1p_restated.argtypes = [d]
+        L.ora_torch_sigmoidf.restype = ctypes.c_float
+        L.ora_torch_sigmoidf.argtypes = [ctypes.c_float]
         L.ora_lrts_update.restype = i32
         L.ora_lrts_update.argtypes = [i64, i32, i32, vp, vp, vp, vp, vp, vp, vp]
         _lib = L
