@@ -135,6 +135,36 @@ AG_HD double exp_fast(double x, const uint64_t *tab) {
 #endif
 }
 
+// glibc 2.35's float expf (the algorithm of sysdeps/ieee754/flt-32/e_expf.c, restated):
+// x 32/ln2 = k + r (k rounded to nearest through the 1.5 2^52 shift, both steps fused as
+// the x86-64 FMA build does), 2^(k/32) from every 4th entry of the exp table above (the
+// same correctly rounded 2^(j/128)), 2^(r/32) by a degree-3 polynomial in double, one
+// rounding to float. What torch.sigmoid's scalar path calls (std::exp on a float); equal
+// to the host libm expf for every float (tests/test_exp_restatement.py, exhaustive).
+constexpr double kInvLn2F = 0x1.71547652b82fep0 * 32.0;
+constexpr double kF0 = 0x1.c6af84b912394p-5 / 32768.0;
+constexpr double kF1 = 0x1.ebfce50fac4f3p-3 / 1024.0;
+constexpr double kF2 = 0x1.62e42ff0c52d6p-1 / 32.0;
+AG_HD float expf_glibc(float x, const uint64_t *tab) {
+  // glibc branches out for |x| >= 88 or nan and otherwise falls through to the main path
+  // below; here the main path always runs and the out-of-range results are selected
+  // (branch-free, for unrolled divergent code)
+  const double xd = (double)x;
+  double kd = fma(kInvLn2F, xd, kShift);
+  const uint64_t ki = asu64(kd);
+  kd -= kShift;
+  const double r = fma(kInvLn2F, xd, -kd);
+  const double s = asf64(tab[8 * (ki & 31) + 1] + (ki << 47));
+  const double z = fma(kF0, r, kF1);
+  const double r2 = r * r;
+  double y = fma(kF2, r, 1.0);
+  y = fma(z, r2, y);
+  float e = (float)(y * s);
+  e = x > 0x1.62e42ep6f ? __builtin_inff() : e;  // overflow (+inf included)
+  e = x < -0x1.9fe368p6f ? 0.0f : e;             // underflow (-inf included)
+  return x != x ? x + x : e;
+}
+
 // src/Models.py:10-12  sigmoid(x) = 1.0 / (1.0 + np.exp(-x))  (IEEE division).
 AG_HD double sigmoid(double z, const uint64_t *tab) { return 1.0 / (1.0 + exp(-z, tab)); }
 AG_HD double sigmoid_fast(double z, const uint64_t *tab) { return 1.0 / (1.0 + exp_fast(-z, tab)); }

@@ -59,7 +59,7 @@ __global__ __launch_bounds__(kPlThreads) void k_estimate_lrts(const float *__res
     float x[AG_LRTS_MAX_DO];
     for (int d = 0; d < Do; ++d) x[d] = (float)context[i * Do + d];  // torch.from_numpy(context.astype(float32))
     const float *nz = noise ? noise + (i * K + k) * Do : nullptr;
-    ctr[j] = (double)ts_ctr(m + (size_t)k * Do, x, Do, nz, 1u, s_tab);
+    ctr[j] = (double)ts_ctr(m + (size_t)k * Do, x, Do, nz, 1u, k, K, s_tab);
   }
 }
 

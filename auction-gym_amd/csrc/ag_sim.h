@@ -367,65 +367,95 @@ struct Resolved {
   double price, second;
 };
 
-// PyTorchLogisticRegression forward CTR in float32 (src/Models.py:28-33), the oracle's
-// ora_ts_ctr: products rounded separately and summed in order, exp from the glibc-identical
-// double exp rounded to float, then 1 / (1 + e) in float.
-__device__ __forceinline__ float ts_ctr(const float *w, const float *x, int Do, const float *nz,
-                                        uint32_t nz_stride, const uint64_t *tab) {
-  float z = 0.0f;
-  for (int d = 0; d < Do; ++d) {
-    const float wd = nz ? w[d] + nz[(uint32_t)d * nz_stride] : w[d];
-    const float t = wd * x[d];
-    z = d == 0 ? t : z + t;
-  }
-  const float e = (float)agexp::exp_fast(-(double)z, tab);
-  return 1.0f / (1.0f + e);
+// torch's float32 exp on the CPU as torch.sigmoid's vectorised path computes it (SLEEF's
+// expf_u10; oracle/ag_oracle_dr.c torch_expf bit for bit): q = round(x / ln 2), the reduced
+// argument in two fused steps, a degree-5 fused Horner polynomial, times 2^q in two steps.
+__device__ __forceinline__ float torch_expf(float d) {
+  const float q = __builtin_rintf(d * 1.442695040888963407359924681001892137426645954152985934135449406931f);
+  float s = __builtin_fmaf(q, -0.693145751953125f, d);
+  s = __builtin_fmaf(q, -1.428606765330187045e-06f, s);
+  float u = 0.000198527617612853646278381f;
+  u = __builtin_fmaf(u, s, 0.00139304355252534151077271f);
+  u = __builtin_fmaf(u, s, 0.00833336077630519866943359f);
+  u = __builtin_fmaf(u, s, 0.0416664853692054748535156f);
+  u = __builtin_fmaf(u, s, 0.166666671633720397949219f);
+  u = __builtin_fmaf(u, s, 0.5f);
+  u = 1.0f + __builtin_fmaf(s * s, u, s);
+  const int e = (int)q, e1 = e >> 1;
+  u = u * __builtin_ldexpf(1.0f, e1) * __builtin_ldexpf(1.0f, e - e1);
+  if (d < -104.0f) u = 0.0f;
+  if (d > 100.0f) u = INFINITY;
+  return u;
 }
 
-// ts_ctr over a compile-time register width DW >= Do (the runtime model width): the terms
-// d >= Do are skipped, so the float32 sum is the same sequence of roundings as ts_ctr's.
+// PyTorchLogisticRegression forward (src/Models.py:28-33) as torch runs it on the CPU for one
+// context, oracle/ag_oracle.c ora_ts_logit / ora_ts_sigmoid bit for bit: F.linear(x[Do],
+// W[K][Do]) is one MKL sgemv -- for Do = 5 (every shipped config) rows in whole blocks of 4
+// sum (fma(w1, x1, w0 x0) + w3 x3) + (w4 x4 + w2 x2), the K % 4 remainder rows
+// w0 x0 + ((w4 x4 + w2 x2) + (w3 x3 + w1 x1)); other Do in order -- then torch.sigmoid:
+// elements of whole 32-lane chunks 1 / (1 + torch_expf(-z)), the rest its scalar path
+// 1 / (1 + expf(-z)) with glibc's expf (agexp::expf_glibc). W = m (+ noise) in float32.
+__device__ __forceinline__ float ts_logit_w(const float *wd, const float *x, int Do, int k, int K) {
+  if (Do == 5) {
+    const float p0 = wd[0] * x[0], p2 = wd[2] * x[2], p3 = wd[3] * x[3], p4 = wd[4] * x[4];
+    if (k < (K & ~3)) return (__builtin_fmaf(wd[1], x[1], p0) + p3) + (p4 + p2);
+    const float p1 = wd[1] * x[1];
+    return p0 + ((p4 + p2) + (p3 + p1));
+  }
+  float z = wd[0] * x[0];
+  for (int d = 1; d < Do; ++d) z = z + wd[d] * x[d];
+  return z;
+}
+__device__ __forceinline__ float ts_ctr_of(float z, int k, int K, const uint64_t *tab) {
+  const float e = k < (K & ~31) ? torch_expf(-z) : agexp::expf_glibc(-z, tab);
+  return 1.0f / (1.0f + e);
+}
+// K < 32: every element on the scalar path
+__device__ __forceinline__ float ts_ctr_scalar(float z, const uint64_t *tab) {
+  return 1.0f / (1.0f + agexp::expf_glibc(-z, tab));
+}
+__device__ __forceinline__ float ts_ctr(const float *w, const float *x, int Do, const float *nz, uint32_t nz_stride,
+                                        int k, int K, const uint64_t *tab) {
+  float wd[AG_LRTS_MAX_DO];
+  for (int d = 0; d < Do; ++d) wd[d] = nz ? w[d] + nz[(uint32_t)d * nz_stride] : w[d];
+  return ts_ctr_of(ts_logit_w(wd, x, Do, k, K), k, K, tab);
+}
+
+// the same logit over a compile-time register width DW >= Do (the runtime model width).
 // nzv: the coefficients' noise, already in registers (noisy = false: the MAP CTR).
 template <int DW>
-__device__ __forceinline__ float ts_ctr_k(const float *w, const float (&x)[DW], const float (&nzv)[DW],
-                                          bool noisy, int Do, const uint64_t *tab) {
+__device__ __forceinline__ float ts_logit(const float *w, const float (&x)[DW], const float (&nzv)[DW], bool noisy,
+                                          int Do, int k, int K) {
+  float wd[DW];
+#pragma unroll
+  for (int d = 0; d < DW; ++d) wd[d] = d < Do ? (noisy ? w[d] + nzv[d] : w[d]) : 0.0f;
   float z = 0.0f;
 #pragma unroll
   for (int d = 0; d < DW; ++d) {
     if (d < Do) {
-      const float wd = noisy ? w[d] + nzv[d] : w[d];
-      const float t = wd * x[d];
+      const float t = wd[d] * x[d];
       z = d == 0 ? t : z + t;
     }
   }
-  const float e = (float)agexp::exp_fast(-(double)z, tab);
-  return 1.0f / (1.0f + e);
-}
-
-// float32 logit of item k: the products rounded separately and summed in order (ts_ctr_k's)
-template <int DW>
-__device__ __forceinline__ float ts_logit(const float *w, const float (&x)[DW], const float (&nzv)[DW], bool noisy,
-                                          int Do) {
-  float z = 0.0f;
-#pragma unroll
-  for (int d = 0; d < DW; ++d) {
-    if (d < Do) {
-      const float wd = noisy ? w[d] + nzv[d] : w[d];
-      const float t = wd * x[d];
-      z = d == 0 ? t : z + t;
-    }
+  if constexpr (DW >= 5) {  // Do = 5: the sgemv kernel's order (branch-free: selects)
+    const float p0 = wd[0] * x[0], p1 = wd[1] * x[1], p2 = wd[2] * x[2], p3 = wd[3] * x[3], p4 = wd[4] * x[4];
+    const float blk = (__builtin_fmaf(wd[1], x[1], p0) + p3) + (p4 + p2);
+    const float rem = p0 + ((p4 + p2) + (p3 + p1));
+    z = Do == 5 ? (k < (K & ~3) ? blk : rem) : z;
   }
   return z;
 }
-__device__ __forceinline__ float ts_ctr_of(float z, const uint64_t *tab) {
-  const float e = (float)agexp::exp_fast(-(double)z, tab);
-  return 1.0f / (1.0f + e);
+template <int DW>
+__device__ __forceinline__ float ts_ctr_k(const float *w, const float (&x)[DW], const float (&nzv)[DW],
+                                          bool noisy, int Do, int k, int K, const uint64_t *tab) {
+  return ts_ctr_of(ts_logit<DW>(w, x, nzv, noisy, Do, k, K), k, K, tab);
 }
 
 // Thompson-sampling item choice of an LR-TS agent (src/Agent.py:29-42): first argmax of
 // sampled CTR * value. The noise of kTsGroup items is loaded together (one memory latency
 // per group instead of one per item), then the group is scored.
 //
-// Screened (K <= kTsScreenK): every item's logit is exact (float32, as ts_ctr's), its score
+// Screened (K <= kTsScreenK): every item's logit is exact (float32, ts_logit's), its score
 // first estimated with the hardware exp2 / reciprocal -- relative error < 2^-16 for |z| <
 // 64 and value > 0 (argument rounding |z| log2 e 2^-23 <= 2^-16.5, v_exp_f32 / v_rcp_f32
 // 1 ulp each, float value and product 2^-24 each) -- then only the items within 2^-13 of
@@ -455,7 +485,7 @@ __device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], 
           zk[k] = 0.0f;
           ek[k] = -1.0f;
           if (k < K) {
-            const float z = ts_logit<DW>(m + k * Do, xo, nzv[g], nz != nullptr, Do);
+            const float z = ts_logit<DW>(m + k * Do, xo, nzv[g], nz != nullptr, Do, k, K);
             const float v = (float)vals[k];
             const bool ok = __builtin_fabsf(z) < 64.0f && v > 0.0f;
             const float e = __builtin_amdgcn_exp2f(-z * 1.44269504f);
@@ -488,7 +518,7 @@ __device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], 
       float z = zk[0];
 #pragma unroll
       for (int kk = 1; kk < kTsScreenK; ++kk) z = k == kk ? zk[kk] : z;
-      const double sc = (double)ts_ctr_of(z, tab) * vals[k];
+      const double sc = (double)ts_ctr_scalar(z, tab) * vals[k];  // K <= kTsScreenK < 32
       if (best < 0 || sc > best_sc) {
         best_sc = sc;
         best = k;
@@ -509,7 +539,7 @@ __device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], 
     for (int g = 0; g < kTsGroup; ++g) {
       const int k = k0 + g;
       if (k < K) {
-        const float ck = ts_ctr_k<DW>(m + k * Do, xo, nzv[g], nz != nullptr, Do, tab);
+        const float ck = ts_ctr_k<DW>(m + k * Do, xo, nzv[g], nz != nullptr, Do, k, K, tab);
         const double sc = (double)ck * vals[k];
         if (k == 0 || sc > best_sc) {
           best_sc = sc;
@@ -548,27 +578,6 @@ __device__ __forceinline__ void policy_bid(const float *p, double ctr, double va
   const double logp = -(z * z) / 2.0 - aglog1p::log1p((double)sg - 1.0) - 0.91893853320467274178;
   prop = (double)(float)agexp::exp_fast(logp, tab);
   gamma = raw < 0.0f ? 0.0 : (raw > 1.0f ? 1.0 : (double)raw);
-}
-
-// torch's float32 exp on the CPU as torch.sigmoid's vectorised path computes it (SLEEF's
-// expf_u10; oracle/ag_oracle_dr.c torch_expf bit for bit): q = round(x / ln 2), the reduced
-// argument in two fused steps, a degree-5 fused Horner polynomial, times 2^q in two steps.
-__device__ __forceinline__ float torch_expf(float d) {
-  const float q = __builtin_rintf(d * 1.442695040888963407359924681001892137426645954152985934135449406931f);
-  float s = __builtin_fmaf(q, -0.693145751953125f, d);
-  s = __builtin_fmaf(q, -1.428606765330187045e-06f, s);
-  float u = 0.000198527617612853646278381f;
-  u = __builtin_fmaf(u, s, 0.00139304355252534151077271f);
-  u = __builtin_fmaf(u, s, 0.00833336077630519866943359f);
-  u = __builtin_fmaf(u, s, 0.0416664853692054748535156f);
-  u = __builtin_fmaf(u, s, 0.166666671633720397949219f);
-  u = __builtin_fmaf(u, s, 0.5f);
-  u = 1.0f + __builtin_fmaf(s * s, u, s);
-  const int e = (int)q, e1 = e >> 1;
-  u = u * __builtin_ldexpf(1.0f, e1) * __builtin_ldexpf(1.0f, e - e1);
-  if (d < -104.0f) u = 0.0f;
-  if (d > 100.0f) u = INFINITY;
-  return u;
 }
 
 // ValueLearningBidder 'search' bid (src/Bidder.py:180-196): the shading factor maximising
@@ -643,7 +652,7 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
 #pragma unroll
       for (int d = 0; d < D; ++d) xo[d] = d < Do - 1 ? (float)x[d] : (d == Do - 1 ? 1.0f : 0.0f);
       best = ts_select<D>(m, xo, nz, K, Do, T.vals + a * T.values_stride, T.tab);
-      est = (double)ts_ctr_k<D>(m + best * Do, xo, xo, false, Do, T.tab);
+      est = (double)ts_ctr_k<D>(m + best * Do, xo, xo, false, Do, best, K, T.tab);
       tru = best == best_t ? c : agexp::sigmoid_fast(dot_ref<D>(itm + best * D, x), T.tab);
     }
   }

@@ -144,15 +144,38 @@ static int32_t oracle_select(const double *items, const double *vals, int32_t K,
   return best;
 }
 
-/* PyTorchLogisticRegression.forward (src/Models.py:28-33) in float32: z = x . w summed in
- * order with separately rounded products, CTR = 1 / (1 + exp(-z)) in float32 with exp
- * rounded from the glibc double exp. torch computes the same quantities with MKL sgemv
- * and a SIMD expf: equal up to a few float32 ulps (parity by tolerance). */
-float ora_ts_ctr(const float *w, const float *x, int32_t Do) {
+/* PyTorchLogisticRegression.forward (src/Models.py:28-33) as torch runs it on the CPU for
+ * one context (src/BidderAllocation.py:67-68): F.linear(x[Do], W[K][Do]) with a 1-D input
+ * is one BLAS sgemv (MKL), then torch.sigmoid over the K logits.
+ *  - logit of item k: products rounded separately; for Do = 5 (obs_embedding_size 4 plus
+ *    the intercept, every shipped config) summed as the sgemv kernel does -- rows in whole
+ *    blocks of 4 as (fma(w1, x1, w0 x0) + w3 x3) + (w4 x4 + w2 x2), the K % 4 remainder
+ *    rows as w0 x0 + ((w4 x4 + w2 x2) + (w3 x3 + w1 x1)) (all of 10800 summation trees
+ *    over the 5 terms searched against torch, these two equal it on every row; test:
+ *    tests/test_oracle_golden.py::test_ts_forward_matches_torch). Other Do: summed in
+ *    order (parity by tolerance there).
+ *  - sigmoid: elements in whole 32-lane chunks take torch's vectorised path (SLEEF expf_u10,
+ *    ora_torch_sigmoidf), the rest its scalar 1 / (1 + expf(-z)) with glibc's expf
+ *    (K = 12 < 32: all scalar). */
+float ora_ts_logit(const float *w, const float *x, int32_t Do, int32_t k, int32_t K) {
+  if (Do == 5) {
+    const float p0 = w[0] * x[0], p2 = w[2] * x[2], p3 = w[3] * x[3], p4 = w[4] * x[4];
+    if (k < (K & ~3)) return (fmaf(w[1], x[1], p0) + p3) + (p4 + p2);
+    const float p1 = w[1] * x[1];
+    return p0 + ((p4 + p2) + (p3 + p1));
+  }
   float z = w[0] * x[0];
   for (int32_t d = 1; d < Do; ++d) z = z + w[d] * x[d];
-  float e = (float)exp(-(double)z);
-  return 1.0f / (1.0f + e);
+  return z;
+}
+
+float ora_ts_sigmoid(float z, int32_t k, int32_t K) {
+  if (k < (K & ~31)) return ora_torch_sigmoidf(z);
+  return 1.0f / (1.0f + expf(-z));
+}
+
+float ora_ts_ctr(const float *w, const float *x, int32_t Do, int32_t k, int32_t K) {
+  return ora_ts_sigmoid(ora_ts_logit(w, x, Do, k, K), k, K);
 }
 
 /* Gaussian shading factor of an uninitialised shading bidder (src/Bidder.py:47-58,
@@ -209,13 +232,13 @@ static void simulate_range(const ora_pop *pp, const double *items, const double 
         it = 0;
         for (int32_t k = 0; k < K; ++k) {
           for (int32_t d = 0; d < Do; ++d) w[d] = m[k * Do + d] + (pp->ts_sample ? nz[k * Do + d] : 0.0f);
-          const double sc = (double)ora_ts_ctr(w, xo, Do) * v_a[k];
+          const double sc = (double)ora_ts_ctr(w, xo, Do, k, K) * v_a[k];
           if (k == 0 || sc > best_s) {
             best_s = sc;
             it = k;
           }
         }
-        est = (double)ora_ts_ctr(m + it * Do, xo, Do);
+        est = (double)ora_ts_ctr(m + it * Do, xo, Do, it, K);
         tru = it == it_t ? ctr_t : ora_sigmoid(ora_dot(it_a + (int64_t)it * D, x, D));
       }
       const double v = v_a[it];
@@ -411,8 +434,7 @@ void ora_gen_participants(uint64_t seed, uint64_t idx, int32_t N, int32_t P, int
  * update of q per item (:58-61, src/Models.py:43-45) and prev_m = m (:62).
  *
  * Arithmetic (the definition the device kernel follows bit for bit):
- *  - z = x . m[a] in float32, products rounded separately, summed in order (as
- *    ora_ts_ctr); p = 1 / (1 + (float)exp(-(double)z)) in float32.
+ *  - z = x . m[a] in float32, products rounded separately, summed in order; p = 1 / (1 + (float)exp(-(double)z)) in float32.
  *  - BCE term (torch.nn.BCELoss, logs clamped at -100) in double: y ? -max(log p, -100)
  *    : -max(log1p(-p), -100); gradient term (p - y) * x_d, exact in double.
  *  - Sums over samples are EXACT: every term is rounded to a fixed-point grid (BCE 2^-32,

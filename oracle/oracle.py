@@ -77,7 +77,9 @@ def lib():
         L.ora_simulate_pop.argtypes = [ctypes.POINTER(_Pop), vp, vp, i64, ctypes.POINTER(_In),
                                        ctypes.POINTER(_Out), vp, vp, i32]
         L.ora_ts_ctr.restype = ctypes.c_float
-        L.ora_ts_ctr.argtypes = [vp, vp, i32]
+        L.ora_ts_ctr.argtypes = [vp, vp, i32, i32, i32]
+        L.ora_ts_logit.restype = ctypes.c_float
+        L.ora_ts_logit.argtypes = [vp, vp, i32, i32, i32]
         L.ora_to_fx.restype = i64
         L.ora_to_fx.argtypes = [d]
         L.ora_gen_uniform.restype = d

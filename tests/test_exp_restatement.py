@@ -49,6 +49,48 @@ def test_host_build_of_device_exp_matches_glibc(tmp_path):
     assert r.returncode == 0, r.stdout
 
 
+EXPF_SRC = r'''
+#include <stdio.h>
+#include <stdlib.h>
+#include <math.h>
+#include "ag_exp.h"
+#include "ag_exp_table.h"
+static long bad = 0, n = 0;
+static void check(unsigned b) {
+  float x; memcpy(&x, &b, 4); ++n;
+  float a = expf(x), m = agexp::expf_glibc(x, ag_exp_tab);
+  if (isnan(a) && isnan(m)) return;
+  if (memcmp(&a, &m, 4)) { if (bad < 5) printf("x=%a libm=%a mine=%a\n", x, a, m); ++bad; }
+}
+int main(int argc, char **argv) {
+  unsigned stride = (unsigned)atoi(argv[1]), off = (unsigned)atoi(argv[2]);
+  for (unsigned long long u = off; u < (1ull << 32); u += stride) check((unsigned)u);
+  /* the range edges: +-0, +-inf, nan, around 88 / 88.72 / -103.28 / -103.97 / -104 */
+  const unsigned edge[] = {0u, 0x80000000u, 0x7f800000u, 0xff800000u, 0x7fc00000u, 0xffc00000u};
+  for (unsigned e : edge) check(e);
+  const unsigned mid[] = {0x42b00000u, 0x42b17218u, 0xc2ce8ed0u, 0xc2cff1b4u, 0xc2d00000u, 0xc2b00000u};
+  for (unsigned c : mid) for (int d = -64; d <= 64; ++d) check(c + d);
+  printf("bad %ld of %ld\n", bad, n);
+  return bad != 0;
+}
+'''
+
+
+def test_host_build_of_device_expf_matches_glibc(tmp_path):
+    """agexp::expf_glibc (torch.sigmoid's scalar path, the LR-TS CTRs) against the host libm
+    expf: every 7th float bit pattern (a sixth of a billion, all exponents and signs) plus
+    the range edges (+-0, +-inf, nan, the overflow / underflow thresholds). The full 2^32
+    sweep (stride 1) also passes; it takes ~90 s, so the suite runs the strided one."""
+    c = tmp_path / "f.cpp"
+    c.write_text(EXPF_SRC)
+    exe = tmp_path / "f"
+    inc = os.path.join(ROOT, "auction-gym_amd", "csrc")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", inc, str(c), "-o", str(exe),
+                    "-lm"], check=True)
+    r = subprocess.run([str(exe), "7", "3"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout
+
+
 def test_log1p_restatement_accuracy():
     """The fdlibm log1p the DR bidder's softplus uses (oracle/ag_oracle_dr.c; the device's
     csrc/ag_log1p.h is the same algorithm): within 1 ulp of libm over its whole use range."""

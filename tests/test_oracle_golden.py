@@ -146,15 +146,11 @@ def test_sp_oracle_full_run_known_answers(oracle, tmp_path):
 # ---- populations beyond Oracle + Truthful (LR-TS allocators, shading bidders) ----
 from conftest import POP_CAPTURES, pop_args  # noqa: E402
 
-TS_EST_RTOL = 2.0 ** -21  # torch's float32 sgemv + SIMD sigmoid vs the restated float32 path
-
-
 @pytest.mark.parametrize("name", POP_CAPTURES)
 def test_population_matches_reference(oracle, name):
     d, meta, agg = load_capture(name)
     o = oracle.simulate_pop(mech_code(meta), d["items"], d["values"], d["ctx"], d["part"], d["u"],
                             **pop_args(d, meta))
-    ts = any(a == "PyTorchLogisticRegressionAllocator" for a in meta["allocators"])
     # the true-CTR side is FP64 libm arithmetic: bit-exact for every population
     assert np.array_equal(o["true_ctr"], d["slot_true_ctr"])
     assert np.array_equal(o["best_ev"], d["slot_best_ev"])
@@ -164,16 +160,10 @@ def test_population_matches_reference(oracle, name):
     assert np.array_equal(o["gamma"][shading], d["slot_gamma"][shading])
     prop = ~np.isnan(d["slot_propensity"])
     np.testing.assert_allclose(o["propensity"][prop], d["slot_propensity"][prop], rtol=1e-15)
-    if ts:
-        # float32 dot of an LR-TS model: a few float32 ulps of the largest term
-        np.testing.assert_allclose(o["est_ctr"], d["slot_est_ctr"], rtol=TS_EST_RTOL, atol=1e-7)
-        np.testing.assert_allclose(o["bid"], d["slot_bid"], rtol=2 * TS_EST_RTOL, atol=2e-7)
-        np.testing.assert_allclose(o["price"], d["price"], rtol=2 * TS_EST_RTOL, atol=2e-7)
-        assert np.mean(o["est_ctr"] == d["slot_est_ctr"]) > 0.85  # most bits identical
-    else:
-        assert np.array_equal(o["bid"], d["slot_bid"])
-        assert np.array_equal(o["price"], d["price"], equal_nan=True)
-        assert np.array_equal(o["est_ctr"], d["slot_est_ctr"])
+    # LR-TS CTRs too: torch's CPU F.linear order and sigmoid paths restated (ora_ts_ctr)
+    assert np.array_equal(o["bid"], d["slot_bid"])
+    assert np.array_equal(o["price"], d["price"], equal_nan=True)
+    assert np.array_equal(o["est_ctr"], d["slot_est_ctr"])
     assert np.array_equal(o["outcome"], d["outcome"])
     C = {n: i for i, n in enumerate(oracle.COUNTERS)}
     cnt = o["counters"]
@@ -187,6 +177,31 @@ def test_population_matches_reference(oracle, name):
     np.testing.assert_allclose(np.sqrt(cnt[:, C["ctr_sqerr"]] / n), agg["ctr_rmse"], rtol=1e-5)
     won = cnt[:, C["n_won"]]
     np.testing.assert_allclose(cnt[:, C["ctr_bias_sum"]] / won, agg["ctr_bias"], rtol=1e-5)
+
+
+def test_ts_forward_matches_torch(oracle):
+    """PyTorchLogisticRegression.forward for one context (src/Models.py:28-33,
+    src/BidderAllocation.py:67-68) -- F.linear then torch.sigmoid on the CPU -- against
+    ora_ts_logit / ora_ts_ctr, element for element: Do = 5 rows in whole sgemv blocks of 4
+    and in the remainder, sigmoids on torch's vectorised (whole 32-lane chunks) and scalar
+    paths, with and without Thompson noise added to the weights."""
+    import torch
+    import torch.nn.functional as F
+    L = oracle.lib()
+    g = np.random.default_rng(5)
+    for K in (1, 3, 4, 5, 7, 12, 16, 33, 40):
+        for t in range(40):
+            W = g.normal(0, 1.5, (K, 5)).astype(np.float32)
+            if t % 2:  # m + torch.normal(0, 1 / sqrt(q)) in float32
+                W = (W + (g.normal(0, 1, (K, 5)) / np.sqrt(g.uniform(1, 60, (K, 5)))).astype(np.float32))
+            x = np.concatenate([g.normal(0, 1, 4), [1.0]]).astype(np.float32)
+            zt = F.linear(torch.from_numpy(x), torch.from_numpy(W))
+            ct = torch.sigmoid(zt).numpy()
+            zt = zt.numpy()
+            for k in range(K):
+                wp, xp = W[k].ctypes.data, x.ctypes.data
+                assert np.float32(L.ora_ts_logit(wp, xp, 5, k, K)) == zt[k], (K, t, k)
+                assert np.float32(L.ora_ts_ctr(wp, xp, 5, k, K)) == ct[k], (K, t, k)
 
 
 # ---- LR-TS allocator update (Agent.update -> PyTorchLogisticRegressionAllocator.update) ----
