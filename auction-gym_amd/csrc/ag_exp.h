@@ -137,15 +137,20 @@ AG_HD double exp_fast(double x, const uint64_t *tab) {
 
 // glibc 2.35's float expf (the algorithm of sysdeps/ieee754/flt-32/e_expf.c, restated):
 // x 32/ln2 = k + r (k rounded to nearest through the 1.5 2^52 shift, both steps fused as
-// the x86-64 FMA build does), 2^(k/32) from every 4th entry of the exp table above (the
-// same correctly rounded 2^(j/128)), 2^(r/32) by a degree-3 polynomial in double, one
-// rounding to float. What torch.sigmoid's scalar path calls (std::exp on a float); equal
-// to the host libm expf for every float (tests/test_exp_restatement.py, exhaustive).
+// the x86-64 FMA build does), 2^(k/32) from a 32-entry table, 2^(r/32) by a degree-3
+// polynomial in double, one rounding to float. What torch.sigmoid's scalar path calls
+// (std::exp on a float); equal to the host libm expf for every float
+// (tests/test_exp_restatement.py, exhaustive).
+// tab32[j] = bits(2^(j/32)) - (j << 47) = ag_exp_tab[8 j + 1] (every 4th 2^(j/128) entry,
+// the same correctly rounded values); kept as its own contiguous 256-B table in LDS
+// (kExpTabLds layout below), where 32 random lanes hit 32 distinct bank pairs.
+constexpr int kExpTabLds = 256 + 32;  // LDS copy: ag_exp_tab, then tab32
+AG_HD uint64_t expf_tab_entry(const uint64_t *exp_tab, int j) { return exp_tab[8 * j + 1]; }
 constexpr double kInvLn2F = 0x1.71547652b82fep0 * 32.0;
 constexpr double kF0 = 0x1.c6af84b912394p-5 / 32768.0;
 constexpr double kF1 = 0x1.ebfce50fac4f3p-3 / 1024.0;
 constexpr double kF2 = 0x1.62e42ff0c52d6p-1 / 32.0;
-AG_HD float expf_glibc(float x, const uint64_t *tab) {
+AG_HD float expf_glibc(float x, const uint64_t *tab32) {
   // glibc branches out for |x| >= 88 or nan and otherwise falls through to the main path
   // below; here the main path always runs and the out-of-range results are selected
   // (branch-free, for unrolled divergent code)
@@ -154,7 +159,7 @@ AG_HD float expf_glibc(float x, const uint64_t *tab) {
   const uint64_t ki = asu64(kd);
   kd -= kShift;
   const double r = fma(kInvLn2F, xd, -kd);
-  const double s = asf64(tab[8 * (ki & 31) + 1] + (ki << 47));
+  const double s = asf64(tab32[ki & 31] + (ki << 47));
   const double z = fma(kF0, r, kF1);
   const double r2 = r * r;
   double y = fma(kF2, r, 1.0);

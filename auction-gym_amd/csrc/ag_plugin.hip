@@ -50,8 +50,9 @@ __global__ __launch_bounds__(kPlThreads) void k_estimate_lrts(const float *__res
                                                               const double *__restrict__ context,
                                                               const float *__restrict__ noise,
                                                               double *__restrict__ ctr) {
-  __shared__ uint64_t s_tab[256];
+  __shared__ uint64_t s_tab[agexp::kExpTabLds];
   for (int i = threadIdx.x; i < 256; i += kPlThreads) s_tab[i] = ag_exp_tab[i];
+  for (int j = threadIdx.x; j < 32; j += kPlThreads) s_tab[256 + j] = agexp::expf_tab_entry(ag_exp_tab, j);
   __syncthreads();
   for (int64_t j = (int64_t)blockIdx.x * kPlThreads + threadIdx.x; j < n * K; j += (int64_t)gridDim.x * kPlThreads) {
     const int64_t i = j / K;

@@ -141,7 +141,7 @@ __host__ inline LdsLayout make_layout(int N, int K, int D, bool counters, bool g
   L.replicas = R;
   int64_t b = 0;
   L.tab = 0;
-  b += 256 * 8;
+  b += agexp::kExpTabLds * 8;  // ag_exp_tab + the expf table
   L.items = align16(b);
   b = L.items + (int64_t)N * L.items_stride * 8;
   L.values = align16(b);
@@ -407,12 +407,12 @@ __device__ __forceinline__ float ts_logit_w(const float *wd, const float *x, int
   return z;
 }
 __device__ __forceinline__ float ts_ctr_of(float z, int k, int K, const uint64_t *tab) {
-  const float e = k < (K & ~31) ? torch_expf(-z) : agexp::expf_glibc(-z, tab);
+  const float e = k < (K & ~31) ? torch_expf(-z) : agexp::expf_glibc(-z, tab + 256);
   return 1.0f / (1.0f + e);
 }
-// K < 32: every element on the scalar path
+// K < 32: every element on the scalar path. `tab`: the kExpTabLds-entry LDS table.
 __device__ __forceinline__ float ts_ctr_scalar(float z, const uint64_t *tab) {
-  return 1.0f / (1.0f + agexp::expf_glibc(-z, tab));
+  return 1.0f / (1.0f + agexp::expf_glibc(-z, tab + 256));
 }
 __device__ __forceinline__ float ts_ctr(const float *w, const float *x, int Do, const float *nz, uint32_t nz_stride,
                                         int k, int K, const uint64_t *tab) {
@@ -763,6 +763,7 @@ __global__ __launch_bounds__(BT, GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES) void
     }
   }
   for (int i = tid; i < 256; i += BT) s_tab[i] = ag_exp_tab[i];
+  for (int j = tid; j < 32; j += BT) s_tab[256 + j] = agexp::expf_tab_entry(ag_exp_tab, j);
   for (int i = tid; i < N * K * D; i += BT) {
     const int a = i / (K * D), r = i - a * (K * D);
     s_items[a * L.items_stride + r] = prm.items[i];

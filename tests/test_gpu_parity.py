@@ -944,8 +944,8 @@ SP_TRUTHFUL_TS = {  # config/SP_Truthful_TS.json as shipped
 def test_driver_sp_truthful_ts_iteration(gpu, oracle, tmp_path):
     """SP_Truthful_TS.json through the drop-in classes with torch seeded as the capture was:
     the same LR-TS initial models (torch.nn.init.normal_), the same Thompson draws
-    (torch.normal in slot order), the reference's rounds (capture sp_ts_r2048: winners and
-    items exact, utilities within float32 CTR tolerance); then Agent.update trains all six
+    (torch.normal in slot order), the reference's rounds (capture sp_ts_r2048: winners,
+    items and the float32 CTRs exact, so utilities and revenue to the exact sums' 1e-11); then Agent.update trains all six
     LR-TS agents on the GPU (== the oracle on the reference's own update samples); the next
     iteration samples with the updated posterior."""
     import torch
@@ -963,7 +963,7 @@ def test_driver_sp_truthful_ts_iteration(gpu, oracle, tmp_path):
     auction, _, _, _ = M.instantiate_auction(rng, config, a2i, a2v, agents, max_slots, E, var, OE)
     for _ in range(meta["rounds"]):
         auction.simulate_opportunity()
-    rt = dict(rtol=1e-5, atol=1e-6)
+    rt = dict(rtol=1e-11, atol=1e-12)
     np.testing.assert_allclose([a.net_utility for a in agents], agg["net_utility"], **rt)
     np.testing.assert_allclose([a.gross_utility for a in agents], agg["gross_utility"], **rt)
     np.testing.assert_allclose(auction.revenue, agg["revenue"], **rt)
@@ -1003,8 +1003,8 @@ def test_driver_memory_matches_reference(gpu, tmp_path, case):
     metrics and in the records its next update trains on. Fixture: the reference's own run
     (tests/golden/make_golden.py --only memory). EmpiricalShaded (FirstPrice, M = 300):
     every iteration's revenue, utilities, metrics and new prev_gamma to 1e-9; LR-TS
-    (SP_Truthful_TS, M = 150): log counts exact, iteration 0 metrics and utilities to float32
-    CTR tolerance, the later iterations (after float32 torch fits: parity unpinned beyond
+    (SP_Truthful_TS, M = 150): log counts exact, iteration 0 metrics and utilities to 1e-9
+    (the float32 CTRs are the reference's bit for bit), the later iterations (after float32 torch fits: parity unpinned beyond
     that) within 2 %."""
     import torch
 
@@ -1022,8 +1022,7 @@ def test_driver_memory_matches_reference(gpu, tmp_path, case):
         auction.simulate_batch(cfg["rounds_per_iter"])
         k = f"{case}_it{it}"
         tight = case == "empirical" or it == 0
-        rt = dict(rtol=1e-9, atol=1e-9) if case == "empirical" else (dict(rtol=1e-5, atol=1e-5) if tight
-                                                                     else dict(rtol=2e-2, atol=2e-2))
+        rt = dict(rtol=1e-9, atol=1e-9) if tight else dict(rtol=2e-2, atol=2e-2)
         np.testing.assert_allclose(auction.revenue, kat[k + "_revenue"], **rt)
         np.testing.assert_allclose([a.net_utility for a in agents], kat[k + "_net"], **rt)
         np.testing.assert_allclose([a.gross_utility for a in agents], kat[k + "_gross"], **rt)
