@@ -304,9 +304,10 @@ __device__ __forceinline__ void adam_step_block(TrainLds &S, float *par, int np,
 
 // The rsample noise of the DR / DM policy fits: the caller's draws (noise != NULL: agent's
 // record i of epoch e at noise[e * n + i]) or synthetic ones -- a standard normal by
-// Marsaglia's polar method on Philox4x32-10 (counter (i, e, attempt, agent), key = seed),
-// its log through the restated log1p, so the host (oracle/ag_oracle_dr.c ora_fit_noise)
-// draws the same bits.
+// Marsaglia's polar method on Philox4x32-10 (counter (i, e, attempt, agent), key = seed), two
+// candidate pairs of 32-bit uniforms per call (a wave's 64 lanes then finish in ~2 calls
+// instead of ~4 with one pair), its log through the restated log1p, so the host
+// (oracle/ag_oracle_dr.c ora_fit_noise) draws the same bits.
 struct FitNoise {
   const float *noise;  // agent's draws or NULL
   int64_t n;           // agent's record count
@@ -321,15 +322,16 @@ __device__ __forceinline__ double fit_eps(const FitNoise &F, int e, int64_t i) {
   // it for every lane together (a wave's lanes accept at different attempts)
   double u = 0.0, s = 0.0;
   bool found = false;
-  for (uint32_t t = 0; t < 64 && !found; ++t) {
+  for (uint32_t t = 0; t < 32 && !found; ++t) {
     uint32_t w[4];
     philox((uint32_t)i, (uint32_t)e, t, F.agent, (uint32_t)F.seed, (uint32_t)(F.seed >> 32), w);
-    const double uu = (double)((((uint64_t)w[0] << 32) | w[1]) >> 11) * 0x1p-52 - 1.0;
-    const double vv = (double)((((uint64_t)w[2] << 32) | w[3]) >> 11) * 0x1p-52 - 1.0;
-    const double ss = uu * uu + vv * vv;
-    if (ss > 0.0 && ss < 1.0) {
-      u = uu;
-      s = ss;
+    const double u0 = (double)w[0] * 0x1p-31 - 1.0, v0 = (double)w[1] * 0x1p-31 - 1.0;
+    const double u1 = (double)w[2] * 0x1p-31 - 1.0, v1 = (double)w[3] * 0x1p-31 - 1.0;
+    const double s0 = u0 * u0 + v0 * v0, s1 = u1 * u1 + v1 * v1;
+    const bool a0 = s0 > 0.0 && s0 < 1.0, a1 = s1 > 0.0 && s1 < 1.0;
+    if (a0 || a1) {
+      u = a0 ? u0 : u1;
+      s = a0 ? s0 : s1;
       found = true;
     }
   }

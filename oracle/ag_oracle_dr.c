@@ -423,34 +423,34 @@ void ora_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t ou
 
 /* Synthetic rsample noise of the DR / DM fits (ag_bidder_update with noise == NULL): record
  * i of epoch e of agent a ~ N(0, 1) by Marsaglia's polar method on Philox4x32-10 (counter (i,
- * e, attempt, a), key = seed), log through the restated log1p, rounded to float32. */
+ * e, attempt, a), key = seed): each call gives two candidate pairs (u, v) = (w0, w1), (w2, w3)
+ * as 32-bit uniforms on [-1, 1), the first accepted pair is taken; log through the restated
+ * log1p, rounded to float32. */
 void ora_fit_noise(uint64_t seed, uint32_t agent, int32_t epochs, int64_t n, float *out) {
   const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
   for (int32_t e = 0; e < epochs; ++e)
     for (int64_t i = 0; i < n; ++i) {
       float z = 0.0f;
-      for (uint32_t t = 0; t < 64; ++t) {
+      for (uint32_t t = 0; t < 32; ++t) {
         const uint32_t ctr[4] = {(uint32_t)i, (uint32_t)e, t, agent};
         uint32_t w[4];
         ora_philox4x32_10(ctr, key, w);
-        const double u = (double)((((uint64_t)w[0] << 32) | w[1]) >> 11) * 0x1p-52 - 1.0;
-        const double v = (double)((((uint64_t)w[2] << 32) | w[3]) >> 11) * 0x1p-52 - 1.0;
-        const double s = u * u + v * v;
-        if (s > 0.0 && s < 1.0) {
-          z = (float)(u * sqrt(-2.0 * fl_log1p(s - 1.0) / s));
-          break;
+        int found = 0;
+        for (int h = 0; h < 2 && !found; ++h) {
+          const double u = (double)w[2 * h] * 0x1p-31 - 1.0;
+          const double v = (double)w[2 * h + 1] * 0x1p-31 - 1.0;
+          const double s = u * u + v * v;
+          if (s > 0.0 && s < 1.0) {
+            z = (float)(u * sqrt(-2.0 * fl_log1p(s - 1.0) / s));
+            found = 1;
+          }
         }
+        if (found) break;
       }
       out[(int64_t)e * n + i] = z;
     }
 }
 
-/* ValueLearningBidder 'search' bid (src/Bidder.py:180-196): x = float32 [ctr, value, g] for
- * the 128 grid gammas, W = sigmoid(((c w0 + v w1) + g w2) + b) in float32 (no FMAs; the
- * sigmoid through libm exp in double, rounded once), utility W (ev - ev g) in double with ev
- * = value * ctr, the first maximum of the sorted grid = the smallest gamma among ties. torch
- * evaluates W with its own float32 kernels (an ulp apart at most): the argmax agrees except
- * where two grid points' utilities are that close. */
 /* torch's float32 exp on the CPU, as torch.sigmoid's vectorised path computes it (ATen's
  * sigmoid kernel: (1 + exp(-x)).reciprocal() with Vectorized<float>::exp = SLEEF's expf_u10):
  * round(x / ln 2) = q, x - q ln 2 in two fused steps, a degree-5 polynomial by fused Horner,

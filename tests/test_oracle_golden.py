@@ -493,3 +493,15 @@ def test_torch_sigmoid_restatement_matches_torch(oracle):
     f = oracle.lib().ora_torch_sigmoidf
     got = np.array([f(ctypes.c_float(v)) for v in x], np.float32)
     assert np.array_equal(got, want)
+
+
+def test_synthetic_fit_noise_is_standard_normal(oracle):
+    """ora_fit_noise (the trainer's synthetic rsample draws, polar method with two candidate
+    pairs per Philox call): 2e5 draws with mean 0, variance 1, the normal's tail mass, no
+    failed (zero) draws, and distinct per epoch and per agent."""
+    z = oracle.fit_noise(77, 0, 4, 50000).astype(np.float64)
+    assert z.shape == (4, 50000) and np.all(z != 0.0)
+    assert abs(z.mean()) < 0.01 and abs(z.var() - 1.0) < 0.02
+    assert abs(np.mean(np.abs(z) > 1.96) - 0.05) < 0.003
+    assert not np.array_equal(z[0], z[1])
+    assert not np.array_equal(z[0], oracle.fit_noise(77, 1, 1, 50000)[0])

@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""profiles/pmc_traffic.json from a tools/prof_r02e.sh run: HBM bytes per launch =
+FETCH_SIZE x 2 x 1024 + WRITE_SIZE x 1024 (gfx950 corrections, MI355X_MICROARCH.md), mean over
+the dispatches, for the headline kernel and the general kernel of every population line,
+with the ratio to the bench line's algorithmic bytes (bench_driver.log of the same run).
+    python tools/make_pmc_traffic.py gpurun_out/prof_<tag> <tag>"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from summarize_pmc import pmc  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    d, tag = sys.argv[1], sys.argv[2]
+    bench = None
+    for ln in open(os.path.join(d, "bench_driver.log")):
+        if ln.startswith("{"):
+            bench = json.loads(ln)
+    out = {}
+
+    def traffic(fetch, write):
+        f, nf = pmc(os.path.join(d, fetch))
+        w, nw = pmc(os.path.join(d, write))
+        if not f or not w:
+            return None, 0
+        return f["FETCH_SIZE"] * 2 * 1024 + w["WRITE_SIZE"] * 1024, min(nf, nw)
+
+    t, n = traffic("fetch", "write")
+    B = bench["config"]["auctions_per_gpu_per_step"]
+    out.update({"batch": B, "hbm_bytes_per_launch": t,
+                "source": f"profiles/{tag}_pmc_summary.json (k_oracle<2,6,false>, FETCH_SIZE*2*1024 + "
+                          f"WRITE_SIZE*1024, mean over {n} dispatches of {B} auctions)",
+                "over_algorithmic": t / (bench["roofline"]["algorithmic_bytes_per_auction"] * B)})
+    for c in (1, 2, 3, 4):
+        key = f"configs_{c}"
+        t, n = traffic(f"c{c}_fetch", f"c{c}_write")
+        if t is None or key not in bench:
+            continue
+        b = bench[key]["auctions_per_gpu_per_step"]
+        out[key] = {"batch": b, "hbm_bytes_per_launch": t,
+                    "source": f"profiles/{tag}_pmc_summary.json (k_simulate, general populations; "
+                              f"mean over {n} dispatches)",
+                    "over_algorithmic": t / (bench[key]["algorithmic_bytes_per_auction"] * b)}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
