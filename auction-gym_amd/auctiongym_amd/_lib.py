@@ -24,6 +24,7 @@ OPT_BIDDER_RECORD_CACHE = 6
 OPT_SIMULATE_KERNEL = 7
 OPT_SIM_BLOCKS_PER_CU = 8
 OPT_SIM_BLOCK_THREADS = 9
+OPT_SIM_GENERAL_MODE = 10
 SIM_KERNEL_AUTO, SIM_KERNEL_GENERIC = 0, 1
 ITEM_SEARCH_AUTO, ITEM_SEARCH_EXACT = 0, 1
 

@@ -291,7 +291,7 @@ __global__ __launch_bounds__(kThreads) void k_stream_copy(const u32x4 *__restric
 // ------------------------------------------------------------------------------------
 // dispatch
 // ------------------------------------------------------------------------------------
-SimKernel pick_kernel(int P, int D, bool prune, int W, bool general, int bt) {
+SimKernel pick_kernel(int P, int D, bool prune, int W, int general, int bt) {
   if (P > kMaxP) return pick_kernel_for<0>(D, prune, W, general, bt);  // runtime-P kernel
   switch (P) {
     case 1: return pick_kernel_for<1>(D, prune, W, general, bt);
@@ -620,6 +620,10 @@ int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
                             kLargeThreads);
       c->block_threads = (int32_t)value;
       return AG_OK;
+    case AG_OPT_SIM_GENERAL_MODE:
+      if (value != 0 && value != 1) return ag_set_error(AG_ERR_INVALID, "ag_set_option: general mode must be 0 or 1");
+      c->gen_mode_all = value == 1;
+      return AG_OK;
     case AG_OPT_SIMULATE_KERNEL:
       if (value != AG_SIM_KERNEL_AUTO && value != AG_SIM_KERNEL_GENERIC)
         return ag_set_error(AG_ERR_INVALID, "ag_set_option: bad simulate kernel %lld", (long long)value);
@@ -742,10 +746,13 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   // image among 16 waves. Same results (the counters are exact sums).
   int bt = c->block_threads;
   if (bt == 0) bt = (c->general && prune && lds > 40 * 1024) ? kLargeThreads : kThreads;
-  SimKernel k = pick_kernel(s.num_participants, D, prune, W, c->general, bt);
+  // AG_OPT_SIM_GENERAL_MODE 0 (auto): TruthfulBidder-only populations take the build
+  // without the bid-shading code (kGenTruthful); 1: always the full general build
+  const int gmode = !c->general ? kGenOracle : (c->has_shading || c->gen_mode_all) ? kGenAll : kGenTruthful;
+  SimKernel k = pick_kernel(s.num_participants, D, prune, W, gmode, bt);
   if (!k && bt != kThreads) {
     bt = kThreads;
-    k = pick_kernel(s.num_participants, D, prune, W, c->general, bt);
+    k = pick_kernel(s.num_participants, D, prune, W, gmode, bt);
   }
   if (!k) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: no kernel for P=%d D=%d", s.num_participants, D);
   hipStream_t st = (hipStream_t)stream;
@@ -753,8 +760,8 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
     AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   // Persistent grid: exactly the blocks the device keeps resident (no partial last round),
   // each striding over bt-auction tiles.
-  int &res = c->resident[(bt == kThreads ? 0 : 16) + (c->general ? 8 : 0) + (W == 2 ? 4 : 0) + (prune ? 2 : 0) +
-                         (prm.want_counters ? 1 : 0)];
+  int &res = c->resident[(gmode == kGenTruthful ? 32 : 0) + (bt == kThreads ? 0 : 16) + (c->general ? 8 : 0) +
+                         (W == 2 ? 4 : 0) + (prune ? 2 : 0) + (prm.want_counters ? 1 : 0)];
   if (res == 0) {
     int per_cu = 0, cus = 0;
     AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k, bt, lds));

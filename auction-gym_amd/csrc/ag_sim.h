@@ -22,6 +22,9 @@ namespace ag {
 #ifndef AG_GEN_MIN_WAVES
 #define AG_GEN_MIN_WAVES 3  // the general kernel: <= 168 VGPRs
 #endif
+#ifndef AG_TB_MIN_WAVES
+#define AG_TB_MIN_WAVES 4  // the general kernel for truthful bidders only: <= 128 VGPRs
+#endif
 #ifndef AG_TS_SCREEN
 #define AG_TS_SCREEN 1  // screened Thompson item choice (ts_select)
 #endif
@@ -37,6 +40,9 @@ constexpr int kThreads = 256;              // 4 waves of 64 lanes
 #define AG_LARGE_BT 1024
 #endif
 constexpr int kLargeThreads = AG_LARGE_BT;  // the general kernel's workgroups for large LDS images
+// k_simulate's GENERAL modes: Oracle + Truthful only; any population; allocators of any
+// kind with TruthfulBidders only (no bid-shading code: fewer VGPRs, 4 waves per SIMD)
+constexpr int kGenOracle = 0, kGenAll = 1, kGenTruthful = 2;
 constexpr int kC = AG_NUM_COUNTERS;
 // Auctions one block may resolve per launch: 1024 per counter replica keeps every replica's
 // int64 sum exact (<= 1024 * P terms of magnitude < 2^50, to_fx).
@@ -622,7 +628,7 @@ struct SlotResult {
   double val, bid, ctr, est, bev, gamma, prop;
 };
 
-template <int D, bool PRUNE, bool GENERAL>
+template <int D, bool PRUNE, int GENERAL>
 __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const double (&x)[kMaxD],
                                                    const float (&xf)[kMaxD], float xabs, int a, int s,
                                                    const ag_batch_in &in, uint32_t B, uint32_t i, bool ts_sample) {
@@ -658,7 +664,7 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
   }
   const double v = T.vals[a * T.values_stride + best];
   double b = v * est;  // Bidder.bid: value * estimated CTR (src/Bidder.py:35, :49, :173, ...)
-  if constexpr (GENERAL) {
+  if constexpr (GENERAL == kGenAll) {  // kGenTruthful: every bidder is a TruthfulBidder
     const int bk = T.bkind[a];
     if (bk >= AG_BIDDER_VALUE_LEARNING && T.drs && T.dri[a] == AG_LEARNER_POLICY) {  // the fitted policy
       policy_bid(T.drs + a * 16 + 4, est, v, in.policy_eps[(size_t)s * B + i], T.tab, g, prop);
@@ -694,7 +700,7 @@ __device__ __forceinline__ void top2_step(int s, double b, double &m1, double &m
   }
 }
 
-template <int P, int D, bool PRUNE, bool GENERAL>
+template <int P, int D, bool PRUNE, int GENERAL>
 __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const double (&x)[kMaxD],
                                         const float (&xf)[kMaxD], float xabs, const int (&ag)[P], double u,
                                         const ag_batch_in &in, uint32_t B, uint32_t i, bool ts_sample,
@@ -726,8 +732,9 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
   r.oc = bernoulli(ctr_w, u);  // src/Auction.py:65 (true CTR of the winner's item)
 }
 
-template <int P, int D, bool PRUNE, int W, bool GENERAL, int BT = kThreads>
-__global__ __launch_bounds__(BT, GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES) void k_simulate(SimParams prm) {
+template <int P, int D, bool PRUNE, int W, int GENERAL, int BT = kThreads>
+__global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
+                                 : (GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES)) void k_simulate(SimParams prm) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = prm.N, K = prm.K;
   const uint32_t B = (uint32_t)prm.B;  // SoA leading dimension (auctions in the batch)
@@ -1107,15 +1114,15 @@ typedef void (*SimKernel)(SimParams);
 // Defined per participant count P in ag_sim_p.hip (one translation unit per P, compiled
 // in parallel): the k_simulate instantiation for (D, screened search, auctions per lane).
 template <int P>
-SimKernel pick_kernel_for(int D, bool prune, int W, bool general, int bt);
-template <> SimKernel pick_kernel_for<0>(int, bool, int, bool, int);
-template <> SimKernel pick_kernel_for<1>(int, bool, int, bool, int);
-template <> SimKernel pick_kernel_for<2>(int, bool, int, bool, int);
-template <> SimKernel pick_kernel_for<3>(int, bool, int, bool, int);
-template <> SimKernel pick_kernel_for<4>(int, bool, int, bool, int);
-template <> SimKernel pick_kernel_for<5>(int, bool, int, bool, int);
-template <> SimKernel pick_kernel_for<6>(int, bool, int, bool, int);
-template <> SimKernel pick_kernel_for<7>(int, bool, int, bool, int);
-template <> SimKernel pick_kernel_for<8>(int, bool, int, bool, int);
+SimKernel pick_kernel_for(int D, bool prune, int W, int general, int bt);
+template <> SimKernel pick_kernel_for<0>(int, bool, int, int, int);
+template <> SimKernel pick_kernel_for<1>(int, bool, int, int, int);
+template <> SimKernel pick_kernel_for<2>(int, bool, int, int, int);
+template <> SimKernel pick_kernel_for<3>(int, bool, int, int, int);
+template <> SimKernel pick_kernel_for<4>(int, bool, int, int, int);
+template <> SimKernel pick_kernel_for<5>(int, bool, int, int, int);
+template <> SimKernel pick_kernel_for<6>(int, bool, int, int, int);
+template <> SimKernel pick_kernel_for<7>(int, bool, int, int, int);
+template <> SimKernel pick_kernel_for<8>(int, bool, int, int, int);
 
 }  // namespace ag

@@ -10,7 +10,7 @@
 namespace ag {
 namespace {
 
-template <int P, bool PRUNE, int W, bool G, int BT = kThreads>
+template <int P, bool PRUNE, int W, int G, int BT = kThreads>
 SimKernel pick_d(int D) {
   switch (D) {
     case 2: return k_simulate<P, 2, PRUNE, W, G, BT>;
@@ -29,36 +29,39 @@ SimKernel pick_d(int D) {
 // prune: the f32-screened item search (D <= 8, K <= 2 kMaxKPairs), W auctions per lane
 // (2 when B is even: 16-B accesses); otherwise the exact scan, one auction per lane.
 // general: populations beyond OracleAllocator + TruthfulBidder (one auction per lane), in
-// 256-lane workgroups or, screened, 1024-lane ones (bt; large populations' LDS images).
+// 256-lane workgroups or, screened, 1024-lane ones (bt; large populations' LDS images);
+// kGenTruthful (TruthfulBidders only) has its own 256-lane build, otherwise the kGenAll one.
 #if AG_P == 0
 // P = 0: the runtime-P kernel (more than kMaxP participants), one auction per lane.
 template <>
-SimKernel pick_kernel_for<0>(int D, bool prune, int W, bool general, int bt) {
+SimKernel pick_kernel_for<0>(int D, bool prune, int W, int general, int bt) {
   if (W != 1 || bt != kThreads || D > 8) return nullptr;
-  if (general) return prune ? pick_d<0, true, 1, true>(D) : pick_d<0, false, 1, true>(D);
-  return prune ? pick_d<0, true, 1, false>(D) : pick_d<0, false, 1, false>(D);
+  if (general) return prune ? pick_d<0, true, 1, kGenAll>(D) : pick_d<0, false, 1, kGenAll>(D);
+  return prune ? pick_d<0, true, 1, kGenOracle>(D) : pick_d<0, false, 1, kGenOracle>(D);
 }
 
 template <>
 OraKernel pick_oracle_for<0>(int, bool) { return nullptr; }
 #else
 template <>
-SimKernel pick_kernel_for<AG_P>(int D, bool prune, int W, bool general, int bt) {
+SimKernel pick_kernel_for<AG_P>(int D, bool prune, int W, int general, int bt) {
   constexpr int P = AG_P;
   if (general) {
     if (D > 8) return nullptr;
-    if (bt == kLargeThreads) return prune ? pick_d<P, true, 1, true, kLargeThreads>(D) : nullptr;
+    if (bt == kLargeThreads) return prune ? pick_d<P, true, 1, kGenAll, kLargeThreads>(D) : nullptr;
     if (bt != kThreads) return nullptr;
-    return prune ? pick_d<P, true, 1, true>(D) : pick_d<P, false, 1, true>(D);
+    if (general == kGenTruthful)
+      return prune ? pick_d<P, true, 1, kGenTruthful>(D) : pick_d<P, false, 1, kGenTruthful>(D);
+    return prune ? pick_d<P, true, 1, kGenAll>(D) : pick_d<P, false, 1, kGenAll>(D);
   }
   if (bt != kThreads) return nullptr;
-  if (prune) return W == 2 ? pick_d<P, true, 2, false>(D) : pick_d<P, true, 1, false>(D);
-  if (D <= 8) return pick_d<P, false, 1, false>(D);
+  if (prune) return W == 2 ? pick_d<P, true, 2, kGenOracle>(D) : pick_d<P, true, 1, kGenOracle>(D);
+  if (D <= 8) return pick_d<P, false, 1, kGenOracle>(D);
   switch (D) {
-    case 9: return k_simulate<P, 9, false, 1, false>;
-    case 11: return k_simulate<P, 11, false, 1, false>;
-    case 13: return k_simulate<P, 13, false, 1, false>;
-    case 16: return k_simulate<P, 16, false, 1, false>;
+    case 9: return k_simulate<P, 9, false, 1, kGenOracle>;
+    case 11: return k_simulate<P, 11, false, 1, kGenOracle>;
+    case 13: return k_simulate<P, 13, false, 1, kGenOracle>;
+    case 16: return k_simulate<P, 16, false, 1, kGenOracle>;
     default: return nullptr;
   }
 }

@@ -213,10 +213,13 @@ typedef enum ag_option {
   AG_OPT_SIMULATE_KERNEL = 7,     /* value: ag_sim_kernel; identical results */
   AG_OPT_SIM_BLOCKS_PER_CU = 8,   /* value: workgroups per CU of the Oracle kernel's persistent
                                      grid (0 = default 4, capped by what fits); identical results */
-  AG_OPT_SIM_BLOCK_THREADS = 9    /* value: lanes per workgroup of the general simulate kernel:
+  AG_OPT_SIM_BLOCK_THREADS = 9,   /* value: lanes per workgroup of the general simulate kernel:
                                      0 = auto (1024 when the population's LDS would keep fewer than
                                      16 waves resident per CU with 256-lane workgroups), 256 or
                                      1024; identical results */
+  AG_OPT_SIM_GENERAL_MODE = 10    /* value: 0 = auto (TruthfulBidder-only populations run the
+                                     general kernel built without the bid-shading code: fewer
+                                     VGPRs), 1 = always the full general build; identical results */
 } ag_option;
 
 typedef enum ag_sim_kernel {

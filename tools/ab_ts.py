@@ -6,6 +6,8 @@ process; outputs checked identical to the base build.
 
     python tools/ab_ts.py name1 name2 ...
     python tools/ab_ts.py bt256 bt1024     (base build, AG_OPT_SIM_BLOCK_THREADS forced)
+    python tools/ab_ts.py gm1              (base build, AG_OPT_SIM_GENERAL_MODE = 1: the full
+                                            general build for TruthfulBidder-only populations)
 """
 import os
 import sys
@@ -68,15 +70,15 @@ def main():
     paths = {"base": _lib.LIB_PATH}
     opts = {}
     for n in sys.argv[1:]:
-        if n.startswith("bt"):
+        if n.startswith("bt") or n.startswith("gm"):
             paths[n] = _lib.LIB_PATH
-            opts[n] = int(n[2:])
+            opts[n] = (_lib.OPT_SIM_BLOCK_THREADS if n.startswith("bt") else _lib.OPT_SIM_GENERAL_MODE, int(n[2:]))
         else:
             paths[n] = os.path.join(vdir, f"libauctiongym_hip_{n}.so")
 
     def apply(n, e):
         if n in opts:
-            e._check(e.L.ag_set_option(e._h, _lib.OPT_SIM_BLOCK_THREADS, opts[n]), "ag_set_option")
+            e._check(e.L.ag_set_option(e._h, opts[n][0], opts[n][1]), "ag_set_option")
         return e
     B = 1 << 20
     engs = {n: apply(n, ts_engine(p)) for n, p in paths.items()}
