@@ -468,7 +468,10 @@ __device__ __forceinline__ float ts_ctr_k(const float *w, const float (&x)[DW], 
 // the best estimate (and any item outside those bounds) are scored exactly, in increasing
 // k: the exact first argmax is always among them (its estimate is >= best * (1 - 2^-15)),
 // so the choice is the plain loop's bit for bit.
-constexpr int kTsGroup = 4;
+#ifndef AG_TS_GROUP
+#define AG_TS_GROUP 4  // items whose noise is loaded together (divides kTsScreenK)
+#endif
+constexpr int kTsGroup = AG_TS_GROUP;
 constexpr int kTsScreenK = 12;
 template <int DW>
 __device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], const float *nz, int K, int Do,

@@ -80,6 +80,8 @@ def lib():
         L.ora_ts_ctr.argtypes = [vp, vp, i32, i32, i32]
         L.ora_ts_logit.restype = ctypes.c_float
         L.ora_ts_logit.argtypes = [vp, vp, i32, i32, i32]
+        L.ora_ts_sigmoid.restype = ctypes.c_float
+        L.ora_ts_sigmoid.argtypes = [ctypes.c_float, i32, i32]
         L.ora_to_fx.restype = i64
         L.ora_to_fx.argtypes = [d]
         L.ora_gen_uniform.restype = d

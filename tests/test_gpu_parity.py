@@ -1676,6 +1676,38 @@ def test_per_call_estimate_and_bid_match_reference(gpu, oracle):
             assert bd.propensities[0] == orc["propensity"][r, s_]
 
 
+def test_per_call_lrts_estimate_matches_oracle_forward(gpu, oracle):
+    """PyTorchLogisticRegressionAllocator.estimate_CTR on the GPU against ora_ts_ctr -- the
+    reference's forward `torch.sigmoid(F.linear(x32, m [+ normal(0, 1/sqrt(q))]))`
+    (src/BidderAllocation.py:67-68, src/Models.py:28-33) as torch computes it on the golden
+    fixtures' machine (tests/test_oracle_golden.py::test_ts_forward_matches_torch pins it
+    there) -- bit for bit: item counts with and without a remainder after the sgemv's 4-row
+    blocks, the Thompson draw and the MAP forward, posteriors of several widths (q). Not
+    compared with the box's own torch: MKL's sgemv summation order depends on the host CPU
+    (this box's AMD EPYC sums in order; the Intel host that ran the reference here does not)."""
+    import torch
+    from auctiongym_amd.BidderAllocation import PyTorchLogisticRegressionAllocator
+    L = oracle.lib()
+    g = np.random.default_rng(8)
+    for K in (1, 2, 3, 5, 7, 11, 12):
+        torch.manual_seed(K)
+        al = PyTorchLogisticRegressionAllocator(None, 4, K)
+        rm = al.response_model
+        rm.q = torch.from_numpy(g.uniform(1.0, 400.0, (K, 5)).astype(np.float32))
+        for r in range(40):
+            x = np.concatenate([g.normal(0, 1, 4), [1.0]])
+            x32 = x.astype(np.float32)
+            for sample in (True, False):
+                state = torch.get_rng_state()
+                got = al.estimate_CTR(x, sample=sample)
+                torch.set_rng_state(state)
+                w = rm.m + torch.normal(mean=0.0, std=1.0 / torch.sqrt(rm.q)) if sample else rm.m
+                W = np.ascontiguousarray(w.numpy(), np.float32)
+                want = np.array([L.ora_ts_ctr(W[k].ctypes.data, x32.ctypes.data, 5, k, K) for k in range(K)],
+                                np.float32)
+                assert got.dtype == np.float32 and np.array_equal(got, want), (K, r, sample)
+
+
 def test_per_call_lrts_estimate_matches_simulate(gpu, oracle):
     """PyTorchLogisticRegressionAllocator.estimate_CTR (Thompson draw patched to the recorded
     torch.normal noise) and Agent.select_item on SP_Truthful_TS's capture: the items the
