@@ -42,8 +42,8 @@ EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params
            "ag_shading_counts", "ag_dr_update", "ag_set_bidder_modes", "ag_bidder_update",
            "ag_generate_search_grid", "ag_simulate_generated", "ag_stream_copy", "ag_estimate_ctr", "ag_bid",
            "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_replay_draw", "ag_last_error",
-           "ag_abi_version")
-ABI_VERSION = 15
+           "ag_abi_version", "ag_ts_noise_index", "ag_generate_ts_noise_compact")
+ABI_VERSION = 16
 LEARNER_UNINITIALISED, LEARNER_POLICY, LEARNER_SEARCH = 0, 1, 2
 VL_SEARCH, VL_POLICY = 0, 1
 PL_LOSSES = {"REINFORCE": 0, "REINFORCE_offpolicy": 1, "TRPO": 2, "PPO": 3}
@@ -70,7 +70,8 @@ class _Sized(ctypes.Structure):
 class AgBatchIn(_Sized):
     _fields_ = [("struct_size", ctypes.c_uint64), ("ctx", ctypes.c_void_p), ("part", ctypes.c_void_p), ("u", ctypes.c_void_p),
                 ("gamma_raw", ctypes.c_void_p), ("ts_noise", ctypes.c_void_p),
-                ("policy_eps", ctypes.c_void_p), ("gamma_grid", ctypes.c_void_p)]
+                ("policy_eps", ctypes.c_void_p), ("gamma_grid", ctypes.c_void_p),
+                ("ts_noise_index", ctypes.c_void_p)]
 
 
 class AgBatchOut(_Sized):
@@ -142,6 +143,8 @@ def load(path=None):
         "ag_bidder_update": (ctypes.c_int, [vp, ctypes.POINTER(AgShadingSamples), vp, vp, vp, i32, vp, vp, vp, vp]),
         "ag_generate_noise": (ctypes.c_int, [vp, u64, u64, i64, vp, vp, vp, vp, vp]),
         "ag_generate_search_grid": (ctypes.c_int, [vp, u64, u64, i64, vp, vp]),
+        "ag_ts_noise_index": (ctypes.c_int, [vp, i64, vp, vp, ctypes.POINTER(i64), vp]),
+        "ag_generate_ts_noise_compact": (ctypes.c_int, [vp, u64, u64, i64, vp, vp, vp, vp]),
         "ag_allocate": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, vp]),
         "ag_simulate": (ctypes.c_int, [vp, i64, ctypes.POINTER(AgBatchIn),
                                        ctypes.POINTER(AgBatchOut), vp, vp]),

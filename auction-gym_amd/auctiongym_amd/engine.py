@@ -32,7 +32,7 @@ def _stream():
 
 def _batch_in(inputs):
     return AgBatchIn(*[_ptr(inputs.get(k)).value for k in ("ctx", "part", "u", "gamma_raw", "ts_noise",
-                                                           "policy_eps", "gamma_grid")])
+                                                           "policy_eps", "gamma_grid", "ts_noise_index")])
 
 
 def require_gpu():
@@ -292,14 +292,60 @@ class AuctionEngine:
         self._check(self.L.ag_generate_search_grid(self._h, int(seed), int(first_auction), B,
                                                    _ptr(inputs["gamma_grid"]), _stream()), "ag_generate_search_grid")
 
-    def generate_noise(self, seed, first_auction, inputs):
-        """Synthetic gamma_raw / ts_noise for the participants already in inputs["part"]."""
+    def generate_noise(self, seed, first_auction, inputs, compact=False):
+        """Synthetic gamma_raw / ts_noise for the participants already in inputs["part"].
+        compact=True: the Thompson noise in the compact layout (ag_ts_noise_index) -- the same
+        values, stored for the LR-TS pairs only; inputs["ts_noise"] is reallocated to fit and
+        inputs["ts_noise_index"] set."""
         B = inputs["u"].shape[0]
+        if compact and "ts_noise" in inputs:
+            self.compact_ts_noise(seed, first_auction, inputs)
+            self._check(self.L.ag_generate_noise(self._h, int(seed), int(first_auction), B,
+                                                 _ptr(inputs["part"]), _ptr(inputs.get("gamma_raw")),
+                                                 None, _ptr(inputs.get("policy_eps")), _stream()),
+                        "ag_generate_noise")
+            return
         self._check(self.L.ag_generate_noise(self._h, int(seed), int(first_auction), B,
                                              _ptr(inputs["part"]), _ptr(inputs.get("gamma_raw")),
                                              _ptr(inputs.get("ts_noise")), _ptr(inputs.get("policy_eps")),
                                              _stream()),
                     "ag_generate_noise")
+
+    def ts_noise_index(self, part):
+        """(index int32 [P][B] dev, pairs): the compact Thompson-noise layout of `part`
+        (ag_ts_noise_index)."""
+        B = part.shape[1]
+        idx = torch.empty((self.P, B), dtype=torch.int32, device=self.device)
+        n = ctypes.c_int64()
+        self._check(self.L.ag_ts_noise_index(self._h, B, _ptr(part), _ptr(idx), ctypes.byref(n), _stream()),
+                    "ag_ts_noise_index")
+        return idx, int(n.value)
+
+    def compact_ts_noise(self, seed, first_auction, inputs):
+        """Replace inputs["ts_noise"] by the compact layout of the same synthetic draws."""
+        B = inputs["u"].shape[0]
+        idx, n = self.ts_noise_index(inputs["part"])
+        inputs.pop("ts_noise", None)
+        inputs["ts_noise_index"] = idx
+        inputs["ts_noise"] = torch.empty((max(1, (n + 63) // 64), self.K * (self.OE + 1), 64),
+                                         dtype=torch.float32, device=self.device)
+        self._check(self.L.ag_generate_ts_noise_compact(self._h, int(seed), int(first_auction), B,
+                                                        _ptr(inputs["part"]), _ptr(idx), _ptr(inputs["ts_noise"]),
+                                                        _stream()), "ag_generate_ts_noise_compact")
+        return n
+
+    @staticmethod
+    def compact_to_dense_ts_noise(compact, index, P, B):
+        """The dense tiles [P][T][K*Do][64] of a compact layout (zeros for non-LR-TS pairs)."""
+        c = compact.detach().cpu().numpy() if torch.is_tensor(compact) else np.asarray(compact)
+        ix = index.detach().cpu().numpy() if torch.is_tensor(index) else np.asarray(index)
+        KDo = c.shape[1]
+        flat = c.transpose(0, 2, 1).reshape(-1, KDo)  # pair j -> its K*Do coefficients
+        T = (B + 63) // 64
+        dense = np.zeros((P, T * 64, KDo), np.float32)
+        m = ix >= 0
+        dense[:, :B][m] = flat[ix[m]]
+        return np.ascontiguousarray(dense.reshape(P, T, 64, KDo).transpose(0, 1, 3, 2))
 
     # ---------------------------------------------------------------- per-call plugin surface
     def _dev(self, a, dtype):

@@ -203,7 +203,8 @@ __global__ __launch_bounds__(kThreads) void k_generate_noise(uint64_t seed, uint
                                                             const int32_t *akind, const int32_t *bkind,
                                                             const double *pg, const double *gs,
                                                             const float *q, double *gamma_raw,
-                                                            float *ts_noise, float *policy_eps) {
+                                                            float *ts_noise, float *policy_eps,
+                                                            const int32_t *ts_index) {
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const int64_t T = (B + 63) >> 6;  // 64-auction tiles of ts_noise
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < B;
@@ -228,8 +229,10 @@ __global__ __launch_bounds__(kThreads) void k_generate_noise(uint64_t seed, uint
         box_muller(w, z0, z1);
         policy_eps[(int64_t)s * B + i] = (float)z0;
       }
-      if (ts_noise) {
+      if (ts_noise && (!ts_index || akind[a] == AG_ALLOCATOR_LRTS)) {
         const bool lr = akind[a] == AG_ALLOCATOR_LRTS;
+        // dense tiles: pair (s, i) at s*T*64 + i; compact: the LR-TS pair's rank j
+        const int64_t pj = ts_index ? (int64_t)(uint32_t)ts_index[(int64_t)s * B + i] : s * T * 64 + i;
         for (int j = 0; j < KDo; j += 2) {
           if (lr) {
             philox(c0, c1, (uint32_t)(j >> 1), 4 + (uint32_t)s, k0, k1, w);
@@ -238,13 +241,93 @@ __global__ __launch_bounds__(kThreads) void k_generate_noise(uint64_t seed, uint
             z0 = z1 = 0.0;
           }
           const float *qa = q + (size_t)a * KDo;
-          float *row = ts_noise + (((int64_t)s * T + (i >> 6)) * KDo + j) * 64 + (i & 63);
+          float *row = ts_noise + ((pj >> 6) * KDo + j) * 64 + (pj & 63);
           row[0] = lr ? (float)z0 * (1.0f / sqrtf(qa[j])) : 0.0f;
           if (j + 1 < KDo) row[64] = lr ? (float)z1 * (1.0f / sqrtf(qa[j + 1])) : 0.0f;
         }
       }
     }
   }
+}
+
+// Compact Thompson-noise index (ag_ts_noise_index): the exclusive prefix count of LR-TS
+// pairs in (slot, auction) order over [P][B] -- three passes: per-workgroup counts, one
+// workgroup scanning the counts, per-workgroup local scans writing the ranks.
+constexpr int kScanTile = kThreads * 4;  // pairs per workgroup
+__device__ __forceinline__ int lrts_flag(const int32_t *part, const int32_t *akind, int64_t n, int64_t k) {
+  return k < n && akind[part[k]] == AG_ALLOCATOR_LRTS;
+}
+__device__ __forceinline__ int block_excl_scan(int v, int *s_w, int &total) {
+  // wave inclusive scan by DPP-free shuffles, then the waves' totals
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_w[wv] = x;
+  __syncthreads();
+  int base = 0, tot = 0;
+  for (int w = 0; w < kThreads / 64; ++w) {
+    if (w < wv) base += s_w[w];
+    tot += s_w[w];
+  }
+  __syncthreads();
+  total = tot;
+  return base + x - v;
+}
+__global__ __launch_bounds__(kThreads) void k_ts_index_count(const int32_t *part, const int32_t *akind, int64_t n,
+                                                            int64_t *counts) {
+  __shared__ int s_w[kThreads / 64];
+  const int64_t k0 = (int64_t)blockIdx.x * kScanTile + threadIdx.x * 4;
+  int v = 0;
+  for (int e = 0; e < 4; ++e) v += lrts_flag(part, akind, n, k0 + e);
+  int tot;
+  block_excl_scan(v, s_w, tot);
+  if (threadIdx.x == 0) counts[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(kThreads) void k_ts_index_offsets(int64_t *counts, int64_t nb) {
+  // one workgroup: exclusive scan of nb counts in place, counts[nb] = the total
+  __shared__ int64_t s_run;
+  if (threadIdx.x == 0) s_run = 0;
+  __syncthreads();
+  for (int64_t b0 = 0; b0 < nb; b0 += kThreads) {
+    __shared__ int64_t s_v[kThreads];
+    const int64_t b = b0 + threadIdx.x;
+    s_v[threadIdx.x] = b < nb ? counts[b] : 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {  // nb / kThreads rounds of a serial kThreads-long scan: tiny
+      int64_t r = s_run;
+      for (int t = 0; t < kThreads; ++t) {
+        const int64_t c = s_v[t];
+        s_v[t] = r;
+        r += c;
+      }
+      s_run = r;
+    }
+    __syncthreads();
+    if (b < nb) counts[b] = s_v[threadIdx.x];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) counts[nb] = s_run;
+}
+__global__ __launch_bounds__(kThreads) void k_ts_index_write(const int32_t *part, const int32_t *akind, int64_t n,
+                                                            const int64_t *offsets, int32_t *index) {
+  __shared__ int s_w[kThreads / 64];
+  const int64_t k0 = (int64_t)blockIdx.x * kScanTile + threadIdx.x * 4;
+  int f[4], v = 0;
+  for (int e = 0; e < 4; ++e) {
+    f[e] = lrts_flag(part, akind, n, k0 + e);
+    v += f[e];
+  }
+  int tot;
+  int64_t r = offsets[blockIdx.x] + block_excl_scan(v, s_w, tot);
+  for (int e = 0; e < 4; ++e)
+    if (k0 + e < n) {
+      index[k0 + e] = f[e] ? (int32_t)r : -1;
+      r += f[e];
+    }
 }
 
 // Synthetic search grids: U(0.1, 1) with 53-bit uniforms, streams 32 + slot (two per
@@ -856,7 +939,53 @@ int ag_generate_noise(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, const
   const int KDo = c->shape.num_items * (c->shape.obs_embedding_size + 1);
   hipLaunchKernelGGL(k_generate_noise, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, seed, first, B,
                      c->shape.num_participants, KDo, part, c->d_akind, c->d_bkind, c->d_pg, c->d_gs,
-                     c->d_tsq, gamma_raw, ts_noise, policy_eps);
+                     c->d_tsq, gamma_raw, ts_noise, policy_eps, (const int32_t *)nullptr);
+  AG_HIP(hipGetLastError());
+  return AG_OK;
+}
+
+int ag_ts_noise_index(ag_ctx *c, int64_t B, const int32_t *part, int32_t *index, int64_t *pairs, void *stream) {
+  if (!c || !part || !index || !pairs) return ag_set_error(AG_ERR_INVALID, "ag_ts_noise_index: null argument");
+  if (B < 0) return ag_set_error(AG_ERR_INVALID, "ag_ts_noise_index: B < 0");
+  const int64_t n = B * c->shape.num_participants;
+  if (n >= ((int64_t)1 << 31)) return ag_set_error(AG_ERR_INVALID, "ag_ts_noise_index: P * B >= 2^31");
+  *pairs = 0;
+  if (n == 0) return AG_OK;
+  AgDeviceGuard g(c->device);
+  hipStream_t st = (hipStream_t)stream;
+  if (!c->has_lrts) {  // no LR-TS agent: no pair
+    AG_HIP(hipMemsetAsync(index, 0xff, (size_t)n * sizeof(int32_t), st));
+    return AG_OK;
+  }
+  const int64_t nb = (n + kScanTile - 1) / kScanTile;
+  int64_t *counts = nullptr;
+  AG_HIP(hipMallocAsync((void **)&counts, (size_t)(nb + 1) * sizeof(int64_t), st));
+  hipLaunchKernelGGL(k_ts_index_count, dim3((unsigned)nb), dim3(kThreads), 0, st, part, c->d_akind, n, counts);
+  hipLaunchKernelGGL(k_ts_index_offsets, dim3(1), dim3(kThreads), 0, st, counts, nb);
+  hipLaunchKernelGGL(k_ts_index_write, dim3((unsigned)nb), dim3(kThreads), 0, st, part, c->d_akind, n,
+                     (const int64_t *)counts, index);
+  hipError_t e = hipGetLastError();
+  int64_t total = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&total, counts + nb, sizeof(int64_t), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  hipFreeAsync(counts, st);
+  AG_HIP(e);
+  *pairs = total;
+  return AG_OK;
+}
+
+int ag_generate_ts_noise_compact(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, const int32_t *part,
+                                 const int32_t *index, float *ts_noise, void *stream) {
+  if (!c || !part || !index || !ts_noise) return ag_set_error(AG_ERR_INVALID, "ag_generate_ts_noise_compact: null argument");
+  if (B < 0) return ag_set_error(AG_ERR_INVALID, "ag_generate_ts_noise_compact: B < 0");
+  if (B == 0) return AG_OK;
+  if (!c->lrts_loaded) return ag_set_error(AG_ERR_STATE, "ag_generate_ts_noise_compact: ag_load_lrts first");
+  AgDeviceGuard g(c->device);
+  const int grid = grid_for(B, (int64_t)1 << 40);
+  const int KDo = c->shape.num_items * (c->shape.obs_embedding_size + 1);
+  hipLaunchKernelGGL(k_generate_noise, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, seed, first, B,
+                     c->shape.num_participants, KDo, part, c->d_akind, c->d_bkind, c->d_pg, c->d_gs,
+                     c->d_tsq, (double *)nullptr, ts_noise, (float *)nullptr, index);
   AG_HIP(hipGetLastError());
   return AG_OK;
 }

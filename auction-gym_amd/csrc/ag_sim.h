@@ -652,10 +652,19 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
       // of that item is the estimate
       const int Do = T.ts_do;
       const float *m = T.tsm + (size_t)a * K * Do;
-      // tiled noise: coefficient c of auction i at ((s*T + i/64)*K*Do + c)*64 + i%64
-      const float *nz = (ts_sample && in.ts_noise)
-                            ? in.ts_noise + ((size_t)(s * ((B + 63) >> 6) + (i >> 6)) * K * Do) * 64 + (i & 63)
-                            : nullptr;
+      // tiled noise: coefficient c of auction i at ((s*T + i/64)*K*Do + c)*64 + i%64; the
+      // compact layout tiles the batch's LR-TS pairs only, pair j = ts_noise_index[s*B + i]
+      // in place of s*T*64 + i (mixed populations: no noise stored or fetched for the
+      // slots of other agents)
+      const float *nz = nullptr;
+      if (ts_sample && in.ts_noise) {
+        if (in.ts_noise_index) {
+          const uint32_t j = (uint32_t)ldg(in.ts_noise_index + (size_t)s * B + i);
+          nz = in.ts_noise + ((size_t)(j >> 6) * K * Do) * 64 + (j & 63);
+        } else {
+          nz = in.ts_noise + ((size_t)(s * ((B + 63) >> 6) + (i >> 6)) * K * Do) * 64 + (i & 63);
+        }
+      }
       // observed context (src/Auction.py:36) in a register row of width D >= Do
       float xo[D];
 #pragma unroll

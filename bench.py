@@ -283,15 +283,16 @@ POPULATIONS = {
 }
 
 
-def algorithmic_bytes_population(E, P, K, Do, ak, bk, init):
+def algorithmic_bytes_population(E, P, K, Do, ak, bk, init, compact=False):
     """Expected bytes per auction of a general population with bids from fitted policies:
     reads ctx, part, u and, per participant (uniform over agents), its Thompson noise (LR-TS),
     its rsample draw (fitted policy) or shading draw (uninitialised shading); writes winner,
     price, second price, outcome and per participant item, bid, est / true CTR, best EV,
-    gamma, propensity."""
+    gamma, propensity. compact: the Thompson noise in the compact layout, located through
+    ts_noise_index (4 B per LR-TS slot)."""
     per_slot = []
     for a in range(len(ak)):
-        b = K * Do * 4 if ak[a] == 1 else 0
+        b = K * Do * 4 + (4 if compact else 0) if ak[a] == 1 else 0  # + its ts_noise_index entry
         if bk[a] != 0:
             b += 4 if init[a] == 1 else 8
         per_slot.append(b)
@@ -399,7 +400,11 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
         eng.set_dr_state(st16, init)
     inp = eng.alloc_inputs(B)  # the fitted policies' rsample draws now
     eng.generate(1, lo, inp)
-    eng.generate_noise(1, lo, inp)
+    # mixed allocators: the Thompson noise in the compact layout (LR-TS pairs only, located
+    # through ts_noise_index); all-LR-TS populations keep the dense tiles (nothing to drop)
+    compact = bool((ak == 1).any() and (ak != 1).any())
+    eng.generate_noise(1, lo, inp, compact=compact)
+    res["ts_noise_layout"] = "compact (ts_noise_index)" if compact else "dense"
     stream = torch.cuda.current_stream()
 
     def step(ev):
@@ -413,7 +418,7 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
             allreduce_counters(cnt)
 
     elapsed, kern_ms = timed_steps(step, steps, warmup, world, stream)
-    bpa = algorithmic_bytes_population(E, P, K, Do, ak, bk, init)
+    bpa = algorithmic_bytes_population(E, P, K, Do, ak, bk, init, compact)
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tfile):

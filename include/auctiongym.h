@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define AG_ABI_VERSION 15
+#define AG_ABI_VERSION 16
 
 typedef enum ag_status {
   AG_OK = 0,
@@ -131,7 +131,7 @@ typedef struct ag_ctx ag_ctx;
 /* Replay inputs of B auctions (dev). The reference draws these from its numpy Generator
  * in the order src/Auction.py:33 (normal), :42 (choice), :65 (binomial's next_double). */
 typedef struct ag_batch_in {
-  uint64_t struct_size; /* sizeof(ag_batch_in) (ABI 15)                                   */
+  uint64_t struct_size; /* sizeof(ag_batch_in) (ABI 16)                                   */
   const double *ctx;   /* [E][B] true context without the intercept                      */
   const int32_t *part; /* [P][B] participating agent index per slot, P distinct of N     */
   const double *u;     /* [B]    uniform in [0,1) consumed by binomial(1, CTR[winner])   */
@@ -149,6 +149,12 @@ typedef struct ag_batch_in {
   const double *gamma_grid; /* [P][128][B] the rng.uniform(0.1, 1.0, 128) grid of a
                               ValueLearningBidder bidding by search (src/Bidder.py:184-186),
                               any order; NULL if none */
+  const int32_t *ts_noise_index; /* [P][B] compact Thompson-noise layout (mixed populations):
+                              NULL = ts_noise is the dense tiling above; else only the
+                              LR-TS pairs are stored, pair (s, i) being the j-th LR-TS pair
+                              of the batch in (slot, auction) order, j = ts_noise_index[s*B+i],
+                              its coefficient c at ((j/64)*K*(OE+1) + c)*64 + j%64 -- made by
+                              ag_ts_noise_index over the same part (ABI 16) */
 } ag_batch_in;
 
 /* Outputs of B auctions (dev). Any pointer may be NULL to skip that array. */
@@ -283,6 +289,20 @@ int ag_generate_search_grid(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, 
 int ag_generate_noise(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B,
                       const int32_t *part, double *gamma_raw, float *ts_noise, float *policy_eps,
                       void *stream);
+
+/* Compact Thompson-noise layout (ag_batch_in.ts_noise_index, ABI 16): index dev int32 [P][B]
+ * = the rank of each LR-TS pair (slot s, auction i) among the batch's LR-TS pairs in
+ * (s, i) order, -1 for other agents' pairs; *pairs (host) = their number, so the compact
+ * ts_noise holds ceil(pairs/64)*64*K*(OE+1) floats. The reference draws Thompson noise only
+ * for LR-TS agents (src/Models.py:30-31 via src/Agent.py:35): a mixed population then reads
+ * no noise for its other slots. Synchronises (the count comes back to the host). */
+int ag_ts_noise_index(ag_ctx *ctx, int64_t B, const int32_t *part, int32_t *index, int64_t *pairs,
+                      void *stream);
+
+/* ag_generate_noise's ts_noise in the compact layout of `index`: the same values for every
+ * LR-TS pair, nothing written for the others. */
+int ag_generate_ts_noise_compact(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B,
+                                 const int32_t *part, const int32_t *index, float *ts_noise, void *stream);
 
 /* ---- Replay-mode draws on the host (src/Auction.py:30-42, :65; src/main.py:29) -----------
  * B rounds of the reference's numpy draws in its order, without a Python round trip per

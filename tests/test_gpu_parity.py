@@ -583,6 +583,57 @@ def test_mixed_population_full_size(gpu, oracle):
     eng.close()
 
 
+@pytest.mark.parametrize("P,B,block", [(2, (1 << 20) + 37, 0), (2, 4099, 1024), (8, 1 << 18, 0), (12, 1 << 14, 0)])
+def test_compact_ts_noise_equals_dense(gpu, P, B, block):
+    """The compact Thompson-noise layout (ag_batch_in.ts_noise_index, ag_ts_noise_index,
+    ag_generate_ts_noise_compact): the index is numpy's exclusive cumsum of the LR-TS flags in
+    (slot, auction) order, the compact draws are the dense generator's values of the LR-TS
+    pairs, and every output and exact counter of ag_simulate is the same bit for bit as with
+    the dense tiles (register-array and runtime-P kernels, both block sizes, ragged B)."""
+    import torch
+    from auctiongym_amd import _lib
+    from auctiongym_amd.engine import AuctionEngine
+    N, K, E, OE = 32, 12, 5, 4
+    g = np.random.default_rng(77 + P)
+    items = np.concatenate([g.normal(0, 1, (N, K, E)), -3.0 - g.random((N, K, 1))], axis=2)
+    values = g.lognormal(0.1, 0.2, (N, K))
+    ak = np.array([1 if i % 3 else 0 for i in range(N)], np.int32)   # 2/3 LR-TS
+    bk = np.array([4 if i % 3 == 2 else 0 for i in range(N)], np.int32)
+    m = g.normal(0, 1, (N, K, OE + 1)).astype(np.float32)
+    q = (1.0 + 3.0 * g.random((N, K, OE + 1))).astype(np.float32)
+    eng = AuctionEngine(N, P, K, E, OE, 0, 1.0)
+    eng.set_agent_params(ak, bk, np.ones(N), np.full(N, 0.02))
+    eng.load_catalog(items, values)
+    eng.load_lrts(m, q, thompson_sampling=True)
+    if block:
+        eng._check(eng.L.ag_set_option(eng._h, _lib.OPT_SIM_BLOCK_THREADS, block), "ag_set_option")
+    inp = eng.alloc_inputs(B)
+    eng.generate(9, 1000, inp)
+    eng.generate_noise(9, 1000, inp)
+    out_d, cnt_d = eng.alloc_outputs(B), eng.new_counters()
+    eng.simulate(inp, out_d, cnt_d)
+    dense = inp["ts_noise"].cpu().numpy()
+    cin = {k: v for k, v in inp.items() if k != "ts_noise"}
+    n = eng.compact_ts_noise(9, 1000, cin)
+    flags = ak[inp["part"].cpu().numpy()] == 1
+    want = np.where(flags, np.cumsum(flags.ravel()).reshape(flags.shape) - 1, -1)
+    assert n == int(flags.sum())
+    assert np.array_equal(cin["ts_noise_index"].cpu().numpy(), want)
+    back = eng.compact_to_dense_ts_noise(cin["ts_noise"], cin["ts_noise_index"], P, B)
+    mask = np.broadcast_to(flags[:, :, None], (P, B, K * (OE + 1)))
+    dn = eng.untile_ts_noise(dense, B).transpose(1, 0, 2)
+    bk_ = eng.untile_ts_noise(back, B).transpose(1, 0, 2)
+    assert np.array_equal(dn[mask], bk_[mask])
+    out_c, cnt_c = eng.alloc_outputs(B), eng.new_counters()
+    eng.simulate(cin, out_c, cnt_c)
+    torch.cuda.synchronize()
+    for k in out_d:
+        assert torch.equal(out_d[k], out_c[k]) or np.array_equal(out_d[k].cpu().numpy(), out_c[k].cpu().numpy(),
+                                                                   equal_nan=True), k
+    assert torch.equal(cnt_d, cnt_c)
+    eng.close()
+
+
 @pytest.mark.parametrize("P,mech,mixed", [(9, 1, False), (16, 0, True), (40, 1, True), (12, 0, False)])
 def test_wide_participants_match_oracle(gpu, oracle, P, mech, mixed):
     """More than 8 participants per round (src/Auction.py:42 has no bound): the runtime-P

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 def test_library_loads_without_gpu_and_reports_abi():
     from auctiongym_amd import _lib
     L = _lib.load()
-    assert L.ag_abi_version() == _lib.ABI_VERSION == 15
+    assert L.ag_abi_version() == _lib.ABI_VERSION == 16
 
 
 def test_ctypes_structs_match_the_c_header(tmp_path):
