@@ -16,6 +16,9 @@ namespace ag {
 // Build knobs (A/B variants, `make variant`): AG_PREFETCH software-pipelines the next
 // tile's input loads; AG_MIN_WAVES caps VGPRs via launch bounds; AG_MAX_REPLICAS caps the
 // per-lane counter replicas (LDS per block).
+#ifndef AG_EARLY_COUNT
+#define AG_EARLY_COUNT 1  // general kernel: per-slot stores and counter terms as slots resolve
+#endif
 #ifndef AG_PREFETCH
 #define AG_PREFETCH 0
 #endif
@@ -626,6 +629,8 @@ __device__ __forceinline__ double shading_propensity(double pg, double sigma, do
 
 // One participant (slot s, agent a) of a round: its item, bid and the values its log
 // record and counters need (src/Auction.py:44-53, src/Agent.py:29-68).
+constexpr int kTsjLoad = -2;  // resolve_slot: no prefetched ts_noise_index entry
+
 struct SlotResult {
   int item;
   double val, bid, ctr, est, bev, gamma, prop;
@@ -634,7 +639,8 @@ struct SlotResult {
 template <int D, bool PRUNE, int GENERAL>
 __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const double (&x)[kMaxD],
                                                    const float (&xf)[kMaxD], float xabs, int a, int s,
-                                                   const ag_batch_in &in, uint32_t B, uint32_t i, bool ts_sample) {
+                                                   const ag_batch_in &in, uint32_t B, uint32_t i, bool ts_sample,
+                                                   int tsj = kTsjLoad) {
   // true CTRs (src/Auction.py:52-53): exact search on the true context; for an Oracle
   // agent this IS Agent.select_item (src/BidderAllocation.py:81-82)
   double c, bs;
@@ -659,7 +665,8 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
       const float *nz = nullptr;
       if (ts_sample && in.ts_noise) {
         if (in.ts_noise_index) {
-          const uint32_t j = (uint32_t)ldg(in.ts_noise_index + (size_t)s * B + i);
+          // prefetched with the tile's inputs (tsj), or loaded here
+          const uint32_t j = (uint32_t)(tsj != kTsjLoad ? tsj : ldg(in.ts_noise_index + (size_t)s * B + i));
           nz = in.ts_noise + ((size_t)(j >> 6) * K * Do) * 64 + (j & 63);
         } else {
           nz = in.ts_noise + ((size_t)(s * ((B + 63) >> 6) + (i >> 6)) * K * Do) * 64 + (i & 63);
@@ -716,14 +723,14 @@ template <int P, int D, bool PRUNE, int GENERAL>
 __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const double (&x)[kMaxD],
                                         const float (&xf)[kMaxD], float xabs, const int (&ag)[P], double u,
                                         const ag_batch_in &in, uint32_t B, uint32_t i, bool ts_sample,
-                                        Resolved<P> &r) {
+                                        const int (&tsj)[P], Resolved<P> &r) {
   double m1 = 0.0, m2 = -INFINITY;
   int w = 0;
 #pragma unroll
   for (int s = 0; s < P; ++s) {
     const int a = ag[s];
     r.ag[s] = a;
-    const SlotResult q = resolve_slot<D, PRUNE, GENERAL>(T, K, x, xf, xabs, a, s, in, B, i, ts_sample);
+    const SlotResult q = resolve_slot<D, PRUNE, GENERAL>(T, K, x, xf, xabs, a, s, in, B, i, ts_sample, tsj[s]);
     r.item[s] = q.item;
     r.val[s] = q.val;
     r.bid[s] = q.bid;
@@ -831,12 +838,23 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
   double xv[kMaxD][W];
   int pv[PA][W];
   double uv[W];
+  int jv[PA][W];  // compact ts_noise_index entries (GENERAL with ts_noise_index; else kTsjLoad)
+  const bool pre_tsj = GENERAL && !AG_PREFETCH && in.ts_noise_index && in.ts_noise && prm.ts_sample;
   auto load_tile = [&](uint32_t i) {
 #pragma unroll
     for (int e = 0; e < D - 1; ++e) ld_f64<W>(in.ctx + e * B + i, xv[e]);
 #pragma unroll
     for (int s = 0; s < P; ++s) ld_i32<W>(in.part + s * B + i, pv[s]);
     ld_f64<W>(in.u + i, uv);
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+      if (pre_tsj) {
+        ld_i32<W>(in.ts_noise_index + s * B + i, jv[s]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < W; ++q) jv[s][q] = kTsjLoad;
+      }
+    }
   };
   const uint32_t stride = gridDim.x * (BT * W);
   // Participation / win counts: a lane resolves at most kAuctionsPerReplica * R / BT
@@ -877,6 +895,44 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
       const double dd = ctr - est;
       add_nz(kSlotSqerr, to_fx(dd * dd));
       if (won) add_raw(kSlotBias, to_fx(est / ctr));
+    }
+  };
+  // count_slot in two parts (the same exact integer terms, added in another order): the
+  // terms that do not depend on the auction's winner as soon as a slot is resolved, so the
+  // slot's CTRs / best EV need not stay live while the other slots are resolved ...
+  auto count_pre = [&](int a, double ctr, double val, double est, double bev) {
+    auto add_raw = [&](int j, unsigned long long v) { atomicAdd(s_cnt + ((size_t)(j * N + a) * R + rep), v); };
+    auto add_nz = [&](int j, unsigned long long v) {
+      if (v != 0ull) add_raw(j, v);
+    };
+    const double tv = ctr * val;
+    add_raw(kSlotBestEv, to_fx(bev));
+    add_nz(kSlotAlloc, to_fx(bev - tv));
+    add_nz(kSlotEst, to_fx(est * val - tv));
+    const double dd = ctr - est;
+    add_nz(kSlotSqerr, to_fx(dd * dd));
+  };
+  // ... and the rest once the winner and price are known (tv = ctr * val, ratio = est / ctr)
+  auto count_post = [&](int a, bool won, double lp, double price, double second, double bid, double tv,
+                        double val, double ratio, int oc) {
+    auto add_raw = [&](int j, unsigned long long v) { atomicAdd(s_cnt + ((size_t)(j * N + a) * R + rep), v); };
+    auto add_nz = [&](int j, unsigned long long v) {
+      if (v != 0ull) add_raw(j, v);
+    };
+    if (won) {
+      add_nz(kSlotGross, to_fx(val * (double)oc));
+      add_raw(kSlotPaid, to_fx(price));
+      if (prm.mech == AG_FIRST_PRICE) add_nz(kSlotOverbid, to_fx(lp - second));
+      add_raw(kSlotBias, to_fx(ratio));
+    } else {
+      add_nz(kSlotUnderbid, to_fx((lp - bid) * (double)(lp < tv)));
+    }
+    if (packed) {
+      const uint64_t bit = 1ull << (8 * a);
+      n_logs_packed += bit;
+      if (won) n_won_packed += bit;
+    } else {
+      add_raw(kSlotCounts, won ? 0x100000001ull : 1ull);
     }
   };
 #if AG_PREFETCH
@@ -962,6 +1018,61 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
 #define UV uv
 #endif
 
+#if AG_EARLY_COUNT
+    if constexpr (GENERAL == kGenAll && W == 1 && P > 0) {  // A/B: +2 % on kGenTruthful (configs_1), -4 % on the mix
+      // each slot's outputs stored and its winner-independent counter terms added as soon
+      // as it is resolved; only bid, value, true EV and est / true CTR stay live per slot
+      double x[kMaxD];
+      float xf[kMaxD];
+      float xabs = 1.0f;
+#pragma unroll
+      for (int e = 0; e < D - 1; ++e) {
+        x[e] = XV[e][0];
+        xf[e] = (float)x[e];
+        xabs += fabsf(xf[e]);
+      }
+      x[D - 1] = 1.0;  // intercept (src/Auction.py:33)
+      xf[D - 1] = 1.0f;
+      xabs *= 1.001f;
+      double m1 = 0.0, m2 = -INFINITY, ctr_w = 0.0;
+      int w = 0;
+      double bidv[PA], valv[PA], tvv[PA], ratv[PA];
+#pragma unroll
+      for (int s = 0; s < P; ++s) {
+        const uint32_t o = s * B + i;
+        const int a = PV[s][0];
+        const SlotResult q = resolve_slot<D, PRUNE, GENERAL>(T, K, x, xf, xabs, a, s, in, B, i, prm.ts_sample != 0,
+                                                             AG_PREFETCH ? kTsjLoad : jv[s][0]);
+        if (out.item) stg(out.item + o, (int32_t)q.item);
+        if (out.bid) stg(out.bid + o, q.bid);
+        if (out.est_ctr) stg(out.est_ctr + o, q.est);
+        if (out.true_ctr) stg(out.true_ctr + o, q.ctr);
+        if (out.best_ev) stg(out.best_ev + o, q.bev);
+        if (out.gamma) stg(out.gamma + o, q.gamma);
+        if (out.propensity) stg(out.propensity + o, q.prop);
+        if (prm.want_counters) count_pre(a, q.ctr, q.val, q.est, q.bev);
+        bidv[s] = q.bid;
+        valv[s] = q.val;
+        tvv[s] = q.ctr * q.val;
+        ratv[s] = q.est / q.ctr;
+        top2_step(s, q.bid, m1, m2, w);
+        if (w == s) ctr_w = q.ctr;  // the current leader's true CTR
+      }
+      const double price = prm.mech == AG_FIRST_PRICE ? m1 : m2;
+      const int oc = bernoulli(ctr_w, UV[0]);  // src/Auction.py:65
+      if (out.winner) stg(out.winner + i, (int32_t)w);
+      if (out.price) stg(out.price + i, charged ? price : (double)NAN);
+      if (out.second_price) stg(out.second_price + i, charged ? m2 : (double)NAN);
+      if (out.outcome) stg(out.outcome + i, (uint8_t)oc);
+      if (prm.want_counters) {
+#pragma unroll
+        for (int s = 0; s < P; ++s)
+          count_post(PV[s][0], charged && s == w, charged ? price : 0.0, price, m2, bidv[s], tvv[s], valv[s],
+                     ratv[s], oc);
+      }
+      continue;
+    }
+#endif
     Resolved<PA> r[W];
 #pragma unroll
     for (int q = 0; q < W; ++q) {
@@ -977,11 +1088,14 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
       x[D - 1] = 1.0;  // intercept (src/Auction.py:33)
       xf[D - 1] = 1.0f;
       xabs *= 1.001f;
-      int ag[PA];
+      int ag[PA], tj[PA];
 #pragma unroll
-      for (int s = 0; s < P; ++s) ag[s] = PV[s][q];
+      for (int s = 0; s < P; ++s) {
+        ag[s] = PV[s][q];
+        tj[s] = AG_PREFETCH ? kTsjLoad : jv[s][q];
+      }
       resolve<PA, D, PRUNE, GENERAL>(T, K, prm.mech, x, xf, xabs, ag, UV[q], in, B, i + q,
-                                    prm.ts_sample != 0, r[q]);
+                                    prm.ts_sample != 0, tj, r[q]);
     }
 
     // SoA stores, W auctions per access

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""A/B timing of library builds (make variant NAME=... VFLAGS=...) on a population line of
+bench.py (configs_2..4, bids from the constructors' policies as bench's --no-update path),
+interleaved in ONE process; outputs and counters checked equal across builds.
+
+    python tools/ab_pop.py configs_4 early [more variants...]
+    AG_AB_DENSE=1: the dense Thompson-noise layout instead of the compact one.
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "auction-gym_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from auctiongym_amd import _lib  # noqa: E402
+
+
+def main():
+    key = sys.argv[1]
+    vdir = os.path.join(ROOT, "auction-gym_amd", "build", "variants")
+    paths = {"base": _lib.LIB_PATH}
+    for n in sys.argv[2:]:
+        paths[n] = os.path.join(vdir, f"libauctiongym_hip_{n}.so")
+    base_path = _lib.LIB_PATH
+    runs = {}
+    for n, p in paths.items():
+        _lib.LIB_PATH = p
+        if key == "configs_1":  # SP_Truthful_TS as bench.run_sp_ts
+            from auctiongym_amd.engine import AuctionEngine
+            items, values = bench.catalogue(bench.SP_TS)
+            N, K, D = items.shape
+            OE = bench.SP_TS["obs_embedding_size"]
+            eng = AuctionEngine(N, 2, K, D - 1, OE, _lib.SECOND_PRICE, bench.SP_TS["embedding_var"], device=0)
+            eng.set_agent_params(np.ones(N, np.int32), np.zeros(N, np.int32))
+            eng.load_catalog(items, values)
+            g = torch.Generator().manual_seed(0)
+            m = torch.empty(N, K, OE + 1)
+            for a in range(N):
+                m[a].normal_(0.0, 1.0, generator=g)
+            eng.load_lrts(m.numpy(), np.ones((N, K, OE + 1), np.float32), thompson_sampling=True)
+            B, ak = 1 << 20, np.ones(N, np.int32)
+        else:
+            eng, what, B, ak, bk, st16, dims = bench.build_population(key, 0)
+            eng.set_dr_state(st16, np.where(bk >= 2, 1, 0).astype(np.int32))
+        inp = eng.alloc_inputs(B)
+        eng.generate(1, 0, inp)
+        compact = not os.environ.get("AG_AB_DENSE") and bool((ak == 1).any() and (ak != 1).any())
+        eng.generate_noise(1, 0, inp, compact=compact)
+        out = eng.alloc_outputs(B)
+        cnt = eng.new_counters()
+        runs[n] = (eng, inp, out, cnt)
+    _lib.LIB_PATH = base_path
+    for n, (eng, inp, out, cnt) in runs.items():  # warm-up
+        for _ in range(20):
+            cnt.zero_()
+            eng.simulate(inp, out, cnt)
+    torch.cuda.synchronize()
+    ref = runs["base"]
+    for n, (eng, inp, out, cnt) in runs.items():
+        for k in out:
+            a, b = out[k].cpu().numpy(), ref[2][k].cpu().numpy()
+            assert np.array_equal(a, b, equal_nan=True), (n, k)
+        assert torch.equal(cnt, ref[3]), n
+    times = {n: [] for n in runs}
+    for rep in range(30):
+        for n, (eng, inp, out, cnt) in runs.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            cnt.zero_()
+            e0.record()
+            eng.simulate(inp, out, cnt)
+            e1.record()
+            torch.cuda.synchronize()
+            times[n].append(e0.elapsed_time(e1))
+    for n, t in times.items():
+        print(f"{key} {n}: median {np.median(t):.4f} ms  min {np.min(t):.4f} ms  (B = {runs[n][1]['u'].shape[0]}, "
+              f"outputs equal to base)", flush=True)
+
+
+if __name__ == "__main__":
+    main()

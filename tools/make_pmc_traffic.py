@@ -31,10 +31,15 @@ def main():
 
     t, n = traffic("fetch", "write")
     B = bench["config"]["auctions_per_gpu_per_step"]
-    out.update({"batch": B, "hbm_bytes_per_launch": t,
-                "source": f"profiles/{tag}_pmc_summary.json (k_oracle<2,6,false>, FETCH_SIZE*2*1024 + "
-                          f"WRITE_SIZE*1024, mean over {n} dispatches of {B} auctions)",
-                "over_algorithmic": t / (bench["roofline"]["algorithmic_bytes_per_auction"] * B)})
+    if t is None:  # no headline pass in this run (k_oracle unchanged): keep the committed one
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            prev = json.load(f)
+        out.update({k: prev[k] for k in ("batch", "hbm_bytes_per_launch", "source", "over_algorithmic")})
+    else:
+        out.update({"batch": B, "hbm_bytes_per_launch": t,
+                    "source": f"profiles/{tag}_pmc_summary.json (k_oracle<2,6,false>, FETCH_SIZE*2*1024 + "
+                              f"WRITE_SIZE*1024, mean over {n} dispatches of {B} auctions)",
+                    "over_algorithmic": t / (bench["roofline"]["algorithmic_bytes_per_auction"] * B)})
     for c in (1, 2, 3, 4):
         key = f"configs_{c}"
         t, n = traffic(f"c{c}_fetch", f"c{c}_write")
