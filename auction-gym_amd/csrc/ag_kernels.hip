@@ -820,7 +820,7 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
     if (OraKernel ok = pick_oracle(s.num_participants, D, false))
       return simulate_oracle(c, ok, B, in, out, counters_fx, (hipStream_t)stream);
   const int W = (prune && (B % 2) == 0 && c->wide && !c->general && s.num_participants <= kMaxP) ? 2 : 1;
-  const size_t lds = (size_t)prm.lds.total;
+  size_t lds = (size_t)prm.lds.total;
   if (lds > 160 * 1024)
     return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
   // Lanes per workgroup: the LDS image (catalogue, screen, LR-TS means, counter replicas) is
@@ -838,6 +838,12 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
     k = pick_kernel(s.num_participants, D, prune, W, gmode, bt);
   }
   if (!k) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: no kernel for P=%d D=%d", s.num_participants, D);
+  if (gmode == kGenAll && bt == kLargeThreads) {  // the compacted fitted-policy pass's per-wave task slots
+    add_policy_tasks(prm.lds, bt);
+    lds = (size_t)prm.lds.total;
+    if (lds > 160 * 1024)
+      return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
+  }
   hipStream_t st = (hipStream_t)stream;
   if (lds > 64 * 1024)
     AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -16,6 +16,9 @@ namespace ag {
 // Build knobs (A/B variants, `make variant`): AG_PREFETCH software-pipelines the next
 // tile's input loads; AG_MIN_WAVES caps VGPRs via launch bounds; AG_MAX_REPLICAS caps the
 // per-lane counter replicas (LDS per block).
+#ifndef AG_POLICY_COMPACT
+#define AG_POLICY_COMPACT 1  // early path: fitted-policy bids compacted across the wave's slots
+#endif
 #ifndef AG_EARLY_COUNT
 #define AG_EARLY_COUNT 1  // general kernel: per-slot stores and counter terms as slots resolve
 #endif
@@ -118,6 +121,7 @@ struct LdsLayout {
   int32_t replicas;        // per-lane counter replicas (power of 2, <= 64)
   int32_t ncnt;            // counter slots held in LDS
   int32_t ts_do;           // LR-TS model width OE + 1 (general populations)
+  int32_t pol;             // per-wave fitted-policy task slots [BT/64][64][32 B] (0: none)
 };
 
 __host__ inline int32_t align16(int64_t b) { return (int32_t)((b + 15) & ~(int64_t)15); }
@@ -178,7 +182,14 @@ __host__ inline LdsLayout make_layout(int N, int K, int D, bool counters, bool g
   L.cnt = align16(b);
   b = L.cnt + (counters ? (int64_t)R * N * L.ncnt * 8 : 0);
   L.total = align16(b);
+  L.pol = 0;
   return L;
+}
+
+// the per-wave task slots of the compacted fitted-policy pass (full general build, bt lanes)
+__host__ inline void add_policy_tasks(LdsLayout &L, int bt) {
+  L.pol = L.total;
+  L.total = align16((int64_t)L.total + (int64_t)bt * 32);
 }
 
 struct SimParams {
@@ -634,9 +645,10 @@ constexpr int kTsjLoad = -2;  // resolve_slot: no prefetched ts_noise_index entr
 struct SlotResult {
   int item;
   double val, bid, ctr, est, bev, gamma, prop;
+  bool pol;  // DEFER: a fitted-policy bid left to the caller (bid = value * est, gamma / prop NaN)
 };
 
-template <int D, bool PRUNE, int GENERAL>
+template <int D, bool PRUNE, int GENERAL, bool DEFER = false>
 __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const double (&x)[kMaxD],
                                                    const float (&xf)[kMaxD], float xabs, int a, int s,
                                                    const ag_batch_in &in, uint32_t B, uint32_t i, bool ts_sample,
@@ -683,11 +695,16 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
   }
   const double v = T.vals[a * T.values_stride + best];
   double b = v * est;  // Bidder.bid: value * estimated CTR (src/Bidder.py:35, :49, :173, ...)
+  bool pol = false;
   if constexpr (GENERAL == kGenAll) {  // kGenTruthful: every bidder is a TruthfulBidder
     const int bk = T.bkind[a];
     if (bk >= AG_BIDDER_VALUE_LEARNING && T.drs && T.dri[a] == AG_LEARNER_POLICY) {  // the fitted policy
-      policy_bid(T.drs + a * 16 + 4, est, v, in.policy_eps[(size_t)s * B + i], T.tab, g, prop);
-      b = b * g;
+      if constexpr (DEFER) {
+        pol = true;
+      } else {
+        policy_bid(T.drs + a * 16 + 4, est, v, in.policy_eps[(size_t)s * B + i], T.tab, g, prop);
+        b = b * g;
+      }
     } else if (bk == AG_BIDDER_VALUE_LEARNING && T.drs && T.dri[a] == AG_LEARNER_SEARCH) {
       g = search_gamma(T.drs + a * 16, est, v, in.gamma_grid + (size_t)s * 128 * B + i, B, T.tab);
       prop = 1.0;  // src/Bidder.py:196
@@ -703,7 +720,7 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
       b = b * g;  // bid *= gamma
     }
   }
-  return SlotResult{best, v, b, tru, est, bs, g, prop};  // bev: max_k true_CTR_k * value_k (src/Auction.py:53)
+  return SlotResult{best, v, b, tru, est, bs, g, prop, pol};  // bev: max_k true_CTR_k * value_k (src/Auction.py:53)
 }
 
 // streaming top-2 of the bids in slot order, ties -> lowest slot (src/AuctionAllocation.py:19-34)
@@ -1034,29 +1051,118 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
       x[D - 1] = 1.0;  // intercept (src/Auction.py:33)
       xf[D - 1] = 1.0f;
       xabs *= 1.001f;
+      // compacted policy bids in the 1024-lane build (large mixed populations); A/B: the
+      // 256-lane build (FP_DM_TS / FP_DR_TS, every slot a policy bidder) is 3 % faster without
+      constexpr bool kCompactPolicy = AG_POLICY_COMPACT != 0 && BT == kLargeThreads;
       double m1 = 0.0, m2 = -INFINITY, ctr_w = 0.0;
       int w = 0;
-      double bidv[PA], valv[PA], tvv[PA], ratv[PA];
+      double bidv[PA], valv[PA], tvv[PA], ratv[PA], ctrv[PA], estv[PA], gmv[PA], prv[PA];
+      int polx[PA];  // the slot's place among the wave's fitted-policy tasks (-1: none)
+      const int lane = (int)(threadIdx.x & 63);
+      const uint64_t below = (1ull << lane) - 1ull;
+      int ntask = 0, nslot = 0;
 #pragma unroll
       for (int s = 0; s < P; ++s) {
         const uint32_t o = s * B + i;
         const int a = PV[s][0];
-        const SlotResult q = resolve_slot<D, PRUNE, GENERAL>(T, K, x, xf, xabs, a, s, in, B, i, prm.ts_sample != 0,
-                                                             AG_PREFETCH ? kTsjLoad : jv[s][0]);
+        const SlotResult q = resolve_slot<D, PRUNE, GENERAL, kCompactPolicy>(
+            T, K, x, xf, xabs, a, s, in, B, i, prm.ts_sample != 0, AG_PREFETCH ? kTsjLoad : jv[s][0]);
         if (out.item) stg(out.item + o, (int32_t)q.item);
-        if (out.bid) stg(out.bid + o, q.bid);
         if (out.est_ctr) stg(out.est_ctr + o, q.est);
         if (out.true_ctr) stg(out.true_ctr + o, q.ctr);
         if (out.best_ev) stg(out.best_ev + o, q.bev);
-        if (out.gamma) stg(out.gamma + o, q.gamma);
-        if (out.propensity) stg(out.propensity + o, q.prop);
         if (prm.want_counters) count_pre(a, q.ctr, q.val, q.est, q.bev);
         bidv[s] = q.bid;
         valv[s] = q.val;
         tvv[s] = q.ctr * q.val;
         ratv[s] = q.est / q.ctr;
-        top2_step(s, q.bid, m1, m2, w);
-        if (w == s) ctr_w = q.ctr;  // the current leader's true CTR
+        ctrv[s] = q.ctr;
+        estv[s] = q.est;
+        gmv[s] = q.gamma;
+        prv[s] = q.prop;
+        const uint64_t m = __ballot(q.pol);
+        polx[s] = q.pol ? ntask + __popcll(m & below) : -1;
+        ntask += __popcll(m);
+        nslot += m != 0ull;
+      }
+      // Fitted-policy bids (src/Bidder.py:466-470) of the wave's slots, compacted: the
+      // tasks of all P slots go through this wave's LDS task slots, 64 per pass, so a wave
+      // whose slots hold t policy bidders runs ceil(t / 64) policy forwards instead of one
+      // per slot holding any. Same function, same inputs: the same bits.
+      // workers: the wave's active lanes (a ragged last tile leaves the top lanes idle),
+      // nact tasks per pass, worker k takes task slot k. Compacted only when that takes
+      // fewer passes than the slots holding tasks (a population of policy bidders only,
+      // FP_DM_TS / FP_DR_TS, has a task in every slot of every lane: each slot in place)
+      const uint64_t act = __ballot(1);
+      const int nact = __popcll(act), wrk = __popcll(act & below);
+      if (!kCompactPolicy) {
+        // policy bids were made in resolve_slot
+      } else if (ntask > 0 && (ntask + nact - 1) / nact >= nslot) {
+#pragma unroll
+        for (int s = 0; s < P; ++s) {
+          if (polx[s] >= 0) {
+            double g, pr;
+            policy_bid(T.drs + PV[s][0] * 16 + 4, estv[s], valv[s], ldg(in.policy_eps + (size_t)s * B + i), T.tab,
+                       g, pr);
+            gmv[s] = g;
+            prv[s] = pr;
+            bidv[s] = bidv[s] * g;
+          }
+        }
+      } else if (kCompactPolicy && ntask > 0) {
+        unsigned char *slots = smem + L.pol + (size_t)(threadIdx.x >> 6) * 64 * 32;
+        for (int base = 0; base < ntask; base += nact) {  // wave-uniform
+#pragma unroll
+          for (int s = 0; s < P; ++s) {
+            const int t = polx[s] - base;
+            if (polx[s] >= 0 && t >= 0 && t < nact) {
+              double *e = reinterpret_cast<double *>(slots + t * 32);
+              e[0] = estv[s];
+              e[1] = valv[s];
+              int32_t *ei = reinterpret_cast<int32_t *>(slots + t * 32 + 16);
+              ei[0] = PV[s][0];
+              reinterpret_cast<float *>(ei)[1] = ldg(in.policy_eps + (size_t)s * B + i);
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          if (wrk < ntask - base) {
+            double *e = reinterpret_cast<double *>(slots + wrk * 32);
+            const int32_t *ei = reinterpret_cast<const int32_t *>(slots + wrk * 32 + 16);
+            const int a = ei[0];
+            const float eps = reinterpret_cast<const float *>(ei)[1];
+            double g, pr;
+            policy_bid(T.drs + a * 16 + 4, e[0], e[1], eps, T.tab, g, pr);
+            e[0] = g;
+            e[1] = pr;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+          for (int s = 0; s < P; ++s) {
+            const int t = polx[s] - base;
+            if (polx[s] >= 0 && t >= 0 && t < nact) {
+              const double *e = reinterpret_cast<const double *>(slots + t * 32);
+              gmv[s] = e[0];
+              prv[s] = e[1];
+              bidv[s] = bidv[s] * e[0];  // bid *= gamma, as resolve_slot does
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < P; ++s) {
+        const uint32_t o = s * B + i;
+        if (out.bid) stg(out.bid + o, bidv[s]);
+        if (out.gamma) stg(out.gamma + o, gmv[s]);
+        if (out.propensity) stg(out.propensity + o, prv[s]);
+        top2_step(s, bidv[s], m1, m2, w);
+        if (w == s) ctr_w = ctrv[s];  // the current leader's true CTR
       }
       const double price = prm.mech == AG_FIRST_PRICE ? m1 : m2;
       const int oc = bernoulli(ctr_w, UV[0]);  // src/Auction.py:65

@@ -13,6 +13,8 @@ step() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 "$secs" 
 step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
 step bench_driver 300 python bench.py --steps 20 --warmup 5
+step ab_c4 200 python tools/ab_pop.py configs_4
+step ab_c2 200 python tools/ab_pop.py configs_2
 for c in 2 3 4; do
   step c${c}_fetch 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$GK" --output-format csv -d "$OUT/c${c}_fetch" -o run -- $(pop configs_$c)
   step c${c}_write 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$GK" --output-format csv -d "$OUT/c${c}_write" -o run -- $(pop configs_$c)
