@@ -249,6 +249,34 @@ def test_ts_noise_tiling_roundtrip():
         assert np.array_equal(AuctionEngine.untile_ts_noise(t, B), z.reshape(B, 2, 60))
 
 
+def test_compact_ts_noise_layout_host():
+    """The compact Thompson-noise layout (ag_batch_in.ts_noise_index, ABI 16): pair j = the
+    rank of an LR-TS pair in (slot, auction) order, coefficient c at ((j/64)*KDo + c)*64 + j%64;
+    compact_to_dense_ts_noise puts every pair's coefficients back at its dense tile place
+    (zeros for other agents' pairs), as the GPU test compares against the dense generator."""
+    from auctiongym_amd.engine import AuctionEngine
+    g = np.random.default_rng(1)
+    P, KDo = 3, 60
+    for B in (1, 64, 65, 300):
+        flags = g.random((P, B)) < 0.6
+        idx = np.where(flags, np.cumsum(flags.ravel()).reshape(P, B) - 1, -1).astype(np.int32)
+        n = int(flags.sum())
+        z = g.normal(size=(B, P, KDo)).astype(np.float32)  # dense draws per (auction, slot)
+        comp = np.zeros(((n + 63) // 64 * 64 * KDo,), np.float32)
+        for s in range(P):
+            for i in range(B):
+                j = idx[s, i]
+                if j >= 0:
+                    for c in range(KDo):
+                        comp[((j // 64) * KDo + c) * 64 + j % 64] = z[i, s, c]
+        comp = comp.reshape(-1, KDo, 64)
+        dense = AuctionEngine.compact_to_dense_ts_noise(comp, idx, P, B)
+        assert dense.shape == (P, (B + 63) // 64, KDo, 64)
+        back = AuctionEngine.untile_ts_noise(dense, B)  # [B][P][KDo]
+        want = np.where(flags.T[:, :, None], z, 0.0)
+        assert np.array_equal(back, want)
+
+
 @pytest.mark.parametrize("budget", [512, 2048])
 def test_torch_noise_rewind_at_every_epoch_boundary(budget):
     """Auction._TorchNoise: rewind(e) leaves torch's generator exactly e epochs of draws past
