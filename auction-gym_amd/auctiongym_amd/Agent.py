@@ -40,6 +40,7 @@ class Agent:
         self._fx = [0] * _lib.NUM_COUNTERS
         self._log_start = 0
         self._call_logs = []
+        self._kept_calls = None  # memory=M: columns of the per-call records clear_logs kept
 
     # engine plumbing --------------------------------------------------------
     def _attach(self, auction, index):
@@ -52,7 +53,17 @@ class Agent:
 
     def _get(self, name):
         self._sync()
-        return fx_to_float(self._fx[C[name]])
+        return fx_to_float(self._fx[C[name]] + self._call_terms().get(C[name], 0))
+
+    def _call_terms(self):
+        """Exact log-counter terms of the per-call records (Agent.bid outside an Auction, their
+        prices / outcomes set by charge / set_price / set_true_CTR), as the kernels add them."""
+        if not self._call_logs:
+            return {}
+        return log_counter_terms(columns_from_records(self._call_logs), True, True)
+
+    def _count(self, name):
+        return self._fx[C[name]] + self._call_terms().get(C[name], 0)
 
     # reference attributes ----------------------------------------------------
     @property
@@ -70,7 +81,8 @@ class Agent:
         self._sync()
         recs = [] if self._auction is None else self._auction._materialise_logs(self._index, self._log_start)
         kept = records_from_columns(self._kept) if self._kept is not None else []
-        return kept + recs + self._call_logs
+        kept_calls = records_from_columns(self._kept_calls) if self._kept_calls is not None else []
+        return kept + recs + kept_calls + self._call_logs
 
     # the per-call surface (src/Agent.py:29-68): one request through the GPU plugins
     def select_item(self, context):
@@ -94,6 +106,26 @@ class Agent:
             estimated_CTR=ctr, price=0.0, second_price=0.0, outcome=False, won=False))
         return b, best
 
+    def charge(self, price, second_price, outcome):
+        """src/Agent.py:70-74: the last per-call record won at `price`; utilities updated
+        (exact fixed-point terms, as the kernels add them: gross += value * outcome, paid +=
+        price)."""
+        if not self._call_logs:
+            raise IndexError("list index out of range")  # the reference's self.logs[-1]
+        rec = self._call_logs[-1]
+        rec.set_price_outcome(price, second_price, outcome, won=True)
+        g = _fx([rec.value * float(outcome)])
+        paid = _fx([price])
+        self._fx[C["gross"]] += g
+        self._fx[C["paid"]] += paid
+        self._fx[C["net"]] += g - paid
+
+    def set_price(self, price):
+        """src/Agent.py:76-77."""
+        if not self._call_logs:
+            raise IndexError("list index out of range")
+        self._call_logs[-1].set_price(price)
+
     def update(self, iteration, plot=False, figsize=(8, 5), fontsize=14):
         """src/Agent.py:79-94. Oracle / Truthful updates are no-ops (src/BidderAllocation.py:
         17-18, src/Bidder.py:21-22); every learner trains on the GPU from the device record
@@ -101,8 +133,30 @@ class Agent:
         (ag_lrts_update), EmpiricalShadedBidder (ag_empirical_update) and the learning bidders
         (ag_bidder_update) on all of its records."""
         self._sync()
-        if self._auction is not None:
+        if self._call_logs:
+            if self._auction is not None:
+                raise NotImplementedError(
+                    "Agent.update on per-call Agent.bid records of an agent that also takes part in a "
+                    "batched Auction: update one or the other")
+            self._update_call_logs(iteration, plot, figsize, fontsize)
+        elif self._auction is not None:
             self._auction._update_agent(self._index, iteration)
+
+    def _update_call_logs(self, iteration, plot, figsize, fontsize):
+        """src/Agent.py:79-94 over the per-call records (kept ones first): the allocator on the
+        won records, the bidder on all of them, through the plugins' GPU updates."""
+        recs = (records_from_columns(self._kept_calls) if self._kept_calls is not None else []) + self._call_logs
+        contexts = np.array([o.context for o in recs])
+        items = np.array([o.item for o in recs])
+        values = np.array([o.value for o in recs])
+        bids = np.array([o.bid for o in recs])
+        prices = np.array([o.price for o in recs])
+        outcomes = np.array([o.outcome for o in recs])
+        est = np.array([o.estimated_CTR for o in recs])
+        won = np.array([o.won for o in recs])
+        self.allocator.update(contexts[won], items[won], outcomes[won], iteration, plot, figsize, fontsize, self.name)
+        self.bidder.update(contexts, values, bids, prices, outcomes, est, won, iteration, plot, figsize, fontsize,
+                           self.name)
 
     def get_allocation_regret(self):
         return self._get("allocation_regret")
@@ -117,23 +171,23 @@ class Agent:
         return self._get("underbid_regret")
 
     def get_CTR_RMSE(self):
-        n = self._fx[C["n_logs"]]
+        n = self._count("n_logs")
         return math.sqrt(self._get("ctr_sqerr") / fx_to_float(n)) if n else float("nan")
 
     def get_CTR_bias(self):
         self._sync()
-        n = self._fx[C["n_won"]]
+        n = self._count("n_won")
         return self._get("ctr_bias_sum") / fx_to_float(n) if n else float("nan")
 
     def get_mean_best_expected_value(self):
         """np.mean(opp.best_expected_value for opp in logs) (src/main.py:147)."""
         self._sync()
-        n = self._fx[C["n_logs"]]
+        n = self._count("n_logs")
         return self._get("best_ev_sum") / fx_to_float(n) if n else float("nan")
 
     def num_logs(self):
         self._sync()
-        return int(round(fx_to_float(self._fx[C["n_logs"]])))
+        return int(round(fx_to_float(self._count("n_logs"))))
 
     def clear_utility(self):
         self._sync()
@@ -160,6 +214,15 @@ class Agent:
         if self._auction is not None:
             self._log_start = self._auction._log_rounds()
             self._auction._cleared_logs(self._index)
+        if self._call_logs:  # per-call records: the last M kept (src/Agent.py:124-129)
+            cols = columns_from_records(self._call_logs)
+            if self._kept_calls is not None:
+                cols = concat_columns(self._kept_calls, cols)
+            self._kept_calls = take_last(cols, self.memory) if self.memory else None
+            if self._kept_calls is not None:
+                terms = log_counter_terms(self._kept_calls, True, True)
+                for i in _LOGS:
+                    self._fx[i] += terms.get(i, 0)
         self._call_logs = []
         self.bidder.clear_logs(memory=self.memory)
 
@@ -264,6 +327,26 @@ def records_from_columns(cols):
         true_CTR=float(cols["true_ctr"][j]), estimated_CTR=float(cols["est_ctr"][j]),
         price=float(cols["price"][j]), second_price=float(cols["second_price"][j]),
         outcome=bool(cols["outcome"][j]), won=bool(cols["won"][j])) for j in range(n)]
+
+
+def columns_from_records(recs):
+    """Columns (COLUMNS) of ImpressionOpportunity records (per-call records; no gamma /
+    propensity / order: those live in the bidder's own lists)."""
+    n = len(recs)
+    if n == 0:
+        return None
+    nan = np.full(n, np.nan)
+    return {"context": np.array([np.asarray(o.context, np.float64) for o in recs]),
+            "item": np.array([o.item for o in recs], np.int64),
+            "value": np.array([o.value for o in recs], np.float64),
+            "bid": np.array([o.bid for o in recs], np.float64),
+            "best_ev": np.array([o.best_expected_value for o in recs], np.float64),
+            "true_ctr": np.array([o.true_CTR for o in recs], np.float64),
+            "est_ctr": np.array([o.estimated_CTR for o in recs], np.float64),
+            "price": np.array([o.price for o in recs], np.float64),
+            "second_price": np.array([o.second_price for o in recs], np.float64),
+            "outcome": np.array([bool(o.outcome) for o in recs]), "won": np.array([bool(o.won) for o in recs]),
+            "gamma": nan, "propensity": nan.copy(), "order": np.arange(n, dtype=np.int64)}
 
 
 def _fx(x):

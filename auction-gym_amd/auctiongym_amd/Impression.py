@@ -24,3 +24,19 @@ class ImpressionOpportunity:
     second_price: float
     outcome: bool
     won: bool
+
+    def set_true_CTR(self, best_expected_value, true_CTR):
+        """src/Impression.py:21-23."""
+        self.best_expected_value = best_expected_value
+        self.true_CTR = true_CTR
+
+    def set_price_outcome(self, price, second_price, outcome, won=True):
+        """src/Impression.py:25-29."""
+        self.price = price
+        self.second_price = second_price
+        self.outcome = outcome
+        self.won = won
+
+    def set_price(self, price):
+        """src/Impression.py:31-32."""
+        self.price = price

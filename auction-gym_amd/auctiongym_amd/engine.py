@@ -162,9 +162,12 @@ class AuctionEngine:
         self._check(self.L.ag_set_option(self._h, _lib.OPT_ITEM_SEARCH, mode), "ag_set_option")
 
     def set_simulate_kernel(self, generic):
-        """generic=True: always the general simulate kernel; False (default): the dedicated
-        Oracle kernel for OracleAllocator + TruthfulBidder populations -- identical results."""
-        mode = _lib.SIM_KERNEL_GENERIC if generic else _lib.SIM_KERNEL_AUTO
+        """generic=True: always the general simulate kernel (k_simulate); False (default): the
+        dedicated kernels (k_oracle for OracleAllocator + TruthfulBidder populations, k_ts_choice
+        + k_pop or k_pop alone for general populations of the shipped shape); "fused": k_pop
+        making its Thompson choices itself; "split": k_ts_choice then k_pop. Identical results."""
+        mode = {"fused": _lib.SIM_KERNEL_FUSED, "split": _lib.SIM_KERNEL_SPLIT}.get(generic) or (
+            _lib.SIM_KERNEL_GENERIC if generic else _lib.SIM_KERNEL_AUTO)
         self._check(self.L.ag_set_option(self._h, _lib.OPT_SIMULATE_KERNEL, mode), "ag_set_option")
 
     def set_blocks_per_cu(self, n):

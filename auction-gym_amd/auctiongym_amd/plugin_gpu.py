@@ -19,15 +19,31 @@ from . import _lib
 _ENGINES = {}
 
 
+def _drop(key):
+    e = _ENGINES.pop(key, None)
+    if e is not None:
+        try:
+            e[2].close()
+        except Exception:  # interpreter shutdown: the runtime may already be gone
+            pass
+
+
 def _engine(owner, K, E, OE):
-    """The owner's one-agent engine (created on first use; re-created if its shape changes)."""
+    """The owner's one-agent engine (created on first use; re-created if its shape changes).
+    Held by id with only a weak reference to the owner: when the plugin is collected its
+    engine (the ag_ctx with its device catalogue and learner workspaces) is closed."""
+    import weakref
+
     from .engine import AuctionEngine
     key = id(owner)
     shape = (K, E, OE)
     e = _ENGINES.get(key)
-    if e is None or e[0] is not owner or e[1] != shape:
+    if e is None or e[0]() is not owner or e[1] != shape:
+        if e is not None:
+            e[3].detach()
+            _drop(key)
         eng = AuctionEngine(1, 1, K, E, OE, _lib.SECOND_PRICE, 1.0)
-        _ENGINES[key] = (owner, shape, eng)
+        _ENGINES[key] = (weakref.ref(owner), shape, eng, weakref.finalize(owner, _drop, key))
         return eng
     return e[2]
 

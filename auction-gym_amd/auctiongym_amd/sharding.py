@@ -190,9 +190,9 @@ def _route(store, owner, group):
         if k == "count":
             continue
         lead = v.shape[:-1]
-        rows = v[..., idx]                                   # [..., m] in destination order
-        rows = rows.reshape(-1, rows.shape[-1]).t().contiguous()   # [m][fields]
-        dst = torch.empty((total, rows.shape[1]), dtype=v.dtype, device=dev)
+        width = int(np.prod(lead)) if len(lead) else 1       # explicit: m may be 0
+        rows = v[..., idx].movedim(-1, 0).reshape(idx.numel(), width).contiguous()  # [m][fields]
+        dst = torch.empty((total, width), dtype=v.dtype, device=dev)
         dist.all_to_all_single(dst, rows, output_split_sizes=rl, input_split_sizes=sl, group=group)
         merged = torch.zeros(lead + (max(total, 1),), dtype=v.dtype, device=dev)
         merged[..., :total] = dst.t().reshape(lead + (total,))

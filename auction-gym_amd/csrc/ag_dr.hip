@@ -918,6 +918,7 @@ static int dr_ws_ready(ag_ctx *c) {
 extern "C" {
 
 int ag_set_dr_state(ag_ctx *c, const float *state, const int32_t *initialised) {
+  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   if (!c || !state || !initialised) return ag_set_error(AG_ERR_INVALID, "ag_set_dr_state: null argument");
   AgDeviceGuard g(c->device);
   if (int rc = dr_ws_ready(c)) return rc;
@@ -969,6 +970,7 @@ int ag_shading_counts(ag_ctx *c, const ag_shading_samples *s, int64_t *counts, v
 int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agents, const float *noise,
                      const int64_t *noise_offsets, int32_t noise_epochs, int32_t *epochs, int32_t *status,
                      float *traces, void *stream) {
+  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   if (!c || !s || !noise_offsets) return ag_set_error(AG_ERR_INVALID, "ag_bidder_update: null argument");
   AG_CHECK_STRUCT(s, "ag_bidder_update", "ag_shading_samples");
   if (!s->ctr || !s->value || !s->propensity || !s->won || !s->order)
@@ -1199,6 +1201,7 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agen
 
 int ag_dr_update(ag_ctx *c, const ag_shading_samples *s, const float *noise, const int64_t *noise_offsets,
                  int32_t noise_epochs, int32_t *epochs, float *traces, void *stream) {
+  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   std::vector<int32_t> stat(c->shape.num_agents);
   if (int rc = ag_bidder_update(c, s, nullptr, noise, noise_offsets, noise_epochs, epochs, stat.data(), traces, stream))
     return rc;
@@ -1209,6 +1212,7 @@ int ag_dr_update(ag_ctx *c, const ag_shading_samples *s, const float *noise, con
 }
 
 int ag_set_bidder_modes(ag_ctx *c, const int32_t *modes) {
+  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   if (!c || !modes) return ag_set_error(AG_ERR_INVALID, "ag_set_bidder_modes: null argument");
   AgDeviceGuard g(c->device);
   if (int rc = dr_ws_ready(c)) return rc;

@@ -472,6 +472,7 @@ int ag_lrts_collect(ag_ctx *c, int64_t B, const ag_batch_in *in, const ag_batch_
 }
 
 int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *loss_trace, void *stream) {
+  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   if (int rc = check_store(c, s, "ag_lrts_update")) return rc;
   if (!c->has_lrts) return AG_OK;
   if (!c->lrts_loaded) return ag_set_error(AG_ERR_STATE, "ag_lrts_update: ag_load_lrts not called");

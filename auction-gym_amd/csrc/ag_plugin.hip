@@ -165,6 +165,9 @@ int ag_bid(ag_ctx *c, int32_t agent, int64_t n, const double *value, const doubl
   const bool learner = kind >= AG_BIDDER_VALUE_LEARNING;
   int32_t state = AG_LEARNER_UNINITIALISED;
   const float *model = nullptr;
+  // the learner state and shading parameters are read back after the caller's stream has
+  // drained: an ag_bidder_update / ag_set_* queued on it (even a non-blocking stream) is seen
+  if (kind != AG_BIDDER_TRUTHFUL) AG_HIP(hipStreamSynchronize((hipStream_t)stream));
   if (learner && c->dr_loaded) {
     AG_HIP(hipMemcpy(&state, c->dr.init + agent, sizeof(int32_t), hipMemcpyDeviceToHost));
     model = c->dr.state + (size_t)agent * 16;

@@ -259,6 +259,7 @@ int ag_shading_collect(ag_ctx *c, int64_t first, int64_t B, const ag_batch_in *i
 }
 
 int ag_empirical_update(ag_ctx *c, const ag_shading_samples *s, double *prev_gamma, void *stream) {
+  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   if (int rc = check_store(c, s, "ag_empirical_update")) return rc;
   const int N = c->shape.num_agents;
   AgDeviceGuard g(c->device);

@@ -370,25 +370,51 @@ __global__ __launch_bounds__(kThreads) void k_oracle(OraParams prm) {
   if (!prm.want_counters) return;
   if (packed) flush_counts();
   __syncthreads();
-  // per (agent, slot): the replicas summed as two limbs (value = lo + hi * 2^42; counts:
-  // logs in lo, wins in hi), then the block's partials in k_simulate's format
-  const unsigned long long *cnt = reinterpret_cast<const unsigned long long *>(s_cnt);
+  // per (agent, slot) pair, one thread each: its replicas summed as two limbs (value = lo +
+  // hi * 2^42; counts: logs in lo, wins in hi), written over the pair's replica-0 / -1 words
+  // (loads pipelined 8 at a time; one thread per agent looping over every slot and replica
+  // cost ~10 us per launch), then the block's partials in k_simulate's format
+  unsigned long long *cnt = reinterpret_cast<unsigned long long *>(s_cnt);
+  auto split = [&](int j, unsigned long long c, long long &l, long long &h) {
+    if (j == kOraSlotCounts) {
+      l = (long long)(c & 0xffffffffull);
+      h = (long long)(c >> 32);
+    } else {
+      l = (long long)c & kLimbMask;
+      h = (long long)c >> AG_FX_LIMB_BITS;
+    }
+  };
+  if (R >= 2) {
+    for (int pr = tid; pr < N * kOraStride; pr += kThreads) {
+      const int a = pr / kOraStride, j = pr - a * kOraStride;
+      const unsigned long long *c0 = cnt + (size_t)a * R * kOraStride + j;
+      long long sl = 0, sh = 0;
+      for (int r0 = 0; r0 < R; r0 += 8) {
+        unsigned long long v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = r0 + u < R ? c0[(size_t)(r0 + u) * kOraStride] : 0ull;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          long long l, h;
+          split(j, v[u], l, h);
+          sl += l;
+          sh += h;
+        }
+      }
+      cnt[(size_t)a * R * kOraStride + j] = (unsigned long long)sl;
+      cnt[((size_t)a * R + 1) * kOraStride + j] = (unsigned long long)sh;
+    }
+    __syncthreads();
+  }
   for (int a = tid; a < N; a += kThreads) {
     long long lo_[kOraStride], hi_[kOraStride];
     for (int j = 0; j < kOraStride; ++j) {
-      long long sl = 0, sh = 0;
-      for (int r = 0; r < R; ++r) {
-        const unsigned long long c = cnt[((size_t)a * R + r) * kOraStride + j];
-        if (j == kOraSlotCounts) {
-          sl += (long long)(c & 0xffffffffull);
-          sh += (long long)(c >> 32);
-        } else {
-          sl += (long long)c & kLimbMask;
-          sh += (long long)c >> AG_FX_LIMB_BITS;
-        }
+      if (R >= 2) {
+        lo_[j] = (long long)cnt[(size_t)a * R * kOraStride + j];
+        hi_[j] = (long long)cnt[((size_t)a * R + 1) * kOraStride + j];
+      } else {
+        split(j, cnt[(size_t)a * kOraStride + j], lo_[j], hi_[j]);
       }
-      lo_[j] = sl;
-      hi_[j] = sh;
     }
     int64_t *dst = prm.partials + ((size_t)blockIdx.x * N + a) * kC * 2;
     auto put = [&](int c, long long l, long long h) {

@@ -349,3 +349,44 @@ def test_store_overflow_raises_on_every_rank(tmp_path):
     mp.spawn(_overflow_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     for r in range(2):
         assert np.load(out + f".{r}.npy").tolist() == [1, 1, 7]
+
+
+def _empty_route_worker(rank, world, port, out_path):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "auction-gym_amd"))
+    from auctiongym_amd.sharding import owners, route_records
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cap = 6
+    res = []
+
+    def store(n):
+        st = {"key": torch.zeros(cap, dtype=torch.int32), "x": torch.zeros((5, cap), dtype=torch.float32),
+              "count": torch.tensor([n], dtype=torch.int64)}
+        st["key"][:n] = torch.arange(n, dtype=torch.int32) % 2 << 16  # agents 0, 1
+        st["x"][:, :n] = torch.arange(5 * n, dtype=torch.float32).reshape(5, n) + 100 * rank
+        return st
+
+    # (a) rank 0 holds no records; (b) every rank empty; (c) an empty owner list
+    for st, own in ((store(0 if rank == 0 else 4), owners([0, 1], world)), (store(0), owners([0, 1], world)),
+                    (store(3), {})):
+        r = route_records(st, own)
+        n = int(r["count"][0])
+        res.append(n)
+        res.append(float(r["x"][:, :n].sum()))
+    np.save(out_path + f".{rank}.npy", np.array(res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_route_records_with_empty_ranks(tmp_path):
+    """route_records when a rank sends nothing (no records, none of an owned agent, no owners,
+    every rank empty): no crash, no rank left waiting, the records that exist arrive."""
+    out = str(tmp_path / "empty")
+    mp.spawn(_empty_route_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    r0, r1 = (np.load(out + f".{r}.npy").tolist() for r in range(2))
+    # (a) rank 1's 4 records: agents 0 (owner 0) and 1 (owner 1), 2 each
+    x1 = np.arange(20, dtype=np.float32).reshape(5, 4) + 100
+    assert r0[:2] == [2, float(x1[:, 0::2].sum())] and r1[:2] == [2, float(x1[:, 1::2].sum())]
+    assert r0[2:4] == [0, 0.0] and r1[2:4] == [0, 0.0]
+    assert r0[4:] == [0, 0.0] and r1[4:] == [0, 0.0]

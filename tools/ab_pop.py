@@ -5,6 +5,8 @@ interleaved in ONE process; outputs and counters checked equal across builds.
 
     python tools/ab_pop.py configs_4 early [more variants...]
     AG_AB_DENSE=1: the dense Thompson-noise layout instead of the compact one.
+    A variant named "generic" is the base library with AG_SIM_KERNEL_GENERIC (k_simulate
+    instead of the dedicated kernels); "bt256" / "bt1024" force the workgroup size.
 """
 import os
 import sys
@@ -25,8 +27,9 @@ def main():
     key = sys.argv[1]
     vdir = os.path.join(ROOT, "auction-gym_amd", "build", "variants")
     paths = {"base": _lib.LIB_PATH}
+    special = {"generic", "fused", "split", "bt256", "bt1024"}
     for n in sys.argv[2:]:
-        paths[n] = os.path.join(vdir, f"libauctiongym_hip_{n}.so")
+        paths[n] = _lib.LIB_PATH if n in special else os.path.join(vdir, f"libauctiongym_hip_{n}.so")
     base_path = _lib.LIB_PATH
     runs = {}
     for n, p in paths.items():
@@ -48,6 +51,10 @@ def main():
         else:
             eng, what, B, ak, bk, st16, dims = bench.build_population(key, 0)
             eng.set_dr_state(st16, np.where(bk >= 2, 1, 0).astype(np.int32))
+        if n in ("generic", "fused", "split"):
+            eng.set_simulate_kernel(True if n == "generic" else n)
+        if n in ("bt256", "bt1024"):
+            eng._check(eng.L.ag_set_option(eng._h, _lib.OPT_SIM_BLOCK_THREADS, int(n[2:])), "ag_set_option")
         inp = eng.alloc_inputs(B)
         eng.generate(1, 0, inp)
         compact = not os.environ.get("AG_AB_DENSE") and bool((ak == 1).any() and (ak != 1).any())
