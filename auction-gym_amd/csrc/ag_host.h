@@ -92,6 +92,7 @@ struct ag_ctx {
   uint8_t *d_ts_item = nullptr;             // k_ts_choice -> k_pop: [P][B] LR-TS item choices
   unsigned char *d_pop_image = nullptr;     // k_pop_image -> k_pop / k_ts_choice LDS images
   bool image_dirty = true;                  // set by every entry point that changes agent state
+  unsigned *d_ticket = nullptr;             // k_pop's last-workgroup ticket (zero between launches)
   int64_t ts_item_cap = 0;
   int32_t resident_tsc = 0;                 // resident blocks of k_ts_choice
   // general populations (anything beyond OracleAllocator + TruthfulBidder)

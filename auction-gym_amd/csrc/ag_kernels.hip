@@ -529,10 +529,12 @@ int simulate_pop(ag_ctx *c, int64_t B, const ag_batch_in *in, const ag_batch_out
   const bool counters = counters_fx != nullptr;
   // workgroup size: 256 lanes while the LDS image (agent records + >= 16 counter replicas)
   // leaves 4 workgroups per CU, else 1024 lanes (one image shared by 16 waves)
-  int bt = c->block_threads;
-  PopLayout L = make_pop_layout<K, D, DO>(s.num_agents, counters, 40 * 1024);
-  if (bt == 0) bt = (L.replicas >= 16 && L.total <= 40 * 1024) ? kThreads : kLargeThreads;
-  if (bt == kLargeThreads) L = make_pop_layout<K, D, DO>(s.num_agents, counters, 150 * 1024);
+  // workgroups of 1024 lanes (one per CU: the prologue's image copy and the epilogue's replica
+  // sums amortised over 16 waves; configs_3 0.124 -> 0.115 ms, profiles/r03j_ab.log) unless
+  // AG_OPT_SIM_BLOCK_THREADS asks for 256
+  int bt = c->block_threads ? c->block_threads : kLargeThreads;
+  PopLayout L = make_pop_layout<K, D, DO>(s.num_agents, counters,
+                                          bt == kLargeThreads ? 150 * 1024 : AG_POP_LDS_BUDGET);
   if (L.total > 160 * 1024) return AG_ERR_UNSUPPORTED;
   // the split pass: k_ts_choice makes every LR-TS participant's Thompson choice into
   // c->d_ts_item, k_pop reads it. AUTO takes it for TruthfulBidder-only populations (k_pop is
@@ -620,6 +622,13 @@ int simulate_pop(ag_ctx *c, int64_t B, const ag_batch_in *in, const ag_batch_out
   prm.in = *in;
   prm.out = *out;
   prm.partials = c->d_partials;
+  // the counters are summed by the launch's last workgroup (no k_reduce_counters launch)
+  if (!c->d_ticket) {
+    AG_HIP(hipMalloc(&c->d_ticket, sizeof(unsigned)));
+    AG_HIP(hipMemset(c->d_ticket, 0, sizeof(unsigned)));
+  }
+  prm.limbs = counters_fx;
+  prm.ticket = c->d_ticket;
   const size_t lds = (size_t)L.total;
   if (lds > 64 * 1024)
     AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -646,11 +655,8 @@ int simulate_pop(ag_ctx *c, int64_t B, const ag_batch_in *in, const ag_batch_out
     prm.hi = (int32_t)hi;
     hipLaunchKernelGGL(k, dim3(grid), dim3(bt), lds, st, prm);
     AG_HIP(hipGetLastError());
-    if (counters_fx) {
-      hipLaunchKernelGGL(k_reduce_counters, dim3(nc), dim3(kThreads), 0, st, c->d_partials, grid, nc, counters_fx);
-      AG_HIP(hipGetLastError());
-    }
   }
+  (void)nc;
   return AG_OK;
 }
 
@@ -740,6 +746,7 @@ int ag_destroy(ag_ctx *c) {
   (void)hipFree(c->d_nz_zero);
   (void)hipFree(c->d_ts_item);
   (void)hipFree(c->d_pop_image);
+  (void)hipFree(c->d_ticket);
   (void)hipFree(c->d_items);
   (void)hipFree(c->d_values);
   (void)hipFree(c->d_partials);

@@ -62,6 +62,12 @@ constexpr int kPopCntStride = 11;  // qwords per (agent, replica): odd
 constexpr int kPopTabBytes = agexp::kExpTabLds * 8;
 constexpr int kPopFlush = 255;  // auctions between flushes of the 8-bit count fields
 // build knobs (A/B variants: make variant NAME=... VFLAGS=-D...)
+#ifndef AG_POP_PREFETCH
+#define AG_POP_PREFETCH 0  // k_pop: the next tile's inputs requested before this tile resolves
+#endif
+#ifndef AG_POP_LDS_BUDGET
+#define AG_POP_LDS_BUDGET 40960  // LDS per 256-lane workgroup: 4 resident per CU
+#endif
 #ifndef AG_POP_TB_WAVES
 #define AG_POP_TB_WAVES 4  // truthful-bidder populations: <= 128 VGPRs
 #endif
@@ -102,7 +108,10 @@ __host__ inline PopLayout make_pop_layout(int N, bool counters, int64_t lds_budg
   int rep = 64;  // one replica per wave lane while the LDS budget allows
   while (rep > 1 && (int64_t)L.cnt + (int64_t)N * rep * kPopCntStride * 8 > lds_budget) rep >>= 1;
   L.replicas = rep;
-  L.total = align16((int64_t)L.cnt + (counters ? (int64_t)N * rep * kPopCntStride * 8 : 0));
+  // the counter region also holds the last workgroup's [N][AG_NUM_COUNTERS][2] sums
+  int64_t cnt_bytes = (int64_t)N * rep * kPopCntStride * 8;
+  if (cnt_bytes < (int64_t)N * AG_NUM_COUNTERS * 16) cnt_bytes = (int64_t)N * AG_NUM_COUNTERS * 16;
+  L.total = align16((int64_t)L.cnt + (counters ? cnt_bytes : 0));
   return L;
 }
 
@@ -117,6 +126,8 @@ struct PopParams {
   ag_batch_in in;
   ag_batch_out out;
   int64_t *partials;  // [grid][N][AG_NUM_COUNTERS][2]
+  int64_t *limbs;     // the caller's exact counters [N][AG_NUM_COUNTERS][3] (NULL: k_reduce_counters)
+  unsigned *ticket;   // [1] zero between launches (the last workgroup resets it)
 };
 
 // ---- the LDS images of k_pop and k_ts_choice, built in global memory by k_pop_image once
@@ -432,16 +443,38 @@ __global__ __launch_bounds__(BT, MODE == kGenTruthful ? AG_POP_TB_WAVES : AG_POP
   const uint32_t T64 = (B + 63u) >> 6;
   const uint32_t stride = gridDim.x * BT;
 
+  // the next tile's inputs are in flight while this tile resolves (AG_POP_PREFETCH; a lane
+  // resolves only a few tiles per launch at the populations' batch sizes, so the first load's
+  // latency is every tile's unless the next one is requested early)
+  double xn[D - 1], un = 0.0;
+  int an[P], tn[P];
+  auto load_in = [&](uint32_t j) {
+#pragma unroll
+    for (int e = 0; e < D - 1; ++e) xn[e] = ldg(in.ctx + e * B + j);
+#pragma unroll
+    for (int s = 0; s < P; ++s) an[s] = ldg(in.part + s * B + j);
+    un = ldg(in.u + j);
+#pragma unroll
+    for (int s = 0; s < P; ++s) tn[s] = TSX ? (int)ldg(prm.ts_item + (size_t)s * B + j) : 0;
+  };
+  constexpr bool kPre = AG_POP_PREFETCH && TSX;  // the fused kernels have no registers to spare
+  if (kPre && lo + blockIdx.x * BT + tid < hi) load_in(lo + blockIdx.x * BT + tid);
+#pragma unroll 1
   for (uint32_t i = lo + blockIdx.x * BT + tid; i < hi; i += stride) {
     double x[kMaxD];
     float xf[kMaxD];
     float xabs = 1.0f;
-    int ag[P];
+    int ag[P], tsi[P];
+    if (!kPre) load_in(i);
 #pragma unroll
-    for (int e = 0; e < D - 1; ++e) x[e] = ldg(in.ctx + e * B + i);
+    for (int e = 0; e < D - 1; ++e) x[e] = xn[e];
 #pragma unroll
-    for (int s = 0; s < P; ++s) ag[s] = ldg(in.part + s * B + i);
-    const double u = ldg(in.u + i);
+    for (int s = 0; s < P; ++s) {
+      ag[s] = an[s];
+      tsi[s] = tn[s];
+    }
+    const double u = un;
+    if (kPre) load_in(i + stride < hi ? i + stride : i);  // branch-free: the last tile re-reads its own
 #pragma unroll
     for (int e = 0; e < D - 1; ++e) {
       xf[e] = (float)x[e];
@@ -549,7 +582,7 @@ __global__ __launch_bounds__(BT, MODE == kGenTruthful ? AG_POP_TB_WAVES : AG_POP
         const float *m = reinterpret_cast<const float *>(rec + R::tsm);
         int tb;
         if constexpr (TSX) {
-          tb = ldg(prm.ts_item + (size_t)s * B + i);
+          tb = tsi[s];
         } else {
         uint32_t u1 = 0xffffffffu, u2 = 0xffffffffu;
         bool bad = false;
@@ -752,6 +785,60 @@ __global__ __launch_bounds__(BT, MODE == kGenTruthful ? AG_POP_TB_WAVES : AG_POP
     put_count(AG_C_N_WON, (unsigned long long)hi_[kSlotCounts]);
     put(AG_C_PAID, lo_[kSlotPaid], hi_[kSlotPaid]);
   }
+  if (!prm.limbs) return;  // k_reduce_counters sums the partials
+  // The last workgroup to finish sums every workgroup's partials into the exact limbs
+  // (k_reduce_counters' arithmetic, without its launch): stores released at agent scope, a
+  // ticket taken with an acq_rel RMW, the last taker acquires and reads them all.
+  __threadfence();
+  __syncthreads();
+  __shared__ int s_last;
+  if (tid == 0) {
+    const unsigned t = __hip_atomic_fetch_add(prm.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = t == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const int NC = N * kC, G = gridDim.x;
+  const int nsub = BT / NC > 1 ? BT / NC : 1;
+  long long *acc = reinterpret_cast<long long *>(s_cnt);  // [NC][2], the replicas are done
+  for (int j = tid; j < 2 * NC; j += BT) acc[j] = 0;
+  __syncthreads();
+  for (int wk = tid; wk < NC * nsub; wk += BT) {
+    const int j = wk % NC, sub = wk / NC;
+    long long a0 = 0, a1 = 0;
+    for (int b0 = sub; b0 < G; b0 += 8 * nsub) {
+      long long v0[8], v1[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int b = b0 + u * nsub;
+        v0[u] = b < G ? prm.partials[((size_t)b * NC + j) * 2] : 0;
+        v1[u] = b < G ? prm.partials[((size_t)b * NC + j) * 2 + 1] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a0 += v0[u];
+        a1 += v1[u];
+      }
+    }
+    atomicAdd(reinterpret_cast<unsigned long long *>(acc + 2 * j), (unsigned long long)a0);
+    atomicAdd(reinterpret_cast<unsigned long long *>(acc + 2 * j + 1), (unsigned long long)a1);
+  }
+  __syncthreads();
+  for (int j = tid; j < NC; j += BT) {
+    int64_t *Lm = prm.limbs + (size_t)j * AG_FX_LIMBS;
+    long long l0 = Lm[0] + acc[2 * j], l1 = Lm[1] + acc[2 * j + 1], l2 = Lm[2];
+    long long c = l0 >> AG_FX_LIMB_BITS;
+    l0 &= kLimbMask;
+    l1 += c;
+    c = l1 >> AG_FX_LIMB_BITS;
+    l1 &= kLimbMask;
+    l2 += c;
+    Lm[0] = l0;
+    Lm[1] = l1;
+    Lm[2] = l2;
+  }
+  if (tid == 0) __hip_atomic_store(prm.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 typedef void (*PopKernel)(PopParams);

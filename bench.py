@@ -92,6 +92,107 @@ def cpu_model():
     return "unknown"
 
 
+def host_threads():
+    """(threads the process may run on, CPU quota of its cgroup in CPUs or None)."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return n, quota
+
+
+def _oracle():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    O.build()
+    return O
+
+
+def timed(fn, min_seconds, max_passes=40):
+    """Run fn() until min_seconds have passed (at least once); returns (passes, seconds, last)."""
+    t0 = time.perf_counter()
+    out = fn()
+    n = 1
+    while time.perf_counter() - t0 < min_seconds and n < max_passes:
+        out = fn()
+        n += 1
+    return n, time.perf_counter() - t0, out
+
+
+def cpu_baseline_population(eng, items, values, inp, out, ak, bk, st16, init, sample, threads, min_seconds=3.0):
+    """The oracle's restatement of the general-population round (oracle.simulate_pop, the C
+    build of the reference path; OpenMP over `threads`) on the first `sample` auctions of the
+    GPU's own inputs: auctions/s, and whether its outputs equal the GPU's on that sample."""
+    O = _oracle()
+    T = lambda t: np.ascontiguousarray(t[..., :sample].cpu().numpy().T)  # noqa: E731
+    B = inp["u"].shape[0]
+    N, P, K, OE = eng.N, eng.P, eng.K, eng.OE
+    m, q, _ = eng.lrts_state()
+    kw = dict(OE=OE, ts_m=m, nthreads=threads)
+    if "ts_noise" in inp:
+        tn = (eng.compact_to_dense_ts_noise(inp["ts_noise"], inp["ts_noise_index"], P, B)
+              if "ts_noise_index" in inp else inp["ts_noise"])
+        kw["ts_noise"] = np.ascontiguousarray(eng.untile_ts_noise(tn, B)[:sample].reshape(sample, P, K, OE + 1))
+    if "gamma_raw" in inp:
+        kw["gamma_raw"] = T(inp["gamma_raw"])
+    if "policy_eps" in inp:
+        kw.update(policy_eps=T(inp["policy_eps"]), dr_state=st16, dr_init=init)
+    ctx, part, u = T(inp["ctx"]), T(inp["part"]), inp["u"][:sample].cpu().numpy()
+    pg, gs = np.ones(N), np.full(N, 0.02)
+    fn = lambda: O.simulate_pop(eng.mechanism, items, values, ctx, part, u, ak, bk, pg, gs, **kw)  # noqa: E731
+    fn()  # warm
+    passes, dt, o = timed(fn, min_seconds)
+    same = all(np.array_equal(out[k][..., :sample].cpu().numpy().T if out[k].dim() == 2 else
+                              out[k][:sample].cpu().numpy(), o[k], equal_nan=True)
+               for k in ("item", "bid", "winner", "price"))
+    return sample * passes / dt, dt, passes, same
+
+
+def cpu_baseline_lrts(state, store, agent, n_max=20000):
+    """The oracle's LR-TS update restatement (oracle/ag_oracle.c ora_lrts_update: Adam,
+    ReduceLROnPlateau, early stop, Laplace q; one thread) on up to n_max of `agent`'s won
+    samples from the GPU's own store: sample-epochs per second."""
+    O = _oracle()
+    n = int(store["count"][0])
+    key = store["key"][:n].cpu().numpy().view(np.uint32)
+    sel = np.nonzero((key >> 16) == agent)[0][:n_max]
+    X = store["x"][:, :n].cpu().numpy().T[sel]
+    A, y = (key[sel] >> 1) & 0x7FFF, key[sel] & 1
+    m, q, pm = state  # the posteriors the update started from
+    t0 = time.perf_counter()
+    _, _, _, ep, _ = O.lrts_update(X, A, y, m[agent], pm[agent], q[agent], trace=False)
+    dt = time.perf_counter() - t0
+    return len(sel) * ep / dt, dt, len(sel), ep
+
+
+def cpu_baseline_bidder(store, agent, st16, kind, n_max=512):
+    """The oracle's learning-bidder update restatement (oracle/ag_oracle_dr.c: ValueLearningBidder
+    'policy' = win-rate fit + policy fit; DoublyRobustBidder = win-rate fit + imitation + DR
+    policy fit; one thread) on up to n_max of `agent`'s records from the GPU's own store:
+    record-epochs per second (epochs of every fit summed, as the GPU's figure counts them)."""
+    O = _oracle()
+    n = int(store["count"][0])
+    ag = store["agent"][:n].cpu().numpy()
+    sel = np.nonzero(ag == agent)[0][:n_max]
+    col = {k: store[k][:n].cpu().numpy()[sel] for k in ("ctr", "value", "gamma", "won", "propensity", "utility")}
+    wr, pol = st16[agent][:4], st16[agent][4:]
+    noise = O.fit_noise(0, agent, 16384, len(sel))
+    t0 = time.perf_counter()
+    if kind == "dr":
+        r = O.dr_update(col["ctr"], col["value"], col["gamma"], col["propensity"], col["won"], col["utility"],
+                        wr, pol, False, noise, trace=False)
+    else:
+        r = O.vl_update(col["ctr"], col["value"], col["gamma"], col["won"], wr, pol, True, noise, trace=False)
+    dt = time.perf_counter() - t0
+    ep = int(np.sum(r["epochs"]))
+    return len(sel) * ep / dt, dt, len(sel), [int(e) for e in r["epochs"]]
+
+
 def measured_copy_peak(nbytes=1 << 32, reps=20):
     """HBM bandwidth of a 16-B non-temporal streaming copy (ag_stream_copy) of nbytes:
     (read + write bytes) / time, HIP events on the launch stream."""
@@ -170,7 +271,13 @@ def timed_steps(step, steps, warmup, world, stream):
     return elapsed, kern_ms
 
 
-def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True):
+def gpu_record_epochs(counts, epochs, ms):
+    """Records x epochs (every fit's epochs summed) per second of a GPU update."""
+    work = sum(int(n) * int(np.sum(e)) for n, e in zip(counts, epochs))
+    return work / (ms * 1e-3)
+
+
+def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True, cpu_threads=0, P=None):
     """configs[1]: SP_Truthful_TS, 8 LR-TS truthful bidders, 1M auctions per GPU, SecondPrice.
     Inputs (contexts, participants, uniforms AND the Thompson noise z / sqrt(q) of both
     participants) generated on the GPU and resident in HBM; initial models as
@@ -182,7 +289,8 @@ def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True):
     from auctiongym_amd.sharding import allreduce_counters, shard_range
     items, values = catalogue(SP_TS)
     N, K, D = items.shape
-    E, P, OE = D - 1, SP_TS["num_participants_per_round"], SP_TS["obs_embedding_size"]
+    E, OE = D - 1, SP_TS["obs_embedding_size"]
+    P = P or SP_TS["num_participants_per_round"]
     Do = OE + 1
     dev = torch.device("cuda", local)
     eng = AuctionEngine(N, P, K, E, OE, _lib.SECOND_PRICE, SP_TS["embedding_var"], device=local)
@@ -218,18 +326,27 @@ def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True):
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tfile):
         with open(tfile) as f:
-            tj = json.load(f).get("configs_1", {})
+            tj = json.load(f).get("configs_1" if P == 2 else f"configs_1_p{P}", {})
         if tj.get("batch") == B:
             traffic = tj.get("hbm_bytes_per_launch")
     res = {"workload": "SP_Truthful_TS (configs[1]): 8 LR-TS Thompson-sampling truthful bidders, "
-                       "K=12, E=5, OE=4, P=2, SecondPrice",
+                       f"K=12, E=5, OE=4, P={P}, SecondPrice",
            "value": B * world * steps / elapsed, "unit": "auctions/s", "ms_per_step": elapsed / steps * 1e3,
            "auctions_per_gpu_per_step": B, "kernel_ms": kern_ms, "algorithmic_bytes_per_auction": bpa,
            "roofline": {"bound": "hbm", "achieved": bpa * B / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": bpa * B / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                         "traffic": traffic}}
+    if cpu_threads:
+        rate, dt, passes, same = cpu_baseline_population(eng, items, values, inp, out, np.ones(N, np.int32),
+                                                         np.zeros(N, np.int32), None, None, 1 << 15, cpu_threads)
+        res["cpu_baseline"] = {"value": rate, "unit": "auctions/s", "cores": cpu_threads, "kind": "port",
+                               "what": "build restatement: oracle.simulate_pop (oracle/ag_oracle.c, the reference "
+                                       "path's round restated in C, OpenMP) on the same inputs",
+                               "sample": f"{passes} passes over the first 32768 auctions of the step's inputs, "
+                                         f"{dt:.1f} s; outputs identical to GPU: {same}"}
     if with_update:
         from auctiongym_amd.sharding import lrts_update_agent_parallel
+        m_pre = eng.lrts_state()
         st = eng.new_lrts_samples(B)
         torch.cuda.synchronize()
         if world > 1:
@@ -251,6 +368,16 @@ def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True):
                                        + (" + won samples routed to their agent's owner rank, posteriors "
                                           "exchanged over RCCL" if world > 1 else "")
                                        + " + ag_lrts_update: Adam, ReduceLROnPlateau, early stop, Laplace q)"}
+        n_all = int(st["count"][0])
+        counts = np.bincount(st["key"][:n_all].cpu().numpy().view(np.uint32) >> 16, minlength=N)
+        res["agent_update"]["sample_epochs_per_s"] = gpu_record_epochs(counts, ep, ms)
+        if cpu_threads:
+            rate, dt, n_s, ep_s = cpu_baseline_lrts(m_pre, st, 0)
+            res["agent_update"]["cpu_baseline"] = {
+                "value": rate, "unit": "sample-epochs/s", "cores": 1, "kind": "port",
+                "what": "build restatement: oracle.lrts_update (oracle/ag_oracle.c ora_lrts_update) of agent 0",
+                "sample": f"{n_s} of agent 0's won samples from the same store, {ep_s} epochs, {dt:.1f} s",
+                "gpu_value": res["agent_update"]["sample_epochs_per_s"]}
     eng.close()
     return res
 
@@ -301,7 +428,7 @@ def algorithmic_bytes_population(E, P, K, Do, ak, bk, init, compact=False):
     return reads + writes
 
 
-def build_population(key, local):
+def build_population(key, local, P=2):
     """Engine for a BASELINE config population: catalogue as src/main.py:60-72, LR-TS posteriors
     and learning bidders' models as the reference constructors draw them (seeded torch)."""
     from auctiongym_amd import _lib
@@ -310,7 +437,7 @@ def build_population(key, local):
     cfg = _agents_cfg(groups, dict(SP_ORACLE, allocation="FirstPrice"))
     items, values = catalogue(cfg)
     N, K, D = items.shape
-    E, P, OE = D - 1, 2, 4
+    E, OE = D - 1, 4
     Do = OE + 1
     ak, bk, modes = [], [], []
     kinds = {"TruthfulBidder": 0, "ValueLearningBidder": 2, "DoublyRobustBidder": 4}
@@ -335,11 +462,11 @@ def build_population(key, local):
         st16[a] = np.concatenate([p.detach().numpy().ravel() for lin in lins for p in lin.parameters()])
     eng.set_dr_state(st16, np.zeros(N, np.int32))
     eng.set_bidder_modes(modes)
-    dims = dict(N=N, K=K, E=E, P=P, Do=Do)
+    dims = dict(N=N, K=K, E=E, P=P, Do=Do, items=items, values=values)
     return eng, what, B0, ak, bk, st16, dims
 
 
-def run_population(key, steps, warmup, world, rank, local, batch=None, with_update=True):
+def run_population(key, steps, warmup, world, rank, local, batch=None, with_update=True, cpu_threads=0, P=2):
     """A BASELINE config population on the GPU at its per-GPU shard size: iteration 0 with
     Gaussian shading (uninitialised learners), the update of every learner (LR-TS allocators
     and learning bidders, on the GPU, synthetic rsample noise; records all-gathered when N > 1)
@@ -347,8 +474,10 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
     and resident in HBM."""
     from auctiongym_amd.sharding import (allreduce_counters, bidder_update_agent_parallel,
                                          lrts_update_agent_parallel, shard_range)
-    eng, what, B0, ak, bk, st16, dims = build_population(key, local)
+    eng, what, B0, ak, bk, st16, dims = build_population(key, local, P)
     B = int(batch or B0)
+    if P != 2:
+        what = what.replace('FirstPrice', f'FirstPrice, P={P}')
     N, K, E, P, Do = (dims[k] for k in ("N", "K", "E", "P", "Do"))
     dev = torch.device("cuda", local)
     lo, _ = shard_range(B * world, rank, world)
@@ -366,6 +495,7 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
     eng.simulate(inp, out, cnt)
     torch.cuda.synchronize()
     if with_update:
+        m_pre = eng.lrts_state()
         lst = eng.new_lrts_samples(B)
         sst = eng.new_shading_samples(B * P, learning=True)
         if world > 1:
@@ -394,10 +524,33 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
                     "(ag_bidder_update: win-rate fit, imitation, policy fit; synthetic on-device rsample noise)"
                     + (f"; agent-parallel over {world} ranks: records routed to their agent's owner "
                        "(all-to-all), owners train, models exchanged (all-gather)" if world > 1 else "")}
-        _, init = eng.dr_state()
+        n_sh = int(sst["count"][0])
+        rec_counts = np.bincount(sst["agent"][:n_sh].cpu().numpy(), minlength=N)
+        res["agent_update"]["bidder_record_epochs_per_s"] = gpu_record_epochs(rec_counts[learners], ep[learners], ms[1])
+        if cpu_threads and len(learners):
+            kind = "dr" if bk[learners[0]] == 4 else "vl"
+            rate, dt, n_s, ep_s = cpu_baseline_bidder(sst, int(learners[0]), st16, kind)
+            res["agent_update"]["cpu_baseline"] = {
+                "value": rate, "unit": "record-epochs/s", "cores": 1, "kind": "port",
+                "what": f"build restatement: oracle.{kind}_update (oracle/ag_oracle_dr.c) of learner {learners[0]}",
+                "sample": f"{n_s} of its records from the same store, epochs {ep_s} (win-rate, imitation, policy), "
+                          f"{dt:.1f} s",
+                "gpu_value": res["agent_update"]["bidder_record_epochs_per_s"]}
+            lts = [a for a in range(N) if ak[a] == 1]
+            if lts:
+                rate, dt, n_s, ep_s = cpu_baseline_lrts(m_pre, lst, lts[0])
+                n_l = int(lst["count"][0])
+                lc = np.bincount(lst["key"][:n_l].cpu().numpy().view(np.uint32) >> 16, minlength=N)
+                res["agent_update"]["lrts_cpu_baseline"] = {
+                    "value": rate, "unit": "sample-epochs/s", "cores": 1, "kind": "port",
+                    "what": f"build restatement: oracle.lrts_update of agent {lts[0]}",
+                    "sample": f"{n_s} of its won samples, {ep_s} epochs, {dt:.1f} s",
+                    "gpu_value": gpu_record_epochs(lc, lep, ms[0])}
+        st_fit, init = eng.dr_state()
     else:
         init = np.where(bk >= 2, 1, 0).astype(np.int32)
         eng.set_dr_state(st16, init)
+        st_fit = st16
     inp = eng.alloc_inputs(B)  # the fitted policies' rsample draws now
     eng.generate(1, lo, inp)
     # mixed allocators: the Thompson noise in the compact layout (LR-TS pairs only, located
@@ -423,9 +576,17 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tfile):
         with open(tfile) as f:
-            tj = json.load(f).get(key, {})
+            tj = json.load(f).get(key if P == 2 else f"{key}_p{P}", {})
         if tj.get("batch") == B:
             traffic = tj.get("hbm_bytes_per_launch")
+    if cpu_threads:
+        rate, dt, passes, same = cpu_baseline_population(eng, dims["items"], dims["values"], inp, out, ak, bk, st_fit,
+                                                         init, 1 << 14, cpu_threads)
+        res["cpu_baseline"] = {"value": rate, "unit": "auctions/s", "cores": cpu_threads, "kind": "port",
+                               "what": "build restatement: oracle.simulate_pop (oracle/ag_oracle.c) on the same inputs "
+                                       "and fitted models",
+                               "sample": f"{passes} passes over the first 16384 auctions of the step's inputs, "
+                                         f"{dt:.1f} s; outputs identical to GPU: {same}"}
     res.update({"value": B * world * steps / elapsed, "unit": "auctions/s", "ms_per_step": elapsed / steps * 1e3,
                 "kernel_ms": kern_ms, "algorithmic_bytes_per_auction": bpa,
                 "roofline": {"bound": "hbm", "achieved": bpa * B / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
@@ -447,11 +608,13 @@ def main():
                          "fresh process, DESIGN.md section 6)")
     ap.add_argument("--no-generate", action="store_true", help="skip the generate-mode line")
     ap.add_argument("--cpu-sample", type=int, default=1 << 24)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu_count)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0: every CPU the process may use (affinity mask capped by the cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ts-batch", type=int, default=1 << 20, help="SP_Truthful_TS auctions per GPU per step")
     ap.add_argument("--no-ts", action="store_true", help="skip the SP_Truthful_TS (configs[1]) line")
     ap.add_argument("--no-update", action="store_true", help="skip timing the Agent.update of learners")
+    ap.add_argument("--no-p8", action="store_true", help="skip the P = 8 variants of configs_1 and configs_4")
     ap.add_argument("--no-populations", action="store_true",
                     help="skip the configs[2..4] lines (FP_DM_TS, FP_DR_TS, mixed population)")
     ap.add_argument("--populations", default=",".join(POPULATIONS),
@@ -620,17 +783,33 @@ def main():
     if gen is not None:
         result["generate_mode"] = gen
 
+    n_threads, quota = host_threads()
+    # every CPU this process may use: its affinity mask, capped by its cgroup's CPU quota (the
+    # GPU box: 256 threads, quota 16 CPUs -- 256 OpenMP threads there are throttled to 16 CPUs'
+    # worth and measured 4.8 M auctions/s against 19-22 M/s on 16, profiles/r03h_bench.log)
+    usable = min(n_threads, int(np.ceil(quota))) if quota else n_threads
+    threads = args.cpu_threads or usable
+    cpu_lines = threads if (rank == 0 and world == 1 and not args.no_cpu_baseline) else 0
     if not args.no_ts:
         result["configs_1"] = run_sp_ts(args.ts_batch, args.steps, args.warmup, world, rank, local,
-                                        with_update=not args.no_update)
+                                        with_update=not args.no_update, cpu_threads=cpu_lines)
 
     if not args.no_populations:
         for key in [k for k in args.populations.split(",") if k]:
             result[key] = run_population(key, max(5, args.steps // 5), max(5, args.warmup // 5), world, rank, local,
-                                         with_update=not args.no_update)
+                                         with_update=not args.no_update, cpu_threads=cpu_lines)
+
+    if not args.no_p8:
+        # configs_1 and configs_4 also at P = 8 participants per round (simulate only:
+        # the learners' updates are timed on the P = 2 lines)
+        if not args.no_ts:
+            result["configs_1_p8"] = run_sp_ts(args.ts_batch, args.steps, args.warmup, world, rank, local,
+                                               with_update=False, P=8)
+        if not args.no_populations and "configs_4" in args.populations.split(","):
+            result["configs_4_p8"] = run_population("configs_4", max(5, args.steps // 5), max(5, args.warmup // 5),
+                                                    world, rank, local, with_update=False, P=8)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         sample = min(args.cpu_sample, B)
         cps, dt, passes, o = cpu_baseline(items, values, inp, sample, threads)
         gpu_bid = out["bid"][:, :sample].cpu().numpy().T
@@ -645,7 +824,8 @@ def main():
                       f"outputs identical to GPU: {same}",
             "one_core": {"value": cps1, "unit": "auctions/s", "cores": 1,
                          "sample": f"{passes1} passes over {s1} auctions, 1 thread, {dt1:.1f} s"},
-            "nproc": os.cpu_count(), "threads_available": len(os.sched_getaffinity(0)),
+            "nproc": os.cpu_count(), "threads_available": n_threads, "cgroup_cpu_quota": quota,
+            "threads_used": f"{threads}: every CPU the process may use (affinity mask capped by the cgroup quota)",
             "cpu_model": cpu_model(),
             "reference_itself": "12.8k auctions/s on one core of the survey container (the reference's "
                                 "Python/numpy path, BASELINE.md section 2; it cannot run on the GPU box)"}

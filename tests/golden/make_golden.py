@@ -666,6 +666,101 @@ def learner_driver_kat(cfg_name, out_name, rounds, iters, torch_seed=0):
     np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
 
 
+def later_update_kat(cfg_name, out_name, rounds, iters, torch_seed=0):
+    """Every Agent.update of the reference's driver loop (src/main.py:113-155) on `cfg_name`
+    for `iters` iterations of `rounds` rounds, recorded at its inputs and outputs so that the
+    oracle can be run from EXACTLY the reference's state at iterations >= 1 (the verdict's
+    "pin later-iteration updates"): per iteration and agent, the LR-TS allocator's won samples
+    and posterior before / after with its per-epoch losses, and (learning bidders) the logged
+    records, the models before / after, every scheduled fit's per-epoch losses and the torch
+    generator state it started from (the DR / DM policy fit's per-epoch rsample noise)."""
+    import torch
+    import main as M
+    import BidderAllocation as BA
+    cfg = load_cfg(cfg_name, num_runs=1, num_iter=iters, rounds_per_iter=rounds)
+    path = write_cfg(cfg)
+    (rng, config, agent_configs, agents2items, agents2item_values, num_runs, max_slots,
+     E, var, OE) = M.parse_config(path)
+    os.unlink(path)
+    torch.manual_seed(torch_seed)
+    agents = M.instantiate_agents(rng, agent_configs, agents2item_values, agents2items)
+    auction, num_iter, rpi, _ = M.instantiate_auction(rng, config, agents2items, agents2item_values,
+                                                      agents, max_slots, E, var, OE)
+    recs = []
+
+    class RecRP(torch.optim.lr_scheduler.ReduceLROnPlateau):
+        def __init__(self, *a, verbose=None, **k):
+            super().__init__(*a, **k)
+            self.rec = {"rng": torch.get_rng_state().clone(), "losses": []}
+            recs.append(self.rec)
+
+        def step(self, metrics, *a, **k):
+            self.rec["losses"].append(float(metrics))
+            return super().step(metrics, *a, **k)
+
+    def params(mod):
+        return np.concatenate([p.detach().numpy().ravel() for p in mod.parameters()])
+
+    saved = torch.optim.lr_scheduler.ReduceLROnPlateau
+    torch.optim.lr_scheduler.ReduceLROnPlateau = RecRP
+    out = {"cfg": np.array(json.dumps(cfg))}
+    try:
+        for it in range(num_iter):
+            for _ in range(rpi):
+                auction.simulate_opportunity()
+            for i, a in enumerate(agents):
+                k = f"it{it}_a{i}_"
+                L = a.logs
+                won = np.array([o.won for o in L], bool)
+                out[k + "won"] = won.astype(np.int8)
+                lrts = isinstance(a.allocator, BA.PyTorchLogisticRegressionAllocator)
+                if lrts:
+                    rm = a.allocator.response_model
+                    ctx = np.array([o.context for o in L])
+                    out[k + "X"] = ctx[won]
+                    out[k + "A"] = np.array([o.item for o in L], np.int64)[won]
+                    out[k + "y"] = np.array([o.outcome for o in L], np.float64)[won]
+                    out[k + "m0"] = rm.m.detach().numpy().copy()
+                    out[k + "prevm0"] = rm.prev_iter_m.numpy().copy()
+                    out[k + "q0"] = rm.q.numpy().copy()
+                b = a.bidder
+                learner = hasattr(b, "winrate_model") or hasattr(b, "bidding_policy")
+                if learner:
+                    out[k + "est_ctr"] = np.array([o.estimated_CTR for o in L])
+                    out[k + "value"] = np.array([o.value for o in L])
+                    out[k + "price"] = np.array([o.price for o in L])
+                    out[k + "outcome"] = np.array([o.outcome for o in L], np.int8)
+                    out[k + "gamma"] = np.array([float(g) for g in b.gammas])
+                    if hasattr(b, "propensities"):
+                        out[k + "propensity"] = np.array([float(p) for p in b.propensities])
+                    out[k + "init0"] = np.array(bool(getattr(b, "model_initialised", False)))
+                    for name in ("winrate_model", "bidding_policy"):
+                        if getattr(b, name, None) is not None:
+                            out[k + name + "0"] = params(getattr(b, name))
+                recs.clear()
+                a.update(iteration=it)
+                fits = [r for r in recs]
+                if lrts:
+                    lr = fits.pop(0)
+                    out[k + "lrts_losses"] = np.array(lr["losses"])
+                    out[k + "m1"] = rm.m.detach().numpy().copy()
+                    out[k + "q1"] = rm.q.numpy().copy()
+                for j, r in enumerate(fits):
+                    out[k + f"fit{j}_losses"] = np.array(r["losses"])
+                    out[k + f"fit{j}_rng"] = r["rng"].numpy()
+                if learner:
+                    for name in ("winrate_model", "bidding_policy"):
+                        if getattr(b, name, None) is not None:
+                            out[k + name + "1"] = params(getattr(b, name))
+                a.clear_utility()
+                a.clear_logs()
+            auction.clear_revenue()
+            print(cfg_name, "iteration", it, flush=True)
+    finally:
+        torch.optim.lr_scheduler.ReduceLROnPlateau = saved
+    np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
+
+
 def search_bid_kat(out_name="search_bid_kat", rounds=1000, bids=4000):
     """ValueLearningBidder 'search' bids (src/Bidder.py:180-196) of FP_DM_Oracle's agents after
     their first update, through the reference's own bid(): per call the (value, estimated
@@ -909,12 +1004,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also run SP_Oracle as shipped (3x20x10k rounds, ~1 min)")
     ap.add_argument("--which", choices=["dm", "ips", "dr", "dmo", "search"], help="with --only learners/drivers: one config")
-    ap.add_argument("--only", choices=["empirical", "csv", "dr", "learners", "drivers", "memory"],
+    ap.add_argument("--only", choices=["empirical", "csv", "dr", "learners", "drivers", "memory", "later"],
                     help="regenerate one fixture family only")
     args = ap.parse_args()
     install_shims()
     if args.only == "memory":
         memory_driver_kat()
+        return
+    if args.only == "later":
+        later_update_kat("SP_Truthful_TS.json", "sp_ts_later_kat", rounds=2000, iters=3)
+        later_update_kat("FP_DR_TS.json", "dr_later_kat", rounds=1000, iters=3)
         return
     if args.only == "empirical":
         empirical_update_kat()

@@ -420,6 +420,12 @@ def test_integration_stub_runs_verbatim(gpu):
     assert np.array_equal(pr, d["price"])
     np.testing.assert_allclose([a.net_utility for a in auction.agents], agg["net_utility"], rtol=1e-9)
     np.testing.assert_allclose(auction.revenue, agg["revenue"], rtol=1e-9)
+    # the buffers are allocated once per batch size and reused; close() frees them with the ctx
+    bufs = list(path_.bufs)
+    path_.run_rounds(B)
+    assert [p.value for p in path_.bufs] == [p.value for p in bufs]
+    path_.close()
+    assert path_.bufs == [] and path_.ctx is None
 
 
 def test_screened_search_adversarial_catalogues(gpu, oracle):

@@ -13,4 +13,5 @@ step ab_c1 200 python tools/ab_pop.py configs_1 generic fused
 step ab_c2 200 python tools/ab_pop.py configs_2 generic split
 step ab_c3 200 python tools/ab_pop.py configs_3 generic split
 step ab_c4 200 python tools/ab_pop.py configs_4 generic split
+step bench_small 600 python bench.py --steps 10 --warmup 3 --batch 16777216 --cpu-sample 1048576
 echo "== done"
