@@ -162,10 +162,10 @@ class AuctionEngine:
         self._check(self.L.ag_set_option(self._h, _lib.OPT_ITEM_SEARCH, mode), "ag_set_option")
 
     def set_simulate_kernel(self, generic):
-        """generic=True: always the general simulate kernel (k_simulate); False (default): the
-        dedicated kernels (k_oracle for OracleAllocator + TruthfulBidder populations, k_ts_choice
-        + k_pop or k_pop alone for general populations of the shipped shape); "fused": k_pop
-        making its Thompson choices itself; "split": k_ts_choice then k_pop. Identical results."""
+        """generic=True: always the general simulate kernel (k_simulate); False (default):
+        k_oracle for OracleAllocator + TruthfulBidder populations, k_simulate for the others;
+        "fused": k_pop (general populations of the shipped shape) making its Thompson choices
+        itself; "split": k_ts_choice then k_pop. Identical results."""
         mode = {"fused": _lib.SIM_KERNEL_FUSED, "split": _lib.SIM_KERNEL_SPLIT}.get(generic) or (
             _lib.SIM_KERNEL_GENERIC if generic else _lib.SIM_KERNEL_AUTO)
         self._check(self.L.ag_set_option(self._h, _lib.OPT_SIMULATE_KERNEL, mode), "ag_set_option")

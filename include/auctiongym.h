@@ -233,13 +233,11 @@ typedef enum ag_sim_kernel {
                                values lie in (0, 1024): the dedicated Oracle kernel; else the
                                general one */
   AG_SIM_KERNEL_GENERIC = 1, /* always the general simulate kernel (A/B and parity tests) */
-  AG_SIM_KERNEL_FUSED = 2,   /* general populations of the shipped shape: the dedicated kernel
-                                k_pop making its Thompson choices itself (AUTO's choice when
-                                any bidder shades: the policy / shading FP64 work overlaps the
-                                noise loads) */
-  AG_SIM_KERNEL_SPLIT = 3    /* ... the split pass, k_ts_choice then k_pop (AUTO's choice for
-                                TruthfulBidder-only populations: the noise streams at high
-                                occupancy); both: A/B and parity tests, identical results */
+  AG_SIM_KERNEL_FUSED = 2,   /* general populations of the shipped shape (K = 12, E = 5, OE = 4):
+                                the dedicated kernel k_pop making its Thompson choices itself */
+  AG_SIM_KERNEL_SPLIT = 3    /* ... the split pass, k_ts_choice then k_pop. FUSED / SPLIT are
+                                A/B and parity variants (identical results); AUTO runs the
+                                general kernel, faster on every population line measured */
 } ag_sim_kernel;
 
 typedef enum ag_item_search {
