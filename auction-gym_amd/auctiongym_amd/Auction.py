@@ -26,7 +26,7 @@ import torch
 from . import Agent as _agent_mod
 from . import _lib
 from .engine import AuctionEngine
-from .replay import draw_round, draw_round_population, draw_rounds_native
+from .replay import draw_round, draw_round_population, draw_rounds_native, draw_rounds_native_population
 
 C = _agent_mod.C
 
@@ -83,6 +83,7 @@ class Auction:
         eng.load_catalog(np.stack([np.asarray(agent2items[a.name], np.float64)
                                    for a in agents]), self._values)
         self._ts = False
+        self._ts_agent = np.zeros(len(agents), bool)
         if self._lrts.any():
             lr = [a.allocator for a in agents if a.allocator.kind == _lib.ALLOCATOR_LRTS]
             for al in lr:
@@ -91,10 +92,13 @@ class Auction:
                         f"PyTorchLogisticRegressionAllocator(embedding_size={al.embedding_size}, "
                         f"num_items={al.num_items}) must model the observed context "
                         f"(obs_embedding_size={obs_embedding_size}) and the K={K} items")
-            ts = {bool(al.thompson_sampling) for al in lr}
-            if len(ts) != 1:
-                raise NotImplementedError("LR-TS agents must all sample or all not sample")
-            self._ts = ts.pop()
+            # thompson_sampling is per allocator (src/BidderAllocation.py:24-26, :67-68): the
+            # kernel runs in sampling mode when any LR-TS agent samples; an agent that does not
+            # sample gets zero noise, so its "sampled" CTRs are its MAP CTRs (m + 0 = m) and it
+            # bids exactly as the reference's sample=False forward (src/Agent.py:29-42)
+            self._ts_agent = np.array([bool(self._lrts[i] and a.allocator.thompson_sampling)
+                                       for i, a in enumerate(agents)])
+            self._ts = bool(self._ts_agent.any())
             self._load_lrts()
         self._learning = np.isin(bk, (_lib.BIDDER_VALUE_LEARNING, _lib.BIDDER_POLICY_LEARNING,
                                       _lib.BIDDER_DOUBLY_ROBUST))
@@ -154,15 +158,7 @@ class Auction:
                                       self.max_slots)
             self._pending.append((ctx, part, u, None, None, None, None))
             return
-        shading = [(a.bidder.prev_gamma, a.bidder.gamma_sigma) if self._shading[i] else None
-                   for i, a in enumerate(self.agents)]
-        models = [a.allocator.response_model if (self._lrts[i] and self._ts) else None
-                  for i, a in enumerate(self.agents)]
-        policy = search = None
-        if self._learning.any():
-            ls = [a.bidder._learner_state() if self._learning[i] else 0 for i, a in enumerate(self.agents)]
-            policy = [x == _lib.LEARNER_POLICY for x in ls]
-            search = [x == _lib.LEARNER_SEARCH for x in ls]
+        shading, models, policy, search = self._population_draws()
         ctx, part, g, u, noise, eps, grid = draw_round_population(
             self.rng, N, P, self.embedding_size, self.embedding_var, shading, models, self.max_slots,
             policy, search)
@@ -177,47 +173,71 @@ class Auction:
         if len(self._pending) >= self._flush_limit():
             self._flush()
 
-    def _native_draws(self):
-        """True when every draw of a round comes from the numpy generator (no torch Thompson
-        or rsample draws, no search grids): then ag_replay_draw makes them in C."""
-        if self._lrts.any() and self._ts:
-            return False
+    def _population_draws(self):
+        """Per agent: shading (prev_gamma, gamma_sigma) or None, the LR-TS model making a
+        Thompson draw or None, and the learning bidders' policy / search flags (None: no such
+        bidder) -- what draw_round_population takes; fixed between updates."""
+        shading = [(a.bidder.prev_gamma, a.bidder.gamma_sigma) if self._shading[i] else None
+                   for i, a in enumerate(self.agents)]
+        models = [a.allocator.response_model if self._ts_agent[i] else None for i, a in enumerate(self.agents)]
+        policy = search = None
         if self._learning.any():
-            for i, a in enumerate(self.agents):
-                if self._learning[i] and a.bidder._learner_state() != _lib.LEARNER_UNINITIALISED:
-                    return False
+            ls = [a.bidder._learner_state() if self._learning[i] else 0 for i, a in enumerate(self.agents)]
+            policy = [x == _lib.LEARNER_POLICY for x in ls]
+            search = [x == _lib.LEARNER_SEARCH for x in ls]
+        return shading, models, policy, search
+
+    def _native_draws(self):
+        """True when the draws can be made in C for a whole batch: numpy's Generator on PCG64
+        (ag_replay_draw / ag_replay_draw_population restate it, and torch's CPU generator for
+        the Thompson and rsample draws)."""
         return isinstance(self.rng.bit_generator, np.random.PCG64)
 
+    NATIVE_ROUNDS = 1 << 20
+    NATIVE_ROUNDS_TS = 1 << 18  # Thompson noise: P * K*(OE+1) floats per round on the host
+
     def simulate_batch(self, B):
-        """B rounds with the reference's draws, run as one batch. Draws that all come from
-        the numpy generator are made in C for the whole batch (replay.draw_rounds_native:
-        the same numbers and generator state as the per-round loop)."""
+        """B rounds with the reference's draws, run as one batch. With numpy's PCG64 generator
+        every draw is made in C for the whole batch (replay.draw_rounds_native /
+        draw_rounds_native_population: the same numbers and the same numpy and torch generator
+        states afterwards as the per-round loop); otherwise the per-round Python loop."""
         B = int(B)
-        if self._native_draws():
+        if not self._native_draws():
+            for _ in range(B):
+                self._draw_round()
+                if len(self._pending) >= self._flush_limit():
+                    self._flush()
             self._flush()
-            N, P = len(self.agents), self.num_participants_per_round
-            shading = None
-            if self._shading.any():
-                shading = [(a.bidder.prev_gamma, a.bidder.gamma_sigma) if self._shading[i] else None
-                           for i, a in enumerate(self.agents)]
-            for lo in range(0, B, self.FLUSH_ROUNDS):
-                n = min(self.FLUSH_ROUNDS, B - lo)
-                ctx, part, u, g = draw_rounds_native(self.rng, n, N, P, self.embedding_size, self.embedding_var,
-                                                     self.max_slots, shading)
-                d = self._engine.device
-                inp = {"ctx": torch.from_numpy(ctx).to(d), "part": torch.from_numpy(part).to(d),
-                       "u": torch.from_numpy(u).to(d)}
-                if self._shading.any():
-                    inp["gamma_raw"] = torch.from_numpy(g).to(d)
-                if self._learning.any():
-                    inp["policy_eps"] = torch.zeros((P, n), dtype=torch.float32, device=d)
-                self._run(inp)
             return
-        for _ in range(B):
-            self._draw_round()
-            if len(self._pending) >= self._flush_limit():
-                self._flush()
         self._flush()
+        N, P = len(self.agents), self.num_participants_per_round
+        shading, models, policy, search = self._population_draws()
+        torch_or_grid = (any(m is not None for m in models) or (policy is not None and any(policy))
+                         or (search is not None and any(search)))
+        step = self.NATIVE_ROUNDS_TS if (self._lrts.any() and self._ts) else self.NATIVE_ROUNDS
+        d = self._engine.device
+        for lo in range(0, B, step):
+            n = min(step, B - lo)
+            if torch_or_grid:
+                ctx, part, g, u, noise, eps, grid = draw_rounds_native_population(
+                    self.rng, n, N, P, self.embedding_size, self.embedding_var,
+                    shading if self._shading.any() else None, models, self.max_slots, policy, search)
+            else:
+                ctx, part, u, g = draw_rounds_native(self.rng, n, N, P, self.embedding_size, self.embedding_var,
+                                                     self.max_slots, shading if self._shading.any() else None)
+                noise = eps = grid = None
+            inp = {"ctx": torch.from_numpy(ctx).to(d), "part": torch.from_numpy(part).to(d),
+                   "u": torch.from_numpy(u).to(d)}
+            if self._shading.any():
+                inp["gamma_raw"] = torch.from_numpy(g).to(d)
+            if self._learning.any():
+                inp["policy_eps"] = (torch.from_numpy(eps).to(d) if eps is not None else
+                                     torch.zeros((P, n), dtype=torch.float32, device=d))
+                if grid is not None:
+                    inp["gamma_grid"] = torch.from_numpy(grid).to(d)
+            if self._lrts.any() and self._ts:
+                inp["ts_noise"] = torch.from_numpy(noise).to(d)
+            self._run(inp)
 
     def simulate_synthetic(self, B, seed, first_auction=0):
         """B rounds with on-device Philox inputs (throughput mode; parity via the oracle)."""
@@ -227,6 +247,13 @@ class Auction:
         eng.generate(seed, first_auction, inp)
         if "gamma_raw" in inp or "ts_noise" in inp:
             eng.generate_noise(seed, first_auction, inp)
+        if "ts_noise" in inp and not self._ts_agent[self._lrts].all():
+            # LR-TS agents that do not sample: zero noise in their slots ([P][T][K*Do][64] tiles)
+            P, T = inp["ts_noise"].shape[0], inp["ts_noise"].shape[1]
+            keep = torch.from_numpy(self._ts_agent).to(eng.device)[inp["part"].long()]  # [P][B]
+            pad = torch.zeros((P, T * 64), dtype=torch.bool, device=eng.device)
+            pad[:, :int(B)] = keep
+            inp["ts_noise"].mul_(pad.view(P, T, 1, 64).to(inp["ts_noise"].dtype))
         if "gamma_grid" in inp:
             eng.generate_search_grid(seed, first_auction, inp)
         self._run(inp)

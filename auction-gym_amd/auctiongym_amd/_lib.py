@@ -41,7 +41,8 @@ EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params
            "ag_shading_collect", "ag_empirical_update", "ag_set_dr_state", "ag_get_dr_state",
            "ag_shading_counts", "ag_dr_update", "ag_set_bidder_modes", "ag_bidder_update",
            "ag_generate_search_grid", "ag_simulate_generated", "ag_stream_copy", "ag_estimate_ctr", "ag_bid",
-           "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_replay_draw", "ag_last_error",
+           "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_replay_draw", "ag_replay_draw_population",
+           "ag_last_error",
            "ag_abi_version", "ag_ts_noise_index", "ag_generate_ts_noise_compact")
 ABI_VERSION = 16
 LEARNER_UNINITIALISED, LEARNER_POLICY, LEARNER_SEARCH = 0, 1, 2
@@ -158,6 +159,9 @@ def load(path=None):
         "ag_bid": (ctypes.c_int, [vp, i32, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "ag_replay_draw": (ctypes.c_int, [ctypes.POINTER(AgPcg64State), i64, i32, i32, i32, ctypes.c_double, i32,
                                           vp, vp, vp, vp, vp, vp, vp]),
+        "ag_replay_draw_population": (ctypes.c_int, [ctypes.POINTER(AgPcg64State), vp, i64, i64, i32, i32, i32,
+                                                     ctypes.c_double, i32, vp, vp, vp, vp, vp, i32, vp, vp,
+                                                     vp, vp, vp, vp, vp, vp, vp]),
         "ag_last_error": (ctypes.c_char_p, []),
         "ag_abi_version": (i32, []),
     }

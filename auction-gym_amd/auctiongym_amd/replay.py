@@ -92,6 +92,75 @@ def draw_rounds_native(rng, B, num_agents, num_participants, embedding_size, emb
     return ctx, part, u, g
 
 
+def _pcg_in(rng):
+    from . import _lib
+    st = rng.bit_generator.state
+    if st.get("bit_generator") != "PCG64":
+        raise NotImplementedError("ag_replay_draw restates numpy's PCG64 only")
+    s, inc = int(st["state"]["state"]), int(st["state"]["inc"])
+    return st, _lib.AgPcg64State(s >> 64, s & M64, inc >> 64, inc & M64, int(st["has_uint32"]), int(st["uinteger"]))
+
+
+def _pcg_out(rng, st, c):
+    st["state"]["state"] = (int(c.state_hi) << 64) | int(c.state_lo)
+    st["state"]["inc"] = (int(c.inc_hi) << 64) | int(c.inc_lo)
+    st["has_uint32"] = int(c.has_uint32)
+    st["uinteger"] = int(c.uinteger)
+    rng.bit_generator.state = st
+
+
+def draw_rounds_native_population(rng, B, num_agents, num_participants, embedding_size, embedding_var,
+                                  shading, ts_models, max_slots=1, policy=None, search=None):
+    """B rounds of draw_round_population in C (ag_replay_draw_population): numpy's draws and
+    torch's (the LR-TS Thompson draws of src/Models.py:31, the fitted policies' rsample draws of
+    src/Models.py:87-88 / :160-161) in the same order, with the same numbers, leaving both
+    generators (rng and torch's global CPU generator) exactly where the Python loop leaves
+    them. Returns ctx [E][B], part [P][B] int32, gamma_raw [P][B] (NaN where nothing is drawn)
+    or None, u [B], ts_noise in the kernel's tile layout [P][ceil(B/64)][K*Do][64] or None,
+    policy_eps [P][B] float32 or None, gamma_grid [P][128][B] or None."""
+    import ctypes
+
+    from . import _lib
+    B, N, P, E = int(B), int(num_agents), int(num_participants), int(embedding_size)
+    st, c = _pcg_in(rng)
+    u8 = lambda flags: None if flags is None or not any(flags) else np.array([bool(x) for x in flags], np.uint8)  # noqa: E731
+    sh, ts, pol, sea = u8(None if shading is None else [x is not None for x in shading]), \
+        u8(None if ts_models is None else [m is not None for m in ts_models]), u8(policy), u8(search)
+    pg = gs = std = None
+    KDo = 0
+    ctx, part, u = np.empty((E, B)), np.empty((P, B), np.int32), np.empty(B)
+    g = noise = eps = grid = None
+    if sh is not None:
+        pg = np.array([x[0] if x is not None else 0.0 for x in shading], np.float64)
+        gs = np.array([x[1] if x is not None else 1.0 for x in shading], np.float64)
+        g = np.empty((P, B))
+    if ts is not None:
+        m0 = next(m for m in ts_models if m is not None)
+        KDo = int(m0.q.numel())
+        std = np.zeros((N, KDo), np.float32)
+        for a, m in enumerate(ts_models):
+            if m is not None:
+                std[a] = (1.0 / torch.sqrt(m.q)).numpy().ravel()  # as src/Models.py:31 computes it
+        noise = np.empty((P, (B + 63) // 64, KDo, 64), np.float32)
+    if pol is not None:
+        eps = np.empty((P, B), np.float32)
+    if sea is not None:
+        grid = np.empty((P, 128, B))
+    blob = None
+    if ts is not None or pol is not None:
+        blob = torch.get_rng_state().numpy().copy()
+    ptr = lambda a: None if a is None else a.ctypes.data  # noqa: E731
+    L = _lib.load()
+    _lib.check(L.ag_replay_draw_population(ctypes.byref(c), ptr(blob), 0 if blob is None else blob.size, B, N, P, E,
+                                           float(embedding_var), int(max_slots), ptr(sh), ptr(pg), ptr(gs), ptr(ts),
+                                           ptr(std), KDo, ptr(pol), ptr(sea), ptr(ctx), ptr(part), ptr(g), ptr(u),
+                                           ptr(noise), ptr(eps), ptr(grid)), "ag_replay_draw_population", L)
+    _pcg_out(rng, st, c)
+    if blob is not None:
+        torch.set_rng_state(torch.from_numpy(blob))
+    return ctx, part, g, u, noise, eps, grid
+
+
 def draw_round_population(rng, num_agents, num_participants, embedding_size, embedding_var,
                           shading, ts_models, max_slots=1, policy=None, search=None):
     """One round of a general population. shading[a] = (prev_gamma, gamma_sigma) of a shading

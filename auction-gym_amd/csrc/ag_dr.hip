@@ -40,17 +40,26 @@ constexpr size_t kRecLdsBytes = 72 * 1024;   // record cache per workgroup, late
 constexpr double kGrid = 0x1p40, kInv = 0x1p-40;
 constexpr int64_t kLo24 = (int64_t(1) << 24) - 1;
 
-// (int64)rint(v * 2^40). For |v * 2^40| < 2^51 (every term in practice) adding 1.5 * 2^52
-// rounds to the integer (nearest, ties to even, as rint) and leaves it in the low mantissa
-// bits: 1 add + 1 integer subtract instead of the long double -> int64 conversion.
-__device__ __forceinline__ int64_t fxr_fast(double v) {  // |v| <= 2^10 guaranteed by the caller
-  return (int64_t)(agexp::asu64(v * kGrid + 0x1.8p52) - agexp::asu64(0x1.8p52));
+// Fixed-point terms (int64)rint(v * 2^40). For |v * 2^40| < 2^51 (every term in practice)
+// adding 1.5 * 2^52 rounds to the integer (nearest, ties to even, as rint) and leaves it in
+// the low mantissa bits.
+// The accumulators hold them biased: fxb(v) = (int64)rint(v * 2^40) + kFxMagic (mod 2^64),
+// kFxMagic = the bits of 1.5 * 2^52 -- for |v * 2^40| < 2^51 simply the bits of v * 2^40 +
+// 1.5 * 2^52, so a term costs one add and the 64-bit accumulate (no subtract); a lane that
+// added n terms to an accumulator takes n * kFxMagic off once (fx_unbias) before the exact
+// sums. Integer arithmetic mod 2^64: the same totals, bit for bit.
+constexpr uint64_t kFxMagic = 0x4338000000000000ull;  // asu64(0x1.8p52)
+__device__ __forceinline__ int64_t fxb_fast(double v) {  // |v| <= 2^10 guaranteed by the caller
+  return (int64_t)agexp::asu64(v * kGrid + 0x1.8p52);
 }
-__device__ __forceinline__ int64_t fxr(double v) {
+__device__ __forceinline__ int64_t fxb(double v) {
   const double x = v * kGrid;
-  if (__builtin_expect(__builtin_fabs(x) < 0x1p51, 1))
-    return (int64_t)(agexp::asu64(x + 0x1.8p52) - agexp::asu64(0x1.8p52));
-  return (int64_t)__builtin_rint(x);
+  if (__builtin_expect(__builtin_fabs(x) < 0x1p51, 1)) return (int64_t)agexp::asu64(x + 0x1.8p52);
+  return (int64_t)((uint64_t)(int64_t)__builtin_rint(x) + kFxMagic);
+}
+__device__ __forceinline__ void addw(int64_t &a, int64_t t) { a = (int64_t)((uint64_t)a + (uint64_t)t); }
+__device__ __forceinline__ void fx_unbias(int64_t &a, int64_t n) {
+  a = (int64_t)((uint64_t)a - (uint64_t)n * kFxMagic);
 }
 
 __device__ __forceinline__ double fxv(int64_t hi, int64_t lo) {
@@ -174,18 +183,19 @@ __device__ __forceinline__ void policy_bwd(const float *p, double c, double v, c
   double ds[2];
   ds[0] = dam * (double)p[6] + das * (double)p[9];
   ds[1] = dam * (double)p[7] + das * (double)p[10];
-  G[off + 6] += fxr(dam * f.s[0]);
-  G[off + 7] += fxr(dam * f.s[1]);
-  G[off + 8] += fxr(dam);
-  G[off + 9] += fxr(das * f.s[0]);
-  G[off + 10] += fxr(das * f.s[1]);
-  G[off + 11] += fxr(das);
+  // biased terms (fxb): one per accumulator per record, fx_unbias'd by the caller
+  addw(G[off + 6], fxb(dam * f.s[0]));
+  addw(G[off + 7], fxb(dam * f.s[1]));
+  addw(G[off + 8], fxb(dam));
+  addw(G[off + 9], fxb(das * f.s[0]));
+  addw(G[off + 10], fxb(das * f.s[1]));
+  addw(G[off + 11], fxb(das));
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const double dh = ds[j] * dsoftplus_e(f.h[j], f.eh[j]);
-    G[off + 2 * j] += fxr(dh * c);
-    G[off + 2 * j + 1] += fxr(dh * v);
-    G[off + 4 + j] += fxr(dh);
+    addw(G[off + 2 * j], fxb(dh * c));
+    addw(G[off + 2 * j + 1], fxb(dh * v));
+    addw(G[off + 4 + j], fxb(dh));
   }
 }
 
@@ -388,7 +398,7 @@ __device__ int fit_winrate(const RecView &V, const Chunk &K, TrainLds &S, Coop &
     int64_t acc[5] = {0, 0, 0, 0, 0};
     const double w0 = (double)S.wr[0], w1 = (double)S.wr[1], w2 = (double)S.wr[2], w3 = (double)S.wr[3];
     // one BCE row: its loss and gradient terms
-    auto row = [&](double c, double v, double g, double y) {
+    auto row = [&](double c, double v, double g, double y, bool aug) {
       const double z = c * w0 + v * w1 + g * w2 + w3;
       // one exp per row (oracle/ag_oracle_dr.c fit_winrate): e = exp(-|z|), L = log1p(e);
       // p = (z >= 0 ? 1 : e) / (1 + e); -log(p) = softplus(-z) for a win, -log(1 - p) =
@@ -407,20 +417,28 @@ __device__ int fit_winrate(const RecView &V, const Chunk &K, TrainLds &S, Coop &
       const double u = y > 0.0 ? -z : z;
       const double t = fmin(u > 20.0 ? u : (u > 0.0 ? a + Lz : Lz), 100.0);
       // |t| <= 100, |pw - y| <= 1, ctr in [0, 1]: these terms are far inside fxr's fast range
-      acc[0] += fxr_fast(t);
+      // biased terms (fxb, one add fewer each), unbiased below
+      addw(acc[0], fxb_fast(t));
       const double gz = pw - y;
-      acc[1] += fxr_fast(gz * c);
-      acc[2] += fxr(gz * v);
-      acc[3] += fxr(gz * g);
-      acc[4] += fxr_fast(gz);
+      addw(acc[1], fxb_fast(gz * c));
+      addw(acc[2], fxb(gz * v));
+      if (!aug) addw(acc[3], fxb(gz * g));  // the augmentation row's g = 0 term is +-0: rounds to 0
+      addw(acc[4], fxb_fast(gz));
     };
     // record j's logged row and its gamma = 0, y = 0 augmentation row together (two
     // independent chains for the scheduler; the sums are exact, so any order)
+    int64_t nrec = 0;
     for (int64_t j = tid; j < K.nb; j += kDrThreads) {
       const double c = V.ctr(j), v = V.val(j);
-      row(c, v, V.gam(j), V.won(j));
-      row(c, v, 0.0, 0.0);
+      row(c, v, V.gam(j), V.won(j), false);
+      row(c, v, 0.0, 0.0, true);
+      ++nrec;
     }
+    fx_unbias(acc[0], 2 * nrec);
+    fx_unbias(acc[1], 2 * nrec);
+    fx_unbias(acc[2], 2 * nrec);
+    fx_unbias(acc[3], nrec);
+    fx_unbias(acc[4], 2 * nrec);
     exact_totals<5>(acc, S, C);
     // every thread: the same loss; threads 0..3 step their parameter
     const float loss = (float)(fxv(S.tot[0], S.tot[1]) / M);
@@ -454,10 +472,13 @@ __device__ int fit_imitation(const RecView &V, const Chunk &K, TrainLds &S, Coop
       PolF f;
       policy_fwd(S.pol, c, v, f, S.tab);
       const double dm = f.mu - V.gam(j), dsg = f.sp_sigma - 0.05;
-      acc[12] += fxr(dm * dm);
-      acc[13] += fxr(dsg * dsg);
+      addw(acc[12], fxb(dm * dm));
+      addw(acc[13], fxb(dsg * dsg));
       policy_bwd(S.pol, c, v, f, 2.0 * dm, 2.0 * dsg, acc, 0, S.tab);
     }
+    const int64_t nrec = K.nb > tid ? (K.nb - tid + kDrThreads - 1) / kDrThreads : 0;
+#pragma unroll
+    for (int q = 0; q < 14; ++q) fx_unbias(acc[q], nrec);
     exact_totals<16>(acc, S, C);
     const float loss = (float)(fxv(S.tot[24], S.tot[25]) / n + fxv(S.tot[26], S.tot[27]) / n);
     const float g = tid < 12 ? (float)(fxv(S.tot[2 * tid], S.tot[2 * tid + 1]) / n) : 0.0f;
@@ -507,7 +528,7 @@ __device__ int fit_dr(const RecView &V, const Chunk &K, TrainLds &S, Coop &C,
       const double zw = c * (double)S.wr[0] + v * (double)S.wr[1] + gs * (double)S.wr[2] + (double)S.wr[3];
       const double Wv = 1.0 / (1.0 + exp_fast(-zw, S.tab));
       const double V = c * v;
-      acc[12] += fxr(-(du * iwc + Wv * (V - V * gs)));
+      addw(acc[12], fxb(-(du * iwc + Wv * (V - V * gs))));
       double dpi_dmu = 0.0, dpi_dsg = 0.0;
       if (pdf_raw >= 1e-30 && iw >= 1.0 / 50.0 && iw <= 50.0) {
         const double k = du / p0;
@@ -518,6 +539,9 @@ __device__ int fit_dr(const RecView &V, const Chunk &K, TrainLds &S, Coop &C,
       if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)S.wr[2];
       policy_bwd(S.pol, c, v, f, -(dpi_dmu + ddm), -(dpi_dsg + ddm * ep), acc, 0, S.tab);
     }
+    const int64_t nrec = K.nb > tid ? (K.nb - tid + kDrThreads - 1) / kDrThreads : 0;
+#pragma unroll
+    for (int q = 0; q < 13; ++q) fx_unbias(acc[q], nrec);
     exact_totals<16>(acc, S, C);
     const float loss = (float)(fxv(S.tot[24], S.tot[25]) / n);
     const float g = tid < 12 ? (float)(fxv(S.tot[2 * tid], S.tot[2 * tid + 1]) / n) : 0.0f;
@@ -561,11 +585,14 @@ __device__ int fit_dm(const RecView &V, const Chunk &K, TrainLds &S, Coop &C, co
       const double zw = c * (double)S.wr[0] + v * (double)S.wr[1] + gs * (double)S.wr[2] + (double)S.wr[3];
       const double Wv = 1.0 / (1.0 + exp_fast(-zw, S.tab));
       const double V = c * v;
-      acc[12] += fxr(-(Wv * (V - V * gs)));
+      addw(acc[12], fxb(-(Wv * (V - V * gs))));
       double ddm = 0.0;
       if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)S.wr[2];
       policy_bwd(S.pol, c, v, f, -ddm, -(ddm * ep), acc, 0, S.tab);
     }
+    const int64_t nrec = K.nb > tid ? (K.nb - tid + kDrThreads - 1) / kDrThreads : 0;
+#pragma unroll
+    for (int q = 0; q < 13; ++q) fx_unbias(acc[q], nrec);
     exact_totals<16>(acc, S, C);
     const float loss = (float)(fxv(S.tot[24], S.tot[25]) / n);
     const float g = tid < 12 ? (float)(fxv(S.tot[2 * tid], S.tot[2 * tid + 1]) / n) : 0.0f;

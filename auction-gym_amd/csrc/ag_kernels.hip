@@ -1000,10 +1000,14 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   if (prune && !c->general && c->ora_catalog && c->sim_kernel != AG_SIM_KERNEL_GENERIC && !c->wide)
     if (OraKernel ok = pick_oracle(s.num_participants, D, false))
       return simulate_oracle(c, ok, B, in, out, counters_fx, (hipStream_t)stream);
-  // k_pop only when asked for: in one-process A/B on the r03 box it is slower than k_simulate
-  // on every population line (configs_1..4: 0.234 / 0.248 / 0.172 / 0.465 ms against 0.178 /
-  // 0.234 / 0.141 / 0.398, 256- and 1024-lane builds alike; profiles/r03_ab_pop_vs_generic.log)
-  const bool want_pop = c->sim_kernel == AG_SIM_KERNEL_FUSED || c->sim_kernel == AG_SIM_KERNEL_SPLIT;
+  // k_pop when asked for, and by AUTO only for TruthfulBidder-only populations at P >= 8 (the
+  // split pass: configs_1 at P = 8 0.632 ms against k_simulate's 0.777). At P = 2 it is slower
+  // than k_simulate on every population line (one-process A/B, configs_1..4: 0.234 / 0.248 /
+  // 0.172 / 0.465 ms against 0.178 / 0.234 / 0.141 / 0.398, 256- and 1024-lane builds alike;
+  // profiles/r03_ab_pop_vs_generic.log)
+  const bool truthful_only = !(c->has_shading || c->gen_mode_all);
+  const bool want_pop = c->sim_kernel == AG_SIM_KERNEL_FUSED || c->sim_kernel == AG_SIM_KERNEL_SPLIT ||
+                        (c->sim_kernel == AG_SIM_KERNEL_AUTO && truthful_only && s.num_participants >= 8);
   if (prune && c->general && want_pop && (c->ts_sample == 0 || !c->has_lrts || in->ts_noise)) {
     const int rc = simulate_pop(c, B, in, out, counters_fx, (hipStream_t)stream);
     if (rc != AG_ERR_UNSUPPORTED) return rc;  // launched (or failed); else k_simulate below

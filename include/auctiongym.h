@@ -237,7 +237,8 @@ typedef enum ag_sim_kernel {
                                 the dedicated kernel k_pop making its Thompson choices itself */
   AG_SIM_KERNEL_SPLIT = 3    /* ... the split pass, k_ts_choice then k_pop. FUSED / SPLIT are
                                 A/B and parity variants (identical results); AUTO runs the
-                                general kernel, faster on every population line measured */
+                                general kernel (faster at P = 2 on every population line),
+                                the split pass for TruthfulBidder-only populations at P >= 8 */
 } ag_sim_kernel;
 
 typedef enum ag_item_search {
@@ -333,6 +334,35 @@ typedef struct ag_pcg64_state {
 int ag_replay_draw(ag_pcg64_state *rng, int64_t B, int32_t N, int32_t P, int32_t E, double embedding_var,
                    int32_t max_slots, const uint8_t *shading, const double *prev_gamma, const double *gamma_sigma,
                    double *ctx, int32_t *part, double *gamma_raw, double *u);
+
+/* ag_replay_draw_population -- B rounds of a general population's draws, in the reference's
+ * order (src/Auction.py:30-42, :65; per participant slot, src/Agent.py:44-53: the LR-TS
+ * allocator's Thompson draw torch.normal(0, 1/sqrt(q)) of src/Models.py:31, then the
+ * bidder's: one rsample of a fitted policy (src/Models.py:87-88, :160-161), or the search
+ * grid rng.uniform(0.1, 1, 128) sorted (src/Bidder.py:184-186), or an uninitialised shading
+ * bidder's rng.normal(prev_gamma, gamma_sigma) (src/Bidder.py:51, 177, 354, 461)).
+ * Replaces the per-round Python loop (auctiongym_amd/replay.py draw_round_population).
+ * numpy's draws as ag_replay_draw; torch's from its CPU generator, restated: mt19937 (the
+ * state blob of torch.get_rng_state(), 5056 bytes: the_initial_seed u64 @0, left i32 @8,
+ * seeded i32 @12, next u64 @16, state u64[624] @24, normal_y f64 @5024, normal_is_valid i32
+ * @5040, next_float_normal f32 @5048, its valid flag u8 @5052) goes in and comes back
+ * advanced (hand it to torch.set_rng_state); Thompson noise = normal_fill<float> of K*Do
+ * values (24-bit uniforms, Box-Muller over blocks of 16, the last 16 recomputed when
+ * K*Do % 16 != 0; glibc logf / cosf / sinf) times ts_std; rsample = normal_distribution
+ * <double> with its cached second value (glibc log1p / cos / sin). Per agent [N]: shading
+ * (uint8, with prev_gamma / gamma_sigma), ts (uint8, with ts_std [N][KDo] = 1/sqrt(q) as
+ * torch computes it), policy (uint8), search (uint8); each may be NULL (none). Outputs:
+ * ctx, part, u, gamma_raw as ag_replay_draw; ts_noise in the kernel's tile layout
+ * [P][ceil(B/64)][KDo][64] (ag_batch_in.ts_noise, zeros where nothing is drawn) when ts;
+ * policy_eps [P][B] float (0 where nothing is drawn) when policy; gamma_grid [P][128][B]
+ * (0 where nothing is drawn) when search. Identical numbers and generator states to the
+ * Python loop (tests/test_host.py::test_replay_population_draws_match_python). */
+int ag_replay_draw_population(ag_pcg64_state *rng, uint8_t *torch_state, int64_t torch_state_bytes, int64_t B,
+                              int32_t N, int32_t P, int32_t E, double embedding_var, int32_t max_slots,
+                              const uint8_t *shading, const double *prev_gamma, const double *gamma_sigma,
+                              const uint8_t *ts, const float *ts_std, int32_t KDo, const uint8_t *policy,
+                              const uint8_t *search, double *ctx, int32_t *part, double *gamma_raw, double *u,
+                              float *ts_noise, float *policy_eps, double *gamma_grid);
 
 /* ---- LR-TS allocator update (Agent.update -> PyTorchLogisticRegressionAllocator.update,
  * src/Agent.py:79-91, src/BidderAllocation.py:29-65) ------------------------------------

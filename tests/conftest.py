@@ -52,7 +52,7 @@ def gpu():
 
 
 POP_CAPTURES = ("sp_ts_r2048", "fp_dr_ts_r1024", "fp_dm_ts_r1024", "fp_ips_ts_r1024",
-                "fp_dm_oracle_r1024", "fp_empirical_r2048")
+                "fp_dm_oracle_r1024", "fp_empirical_r2048", "sp_ts_mixed_flags_r2048")
 
 
 def pop_args(d, meta):

@@ -197,7 +197,7 @@ def capture(cfg, rounds, torch_seed=0, keep=False):
             ctx[r] = c
             part[r] = pa
             u[r] = uu
-            nts = [s_ for s_, a_ in enumerate(pa) if is_ts[a_]]
+            nts = [s_ for s_, a_ in enumerate(pa) if is_ts[a_] and agents[a_].allocator.thompson_sampling]
             assert len(noise_log) - n0 == len(nts)
             for j, s_ in enumerate(nts):
                 ts_noise[r, s_] = noise_log[n0 + j]
@@ -1000,14 +1000,33 @@ def csv_outputs(runs=2, iters=3, rounds=2000):
         print("csv", name, sorted(os.listdir(dst)), flush=True)
 
 
+def mixed_ts_flags_capture(out_name="sp_ts_mixed_flags_r2048", rounds=2048):
+    """SP_Truthful_TS with thompson_sampling set per allocator (src/BidderAllocation.py:24-26):
+    4 LR-TS agents sample, 4 bid from their MAP estimates (estimate_CTR(sample=False),
+    src/BidderAllocation.py:67-68). The config travels in the fixture's meta."""
+    cfg = load_cfg("SP_Truthful_TS.json")
+    base = cfg["agents"][0]
+    cfg["agents"] = [dict(base, name="Truthful TS", num_copies=4),
+                     dict(base, name="Truthful MAP", num_copies=4,
+                          allocator={"type": base["allocator"]["type"],
+                                     "kwargs": dict(base["allocator"]["kwargs"], thompson_sampling=False)})]
+    cfg["output_dir"] = "/tmp/ag_golden_unused/"
+    a, g, m = capture(cfg, rounds)
+    m["config"] = cfg
+    save_capture(out_name, a, g, m)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also run SP_Oracle as shipped (3x20x10k rounds, ~1 min)")
     ap.add_argument("--which", choices=["dm", "ips", "dr", "dmo", "search"], help="with --only learners/drivers: one config")
-    ap.add_argument("--only", choices=["empirical", "csv", "dr", "learners", "drivers", "memory", "later"],
+    ap.add_argument("--only", choices=["empirical", "csv", "dr", "learners", "drivers", "memory", "later", "mixedts"],
                     help="regenerate one fixture family only")
     args = ap.parse_args()
     install_shims()
+    if args.only == "mixedts":
+        mixed_ts_flags_capture()
+        return
     if args.only == "memory":
         memory_driver_kat()
         return

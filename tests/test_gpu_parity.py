@@ -1010,6 +1010,49 @@ SP_TRUTHFUL_TS = {  # config/SP_Truthful_TS.json as shipped
     "output_dir": "results/SP_Truthful_TS/"}
 
 
+@pytest.mark.parametrize("path", ["per_round", "batch"])
+def test_dropin_per_allocator_thompson_flags(gpu, tmp_path, path):
+    """thompson_sampling set per allocator (src/BidderAllocation.py:24-26): 4 LR-TS agents sample,
+    4 bid from their MAP estimates (tests/golden/sp_ts_mixed_flags_r2048, the reference's own
+    run). Through the drop-in classes, per round (simulate_opportunity: torch.normal for the
+    sampling agents only) and as one batch (simulate_batch: ag_replay_draw_population): the
+    reference's items per agent, utilities and revenue to the exact sums' 1e-11, and torch's
+    generator left where the per-round loop leaves it."""
+    import torch
+
+    import auctiongym_amd.main as M
+    d, meta, agg = load_capture("sp_ts_mixed_flags_r2048")
+    p = tmp_path / "cfg.json"
+    p.write_text(json.dumps(meta["config"]))
+    rng, config, agent_configs, a2i, a2v, _, max_slots, E, var, OE = M.parse_config(str(p))
+    torch.manual_seed(meta["torch_seed"])
+    agents = M.instantiate_agents(rng, agent_configs, a2v, a2i)
+    assert [a.allocator.thompson_sampling for a in agents] == [True] * 4 + [False] * 4
+    auction, _, _, _ = M.instantiate_auction(rng, config, a2i, a2v, agents, max_slots, E, var, OE)
+    if path == "per_round":
+        for _ in range(meta["rounds"]):
+            auction.simulate_opportunity()
+    else:
+        auction.simulate_batch(meta["rounds"])
+    rt = dict(rtol=1e-11, atol=1e-12)
+    np.testing.assert_allclose([a.net_utility for a in agents], agg["net_utility"], **rt)
+    np.testing.assert_allclose([a.gross_utility for a in agents], agg["gross_utility"], **rt)
+    np.testing.assert_allclose(auction.revenue, agg["revenue"], **rt)
+    assert [a.num_logs() for a in agents] == list(agg["n_logs"])
+    for i, a in enumerate(agents):
+        rows, slots = np.nonzero(d["part"] == i)
+        assert [o.item for o in a.logs] == list(d["item"][rows, slots])
+        np.testing.assert_array_equal([o.estimated_CTR for o in a.logs], d["slot_est_ctr"][rows, slots])
+    # the generator: 60 torch.normal values per sampling participation, none for the others
+    ref = torch.Generator().manual_seed(meta["torch_seed"])
+    for a in range(8):
+        torch.empty(12, 5).normal_(generator=ref)  # the agents' initial m (torch.nn.init.normal_)
+    n_ts = int(np.isin(d["part"], np.arange(4)).sum())
+    for _ in range(n_ts):
+        torch.empty(60).normal_(generator=ref)
+    assert torch.equal(torch.get_rng_state(), ref.get_state())
+
+
 def test_driver_sp_truthful_ts_iteration(gpu, oracle, tmp_path):
     """SP_Truthful_TS.json through the drop-in classes with torch seeded as the capture was:
     the same LR-TS initial models (torch.nn.init.normal_), the same Thompson draws

@@ -25,6 +25,9 @@ from auctiongym_amd import _lib  # noqa: E402
 
 def main():
     key = sys.argv[1]
+    P = 2
+    if ":" in key:  # configs_1:8 -> P = 8 participants per auction
+        key, P = key.split(":")[0], int(key.split(":")[1])
     vdir = os.path.join(ROOT, "auction-gym_amd", "build", "variants")
     paths = {"base": _lib.LIB_PATH}
     special = {"generic", "fused", "split", "bt256", "bt1024", "nocnt"}
@@ -39,7 +42,7 @@ def main():
             items, values = bench.catalogue(bench.SP_TS)
             N, K, D = items.shape
             OE = bench.SP_TS["obs_embedding_size"]
-            eng = AuctionEngine(N, 2, K, D - 1, OE, _lib.SECOND_PRICE, bench.SP_TS["embedding_var"], device=0)
+            eng = AuctionEngine(N, P, K, D - 1, OE, _lib.SECOND_PRICE, bench.SP_TS["embedding_var"], device=0)
             eng.set_agent_params(np.ones(N, np.int32), np.zeros(N, np.int32))
             eng.load_catalog(items, values)
             g = torch.Generator().manual_seed(0)
@@ -49,7 +52,7 @@ def main():
             eng.load_lrts(m.numpy(), np.ones((N, K, OE + 1), np.float32), thompson_sampling=True)
             B, ak = 1 << 20, np.ones(N, np.int32)
         else:
-            eng, what, B, ak, bk, st16, dims = bench.build_population(key, 0)
+            eng, what, B, ak, bk, st16, dims = bench.build_population(key, 0, P=P)
             eng.set_dr_state(st16, np.where(bk >= 2, 1, 0).astype(np.int32))
         if n in ("generic", "fused", "split"):
             eng.set_simulate_kernel(True if n == "generic" else n)

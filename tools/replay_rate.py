@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
-"""Drop-in replay rate: Auction.simulate_batch(B) on SP_Oracle.json as shipped
--- the reference's own numpy draws made in C (ag_replay_draw), copied to the GPU, resolved by
-the kernel -- against the draws alone and the per-round Python loop they replace.
+"""Drop-in replay rate: Auction.simulate_batch(B) through the drop-in driver's objects -- the
+reference's own numpy and torch draws made in C for the whole batch (ag_replay_draw /
+ag_replay_draw_population), copied to the GPU, resolved by the kernel -- against the per-round
+Python loop they replace (replay.draw_round / draw_round_population, the reference's calls).
 
-    python tools/replay_rate.py [B]
+    python tools/replay_rate.py [config] [B]
+    config: SP_Oracle (default), SP_Truthful_TS, FP_DR_TS (iteration 0: Gaussian shading, numpy
+            draws), FP_DR_TS_policy (after the first update: one torch rsample per DR slot)
 """
 import json
 import os
@@ -13,40 +16,74 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "auction-gym_amd"), ROOT]
-import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import bench  # noqa: E402
 import auctiongym_amd.main as M  # noqa: E402
-from auctiongym_amd.replay import draw_rounds, draw_rounds_native  # noqa: E402
+
+FP_DR_TS = dict(bench.SP_ORACLE, allocation="FirstPrice", num_iter=3, agents=[{
+    "name": "DR", "num_copies": 3, "num_items": 12,
+    "allocator": {"type": "PyTorchLogisticRegressionAllocator", "kwargs": {"embedding_size": 4, "num_items": 12}},
+    "bidder": {"type": "DoublyRobustBidder", "kwargs": {"gamma_sigma": 0.02, "init_gamma": 1.0}}}],
+    output_dir="results/FP_DR_TS/")  # reference config/FP_DR_TS.json
+CONFIGS = {"SP_Oracle": bench.SP_ORACLE, "SP_Truthful_TS": bench.SP_TS, "FP_DR_TS": FP_DR_TS,
+           "FP_DR_TS_policy": FP_DR_TS}
 
 
-def main():
-    B = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+def build(cfg):
     with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
-        json.dump(bench.SP_ORACLE, f)
+        json.dump(cfg, f)
     rng, config, agent_configs, a2i, a2v, _, max_slots, E, var, OE = M.parse_config(f.name)
     os.unlink(f.name)
     agents = M.instantiate_agents(rng, agent_configs, a2v, a2i)
     auction, *_ = M.instantiate_auction(rng, config, a2i, a2v, agents, max_slots, E, var, OE)
-    N, P = len(agents), config["num_participants_per_round"]
-    auction.simulate_batch(1 << 14)  # warm: kernels, allocator
+    return rng, auction, agents
+
+
+def python_loop_ms_per_2_20(auction, n):
+    """The per-round Python loop (the reference's calls, replay.py) on a copy of the state."""
+    import copy
+    rng = copy.deepcopy(auction.rng)
+    ts = torch.get_rng_state()
+    save = auction.rng
+    auction.rng = rng
+    t = time.perf_counter()
+    for _ in range(n):
+        auction._draw_round()
+    dt = time.perf_counter() - t
+    auction._pending = []
+    auction.rng = save
+    torch.set_rng_state(ts)
+    return dt * 1e3 * (1 << 20) / n
+
+
+def main():
+    name = sys.argv[1] if len(sys.argv) > 1 else "SP_Oracle"
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
+    rng, auction, agents = build(CONFIGS[name])
+    res = {"config": name, "rounds": B}
+    if name.endswith("_policy"):  # iteration 0, then every agent's update: bids from the fitted policies
+        auction.simulate_batch(10000)
+        t = time.perf_counter()
+        for i, a in enumerate(agents):
+            a.update(iteration=0, plot=False)
+        res["update_s"] = time.perf_counter() - t
+        for a in agents:
+            a.clear_logs()
+        res["learner_states"] = [int(a.bidder._learner_state()) for a in agents]
+    auction.simulate_batch(1 << 12)  # warm: kernels, allocator
+    _ = auction.revenue
     torch.cuda.synchronize()
-    res = {"rounds": B}
-    t = time.perf_counter()
-    draw_rounds_native(np.random.default_rng(1), B, N, P, E, var, max_slots)
-    res["draw_native_ms"] = (time.perf_counter() - t) * 1e3
-    n = min(B, 1 << 15)
-    t = time.perf_counter()
-    draw_rounds(np.random.default_rng(1), n, N, P, E, var, max_slots)
-    res["draw_python_ms_per_2^20"] = (time.perf_counter() - t) * 1e3 * (1 << 20) / n
+    auction.keep_logs = False
+    res["python_loop_ms_per_2^20"] = python_loop_ms_per_2_20(auction, min(B, 1 << 12))
     t = time.perf_counter()
     auction.simulate_batch(B)
     _ = auction.revenue  # reads the counters back (synchronises)
     torch.cuda.synchronize()
     res["simulate_batch_ms"] = (time.perf_counter() - t) * 1e3
     res["simulate_batch_rounds_per_s"] = B / (res["simulate_batch_ms"] * 1e-3)
-    print(json.dumps(res))
+    res["speedup_vs_python_loop"] = res["python_loop_ms_per_2^20"] * B / (1 << 20) / res["simulate_batch_ms"]
+    print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":
