@@ -342,8 +342,10 @@ int32_t ora_dr_update(int64_t n, const double *ctr, const double *value, const d
     vf[i] = (float)value[i];
     gf[i] = (float)gamma[i];
   }
-  /* ---- 1. win-rate fit */
-  epochs[0] = fit_winrate(n, cf, vf, gf, won, wr, 256, 0.2, 1024, wr_trace);
+  /* ---- 1. win-rate fit (initialised bit 1, a test hook: skipped, wr is taken as already
+   * fitted -- to run the later fits from the reference's own fitted model) */
+  epochs[0] = (initialised & 2) ? 0 : fit_winrate(n, cf, vf, gf, won, wr, 256, 0.2, 1024, wr_trace);
+  initialised &= 1;
   /* ---- 2. estimated utilities with the fitted model (float32 W, as .numpy() of it) */
   for (int64_t i = 0; i < n; ++i) {
     const float W = (float)winrate(wr, cf[i], vf[i], gf[i]);

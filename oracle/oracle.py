@@ -287,10 +287,11 @@ def empirical_update(gammas, utilities):
     return float(out[0])
 
 
-def dr_update(ctr, value, gamma, prop, won, util, wr, pol, initialised, noise, trace=True):
+def dr_update(ctr, value, gamma, prop, won, util, wr, pol, initialised, noise, trace=True, skip_winrate=False):
     """DoublyRobustBidder.update (src/Bidder.py:473-615) of one agent; noise [E][n] float32
-    per-epoch rsample draws of the DR fit. Returns dict(wr, pol, epochs, wr_losses,
-    init_losses, dr_losses, est_util)."""
+    per-epoch rsample draws of the DR fit. skip_winrate: wr is an already fitted win-rate
+    model (test hook: the later fits from the reference's own fitted model). Returns dict(wr,
+    pol, epochs, wr_losses, init_losses, dr_losses, est_util)."""
     n = len(ctr)
     a = [np.ascontiguousarray(v, np.float64) for v in (ctr, value, gamma, prop)]
     w = np.ascontiguousarray(np.asarray(won) != 0, np.uint8)
@@ -302,7 +303,8 @@ def dr_update(ctr, value, gamma, prop, won, util, wr, pol, initialised, noise, t
     ep = np.zeros(3, np.int32)
     tr = [np.zeros(32768, np.float32), np.zeros(16384, np.float32), np.zeros(32768, np.float32)]
     eu = np.zeros(n)
-    rc = lib().ora_dr_update(n, *[_p(v) for v in a], _p(w), _p(u), _p(wr), _p(pol), int(bool(initialised)),
+    rc = lib().ora_dr_update(n, *[_p(v) for v in a], _p(w), _p(u), _p(wr), _p(pol),
+                             int(bool(initialised)) | (2 if skip_winrate else 0),
                              _p(noise), E, _p(ep), *[(_p(t) if trace else None) for t in tr], _p(eu))
     if rc:
         raise ValueError("DoublyRobustBidder.update without logs")
