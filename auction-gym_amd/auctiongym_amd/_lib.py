@@ -8,6 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libauctiongym_hip.so")
+LIB_DEFAULT = LIB_PATH  # the product build: every entry point must be there
 
 AG_OK, AG_ERR_INVALID, AG_ERR_UNSUPPORTED, AG_ERR_HIP, AG_ERR_STATE = 0, -1, -2, -3, -4
 FIRST_PRICE, SECOND_PRICE = 0, 1
@@ -25,6 +26,7 @@ OPT_SIMULATE_KERNEL = 7
 OPT_SIM_BLOCKS_PER_CU = 8
 OPT_SIM_BLOCK_THREADS = 9
 OPT_SIM_GENERAL_MODE = 10
+OPT_SIM_SHIPPED_SHAPE = 11
 SIM_KERNEL_AUTO, SIM_KERNEL_GENERIC, SIM_KERNEL_FUSED, SIM_KERNEL_SPLIT = 0, 1, 2, 3
 ITEM_SEARCH_AUTO, ITEM_SEARCH_EXACT = 0, 1
 
@@ -166,6 +168,8 @@ def load(path=None):
         "ag_abi_version": (i32, []),
     }
     for name, (res, args) in sig.items():
+        if path != LIB_DEFAULT and not hasattr(L, name):
+            continue  # an older A/B build (tools/ab_*.py) without an entry point added since
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

@@ -887,6 +887,10 @@ int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
       if (value != 0 && value != 1) return ag_set_error(AG_ERR_INVALID, "ag_set_option: general mode must be 0 or 1");
       c->gen_mode_all = value == 1;
       return AG_OK;
+    case AG_OPT_SIM_SHIPPED_SHAPE:
+      if (value != 0 && value != 1) return ag_set_error(AG_ERR_INVALID, "ag_set_option: shipped shape must be 0 or 1");
+      c->ship_shape = value == 1;
+      return AG_OK;
     case AG_OPT_SIMULATE_KERNEL:
       if (value < AG_SIM_KERNEL_AUTO || value > AG_SIM_KERNEL_SPLIT)
         return ag_set_error(AG_ERR_INVALID, "ag_set_option: bad simulate kernel %lld", (long long)value);
@@ -1025,10 +1029,13 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   // AG_OPT_SIM_GENERAL_MODE 0 (auto): TruthfulBidder-only populations take the build
   // without the bid-shading code (kGenTruthful); 1: always the full general build
   const int gmode = !c->general ? kGenOracle : (c->has_shading || c->gen_mode_all) ? kGenAll : kGenTruthful;
-  SimKernel k = pick_kernel(s.num_participants, D, prune, W, gmode, bt);
+  // the shipped shape (E = 5, LR-TS width OE + 1 = 5 in the layout) has builds with the LR-TS
+  // width compile-time (k_simulate's DOS); AG_OPT_SIM_SHIPPED_SHAPE 0 turns them off (A/B)
+  const int ship = (c->general && c->ship_shape && D == 6 && prm.lds.ts_do == kShipDo) ? kGenShip : 0;
+  SimKernel k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
   if (!k && bt != kThreads) {
     bt = kThreads;
-    k = pick_kernel(s.num_participants, D, prune, W, gmode, bt);
+    k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
   }
   if (!k) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: no kernel for P=%d D=%d", s.num_participants, D);
   if (gmode == kGenAll && bt == kLargeThreads) {  // the compacted fitted-policy pass's per-wave task slots
@@ -1042,7 +1049,7 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
     AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   // Persistent grid: exactly the blocks the device keeps resident (no partial last round),
   // each striding over bt-auction tiles.
-  int &res = c->resident[(gmode == kGenTruthful ? 32 : 0) + (bt == kThreads ? 0 : 16) + (c->general ? 8 : 0) +
+  int &res = c->resident[(ship ? 64 : 0) + (gmode == kGenTruthful ? 32 : 0) + (bt == kThreads ? 0 : 16) + (c->general ? 8 : 0) +
                          (W == 2 ? 4 : 0) + (prune ? 2 : 0) + (prm.want_counters ? 1 : 0)];
   if (res == 0) {
     int per_cu = 0, cus = 0;

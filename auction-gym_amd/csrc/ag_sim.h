@@ -487,6 +487,8 @@ __device__ __forceinline__ float ts_ctr_k(const float *w, const float (&x)[DW], 
 #endif
 constexpr int kTsGroup = AG_TS_GROUP;
 constexpr int kTsScreenK = 12;
+constexpr int kShipDo = 5;   // the shipped configs' LR-TS model width (OE = 4)
+constexpr int kGenShip = 8;  // pick_kernel_for: OR-ed into `general` for that width (D = 6)
 template <int DW>
 __device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], const float *nz, int K, int Do,
                                          const double *vals, const uint64_t *tab) {
@@ -768,14 +770,22 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
   r.oc = bernoulli(ctr_w, u);  // src/Auction.py:65 (true CTR of the winner's item)
 }
 
-template <int P, int D, bool PRUNE, int W, int GENERAL, int BT = kThreads>
+// DOS: 0, or the LR-TS model width Do = OE + 1 as a compile-time constant (the host picks
+// DOS = 5, the shipped configs' OE = 4, when the layout's ts_do is 5): the width masks of the
+// observed-context row, the generic-width logit chain and the sgemv order's Do == 5 test fold
+// away, and fewer values stay live (P = 2, 256 lanes, TruthfulBidders: 128 -> 115 VGPRs,
+// 441 -> 155 SGPRs spilled to VGPR lanes; the full build at 1024 lanes: 112 -> 52 B of
+// scratch per lane). K stays a runtime value: with it compile-time the item loops unroll
+// fully and spill (200 VGPRs at P = 2), measured.
+template <int P, int D, bool PRUNE, int W, int GENERAL, int BT = kThreads, int DOS = 0>
 __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
                                  : (GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES)) void k_simulate(SimParams prm) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = prm.N, K = prm.K;
   const uint32_t B = (uint32_t)prm.B;  // SoA leading dimension (auctions in the batch)
   const uint32_t lo = (uint32_t)prm.lo, hi = (uint32_t)prm.hi;  // this launch's auctions
-  const LdsLayout L = prm.lds;
+  LdsLayout L = prm.lds;
+  if constexpr (DOS > 0) L.ts_do = DOS;
   uint64_t *s_tab = reinterpret_cast<uint64_t *>(smem + L.tab);
   double *s_items = reinterpret_cast<double *>(smem + L.items);
   double *s_vals = reinterpret_cast<double *>(smem + L.values);

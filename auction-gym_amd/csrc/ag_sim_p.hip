@@ -35,6 +35,7 @@ SimKernel pick_d(int D) {
 // P = 0: the runtime-P kernel (more than kMaxP participants), one auction per lane.
 template <>
 SimKernel pick_kernel_for<0>(int D, bool prune, int W, int general, int bt) {
+  general &= ~kGenShip;  // no shipped-shape build of the runtime-P kernel
   if (W != 1 || bt != kThreads || D > 8) return nullptr;
   if (general) return prune ? pick_d<0, true, 1, kGenAll>(D) : pick_d<0, false, 1, kGenAll>(D);
   return prune ? pick_d<0, true, 1, kGenOracle>(D) : pick_d<0, false, 1, kGenOracle>(D);
@@ -46,6 +47,14 @@ OraKernel pick_oracle_for<0>(int, bool) { return nullptr; }
 template <>
 SimKernel pick_kernel_for<AG_P>(int D, bool prune, int W, int general, int bt) {
   constexpr int P = AG_P;
+  const bool ship = (general & kGenShip) != 0;
+  general &= ~kGenShip;
+  if (general && ship && prune && D == 6) {  // the shipped shape: LR-TS width 5 compile-time
+    if (bt == kLargeThreads) return k_simulate<P, 6, true, 1, kGenAll, kLargeThreads, kShipDo>;
+    if (bt != kThreads) return nullptr;
+    if (general == kGenTruthful) return k_simulate<P, 6, true, 1, kGenTruthful, kThreads, kShipDo>;
+    return k_simulate<P, 6, true, 1, kGenAll, kThreads, kShipDo>;
+  }
   if (general) {
     if (D > 8) return nullptr;
     if (bt == kLargeThreads) return prune ? pick_d<P, true, 1, kGenAll, kLargeThreads>(D) : nullptr;

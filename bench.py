@@ -524,6 +524,16 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
                     "(ag_bidder_update: win-rate fit, imitation, policy fit; synthetic on-device rsample noise)"
                     + (f"; agent-parallel over {world} ranks: records routed to their agent's owner "
                        "(all-to-all), owners train, models exchanged (all-gather)" if world > 1 else "")}
+        tp = os.path.join(ROOT, "profiles", "trainer_pmc.json")
+        if key == "configs_2" and os.path.exists(tp):  # PMC passes of this same update (tools/trainer_pmc.py)
+            pm = json.load(open(tp))
+            vr = {k: {"frac": round(v["valu_roofline_frac"], 3), "valu_issue_ms": round(v["valu_issue_ms"], 1),
+                      "kernel_ms": round(v["ms_mean_over_passes"], 1), "clock_ghz": round(v["clock_ghz"], 2)}
+                  for k, v in pm.items() if isinstance(v, dict) and "valu_roofline_frac" in v}
+            vr["what"] = ("VALU-issue roofline: wave-level VALU instructions x 4 cycles over 1024 SIMDs at the "
+                          "measured clock, / the dispatch time")
+            vr["source"] = "profiles/trainer_pmc.json (rocprofv3 --pmc passes of this update)"
+            res["agent_update"]["valu_roofline"] = vr
         n_sh = int(sst["count"][0])
         rec_counts = np.bincount(sst["agent"][:n_sh].cpu().numpy(), minlength=N)
         res["agent_update"]["bidder_record_epochs_per_s"] = gpu_record_epochs(rec_counts[learners], ep[learners], ms[1])

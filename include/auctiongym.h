@@ -223,9 +223,13 @@ typedef enum ag_option {
                                      0 = auto (1024 when the population's LDS would keep fewer than
                                      16 waves resident per CU with 256-lane workgroups), 256 or
                                      1024; identical results */
-  AG_OPT_SIM_GENERAL_MODE = 10    /* value: 0 = auto (TruthfulBidder-only populations run the
+  AG_OPT_SIM_GENERAL_MODE = 10,   /* value: 0 = auto (TruthfulBidder-only populations run the
                                      general kernel built without the bid-shading code: fewer
                                      VGPRs), 1 = always the full general build; identical results */
+  AG_OPT_SIM_SHIPPED_SHAPE = 11   /* value: 1 (default) = general populations of the shipped
+                                     shape (E = 5, OE = 4) run a build of the general kernel
+                                     with the LR-TS model width compile-time; 0 = the
+                                     runtime-width build; identical results */
 } ag_option;
 
 typedef enum ag_sim_kernel {

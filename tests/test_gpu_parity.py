@@ -1921,7 +1921,8 @@ POP_CASES = [  # (P, mech, ts_sample, compact, block, B, launch cap, counters, p
 @pytest.mark.parametrize("case", POP_CASES)
 def test_pop_kernel_equals_general_kernel(gpu, oracle, case):
     """The general-population kernels of the shipped catalogue shape (K = 12, E = 5, OE = 4;
-    ag_sim_pop.h) -- the AUTO choice, k_pop making its Thompson choices itself
+    ag_sim_pop.h; k_simulate's compile-time LR-TS width build, DOS = 5, against its runtime-width
+    build) -- the AUTO choice, k_pop making its Thompson choices itself
     (AG_SIM_KERNEL_FUSED) and k_ts_choice + k_pop (AG_SIM_KERNEL_SPLIT) -- against k_simulate
     (AG_SIM_KERNEL_GENERIC) on the same inputs: every
     output and the exact counter limbs bit for bit -- LR-TS + truthful, fitted-policy and search
@@ -1961,8 +1962,11 @@ def test_pop_kernel_equals_general_kernel(gpu, oracle, case):
         init = np.array([1 if bk[a] >= 2 and (pop == "dm" or a % 3 != 1) else 0 for a in range(N)], np.int32)
         modes = np.full(N, _lib.VL_POLICY, np.int32)
     runs = []
-    for generic in (False, True, "fused", "split"):
+    for generic in (False, True, "fused", "split", "noship"):
         eng = AuctionEngine(N, P, K, E, OE, mech, 1.0)
+        if generic == "noship":  # k_simulate's runtime-width build (AUTO / GENERIC: the DOS = 5 one)
+            eng._check(eng.L.ag_set_option(eng._h, _lib.OPT_SIM_SHIPPED_SHAPE, 0), "ag_set_option")
+            generic = True
         eng.set_agent_params(ak, bk, pg, gs)
         eng.load_catalog(items, values)
         if ak.any():
