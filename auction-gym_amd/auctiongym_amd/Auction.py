@@ -52,10 +52,10 @@ class Auction:
         if max_slots != 1:
             raise NotImplementedError("max_slots must be 1 (src/main.py:37)")
 
-        ks = {len(agents2item_values[a.name]) for a in agents}
-        if len(ks) != 1:
-            raise NotImplementedError("all agents must have the same num_items")
-        K = ks.pop()
+        # each agent's own num_items (src/main.py:61,66): catalogues padded to the largest K
+        # with value-0 rows (ag_set_agent_items)
+        self._num_items = np.array([len(agents2item_values[a.name]) for a in agents], np.int32)
+        K = int(self._num_items.max())
         N = len(agents)
         D = embedding_size + 1
         if K == 1 or (D >= 8 and K % 4 != 0):
@@ -79,19 +79,27 @@ class Auction:
         gs = np.array([getattr(a.bidder, "gamma_sigma", 1.0) for a in agents], np.float64)
         eng.set_agent_params(ak, bk, pg if self._shading.any() else None,
                              gs if self._shading.any() else None)
-        self._values = np.stack([np.asarray(agents2item_values[a.name], np.float64) for a in agents])
-        eng.load_catalog(np.stack([np.asarray(agent2items[a.name], np.float64)
-                                   for a in agents]), self._values)
+        self._values = np.zeros((N, K))
+        items = np.zeros((N, K, embedding_size + 1))
+        for i, a in enumerate(agents):
+            self._values[i, :self._num_items[i]] = agents2item_values[a.name]
+            items[i, :self._num_items[i]] = agent2items[a.name]
+        if (self._num_items < K).any():
+            eng.set_agent_items(self._num_items)
+        eng.load_catalog(items, self._values)
         self._ts = False
         self._ts_agent = np.zeros(len(agents), bool)
         if self._lrts.any():
             lr = [a.allocator for a in agents if a.allocator.kind == _lib.ALLOCATOR_LRTS]
-            for al in lr:
-                if al.embedding_size != obs_embedding_size or al.num_items != K:
+            for i, a in enumerate(agents):
+                al = a.allocator
+                if al.kind != _lib.ALLOCATOR_LRTS:
+                    continue
+                if al.embedding_size != obs_embedding_size or al.num_items != self._num_items[i]:
                     raise ValueError(
                         f"PyTorchLogisticRegressionAllocator(embedding_size={al.embedding_size}, "
                         f"num_items={al.num_items}) must model the observed context "
-                        f"(obs_embedding_size={obs_embedding_size}) and the K={K} items")
+                        f"(obs_embedding_size={obs_embedding_size}) and the agent's {self._num_items[i]} items")
             # thompson_sampling is per allocator (src/BidderAllocation.py:24-26, :67-68): the
             # kernel runs in sampling mode when any LR-TS agent samples; an agent that does not
             # sample gets zero noise, so its "sampled" CTRs are its MAP CTRs (m + 0 = m) and it
@@ -132,7 +140,8 @@ class Auction:
         for i, a in enumerate(self.agents):
             if self._lrts[i]:
                 rm = a.allocator.response_model
-                m[i], q[i], pm[i] = rm.m.numpy(), rm.q.numpy(), rm.prev_iter_m.numpy()
+                k = self._num_items[i]  # rows beyond the agent's own items: m = prev_m = 0, q = 1
+                m[i, :k], q[i, :k], pm[i, :k] = rm.m.numpy(), rm.q.numpy(), rm.prev_iter_m.numpy()
         self._engine.load_lrts(m, q, pm, thompson_sampling=self._ts)
 
     def _load_learners(self):
@@ -161,7 +170,7 @@ class Auction:
         shading, models, policy, search = self._population_draws()
         ctx, part, g, u, noise, eps, grid = draw_round_population(
             self.rng, N, P, self.embedding_size, self.embedding_var, shading, models, self.max_slots,
-            policy, search)
+            policy, search, kdo_max=self._engine.K * (self.obs_embedding_size + 1))
         self._pending.append((ctx, part, u, g, noise, eps, grid))
 
     def _flush_limit(self):
@@ -221,7 +230,8 @@ class Auction:
             if torch_or_grid:
                 ctx, part, g, u, noise, eps, grid = draw_rounds_native_population(
                     self.rng, n, N, P, self.embedding_size, self.embedding_var,
-                    shading if self._shading.any() else None, models, self.max_slots, policy, search)
+                    shading if self._shading.any() else None, models, self.max_slots, policy, search,
+                    kdo_max=self._engine.K * (self.obs_embedding_size + 1))
             else:
                 ctx, part, u, g = draw_rounds_native(self.rng, n, N, P, self.embedding_size, self.embedding_var,
                                                      self.max_slots, shading if self._shading.any() else None)
@@ -398,7 +408,8 @@ class Auction:
         if "lrts" in state:
             m, q, pm, ep = state["lrts"]
             rm = ag.allocator.response_model
-            rm.m, rm.q, rm.prev_iter_m = torch.from_numpy(m), torch.from_numpy(q), torch.from_numpy(pm)
+            k = self._num_items[index]  # the agent's own rows
+            rm.m, rm.q, rm.prev_iter_m = (torch.from_numpy(np.ascontiguousarray(x[:k])) for x in (m, q, pm))
             ag.allocator.epochs = ep
         if "prev_gamma" in state:
             ag.bidder.prev_gamma = state["prev_gamma"]

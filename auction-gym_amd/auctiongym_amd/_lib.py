@@ -37,7 +37,8 @@ NUM_COUNTERS = len(COUNTERS)
 FX_FRAC_BITS, FX_LIMB_BITS, FX_LIMBS = 36, 42, 3
 
 # Every symbol include/auctiongym.h declares (tests check the .so exports all of them).
-EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params", "ag_load_lrts",
+EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params", "ag_set_agent_items",
+           "ag_load_lrts",
            "ag_set_option", "ag_load_catalog", "ag_allocate", "ag_simulate", "ag_generate",
            "ag_generate_noise", "ag_lrts_collect", "ag_lrts_update", "ag_lrts_read",
            "ag_shading_collect", "ag_empirical_update", "ag_set_dr_state", "ag_get_dr_state",
@@ -130,6 +131,7 @@ def load(path=None):
         "ag_load_catalog": (ctypes.c_int, [vp, vp, vp]),
         "ag_set_option": (ctypes.c_int, [vp, i32, i64]),
         "ag_set_agent_params": (ctypes.c_int, [vp, vp, vp, vp, vp]),
+        "ag_set_agent_items": (ctypes.c_int, [vp, vp]),
         "ag_load_lrts": (ctypes.c_int, [vp, vp, vp, vp, i32]),
         "ag_lrts_collect": (ctypes.c_int, [vp, i64, ctypes.POINTER(AgBatchIn),
                                            ctypes.POINTER(AgBatchOut), ctypes.POINTER(AgLrtsSamples), vp]),
@@ -162,7 +164,7 @@ def load(path=None):
         "ag_replay_draw": (ctypes.c_int, [ctypes.POINTER(AgPcg64State), i64, i32, i32, i32, ctypes.c_double, i32,
                                           vp, vp, vp, vp, vp, vp, vp]),
         "ag_replay_draw_population": (ctypes.c_int, [ctypes.POINTER(AgPcg64State), vp, i64, i64, i32, i32, i32,
-                                                     ctypes.c_double, i32, vp, vp, vp, vp, vp, i32, vp, vp,
+                                                     ctypes.c_double, i32, vp, vp, vp, vp, vp, i32, vp, vp, vp,
                                                      vp, vp, vp, vp, vp, vp, vp]),
         "ag_last_error": (ctypes.c_char_p, []),
         "ag_abi_version": (i32, []),

@@ -83,6 +83,11 @@ class AuctionEngine:
         assert a.shape == (self.N,) and b.shape == (self.N,)
         self._check(self.L.ag_set_agent_kinds(self._h, a.ctypes.data, b.ctypes.data), "ag_set_agent_kinds")
 
+    def set_agent_items(self, num_items):
+        """Each agent's own item count (ag_set_agent_items; None: all K)."""
+        n = None if num_items is None else np.ascontiguousarray(num_items, np.int32)
+        self._check(self.L.ag_set_agent_items(self._h, None if n is None else n.ctypes.data), "ag_set_agent_items")
+
     def set_agent_params(self, allocator_kinds, bidder_kinds, prev_gamma=None, gamma_sigma=None):
         """Plugin kinds + shading parameters (ag_set_agent_params)."""
         a = np.ascontiguousarray(allocator_kinds, np.int32)

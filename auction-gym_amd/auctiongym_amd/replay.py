@@ -110,14 +110,15 @@ def _pcg_out(rng, st, c):
 
 
 def draw_rounds_native_population(rng, B, num_agents, num_participants, embedding_size, embedding_var,
-                                  shading, ts_models, max_slots=1, policy=None, search=None):
+                                  shading, ts_models, max_slots=1, policy=None, search=None, kdo_max=None):
     """B rounds of draw_round_population in C (ag_replay_draw_population): numpy's draws and
     torch's (the LR-TS Thompson draws of src/Models.py:31, the fitted policies' rsample draws of
     src/Models.py:87-88 / :160-161) in the same order, with the same numbers, leaving both
     generators (rng and torch's global CPU generator) exactly where the Python loop leaves
     them. Returns ctx [E][B], part [P][B] int32, gamma_raw [P][B] (NaN where nothing is drawn)
     or None, u [B], ts_noise in the kernel's tile layout [P][ceil(B/64)][K*Do][64] or None,
-    policy_eps [P][B] float32 or None, gamma_grid [P][128][B] or None."""
+    policy_eps [P][B] float32 or None, gamma_grid [P][128][B] or None. kdo_max: the noise rows'
+    width K*Do (default: the largest model's)."""
     import ctypes
 
     from . import _lib
@@ -134,13 +135,16 @@ def draw_rounds_native_population(rng, B, num_agents, num_participants, embeddin
         pg = np.array([x[0] if x is not None else 0.0 for x in shading], np.float64)
         gs = np.array([x[1] if x is not None else 1.0 for x in shading], np.float64)
         g = np.empty((P, B))
+    kdo = None
     if ts is not None:
-        m0 = next(m for m in ts_models if m is not None)
-        KDo = int(m0.q.numel())
+        # an agent's own K*Do (src/main.py:61,66: per-agent num_items); the noise rows of the
+        # largest model's width, an agent's draws in its first K_a*Do coefficients
+        kdo = np.array([int(m.q.numel()) if m is not None else 0 for m in ts_models], np.int32)
+        KDo = int(kdo_max) if kdo_max else int(kdo.max())
         std = np.zeros((N, KDo), np.float32)
         for a, m in enumerate(ts_models):
             if m is not None:
-                std[a] = (1.0 / torch.sqrt(m.q)).numpy().ravel()  # as src/Models.py:31 computes it
+                std[a, :kdo[a]] = (1.0 / torch.sqrt(m.q)).numpy().ravel()  # as src/Models.py:31 computes it
         noise = np.empty((P, (B + 63) // 64, KDo, 64), np.float32)
     if pol is not None:
         eps = np.empty((P, B), np.float32)
@@ -153,7 +157,7 @@ def draw_rounds_native_population(rng, B, num_agents, num_participants, embeddin
     L = _lib.load()
     _lib.check(L.ag_replay_draw_population(ctypes.byref(c), ptr(blob), 0 if blob is None else blob.size, B, N, P, E,
                                            float(embedding_var), int(max_slots), ptr(sh), ptr(pg), ptr(gs), ptr(ts),
-                                           ptr(std), KDo, ptr(pol), ptr(sea), ptr(ctx), ptr(part), ptr(g), ptr(u),
+                                           ptr(std), KDo, ptr(kdo), ptr(pol), ptr(sea), ptr(ctx), ptr(part), ptr(g), ptr(u),
                                            ptr(noise), ptr(eps), ptr(grid)), "ag_replay_draw_population", L)
     _pcg_out(rng, st, c)
     if blob is not None:
@@ -162,7 +166,7 @@ def draw_rounds_native_population(rng, B, num_agents, num_participants, embeddin
 
 
 def draw_round_population(rng, num_agents, num_participants, embedding_size, embedding_var,
-                          shading, ts_models, max_slots=1, policy=None, search=None):
+                          shading, ts_models, max_slots=1, policy=None, search=None, kdo_max=None):
     """One round of a general population. shading[a] = (prev_gamma, gamma_sigma) of a shading
     bidder in its uninitialised state (else None); ts_models[a] = the LR-TS model whose
     Thompson draw the round makes (else None); policy[a] = True for a learning bidder bidding
@@ -185,8 +189,8 @@ def draw_round_population(rng, num_agents, num_participants, embedding_size, emb
         if m is not None:  # Agent.select_item: the allocator's Thompson draw first
             z = m.sample_noise().numpy().ravel()
             if noise is None:
-                noise = np.zeros((num_participants, z.size), np.float32)
-            noise[s] = z
+                noise = np.zeros((num_participants, kdo_max or z.size), np.float32)
+            noise[s, :z.size] = z  # an agent with fewer items: its rows first, zeros after
         if policy is not None and policy[a]:  # then the bidder's
             if eps is None:
                 eps = np.zeros(num_participants, np.float32)

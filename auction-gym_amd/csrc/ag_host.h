@@ -108,6 +108,8 @@ struct ag_ctx {
   uint64_t fit_noise_seed = 0;                   // AG_OPT_FIT_NOISE_SEED
   ag_dr_ws dr;
   int32_t *d_akind = nullptr, *d_bkind = nullptr;
+  int32_t *d_kag = nullptr;    // [N] each agent's own item count (ag_set_agent_items); lazily allocated
+  bool ragged = false;         // some agent has fewer than K items
   double *d_pg = nullptr, *d_gs = nullptr;
   float *d_tsm = nullptr, *d_tsq = nullptr, *d_tsprev = nullptr;  // LR-TS m, q, prev_iter_m
   ag_lrts_ws lrts;

@@ -523,8 +523,8 @@ int simulate_pop(ag_ctx *c, int64_t B, const ag_batch_in *in, const ag_batch_out
                  hipStream_t st) {
   const ag_shape &s = c->shape;
   constexpr int K = 12, D = 6, DO = 5;  // the instantiated shape (ag_sim_p.hip pick_pop_for)
-  if (c->D != D || s.num_items != K || s.obs_embedding_size + 1 != DO || s.num_participants > kMaxP)
-    return AG_ERR_UNSUPPORTED;
+  if (c->D != D || s.num_items != K || s.obs_embedding_size + 1 != DO || s.num_participants > kMaxP || c->ragged)
+    return AG_ERR_UNSUPPORTED;  // (per-agent item counts: k_simulate)
   const int mode = (c->has_shading || c->gen_mode_all) ? kGenAll : kGenTruthful;
   const bool counters = counters_fx != nullptr;
   // workgroup size: 256 lanes while the LDS image (agent records + >= 16 counter replicas)
@@ -752,6 +752,7 @@ int ag_destroy(ag_ctx *c) {
   (void)hipFree(c->d_partials);
   (void)hipFree(c->d_akind);
   (void)hipFree(c->d_bkind);
+  (void)hipFree(c->d_kag);
   (void)hipFree(c->d_pg);
   (void)hipFree(c->d_gs);
   (void)hipFree(c->d_tsm);
@@ -763,6 +764,26 @@ int ag_destroy(ag_ctx *c) {
   delete[] c->h_akind;
   delete[] c->h_bkind;
   delete c;
+  return AG_OK;
+}
+
+int ag_set_agent_items(ag_ctx *c, const int32_t *num_items) {
+  if (!c) return ag_set_error(AG_ERR_INVALID, "ag_set_agent_items: null ctx");
+  const int N = c->shape.num_agents, K = c->shape.num_items;
+  bool ragged = false;
+  for (int a = 0; num_items && a < N; ++a) {
+    if (num_items[a] < 1 || num_items[a] > K)
+      return ag_set_error(AG_ERR_INVALID, "ag_set_agent_items: agent %d has %d items, not in [1, K = %d]", a,
+                          num_items[a], K);
+    ragged |= num_items[a] < K;
+  }
+  AgDeviceGuard g(c->device);
+  if (ragged) {
+    if (!c->d_kag) AG_HIP(hipMalloc(&c->d_kag, sizeof(int32_t) * N));
+    AG_HIP(hipMemcpy(c->d_kag, num_items, sizeof(int32_t) * N, hipMemcpyHostToDevice));
+  }
+  c->ragged = ragged;
+  c->image_dirty = true;
   return AG_OK;
 }
 
@@ -995,6 +1016,7 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   prm.tsm = c->d_tsm;
   prm.drs = c->dr_loaded ? c->dr.state : nullptr;
   prm.dri = c->dr_loaded ? c->dr.init : nullptr;
+  prm.kag = c->ragged ? c->d_kag : nullptr;
   prm.items = c->d_items;
   prm.values = c->d_values;
   prm.in = *in;

@@ -412,7 +412,8 @@ extern "C" int ag_replay_draw_population(ag_pcg64_state *rng, uint8_t *torch_sta
                                          int64_t B, int32_t N, int32_t P, int32_t E, double embedding_var,
                                          int32_t max_slots, const uint8_t *shading, const double *prev_gamma,
                                          const double *gamma_sigma, const uint8_t *ts, const float *ts_std,
-                                         int32_t KDo, const uint8_t *policy, const uint8_t *search, double *ctx,
+                                         int32_t KDo, const int32_t *ts_kdo, const uint8_t *policy,
+                                         const uint8_t *search, double *ctx,
                                          int32_t *part, double *gamma_raw, double *u, float *ts_noise,
                                          float *policy_eps, double *gamma_grid) {
   const char *who = "ag_replay_draw_population";
@@ -430,6 +431,9 @@ extern "C" int ag_replay_draw_population(ag_pcg64_state *rng, uint8_t *torch_sta
   if (ts && (!ts_std || !ts_noise || KDo < 16 || KDo > 4096))
     return ag_set_error(AG_ERR_INVALID, "%s: Thompson draws need ts_std, ts_noise and 16 <= K*Do <= 4096 "
                         "(torch's >= 16-element normal kernel)", who);
+  for (int a = 0; ts && ts_kdo && a < N; ++a)
+    if (ts[a] && (ts_kdo[a] < 16 || ts_kdo[a] > KDo))
+      return ag_set_error(AG_ERR_INVALID, "%s: agent %d's K*Do = %d not in [16, %d]", who, a, ts_kdo[a], KDo);
   if (policy && !policy_eps) return ag_set_error(AG_ERR_INVALID, "%s: policy draws need policy_eps", who);
   if (search && !gamma_grid) return ag_set_error(AG_ERR_INVALID, "%s: search draws need gamma_grid", who);
   Pcg64 st;
@@ -444,7 +448,7 @@ extern "C" int ag_replay_draw_population(ag_pcg64_state *rng, uint8_t *torch_sta
   if (ts) memset(ts_noise, 0, sizeof(float) * (size_t)P * (size_t)T * (size_t)KDo * 64);
   std::vector<int64_t> sample((size_t)P), arange;
   std::vector<uint64_t> hash_set;
-  const int NU = ts ? normal_fill_uniforms(KDo) : 0;
+  const int NU = ts ? KDo + 16 : 0;  // >= normal_fill_uniforms(n) for every n <= KDo
   std::vector<float> tsu(ts ? (size_t)B * P * NU : 0);  // the Thompson draws' uniforms, [B][P][NU]
   double grid[128];
   for (int64_t r = 0; r < B; ++r) {
@@ -462,7 +466,7 @@ extern "C" int ag_replay_draw_population(ag_pcg64_state *rng, uint8_t *torch_sta
       if (search)
         for (int i = 0; i < 128; ++i) gamma_grid[((int64_t)s * 128 + i) * B + r] = 0.0;
       if (ts && ts[a])  // Agent.select_item: the allocator's Thompson draw (src/Models.py:31)
-        torch_normal_fill_uniforms(tr, tsu.data() + ((size_t)r * P + s) * NU, KDo);  // transformed below
+        torch_normal_fill_uniforms(tr, tsu.data() + ((size_t)r * P + s) * NU, ts_kdo ? ts_kdo[a] : KDo);
       if (policy && policy[a]) {  // the bidder's rsample (src/Models.py:87-88, :160-161)
         policy_eps[(int64_t)s * B + r] = (float)torch_normal_double(tr);
         continue;
@@ -485,10 +489,11 @@ extern "C" int ag_replay_draw_population(ag_pcg64_state *rng, uint8_t *torch_sta
         for (int s = 0; s < P; ++s) {
           const int64_t a = part[(int64_t)s * B + r];
           if (!ts[a]) continue;
-          torch_normal_fill_transform(z.data(), tsu.data() + ((size_t)r * P + s) * NU, KDo);
+          const int n = ts_kdo ? ts_kdo[a] : KDo;  // the agent's own K*Do (its rows first)
+          torch_normal_fill_transform(z.data(), tsu.data() + ((size_t)r * P + s) * NU, n);
           const float *sd = ts_std + a * KDo;
           float *dst = ts_noise + (((int64_t)s * T + r / 64) * KDo) * 64 + (r % 64);
-          for (int i = 0; i < KDo; ++i) dst[(int64_t)i * 64] = z[(size_t)i] * sd[i] + 0.0f;  // .mul_(std).add_(0.0)
+          for (int i = 0; i < n; ++i) dst[(int64_t)i * 64] = z[(size_t)i] * sd[i] + 0.0f;  // .mul_(std).add_(0.0)
         }
     });
   rng->state_hi = (uint64_t)(st.state >> 64);

@@ -112,7 +112,7 @@ __device__ __forceinline__ unsigned long long to_fx(double x) {
 
 // LDS carve of k_simulate (all pieces 16-B aligned; offsets in bytes).
 struct LdsLayout {
-  int32_t tab, items, values, scr, scr_val, amax, akind, bkind, pg, gs, tsm, drs, dri, cnt, total;
+  int32_t tab, items, values, scr, scr_val, amax, akind, bkind, pg, gs, tsm, drs, dri, kag, cnt, total;
   int32_t items_stride;    // doubles between agents (odd: spreads agents over banks)
   int32_t values_stride;   // doubles
   int32_t scr_stride;      // floats between agents in the screening catalogue
@@ -179,6 +179,8 @@ __host__ inline LdsLayout make_layout(int N, int K, int D, bool counters, bool g
   b = L.drs + (general ? (int64_t)N * 16 * 4 : 0);
   L.dri = align16(b);
   b = L.dri + (general ? (int64_t)N * 4 : 0);
+  L.kag = align16(b);
+  b = L.kag + (general ? (int64_t)N * 4 : 0);
   L.cnt = align16(b);
   b = L.cnt + (counters ? (int64_t)R * N * L.ncnt * 8 : 0);
   L.total = align16(b);
@@ -208,6 +210,7 @@ struct SimParams {
   const float *tsm;       // general: [N][K][OE+1] LR-TS posterior means
   const float *drs;       // general: [N][16] DoublyRobustBidder models (NULL: none)
   const int32_t *dri;     // general: [N] fitted policy flags
+  const int32_t *kag;     // general: [N] each agent's own item count (NULL: all K)
   ag_batch_in in;
   ag_batch_out out;
   int64_t *partials;      // [grid][N][AG_NUM_COUNTERS][2]
@@ -376,6 +379,7 @@ struct Lds {
   int ts_do;
   const float *drs;
   const int32_t *dri;
+  const int32_t *kag;  // general: each agent's own item count (src/main.py:61,66)
 };
 
 // One auction resolved (src/Auction.py:28-74 minus the draws).
@@ -690,8 +694,11 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
       float xo[D];
 #pragma unroll
       for (int d = 0; d < D; ++d) xo[d] = d < Do - 1 ? (float)x[d] : (d == Do - 1 ? 1.0f : 0.0f);
-      best = ts_select<D>(m, xo, nz, K, Do, T.vals + a * T.values_stride, T.tab);
-      est = (double)ts_ctr_k<D>(m + best * Do, xo, xo, false, Do, best, K, T.tab);
+      // the agent's own Ka items: its torch model's rows (the sgemv block / remainder rows and
+      // the sigmoid's chunks follow Ka); the catalogue rows beyond are padding (value 0)
+      const int Ka = T.kag[a];
+      best = ts_select<D>(m, xo, nz, Ka, Do, T.vals + a * T.values_stride, T.tab);
+      est = (double)ts_ctr_k<D>(m + best * Do, xo, xo, false, Do, best, Ka, T.tab);
       tru = best == best_t ? c : agexp::sigmoid_fast(dot_ref<D>(itm + best * D, x), T.tab);
     }
   }
@@ -799,6 +806,7 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
   float *s_tsm = reinterpret_cast<float *>(smem + L.tsm);
   float *s_drs = reinterpret_cast<float *>(smem + L.drs);
   int32_t *s_dri = reinterpret_cast<int32_t *>(smem + L.dri);
+  int32_t *s_kag = reinterpret_cast<int32_t *>(smem + L.kag);
   unsigned long long *s_cnt = reinterpret_cast<unsigned long long *>(smem + L.cnt);
 
   const int tid = threadIdx.x;
@@ -808,6 +816,7 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
       s_bkind[a] = prm.bkind[a];
       s_pg[a] = prm.pg[a];
       s_gs[a] = prm.gs[a];
+      s_kag[a] = prm.kag ? prm.kag[a] : K;
     }
     for (int j = tid; j < N * K * L.ts_do; j += BT) s_tsm[j] = prm.tsm[j];
     if (prm.drs) {
@@ -851,7 +860,7 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
 
   const Lds T{s_tab, s_items, s_vals, s_scr, s_scr_val, s_amax, L.items_stride, L.values_stride,
               L.scr_stride, L.scr_val_stride, L.kpairs, s_akind, s_bkind, s_pg, s_gs, s_tsm, L.ts_do,
-              (GENERAL && prm.drs) ? s_drs : nullptr, s_dri};
+              (GENERAL && prm.drs) ? s_drs : nullptr, s_dri, GENERAL ? s_kag : nullptr};
   const int rep = tid & (R - 1);
   const ag_batch_in in = prm.in;
   const ag_batch_out out = prm.out;

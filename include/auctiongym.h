@@ -189,6 +189,15 @@ int ag_set_agent_kinds(ag_ctx *ctx, const int32_t *allocator_kind, const int32_t
 int ag_set_agent_params(ag_ctx *ctx, const int32_t *allocator_kind, const int32_t *bidder_kind,
                         const double *prev_gamma, const double *gamma_sigma);
 
+/* Each agent's own item count (src/main.py:61,66 num_items per agent config; Agent.__init__):
+ * host int32 [N], each in [1, K], K = ag_shape.num_items the largest. The catalogue
+ * (ag_load_catalog) and LR-TS models (ag_load_lrts) stay [N][K][...]: an agent's rows beyond
+ * its count are padding, values 0 (never the first argmax of CTR * value) and LR-TS rows 0 (no
+ * samples reach them: the update leaves them 0). The general kernel scores an LR-TS agent's
+ * Thompson choice over its own rows (the sgemv block / remainder rows follow its count).
+ * NULL: every agent has K. */
+int ag_set_agent_items(ag_ctx *c, const int32_t *num_items);
+
 /* LR-TS posterior of every AG_ALLOCATOR_LRTS agent, host float32 [N][K][OE+1] m, q and
  * prev_m (PyTorchLogisticRegression.m / .q / .prev_iter_m, src/Models.py:21-24; rows of
  * other agents ignored; prev_m NULL = m, as at construction); thompson_sampling: add the
@@ -355,7 +364,9 @@ int ag_replay_draw(ag_pcg64_state *rng, int64_t B, int32_t N, int32_t P, int32_t
  * K*Do % 16 != 0; glibc logf / cosf / sinf) times ts_std; rsample = normal_distribution
  * <double> with its cached second value (glibc log1p / cos / sin). Per agent [N]: shading
  * (uint8, with prev_gamma / gamma_sigma), ts (uint8, with ts_std [N][KDo] = 1/sqrt(q) as
- * torch computes it), policy (uint8), search (uint8); each may be NULL (none). Outputs:
+ * torch computes it; ts_kdo [N] int32: an agent's own K*Do when it has fewer items than K --
+ * ag_set_agent_items -- its draws fill the first ts_kdo[a] coefficients; NULL: all KDo),
+ * policy (uint8), search (uint8); each may be NULL (none). Outputs:
  * ctx, part, u, gamma_raw as ag_replay_draw; ts_noise in the kernel's tile layout
  * [P][ceil(B/64)][KDo][64] (ag_batch_in.ts_noise, zeros where nothing is drawn) when ts;
  * policy_eps [P][B] float (0 where nothing is drawn) when policy; gamma_grid [P][128][B]
@@ -364,9 +375,9 @@ int ag_replay_draw(ag_pcg64_state *rng, int64_t B, int32_t N, int32_t P, int32_t
 int ag_replay_draw_population(ag_pcg64_state *rng, uint8_t *torch_state, int64_t torch_state_bytes, int64_t B,
                               int32_t N, int32_t P, int32_t E, double embedding_var, int32_t max_slots,
                               const uint8_t *shading, const double *prev_gamma, const double *gamma_sigma,
-                              const uint8_t *ts, const float *ts_std, int32_t KDo, const uint8_t *policy,
-                              const uint8_t *search, double *ctx, int32_t *part, double *gamma_raw, double *u,
-                              float *ts_noise, float *policy_eps, double *gamma_grid);
+                              const uint8_t *ts, const float *ts_std, int32_t KDo, const int32_t *ts_kdo,
+                              const uint8_t *policy, const uint8_t *search, double *ctx, int32_t *part,
+                              double *gamma_raw, double *u, float *ts_noise, float *policy_eps, double *gamma_grid);
 
 /* ---- LR-TS allocator update (Agent.update -> PyTorchLogisticRegressionAllocator.update,
  * src/Agent.py:79-91, src/BidderAllocation.py:29-65) ------------------------------------

@@ -225,20 +225,23 @@ static void simulate_range(const ora_pop *pp, const double *items, const double 
         est = ctr_t;
         tru = ctr_t;
       } else { /* LR-TS: sampled CTRs pick the item, the MAP CTR of it is the estimate */
+        /* the agent's own model: its Ka items (the sgemv block / remainder rows and the
+         * sigmoid's chunks follow Ka, the tensor torch sees) */
+        const int32_t Ka = pp->num_items ? pp->num_items[a] : K;
         const float *m = pp->ts_m + (int64_t)a * K * Do;
         const float *nz = in->ts_noise + o * K * Do;
         float w[64];
         double best_s = 0.0;
         it = 0;
-        for (int32_t k = 0; k < K; ++k) {
+        for (int32_t k = 0; k < Ka; ++k) {
           for (int32_t d = 0; d < Do; ++d) w[d] = m[k * Do + d] + (pp->ts_sample ? nz[k * Do + d] : 0.0f);
-          const double sc = (double)ora_ts_ctr(w, xo, Do, k, K) * v_a[k];
+          const double sc = (double)ora_ts_ctr(w, xo, Do, k, Ka) * v_a[k];
           if (k == 0 || sc > best_s) {
             best_s = sc;
             it = k;
           }
         }
-        est = (double)ora_ts_ctr(m + it * Do, xo, Do, it, K);
+        est = (double)ora_ts_ctr(m + it * Do, xo, Do, it, Ka);
         tru = it == it_t ? ctr_t : ora_sigmoid(ora_dot(it_a + (int64_t)it * D, x, D));
       }
       const double v = v_a[it];
@@ -358,7 +361,7 @@ void ora_simulate(const ora_shape *s, const double *items, const double *values,
                   double *counters, int64_t *counters_fx, int32_t nthreads) {
   int32_t *ak = (int32_t *)calloc((size_t)s->N, sizeof(int32_t));
   int32_t *bk = (int32_t *)calloc((size_t)s->N, sizeof(int32_t));
-  ora_pop pp = {s->N, s->P, s->K, s->E, s->E, s->mech, ak, bk, NULL, NULL, NULL, 0, NULL, NULL};
+  ora_pop pp = {s->N, s->P, s->K, s->E, s->E, s->mech, ak, bk, NULL, NULL, NULL, 0, NULL, NULL, NULL};
   ora_in in = {ctx, part, u, NULL, NULL, NULL, NULL};
   ora_out out = {winner, price, second_price, outcome, item, value, bid, est_ctr, true_ctr,
                  best_ev, NULL, NULL};

@@ -36,7 +36,7 @@ class _Pop(ctypes.Structure):
                 ("alloc_kind", ctypes.c_void_p), ("bid_kind", ctypes.c_void_p),
                 ("prev_gamma", ctypes.c_void_p), ("gamma_sigma", ctypes.c_void_p),
                 ("ts_m", ctypes.c_void_p), ("ts_sample", ctypes.c_int32),
-                ("dr_state", ctypes.c_void_p), ("dr_init", ctypes.c_void_p)]
+                ("dr_state", ctypes.c_void_p), ("dr_init", ctypes.c_void_p), ("num_items", ctypes.c_void_p)]
 
 
 class _In(ctypes.Structure):
@@ -163,9 +163,11 @@ def simulate(mech, items, values, ctx, part, u, nthreads=1):
 
 def simulate_pop(mech, items, values, ctx, part, u, alloc_kind, bid_kind, prev_gamma=None,
                  gamma_sigma=None, OE=None, ts_m=None, ts_noise=None, gamma_raw=None,
-                 ts_sample=True, dr_state=None, dr_init=None, policy_eps=None, gamma_grid=None, nthreads=1):
+                 ts_sample=True, dr_state=None, dr_init=None, policy_eps=None, gamma_grid=None, nthreads=1,
+                 num_items=None):
     """General population (OracleAllocator / LR-TS allocators; truthful / shading bidders in
-    their first iteration). Row-major replay inputs; returns outputs + counters."""
+    their first iteration). Row-major replay inputs; returns outputs + counters. num_items [N]:
+    each agent's own item count (catalogues padded to K with value-0 rows), None: all K."""
     items = np.ascontiguousarray(items, np.float64)
     values = np.ascontiguousarray(values, np.float64)
     ctx = np.ascontiguousarray(ctx, np.float64)
@@ -194,8 +196,10 @@ def simulate_pop(mech, items, values, ctx, part, u, alloc_kind, bid_kind, prev_g
     di = arr(dr_init if dr_init is not None else np.zeros(N), np.int32)
     pe = arr(policy_eps if policy_eps is not None else np.zeros((B, P)), np.float32)
     gg = arr(gamma_grid if gamma_grid is not None else np.zeros((1, 1, 128)), np.float64)
+    ni = arr(num_items, np.int32)
     pop = _Pop(N, P, K, E, OE, int(mech), ak.ctypes.data, bk.ctypes.data, pg.ctypes.data,
-               gs.ctypes.data, tm.ctypes.data, int(bool(ts_sample)), ds.ctypes.data, di.ctypes.data)
+               gs.ctypes.data, tm.ctypes.data, int(bool(ts_sample)), ds.ctypes.data, di.ctypes.data,
+               None if ni is None else ni.ctypes.data)
     out = dict(winner=np.empty(B, np.int32), price=np.empty(B), second_price=np.empty(B),
                outcome=np.empty(B, np.uint8), item=np.empty((B, P), np.int32),
                value=np.empty((B, P)), bid=np.empty((B, P)), est_ctr=np.empty((B, P)),

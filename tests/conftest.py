@@ -52,7 +52,8 @@ def gpu():
 
 
 POP_CAPTURES = ("sp_ts_r2048", "fp_dr_ts_r1024", "fp_dm_ts_r1024", "fp_ips_ts_r1024",
-                "fp_dm_oracle_r1024", "fp_empirical_r2048", "sp_ts_mixed_flags_r2048")
+                "fp_dm_oracle_r1024", "fp_empirical_r2048", "sp_ts_mixed_flags_r2048",
+                "ragged_items_r2048")
 
 
 def pop_args(d, meta):
@@ -60,4 +61,5 @@ def pop_args(d, meta):
     from auctiongym_amd.population import kinds_from_names
     ak, bk, pg, gs = kinds_from_names(meta["allocators"], meta["bidders"], meta["bidder_kwargs"])
     return dict(alloc_kind=ak, bid_kind=bk, prev_gamma=pg, gamma_sigma=gs, OE=meta["OE"],
-                ts_m=d.get("ts_m"), ts_noise=d.get("ts_noise"), gamma_raw=d["gamma_raw"])
+                ts_m=d.get("ts_m"), ts_noise=d.get("ts_noise"), gamma_raw=d["gamma_raw"],
+                num_items=meta.get("num_items"))

@@ -127,9 +127,16 @@ def capture(cfg, rounds, torch_seed=0, keep=False):
     N = len(agents)
     P = config["num_participants_per_round"]
     names = [a.name for a in agents]
-    items = np.stack([agents2items[n] for n in names])          # [N][K][D]
-    values = np.stack([agents2item_values[n] for n in names])   # [N][K]
-    K = items.shape[1]
+    # per-agent item counts (src/main.py:61,66): catalogues padded to the largest K with
+    # value-0 rows (num_items in the meta says which rows are the agent's own)
+    num_items = [len(agents2item_values[n]) for n in names]
+    K = max(num_items)
+    D = agents2items[names[0]].shape[1]
+    items = np.zeros((N, K, D))                                 # [N][K][D]
+    values = np.zeros((N, K))                                   # [N][K]
+    for i, n in enumerate(names):
+        items[i, :num_items[i]] = agents2items[n]
+        values[i, :num_items[i]] = agents2item_values[n]
     is_ts = [type(a.allocator).__name__ == "PyTorchLogisticRegressionAllocator" for a in agents]
     Do = None
     ts_m = ts_q = None
@@ -139,8 +146,8 @@ def capture(cfg, rounds, torch_seed=0, keep=False):
         ts_q = np.ones((N, K, Do), np.float32)
         for i, a in enumerate(agents):
             if is_ts[i]:
-                ts_m[i] = a.allocator.response_model.m.detach().numpy()
-                ts_q[i] = a.allocator.response_model.q.numpy()
+                ts_m[i, :num_items[i]] = a.allocator.response_model.m.detach().numpy()
+                ts_q[i, :num_items[i]] = a.allocator.response_model.q.numpy()
     shading = [hasattr(a.bidder, "prev_gamma") for a in agents]
 
     clone = np.random.Generator(np.random.PCG64())
@@ -200,7 +207,7 @@ def capture(cfg, rounds, torch_seed=0, keep=False):
             nts = [s_ for s_, a_ in enumerate(pa) if is_ts[a_] and agents[a_].allocator.thompson_sampling]
             assert len(noise_log) - n0 == len(nts)
             for j, s_ in enumerate(nts):
-                ts_noise[r, s_] = noise_log[n0 + j]
+                ts_noise[r, s_, :num_items[pa[s_]]] = noise_log[n0 + j]
             for s, a in enumerate(pa):
                 lg = agents[a].logs[-1]
                 rec["bid"][r, s] = lg.bid
@@ -259,7 +266,7 @@ def capture(cfg, rounds, torch_seed=0, keep=False):
                 allocators=[type(a.allocator).__name__ for a in agents],
                 bidders=[_bidder_kind(a.bidder) for a in agents],
                 bidder_kwargs=[c["bidder"]["kwargs"] for c in agent_configs],
-                ts_dim=Do)
+                ts_dim=Do, num_items=num_items)
     if keep:
         return arrays, agg, meta, (agents, auction, rng)
     return arrays, agg, meta
@@ -1000,6 +1007,28 @@ def csv_outputs(runs=2, iters=3, rounds=2000):
         print("csv", name, sorted(os.listdir(dst)), flush=True)
 
 
+def ragged_items_capture(out_name="ragged_items_r2048", rounds=2048):
+    """Agents with their own num_items (src/main.py:61,66): 3 Oracle agents with 12 items, 3
+    LR-TS (Thompson sampling) agents with 9, 2 with 6 and 1 with 13 -- the sgemv block /
+    remainder rows and the catalogue draw order follow each agent's count. The config travels
+    in the fixture's meta."""
+    cfg = load_cfg("SP_Truthful_TS.json")
+    base = cfg["agents"][0]
+    orc = {"type": "OracleAllocator", "kwargs": {}}
+
+    def lrts(k):
+        return {"type": base["allocator"]["type"], "kwargs": dict(base["allocator"]["kwargs"], num_items=k)}
+    cfg["agents"] = [dict(base, name="Oracle 12", num_copies=3, num_items=12, allocator=orc),
+                     dict(base, name="TS 9", num_copies=3, num_items=9, allocator=lrts(9)),
+                     dict(base, name="TS 6", num_copies=2, num_items=6, allocator=lrts(6)),
+                     dict(base, name="TS 13", num_items=13, allocator=lrts(13))]
+    cfg["agents"][3].pop("num_copies", None)
+    cfg["output_dir"] = "/tmp/ag_golden_unused/"
+    a, g, m = capture(cfg, rounds)
+    m["config"] = cfg
+    save_capture(out_name, a, g, m)
+
+
 def mixed_ts_flags_capture(out_name="sp_ts_mixed_flags_r2048", rounds=2048):
     """SP_Truthful_TS with thompson_sampling set per allocator (src/BidderAllocation.py:24-26):
     4 LR-TS agents sample, 4 bid from their MAP estimates (estimate_CTR(sample=False),
@@ -1020,12 +1049,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also run SP_Oracle as shipped (3x20x10k rounds, ~1 min)")
     ap.add_argument("--which", choices=["dm", "ips", "dr", "dmo", "search"], help="with --only learners/drivers: one config")
-    ap.add_argument("--only", choices=["empirical", "csv", "dr", "learners", "drivers", "memory", "later", "mixedts"],
+    ap.add_argument("--only", choices=["empirical", "csv", "dr", "learners", "drivers", "memory", "later", "mixedts", "ragged"],
                     help="regenerate one fixture family only")
     args = ap.parse_args()
     install_shims()
     if args.only == "mixedts":
         mixed_ts_flags_capture()
+        return
+    if args.only == "ragged":
+        ragged_items_capture()
         return
     if args.only == "memory":
         memory_driver_kat()

@@ -487,6 +487,8 @@ def _pop_engine(meta, d, gpu):
     eng = AuctionEngine(meta["N"], meta["P"], meta["K"], meta["E"], meta["OE"], mech_code(meta),
                         meta["var"])
     eng.set_agent_params(args["alloc_kind"], args["bid_kind"], args["prev_gamma"], args["gamma_sigma"])
+    if meta.get("num_items") and min(meta["num_items"]) < meta["K"]:
+        eng.set_agent_items(meta["num_items"])  # per-agent item counts (catalogue rows padded)
     eng.load_catalog(d["items"], d["values"])
     if args["ts_m"] is not None:
         eng.load_lrts(args["ts_m"], np.ones_like(args["ts_m"]), thompson_sampling=True)
@@ -1011,23 +1013,28 @@ SP_TRUTHFUL_TS = {  # config/SP_Truthful_TS.json as shipped
 
 
 @pytest.mark.parametrize("path", ["per_round", "batch"])
-def test_dropin_per_allocator_thompson_flags(gpu, tmp_path, path):
-    """thompson_sampling set per allocator (src/BidderAllocation.py:24-26): 4 LR-TS agents sample,
-    4 bid from their MAP estimates (tests/golden/sp_ts_mixed_flags_r2048, the reference's own
-    run). Through the drop-in classes, per round (simulate_opportunity: torch.normal for the
-    sampling agents only) and as one batch (simulate_batch: ag_replay_draw_population): the
-    reference's items per agent, utilities and revenue to the exact sums' 1e-11, and torch's
-    generator left where the per-round loop leaves it."""
+@pytest.mark.parametrize("name", ["sp_ts_mixed_flags_r2048", "ragged_items_r2048"])
+def test_dropin_surface_captures(gpu, tmp_path, path, name):
+    """Two surfaces the reference allows, through the drop-in classes against the reference's
+    own runs, per round (simulate_opportunity) and as one batch (simulate_batch:
+    ag_replay_draw_population): thompson_sampling set per allocator (src/BidderAllocation.py:
+    24-26; sp_ts_mixed_flags_r2048: 4 LR-TS agents sample, 4 bid from their MAP estimates), and
+    per-agent num_items (src/main.py:61,66; ragged_items_r2048: Oracle agents with 12 items,
+    LR-TS agents with 9, 6 and 13 -- catalogues padded, each LR-TS choice over the agent's own
+    rows, its torch draws of its own K*Do). The reference's items and estimated CTRs per agent,
+    utilities and revenue to the exact sums' 1e-11, and torch's generator left where the
+    reference's calls leave it."""
     import torch
 
     import auctiongym_amd.main as M
-    d, meta, agg = load_capture("sp_ts_mixed_flags_r2048")
+    d, meta, agg = load_capture(name)
     p = tmp_path / "cfg.json"
     p.write_text(json.dumps(meta["config"]))
     rng, config, agent_configs, a2i, a2v, _, max_slots, E, var, OE = M.parse_config(str(p))
     torch.manual_seed(meta["torch_seed"])
     agents = M.instantiate_agents(rng, agent_configs, a2v, a2i)
-    assert [a.allocator.thompson_sampling for a in agents] == [True] * 4 + [False] * 4
+    if name.startswith("sp_ts_mixed"):
+        assert [a.allocator.thompson_sampling for a in agents] == [True] * 4 + [False] * 4
     auction, _, _, _ = M.instantiate_auction(rng, config, a2i, a2v, agents, max_slots, E, var, OE)
     if path == "per_round":
         for _ in range(meta["rounds"]):
@@ -1043,13 +1050,17 @@ def test_dropin_per_allocator_thompson_flags(gpu, tmp_path, path):
         rows, slots = np.nonzero(d["part"] == i)
         assert [o.item for o in a.logs] == list(d["item"][rows, slots])
         np.testing.assert_array_equal([o.estimated_CTR for o in a.logs], d["slot_est_ctr"][rows, slots])
-    # the generator: 60 torch.normal values per sampling participation, none for the others
+    # the generator: the LR-TS agents' initial m (torch.nn.init.normal_ of [K_a][OE+1], agent
+    # order), then K_a*(OE+1) torch.normal values per sampling participation, in round order
     ref = torch.Generator().manual_seed(meta["torch_seed"])
-    for a in range(8):
-        torch.empty(12, 5).normal_(generator=ref)  # the agents' initial m (torch.nn.init.normal_)
-    n_ts = int(np.isin(d["part"], np.arange(4)).sum())
-    for _ in range(n_ts):
-        torch.empty(60).normal_(generator=ref)
+    kdo = [a.allocator.response_model.q.numel() if hasattr(a.allocator, "response_model") else 0 for a in agents]
+    for k in kdo:
+        if k:
+            torch.empty(k).normal_(generator=ref)
+    samp = [bool(k) and a.allocator.thompson_sampling for k, a in zip(kdo, agents)]
+    for a in d["part"].ravel():
+        if samp[a]:
+            torch.empty(kdo[a]).normal_(generator=ref)
     assert torch.equal(torch.get_rng_state(), ref.get_state())
 
 

@@ -165,7 +165,7 @@ class _TsModel:
         return torch.normal(mean=0.0, std=1.0 / torch.sqrt(self.q))
 
 
-@pytest.mark.parametrize("case", ["ts", "ts_policy", "mixed", "search", "ts_kdo_mult16", "ts_threads"])
+@pytest.mark.parametrize("case", ["ts", "ts_policy", "mixed", "search", "ts_kdo_mult16", "ts_threads", "ragged"])
 def test_replay_population_draws_match_python(case):
     """ag_replay_draw_population (C: torch's mt19937 CPU generator and its normal kernels
     restated, numpy's PCG64 and distributions) against the Python loop that makes the
@@ -181,6 +181,10 @@ def test_replay_population_draws_match_python(case):
     KDo = 64 if case == "ts_kdo_mult16" else 60
     gen = torch.Generator().manual_seed(5)
     qs = [torch.rand(KDo // 5 if KDo == 60 else 16, 5 if KDo == 60 else 4, generator=gen) * 3 + 0.05 for _ in range(N)]
+    kdo_max = None
+    if case == "ragged":  # per-agent num_items (src/main.py:61,66): models of 12, 9, 6, 13 rows
+        qs = [torch.rand((12, 9, 6, 13)[a % 4], 5, generator=gen) * 3 + 0.05 for a in range(N)]
+        kdo_max = KDo = 13 * 5
     ts = [_TsModel(qs[a]) if case != "search" and a % 3 != 1 else None for a in range(N)]
     policy = search = None
     shading = [None] * N
@@ -194,10 +198,11 @@ def test_replay_population_draws_match_python(case):
     torch.empty(1).normal_()  # a cached second normal on entry
     t0 = torch.get_rng_state()
     ctx, part, g, u, noise, eps, grid = draw_rounds_native_population(a_rng, B, N, P, E, 1.0, shading, ts, 1,
-                                                                      policy, search)
+                                                                      policy, search, kdo_max=kdo_max)
     t_native = torch.get_rng_state()
     torch.set_rng_state(t0)
-    rows = [draw_round_population(b_rng, N, P, E, 1.0, shading, ts, 1, policy, search) for _ in range(B)]
+    rows = [draw_round_population(b_rng, N, P, E, 1.0, shading, ts, 1, policy, search, kdo_max=kdo_max)
+            for _ in range(B)]
     assert torch.equal(torch.get_rng_state(), t_native)
     assert a_rng.bit_generator.state == b_rng.bit_generator.state
     z = np.zeros((B, P, KDo), np.float32)
