@@ -2020,3 +2020,17 @@ def test_pop_kernel_equals_general_kernel(gpu, oracle, case):
         assert np.array_equal(c0.cpu().numpy(), orc["counters_fx"])
     for e, *_ in runs:
         e.close()
+
+
+def test_agent_items_validation(gpu):
+    """ag_set_agent_items refuses counts outside [1, K] loudly (ValueError) and accepts NULL
+    (every agent has K); a padded catalogue with per-agent counts equal to K runs the plain path."""
+    from auctiongym_amd.engine import AuctionEngine
+    eng = AuctionEngine(4, 2, 12, 5, 4, 1)
+    with pytest.raises(ValueError):
+        eng.set_agent_items([12, 0, 5, 7])
+    with pytest.raises(ValueError):
+        eng.set_agent_items([12, 13, 5, 7])
+    eng.set_agent_items([12, 3, 5, 7])
+    eng.set_agent_items(None)
+    eng.close()
