@@ -28,6 +28,9 @@ namespace ag {
 #ifndef AG_GEN_MIN_WAVES
 #define AG_GEN_MIN_WAVES 3  // the general kernel: <= 168 VGPRs
 #endif
+#ifndef AG_GEN_DOS_MIN_WAVES
+#define AG_GEN_DOS_MIN_WAVES 3  // the full general build with the LR-TS width compile-time (DOS), P <= 2
+#endif
 #ifndef AG_TB_MIN_WAVES
 #define AG_TB_MIN_WAVES 4  // the general kernel for truthful bidders only: <= 128 VGPRs
 #endif
@@ -786,7 +789,8 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
 // fully and spill (200 VGPRs at P = 2), measured.
 template <int P, int D, bool PRUNE, int W, int GENERAL, int BT = kThreads, int DOS = 0>
 __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
-                                 : (GENERAL ? AG_GEN_MIN_WAVES : AG_MIN_WAVES)) void k_simulate(SimParams prm) {
+                                 : (GENERAL ? ((DOS && P > 0 && P <= 2) ? AG_GEN_DOS_MIN_WAVES : AG_GEN_MIN_WAVES)
+                                            : AG_MIN_WAVES)) void k_simulate(SimParams prm) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = prm.N, K = prm.K;
   const uint32_t B = (uint32_t)prm.B;  // SoA leading dimension (auctions in the batch)
