@@ -29,7 +29,10 @@ namespace ag {
 #define AG_GEN_MIN_WAVES 3  // the general kernel: <= 168 VGPRs
 #endif
 #ifndef AG_GEN_DOS_MIN_WAVES
-#define AG_GEN_DOS_MIN_WAVES 3  // the full general build with the LR-TS width compile-time (DOS), P <= 2
+#define AG_GEN_DOS_MIN_WAVES 4  // the full general build with the LR-TS width compile-time (DOS), P <= 2:
+                                // 128 VGPRs (3 spilled) at 4 waves per SIMD instead of 140 at 3 --
+                                // configs_2 0.212 -> 0.203 ms, configs_3 0.129 -> 0.121 ms in one
+                                // process (profiles/r03s11_ab_w4.log)
 #endif
 #ifndef AG_TB_MIN_WAVES
 #define AG_TB_MIN_WAVES 4  // the general kernel for truthful bidders only: <= 128 VGPRs
