@@ -223,7 +223,10 @@ class Auction:
         shading, models, policy, search = self._population_draws()
         torch_or_grid = (any(m is not None for m in models) or (policy is not None and any(policy))
                          or (search is not None and any(search)))
-        step = self.NATIVE_ROUNDS_TS if (self._lrts.any() and self._ts) else self.NATIVE_ROUNDS
+        # Thompson draws hold P * (K*Do + 16) floats of uniforms per round on the host before the
+        # transforms (plus the tiled noise): bounded per chunk, whatever P
+        step = (max(1 << 12, (self.NATIVE_ROUNDS_TS * 2) // P) if (self._lrts.any() and self._ts)
+                else self.NATIVE_ROUNDS)
         d = self._engine.device
         for lo in range(0, B, step):
             n = min(step, B - lo)
