@@ -913,7 +913,7 @@ int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
       c->ship_shape = value == 1;
       return AG_OK;
     case AG_OPT_SIMULATE_KERNEL:
-      if (value < AG_SIM_KERNEL_AUTO || value > AG_SIM_KERNEL_SPLIT)
+      if (value < AG_SIM_KERNEL_AUTO || value > AG_SIM_KERNEL_WIDE)
         return ag_set_error(AG_ERR_INVALID, "ag_set_option: bad simulate kernel %lld", (long long)value);
       c->sim_kernel = (int32_t)value;
       return AG_OK;
@@ -1058,6 +1058,10 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   if (!k && bt != kThreads) {
     bt = kThreads;
     k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
+  }
+  if (c->general && c->sim_kernel == AG_SIM_KERNEL_WIDE) {  // the runtime-P kernel at any P (A/B)
+    bt = kThreads;
+    k = pick_kernel_for<0>(D, prune, 1, kGenAll, kThreads);
   }
   if (!k) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: no kernel for P=%d D=%d", s.num_participants, D);
   if (gmode == kGenAll && bt == kLargeThreads) {  // the compacted fitted-policy pass's per-wave task slots

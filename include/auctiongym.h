@@ -248,10 +248,13 @@ typedef enum ag_sim_kernel {
   AG_SIM_KERNEL_GENERIC = 1, /* always the general simulate kernel (A/B and parity tests) */
   AG_SIM_KERNEL_FUSED = 2,   /* general populations of the shipped shape (K = 12, E = 5, OE = 4):
                                 the dedicated kernel k_pop making its Thompson choices itself */
-  AG_SIM_KERNEL_SPLIT = 3    /* ... the split pass, k_ts_choice then k_pop. FUSED / SPLIT are
+  AG_SIM_KERNEL_SPLIT = 3,   /* ... the split pass, k_ts_choice then k_pop. FUSED / SPLIT are
                                 A/B and parity variants (identical results); AUTO runs the
                                 general kernel (faster at P = 2 on every population line),
                                 the split pass for TruthfulBidder-only populations at P >= 8 */
+  AG_SIM_KERNEL_WIDE = 4     /* general populations: the runtime-P kernel (slot results not
+                                kept in registers, resolved again for the counters) at any P;
+                                A/B of wide auctions, identical results */
 } ag_sim_kernel;
 
 typedef enum ag_item_search {

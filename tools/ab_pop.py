@@ -30,7 +30,7 @@ def main():
         key, P = key.split(":")[0], int(key.split(":")[1])
     vdir = os.path.join(ROOT, "auction-gym_amd", "build", "variants")
     paths = {"base": _lib.LIB_PATH}
-    special = {"generic", "fused", "split", "bt256", "bt1024", "nocnt", "noship"}
+    special = {"generic", "fused", "split", "wide", "bt256", "bt1024", "nocnt", "noship"}
     for n in sys.argv[2:]:
         paths[n] = _lib.LIB_PATH if n in special else os.path.join(vdir, f"libauctiongym_hip_{n}.so")
     base_path = _lib.LIB_PATH
@@ -54,7 +54,7 @@ def main():
         else:
             eng, what, B, ak, bk, st16, dims = bench.build_population(key, 0, P=P)
             eng.set_dr_state(st16, np.where(bk >= 2, 1, 0).astype(np.int32))
-        if n in ("generic", "fused", "split"):
+        if n in ("generic", "fused", "split", "wide"):
             eng.set_simulate_kernel(True if n == "generic" else n)
         if n == "noship":  # k_simulate's runtime-shape build
             eng._check(eng.L.ag_set_option(eng._h, _lib.OPT_SIM_SHIPPED_SHAPE, 0), "ag_set_option")
