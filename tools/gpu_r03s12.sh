@@ -1,7 +1,7 @@
 #!/bin/bash
 # r03s12: the round's final build -- smoke, GPU suite, the driver-shaped bench line.
 set -u
-OUT=gpurun_out/prof_r03s12
+OUT=gpurun_out/prof_${TAG:-r03s12}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "rc=$rc"; tail -n 2 "$OUT/$name.log" | cut -c1-200; if [ $rc -ne 0 ]; then exit $rc; fi; }
