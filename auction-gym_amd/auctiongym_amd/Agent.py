@@ -133,7 +133,7 @@ class Agent:
         (ag_lrts_update), EmpiricalShadedBidder (ag_empirical_update) and the learning bidders
         (ag_bidder_update) on all of its records."""
         self._sync()
-        if self._call_logs:
+        if self._call_logs or self._kept_calls is not None:
             if self._auction is not None:
                 raise NotImplementedError(
                     "Agent.update on per-call Agent.bid records of an agent that also takes part in a "
@@ -219,10 +219,10 @@ class Agent:
             if self._kept_calls is not None:
                 cols = concat_columns(self._kept_calls, cols)
             self._kept_calls = take_last(cols, self.memory) if self.memory else None
-            if self._kept_calls is not None:
-                terms = log_counter_terms(self._kept_calls, True, True)
-                for i in _LOGS:
-                    self._fx[i] += terms.get(i, 0)
+        if self._kept_calls is not None:  # kept records stay in the metrics, new ones or not
+            terms = log_counter_terms(self._kept_calls, True, True)
+            for i in _LOGS:
+                self._fx[i] += terms.get(i, 0)
         self._call_logs = []
         self.bidder.clear_logs(memory=self.memory)
 

@@ -196,11 +196,26 @@ class Auction:
             search = [x == _lib.LEARNER_SEARCH for x in ls]
         return shading, models, policy, search
 
+    # torch CPU builds whose float normal_ of >= 16 elements runs normal_fill_16_AVX2 (the
+    # kernel ag_replay.cpp restates: compiled under __AVX2__, which the AVX512 build defines
+    # too); the DEFAULT build takes the scalar normal_fill with libm logf / cosf
+    _TORCH_NORMAL_AVX2 = ("AVX2", "AVX512")
+
     def _native_draws(self):
         """True when the draws can be made in C for a whole batch: numpy's Generator on PCG64
         (ag_replay_draw / ag_replay_draw_population restate it, and torch's CPU generator for
-        the Thompson and rsample draws)."""
-        return isinstance(self.rng.bit_generator, np.random.PCG64)
+        the Thompson and rsample draws). Thompson draws are restated for torch's >= 16-element
+        vectorised normal kernel only: a sampling LR-TS agent with K*(OE+1) < 16 (torch's
+        scalar path) or a torch build without that kernel keeps the per-round loop."""
+        if not isinstance(self.rng.bit_generator, np.random.PCG64):
+            return False
+        if self._lrts.any() and self._ts:
+            if torch.backends.cpu.get_cpu_capability() not in self._TORCH_NORMAL_AVX2:
+                return False
+            kdo = self._num_items * (self.obs_embedding_size + 1)
+            if (kdo[self._ts_agent] < 16).any():
+                return False
+        return True
 
     NATIVE_ROUNDS = 1 << 20
     NATIVE_ROUNDS_TS = 1 << 18  # Thompson noise: P * K*(OE+1) floats per round on the host

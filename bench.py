@@ -124,10 +124,11 @@ def timed(fn, min_seconds, max_passes=40):
     return n, time.perf_counter() - t0, out
 
 
-def cpu_baseline_population(eng, items, values, inp, out, ak, bk, st16, init, sample, threads, min_seconds=3.0):
-    """The oracle's restatement of the general-population round (oracle.simulate_pop, the C
-    build of the reference path; OpenMP over `threads`) on the first `sample` auctions of the
-    GPU's own inputs: auctions/s, and whether its outputs equal the GPU's on that sample."""
+def oracle_population_args(eng, items, values, inp, ak, bk, st16, init, sample, threads):
+    """The oracle's (oracle.simulate_pop) arguments for the first `sample` auctions of a
+    population batch resident on the GPU: the same inputs, LR-TS posteriors, Thompson noise
+    (compact layouts expanded to dense), shading / rsample draws and fitted models. Returns
+    (O, args, kwargs)."""
     O = _oracle()
     T = lambda t: np.ascontiguousarray(t[..., :sample].cpu().numpy().T)  # noqa: E731
     B = inp["u"].shape[0]
@@ -138,13 +139,22 @@ def cpu_baseline_population(eng, items, values, inp, out, ak, bk, st16, init, sa
         tn = (eng.compact_to_dense_ts_noise(inp["ts_noise"], inp["ts_noise_index"], P, B)
               if "ts_noise_index" in inp else inp["ts_noise"])
         kw["ts_noise"] = np.ascontiguousarray(eng.untile_ts_noise(tn, B)[:sample].reshape(sample, P, K, OE + 1))
+        del tn
     if "gamma_raw" in inp:
         kw["gamma_raw"] = T(inp["gamma_raw"])
     if "policy_eps" in inp:
         kw.update(policy_eps=T(inp["policy_eps"]), dr_state=st16, dr_init=init)
     ctx, part, u = T(inp["ctx"]), T(inp["part"]), inp["u"][:sample].cpu().numpy()
     pg, gs = np.ones(N), np.full(N, 0.02)
-    fn = lambda: O.simulate_pop(eng.mechanism, items, values, ctx, part, u, ak, bk, pg, gs, **kw)  # noqa: E731
+    return O, (eng.mechanism, items, values, ctx, part, u, ak, bk, pg, gs), kw
+
+
+def cpu_baseline_population(eng, items, values, inp, out, ak, bk, st16, init, sample, threads, min_seconds=3.0):
+    """The oracle's restatement of the general-population round (oracle.simulate_pop, the C
+    build of the reference path; OpenMP over `threads`) on the first `sample` auctions of the
+    GPU's own inputs: auctions/s, and whether its outputs equal the GPU's on that sample."""
+    O, args, kw = oracle_population_args(eng, items, values, inp, ak, bk, st16, init, sample, threads)
+    fn = lambda: O.simulate_pop(*args, **kw)  # noqa: E731
     fn()  # warm
     passes, dt, o = timed(fn, min_seconds)
     same = all(np.array_equal(out[k][..., :sample].cpu().numpy().T if out[k].dim() == 2 else
@@ -277,22 +287,20 @@ def gpu_record_epochs(counts, epochs, ms):
     return work / (ms * 1e-3)
 
 
-def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True, cpu_threads=0, P=None):
-    """configs[1]: SP_Truthful_TS, 8 LR-TS truthful bidders, 1M auctions per GPU, SecondPrice.
-    Inputs (contexts, participants, uniforms AND the Thompson noise z / sqrt(q) of both
-    participants) generated on the GPU and resident in HBM; initial models as
-    src/Models.py:21-24 (m ~ N(0,1) from torch seeded 0, q = 1). One step = ag_simulate.
-    Then one Agent.update of all 8 agents on the last batch's won samples (collect + the
-    GPU training loop), timed separately (the reference: 14.3 s per 10k-round iteration)."""
+def build_sp_ts(B, local, P=None, world=1, rank=0):
+    """configs[1]'s engine and resident inputs (what run_sp_ts times and what the configs tests
+    check against the oracle): SP_Truthful_TS, 8 LR-TS truthful bidders, SecondPrice; initial
+    models as src/Models.py:21-24 (m ~ N(0,1) from torch seeded 0, q = 1); contexts,
+    participants, uniforms and the Thompson noise of every participant generated on the GPU
+    for this rank's shard. Returns (eng, inp, out, cnt, dims)."""
     from auctiongym_amd import _lib
     from auctiongym_amd.engine import AuctionEngine
-    from auctiongym_amd.sharding import allreduce_counters, shard_range
+    from auctiongym_amd.sharding import shard_range
     items, values = catalogue(SP_TS)
     N, K, D = items.shape
     E, OE = D - 1, SP_TS["obs_embedding_size"]
     P = P or SP_TS["num_participants_per_round"]
     Do = OE + 1
-    dev = torch.device("cuda", local)
     eng = AuctionEngine(N, P, K, E, OE, _lib.SECOND_PRICE, SP_TS["embedding_var"], device=local)
     eng.set_agent_params(np.ones(N, np.int32), np.zeros(N, np.int32))
     eng.load_catalog(items, values)
@@ -308,8 +316,24 @@ def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True, cpu_thread
     out = eng.alloc_outputs(B)
     cnt = eng.new_counters()
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
+    dims = dict(N=N, K=K, E=E, P=P, OE=OE, Do=Do, items=items, values=values, lo=lo,
+                ak=np.ones(N, np.int32), bk=np.zeros(N, np.int32))
+    return eng, inp, out, cnt, dims
 
+
+def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True, cpu_threads=0, P=None):
+    """configs[1]: SP_Truthful_TS, 8 LR-TS truthful bidders, 1M auctions per GPU, SecondPrice.
+    Inputs (contexts, participants, uniforms AND the Thompson noise z / sqrt(q) of both
+    participants) generated on the GPU and resident in HBM (build_sp_ts). One step =
+    ag_simulate. Then one Agent.update of all 8 agents on the last batch's won samples
+    (collect + the GPU training loop), timed separately (the reference: 14.3 s per 10k-round
+    iteration)."""
+    from auctiongym_amd.sharding import allreduce_counters
+    eng, inp, out, cnt, dims = build_sp_ts(B, local, P, world, rank)
+    N, K, E, P, OE, Do = (dims[k] for k in ("N", "K", "E", "P", "OE", "Do"))
+    items, values = dims["items"], dims["values"]
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream()
     def step(ev):
         cnt.zero_()
         if ev is not None:
@@ -466,55 +490,87 @@ def build_population(key, local, P=2):
     return eng, what, B0, ak, bk, st16, dims
 
 
-def run_population(key, steps, warmup, world, rank, local, batch=None, with_update=True, cpu_threads=0, P=2):
-    """A BASELINE config population on the GPU at its per-GPU shard size: iteration 0 with
-    Gaussian shading (uninitialised learners), the update of every learner (LR-TS allocators
-    and learning bidders, on the GPU, synthetic rsample noise; records all-gathered when N > 1)
-    timed, then the timed steps with bids from the fitted policies. Inputs Philox-generated
-    and resident in HBM."""
-    from auctiongym_amd.sharding import (allreduce_counters, bidder_update_agent_parallel,
-                                         lrts_update_agent_parallel, shard_range)
+def population_first_iteration(key, local, P=2, batch=None, world=1, rank=0):
+    """A BASELINE config population (build_population) at its per-GPU shard size, its
+    iteration 0 simulated once: Gaussian shading (uninitialised learners), Philox inputs for
+    this rank's shard resident in HBM. Returns (eng, what, B, ak, bk, st16, dims, lo, inp,
+    out, cnt)."""
+    from auctiongym_amd.sharding import shard_range
     eng, what, B0, ak, bk, st16, dims = build_population(key, local, P)
     B = int(batch or B0)
-    if P != 2:
-        what = what.replace('FirstPrice', f'FirstPrice, P={P}')
-    N, K, E, P, Do = (dims[k] for k in ("N", "K", "E", "P", "Do"))
-    dev = torch.device("cuda", local)
     lo, _ = shard_range(B * world, rank, world)
     inp = eng.alloc_inputs(B)
     eng.generate(0, lo, inp)
     eng.generate_noise(0, lo, inp)
     out = eng.alloc_outputs(B)
     cnt = eng.new_counters()
+    eng.simulate(inp, out, cnt)
+    torch.cuda.synchronize()
+    dims = dict(dims, lo=lo, ak=ak, bk=bk)
+    return eng, what, B, ak, bk, st16, dims, lo, inp, out, cnt
+
+
+def population_update(eng, inp, out, B, lo, ak, bk, world):
+    """The update of every learner on iteration 0's records (LR-TS allocators: won samples;
+    learning bidders: every record; synthetic on-device rsample noise), agent-parallel over
+    ranks at N > 1. Returns (ms [lrts, bidders] max over ranks, LR-TS epochs, bidder epochs,
+    LR-TS store, shading store, the LR-TS state before the update)."""
+    from auctiongym_amd.sharding import bidder_update_agent_parallel, lrts_update_agent_parallel
+    N = eng.N
+    P = eng.P
+    m_pre = eng.lrts_state()
+    lst = eng.new_lrts_samples(B)
+    sst = eng.new_shading_samples(B * P, learning=True)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    eng.lrts_collect(inp, out, lst)
+    eng.shading_collect(inp, out, sst, first_auction=lo)
+    # agent-parallel at N > 1 (each learner trained by one owner rank on every rank's
+    # records of it; sharding.*_agent_parallel); identical to one process
+    lep = lrts_update_agent_parallel(eng, lst, [a for a in range(N) if ak[a] == 1])
+    t1 = time.perf_counter()
+    ep, stat = bidder_update_agent_parallel(eng, sst, [a for a in range(N) if bk[a] >= 2])
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    ms = [(t1 - t0) * 1e3, (t2 - t1) * 1e3]
+    if world > 1:
+        t = torch.tensor(ms, dtype=torch.float64, device=eng.device)
+        all_reduce_max(t)
+        ms = [float(x) for x in t]
+    return ms, lep, ep, lst, sst, m_pre
+
+
+def population_fitted_inputs(eng, B, lo, ak):
+    """The timed steps' inputs: the fitted policies' rsample draws now; for mixed allocators
+    the Thompson noise in the compact layout (LR-TS pairs only, located through
+    ts_noise_index); all-LR-TS populations keep the dense tiles (nothing to drop)."""
+    inp = eng.alloc_inputs(B)
+    eng.generate(1, lo, inp)
+    compact = bool((ak == 1).any() and (ak != 1).any())
+    eng.generate_noise(1, lo, inp, compact=compact)
+    return inp, compact
+
+
+def run_population(key, steps, warmup, world, rank, local, batch=None, with_update=True, cpu_threads=0, P=2):
+    """A BASELINE config population on the GPU at its per-GPU shard size: iteration 0 with
+    Gaussian shading (uninitialised learners), the update of every learner (LR-TS allocators
+    and learning bidders, on the GPU, synthetic rsample noise; records routed agent-parallel
+    when N > 1) timed, then the timed steps with bids from the fitted policies. Inputs
+    Philox-generated and resident in HBM."""
+    from auctiongym_amd.sharding import allreduce_counters
+    eng, what, B, ak, bk, st16, dims, lo, inp, out, cnt = population_first_iteration(key, local, P, batch,
+                                                                                      world, rank)
+    if P != 2:
+        what = what.replace('FirstPrice', f'FirstPrice, P={P}')
+    N, K, E, P, Do = (dims[k] for k in ("N", "K", "E", "P", "Do"))
     res = {"workload": what, "auctions_per_gpu_per_step": B,
            "parity": "simulate: bit-exact vs the oracle; learner updates: bit-exact vs the oracle, which tracks "
                      "the reference's float32 torch fits -- after the first update their stopping epochs are "
                      "chaotic, so later iterations match the reference within 7e-6 (FP_DM_TS) .. 2.6e-3 "
                      "(FP_DR_TS) of revenue, not bit for bit (DESIGN.md section 5)"}
-    # iteration 0 (uninitialised learners) and the update of every learner
-    eng.simulate(inp, out, cnt)
-    torch.cuda.synchronize()
     if with_update:
-        m_pre = eng.lrts_state()
-        lst = eng.new_lrts_samples(B)
-        sst = eng.new_shading_samples(B * P, learning=True)
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        eng.lrts_collect(inp, out, lst)
-        eng.shading_collect(inp, out, sst, first_auction=lo)
-        # agent-parallel at N > 1 (each learner trained by one owner rank on every rank's
-        # records of it; sharding.*_agent_parallel); identical to one process
-        lep = lrts_update_agent_parallel(eng, lst, [a for a in range(N) if ak[a] == 1])
-        t1 = time.perf_counter()
-        ep, stat = bidder_update_agent_parallel(eng, sst, [a for a in range(N) if bk[a] >= 2])
-        torch.cuda.synchronize()
-        t2 = time.perf_counter()
-        ms = [(t1 - t0) * 1e3, (t2 - t1) * 1e3]
-        if world > 1:
-            t = torch.tensor(ms, dtype=torch.float64, device=dev)
-            all_reduce_max(t)
-            ms = [float(x) for x in t]
+        ms, lep, ep, lst, sst, m_pre = population_update(eng, inp, out, B, lo, ak, bk, world)
         learners = np.nonzero(bk >= 2)[0]
         res["agent_update"] = {
             "ms": ms[0] + ms[1], "lrts_ms": ms[0], "bidders_ms": ms[1],
@@ -561,12 +617,7 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
         init = np.where(bk >= 2, 1, 0).astype(np.int32)
         eng.set_dr_state(st16, init)
         st_fit = st16
-    inp = eng.alloc_inputs(B)  # the fitted policies' rsample draws now
-    eng.generate(1, lo, inp)
-    # mixed allocators: the Thompson noise in the compact layout (LR-TS pairs only, located
-    # through ts_noise_index); all-LR-TS populations keep the dense tiles (nothing to drop)
-    compact = bool((ak == 1).any() and (ak != 1).any())
-    eng.generate_noise(1, lo, inp, compact=compact)
+    inp, compact = population_fitted_inputs(eng, B, lo, ak)
     res["ts_noise_layout"] = "compact (ts_noise_index)" if compact else "dense"
     stream = torch.cuda.current_stream()
 

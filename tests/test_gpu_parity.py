@@ -103,37 +103,7 @@ def test_allocate_ragged_and_large(gpu, oracle):
             eng.close()
 
 
-@pytest.mark.parametrize("exact", [False, True], ids=["screened", "exact"])
-@pytest.mark.parametrize("name", CAPTURES)
-def test_simulate_replay_matches_reference(gpu, oracle, name, exact):
-    d, meta, agg = load_capture(name)
-    eng = _engine(meta, gpu)
-    eng.set_item_search(exact)
-    eng.load_catalog(d["items"], d["values"])
-    o = _run(eng, d["ctx"], d["part"], d["u"])
-    for mine, ref in (("item", "item"), ("bid", "slot_bid"), ("est_ctr", "slot_est_ctr"),
-                      ("true_ctr", "slot_true_ctr"), ("best_ev", "slot_best_ev")):
-        assert np.array_equal(o[mine], d[ref]), mine
-    assert np.array_equal(o["winner"], d["winner"])
-    if meta["P"] >= 2:
-        assert np.array_equal(o["price"], d["price"])
-        assert np.array_equal(o["second_price"], d["second_price"])
-        assert np.array_equal(o["outcome"], d["outcome"])
-    else:
-        assert np.isnan(o["price"]).all()
-    # exact fixed-point counters == the oracle's, bit for bit
-    orc = oracle.simulate(mech_code(meta), d["items"], d["values"], d["ctx"], d["part"], d["u"])
-    assert np.array_equal(o["counters_fx"], orc["counters_fx"])
-    from auctiongym_amd.engine import AuctionEngine
-    cnt = AuctionEngine.counters_to_numpy(o["counters_fx"])
-    C = {n: i for i, n in enumerate(oracle.COUNTERS)}
-    rt = dict(rtol=1e-9, atol=1e-9)
-    np.testing.assert_allclose(cnt[:, C["net"]], agg["net_utility"], **rt)
-    np.testing.assert_allclose(cnt[:, C["gross"]], agg["gross_utility"], **rt)
-    np.testing.assert_allclose(cnt[:, C["paid"]].sum(), agg["revenue"], **rt)
-    np.testing.assert_allclose(cnt[:, C["underbid_regret"]], agg["underbid_regret"], **rt)
-    np.testing.assert_allclose(cnt[:, C["overbid_regret"]], agg["overbid_regret"], **rt)
-    eng.close()
+# test_simulate_replay_matches_reference: tests/test_00_configs_gpu.py (first in the suite)
 
 
 def test_generator_matches_oracle(gpu, oracle):
@@ -1062,6 +1032,40 @@ def test_dropin_surface_captures(gpu, tmp_path, path, name):
         if samp[a]:
             torch.empty(kdo[a]).normal_(generator=ref)
     assert torch.equal(torch.get_rng_state(), ref.get_state())
+
+
+def test_dropin_batch_small_thompson_model(gpu, tmp_path):
+    """a sampling LR-TS agent whose K*(OE+1) < 16 (num_items = 3, OE = 4: 15 draws per
+    participation, torch's scalar normal path, which ag_replay_draw_population does not restate)
+    -- simulate_batch takes the per-round loop and gives exactly the per-round run's results and
+    torch / numpy generator states, instead of raising."""
+    import torch
+
+    import auctiongym_amd.main as M
+    cfg = dict(SP_TRUTHFUL_TS, agents=[
+        {"name": "Small TS", "num_copies": 3, "num_items": 3,
+         "allocator": {"type": "PyTorchLogisticRegressionAllocator", "kwargs": {"embedding_size": 4, "num_items": 3}},
+         "bidder": {"type": "TruthfulBidder", "kwargs": {}}},
+        {"name": "Oracle", "num_copies": 2, "num_items": 12,
+         "allocator": {"type": "OracleAllocator", "kwargs": {}}, "bidder": {"type": "TruthfulBidder", "kwargs": {}}}])
+    p = tmp_path / "small.json"
+    p.write_text(json.dumps(cfg))
+    res = {}
+    for path in ("per_round", "batch"):
+        rng, config, agent_configs, a2i, a2v, _, max_slots, E, var, OE = M.parse_config(str(p))
+        torch.manual_seed(5)
+        agents = M.instantiate_agents(rng, agent_configs, a2v, a2i)
+        auction, _, _, _ = M.instantiate_auction(rng, config, a2i, a2v, agents, max_slots, E, var, OE)
+        assert not auction._native_draws()
+        if path == "per_round":
+            for _ in range(700):
+                auction.simulate_opportunity()
+        else:
+            auction.simulate_batch(700)
+        res[path] = ([a.net_utility for a in agents], auction.revenue, torch.get_rng_state(),
+                     rng.bit_generator.state["state"]["state"], [[o.item for o in a.logs] for a in agents])
+    a, b = res["per_round"], res["batch"]
+    assert a[0] == b[0] and a[1] == b[1] and torch.equal(a[2], b[2]) and a[3] == b[3] and a[4] == b[4]
 
 
 def test_driver_sp_truthful_ts_iteration(gpu, oracle, tmp_path):

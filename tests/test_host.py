@@ -475,3 +475,38 @@ def test_per_call_agent_charge_metrics_and_update():
         assert len(ag.logs) == 4 and [o.bid for o in ag.logs] == [o["bid"] for o in L[-4:]]
         assert ag.num_logs() == 4
         assert close(ag.get_allocation_regret(), sum(o["bev"] - o["tru"] * o["value"] for o in L[-4:]))
+        # a second clear_logs with no new records keeps the same M records in the metrics
+        # (src/Agent.py:124-129 keeps logs[-M:] of the kept ones), and update() still trains on them
+        ag.clear_logs()
+        assert len(ag.logs) == 4 and ag.num_logs() == 4
+        assert close(ag.get_allocation_regret(), sum(o["bev"] - o["tru"] * o["value"] for o in L[-4:]))
+        ag.update(1)
+        assert len(ag.allocator.calls) == 2 and len(ag.bidder.calls) == 2
+        assert np.array_equal(ag.bidder.calls[1][2], np.array([o["bid"] for o in L[-4:]]))
+
+
+def test_native_draws_gate():
+    """Auction._native_draws: the C restatement of torch's normal_ covers the
+    >= 16-element vectorised kernel of AVX2 / AVX512 builds; a sampling LR-TS agent with
+    K*(OE+1) < 16, or a torch build on its DEFAULT kernels, keeps the per-round loop (which makes
+    the reference's own torch calls) instead of raising in ag_replay_draw_population."""
+    from types import SimpleNamespace
+    from unittest import mock
+
+    from auctiongym_amd.Auction import Auction
+
+    def ns(K, OE, ts=True, lrts=True, rng=None):
+        return SimpleNamespace(rng=rng or np.random.default_rng(0), _lrts=np.array([lrts, False]), _ts=ts,
+                               _num_items=np.array([K, 12]), obs_embedding_size=OE,
+                               _ts_agent=np.array([ts and lrts, False]),
+                               _TORCH_NORMAL_AVX2=Auction._TORCH_NORMAL_AVX2)
+    cap = torch.backends.cpu.get_cpu_capability()
+    native = cap in Auction._TORCH_NORMAL_AVX2
+    assert Auction._native_draws(ns(12, 4)) == native
+    assert not Auction._native_draws(ns(3, 4))             # 3 * 5 = 15 draws: torch's scalar path
+    assert Auction._native_draws(ns(3, 4, ts=False))       # no Thompson draws at all
+    assert Auction._native_draws(ns(4, 3)) == native       # 4 * 4 = 16
+    assert not Auction._native_draws(ns(12, 4, rng=np.random.Generator(np.random.MT19937(0))))
+    with mock.patch("torch.backends.cpu.get_cpu_capability", return_value="DEFAULT"):
+        assert not Auction._native_draws(ns(12, 4))
+        assert Auction._native_draws(ns(12, 4, ts=False))

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round-4 GPU session: smoke, the per-config full-size oracle tests (first), the whole GPU
+# suite, the driver-shaped bench line. TAG names the output directory; STEPS picks the steps.
+set -u
+OUT=gpurun_out/prof_${TAG:-r04}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "rc=$rc"; tail -n 3 "$OUT/$name.log" | cut -c1-300; if [ $rc -ne 0 ]; then exit $rc; fi; }
+for s in ${STEPS:-smoke configs suite bench}; do
+  case $s in
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    configs) step pytest_configs 600 python -u -m pytest tests/test_00_configs_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    suite) step pytest_gpu 1200 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
+    bench) step bench_driver 400 python bench.py --steps 20 --warmup 5 ;;
+    stats) step kernel_stats 500 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+  esac
+done
+echo "== done"
