@@ -547,38 +547,30 @@ class Auction:
         self._revenue_fx = 0
 
 
-NOISE_EPOCHS0 = 2048
+NOISE_WINDOW_FLOATS = 1 << 26  # host-drawn rsample noise per window (256 MB)
 
 
 def learner_update(eng, store, index, bidder, name):
     """Bidder.update of the learning bidder at engine slot `index` from the records of the
-    device store (ag_bidder_update with a one-agent mask), the bidder's host mirror refreshed
-    afterwards. The DR and ValueLearning 'policy' fits draw one rsample per record per epoch
-    from torch's global generator (src/Models.py:160, :87): the draws are made here, on the
-    host, with the same torch calls, for a growing epoch budget (the fit's length is only
-    known after it ran; a fit that exhausts its budget is re-run with twice as many epochs,
-    same result), and the generator is left exactly where the reference's is after the update
-    (including the rsample of every record after DR / PolicyLearning fits, src/Bidder.py:605,
-    :423). Returns the epochs [3] the fits ran."""
+    device store, the bidder's host mirror refreshed afterwards. The DR and ValueLearning
+    'policy' fits draw one rsample per record per epoch from torch's global generator
+    (src/Models.py:160, :87): they train as the resumable one-launch-per-epoch update
+    (ag_bidder_rp_*), fed the reference's draws window by window -- made in C from the
+    generator's state (ag_torch_normal_epochs: torch's own normal kernels, the same numbers) --
+    so the fit runs once, however long; the generator is then left exactly where the
+    reference's is after the update (its fit's epochs drawn, plus the rsample of every record
+    after DR / PolicyLearning fits, src/Bidder.py:605, :423). Returns the epochs [3] the fits
+    ran."""
     b = bidder
     n = int(eng.shading_counts(store)[index])
     mask = np.zeros(eng.N, np.int32)
     mask[index] = 1
-    offs = np.zeros(eng.N, np.int64)
     noisy = b.kind == _lib.BIDDER_DOUBLY_ROBUST or (b.kind == _lib.BIDDER_VALUE_LEARNING
                                                      and b.inference == "policy")
     if noisy and n > 0:
-        max_ep = 32768 if b.kind == _lib.BIDDER_DOUBLY_ROBUST else 16384
-        stream = _TorchNoise(n, eng.device)
-        E = min(NOISE_EPOCHS0, max_ep)
-        while True:
-            ep, stat = eng.bidder_update(store, stream.upto(E), offs, E, agents=mask)
-            if stat[index] != -3 or E >= max_ep:
-                break
-            E = min(2 * E, max_ep)
-        stream.rewind(int(ep[index, 2]))
+        ep, stat = _fit_with_torch_noise(eng, store, mask, index, n)
     else:
-        ep, stat = eng.bidder_update(store, None, offs, 0, agents=mask)
+        ep, stat = eng.bidder_update(store, None, np.zeros(eng.N, np.int64), 0, agents=mask)
     state, init = eng.dr_state()
     b._load_state16(state[index])
     b.model_initialised = bool(init[index] != _lib.LEARNER_UNINITIALISED)
@@ -590,32 +582,29 @@ def learner_update(eng, store, index, bidder, name):
     return ep[index].copy()
 
 
-class _TorchNoise:
-    """Per-epoch rsample draws of one agent's fit, torch.empty(n).normal_() per epoch from
-    torch's global generator (torch.distributions.Normal.rsample of an [n, 1] batch), made on
-    demand; rewind(e) leaves the generator as if exactly e epochs had been drawn."""
-
-    SNAP = 256
-
-    def __init__(self, n, device):
-        self.n, self.device = n, device
-        self.snaps = [torch.get_rng_state()]
-        self.host = []
-        self.dev = None
-
-    def upto(self, E):
-        while len(self.host) < E:
-            if len(self.host) % self.SNAP == 0 and len(self.host) // self.SNAP >= len(self.snaps):
-                self.snaps.append(torch.get_rng_state())
-            self.host.append(torch.empty(self.n).normal_())
-        if self.dev is None or self.dev.numel() < E * self.n:
-            self.dev = torch.cat(self.host[:E]).to(self.device)
-        return self.dev
-
-    def rewind(self, e):
-        # the nearest snapshot at or before epoch e (a fit that ran every epoch of the budget
-        # E returns e == E, one past the last snapshot taken), then replay forward to e
-        k = min(e // self.SNAP, len(self.snaps) - 1)
-        torch.set_rng_state(self.snaps[k])
-        for _ in range(e - k * self.SNAP):
-            torch.empty(self.n).normal_()
+def _fit_with_torch_noise(eng, store, mask, index, n, launches=256):
+    """One agent's update with the reference's torch rsample draws, single pass: windows of
+    W policy-fit epochs drawn from the generator state as the fit reaches them."""
+    from .engine import torch_normal_epochs
+    W = int(min(4096, max(16, NOISE_WINDOW_FLOATS // n)))
+    state = torch.get_rng_state().numpy().copy()  # advanced window by window
+    w0, w_state = 0, state.copy()                 # the window's first epoch and its generator
+    eng.bidder_rp_begin(store, agents=mask)
+    win = torch.from_numpy(torch_normal_epochs(state, n, W)).to(eng.device)
+    eng.bidder_rp_noise(win, n, w0, W)
+    while True:
+        eng.bidder_rp_epoch(launches)
+        fit, ep, need = eng.bidder_rp_poll()
+        if fit[index] < 0:
+            break
+        if need[index] >= 0:  # the policy fit reached the end of the window: the next one
+            w0, w_state = int(need[index]), state.copy()
+            win = torch.from_numpy(torch_normal_epochs(state, n, W)).to(eng.device)
+            eng.bidder_rp_noise(win, n, w0, W)
+    ep, stat = eng.bidder_rp_end()
+    # the generator after exactly the fit's epochs: the last window's start + its used epochs
+    used = int(ep[index, 2]) - w0
+    if used > 0:
+        torch_normal_epochs(w_state, n, used)
+    torch.set_rng_state(torch.from_numpy(w_state))
+    return ep, stat

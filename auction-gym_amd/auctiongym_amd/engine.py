@@ -484,6 +484,59 @@ class AuctionEngine:
                                             _ptr(tr), _stream()), "ag_bidder_update")
         return (ep, stat, tr) if trace else (ep, stat)
 
+    # ---- resumable / record-parallel learning-bidder training (ag_bidder_rp_*) ----
+    def bidder_rp_begin(self, store, agents=None, records_total=None, records_base=None):
+        """Start a resumable update of the exact-sum learning bidders (ag_bidder_rp_begin):
+        agents [N] mask (None: every ValueLearning / DoublyRobust bidder); records_total /
+        records_base [N]: the agents' records over all ranks and the global index of this
+        rank's first one (None: this process holds them all). Returns the totals tensor
+        (int64 [2][N][32] on the device) whose slot launch_index & 1 a multi-rank caller
+        all-reduces (SUM) after every epoch launch."""
+        mask = None if agents is None else np.ascontiguousarray(agents, np.int32).reshape(self.N)
+        tot = np.ascontiguousarray(records_total, np.int64) if records_total is not None else None
+        base = np.ascontiguousarray(records_base, np.int64) if records_base is not None else None
+        self._rp_tot = torch.zeros((2, self.N, 32), dtype=torch.int64, device=self.device)
+        self._rp_store = self._shading(store)
+        self._check(self.L.ag_bidder_rp_begin(self._h, ctypes.byref(self._rp_store),
+                                              None if mask is None else mask.ctypes.data,
+                                              None if tot is None else tot.ctypes.data,
+                                              None if base is None else base.ctypes.data,
+                                              _ptr(self._rp_tot), _stream()), "ag_bidder_rp_begin")
+        self._rp_noise = None
+        return self._rp_tot
+
+    def bidder_rp_epoch(self, launches=1, traces=None):
+        """Queue `launches` epoch launches; returns the last launch's index (its totals:
+        totals[index & 1])."""
+        k = ctypes.c_int64(-1)
+        self._check(self.L.ag_bidder_rp_epoch(self._h, int(launches), ctypes.byref(k), _ptr(traces), _stream()),
+                    "ag_bidder_rp_epoch")
+        return k.value
+
+    def bidder_rp_noise(self, noise, noise_n, first_epoch, epochs):
+        """The host-drawn rsample window (device float32 [epochs][noise_n]) of the policy fits."""
+        self._rp_noise = noise  # kept alive while the launches read it
+        self._check(self.L.ag_bidder_rp_noise(self._h, _ptr(noise), int(noise_n), int(first_epoch), int(epochs)),
+                    "ag_bidder_rp_noise")
+
+    def bidder_rp_poll(self):
+        """(fit [N] (-1 done), epoch [N], need_noise [N] (-1 or the policy epoch waiting))."""
+        fit, ep, nn = (np.zeros(self.N, np.int32) for _ in range(3))
+        self._check(self.L.ag_bidder_rp_poll(self._h, fit.ctypes.data, ep.ctypes.data, nn.ctypes.data, _stream()),
+                    "ag_bidder_rp_poll")
+        return fit, ep, nn
+
+    def bidder_rp_end(self):
+        """Apply the trained states; returns (epochs [N][3], status [N])."""
+        ep = np.zeros((self.N, 3), np.int32)
+        stat = np.zeros(self.N, np.int32)
+        try:
+            self._check(self.L.ag_bidder_rp_end(self._h, ep.ctypes.data, stat.ctypes.data, _stream()),
+                        "ag_bidder_rp_end")
+        finally:
+            self._rp_noise = self._rp_store = None
+        return ep, stat
+
     def shading_collect(self, inputs, outputs, store, first_auction=0):
         """Append the shading-bidder records of a simulated batch of auctions
         [first_auction, first_auction + B) (ag_shading_collect)."""
@@ -514,6 +567,18 @@ class AuctionEngine:
         _check(_lib.load().ag_counters_to_double(fx.ctypes.data, n, out.ctypes.data),
                "ag_counters_to_double")
         return out.reshape(fx.shape[:-1])
+
+
+def torch_normal_epochs(state, n, epochs):
+    """`epochs` x torch.empty(n).normal_() from the torch CPU generator state blob `state`
+    (numpy uint8 [5056], advanced in place): float32 [epochs][n] (ag_torch_normal_epochs, the C
+    restatement of torch's normal kernels; the same numbers as the calls themselves)."""
+    from . import _lib
+    L = _lib.load()
+    out = np.empty((int(epochs), int(n)), np.float32)
+    rc = L.ag_torch_normal_epochs(state.ctypes.data, state.nbytes, int(n), int(epochs), out.ctypes.data)
+    _lib.check(rc, "ag_torch_normal_epochs", L)
+    return out
 
 
 def device_exp(x, sigmoid=False):

@@ -14,6 +14,14 @@ are agent-parallel: each learning agent has an owner rank (round robin over the 
 all-to-all), the owner trains its agents alone, and the trained states are exchanged
 (`take_owned_rows`, one all-gather of a few KB). A rank's update work is its own agents'
 records only -- not every agent's, as training on all-gathered records would be.
+
+With fewer learners than ranks (A < G: FP_DR_TS's 3 learners on 8 GPUs) agent-parallel leaves
+ranks idle and gives each owner G/A times one GPU's records; the exact-sum learning bidders
+then train record-parallel (`bidder_update_record_parallel`): every rank keeps its own
+records, the fits run as one launch per epoch (ag_bidder_rp_*), and each epoch's exact int64
+partial sums are all-reduced, so every rank steps to the same model -- the model one process
+fits on all the records. `bidder_update` picks the mode by the cost model of DESIGN.md
+section 7.
 """
 import numpy as np
 import torch
@@ -270,3 +278,84 @@ def bidder_update_agent_parallel(eng, store, learners, group=None):
     state, init = take_owned_rows(state, own, group, dev), take_owned_rows(init, own, group, dev)
     eng.set_dr_state(state, init)
     return take_owned_rows(ep, own, group, dev), take_owned_rows(stat, own, group, dev)
+
+
+def _allreduce_sum(t, group=None):
+    """In-place int64 SUM over the ranks (RCCL on the device; gloo through host memory)."""
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
+def record_counts_over_ranks(eng, store, group=None):
+    """(records_total [N], records_base [N]) of a shading store over the ranks: every agent's
+    records on all ranks, and the global log-order index of this rank's first one (the ranks
+    hold contiguous auction shards in rank order, so a rank's records follow every lower
+    rank's). One all-gather of N counts."""
+    world = _world(group)
+    cnt = np.asarray(eng.shading_counts(store), np.int64)
+    if world == 1:
+        return cnt, np.zeros_like(cnt)
+    dev = _gather_device(eng, group)
+    t = torch.from_numpy(cnt.copy())
+    if dev is not None:
+        t = t.to(dev)
+    bufs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(bufs, t, group=group)
+    allc = np.stack([b.cpu().numpy() for b in bufs])
+    rank = dist.get_rank(group)
+    return allc.sum(0), allc[:rank].sum(0)
+
+
+RP_POLL_LAUNCHES = 64  # epoch launches between two polls of the learners' progress
+
+
+def bidder_update_record_parallel(eng, store, learners, group=None, poll=RP_POLL_LAUNCHES):
+    """Agent.update of the exact-sum learning bidders (ValueLearningBidder, DoublyRobustBidder;
+    src/Bidder.py:204-325, :473-615) record-parallel: every rank trains every learner on its own
+    records, one launch per epoch (ag_bidder_rp_epoch), each epoch's exact int64 partial sums
+    all-reduced (SUM) before the next launch -- every rank steps to the same model, bit for bit
+    the model one process fits on all the records (synthetic rsample draws keyed by the
+    records' global log-order index). Returns (epochs [N][3], status [N])."""
+    N = eng.N
+    world = _world(group)
+    mask = np.zeros(N, np.int32)
+    mask[list(learners)] = 1
+    total, base = record_counts_over_ranks(eng, store, group)
+    tot = eng.bidder_rp_begin(store, agents=mask, records_total=total, records_base=base)
+    sel = mask.astype(bool)
+    while True:
+        if world > 1:
+            for _ in range(poll):
+                k = eng.bidder_rp_epoch(1)
+                _allreduce_sum(tot[k & 1], group)
+        else:
+            eng.bidder_rp_epoch(4 * poll)
+        fit, ep, _ = eng.bidder_rp_poll()
+        if (fit[sel] < 0).all():
+            break
+    return eng.bidder_rp_end()
+
+
+def record_parallel_pays(num_learners, world):
+    """DESIGN.md section 7's cost model: agent-parallel gives each owner ceil(A / G) agents of
+    G times one GPU's records, i.e. ceil(A / G) * G / A of one GPU's update work; record-parallel
+    keeps one GPU's work plus one small all-reduce per epoch (measured ~0.6 of it at G = 8)."""
+    A = int(num_learners)
+    if world <= 1 or A == 0:
+        return False
+    return -(-A // world) * world / A > 1.6
+
+
+def bidder_update(eng, store, learners, group=None):
+    """Agent.update of every learning bidder across ranks: record-parallel where it pays
+    (exact-sum learners only, A < G per record_parallel_pays), else agent-parallel."""
+    learners = [int(a) for a in learners]
+    exact = all(int(eng._bkind[a]) in (2, 4) for a in learners)  # ValueLearning, DoublyRobust
+    if exact and record_parallel_pays(len(learners), _world(group)):
+        return bidder_update_record_parallel(eng, store, learners, group)
+    return bidder_update_agent_parallel(eng, store, learners, group)

@@ -146,4 +146,54 @@ __device__ __forceinline__ void agent_allreduce_i64(unsigned *bar, int64_t *acc,
   __syncthreads();
 }
 
+// The same combining-tree sum without the wait (per-epoch launches, ag_dr.hip k_bidder_epoch):
+// each workgroup adds its W words (LDS vals) up the tree and the root's last arriver stores
+// the totals to `out` (a global row read by the NEXT launch: the kernel boundary orders it);
+// nobody spins, so the workgroups need not be co-resident. acc / bar: as agent_allreduce_i64
+// (zero on entry, zero again on return). nblk <= 1 stores vals to out.
+__device__ __forceinline__ void agent_reduce_nowait(unsigned *bar, int64_t *acc, int stride, int rank, int nblk,
+                                                    const int64_t *vals, int W, int64_t *out, int *s_flag) {
+  const int t = threadIdx.x, nt = blockDim.x;
+  __syncthreads();
+  if (nblk <= 1) {
+    for (int j = t; j < W; j += nt) out[j] = vals[j];
+    return;
+  }
+  for (int j = t; j < W; j += nt)
+    __hip_atomic_fetch_add(acc + (size_t)(1 + rank / kBarFanIn) * stride + j, vals[j], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  int idx = rank, members_prev = nblk, base = 1;
+  for (;;) {
+    const int nodes = (members_prev + kBarFanIn - 1) / kBarFanIn, q = idx / kBarFanIn;
+    const int members = members_prev - q * kBarFanIn < kBarFanIn ? members_prev - q * kBarFanIn : kBarFanIn;
+    __syncthreads();  // this workgroup's additions to the node are issued before it arrives
+    if (t == 0) {
+      unsigned *cnt = bar + (size_t)(base + q) * kBarLineWords;
+      const bool last =
+          __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)members - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      *s_flag = last;
+    }
+    __syncthreads();
+    if (!*s_flag) return;
+    int64_t *node = acc + (size_t)(base + q) * stride;
+    int64_t *dst = nodes == 1 ? out : acc + (size_t)(base + nodes + q / kBarFanIn) * stride;
+    for (int j = t; j < W; j += nt) {
+      const int64_t v = __hip_atomic_load(node + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(node + j, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (nodes == 1)
+        dst[j] = v;
+      else
+        __hip_atomic_fetch_add(dst + j, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (nodes == 1) return;
+    base += nodes;
+    idx = q;
+    members_prev = nodes;
+  }
+}
+
 }  // namespace agcoop

@@ -381,6 +381,43 @@ struct RecView {
   __device__ __forceinline__ double won(int64_t j) const { return (double)(j < cap ? lw[j] : R.won[c0 + j]); }
 };
 
+// One BCE row of the win-rate fit (its loss and gradient terms, biased: see fxb) at the model
+// (w0, w1, w2, w3). One exp per row (oracle/ag_oracle_dr.c fit_winrate): e = exp(-|z|), L =
+// log1p(e); p = (z >= 0 ? 1 : e) / (1 + e); -log(p) = softplus(-z) for a win, -log(1 - p) =
+// softplus(z) otherwise, softplus(u) = L for u <= 0, |z| + L for u > 0 (u past 20: u).
+// Branch-free main paths of exp and log1p (the same bits), the rare inputs outside them
+// patched with the full functions afterwards. aug: the gamma = 0, y = 0 augmentation row.
+__device__ __forceinline__ void wr_row(int64_t (&acc)[5], double c, double v, double g, double y, bool aug,
+                                       double w0, double w1, double w2, double w3, const uint64_t *tab) {
+  const double z = c * w0 + v * w1 + g * w2 + w3;
+  const double a = __builtin_fabs(z);
+  double e = agexp::exp_main(-a, tab);
+  bool lok;
+  double Lz = aglog1p::log1p_main(e, lok);
+  if (__builtin_expect(!(agexp::exp_in_main(a) && lok), 0)) {
+    e = agexp::exp(-a, tab);
+    Lz = aglog1p::log1p(e);
+  }
+  const double pw = (z >= 0.0 ? 1.0 : e) / (1.0 + e);
+  const double u = y > 0.0 ? -z : z;
+  const double t = fmin(u > 20.0 ? u : (u > 0.0 ? a + Lz : Lz), 100.0);
+  // |t| <= 100, |pw - y| <= 1, ctr in [0, 1]: these terms are far inside fxr's fast range
+  addw(acc[0], fxb_fast(t));
+  const double gz = pw - y;
+  addw(acc[1], fxb_fast(gz * c));
+  addw(acc[2], fxb(gz * v));
+  if (!aug) addw(acc[3], fxb(gz * g));  // the augmentation row's g = 0 term is +-0: rounds to 0
+  addw(acc[4], fxb_fast(gz));
+}
+// a lane that ran wr_row for nrec records (both rows each): its accumulators unbiased
+__device__ __forceinline__ void wr_unbias(int64_t (&acc)[5], int64_t nrec) {
+  fx_unbias(acc[0], 2 * nrec);
+  fx_unbias(acc[1], 2 * nrec);
+  fx_unbias(acc[2], 2 * nrec);
+  fx_unbias(acc[3], nrec);
+  fx_unbias(acc[4], 2 * nrec);
+}
+
 // PyTorchWinRateEstimator fit (src/Bidder.py:229-252 ValueLearningBidder, :500-530
 // DoublyRobustBidder): BCE (mean) over the logs plus the gamma = 0, y = 0 augmentation,
 // Adam(lr 3e-3, wd 1e-6, AMSGrad), ReduceLROnPlateau(patience, factor, min_lr 1e-7),
@@ -397,48 +434,16 @@ __device__ int fit_winrate(const RecView &V, const Chunk &K, TrainLds &S, Coop &
   for (; e < kWrEpochs; ++e) {
     int64_t acc[5] = {0, 0, 0, 0, 0};
     const double w0 = (double)S.wr[0], w1 = (double)S.wr[1], w2 = (double)S.wr[2], w3 = (double)S.wr[3];
-    // one BCE row: its loss and gradient terms
-    auto row = [&](double c, double v, double g, double y, bool aug) {
-      const double z = c * w0 + v * w1 + g * w2 + w3;
-      // one exp per row (oracle/ag_oracle_dr.c fit_winrate): e = exp(-|z|), L = log1p(e);
-      // p = (z >= 0 ? 1 : e) / (1 + e); -log(p) = softplus(-z) for a win, -log(1 - p) =
-      // softplus(z) otherwise, softplus(u) = L for u <= 0, |z| + L for u > 0 (u past 20: u).
-      // Branch-free main paths of exp and log1p (the same bits), the rare inputs outside them
-      // patched with the full functions afterwards
-      const double a = __builtin_fabs(z);
-      double e = agexp::exp_main(-a, S.tab);
-      bool lok;
-      double Lz = aglog1p::log1p_main(e, lok);
-      if (__builtin_expect(!(agexp::exp_in_main(a) && lok), 0)) {
-        e = agexp::exp(-a, S.tab);
-        Lz = aglog1p::log1p(e);
-      }
-      const double pw = (z >= 0.0 ? 1.0 : e) / (1.0 + e);
-      const double u = y > 0.0 ? -z : z;
-      const double t = fmin(u > 20.0 ? u : (u > 0.0 ? a + Lz : Lz), 100.0);
-      // |t| <= 100, |pw - y| <= 1, ctr in [0, 1]: these terms are far inside fxr's fast range
-      // biased terms (fxb, one add fewer each), unbiased below
-      addw(acc[0], fxb_fast(t));
-      const double gz = pw - y;
-      addw(acc[1], fxb_fast(gz * c));
-      addw(acc[2], fxb(gz * v));
-      if (!aug) addw(acc[3], fxb(gz * g));  // the augmentation row's g = 0 term is +-0: rounds to 0
-      addw(acc[4], fxb_fast(gz));
-    };
     // record j's logged row and its gamma = 0, y = 0 augmentation row together (two
     // independent chains for the scheduler; the sums are exact, so any order)
     int64_t nrec = 0;
     for (int64_t j = tid; j < K.nb; j += kDrThreads) {
       const double c = V.ctr(j), v = V.val(j);
-      row(c, v, V.gam(j), V.won(j), false);
-      row(c, v, 0.0, 0.0, true);
+      wr_row(acc, c, v, V.gam(j), V.won(j), false, w0, w1, w2, w3, S.tab);
+      wr_row(acc, c, v, 0.0, 0.0, true, w0, w1, w2, w3, S.tab);
       ++nrec;
     }
-    fx_unbias(acc[0], 2 * nrec);
-    fx_unbias(acc[1], 2 * nrec);
-    fx_unbias(acc[2], 2 * nrec);
-    fx_unbias(acc[3], nrec);
-    fx_unbias(acc[4], 2 * nrec);
+    wr_unbias(acc, nrec);
     exact_totals<5>(acc, S, C);
     // every thread: the same loss; threads 0..3 step their parameter
     const float loss = (float)(fxv(S.tot[0], S.tot[1]) / M);
@@ -451,6 +456,18 @@ __device__ int fit_winrate(const RecView &V, const Chunk &K, TrainLds &S, Coop &
     if (stop) return e + 1;
   }
   return e;
+}
+
+// one record of the imitation fit: MSE terms of mu to the logged gamma and of softplus(sigma)
+// to 0.05 (acc[12], acc[13]) and their gradient (acc[0..11]), biased
+__device__ __forceinline__ void imit_rec(int64_t (&acc)[16], const float *pol, double c, double v, double g,
+                                         const uint64_t *tab) {
+  PolF f;
+  policy_fwd(pol, c, v, f, tab);
+  const double dm = f.mu - g, dsg = f.sp_sigma - 0.05;
+  addw(acc[12], fxb(dm * dm));
+  addw(acc[13], fxb(dsg * dsg));
+  policy_bwd(pol, c, v, f, 2.0 * dm, 2.0 * dsg, acc, 0, tab);
 }
 
 // BidShadingContextualBandit.initialise_policy (src/Models.py:106-137): imitation of the
@@ -467,15 +484,7 @@ __device__ int fit_imitation(const RecView &V, const Chunk &K, TrainLds &S, Coop
     int64_t acc[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = 0;
-    for (int64_t j = tid; j < K.nb; j += kDrThreads) {
-      const double c = V.ctr(j), v = V.val(j);
-      PolF f;
-      policy_fwd(S.pol, c, v, f, S.tab);
-      const double dm = f.mu - V.gam(j), dsg = f.sp_sigma - 0.05;
-      addw(acc[12], fxb(dm * dm));
-      addw(acc[13], fxb(dsg * dsg));
-      policy_bwd(S.pol, c, v, f, 2.0 * dm, 2.0 * dsg, acc, 0, S.tab);
-    }
+    for (int64_t j = tid; j < K.nb; j += kDrThreads) imit_rec(acc, S.pol, V.ctr(j), V.val(j), V.gam(j), S.tab);
     const int64_t nrec = K.nb > tid ? (K.nb - tid + kDrThreads - 1) / kDrThreads : 0;
 #pragma unroll
     for (int q = 0; q < 14; ++q) fx_unbias(acc[q], nrec);
@@ -491,6 +500,37 @@ __device__ int fit_imitation(const RecView &V, const Chunk &K, TrainLds &S, Coop
   return e;
 }
 
+// one record of the DR policy fit (fit_dr): its loss term (acc[12]) and gradient (acc[0..11]),
+// biased; du = utility - estimated utility, ep = the epoch's rsample draw
+__device__ __forceinline__ void dr_rec(int64_t (&acc)[16], const float *pol, const float *wr, double c, double v,
+                                       double g, float prop, double du, double ep, const uint64_t *tab) {
+  const double inv_sqrt2pi = 1.0 / __builtin_sqrt(2.0 * 3.141592653589793);
+  PolF f;
+  policy_fwd(pol, c, v, f, tab);
+  const double mu = f.mu, sg = f.sigma;
+  const double zz = (mu - g) / sg;
+  const double pdf_raw = exp_fast(-(zz * zz) / 2.0, tab) / sg * inv_sqrt2pi;
+  const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
+  const double p0 = (double)fmaxf(prop, 1e-15f);
+  const double iw = pi / p0;
+  const double iwc = iw < 1.0 / 50.0 ? 1.0 / 50.0 : (iw > 50.0 ? 50.0 : iw);
+  const double raw = mu + sg * ep;
+  const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
+  const double zw = c * (double)wr[0] + v * (double)wr[1] + gs * (double)wr[2] + (double)wr[3];
+  const double Wv = 1.0 / (1.0 + exp_fast(-zw, tab));
+  const double V = c * v;
+  addw(acc[12], fxb(-(du * iwc + Wv * (V - V * gs))));
+  double dpi_dmu = 0.0, dpi_dsg = 0.0;
+  if (pdf_raw >= 1e-30 && iw >= 1.0 / 50.0 && iw <= 50.0) {
+    const double k = du / p0;
+    dpi_dmu = k * pdf_raw * (g - mu) / (sg * sg);
+    dpi_dsg = k * pdf_raw * ((g - mu) * (g - mu) / (sg * sg * sg) - 1.0 / sg);
+  }
+  double ddm = 0.0;
+  if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)wr[2];
+  policy_bwd(pol, c, v, f, -(dpi_dmu + ddm), -(dpi_dsg + ddm * ep), acc, 0, tab);
+}
+
 // DoublyRobustBidder's policy fit (src/Bidder.py:562-590, src/Models.py:201-218): loss
 // -mean((u - u^) clip(pi / pi0, 1/50, 50) + W(ctr, value, g~) (V - V g~)), g~ = clip(mu +
 // sigma eps, 0, 1); Adam(lr 7e-3, wd 1e-4, AMSGrad), ReduceLROnPlateau(patience 100, factor
@@ -502,43 +542,15 @@ __device__ int fit_dr(const RecView &V, const Chunk &K, TrainLds &S, Coop &C,
   double lr = 7e-3;
   Plateau pl{INFINITY, 5e-3, 0.2, 1e-8, 0, 100};
   Stopper sp{INFINITY, -1, 512};
-  const double inv_sqrt2pi = 1.0 / __builtin_sqrt(2.0 * 3.141592653589793);
   const double n = (double)K.n;
   int e = 0;
   for (; e < kDrEpochs && e < F.epochs; ++e) {
     int64_t acc[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = 0;
-    for (int64_t j = tid; j < K.nb; j += kDrThreads) {
-      const int64_t i = K.c0 + j;
-      const double c = V.ctr(j), v = V.val(j), g = V.gam(j);
-      PolF f;
-      policy_fwd(S.pol, c, v, f, S.tab);
-      const double mu = f.mu, sg = f.sigma;
-      const double zz = (mu - g) / sg;
-      const double pdf_raw = exp_fast(-(zz * zz) / 2.0, S.tab) / sg * inv_sqrt2pi;
-      const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
-      const double p0 = (double)fmaxf(V.prop(j), 1e-15f);
-      const double iw = pi / p0;
-      const double iwc = iw < 1.0 / 50.0 ? 1.0 / 50.0 : (iw > 50.0 ? 50.0 : iw);
-      const double du = V.util(j) - V.eut(j);
-      const double ep = fit_eps(F, e, i);
-      const double raw = mu + sg * ep;
-      const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
-      const double zw = c * (double)S.wr[0] + v * (double)S.wr[1] + gs * (double)S.wr[2] + (double)S.wr[3];
-      const double Wv = 1.0 / (1.0 + exp_fast(-zw, S.tab));
-      const double V = c * v;
-      addw(acc[12], fxb(-(du * iwc + Wv * (V - V * gs))));
-      double dpi_dmu = 0.0, dpi_dsg = 0.0;
-      if (pdf_raw >= 1e-30 && iw >= 1.0 / 50.0 && iw <= 50.0) {
-        const double k = du / p0;
-        dpi_dmu = k * pdf_raw * (g - mu) / (sg * sg);
-        dpi_dsg = k * pdf_raw * ((g - mu) * (g - mu) / (sg * sg * sg) - 1.0 / sg);
-      }
-      double ddm = 0.0;
-      if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)S.wr[2];
-      policy_bwd(S.pol, c, v, f, -(dpi_dmu + ddm), -(dpi_dsg + ddm * ep), acc, 0, S.tab);
-    }
+    for (int64_t j = tid; j < K.nb; j += kDrThreads)
+      dr_rec(acc, S.pol, S.wr, V.ctr(j), V.val(j), V.gam(j), V.prop(j), V.util(j) - V.eut(j),
+             fit_eps(F, e, K.c0 + j), S.tab);
     const int64_t nrec = K.nb > tid ? (K.nb - tid + kDrThreads - 1) / kDrThreads : 0;
 #pragma unroll
     for (int q = 0; q < 13; ++q) fx_unbias(acc[q], nrec);
@@ -555,6 +567,22 @@ __device__ int fit_dr(const RecView &V, const Chunk &K, TrainLds &S, Coop &C,
   }
   if (e < kDrEpochs && tid == 0) S.exhausted = 1;
   return e;
+}
+
+// one record of the ValueLearningBidder policy fit (fit_dm), biased
+__device__ __forceinline__ void dm_rec(int64_t (&acc)[16], const float *pol, const float *wr, double c, double v,
+                                       double ep, const uint64_t *tab) {
+  PolF f;
+  policy_fwd(pol, c, v, f, tab);
+  const double raw = f.mu + f.sigma * ep;
+  const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
+  const double zw = c * (double)wr[0] + v * (double)wr[1] + gs * (double)wr[2] + (double)wr[3];
+  const double Wv = 1.0 / (1.0 + exp_fast(-zw, tab));
+  const double V = c * v;
+  addw(acc[12], fxb(-(Wv * (V - V * gs))));
+  double ddm = 0.0;
+  if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)wr[2];
+  policy_bwd(pol, c, v, f, -ddm, -(ddm * ep), acc, 0, tab);
 }
 
 // ValueLearningBidder's policy fit (inference 'policy', src/Bidder.py:258-303): loss
@@ -574,22 +602,8 @@ __device__ int fit_dm(const RecView &V, const Chunk &K, TrainLds &S, Coop &C, co
     int64_t acc[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = 0;
-    for (int64_t j = tid; j < K.nb; j += kDrThreads) {
-      const int64_t i = K.c0 + j;
-      const double c = V.ctr(j), v = V.val(j);
-      PolF f;
-      policy_fwd(S.pol, c, v, f, S.tab);
-      const double ep = fit_eps(F, e, i);
-      const double raw = f.mu + f.sigma * ep;
-      const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
-      const double zw = c * (double)S.wr[0] + v * (double)S.wr[1] + gs * (double)S.wr[2] + (double)S.wr[3];
-      const double Wv = 1.0 / (1.0 + exp_fast(-zw, S.tab));
-      const double V = c * v;
-      addw(acc[12], fxb(-(Wv * (V - V * gs))));
-      double ddm = 0.0;
-      if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)S.wr[2];
-      policy_bwd(S.pol, c, v, f, -ddm, -(ddm * ep), acc, 0, S.tab);
-    }
+    for (int64_t j = tid; j < K.nb; j += kDrThreads)
+      dm_rec(acc, S.pol, S.wr, V.ctr(j), V.val(j), fit_eps(F, e, K.c0 + j), S.tab);
     const int64_t nrec = K.nb > tid ? (K.nb - tid + kDrThreads - 1) / kDrThreads : 0;
 #pragma unroll
     for (int q = 0; q < 13; ++q) fx_unbias(acc[q], nrec);
@@ -840,6 +854,279 @@ __global__ __launch_bounds__(kDrThreads, PH == 0 ? 4 : 1) void k_bidder_train(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Resumable, record-parallel training (ag_bidder_rp_*): the exact-sum learners' fits --
+// ValueLearningBidder (win count, win-rate fit, 'policy' fit) and DoublyRobustBidder (win-rate
+// fit, estimated utilities, imitation, DR policy fit) -- as ONE LAUNCH PER EPOCH, the whole
+// training state of a learner (FitSt) in HBM between launches. Launch k, every workgroup of
+// every learner:
+//   1. steps the learner's state with the summed partials of launch k - 1 (summed over this
+//      rank's workgroups by launch k - 1's tree root, then over the ranks by the caller's
+//      all-reduce of those int64 words): loss, Adam, scheduler, early stop and the move to the
+//      next fit, exactly as the persistent fits do it -- every workgroup computes the same
+//      step from the same integers;
+//   2. adds its records' exact fixed-point terms of the next epoch at the new state;
+//   3. sums them up the agent's combining tree without waiting (agent_reduce_nowait): the
+//      root stores the rank's totals for launch k + 1 (or the caller's all-reduce).
+// No workgroup waits for another: no co-residency, no device-wide barrier. The sums are
+// integers, so a rank holding a shard of the records (its records' global indices keep the
+// synthetic rsample draws) steps to the model one process fits on all of them, bit for bit --
+// and that model is the persistent fits' (k_bidder_train), which the GPU tests check.
+// A policy fit that runs out of host-drawn noise epochs (ag_bidder_rp_noise) waits, with its
+// state kept, for the next window: the drop-in update draws the reference's torch noise
+// window by window and never re-runs a fit.
+enum { kFitWins = 0, kFitWr, kFitEu, kFitInit, kFitPol, kFitDone };
+struct FitSt {
+  int32_t fit, epoch, status, have_tot, need_noise, pad0;
+  int32_t ep[3], pad1;
+  double lr;
+  Plateau pl;
+  Stopper sp;
+  float wr[4], pol[12];
+  AdamState adam;
+};
+
+// the learner's state on entering `fit` (the persistent fits' initialisations)
+__device__ __forceinline__ void fit_enter(FitSt &st, int fit, int bk, int mode) {
+  st.fit = fit;
+  st.epoch = 0;
+  for (int j = 0; j < 16; ++j) st.adam.ea[j] = st.adam.es[j] = st.adam.mx[j] = 0.0f;
+  const bool dr = bk == AG_BIDDER_DOUBLY_ROBUST;
+  if (fit == kFitWr) {
+    st.lr = 3e-3;
+    st.pl = dr ? Plateau{INFINITY, 1e-4, 0.2, 1e-7, 0, 256} : Plateau{INFINITY, 1e-4, 0.1, 1e-7, 0, 100};
+    st.sp = Stopper{INFINITY, -1, dr ? 1024 : 512};
+  } else if (fit == kFitInit) {
+    st.lr = 1e-3;
+    st.sp = Stopper{INFINITY, -1, 512};
+  } else if (fit == kFitPol) {
+    if (dr) {
+      st.lr = 7e-3;
+      st.pl = Plateau{INFINITY, 5e-3, 0.2, 1e-8, 0, 100};
+      st.sp = Stopper{INFINITY, -1, 512};
+    } else {
+      st.lr = 2e-3;
+      st.pl = Plateau{INFINITY, 1e-4, 0.1, 1e-7, 0, 100};
+      st.sp = Stopper{INFINITY, -1, 256};
+    }
+  }
+  (void)mode;
+}
+
+// the fit after `st.fit` ended (the reference's order, src/Bidder.py:229-325, :500-615)
+__device__ __forceinline__ void fit_after(FitSt &st, int bk, int mode, int init) {
+  int nxt = kFitDone;
+  switch (st.fit) {
+    case kFitWins: nxt = kFitWr; break;
+    case kFitWr: nxt = bk == AG_BIDDER_DOUBLY_ROBUST ? kFitEu : (mode == AG_VL_POLICY ? kFitPol : kFitDone); break;
+    case kFitEu: nxt = init ? kFitPol : kFitInit; break;
+    case kFitInit: nxt = kFitPol; break;
+    default: nxt = kFitDone;
+  }
+  fit_enter(st, nxt, bk, mode);
+}
+
+__device__ __forceinline__ int fit_max_epochs(int fit, int bk) {
+  if (fit == kFitWr) return kWrEpochs;
+  if (fit == kFitInit) return kInitEpochs;
+  return bk == AG_BIDDER_DOUBLY_ROBUST ? kDrEpochs : kInitEpochs;
+}
+
+// step 1 (thread 0 with threads 0..15 for Adam): the learner's state after the epoch whose
+// summed partials are tot (hi, lo pairs); n: the learner's records over all ranks
+__device__ void fit_step(FitSt &st, const int64_t *tot, double n, int bk, int mode, int init, const double *adam_tab,
+                         float *s_grad, float *s_loss, int *s_np, float *tr) {
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    *s_np = 0;
+    if (st.fit == kFitWins) {
+      if (tot[0] == 0 && tot[1] == 0) {  // no wins: revert to Gaussian shading (src/Bidder.py:206-211)
+        st.status = 1;
+        fit_enter(st, kFitDone, bk, mode);
+      } else {
+        fit_after(st, bk, mode, init);
+      }
+    } else if (st.fit == kFitWr) {
+      const double M = 2.0 * n;
+      *s_loss = (float)(fxv(tot[0], tot[1]) / M);
+      for (int j = 0; j < 4; ++j) s_grad[j] = (float)(fxv(tot[2 + 2 * j], tot[3 + 2 * j]) / M);
+      *s_np = 4;
+    } else {  // imitation / policy fits: 12 parameters
+      *s_loss = st.fit == kFitInit ? (float)(fxv(tot[24], tot[25]) / n + fxv(tot[26], tot[27]) / n)
+                                   : (float)(fxv(tot[24], tot[25]) / n);
+      for (int j = 0; j < 12; ++j) s_grad[j] = (float)(fxv(tot[2 * j], tot[2 * j + 1]) / n);
+      *s_np = 12;
+    }
+  }
+  __syncthreads();
+  const int np = *s_np;
+  if (np == 0) return;
+  // Adam: thread j steps parameter j (adam_step_block's arithmetic)
+  const int e = st.epoch;
+  const float wd = st.fit == kFitWr ? (float)1e-6 : (st.fit == kFitInit || bk == AG_BIDDER_DOUBLY_ROBUST ? (float)1e-4
+                                                                                                         : (float)1e-6);
+  double bc1;
+  float bc2f;
+  bias_corrections(e, adam_tab, bc2f, bc1);
+  const float neg_step = (float)(-(st.lr / bc1));
+  float *par = st.fit == kFitWr ? st.wr : st.pol;
+  __syncthreads();
+  if (tid < np) {
+    float p = par[tid];
+    adam_param(p, s_grad[tid], tid, st.adam, neg_step, bc2f, wd);
+    par[tid] = p;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const float loss = *s_loss;
+    if (tr) tr[e] = loss;
+    if (st.fit != kFitInit) plateau_step(st.pl, loss, st.lr);
+    const bool stop = stop_step(st.sp, e, loss);
+    const bool nan = loss != loss && st.fit == kFitPol && bk == AG_BIDDER_DOUBLY_ROBUST;
+    st.epoch = e + 1;
+    if (stop || nan || st.epoch >= fit_max_epochs(st.fit, bk)) {
+      st.ep[st.fit == kFitWr ? 0 : (st.fit == kFitInit ? 1 : 2)] = st.epoch;
+      if (nan) {
+        st.status = -2;  // the reference exits (src/Bidder.py:592-600)
+        fit_enter(st, kFitDone, bk, mode);
+      } else {
+        fit_after(st, bk, mode, init);
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// step 2: this workgroup's exact partial sums (S.tot, 2 NV words) of the learner's epoch
+template <int NV>
+__device__ __forceinline__ void rp_block(const int64_t (&acc)[NV], TrainLds &S) {
+  block_sums<NV>(acc, S.w, S.tot);
+}
+
+__global__ __launch_bounds__(kDrThreads) void k_bidder_epoch(
+    const int32_t *__restrict__ bkind, const int32_t *__restrict__ bmode, const int32_t *__restrict__ initialised,
+    const int32_t *__restrict__ blk_agent, const int32_t *__restrict__ blk_rank,
+    const int32_t *__restrict__ agent_nblk, const int64_t *__restrict__ offsets, const int64_t *__restrict__ n_total,
+    const int64_t *__restrict__ g_base, DrRecords R0, double *__restrict__ eu_ws, const FitSt *__restrict__ st_in,
+    FitSt *__restrict__ st_out, const int64_t *__restrict__ tot_in, int64_t *__restrict__ tot_out,
+    int64_t *__restrict__ acc_rows, unsigned *__restrict__ bars, const int32_t *__restrict__ bar_off,
+    const float *__restrict__ noise, int64_t noise_n, int32_t noise_e0, int32_t noise_epochs, uint64_t noise_seed,
+    const double *__restrict__ adam_tab, float *__restrict__ traces) {
+  const int a = blk_agent[blockIdx.x], rank = blk_rank[blockIdx.x], nblk = agent_nblk[a];
+  const int tid = threadIdx.x;
+  const int bk = bkind[a], mode = bmode[a], init = initialised[a];
+  __shared__ TrainLds S;
+  __shared__ FitSt st;
+  __shared__ float s_grad[16], s_loss;
+  __shared__ int s_np;
+  for (int i = tid; i < 256; i += kDrThreads) S.tab[i] = ag_exp_tab[i];
+  if (tid == 0) st = st_in[a];
+  __syncthreads();
+  const double n = (double)n_total[a];
+  if (st.fit != kFitDone && st.have_tot) {
+    float *tr = (traces && g_base[a] == 0 && rank == 0 && st.fit >= kFitWr)
+                    ? traces + ((size_t)a * 3 + (st.fit == kFitWr ? 0 : (st.fit == kFitInit ? 1 : 2))) * kDrEpochs
+                    : nullptr;
+    fit_step(st, tot_in + (size_t)a * 32, n, bk, mode, init, adam_tab, s_grad, &s_loss, &s_np, tr);
+  }
+  const int64_t s0 = offsets[a], nl = offsets[a + 1] - s0;
+  const int64_t per = (nl + nblk - 1) / nblk;
+  const int64_t c0 = (int64_t)rank * per < nl ? (int64_t)rank * per : nl;
+  const int64_t nb = (c0 + per < nl ? c0 + per : nl) - c0;
+  const DrRecords R{R0.ctr + s0 + c0, R0.value + s0 + c0, R0.gamma + s0 + c0, R0.prop + s0 + c0, R0.util + s0 + c0,
+                    R0.won + s0 + c0};
+  double *eu = eu_ws + s0 + c0;
+  if (st.fit == kFitEu) {
+    // estimated utilities of this workgroup's records with the fitted win-rate model
+    // (src/Bidder.py:541-546; k_bidder_train<1>'s arithmetic); the same thread reads them back
+    for (int64_t j = tid; j < nb; j += kDrThreads) {
+      const double c = (double)(float)R.ctr[j], v = (double)(float)R.value[j], g = (double)(float)R.gamma[j];
+      const double z = c * (double)st.wr[0] + v * (double)st.wr[1] + g * (double)st.wr[2] + (double)st.wr[3];
+      const float W = (float)(1.0 / (1.0 + agexp::exp(-z, S.tab)));
+      const double Vv = R.ctr[j] * R.value[j], P = R.ctr[j] * R.value[j] * R.gamma[j];
+      eu[j] = (double)W * (Vv - P);
+    }
+    __syncthreads();
+    if (tid == 0) fit_after(st, bk, mode, init);
+    __syncthreads();
+  }
+  const bool noisy = st.fit == kFitPol;  // the DR / DM policy fits draw an rsample per record per epoch
+  if (tid == 0)
+    st.need_noise = noisy && noise && (st.epoch < noise_e0 || st.epoch >= noise_e0 + noise_epochs) ? 1 : 0;
+  __syncthreads();
+  const bool active = st.fit != kFitDone && !st.need_noise;
+  if (active) {
+    const FitNoise F{noise ? noise - (int64_t)noise_e0 * noise_n : nullptr, noise_n, noise_seed, (uint32_t)a,
+                     1 << 30};
+    const int64_t gb = g_base[a] + c0;  // the global index of record 0 of this chunk (the noise's)
+    const int e = st.epoch;
+    const int64_t nrec = nb > tid ? (nb - tid + kDrThreads - 1) / kDrThreads : 0;
+    if (st.fit == kFitWins) {
+      int64_t acc[1] = {0};
+      for (int64_t j = tid; j < nb; j += kDrThreads) acc[0] += R.won[j] != 0 ? 1 : 0;
+      rp_block<1>(acc, S);
+    } else if (st.fit == kFitWr) {
+      int64_t acc[5] = {0, 0, 0, 0, 0};
+      const double w0 = (double)st.wr[0], w1 = (double)st.wr[1], w2 = (double)st.wr[2], w3 = (double)st.wr[3];
+      for (int64_t j = tid; j < nb; j += kDrThreads) {
+        const double c = (double)(float)R.ctr[j], v = (double)(float)R.value[j];
+        wr_row(acc, c, v, (double)(float)R.gamma[j], (double)R.won[j], false, w0, w1, w2, w3, S.tab);
+        wr_row(acc, c, v, 0.0, 0.0, true, w0, w1, w2, w3, S.tab);
+      }
+      wr_unbias(acc, nrec);
+      rp_block<5>(acc, S);
+    } else {
+      int64_t acc[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[j] = 0;
+      if (st.fit == kFitInit) {
+        for (int64_t j = tid; j < nb; j += kDrThreads)
+          imit_rec(acc, st.pol, (double)(float)R.ctr[j], (double)(float)R.value[j], (double)(float)R.gamma[j], S.tab);
+#pragma unroll
+        for (int q = 0; q < 14; ++q) fx_unbias(acc[q], nrec);
+      } else if (bk == AG_BIDDER_DOUBLY_ROBUST) {
+        for (int64_t j = tid; j < nb; j += kDrThreads)
+          dr_rec(acc, st.pol, st.wr, (double)(float)R.ctr[j], (double)(float)R.value[j], (double)(float)R.gamma[j],
+                 (float)R.prop[j], (double)(float)R.util[j] - (double)(float)eu[j], fit_eps(F, e, gb + j), S.tab);
+#pragma unroll
+        for (int q = 0; q < 13; ++q) fx_unbias(acc[q], nrec);
+      } else {
+        for (int64_t j = tid; j < nb; j += kDrThreads)
+          dm_rec(acc, st.pol, st.wr, (double)(float)R.ctr[j], (double)(float)R.value[j], fit_eps(F, e, gb + j), S.tab);
+#pragma unroll
+        for (int q = 0; q < 13; ++q) fx_unbias(acc[q], nrec);
+      }
+      rp_block<16>(acc, S);
+    }
+    const int W = st.fit == kFitWins ? 2 : (st.fit == kFitWr ? 10 : 32);
+    // the agent's region: accumulator rows [bar_lines(nblk)][32], barrier lines
+    agcoop::agent_reduce_nowait(bars + (size_t)bar_off[a] * agcoop::kBarLineWords,
+                                acc_rows + (size_t)bar_off[a] * 32, 32, rank, nblk, S.tot, W,
+                                tot_out + (size_t)a * 32, &S.flag);
+  }
+  if (rank == 0 && tid == 0) {
+    st.have_tot = active ? 1 : 0;
+    st_out[a] = st;
+  }
+}
+
+// the learners' FitSt at the start of a resumable update (state16: win-rate model, policy)
+__global__ void k_rp_init(int N, const int32_t *__restrict__ bkind, const int32_t *__restrict__ bmode,
+                          const int32_t *__restrict__ mask, const float *__restrict__ state, FitSt *__restrict__ st) {
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= N) return;
+  FitSt f;
+  memset(&f, 0, sizeof f);
+  for (int j = 0; j < 4; ++j) f.wr[j] = state[(size_t)a * 16 + j];
+  for (int j = 0; j < 12; ++j) f.pol[j] = state[(size_t)a * 16 + 4 + j];
+  const int bk = bkind[a];
+  if (mask[a])
+    fit_enter(f, bk == AG_BIDDER_DOUBLY_ROBUST ? kFitWr : kFitWins, bk, bmode[a]);
+  else
+    fit_enter(f, kFitDone, bk, bmode[a]);
+  st[a] = f;
+}
+
 __global__ __launch_bounds__(kDrThreads) void k_sh_hist(const int32_t *__restrict__ agent, int64_t n, int N,
                                                         int64_t *__restrict__ counts) {
   extern __shared__ unsigned int s_hist[];
@@ -895,6 +1182,9 @@ void ag_dr_release(ag_ctx *c) {
   (void)hipFree(w.mode);
   (void)hipFree(w.scratch);
   (void)hipFree(w.coop);
+  (void)hipFree(w.rp.st);
+  (void)hipFree(w.rp.acc);
+  (void)hipFree(w.rp.tables);
   w = ag_dr_ws();
 }
 
@@ -939,6 +1229,63 @@ static int dr_ws_ready(ag_ctx *c) {
     ag_dr_release(c);
     return ag_set_error(AG_ERR_HIP, "DR workspace: %s", hipGetErrorString(e));
   }
+  return AG_OK;
+}
+
+// The learning bidders' records of a store sorted into (agent, log order) in the workspace
+// (radix sort on agent << 40 | order, then every field gathered): cnt / off host [N] / [N + 1];
+// SortedRecs: device arrays [n] (eu: the estimated-utility workspace) and d_off [N + 1].
+struct SortedRecs {
+  double *ctr, *val, *gam, *prop, *util, *eu;
+  uint8_t *won;
+  int64_t *d_off;
+  int64_t n;
+};
+static int sort_records(ag_ctx *c, const ag_shading_samples *s, std::vector<int64_t> &cnt, std::vector<int64_t> &off,
+                        SortedRecs &out, hipStream_t st) {
+  const int N = c->shape.num_agents;
+  if (int rc = ag_shading_counts(c, s, cnt.data(), st)) return rc;
+  int64_t n = 0;
+  for (int a = 0; a < N; ++a) n += cnt[a];
+  ag_dr_ws &w = c->dr;
+  off.assign((size_t)N + 1, 0);
+  for (int a = 0; a < N; ++a) off[a + 1] = off[a] + cnt[a];
+  int64_t *d_off = w.counts + N;  // [N + 1] offsets
+  AG_HIP(hipMemcpyAsync(d_off, off.data(), sizeof(int64_t) * ((size_t)N + 1), hipMemcpyHostToDevice, st));
+  if (n >= ((int64_t)1 << 32)) return ag_set_error(AG_ERR_UNSUPPORTED, "learning bidders' update: >= 2^32 records");
+  // radix-sort workspace: keys in/out (8 B), indices in/out (4 B), then hipcub's temp
+  size_t sort_tmp = 0;
+  AG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint64_t *)nullptr, (uint64_t *)nullptr,
+                                            (uint32_t *)nullptr, (uint32_t *)nullptr, (int)(n > 0 ? n : 1), 0, 64,
+                                            st));
+  const size_t rec_bytes = (size_t)6 * sizeof(double) + 1;
+  const size_t need = (size_t)(n > 0 ? n : 1) * (rec_bytes + 24) + sort_tmp + 256;
+  if (need > w.buf_bytes) {
+    (void)hipFree(w.buf);
+    w.buf = nullptr;
+    const size_t bytes = need + (need >> 2);
+    AG_HIP(hipMalloc(&w.buf, bytes));
+    w.buf_bytes = bytes;
+  }
+  const size_t cap = (size_t)(n > 0 ? n : 1);
+  double *b_ctr = (double *)w.buf, *b_val = b_ctr + cap, *b_gam = b_val + cap, *b_prop = b_gam + cap,
+         *b_util = b_prop + cap, *b_eu = b_util + cap;
+  uint64_t *k_in = (uint64_t *)(b_eu + cap), *k_out = k_in + cap;
+  uint32_t *i_in = (uint32_t *)(k_out + cap), *i_out = i_in + cap;
+  uint8_t *b_won = (uint8_t *)(i_out + cap);
+  void *tmp = (void *)(((uintptr_t)(b_won + cap) + 255) & ~(uintptr_t)255);
+  if (n > 0) {
+    if (!s->order) return ag_set_error(AG_ERR_INVALID, "learning bidders' update: the store needs order");
+    hipLaunchKernelGGL(k_sh_keys, dim3(grid_over(n)), dim3(kDrThreads), 0, st, *s, n, k_in, i_in);
+    AG_HIP(hipGetLastError());
+    int end_bit = 40;
+    while ((1ll << (end_bit - 40)) < N) ++end_bit;
+    AG_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, sort_tmp, k_in, k_out, i_in, i_out, (int)n, 0, end_bit, st));
+    hipLaunchKernelGGL(k_sh_gather, dim3(grid_over(n)), dim3(kDrThreads), 0, st, *s, n, i_out, b_ctr, b_val, b_gam,
+                       b_prop, b_util, b_won);
+    AG_HIP(hipGetLastError());
+  }
+  out = SortedRecs{b_ctr, b_val, b_gam, b_prop, b_util, b_eu, b_won, d_off, n};
   return AG_OK;
 }
 
@@ -1006,50 +1353,13 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agen
   AgDeviceGuard g(c->device);
   const int N = c->shape.num_agents;
   hipStream_t st = (hipStream_t)stream;
-  std::vector<int64_t> cnt(N);
-  if (int rc = ag_shading_counts(c, s, cnt.data(), stream)) return rc;
-  int64_t n = 0;
-  for (int a = 0; a < N; ++a) n += cnt[a];
+  std::vector<int64_t> cnt(N), off;
+  SortedRecs SR;
+  if (int rc = sort_records(c, s, cnt, off, SR, st)) return rc;
   ag_dr_ws &w = c->dr;
-  // offsets (exclusive scan, host)
-  std::vector<int64_t> off((size_t)N + 1);
-  off[0] = 0;
-  for (int a = 0; a < N; ++a) off[a + 1] = off[a] + cnt[a];
-  int64_t *d_off = w.counts + N;  // [N + 1] offsets
-  AG_HIP(hipMemcpyAsync(d_off, off.data(), sizeof(int64_t) * ((size_t)N + 1), hipMemcpyHostToDevice, st));
-  if (n >= ((int64_t)1 << 32)) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_bidder_update: >= 2^32 records");
-  // radix-sort workspace: keys in/out (8 B), indices in/out (4 B), then hipcub's temp
-  size_t sort_tmp = 0;
-  AG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint64_t *)nullptr, (uint64_t *)nullptr,
-                                            (uint32_t *)nullptr, (uint32_t *)nullptr, (int)(n > 0 ? n : 1), 0, 64,
-                                            st));
-  const size_t rec_bytes = (size_t)6 * sizeof(double) + 1;
-  const size_t need = (size_t)(n > 0 ? n : 1) * (rec_bytes + 24) + sort_tmp + 256;
-  if (need > w.buf_bytes) {
-    (void)hipFree(w.buf);
-    w.buf = nullptr;
-    const size_t bytes = need + (need >> 2);
-    AG_HIP(hipMalloc(&w.buf, bytes));
-    w.buf_bytes = bytes;
-  }
-  const size_t cap = (size_t)(n > 0 ? n : 1);
-  double *b_ctr = (double *)w.buf, *b_val = b_ctr + cap, *b_gam = b_val + cap, *b_prop = b_gam + cap,
-         *b_util = b_prop + cap, *b_eu = b_util + cap;
-  uint64_t *k_in = (uint64_t *)(b_eu + cap), *k_out = k_in + cap;
-  uint32_t *i_in = (uint32_t *)(k_out + cap), *i_out = i_in + cap;
-  uint8_t *b_won = (uint8_t *)(i_out + cap);
-  void *tmp = (void *)(((uintptr_t)(b_won + cap) + 255) & ~(uintptr_t)255);
-  if (n > 0) {
-    if (!s->order) return ag_set_error(AG_ERR_INVALID, "ag_bidder_update: the store needs order");
-    hipLaunchKernelGGL(k_sh_keys, dim3(grid_over(n)), dim3(kDrThreads), 0, st, *s, n, k_in, i_in);
-    AG_HIP(hipGetLastError());
-    int end_bit = 40;
-    while ((1ll << (end_bit - 40)) < N) ++end_bit;
-    AG_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, sort_tmp, k_in, k_out, i_in, i_out, (int)n, 0, end_bit, st));
-    hipLaunchKernelGGL(k_sh_gather, dim3(grid_over(n)), dim3(kDrThreads), 0, st, *s, n, i_out, b_ctr, b_val, b_gam,
-                       b_prop, b_util, b_won);
-    AG_HIP(hipGetLastError());
-  }
+  const int64_t *d_off = SR.d_off;
+  double *b_ctr = SR.ctr, *b_val = SR.val, *b_gam = SR.gam, *b_prop = SR.prop, *b_util = SR.util, *b_eu = SR.eu;
+  uint8_t *b_won = SR.won;
   int64_t *d_noff = w.scratch;                       // [N] noise offsets
   int32_t *d_epochs = (int32_t *)(w.scratch + N);     // [N][3] epochs, then [N] status
   int32_t *d_stat = d_epochs + 3 * (size_t)N;
@@ -1236,6 +1546,217 @@ int ag_dr_update(ag_ctx *c, const ag_shading_samples *s, const float *noise, con
     if (stat[a] == -3)
       return ag_set_error(AG_ERR_INVALID, "agent %d: the DR fit needs more than %d noise epochs", a, noise_epochs);
   return AG_OK;
+}
+
+// ---- resumable / record-parallel training (k_bidder_epoch) ----
+int ag_bidder_rp_begin(ag_ctx *c, const ag_shading_samples *s, const int32_t *agents, const int64_t *records_total,
+                       const int64_t *records_base, int64_t *totals, void *stream) {
+  if (c) c->image_dirty = true;
+  if (!c || !s || !totals) return ag_set_error(AG_ERR_INVALID, "ag_bidder_rp_begin: null argument");
+  AG_CHECK_STRUCT(s, "ag_bidder_rp_begin", "ag_shading_samples");
+  if (!s->ctr || !s->value || !s->propensity || !s->won || !s->order)
+    return ag_set_error(AG_ERR_INVALID, "ag_bidder_rp_begin: the store needs ctr, value, propensity, won, order");
+  if (!c->dr_loaded) return ag_set_error(AG_ERR_STATE, "ag_bidder_rp_begin: ag_set_dr_state not called");
+  AgDeviceGuard g(c->device);
+  const int N = c->shape.num_agents;
+  hipStream_t st = (hipStream_t)stream;
+  ag_dr_ws &w = c->dr;
+  ag_dr_rp &rp = w.rp;
+  std::vector<int32_t> mode(N), mask(N, 0);
+  AG_HIP(hipMemcpy(mode.data(), w.mode, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
+  for (int a = 0; a < N; ++a) {
+    const int bk = c->h_bkind ? c->h_bkind[a] : -1;
+    if (agents && !agents[a]) continue;
+    if (bk == AG_BIDDER_DOUBLY_ROBUST || bk == AG_BIDDER_VALUE_LEARNING) mask[a] = 1;
+    else if (bk == AG_BIDDER_POLICY_LEARNING && agents)
+      return ag_set_error(AG_ERR_UNSUPPORTED, "ag_bidder_rp_begin: agent %d: PolicyLearningBidder fits use "
+                          "fixed-order float sums (their result follows the record split): ag_bidder_update", a);
+  }
+  std::vector<int64_t> cnt(N), off;
+  SortedRecs SR;
+  if (int rc = sort_records(c, s, cnt, off, SR, st)) return rc;
+  // workgroups: one per kRpChunk of an agent's records on this rank, at least one per trained
+  // agent (a rank without records of it still steps its state and adds zeros)
+  constexpr int64_t kRpChunk = 2048;
+  std::vector<int32_t> nblk(N, 0), blk_agent, blk_rank, bar_off(N, 0);
+  int lines = 0;
+  for (int a = 0; a < N; ++a) {
+    if (!mask[a]) continue;
+    nblk[a] = (int32_t)std::max<int64_t>(1, (cnt[a] + kRpChunk - 1) / kRpChunk);
+    bar_off[a] = lines;
+    lines += std::max(1, agcoop::bar_lines(nblk[a]));
+    for (int r = 0; r < nblk[a]; ++r) {
+      blk_agent.push_back(a);
+      blk_rank.push_back(r);
+    }
+  }
+  const int G = (int)blk_agent.size();
+  if ((size_t)G > rp.cap_g || (size_t)lines > rp.cap_lines || !rp.st) {
+    (void)hipFree(rp.st);
+    (void)hipFree(rp.acc);
+    (void)hipFree(rp.tables);
+    rp.st = nullptr;
+    rp.acc = nullptr;
+    rp.tables = nullptr;
+    rp.cap_g = (size_t)G + 64;
+    rp.cap_lines = (size_t)lines + 16;
+    AG_HIP(hipMalloc(&rp.st, sizeof(FitSt) * 2 * (size_t)N));
+    // accumulator rows and barrier lines: [cap_lines][32] each
+    AG_HIP(hipMalloc(&rp.acc, (sizeof(int64_t) + sizeof(unsigned)) * 32 * rp.cap_lines));
+    AG_HIP(hipMalloc(&rp.tables, sizeof(int32_t) * (2 * rp.cap_g + 3 * (size_t)N) + sizeof(int64_t) * 2 * N + 16));
+  }
+  rp.bar = (unsigned *)(rp.acc + 32 * rp.cap_lines);
+  int32_t *d_bagent = rp.tables, *d_brank = d_bagent + rp.cap_g, *d_nblk = d_brank + rp.cap_g,
+          *d_baroff = d_nblk + N, *d_mask = d_baroff + N;
+  rp.ntot = (int64_t *)(((uintptr_t)(d_mask + N) + 15) & ~(uintptr_t)15);
+  rp.mask = d_mask;
+  AG_HIP(hipMemcpyAsync(d_bagent, blk_agent.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
+  AG_HIP(hipMemcpyAsync(d_brank, blk_rank.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
+  AG_HIP(hipMemcpyAsync(d_nblk, nblk.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
+  AG_HIP(hipMemcpyAsync(d_baroff, bar_off.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
+  AG_HIP(hipMemcpyAsync(d_mask, mask.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
+  std::vector<int64_t> nt(2 * (size_t)N);
+  for (int a = 0; a < N; ++a) {
+    nt[a] = records_total ? records_total[a] : cnt[a];
+    nt[N + a] = records_base ? records_base[a] : 0;
+    if (mask[a] && nt[a] < 1)
+      return ag_set_error(AG_ERR_INVALID, "agent %d: %s.update without logs", a,
+                          c->h_bkind[a] == AG_BIDDER_DOUBLY_ROBUST ? "DoublyRobustBidder" : "ValueLearningBidder");
+    if (nt[N + a] < 0 || nt[N + a] + cnt[a] > nt[a])
+      return ag_set_error(AG_ERR_INVALID, "ag_bidder_rp_begin: agent %d: records_base %lld + %lld local records "
+                          "> records_total %lld", a, (long long)nt[N + a], (long long)cnt[a], (long long)nt[a]);
+  }
+  AG_HIP(hipMemcpyAsync(rp.ntot, nt.data(), sizeof(int64_t) * 2 * N, hipMemcpyHostToDevice, st));
+  if (lines) AG_HIP(hipMemsetAsync(rp.acc, 0, (sizeof(int64_t) + sizeof(unsigned)) * 32 * rp.cap_lines, st));
+  AG_HIP(hipMemsetAsync(totals, 0, sizeof(int64_t) * 2 * 32 * (size_t)N, st));
+  hipLaunchKernelGGL(k_rp_init, dim3((N + 255) / 256), dim3(256), 0, st, N, c->d_bkind, w.mode, d_mask, w.state,
+                     (FitSt *)rp.st);
+  AG_HIP(hipGetLastError());
+  if (int rc = dr_ws_ready(c)) return rc;  // the Adam table
+  rp.G = G;
+  rp.lines = lines;
+  rp.k = 0;
+  rp.totals = totals;
+  rp.noise = nullptr;
+  rp.noise_n = 0;
+  rp.noise_e0 = rp.noise_epochs = 0;
+  rp.n_local = SR.n;
+  rp.active = true;
+  (void)mode;
+  return AG_OK;
+}
+
+int ag_bidder_rp_noise(ag_ctx *c, const float *noise, int64_t noise_n, int32_t first_epoch, int32_t epochs) {
+  if (!c || !c->dr.rp.active) return ag_set_error(AG_ERR_STATE, "ag_bidder_rp_noise: no ag_bidder_rp_begin");
+  if (noise && (noise_n < 1 || first_epoch < 0 || epochs < 0))
+    return ag_set_error(AG_ERR_INVALID, "ag_bidder_rp_noise: bad window");
+  ag_dr_rp &rp = c->dr.rp;
+  rp.noise = noise;
+  rp.noise_n = noise_n;
+  rp.noise_e0 = first_epoch;
+  rp.noise_epochs = epochs;
+  return AG_OK;
+}
+
+int ag_bidder_rp_epoch(ag_ctx *c, int32_t launches, int64_t *launch_index, float *traces, void *stream) {
+  if (!c || !c->dr.rp.active) return ag_set_error(AG_ERR_STATE, "ag_bidder_rp_epoch: no ag_bidder_rp_begin");
+  if (launches < 0) return ag_set_error(AG_ERR_INVALID, "ag_bidder_rp_epoch: launches < 0");
+  AgDeviceGuard g(c->device);
+  const int N = c->shape.num_agents;
+  hipStream_t st = (hipStream_t)stream;
+  ag_dr_ws &w = c->dr;
+  ag_dr_rp &rp = w.rp;
+  const int64_t cap = rp.n_local > 0 ? rp.n_local : 1;
+  double *b_ctr = (double *)w.buf;
+  DrRecords R{b_ctr, b_ctr + cap, b_ctr + 2 * cap, b_ctr + 3 * cap, b_ctr + 4 * cap,
+              (const uint8_t *)((uint32_t *)((uint64_t *)(b_ctr + 6 * cap) + 2 * cap) + 2 * cap)};
+  double *b_eu = b_ctr + 5 * cap;
+  int32_t *d_bagent = rp.tables, *d_brank = d_bagent + rp.cap_g, *d_nblk = d_brank + rp.cap_g, *d_baroff = d_nblk + N;
+  FitSt *S = (FitSt *)rp.st;
+  for (int32_t l = 0; l < launches; ++l) {
+    const int64_t k = rp.k;
+    if (rp.G > 0)
+      hipLaunchKernelGGL(k_bidder_epoch, dim3(rp.G), dim3(kDrThreads), 0, st, c->d_bkind, w.mode, w.init, d_bagent,
+                         d_brank, d_nblk, w.counts + N, rp.ntot, rp.ntot + N, R, b_eu, S + (size_t)(k & 1) * N,
+                         S + (size_t)((k + 1) & 1) * N, rp.totals + (size_t)((k + 1) & 1) * 32 * N,
+                         rp.totals + (size_t)(k & 1) * 32 * N, rp.acc, rp.bar, d_baroff, rp.noise, rp.noise_n,
+                         rp.noise_e0, rp.noise_epochs, c->fit_noise_seed, w.adam_tab, traces);
+    AG_HIP(hipGetLastError());
+    rp.k = k + 1;
+  }
+  if (launch_index) *launch_index = rp.k - 1;  // the last launch: its totals are at totals + 32 N (index & 1)
+  return AG_OK;
+}
+
+int ag_bidder_rp_poll(ag_ctx *c, int32_t *fit, int32_t *epoch, int32_t *need_noise, void *stream) {
+  if (!c || !c->dr.rp.active) return ag_set_error(AG_ERR_STATE, "ag_bidder_rp_poll: no ag_bidder_rp_begin");
+  AgDeviceGuard g(c->device);
+  const int N = c->shape.num_agents;
+  ag_dr_rp &rp = c->dr.rp;
+  std::vector<FitSt> h(N);
+  hipStream_t st = (hipStream_t)stream;
+  AG_HIP(hipMemcpyAsync(h.data(), (FitSt *)rp.st + (size_t)(rp.k & 1) * N, sizeof(FitSt) * N, hipMemcpyDeviceToHost,
+                        st));
+  AG_HIP(hipStreamSynchronize(st));
+  for (int a = 0; a < N; ++a) {
+    if (fit) fit[a] = h[a].fit == kFitDone ? -1 : h[a].fit;
+    if (epoch) epoch[a] = h[a].epoch;
+    if (need_noise) need_noise[a] = h[a].need_noise ? h[a].epoch : -1;
+  }
+  return AG_OK;
+}
+
+int ag_bidder_rp_end(ag_ctx *c, int32_t *epochs, int32_t *status, void *stream) {
+  if (!c || !c->dr.rp.active) return ag_set_error(AG_ERR_STATE, "ag_bidder_rp_end: no ag_bidder_rp_begin");
+  c->image_dirty = true;
+  AgDeviceGuard g(c->device);
+  const int N = c->shape.num_agents;
+  ag_dr_ws &w = c->dr;
+  ag_dr_rp &rp = w.rp;
+  hipStream_t st = (hipStream_t)stream;
+  std::vector<FitSt> h(N);
+  std::vector<int32_t> mask(N), init(N), mode(N);
+  std::vector<float> state(16 * (size_t)N);
+  AG_HIP(hipMemcpyAsync(h.data(), (FitSt *)rp.st + (size_t)(rp.k & 1) * N, sizeof(FitSt) * N, hipMemcpyDeviceToHost,
+                        st));
+  AG_HIP(hipMemcpyAsync(mask.data(), rp.mask, sizeof(int32_t) * N, hipMemcpyDeviceToHost, st));
+  AG_HIP(hipStreamSynchronize(st));
+  rp.active = false;
+  for (int a = 0; a < N; ++a)
+    if (mask[a] && h[a].fit != kFitDone)
+      return ag_set_error(AG_ERR_STATE, "ag_bidder_rp_end: agent %d is still training (fit %d, epoch %d)", a,
+                          h[a].fit, h[a].epoch);
+  AG_HIP(hipMemcpy(state.data(), w.state, sizeof(float) * 16 * N, hipMemcpyDeviceToHost));
+  AG_HIP(hipMemcpy(init.data(), w.init, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
+  AG_HIP(hipMemcpy(mode.data(), w.mode, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
+  static const char *names[] = {"", "", "ValueLearningBidder", "PolicyLearningBidder", "DoublyRobustBidder"};
+  int rc = AG_OK;
+  for (int a = 0; a < N; ++a) {
+    if (epochs) epochs[3 * a] = epochs[3 * a + 1] = epochs[3 * a + 2] = 0;
+    if (status) status[a] = 0;
+    if (!mask[a]) continue;
+    if (epochs)
+      for (int j = 0; j < 3; ++j) epochs[3 * a + j] = h[a].ep[j];
+    if (status) status[a] = h[a].status;
+    const int bk = c->h_bkind[a];
+    if (h[a].status == -2 && rc == AG_OK)
+      rc = ag_set_error(AG_ERR_INVALID, "agent %d: %s: NAN DETECTED! in losses (src/Bidder.py:%d)", a, names[bk],
+                        bk == AG_BIDDER_DOUBLY_ROBUST ? 592 : 409);
+    if (h[a].status != 1) {  // the fallback trains nothing (src/Bidder.py:206-211)
+      for (int j = 0; j < 4; ++j) state[16 * (size_t)a + j] = h[a].wr[j];
+      for (int j = 0; j < 12; ++j) state[16 * (size_t)a + 4 + j] = h[a].pol[j];
+    }
+    // from now on the agent bids from what it fitted (ag_bidder_update's rule)
+    if (bk == AG_BIDDER_DOUBLY_ROBUST)
+      init[a] = AG_LEARNER_POLICY;
+    else
+      init[a] = h[a].status == 1 ? AG_LEARNER_UNINITIALISED
+                                 : (mode[a] == AG_VL_POLICY ? AG_LEARNER_POLICY : AG_LEARNER_SEARCH);
+  }
+  AG_HIP(hipMemcpy(w.state, state.data(), sizeof(float) * 16 * N, hipMemcpyHostToDevice));
+  AG_HIP(hipMemcpy(w.init, init.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice));
+  learner_flags(c, init.data());
+  return rc;
 }
 
 int ag_set_bidder_modes(ag_ctx *c, const int32_t *modes) {

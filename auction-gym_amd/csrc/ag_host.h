@@ -48,6 +48,26 @@ struct ag_lrts_ws {
   int32_t *status = nullptr;  // [1] device-side error flags
 };
 
+// Resumable / record-parallel training of the exact-sum learning bidders (ag_bidder_rp_*,
+// ag_dr.hip): one launch per epoch, the training state in HBM.
+struct ag_dr_rp {
+  bool active = false;
+  void *st = nullptr;           // FitSt [2][N], by launch parity
+  int64_t *acc = nullptr;       // agents' combining-tree accumulator rows [lines][32]
+  unsigned *bar = nullptr;      // agents' barrier lines [lines][32]
+  int32_t *tables = nullptr;    // blk_agent [G], blk_rank [G], agent_nblk [N], bar_off [N]
+  int64_t *ntot = nullptr;      // [N] records over all ranks, [N] global index of this rank's first
+  size_t cap_g = 0, cap_lines = 0;
+  int G = 0, lines = 0;
+  int64_t k = 0;                // launches so far
+  int64_t *totals = nullptr;    // the caller's dev int64 [2][N][32]
+  const float *noise = nullptr; // host-drawn rsample window (ag_bidder_rp_noise)
+  int64_t noise_n = 0;
+  int32_t noise_e0 = 0, noise_epochs = 0;
+  int32_t *mask = nullptr;      // [N] the agents under training (host copy in `agents`)
+  int64_t n_local = 0;
+};
+
 // DoublyRobustBidder workspace (ag_dr.hip)
 struct ag_dr_ws {
   void *buf = nullptr;          // records in log order (ctr, value, gamma, prop, util, est_util,
@@ -63,6 +83,7 @@ struct ag_dr_ws {
   size_t coop_bytes = 0;
   int coop_blocks = 0;          // co-resident workgroups of k_bidder_train<1>
   int coop_blocks0 = 0;         // co-resident workgroups of k_bidder_train<0>
+  ag_dr_rp rp;
 };
 
 struct ag_ctx {

@@ -168,7 +168,9 @@ void torch_store(const TorchRng &t, uint8_t *b) {
     const uint64_t w = t.state[i];
     memcpy(b + 24 + 8 * i, &w, 8);
   }
-  memcpy(b + 5024, &t.normal_y, 8);
+  // torch's get_state() fills normal_y only while the cached value is valid (0 otherwise)
+  const double y = t.normal_valid ? t.normal_y : 0.0;
+  memcpy(b + 5024, &y, 8);
   memcpy(b + 5040, &t.normal_valid, 4);
 }
 
@@ -503,5 +505,45 @@ extern "C" int ag_replay_draw_population(ag_pcg64_state *rng, uint8_t *torch_sta
   rng->has_uint32 = st.has_uint32;
   rng->uinteger = st.uinteger;
   if (torch_draws) torch_store(tr, torch_state);
+  return AG_OK;
+}
+
+// `epochs` x torch.empty(n).normal_() from torch's CPU generator (the rsample draws of the
+// learning bidders' policy fits, Normal.rsample -> _standard_normal, src/Models.py:160, :87),
+// one epoch per row of out [epochs][n]; the generator (the torch.get_rng_state() blob) is
+// advanced in place. n >= 16: normal_fill_AVX2 (n uniforms, + 16 for the recomputed last block);
+// n < 16: the scalar kernel, (float) normal_distribution<double> per element with its cached
+// second value. The generator pass runs in draw order, the transforms in parallel.
+extern "C" int ag_torch_normal_epochs(uint8_t *torch_state, int64_t torch_state_bytes, int64_t n, int32_t epochs,
+                                      float *out) {
+  if (!torch_state || torch_state_bytes != kTorchStateBytes || (!out && epochs > 0))
+    return ag_set_error(AG_ERR_INVALID, "ag_torch_normal_epochs: needs the %lld-byte torch.get_rng_state() blob "
+                        "and out", (long long)kTorchStateBytes);
+  if (n < 1 || epochs < 0 || n > (int64_t)1 << 31)
+    return ag_set_error(AG_ERR_INVALID, "ag_torch_normal_epochs: bad sizes");
+  TorchRng tr;
+  torch_load(tr, torch_state);
+  if (n < 16) {
+    for (int64_t e = 0; e < epochs; ++e)
+      for (int64_t i = 0; i < n; ++i) out[e * n + i] = (float)torch_normal_double(tr);
+  } else {
+    const int64_t U = normal_fill_uniforms((int)n);
+    std::vector<float> u((size_t)U * (size_t)epochs);
+    for (int64_t e = 0; e < epochs; ++e) torch_normal_fill_uniforms(tr, u.data() + (size_t)e * U, (int)n);
+    // epochs split over the host threads (the per-epoch work is n floats: split by epochs * n)
+    const int T = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(host_threads(), epochs),
+                                                              (int64_t)epochs * n / 4096));
+    auto run = [&](int64_t e0, int64_t e1) {
+      for (int64_t e = e0; e < e1; ++e) torch_normal_fill_transform(out + e * n, u.data() + (size_t)e * U, (int)n);
+    };
+    if (T <= 1) {
+      run(0, epochs);
+    } else {
+      std::vector<std::thread> th;
+      for (int k = 0; k < T; ++k) th.emplace_back([&, k] { run((int64_t)epochs * k / T, (int64_t)epochs * (k + 1) / T); });
+      for (auto &t : th) t.join();
+    }
+  }
+  torch_store(tr, torch_state);
   return AG_OK;
 }

@@ -43,6 +43,9 @@ namespace ag {
 #ifndef AG_MIN_WAVES
 #define AG_MIN_WAVES 1
 #endif
+#ifndef AG_STREAM_MIN_P
+#define AG_STREAM_MIN_P 3  // general kernel: streamed slots (no per-slot result arrays) from this P on
+#endif
 #ifndef AG_MAX_REPLICAS
 #define AG_MAX_REPLICAS 16
 #endif
@@ -883,9 +886,15 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
   double uv[W];
   int jv[PA][W];  // compact ts_noise_index entries (GENERAL with ts_noise_index; else kTsjLoad)
   const bool pre_tsj = GENERAL && !AG_PREFETCH && in.ts_noise_index && in.ts_noise && prm.ts_sample;
+  // streamed slots (below): each slot's participant / noise index loaded with the slot
+  constexpr bool kStream = GENERAL != kGenOracle && W == 1 && P >= AG_STREAM_MIN_P;
   auto load_tile = [&](uint32_t i) {
 #pragma unroll
     for (int e = 0; e < D - 1; ++e) ld_f64<W>(in.ctx + e * B + i, xv[e]);
+    if constexpr (kStream) {
+      ld_f64<W>(in.u + i, uv);
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < P; ++s) ld_i32<W>(in.part + s * B + i, pv[s]);
     ld_f64<W>(in.u + i, uv);
@@ -1061,6 +1070,71 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
 #define UV uv
 #endif
 
+    if constexpr (kStream) {
+      // Streamed slots (wide auctions): each slot resolved with its bid made in place (a fitted
+      // policy's forward included), its outputs stored and its winner-independent counter terms
+      // added at once, the top-2 carried along in slot order together with the leader's true
+      // CTR, value and est / true ratio. Only each slot's bid and true EV stay live, for the
+      // losers' underbid terms: 4 VGPRs per slot instead of the 16+ the deferred paths keep
+      // (at P = 8 those spilled 880 B per lane to scratch in the 1024-lane build, more than
+      // doubling its HBM traffic). The same values, the same exact integer counter terms.
+      double x[kMaxD];
+      float xf[kMaxD];
+      float xabs = 1.0f;
+#pragma unroll
+      for (int e = 0; e < D - 1; ++e) {
+        x[e] = XV[e][0];
+        xf[e] = (float)x[e];
+        xabs += fabsf(xf[e]);
+      }
+      x[D - 1] = 1.0;  // intercept (src/Auction.py:33)
+      xf[D - 1] = 1.0f;
+      xabs *= 1.001f;
+      double m1 = 0.0, m2 = -INFINITY, ctr_w = 0.0, val_w = 0.0, rat_w = 0.0;
+      int w = 0;
+      double bidv[PA], tvv[PA];
+#pragma unroll
+      for (int s = 0; s < P; ++s) {
+        const uint32_t o = s * B + i;
+        const int a = ldg(in.part + o);
+        const SlotResult q = resolve_slot<D, PRUNE, GENERAL, false>(T, K, x, xf, xabs, a, s, in, B, i,
+                                                                    prm.ts_sample != 0);
+        if (out.item) stg(out.item + o, (int32_t)q.item);
+        if (out.bid) stg(out.bid + o, q.bid);
+        if (out.est_ctr) stg(out.est_ctr + o, q.est);
+        if (out.true_ctr) stg(out.true_ctr + o, q.ctr);
+        if (out.best_ev) stg(out.best_ev + o, q.bev);
+        if (out.gamma) stg(out.gamma + o, q.gamma);
+        if (out.propensity) stg(out.propensity + o, q.prop);
+        if (prm.want_counters) count_pre(a, q.ctr, q.val, q.est, q.bev);
+        bidv[s] = q.bid;
+        tvv[s] = q.ctr * q.val;
+        // top2_step, with the leader's values captured as it changes (ties -> lowest slot)
+        if (s == 0 || q.bid > m1) {
+          if (s != 0) m2 = m1;
+          m1 = q.bid;
+          w = s;
+          ctr_w = q.ctr;
+          val_w = q.val;
+          rat_w = q.est / q.ctr;
+        } else if (q.bid > m2) {
+          m2 = q.bid;
+        }
+      }
+      const double price = prm.mech == AG_FIRST_PRICE ? m1 : m2;
+      const int oc = bernoulli(ctr_w, UV[0]);  // src/Auction.py:65
+      if (out.winner) stg(out.winner + i, (int32_t)w);
+      if (out.price) stg(out.price + i, charged ? price : (double)NAN);
+      if (out.second_price) stg(out.second_price + i, charged ? m2 : (double)NAN);
+      if (out.outcome) stg(out.outcome + i, (uint8_t)oc);
+      if (prm.want_counters) {
+#pragma unroll
+        for (int s = 0; s < P; ++s)
+          count_post(ldg(in.part + s * B + i), charged && s == w, charged ? price : 0.0, price, m2, bidv[s], tvv[s],
+                     val_w, rat_w, oc);
+      }
+      continue;
+    }
 #if AG_EARLY_COUNT
     if constexpr (GENERAL == kGenAll && W == 1 && P > 0) {  // A/B: +2 % on kGenTruthful (configs_1), -4 % on the mix
       // each slot's outputs stored and its winner-independent counter terms added as soon

@@ -375,6 +375,13 @@ int ag_replay_draw(ag_pcg64_state *rng, int64_t B, int32_t N, int32_t P, int32_t
  * policy_eps [P][B] float (0 where nothing is drawn) when policy; gamma_grid [P][128][B]
  * (0 where nothing is drawn) when search. Identical numbers and generator states to the
  * Python loop (tests/test_host.py::test_replay_population_draws_match_python). */
+/* `epochs` x torch.empty(n).normal_() from torch's CPU generator: the learning bidders'
+ * per-epoch rsample draws of their policy fits (src/Models.py:160, :87 via src/Bidder.py:
+ * 278-303, :574-595), epoch e at out[e * n + i] (host float32 [epochs][n]); torch_state: the
+ * torch.get_rng_state() blob (host, 5056 B), advanced in place as the reference's draws
+ * advance the global generator. Host only (no device). */
+int ag_torch_normal_epochs(uint8_t *torch_state, int64_t torch_state_bytes, int64_t n, int32_t epochs, float *out);
+
 int ag_replay_draw_population(ag_pcg64_state *rng, uint8_t *torch_state, int64_t torch_state_bytes, int64_t B,
                               int32_t N, int32_t P, int32_t E, double embedding_var, int32_t max_slots,
                               const uint8_t *shading, const double *prev_gamma, const double *gamma_sigma,
@@ -504,6 +511,45 @@ int ag_set_bidder_modes(ag_ctx *ctx, const int32_t *modes);
 int ag_bidder_update(ag_ctx *ctx, const ag_shading_samples *samples, const int32_t *agents, const float *noise,
                      const int64_t *noise_offsets, int32_t noise_epochs, int32_t *epochs, int32_t *status,
                      float *traces, void *stream);
+
+/* ---- Resumable, record-parallel update of the exact-sum learning bidders ----
+ * ValueLearningBidder and DoublyRobustBidder (src/Bidder.py:204-325, :473-615; replaces the
+ * per-epoch loops of src/Bidder.py:239-260, :278-323, :517-538, :574-595) as ONE LAUNCH PER
+ * EPOCH with each learner's training state (model, Adam, scheduler, early stop, fit) in
+ * device memory between launches. Two uses:
+ *  - record-parallel over G ranks (one process per GPU, each holding the records of its own
+ *    auction shard): after every ag_bidder_rp_epoch(launches = 1) the caller SUMs the int64
+ *    words totals[launch_index & 1] ([N][32], dev) over the ranks in place (an all-reduce;
+ *    the sums are exact integers) before the next call; every rank then steps to the same
+ *    model, bit for bit the model ag_bidder_update fits in one process on all the records;
+ *  - one process feeding a fit host-drawn rsample noise window by window (ag_bidder_rp_noise):
+ *    a policy fit reaching an epoch outside the window waits (ag_bidder_rp_poll need_noise)
+ *    with its state kept -- nothing is re-run.
+ * records_total / records_base: host int64 [N], agent a's records over all ranks and the
+ * global log-order index of this rank's first one (NULL: this process holds them all); the
+ * synthetic rsample draws are keyed by that global index. agents: host int32 [N] mask (NULL:
+ * every ValueLearning / DoublyRobust bidder; a PolicyLearningBidder is refused: its fits sum
+ * floats in a fixed order). totals: caller-owned dev int64 [2][N][32]. The store's records
+ * stay in the workspace until ag_bidder_rp_end: no other learning-bidder update in between. */
+int ag_bidder_rp_begin(ag_ctx *ctx, const ag_shading_samples *samples, const int32_t *agents,
+                       const int64_t *records_total, const int64_t *records_base, int64_t *totals, void *stream);
+/* Queue `launches` epoch launches (stream-ordered, asynchronous); launch_index (host, may be
+ * NULL) = the last launch's index: its rank totals are at totals + 32 N (launch_index & 1).
+ * traces: dev float32 [N][3][32768] per-epoch losses (the rank holding global record 0), or NULL. */
+int ag_bidder_rp_epoch(ag_ctx *ctx, int32_t launches, int64_t *launch_index, float *traces, void *stream);
+/* The host-drawn rsample window of the noisy policy fits: noise dev float32, policy-fit epoch e
+ * of record i (global index) at noise[(e - first_epoch) * noise_n + i], first_epoch <= e <
+ * first_epoch + epochs; NULL: synthetic draws (AG_OPT_FIT_NOISE_SEED). */
+int ag_bidder_rp_noise(ag_ctx *ctx, const float *noise, int64_t noise_n, int32_t first_epoch, int32_t epochs);
+/* After the queued launches (synchronises): per agent, host int32 [N] each (any may be NULL):
+ * fit = the fit in progress (0 win count, 1 win-rate, 2 estimated utilities, 3 imitation, 4
+ * policy) or -1 done; epoch = epochs run in it; need_noise = the policy epoch waiting for
+ * noise, or -1. */
+int ag_bidder_rp_poll(ag_ctx *ctx, int32_t *fit, int32_t *epoch, int32_t *need_noise, void *stream);
+/* Every trained agent done: its model and bidding state applied as ag_bidder_update applies
+ * them; epochs host int32 [N][3], status host int32 [N] as ag_bidder_update's (may be NULL).
+ * AG_ERR_INVALID on a NaN loss (the reference exits), AG_ERR_STATE while an agent trains. */
+int ag_bidder_rp_end(ag_ctx *ctx, int32_t *epochs, int32_t *status, void *stream);
 
 /* ---- Per-call plugin surface (one agent, n requests; n = 1 is the reference's call) ----
  * Allocator.estimate_CTR of agent `agent` for n contexts (dev), ctr dev [n][K]:

@@ -458,6 +458,29 @@ void ora_gen_participants(uint64_t seed, uint64_t idx, int32_t N, int32_t P, int
 
 static int64_t fx_round(double v, double scale) { return (int64_t)nearbyint(v * scale); }
 
+/* ---- record-parallel hook (ag_oracle.h ora_set_reduce): exact sums over the ranks ---- */
+static ora_reduce_fn g_reduce = NULL;
+static int64_t g_n_total = 0;
+void ora_set_reduce(ora_reduce_fn fn, int64_t n_total) {
+  g_reduce = fn;
+  g_n_total = n_total;
+}
+int ora_reducing(void) { return g_reduce != NULL; }
+/* records of the fit over all ranks (the means' denominators, the reference's checks) */
+int64_t ora_total(int64_t n) { return g_reduce && g_n_total > 0 ? g_n_total : n; }
+/* s[0..k) summed over the ranks, exactly (32-bit halves as int64 words: no overflow) */
+void ora_reduce128(__int128 *s, int32_t k) {
+  if (!g_reduce || k <= 0) return;
+  int64_t *w = malloc(sizeof(int64_t) * 2 * (size_t)k);
+  for (int32_t j = 0; j < k; ++j) {
+    w[2 * j] = (int64_t)(s[j] >> 32);
+    w[2 * j + 1] = (int64_t)(s[j] & 0xffffffff);
+  }
+  g_reduce(w, 2 * k);
+  for (int32_t j = 0; j < k; ++j) s[j] = ((__int128)w[2 * j] << 32) + (__int128)w[2 * j + 1];
+  free(w);
+}
+
 static double fx_read(__int128 s, double inv_scale) {
   /* the device holds these sums split at bit 24; same read-back */
   int64_t hi = (int64_t)(s >> 24), lo = (int64_t)(s & 0xFFFFFF);
@@ -480,6 +503,15 @@ static float lrts_loss_grad(int64_t n, int32_t K, int32_t Do, const float *X, co
     L += fx_round(t, 0x1p32);
     double gz = (double)p - (double)y[i];
     for (int32_t d = 0; d < Do; ++d) G[A[i] * Do + d] += fx_round(gz * (double)x[d], 0x1p40);
+  }
+  if (ora_reducing()) { /* one exchange of the KD gradient sums and the loss */
+    __int128 *t = malloc(sizeof(__int128) * (size_t)(KD + 1));
+    for (int32_t c = 0; c < KD; ++c) t[c] = G[c];
+    t[KD] = L;
+    ora_reduce128(t, KD + 1);
+    for (int32_t c = 0; c < KD; ++c) G[c] = t[c];
+    L = t[KD];
+    free(t);
   }
   double prior = 0.0;
   for (int32_t k = 0; k < K; ++k)
@@ -504,7 +536,7 @@ float ora_lrts_loss_grad(int64_t n, int32_t K, int32_t Do, const float *X, const
 
 int32_t ora_lrts_update(int64_t n, int32_t K, int32_t Do, const float *X, const int32_t *A,
                         const uint8_t *y, float *m, float *pm, float *q, float *loss_trace) {
-  if (n < 2) return 0;
+  if (ora_total(n) < 2) return 0;
   const int32_t KD = K * Do;
   float *ea = calloc(KD, sizeof(float)), *es = calloc(KD, sizeof(float)), *g = malloc(KD * sizeof(float));
   __int128 *G = malloc(KD * sizeof(__int128));
@@ -551,6 +583,7 @@ int32_t ora_lrts_update(int64_t n, int32_t K, int32_t Do, const float *X, const 
     float wgt = P * (1.0f - P);
     for (int32_t d = 0; d < Do; ++d) G[A[i] * Do + d] += fx_round((double)wgt * (double)(x[d] * x[d]), 0x1p40);
   }
+  ora_reduce128(G, KD);
   for (int32_t c = 0; c < KD; ++c) {
     q[c] = q[c] + (float)fx_read(G[c], 0x1p-40);
     pm[c] = m[c];

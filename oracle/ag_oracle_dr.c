@@ -117,6 +117,10 @@ static double dsoftplus(double u) {
   return e / (e + 1.0);
 }
 
+/* the record-parallel hook (ag_oracle.c): sums over the ranks, records over the ranks */
+int64_t ora_total(int64_t n);
+void ora_reduce128(__int128 *s, int32_t k);
+
 #define DR_GRID 0x1p40
 #define DR_INV 0x1p-40
 
@@ -253,7 +257,7 @@ static void policy_bwd(const float *p, double c, double v, const polf_t *f, doub
  * 1e-7), early stop after `wait` epochs without a 1e-6 improvement, <= 32768 epochs. */
 static int32_t fit_winrate(int64_t n, const float *cf, const float *vf, const float *gf, const uint8_t *won,
                            float *wr, int32_t patience, double factor, int32_t wait, float *trace) {
-  const double M = 2.0 * (double)n;
+  const double M = 2.0 * (double)ora_total(n);
   adam_t ad;
   adam_init(&ad, 4, 3e-3, 1e-6);
   plateau_t pl;
@@ -281,6 +285,12 @@ static int32_t fit_winrate(int64_t n, const float *cf, const float *vf, const fl
       G[1] += fxr(gz * v);
       G[2] += fxr(gz * g);
       G[3] += fxr(gz);
+    }
+    {
+      __int128 t[5] = {L, G[0], G[1], G[2], G[3]};
+      ora_reduce128(t, 5);
+      L = t[0];
+      for (int j = 0; j < 4; ++j) G[j] = t[1 + j];
     }
     const float loss = (float)(fxv(L) / M);
     float grad[4];
@@ -317,9 +327,20 @@ static int32_t fit_imitation(int64_t n, const float *cf, const float *vf, const 
       L2 += fxr(dsg * dsg);
       policy_bwd(pol, cf[i], vf[i], &f, 2.0 * dm, 2.0 * dsg, G);
     }
-    const float loss = (float)(fxv(L1) / (double)n + fxv(L2) / (double)n);
+    {
+      __int128 t[14];
+      t[0] = L1;
+      t[1] = L2;
+      for (int j = 0; j < 12; ++j) t[2 + j] = G[j];
+      ora_reduce128(t, 14);
+      L1 = t[0];
+      L2 = t[1];
+      for (int j = 0; j < 12; ++j) G[j] = t[2 + j];
+    }
+    const double nt = (double)ora_total(n);
+    const float loss = (float)(fxv(L1) / nt + fxv(L2) / nt);
     float grad[12];
-    for (int j = 0; j < 12; ++j) grad[j] = (float)(fxv(G[j]) / (double)n);
+    for (int j = 0; j < 12; ++j) grad[j] = (float)(fxv(G[j]) / nt);
     adam_step(&ad, pol, grad);
     if (trace) trace[e] = loss;
     if (stop_step(&st, e, loss)) {
@@ -334,7 +355,7 @@ int32_t ora_dr_update(int64_t n, const double *ctr, const double *value, const d
                       const double *prop, const uint8_t *won, const double *util, float *wr, float *pol,
                       int32_t initialised, const float *noise, int64_t noise_epochs, int32_t *epochs,
                       float *wr_trace, float *init_trace, float *dr_trace, double *est_util_out) {
-  if (n < 1) return -1;
+  if (ora_total(n) < 1) return -1;
   float *cf = malloc(n * sizeof(float)), *vf = malloc(n * sizeof(float)), *gf = malloc(n * sizeof(float));
   double *eu = malloc(n * sizeof(double));
   for (int64_t i = 0; i < n; ++i) {
@@ -400,9 +421,17 @@ int32_t ora_dr_update(int64_t n, const double *ctr, const double *value, const d
         const double dsg = -(dpi_dsg + ddm_dgs * (double)eps[i]);
         policy_bwd(pol, c, v, &f, dmu, dsg, G);
       }
-      const float loss = (float)(fxv(L) / (double)n);
+      {
+        __int128 t[13];
+        t[0] = L;
+        for (int j = 0; j < 12; ++j) t[1 + j] = G[j];
+        ora_reduce128(t, 13);
+        L = t[0];
+        for (int j = 0; j < 12; ++j) G[j] = t[1 + j];
+      }
+      const float loss = (float)(fxv(L) / (double)ora_total(n));
       float grad[12];
-      for (int j = 0; j < 12; ++j) grad[j] = (float)(fxv(G[j]) / (double)n);
+      for (int j = 0; j < 12; ++j) grad[j] = (float)(fxv(G[j]) / (double)ora_total(n));
       adam_step(&ad, pol, grad);
       if (dr_trace) dr_trace[e] = loss;
       plateau_step(&pl, loss, &ad.lr);
@@ -532,9 +561,10 @@ int32_t ora_vl_update(int64_t n, const double *ctr, const double *value, const d
                       const uint8_t *won, float *wr, float *pol, int32_t policy, const float *noise,
                       int64_t noise_epochs, int32_t *epochs, float *wr_trace, float *pol_trace) {
   epochs[0] = epochs[1] = epochs[2] = 0;
-  if (n < 1) return -1;
-  int64_t wins = 0;
+  if (ora_total(n) < 1) return -1;
+  __int128 wins = 0;
   for (int64_t i = 0; i < n; ++i) wins += won[i] != 0;
+  ora_reduce128(&wins, 1);
   if (!wins) return 1;
   float *cf = malloc(n * sizeof(float)), *vf = malloc(n * sizeof(float)), *gf = malloc(n * sizeof(float));
   for (int64_t i = 0; i < n; ++i) {
@@ -567,9 +597,17 @@ int32_t ora_vl_update(int64_t n, const double *ctr, const double *value, const d
         if (raw >= 0.0 && raw <= 1.0) ddm_dgs = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)wr[2];
         policy_bwd(pol, c, v, &f, -ddm_dgs, -(ddm_dgs * (double)eps[i]), G);
       }
-      const float loss = (float)(fxv(L) / (double)n);
+      {
+        __int128 t[13];
+        t[0] = L;
+        for (int j = 0; j < 12; ++j) t[1 + j] = G[j];
+        ora_reduce128(t, 13);
+        L = t[0];
+        for (int j = 0; j < 12; ++j) G[j] = t[1 + j];
+      }
+      const float loss = (float)(fxv(L) / (double)ora_total(n));
       float grad[12];
-      for (int j = 0; j < 12; ++j) grad[j] = (float)(fxv(G[j]) / (double)n);
+      for (int j = 0; j < 12; ++j) grad[j] = (float)(fxv(G[j]) / (double)ora_total(n));
       adam_step(&ad, pol, grad);
       if (pol_trace) pol_trace[e] = loss;
       plateau_step(&pl, loss, &ad.lr);

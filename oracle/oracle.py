@@ -63,6 +63,8 @@ def lib():
         L = ctypes.CDLL(_SO)
         d, i32, i64, u64 = ctypes.c_double, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
         vp = ctypes.c_void_p
+        L.ora_set_reduce.restype = None
+        L.ora_set_reduce.argtypes = [ctypes.c_void_p, i64]
         L.ora_sigmoid.restype = d
         L.ora_sigmoid.argtypes = [d]
         L.ora_dot.restype = d
@@ -374,6 +376,28 @@ def search_gamma(wr, ctr, value, grid):
     wr = np.ascontiguousarray(wr, np.float32)
     grid = np.ascontiguousarray(grid, np.float64)
     return float(lib().ora_search_gamma(_p(wr), float(ctr), float(value), _p(grid), 1))
+
+
+REDUCE_FN = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_int64), ctypes.c_int32)
+_reduce_cb = None
+
+
+def set_reduce(fn, n_total=0):
+    """Record-parallel fits (oracle/ag_oracle.h ora_set_reduce): fn(words) sums an int64 numpy
+    array in place over the ranks (e.g. a torch.distributed all-reduce); the updates then run
+    on this process's records with every exact per-epoch sum taken over all ranks, and means
+    over n_total records. fn None: back to single-process fits."""
+    global _reduce_cb
+    if fn is None:
+        _reduce_cb = None
+        lib().ora_set_reduce(None, 0)
+        return
+
+    def cb(ptr, n):
+        w = np.ctypeslib.as_array(ptr, shape=(n,))
+        fn(w)
+    _reduce_cb = REDUCE_FN(cb)
+    lib().ora_set_reduce(ctypes.cast(_reduce_cb, ctypes.c_void_p), int(n_total))
 
 
 def fit_noise(seed, agent, epochs, n):

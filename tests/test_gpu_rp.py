@@ -1,0 +1,173 @@
+"""The resumable, record-parallel learning-bidder update (ag_bidder_rp_*: one launch per epoch,
+the training state in HBM) against the persistent trainer (ag_bidder_update), which the other
+GPU tests pin to the oracle bit for bit. src/Bidder.py:204-325 (ValueLearningBidder), :473-615
+(DoublyRobustBidder)."""
+import numpy as np
+import pytest
+
+from test_gpu_parity import _dr_noise, _kat_learners, _learner_store
+
+pytestmark = pytest.mark.gpu
+
+SPECS = [("dm", "dm_update_kat.npz", 0), ("dr", "dr_update_kat.npz", 0), ("dm", "dm_update_kat.npz", 2),
+         ("dr", "dr_update_kat.npz", 1)]
+
+
+def _engine(bk, modes, state0):
+    from auctiongym_amd.engine import AuctionEngine
+    N = len(bk)
+    eng = AuctionEngine(N, min(2, N), 12, 5, 4, 0, 1.0)
+    eng.set_agent_params(np.ones(N, np.int32), bk, np.ones(N), np.full(N, 0.02))
+    eng.set_dr_state(state0, np.zeros(N, np.int32))
+    eng.set_bidder_modes(modes)
+    eng.set_fit_noise_seed(5)
+    return eng
+
+
+def _rp_run(engines, stores, mask, totals=None, bases=None, poll=64):
+    """The record-parallel loop over `engines` (ranks) in ONE process: after each epoch launch
+    the ranks' int64 totals are summed (what sharding.bidder_update_record_parallel's
+    all-reduce does across processes)."""
+    import torch
+    tots = [eng.bidder_rp_begin(st, agents=mask, records_total=totals,
+                                records_base=None if bases is None else bases[r])
+            for r, (eng, st) in enumerate(zip(engines, stores))]
+    sel = mask.astype(bool)
+    while True:
+        for _ in range(poll):
+            ks = [eng.bidder_rp_epoch(1) for eng in engines]
+            if len(engines) > 1:
+                s = sum(t[k & 1] for t, k in zip(tots, ks))
+                for t, k in zip(tots, ks):
+                    t[k & 1].copy_(s)
+        torch.cuda.synchronize()
+        fits = [eng.bidder_rp_poll()[0] for eng in engines]
+        for f in fits[1:]:
+            assert np.array_equal(f, fits[0])
+        if (fits[0][sel] < 0).all():
+            break
+    return [eng.bidder_rp_end() for eng in engines]
+
+
+def test_rp_update_equals_persistent_trainer(gpu):
+    """One process: the per-epoch-launch update (synthetic rsample draws) gives the persistent
+    trainer's epochs, status and models bit for bit, for ValueLearningBidder 'policy' and
+    DoublyRobustBidder agents trained together."""
+    bk, modes, state0, recs, _ = _kat_learners(SPECS)
+    N = len(SPECS)
+    eng = _engine(bk, modes, state0)
+    st = _learner_store(eng, recs)
+    ep, stat = eng.bidder_update(st, None, np.zeros(N, np.int64), 0)
+    state, init = eng.dr_state()
+    assert (stat == 0).all() and (ep[:, 2] > 0).all()
+    eng.set_dr_state(state0, np.zeros(N, np.int32))
+    (ep2, stat2), = _rp_run([eng], [st], np.ones(N, np.int32))
+    state2, init2 = eng.dr_state()
+    assert np.array_equal(ep2, ep) and np.array_equal(stat2, stat)
+    assert np.array_equal(state2, state) and np.array_equal(init2, init)
+    eng.close()
+
+
+@pytest.mark.parametrize("shards", [2, 3])
+def test_rp_sharded_records_equal_one_process(gpu, shards):
+    """`shards` ranks (engines on the one GPU, each holding a contiguous part of every agent's
+    records in log order) whose per-epoch totals are summed: every rank ends with the model the
+    persistent trainer fits on all the records in one process -- the record-parallel multi-GPU
+    update (sharding.bidder_update_record_parallel) without the processes. A rank may hold no
+    record of an agent."""
+    bk, modes, state0, recs, _ = _kat_learners(SPECS)
+    N = len(SPECS)
+    ref = _engine(bk, modes, state0)
+    ep, stat = ref.bidder_update(_learner_store(ref, recs), None, np.zeros(N, np.int64), 0)
+    state, init = ref.dr_state()
+    ref.close()
+    # split every agent's records (log order) into `shards` contiguous parts; the last rank gets
+    # none of agent 0's
+    engines, stores, counts = [], [], np.zeros((shards, N), np.int64)
+    for r in range(shards):
+        part = {f: [] for f in recs}
+        for a in range(N):
+            n = len(recs["agent"][a])
+            cut = [0] + [n * (j + 1) // shards for j in range(shards)]
+            if a == 0:
+                cut = [0] + [n * (j + 1) // (shards - 1) for j in range(shards - 1)] + [n]
+            lo, hi = cut[r], cut[r + 1]
+            for f in recs:
+                part[f].append(recs[f][a][lo:hi])
+            counts[r, a] = hi - lo
+        eng = _engine(bk, modes, state0)
+        engines.append(eng)
+        stores.append(_learner_store(eng, part))
+    assert counts[-1, 0] == 0
+    res = _rp_run(engines, stores, np.ones(N, np.int32), totals=counts.sum(0),
+                  bases=[counts[:r].sum(0) for r in range(shards)])
+    for r, eng in enumerate(engines):
+        s2, i2 = eng.dr_state()
+        assert np.array_equal(res[r][0], ep) and np.array_equal(res[r][1], stat), r
+        assert np.array_equal(s2, state) and np.array_equal(i2, init), r
+        eng.close()
+
+
+def test_rp_host_noise_windows_equal_one_shot(gpu, oracle):
+    """A policy fit fed its rsample noise window by window (ag_bidder_rp_noise: it waits at a
+    window's end with its state kept) equals the persistent trainer given all the epochs' noise
+    at once, and the oracle -- the drop-in update's single pass (no fit is re-run)."""
+    import torch
+    specs = [("dr", "dr_update_kat.npz", 0)]
+    bk, modes, state0, recs, data = _kat_learners(specs)
+    k = data[0]
+    n = len(k("est_ctr"))
+    E = 6000
+    z = _dr_noise(k("dr_rng_state"), n, E)
+    eng = _engine(bk, modes, state0)
+    st = _learner_store(eng, recs)
+    ep, stat = eng.bidder_update(st, torch.from_numpy(z.ravel()).to(eng.device), np.zeros(1, np.int64), E)
+    state, _ = eng.dr_state()
+    assert stat[0] == 0 and ep[0, 2] < E
+    r = oracle.dr_update(k("est_ctr"), k("value"), k("gamma"), k("propensity"), k("won"), k("util"),
+                         state0[0, :4], state0[0, 4:], False, z)
+    assert list(ep[0]) == list(r["epochs"]) and np.array_equal(state[0, 4:], r["pol"])
+    eng.set_dr_state(state0, np.zeros(1, np.int32))
+    eng.bidder_rp_begin(st, agents=np.ones(1, np.int32))
+    W, w0, waits = 333, 0, 0
+    eng.bidder_rp_noise(torch.from_numpy(z[:W].ravel()).to(eng.device), n, 0, W)
+    while True:
+        eng.bidder_rp_epoch(200)
+        fit, epoch, need = eng.bidder_rp_poll()
+        if fit[0] < 0:
+            break
+        if need[0] >= 0:
+            assert need[0] == w0 + W and fit[0] == 4
+            w0 = int(need[0])
+            waits += 1
+            eng.bidder_rp_noise(torch.from_numpy(z[w0:w0 + W].ravel()).to(eng.device), n, w0, W)
+    ep2, stat2 = eng.bidder_rp_end()
+    state2, _ = eng.dr_state()
+    assert waits >= ep[0, 2] // W - 1
+    assert np.array_equal(ep2, ep) and np.array_equal(stat2, stat) and np.array_equal(state2, state)
+    eng.close()
+
+
+def test_rp_fallback_and_errors(gpu):
+    """A ValueLearningBidder without a won record falls back (status 1, nothing trained, bids
+    stay Gaussian) as in ag_bidder_update; a PolicyLearningBidder is refused (float sums in a
+    fixed order cannot be split over ranks); ending while an agent still trains is an error."""
+    from auctiongym_amd import _lib
+    bk, modes, state0, recs, _ = _kat_learners([("dm", "dm_update_kat.npz", 1), ("dm", "dm_update_kat.npz", 2)])
+    recs["won"][0] = np.zeros_like(recs["won"][0])
+    eng = _engine(bk, modes, state0)
+    st = _learner_store(eng, recs)
+    (ep, stat), = _rp_run([eng], [st], np.ones(2, np.int32))
+    state, init = eng.dr_state()
+    assert stat[0] == 1 and list(ep[0]) == [0, 0, 0] and init[0] == _lib.LEARNER_UNINITIALISED
+    assert np.array_equal(state[0], state0[0]) and stat[1] == 0 and init[1] == _lib.LEARNER_POLICY
+    eng.bidder_rp_begin(st, agents=np.ones(2, np.int32))
+    eng.bidder_rp_epoch(3)
+    with pytest.raises(_lib.AgError, match="still training"):
+        eng.bidder_rp_end()
+    eng.close()
+    bk3, modes3, s3, recs3, _ = _kat_learners([("ips", "ips_update_kat.npz", 0)])
+    eng = _engine(bk3, modes3, s3)
+    with pytest.raises(NotImplementedError, match="PolicyLearningBidder"):
+        eng.bidder_rp_begin(_learner_store(eng, recs3), agents=np.ones(1, np.int32))
+    eng.close()

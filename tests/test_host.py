@@ -369,25 +369,20 @@ def test_compact_ts_noise_layout_host():
         assert np.array_equal(back, want)
 
 
-@pytest.mark.parametrize("budget", [512, 2048])
-def test_torch_noise_rewind_at_every_epoch_boundary(budget):
-    """Auction._TorchNoise: rewind(e) leaves torch's generator exactly e epochs of draws past
-    its start for every e up to and including the budget E (a fit that uses every epoch of
-    its budget stops at e == E, one past the last snapshot)."""
-    import torch
-    from auctiongym_amd.Auction import _TorchNoise
-    n = 5
-    torch.manual_seed(1234)
-    start = torch.get_rng_state()
-    s = _TorchNoise(n, "cpu")
-    s.upto(budget)
-    for e in (0, 1, 255, 256, 257, budget - 1, budget):
-        s.rewind(e)
-        got = torch.empty(n).normal_()
-        torch.set_rng_state(start)
-        for _ in range(e):
-            torch.empty(n).normal_()
-        assert torch.equal(torch.empty(n).normal_(), got), e
+@pytest.mark.parametrize("n", [1, 5, 15, 16, 17, 48, 1000, 6001])
+def test_torch_normal_epochs_restatement(n):
+    """ag_torch_normal_epochs (the drop-in learner update's rsample draws, host C): `epochs` x
+    torch.empty(n).normal_() -- the same float32 numbers as torch's own calls (its scalar kernel
+    below 16 elements, normal_fill_AVX2 from 16 on) and the generator blob left where torch's
+    is, so a fit fed window by window leaves torch's global generator as the reference's."""
+    from auctiongym_amd.engine import torch_normal_epochs
+    torch.manual_seed(11 + n)
+    torch.empty(3).normal_()  # a cached second Box-Muller value in the generator
+    state = torch.get_rng_state().numpy().copy()
+    ref = torch.stack([torch.empty(n).normal_() for _ in range(9)]).numpy()
+    got = np.concatenate([torch_normal_epochs(state, n, 4), torch_normal_epochs(state, n, 5)])
+    assert np.array_equal(got, ref)
+    assert np.array_equal(state, torch.get_rng_state().numpy())
 
 
 def test_per_call_agent_charge_metrics_and_update():

@@ -10,8 +10,16 @@ for s in ${STEPS:-smoke configs suite bench}; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     configs) step pytest_configs 600 python -u -m pytest tests/test_00_configs_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    rp) step pytest_rp 900 python -u -m pytest tests/test_gpu_rp.py tests/test_gpu_parity.py -m gpu -v --timeout 300 --timeout-method thread -k "rp_ or driver_fp or dropin_batch_small" ;;
     suite) step pytest_gpu 1200 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
     bench) step bench_driver 400 python bench.py --steps 20 --warmup 5 ;;
+    ab_stream)
+      step ab_c4p8 300 python tools/ab_pop.py configs_4:8 nostream stream1 &&
+      step ab_c1p8 300 python tools/ab_pop.py configs_1:8 generic &&
+      step ab_c4 300 python tools/ab_pop.py configs_4 stream1 nostream &&
+      step ab_c3 300 python tools/ab_pop.py configs_3 stream1 &&
+      step ab_c2 300 python tools/ab_pop.py configs_2 stream1 &&
+      step ab_c1 300 python tools/ab_pop.py configs_1 stream1 ;;
     stats) step kernel_stats 500 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
   esac
 done
