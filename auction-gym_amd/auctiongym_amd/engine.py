@@ -160,6 +160,39 @@ class AuctionEngine:
                                           _stream()), "ag_lrts_update")
         return (ep, tr) if trace else ep
 
+    def lrts_rp_begin(self, store, agents=None, samples_total=None):
+        """Start a resumable LR-TS update (ag_lrts_rp_begin); returns the totals tensor (int64
+        [2][N][144], device) whose slot launch_index & 1 a multi-rank caller all-reduces."""
+        mask = None if agents is None else np.ascontiguousarray(agents, np.int32).reshape(self.N)
+        tot = np.ascontiguousarray(samples_total, np.int64) if samples_total is not None else None
+        self._lrp_tot = torch.zeros((2, self.N, 144), dtype=torch.int64, device=self.device)
+        self._lrp_store = self._samples(store)
+        self._check(self.L.ag_lrts_rp_begin(self._h, ctypes.byref(self._lrp_store),
+                                            None if mask is None else mask.ctypes.data,
+                                            None if tot is None else tot.ctypes.data, _ptr(self._lrp_tot),
+                                            _stream()), "ag_lrts_rp_begin")
+        return self._lrp_tot
+
+    def lrts_rp_epoch(self, launches=1):
+        k = ctypes.c_int64(-1)
+        self._check(self.L.ag_lrts_rp_epoch(self._h, int(launches), ctypes.byref(k), _stream()), "ag_lrts_rp_epoch")
+        return k.value
+
+    def lrts_rp_poll(self):
+        """Agents still training (0: done)."""
+        n = ctypes.c_int32(0)
+        self._check(self.L.ag_lrts_rp_poll(self._h, ctypes.byref(n), _stream()), "ag_lrts_rp_poll")
+        return n.value
+
+    def lrts_rp_end(self):
+        """Epochs [N] of the trained agents (m, q, prev_m are on the device)."""
+        ep = np.zeros(self.N, np.int32)
+        try:
+            self._check(self.L.ag_lrts_rp_end(self._h, ep.ctypes.data, _stream()), "ag_lrts_rp_end")
+        finally:
+            self._lrp_store = None
+        return ep
+
     def set_item_search(self, exact):
         """exact=True: score every item in FP64 (the reference loop); False (default): f32
         screen + exact re-score of the near-best items -- identical results."""

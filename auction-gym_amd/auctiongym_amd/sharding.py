@@ -359,3 +359,42 @@ def bidder_update(eng, store, learners, group=None):
     if exact and record_parallel_pays(len(learners), _world(group)):
         return bidder_update_record_parallel(eng, store, learners, group)
     return bidder_update_agent_parallel(eng, store, learners, group)
+
+
+def lrts_update_record_parallel(eng, store, lrts_agents, group=None, poll=RP_POLL_LAUNCHES):
+    """Agent.update of the LR-TS allocators (src/BidderAllocation.py:29-65) record-parallel:
+    every rank keeps its own won samples, the fit runs one launch per epoch (ag_lrts_rp_epoch)
+    with each epoch's exact partials (and the Laplace terms) all-reduced -- every rank ends
+    with the posterior one process computes from all samples. Returns the epochs [N]."""
+    N = eng.N
+    world = _world(group)
+    mask = np.zeros(N, np.int32)
+    mask[list(lrts_agents)] = 1
+    n = int(store["count"][0].item())
+    key = store["key"][:n]
+    cnt = torch.bincount((key.to(torch.int64) >> 16) & 0xFFFF, minlength=N)[:N].to(torch.int64)
+    if world > 1:
+        dev = _gather_device(eng, group)
+        t = cnt.to(dev) if dev is not None else cnt.cpu()
+        _allreduce_sum(t, group)
+        cnt = t
+    tot = eng.lrts_rp_begin(store, agents=mask, samples_total=cnt.cpu().numpy())
+    while True:
+        if world > 1:
+            for _ in range(poll):
+                k = eng.lrts_rp_epoch(1)
+                _allreduce_sum(tot[k & 1], group)
+        else:
+            eng.lrts_rp_epoch(4 * poll)
+        if eng.lrts_rp_poll() == 0:
+            break
+    return eng.lrts_rp_end()
+
+
+def lrts_update(eng, store, lrts_agents, group=None):
+    """Agent.update of every LR-TS allocator across ranks: record-parallel where it pays (few
+    allocators for the ranks, record_parallel_pays), else agent-parallel."""
+    lrts_agents = [int(a) for a in lrts_agents]
+    if record_parallel_pays(len(lrts_agents), _world(group)):
+        return lrts_update_record_parallel(eng, store, lrts_agents, group)
+    return lrts_update_agent_parallel(eng, store, lrts_agents, group)

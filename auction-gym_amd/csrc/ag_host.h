@@ -46,6 +46,18 @@ struct ag_lrts_ws {
   size_t tab_cap = 0, part_cap = 0, bar_cap = 0;
   int coop_blocks = 0;        // co-resident workgroups of the training kernel
   int32_t *status = nullptr;  // [1] device-side error flags
+  // resumable / record-parallel training (ag_lrts_rp_*): one launch per epoch
+  struct {
+    bool active = false;
+    void *st = nullptr;          // LrSt [2][N], by launch parity
+    int64_t *acc = nullptr;      // combining-tree accumulator rows [lines][144]
+    unsigned *bar = nullptr;     // barrier lines [lines][32]
+    int32_t *tables = nullptr;   // blk_agent [G], blk_rank [G], agent_nblk [N], bar_off [N], mask [N]
+    size_t cap_g = 0, cap_lines = 0;
+    int G = 0;
+    int64_t k = 0;               // launches so far
+    int64_t *totals = nullptr;   // the caller's dev int64 [2][N][144]
+  } rp;
 };
 
 // Resumable / record-parallel training of the exact-sum learning bidders (ag_bidder_rp_*,

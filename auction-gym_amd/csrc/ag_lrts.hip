@@ -401,6 +401,184 @@ __global__ __launch_bounds__(kLrThreads) void k_lrts_train(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// 4. resumable / record-parallel training (ag_lrts_rp_*): the same fit as k_lrts_train, one
+//    launch per epoch, each agent's state (m, Adam moments, scheduler, loss history, phase) in
+//    HBM between launches. Launch k steps the state with the totals of launch k - 1 (this
+//    rank's workgroups summed up the agent's combining tree without waiting, then -- G ranks --
+//    the caller's int64 all-reduce), then adds the next epoch's exact partials at the new m:
+//    every rank holding a shard of an agent's won samples steps to the posterior one process
+//    computes from all of them (ag_dr.hip k_bidder_epoch has the same structure).
+// ---------------------------------------------------------------------------------------
+enum { kLrTrain = 0, kLrLaplace, kLrDone };
+struct LrSt {
+  int32_t phase, epoch, have_tot, bad;
+  double lr, best;
+  float m[kLrMaxKD], ea[kLrMaxKD], es[kLrMaxKD];
+  float hist[kHistory];
+};
+
+__global__ void k_lrts_rp_init(int N, int KD, const int32_t *__restrict__ mask, const float *__restrict__ gm,
+                               LrSt *__restrict__ st) {
+  const int a = blockIdx.x;
+  if (a >= N) return;
+  LrSt &f = st[a];
+  for (int c = threadIdx.x; c < kLrMaxKD; c += blockDim.x) {
+    f.m[c] = c < KD ? gm[(size_t)a * KD + c] : 0.0f;
+    f.ea[c] = f.es[c] = 0.0f;
+  }
+  for (int c = threadIdx.x; c < kHistory; c += blockDim.x) f.hist[c] = 0.0f;
+  if (threadIdx.x == 0) {
+    f.phase = mask[a] ? kLrTrain : kLrDone;
+    f.epoch = f.have_tot = f.bad = 0;
+    f.lr = 2e-3;
+    f.best = INFINITY;
+  }
+}
+
+template <int DO>
+__global__ __launch_bounds__(kLrThreads) void k_lrts_epoch(
+    int K, const int32_t *__restrict__ blk_agent, const int32_t *__restrict__ blk_rank,
+    const int32_t *__restrict__ agent_nblk, const int64_t *__restrict__ offsets, const uint32_t *__restrict__ key,
+    const float *__restrict__ xs, int64_t cap, float *__restrict__ gm, float *__restrict__ gq,
+    float *__restrict__ gpm, const double *__restrict__ adam_tab, int32_t *__restrict__ epochs_out,
+    const LrSt *__restrict__ st_in, LrSt *__restrict__ st_out, const int64_t *__restrict__ tot_in,
+    int64_t *__restrict__ tot_out, int64_t *__restrict__ acc_rows, unsigned *__restrict__ bars,
+    const int32_t *__restrict__ bar_off) {
+  const int a = blk_agent[blockIdx.x], rank = blk_rank[blockIdx.x], nblk = agent_nblk[a];
+  const int tid = threadIdx.x;
+  const int KD = K * DO;
+  const int PW = 2 * (KD + 1);
+  extern __shared__ int64_t s_acc[];  // [KD][kAccStride]
+  __shared__ uint64_t s_tab[256];
+  __shared__ LrSt st;
+  __shared__ float s_q[kLrMaxKD], s_pm[kLrMaxKD];
+  __shared__ int64_t s_hi[4][kLrMaxKD + 1], s_lo[4][kLrMaxKD + 1];
+  __shared__ float s_loss, s_negstep, s_bc2;
+  __shared__ int s_flag;
+  __shared__ int64_t s_part[2 * (kLrMaxKD + 1)];
+  for (int i = tid; i < 256; i += kLrThreads) s_tab[i] = ag_exp_tab[i];
+  for (int i = tid; i < (int)(sizeof(LrSt) / 4); i += kLrThreads)
+    reinterpret_cast<uint32_t *>(&st)[i] = reinterpret_cast<const uint32_t *>(st_in + a)[i];
+  float *q_g = gq + (size_t)a * KD, *pm_g = gpm + (size_t)a * KD, *m_g = gm + (size_t)a * KD;
+  for (int c = tid; c < KD; c += kLrThreads) {
+    s_q[c] = q_g[c];
+    s_pm[c] = pm_g[c];
+  }
+  for (int i = tid; i < KD * kAccStride; i += kLrThreads) s_acc[i] = 0;
+  __syncthreads();
+  const int64_t *T = tot_in + (size_t)a * kLrAccStride;
+  if (st.phase == kLrTrain && st.have_tot) {
+    // k_lrts_train's step C from the summed partials of epoch st.epoch
+    const int epoch = st.epoch;
+    if (tid == 0) {
+      double prior = 0.0;
+      for (int k = 0; k < K; ++k)
+        for (int d = 0; d < DO - 1; ++d) {
+          const double df = (double)s_pm[k * DO + d] - (double)st.m[k * DO + d];
+          prior += (double)s_q[k * DO + d] * (df * df);
+        }
+      s_loss = (float)(0.5 * prior + fx_read(T[2 * KD], T[2 * KD + 1], 1.0 / kLossScale));
+      s_negstep = (float)(-(st.lr / adam_tab[epoch]));
+      s_bc2 = (float)adam_tab[kLrEpochs + epoch];
+    }
+    __syncthreads();
+    if (tid < KD) {
+      const int c = tid;
+      const double gp = (c % DO) < DO - 1 ? -(double)s_q[c] * ((double)s_pm[c] - (double)st.m[c]) : 0.0;
+      const float g = (float)(fx_read(T[2 * c], T[2 * c + 1], 1.0 / kGradScale) + gp);
+      const float ea = st.ea[c] + 0.1f * (g - st.ea[c]);
+      const float es = st.es[c] * 0.999f + (0.001f * g) * g;
+      const float den = (float)__builtin_sqrt((double)es) / s_bc2 + 1e-8f;
+      st.ea[c] = ea;
+      st.es[c] = es;
+      st.m[c] = st.m[c] + s_negstep * (ea / den);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const float loss = s_loss;
+      st.hist[epoch % kHistory] = loss;
+      if ((double)loss < st.best * (1.0 - 1e-4)) {
+        st.best = (double)loss;
+        st.bad = 0;
+      } else {
+        st.bad += 1;
+      }
+      if (st.bad > 10) {
+        const double nl = st.lr * 0.5;
+        if (st.lr - nl > 1e-8) st.lr = nl;
+        st.bad = 0;
+      }
+      const bool stop = epoch > 1024 && fabs((double)st.hist[(epoch - 99) % kHistory] - (double)loss) < 1e-6;
+      st.epoch = epoch + 1;
+      if (stop || st.epoch >= kLrEpochs) st.phase = kLrLaplace;
+      st.have_tot = 0;
+    }
+    __syncthreads();
+  } else if (st.phase == kLrLaplace && st.have_tot) {
+    // the Laplace q from the summed terms, then prev_m = m (src/Models.py:43-48)
+    if (rank == 0) {
+      for (int c = tid; c < KD; c += kLrThreads) {
+        q_g[c] = s_q[c] + (float)fx_read(T[2 * c], T[2 * c + 1], 1.0 / kGradScale);
+        m_g[c] = st.m[c];
+        pm_g[c] = st.m[c];
+      }
+      if (tid == 0) epochs_out[a] = st.epoch;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      st.phase = kLrDone;
+      st.have_tot = 0;
+    }
+    __syncthreads();
+  }
+  const bool active = st.phase != kLrDone;
+  if (active) {
+    const int64_t s0 = offsets[a], n = offsets[a + 1] - s0;
+    const int64_t per = (n + nblk - 1) / nblk;
+    const int64_t c0 = (int64_t)rank * per < n ? (int64_t)rank * per : n;
+    const int64_t c1 = c0 + per < n ? c0 + per : n;
+    int64_t *acc = s_acc + tid;
+    int64_t lsum = 0;
+    const bool train = st.phase == kLrTrain;
+    for (int64_t i = c0 + tid; i < c1; i += kLrThreads) {
+      LrSample sm;
+      lr_load<DO>(key, xs, cap, s0 + i, sm);
+      if (train)
+        lsum += lr_epoch_sample<DO>(sm, st.m, acc, s_tab);
+      else
+        lr_laplace_sample<DO>(sm, st.m, acc, s_tab);
+    }
+    __syncthreads();
+    lr_block_partials(s_acc, KD, lsum >> 24, lsum & kLo24, s_hi, s_lo, s_part);
+    agcoop::agent_reduce_nowait(bars + (size_t)bar_off[a] * agcoop::kBarLineWords,
+                                acc_rows + (size_t)bar_off[a] * kLrAccStride, kLrAccStride, rank, nblk, s_part, PW,
+                                tot_out + (size_t)a * kLrAccStride, &s_flag);
+  }
+  if (rank == 0 && tid == 0) {
+    st.have_tot = active ? 1 : 0;
+    st_out[a] = st;
+  }
+}
+
+using EpochKernel = void (*)(int, const int32_t *, const int32_t *, const int32_t *, const int64_t *,
+                             const uint32_t *, const float *, int64_t, float *, float *, float *, const double *,
+                             int32_t *, const LrSt *, LrSt *, const int64_t *, int64_t *, int64_t *, unsigned *,
+                             const int32_t *);
+EpochKernel pick_epoch(int Do) {
+  switch (Do) {
+    case 1: return k_lrts_epoch<1>;
+    case 2: return k_lrts_epoch<2>;
+    case 3: return k_lrts_epoch<3>;
+    case 4: return k_lrts_epoch<4>;
+    case 5: return k_lrts_epoch<5>;
+    case 6: return k_lrts_epoch<6>;
+    case 7: return k_lrts_epoch<7>;
+    case 8: return k_lrts_epoch<8>;
+    default: return nullptr;
+  }
+}
+
 using TrainKernel = void (*)(int, const int32_t *, const int32_t *, const int32_t *, const int64_t *,
                              const int64_t *, const uint32_t *, const float *, int64_t, float *, float *,
                              float *, const double *, int32_t *, float *, int64_t *, unsigned *, const int32_t *);
@@ -444,6 +622,9 @@ void ag_lrts_release(ag_ctx *c) {
   (void)hipFree(w.epochs);
   (void)hipFree(w.tables);
   (void)hipFree(w.partials);
+  (void)hipFree(w.rp.st);
+  (void)hipFree(w.rp.acc);
+  (void)hipFree(w.rp.tables);
   w = ag_lrts_ws();
 }
 
@@ -471,24 +652,17 @@ int ag_lrts_collect(ag_ctx *c, int64_t B, const ag_batch_in *in, const ag_batch_
   return AG_OK;
 }
 
-int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *loss_trace, void *stream) {
-  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
-  if (int rc = check_store(c, s, "ag_lrts_update")) return rc;
-  if (!c->has_lrts) return AG_OK;
-  if (!c->lrts_loaded) return ag_set_error(AG_ERR_STATE, "ag_lrts_update: ag_load_lrts not called");
-  const int N = c->shape.num_agents, K = c->shape.num_items, Do = c->shape.obs_embedding_size + 1;
-  TrainKernel train = pick_train(Do);
-  if (!train || K * Do > kLrMaxKD)
-    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_lrts_update: needs OE+1 <= %d and K*(OE+1) <= %d (K=%d, OE+1=%d)",
-                        AG_LRTS_MAX_DO, kLrMaxKD, K, Do);
-  AgDeviceGuard g(c->device);
-  hipStream_t st = (hipStream_t)stream;
+// The won samples of a store bucketed by agent into the workspace (w.key, w.x with stride
+// w.cap; w.offsets [N + 1]): histogram -> exclusive scan -> scatter. Shared by ag_lrts_update
+// and ag_lrts_rp_begin. Synchronises for the count.
+static int bucket_samples(ag_ctx *c, const ag_lrts_samples *s, hipStream_t st, const char *who) {
+  const int N = c->shape.num_agents, Do = c->shape.obs_embedding_size + 1;
   uint64_t n = 0;
   AG_HIP(hipMemcpyAsync(&n, s->count, sizeof n, hipMemcpyDeviceToHost, st));
   AG_HIP(hipStreamSynchronize(st));
   if ((int64_t)n > s->capacity)
-    return ag_set_error(AG_ERR_INVALID, "ag_lrts_update: %llu won samples overflowed the store (capacity %lld)",
-                        (unsigned long long)n, (long long)s->capacity);
+    return ag_set_error(AG_ERR_INVALID, "%s: %llu won samples overflowed the store (capacity %lld)",
+                        who, (unsigned long long)n, (long long)s->capacity);
   ag_lrts_ws &w = c->lrts;
   if (!w.adam_tab) {
     double *tab = new double[2 * kLrEpochs];
@@ -503,7 +677,7 @@ int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *
     if (e == hipSuccess) e = hipMalloc(&w.epochs, sizeof(int32_t) * N);
     if (e != hipSuccess) {
       ag_lrts_release(c);
-      return ag_set_error(AG_ERR_HIP, "ag_lrts_update: workspace: %s", hipGetErrorString(e));
+      return ag_set_error(AG_ERR_HIP, "%s: workspace: %s", who, hipGetErrorString(e));
     }
   }
   if ((int64_t)n > w.cap) {
@@ -516,7 +690,7 @@ int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *
     if (e == hipSuccess) e = hipMalloc(&w.x, sizeof(float) * (size_t)Do * cap);
     if (e != hipSuccess) {
       w.cap = 0;
-      return ag_set_error(AG_ERR_HIP, "ag_lrts_update: sample workspace: %s", hipGetErrorString(e));
+      return ag_set_error(AG_ERR_HIP, "%s: sample workspace: %s", who, hipGetErrorString(e));
     }
     w.cap = cap;
   }
@@ -524,7 +698,7 @@ int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *
   AG_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * N, st));
   if (n > 0) {
     if ((size_t)N * 4 > 64 * 1024)
-      return ag_set_error(AG_ERR_UNSUPPORTED, "ag_lrts_update: N=%d agents > 16384", N);
+      return ag_set_error(AG_ERR_UNSUPPORTED, "%s: N=%d agents > 16384", who, N);
     hipLaunchKernelGGL(k_lrts_hist, dim3(grid_over((int64_t)n)), dim3(kLrThreads), (size_t)N * 4, st, s->key,
                        (int64_t)n, N, counts);
     AG_HIP(hipGetLastError());
@@ -536,6 +710,23 @@ int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *
                        (int64_t)n, s->capacity, Do, cursors, w.key, w.x, w.cap);
     AG_HIP(hipGetLastError());
   }
+  return AG_OK;
+}
+
+int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *loss_trace, void *stream) {
+  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
+  if (int rc = check_store(c, s, "ag_lrts_update")) return rc;
+  if (!c->has_lrts) return AG_OK;
+  if (!c->lrts_loaded) return ag_set_error(AG_ERR_STATE, "ag_lrts_update: ag_load_lrts not called");
+  const int N = c->shape.num_agents, K = c->shape.num_items, Do = c->shape.obs_embedding_size + 1;
+  TrainKernel train = pick_train(Do);
+  if (!train || K * Do > kLrMaxKD)
+    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_lrts_update: needs OE+1 <= %d and K*(OE+1) <= %d (K=%d, OE+1=%d)",
+                        AG_LRTS_MAX_DO, kLrMaxKD, K, Do);
+  AgDeviceGuard g(c->device);
+  hipStream_t st = (hipStream_t)stream;
+  if (int rc = bucket_samples(c, s, st, "ag_lrts_update")) return rc;
+  ag_lrts_ws &w = c->lrts;
   // agents' sample counts -> workgroups per agent (kLrCache samples per lane each)
   int64_t *h_off = new int64_t[N + 1];
   hipError_t e = hipMemcpyAsync(h_off, w.offsets, sizeof(int64_t) * (N + 1), hipMemcpyDeviceToHost, st);
@@ -650,6 +841,140 @@ int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *
   if (epochs) {
     AG_HIP(hipMemcpyAsync(epochs, w.epochs, sizeof(int32_t) * N, hipMemcpyDeviceToHost, st));
     AG_HIP(hipStreamSynchronize(st));
+  }
+  return AG_OK;
+}
+
+// ---- resumable / record-parallel LR-TS training (k_lrts_epoch) ----
+int ag_lrts_rp_begin(ag_ctx *c, const ag_lrts_samples *s, const int32_t *agents, const int64_t *samples_total,
+                     int64_t *totals, void *stream) {
+  if (c) c->image_dirty = true;
+  if (int rc = check_store(c, s, "ag_lrts_rp_begin")) return rc;
+  if (!totals) return ag_set_error(AG_ERR_INVALID, "ag_lrts_rp_begin: null totals");
+  if (!c->lrts_loaded) return ag_set_error(AG_ERR_STATE, "ag_lrts_rp_begin: ag_load_lrts not called");
+  const int N = c->shape.num_agents, K = c->shape.num_items, Do = c->shape.obs_embedding_size + 1;
+  EpochKernel kern = pick_epoch(Do);
+  if (!kern || K * Do > kLrMaxKD)
+    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_lrts_rp_begin: needs OE+1 <= %d and K*(OE+1) <= %d", AG_LRTS_MAX_DO,
+                        kLrMaxKD);
+  AgDeviceGuard g(c->device);
+  hipStream_t st = (hipStream_t)stream;
+  if (int rc = bucket_samples(c, s, st, "ag_lrts_rp_begin")) return rc;
+  ag_lrts_ws &w = c->lrts;
+  auto &rp = w.rp;
+  std::vector<int64_t> off((size_t)N + 1);
+  AG_HIP(hipMemcpyAsync(off.data(), w.offsets, sizeof(int64_t) * (N + 1), hipMemcpyDeviceToHost, st));
+  AG_HIP(hipStreamSynchronize(st));
+  // agents trained: LR-TS allocators in the mask with >= 2 won samples over all ranks (the
+  // reference skips the update below that, src/BidderAllocation.py:33-34)
+  constexpr int64_t kRpChunk = 2048;
+  std::vector<int32_t> mask(N, 0), nblk(N, 0), blk_agent, blk_rank, bar_off(N, 0);
+  int lines = 0;
+  for (int a = 0; a < N; ++a) {
+    const int64_t na = off[a + 1] - off[a], nt = samples_total ? samples_total[a] : na;
+    if (c->h_akind[a] != AG_ALLOCATOR_LRTS || (agents && !agents[a]) || nt < 2) continue;
+    mask[a] = 1;
+    nblk[a] = (int32_t)std::max<int64_t>(1, (na + kRpChunk - 1) / kRpChunk);
+    bar_off[a] = lines;
+    lines += std::max(1, agcoop::bar_lines(nblk[a]));
+    for (int r = 0; r < nblk[a]; ++r) {
+      blk_agent.push_back(a);
+      blk_rank.push_back(r);
+    }
+  }
+  const int G = (int)blk_agent.size();
+  if ((size_t)G > rp.cap_g || (size_t)lines > rp.cap_lines || !rp.st) {
+    (void)hipFree(rp.st);
+    (void)hipFree(rp.acc);
+    (void)hipFree(rp.tables);
+    rp.st = nullptr;
+    rp.acc = nullptr;
+    rp.tables = nullptr;
+    rp.cap_g = (size_t)G + 64;
+    rp.cap_lines = (size_t)lines + 16;
+    AG_HIP(hipMalloc(&rp.st, sizeof(LrSt) * 2 * (size_t)N));
+    AG_HIP(hipMalloc(&rp.acc, sizeof(int64_t) * kLrAccStride * rp.cap_lines + sizeof(unsigned) * 32 * rp.cap_lines));
+    AG_HIP(hipMalloc(&rp.tables, sizeof(int32_t) * (2 * rp.cap_g + 3 * (size_t)N)));
+  }
+  rp.bar = (unsigned *)(rp.acc + kLrAccStride * rp.cap_lines);
+  int32_t *d_bagent = rp.tables, *d_brank = d_bagent + rp.cap_g, *d_nblk = d_brank + rp.cap_g,
+          *d_baroff = d_nblk + N, *d_mask = d_baroff + N;
+  if (G) {
+    AG_HIP(hipMemcpyAsync(d_bagent, blk_agent.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
+    AG_HIP(hipMemcpyAsync(d_brank, blk_rank.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
+  }
+  AG_HIP(hipMemcpyAsync(d_nblk, nblk.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
+  AG_HIP(hipMemcpyAsync(d_baroff, bar_off.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
+  AG_HIP(hipMemcpyAsync(d_mask, mask.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
+  AG_HIP(hipMemsetAsync(rp.acc, 0, sizeof(int64_t) * kLrAccStride * rp.cap_lines + sizeof(unsigned) * 32 * rp.cap_lines,
+                        st));
+  AG_HIP(hipMemsetAsync(totals, 0, sizeof(int64_t) * 2 * kLrAccStride * (size_t)N, st));
+  AG_HIP(hipMemsetAsync(w.epochs, 0, sizeof(int32_t) * N, st));
+  hipLaunchKernelGGL(k_lrts_rp_init, dim3(N), dim3(64), 0, st, N, K * Do, d_mask, c->d_tsm, (LrSt *)rp.st);
+  AG_HIP(hipGetLastError());
+  const size_t lds = sizeof(int64_t) * (size_t)K * Do * kAccStride;
+  AG_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  rp.G = G;
+  rp.k = 0;
+  rp.totals = totals;
+  rp.active = true;
+  return AG_OK;
+}
+
+int ag_lrts_rp_epoch(ag_ctx *c, int32_t launches, int64_t *launch_index, void *stream) {
+  if (!c || !c->lrts.rp.active) return ag_set_error(AG_ERR_STATE, "ag_lrts_rp_epoch: no ag_lrts_rp_begin");
+  if (launches < 0) return ag_set_error(AG_ERR_INVALID, "ag_lrts_rp_epoch: launches < 0");
+  AgDeviceGuard g(c->device);
+  const int N = c->shape.num_agents, K = c->shape.num_items, Do = c->shape.obs_embedding_size + 1;
+  ag_lrts_ws &w = c->lrts;
+  auto &rp = w.rp;
+  EpochKernel kern = pick_epoch(Do);
+  const size_t lds = sizeof(int64_t) * (size_t)K * Do * kAccStride;
+  int32_t *d_bagent = rp.tables, *d_brank = d_bagent + rp.cap_g, *d_nblk = d_brank + rp.cap_g, *d_baroff = d_nblk + N;
+  LrSt *S = (LrSt *)rp.st;
+  hipStream_t st = (hipStream_t)stream;
+  for (int32_t l = 0; l < launches; ++l) {
+    const int64_t k = rp.k;
+    if (rp.G > 0)
+      hipLaunchKernelGGL(kern, dim3(rp.G), dim3(kLrThreads), lds, st, K, d_bagent, d_brank, d_nblk, w.offsets, w.key,
+                         w.x, w.cap, c->d_tsm, c->d_tsq, c->d_tsprev, w.adam_tab, w.epochs, S + (size_t)(k & 1) * N,
+                         S + (size_t)((k + 1) & 1) * N, rp.totals + (size_t)((k + 1) & 1) * kLrAccStride * N,
+                         rp.totals + (size_t)(k & 1) * kLrAccStride * N, rp.acc, rp.bar, d_baroff);
+    AG_HIP(hipGetLastError());
+    rp.k = k + 1;
+  }
+  if (launch_index) *launch_index = rp.k - 1;
+  return AG_OK;
+}
+
+int ag_lrts_rp_poll(ag_ctx *c, int32_t *training, void *stream) {
+  if (!c || !c->lrts.rp.active) return ag_set_error(AG_ERR_STATE, "ag_lrts_rp_poll: no ag_lrts_rp_begin");
+  AgDeviceGuard g(c->device);
+  const int N = c->shape.num_agents;
+  auto &rp = c->lrts.rp;
+  hipStream_t st = (hipStream_t)stream;
+  std::vector<int32_t> ph(N);
+  // the phase word of every agent's latest state (LrSt starts with it)
+  AG_HIP(hipMemcpy2DAsync(ph.data(), sizeof(int32_t), (LrSt *)rp.st + (size_t)(rp.k & 1) * N, sizeof(LrSt),
+                          sizeof(int32_t), N, hipMemcpyDeviceToHost, st));
+  AG_HIP(hipStreamSynchronize(st));
+  int32_t n = 0;
+  for (int a = 0; a < N; ++a) n += ph[a] != kLrDone;
+  if (training) *training = n;
+  return AG_OK;
+}
+
+int ag_lrts_rp_end(ag_ctx *c, int32_t *epochs, void *stream) {
+  if (!c || !c->lrts.rp.active) return ag_set_error(AG_ERR_STATE, "ag_lrts_rp_end: no ag_lrts_rp_begin");
+  c->image_dirty = true;
+  int32_t training = 0;
+  if (int rc = ag_lrts_rp_poll(c, &training, stream)) return rc;
+  c->lrts.rp.active = false;
+  if (training) return ag_set_error(AG_ERR_STATE, "ag_lrts_rp_end: %d agents still training", training);
+  if (epochs) {
+    AG_HIP(hipMemcpyAsync(epochs, c->lrts.epochs, sizeof(int32_t) * c->shape.num_agents, hipMemcpyDeviceToHost,
+                          (hipStream_t)stream));
+    AG_HIP(hipStreamSynchronize((hipStream_t)stream));
   }
   return AG_OK;
 }

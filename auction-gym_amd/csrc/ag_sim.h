@@ -130,6 +130,8 @@ struct LdsLayout {
   int32_t replicas;        // per-lane counter replicas (power of 2, <= 64)
   int32_t ncnt;            // counter slots held in LDS
   int32_t ts_do;           // LR-TS model width OE + 1 (general populations)
+  int32_t tsm_stride;      // floats between agents' LR-TS means (K * ts_do, made odd)
+  int32_t drs_stride;      // floats between agents' learner models (17: odd)
   int32_t pol;             // per-wave fitted-policy task slots [BT/64][64][32 B] (0: none)
 };
 
@@ -153,13 +155,24 @@ __host__ inline LdsLayout make_layout(int N, int K, int D, bool counters, bool g
   L.items_stride = (K * D) | 1;
   L.values_stride = K | 1;
   L.kpairs = (K + 1) / 2;
-  // [pair][dim 0..7][2 items] floats; + 4 floats so agents start on different 16-B slots
-  L.scr_stride = L.kpairs * 16 + 4;
+  // [pair][dim 0..7][2 items] floats; + 2 floats: the agent stride is 2 x odd dwords (mod 64),
+  // so the lanes of a wave reading one (pair, dim) of up to 32 different agents hit 32
+  // different 8-B bank pairs (+4 made it a multiple of 4: 16 pairs, 2-way conflicts beyond
+  // 16 agents)
+  L.scr_stride = L.kpairs * 16 + 2;
   L.scr_val_stride = L.kpairs * 2 + 2;
   L.ncnt = general ? kGeneralSlots : kOracleSlots;
   L.ts_do = general ? ts_do : 0;
+  // agent strides odd in dwords: lanes reading the same coefficient of different agents'
+  // LR-TS means / learner models hit different banks (K * 5 = 60 and 16 were multiples of 4:
+  // 4- and 16-way conflicts in large populations)
+  L.tsm_stride = general ? ((K * ts_do) | 1) : 0;
+  L.drs_stride = 17;
+  // counter replicas [slot][agent][R]: with R = 16 the 16 lanes of a 64-bit LDS atomic's lane
+  // group hit 16 distinct 8-B bank pairs whatever their agents; fewer replicas put lanes l and
+  // l + R on one pair. 16 kept up to 64 KB of replicas (32 agents x 10 slots = 40 KB)
   int R = AG_MAX_REPLICAS;
-  while (R > 1 && (int64_t)R * N * L.ncnt * 8 > 32768) R >>= 1;
+  while (R > 1 && (int64_t)R * N * L.ncnt * 8 > 65536) R >>= 1;
   L.replicas = R;
   int64_t b = 0;
   L.tab = 0;
@@ -183,9 +196,9 @@ __host__ inline LdsLayout make_layout(int N, int K, int D, bool counters, bool g
   L.gs = align16(b);
   b = L.gs + (general ? (int64_t)N * 8 : 0);
   L.tsm = align16(b);
-  b = L.tsm + (general ? (int64_t)N * K * ts_do * 4 : 0);
+  b = L.tsm + (general ? (int64_t)N * L.tsm_stride * 4 : 0);
   L.drs = align16(b);
-  b = L.drs + (general ? (int64_t)N * 16 * 4 : 0);
+  b = L.drs + (general ? (int64_t)N * L.drs_stride * 4 : 0);
   L.dri = align16(b);
   b = L.dri + (general ? (int64_t)N * 4 : 0);
   L.kag = align16(b);
@@ -385,7 +398,7 @@ struct Lds {
   const int32_t *akind, *bkind;
   const double *pg, *gs;
   const float *tsm;
-  int ts_do;
+  int ts_do, tsm_stride, drs_stride;
   const float *drs;
   const int32_t *dri;
   const int32_t *kag;  // general: each agent's own item count (src/main.py:61,66)
@@ -684,7 +697,7 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
       // item by first argmax of CTR * value (float32 CTR widened to double), the MAP CTR
       // of that item is the estimate
       const int Do = T.ts_do;
-      const float *m = T.tsm + (size_t)a * K * Do;
+      const float *m = T.tsm + (size_t)a * T.tsm_stride;
       // tiled noise: coefficient c of auction i at ((s*T + i/64)*K*Do + c)*64 + i%64; the
       // compact layout tiles the batch's LR-TS pairs only, pair j = ts_noise_index[s*B + i]
       // in place of s*T*64 + i (mixed populations: no noise stored or fetched for the
@@ -720,11 +733,11 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
       if constexpr (DEFER) {
         pol = true;
       } else {
-        policy_bid(T.drs + a * 16 + 4, est, v, in.policy_eps[(size_t)s * B + i], T.tab, g, prop);
+        policy_bid(T.drs + a * T.drs_stride + 4, est, v, in.policy_eps[(size_t)s * B + i], T.tab, g, prop);
         b = b * g;
       }
     } else if (bk == AG_BIDDER_VALUE_LEARNING && T.drs && T.dri[a] == AG_LEARNER_SEARCH) {
-      g = search_gamma(T.drs + a * 16, est, v, in.gamma_grid + (size_t)s * 128 * B + i, B, T.tab);
+      g = search_gamma(T.drs + a * T.drs_stride, est, v, in.gamma_grid + (size_t)s * 128 * B + i, B, T.tab);
       prop = 1.0;  // src/Bidder.py:196
       b = b * g;
     } else if (bk != AG_BIDDER_TRUTHFUL) {
@@ -828,9 +841,12 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
       s_gs[a] = prm.gs[a];
       s_kag[a] = prm.kag ? prm.kag[a] : K;
     }
-    for (int j = tid; j < N * K * L.ts_do; j += BT) s_tsm[j] = prm.tsm[j];
+    for (int j = tid; j < N * K * L.ts_do; j += BT) {
+      const int a = j / (K * L.ts_do);
+      s_tsm[a * L.tsm_stride + (j - a * K * L.ts_do)] = prm.tsm[j];
+    }
     if (prm.drs) {
-      for (int j = tid; j < N * 16; j += BT) s_drs[j] = prm.drs[j];
+      for (int j = tid; j < N * 16; j += BT) s_drs[(j >> 4) * L.drs_stride + (j & 15)] = prm.drs[j];
       for (int a = tid; a < N; a += BT) s_dri[a] = prm.dri[a];
     }
   }
@@ -870,7 +886,8 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
 
   const Lds T{s_tab, s_items, s_vals, s_scr, s_scr_val, s_amax, L.items_stride, L.values_stride,
               L.scr_stride, L.scr_val_stride, L.kpairs, s_akind, s_bkind, s_pg, s_gs, s_tsm, L.ts_do,
-              (GENERAL && prm.drs) ? s_drs : nullptr, s_dri, GENERAL ? s_kag : nullptr};
+              L.tsm_stride, L.drs_stride, (GENERAL && prm.drs) ? s_drs : nullptr, s_dri,
+              GENERAL ? s_kag : nullptr};
   const int rep = tid & (R - 1);
   const ag_batch_in in = prm.in;
   const ag_batch_out out = prm.out;
@@ -1202,7 +1219,7 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
         for (int s = 0; s < P; ++s) {
           if (polx[s] >= 0) {
             double g, pr;
-            policy_bid(T.drs + PV[s][0] * 16 + 4, estv[s], valv[s], ldg(in.policy_eps + (size_t)s * B + i), T.tab,
+            policy_bid(T.drs + PV[s][0] * T.drs_stride + 4, estv[s], valv[s], ldg(in.policy_eps + (size_t)s * B + i), T.tab,
                        g, pr);
             gmv[s] = g;
             prv[s] = pr;
@@ -1216,26 +1233,25 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
           for (int s = 0; s < P; ++s) {
             const int t = polx[s] - base;
             if (polx[s] >= 0 && t >= 0 && t < nact) {
-              double *e = reinterpret_cast<double *>(slots + t * 32);
-              e[0] = estv[s];
-              e[1] = valv[s];
-              int32_t *ei = reinterpret_cast<int32_t *>(slots + t * 32 + 16);
-              ei[0] = PV[s][0];
-              reinterpret_cast<float *>(ei)[1] = ldg(in.policy_eps + (size_t)s * B + i);
+              // the wave's task slots as structure of arrays (est, value [64] doubles, agent,
+              // eps [64] words): a wave's lanes touch consecutive words, no bank conflict
+              reinterpret_cast<double *>(slots)[t] = estv[s];
+              reinterpret_cast<double *>(slots)[64 + t] = valv[s];
+              reinterpret_cast<int32_t *>(slots + 1024)[t] = PV[s][0];
+              reinterpret_cast<float *>(slots + 1280)[t] = ldg(in.policy_eps + (size_t)s * B + i);
             }
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           if (wrk < ntask - base) {
-            double *e = reinterpret_cast<double *>(slots + wrk * 32);
-            const int32_t *ei = reinterpret_cast<const int32_t *>(slots + wrk * 32 + 16);
-            const int a = ei[0];
-            const float eps = reinterpret_cast<const float *>(ei)[1];
+            double *e0 = reinterpret_cast<double *>(slots) + wrk, *e1 = e0 + 64;
+            const int a = reinterpret_cast<const int32_t *>(slots + 1024)[wrk];
+            const float eps = reinterpret_cast<const float *>(slots + 1280)[wrk];
             double g, pr;
-            policy_bid(T.drs + a * 16 + 4, e[0], e[1], eps, T.tab, g, pr);
-            e[0] = g;
-            e[1] = pr;
+            policy_bid(T.drs + a * T.drs_stride + 4, *e0, *e1, eps, T.tab, g, pr);
+            *e0 = g;
+            *e1 = pr;
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
@@ -1244,10 +1260,10 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
           for (int s = 0; s < P; ++s) {
             const int t = polx[s] - base;
             if (polx[s] >= 0 && t >= 0 && t < nact) {
-              const double *e = reinterpret_cast<const double *>(slots + t * 32);
-              gmv[s] = e[0];
-              prv[s] = e[1];
-              bidv[s] = bidv[s] * e[0];  // bid *= gamma, as resolve_slot does
+              const double g = reinterpret_cast<const double *>(slots)[t];
+              gmv[s] = g;
+              prv[s] = reinterpret_cast<const double *>(slots)[64 + t];
+              bidv[s] = bidv[s] * g;  // bid *= gamma, as resolve_slot does
             }
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -490,6 +490,14 @@ def build_population(key, local, P=2):
     return eng, what, B0, ak, bk, st16, dims
 
 
+def _record_parallel(bk, world):
+    from auctiongym_amd.sharding import record_parallel_pays
+    learners = [a for a in range(len(bk)) if bk[a] >= 2]
+    if LEARNER_PARALLEL != "auto":
+        return LEARNER_PARALLEL == "record" and world > 1
+    return all(bk[a] in (2, 4) for a in learners) and record_parallel_pays(len(learners), world)
+
+
 def population_first_iteration(key, local, P=2, batch=None, world=1, rank=0):
     """A BASELINE config population (build_population) at its per-GPU shard size, its
     iteration 0 simulated once: Gaussian shading (uninitialised learners), Philox inputs for
@@ -510,12 +518,22 @@ def population_first_iteration(key, local, P=2, batch=None, world=1, rank=0):
     return eng, what, B, ak, bk, st16, dims, lo, inp, out, cnt
 
 
+LEARNER_PARALLEL = "auto"  # --learner-parallel: multi-GPU learning-bidder updates
+
+
 def population_update(eng, inp, out, B, lo, ak, bk, world):
     """The update of every learner on iteration 0's records (LR-TS allocators: won samples;
-    learning bidders: every record; synthetic on-device rsample noise), agent-parallel over
-    ranks at N > 1. Returns (ms [lrts, bidders] max over ranks, LR-TS epochs, bidder epochs,
-    LR-TS store, shading store, the LR-TS state before the update)."""
-    from auctiongym_amd.sharding import bidder_update_agent_parallel, lrts_update_agent_parallel
+    learning bidders: every record; synthetic on-device rsample noise); at N > 1 LR-TS
+    agent-parallel and the learning bidders agent- or record-parallel (sharding.bidder_update's
+    cost model, or --learner-parallel). Returns (ms [lrts, bidders] max over ranks, LR-TS
+    epochs, bidder epochs, LR-TS store, shading store, the LR-TS state before the update)."""
+    from auctiongym_amd.sharding import (bidder_update, bidder_update_agent_parallel,
+                                         bidder_update_record_parallel, lrts_update_agent_parallel)
+    from auctiongym_amd.sharding import lrts_update, lrts_update_record_parallel
+    bidder_fn = {"auto": bidder_update, "agent": bidder_update_agent_parallel,
+                 "record": bidder_update_record_parallel}[LEARNER_PARALLEL]
+    lrts_fn = {"auto": lrts_update, "agent": lrts_update_agent_parallel,
+               "record": lrts_update_record_parallel}[LEARNER_PARALLEL]
     N = eng.N
     P = eng.P
     m_pre = eng.lrts_state()
@@ -528,9 +546,9 @@ def population_update(eng, inp, out, B, lo, ak, bk, world):
     eng.shading_collect(inp, out, sst, first_auction=lo)
     # agent-parallel at N > 1 (each learner trained by one owner rank on every rank's
     # records of it; sharding.*_agent_parallel); identical to one process
-    lep = lrts_update_agent_parallel(eng, lst, [a for a in range(N) if ak[a] == 1])
+    lep = lrts_fn(eng, lst, [a for a in range(N) if ak[a] == 1])
     t1 = time.perf_counter()
-    ep, stat = bidder_update_agent_parallel(eng, sst, [a for a in range(N) if bk[a] >= 2])
+    ep, stat = bidder_fn(eng, sst, [a for a in range(N) if bk[a] >= 2])
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     ms = [(t1 - t0) * 1e3, (t2 - t1) * 1e3]
@@ -578,8 +596,11 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
             "bidder_epochs": [[int(x) for x in ep[a]] for a in learners[:4]],
             "what": "Agent.update of every learner: LR-TS allocators (ag_lrts_update) + learning bidders "
                     "(ag_bidder_update: win-rate fit, imitation, policy fit; synthetic on-device rsample noise)"
-                    + (f"; agent-parallel over {world} ranks: records routed to their agent's owner "
-                       "(all-to-all), owners train, models exchanged (all-gather)" if world > 1 else "")}
+                    + (f"; over {world} ranks: "
+                       + ("record-parallel (every rank its own records, each epoch's exact partials all-reduced)"
+                          if _record_parallel(bk, world) else
+                          "agent-parallel (records routed to their agent's owner, owners train, models exchanged)")
+                       if world > 1 else "")}
         tp = os.path.join(ROOT, "profiles", "trainer_pmc.json")
         if key == "configs_2" and os.path.exists(tp):  # PMC passes of this same update (tools/trainer_pmc.py)
             pm = json.load(open(tp))
@@ -680,11 +701,16 @@ def main():
                     help="skip the configs[2..4] lines (FP_DM_TS, FP_DR_TS, mixed population)")
     ap.add_argument("--populations", default=",".join(POPULATIONS),
                     help="comma-separated subset of the configs[2..4] lines to run")
+    ap.add_argument("--learner-parallel", choices=("auto", "agent", "record"), default="auto",
+                    help="N > 1: learning-bidder updates agent-parallel, record-parallel, or by the cost model "
+                         "(sharding.record_parallel_pays: record-parallel when the learners are few for the ranks)")
     ap.add_argument("--rehearse-on-one-gpu", action="store_true",
                     help="N > 1 ranks sharing the visible GPU(s) over gloo: exercises the multi-GPU code path "
                          "(shards, counter all-reduce, agent-parallel updates) where only one GPU is at hand; "
                          "its timings mean nothing")
     args = ap.parse_args()
+    global LEARNER_PARALLEL
+    LEARNER_PARALLEL = args.learner_parallel
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -512,6 +512,25 @@ int ag_bidder_update(ag_ctx *ctx, const ag_shading_samples *samples, const int32
                      const int64_t *noise_offsets, int32_t noise_epochs, int32_t *epochs, int32_t *status,
                      float *traces, void *stream);
 
+/* ---- Resumable, record-parallel LR-TS allocator update ----
+ * PyTorchLogisticRegressionAllocator.update (src/BidderAllocation.py:29-65: the epoch loop
+ * :45-55, the Laplace q :58-63) as ONE LAUNCH PER EPOCH, each agent's state (m, Adam
+ * moments, scheduler, loss history) in device memory between launches: G ranks holding shards
+ * of the won samples SUM the int64 words totals[launch_index & 1] ([N][144], dev) over the
+ * ranks after every ag_lrts_rp_epoch(launches = 1); every rank then ends with the posterior
+ * ag_lrts_update computes in one process from all the samples, bit for bit. samples_total:
+ * host int64 [N], each agent's won samples over all ranks (NULL: this process holds them
+ * all); agents with < 2 of them are not trained (the reference's :33-34). totals: caller-owned
+ * dev int64 [2][N][144]. The samples stay in the workspace until ag_lrts_rp_end. */
+int ag_lrts_rp_begin(ag_ctx *ctx, const ag_lrts_samples *samples, const int32_t *agents, const int64_t *samples_total,
+                     int64_t *totals, void *stream);
+int ag_lrts_rp_epoch(ag_ctx *ctx, int32_t launches, int64_t *launch_index, void *stream);
+/* Synchronises; training = agents still training (0: done). */
+int ag_lrts_rp_poll(ag_ctx *ctx, int32_t *training, void *stream);
+/* Every agent done: m, q, prev_m are where ag_simulate and ag_lrts_read read them; epochs host
+ * int32 [N] (may be NULL). AG_ERR_STATE while an agent trains. */
+int ag_lrts_rp_end(ag_ctx *ctx, int32_t *epochs, void *stream);
+
 /* ---- Resumable, record-parallel update of the exact-sum learning bidders ----
  * ValueLearningBidder and DoublyRobustBidder (src/Bidder.py:204-325, :473-615; replaces the
  * per-epoch loops of src/Bidder.py:239-260, :278-323, :517-538, :574-595) as ONE LAUNCH PER

@@ -98,3 +98,50 @@ def test_bench_multi_rank_rehearsal(gpu, tmp_path):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["configs_1"]["agent_update"]["epochs"] and d["configs_4"]["agent_update"]["bidder_epochs"]
+
+
+def _rp_worker(rank, world, port, B, out_path):
+    import sys
+    for p in (os.path.join(ROOT, "auction-gym_amd"), ROOT):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    from auctiongym_amd.sharding import bidder_update_agent_parallel, bidder_update_record_parallel
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    # FP_DR_TS (configs[3]): 3 DoublyRobust learners -- the A < G case record-parallel is for
+    eng, what, _, ak, bk, st16, dims, lo, inp, out, cnt = bench.population_first_iteration(
+        "configs_3", 0, batch=B // world, world=world, rank=rank)
+    sst = eng.new_shading_samples(B // world * dims["P"], learning=True)
+    eng.shading_collect(inp, out, sst, first_auction=lo)
+    learners = [a for a in range(dims["N"]) if bk[a] >= 2]
+    fn = bidder_update_agent_parallel if world == 1 else bidder_update_record_parallel
+    ep, stat = fn(eng, sst, learners)
+    state, init = eng.dr_state()
+    np.savez(out_path + f".{world}.{rank}.npz", state=state, init=init, ep=ep, stat=stat)
+    eng.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_record_parallel_bidder_update_equals_single_process(gpu, tmp_path):
+    """sharding.bidder_update_record_parallel with 2 ranks sharing cuda:0 over gloo: each rank
+    simulates its shard of FP_DR_TS's auctions and keeps its own records; the fits run one
+    launch per epoch with each epoch's exact partials all-reduced. Every rank ends with exactly
+    the models, epochs and status of one process that simulated and trained on all auctions
+    (the persistent trainer)."""
+    B = 1 << 14
+    out = str(tmp_path / "rp")
+    mp.spawn(_rp_worker, args=(1, 0, B, out), nprocs=1, join=True)
+    mp.spawn(_rp_worker, args=(2, _free_port(), B, out), nprocs=2, join=True)
+    ref = np.load(out + ".1.0.npz")
+    assert (ref["stat"] == 0).all() and ref["ep"][:, 2].max() > 0
+    for r in range(2):
+        got = np.load(out + f".2.{r}.npz")
+        for k in ("state", "init", "ep", "stat"):
+            assert np.array_equal(got[k], ref[k]), (r, k)

@@ -171,3 +171,67 @@ def test_rp_fallback_and_errors(gpu):
     with pytest.raises(NotImplementedError, match="PolicyLearningBidder"):
         eng.bidder_rp_begin(_learner_store(eng, recs3), agents=np.ones(1, np.int32))
     eng.close()
+
+
+# ---- LR-TS allocators (ag_lrts_rp_*: src/BidderAllocation.py:29-65) ----
+def _lrts_setup(shards):
+    """The SP_Truthful_TS KAT population (6 LR-TS agents, the reference's own update samples):
+    a reference engine, and `shards` engines each holding a slice of every agent's samples."""
+    from test_gpu_parity import _fill_store, _kat_population, _lrts_engine
+    kat, m0, q0, pm0 = _kat_population()
+    per = {a: (kat[f"a{a}_X"], kat[f"a{a}_A"], kat[f"a{a}_y"]) for a in range(6)}
+
+    def engine():
+        eng = _lrts_engine()
+        eng.load_lrts(m0, q0, pm0)
+        return eng
+    ref = engine()
+    ref_st = _fill_store(ref, per)
+    parts = []
+    for r in range(shards):
+        sub = {}
+        for a, (X, A, y) in per.items():
+            n = len(y)
+            lo, hi = n * r // shards, n * (r + 1) // shards
+            if shards > 1 and a == 1 and r == shards - 1:  # this rank holds none of agent 1's samples
+                lo = hi
+            if shards > 1 and a == 1 and r == shards - 2:
+                hi = n
+            sub[a] = (X[lo:hi], A[lo:hi], y[lo:hi])
+        eng = engine()
+        parts.append((eng, _fill_store(eng, sub, seed=r + 1)))
+    return ref, ref_st, parts
+
+
+@pytest.mark.parametrize("shards", [1, 2, 3])
+def test_lrts_rp_equals_persistent_trainer(gpu, shards):
+    """The per-epoch-launch LR-TS update over `shards` ranks (engines on the one GPU whose
+    per-epoch totals are summed, as the multi-GPU all-reduce does; shards = 1: one process)
+    ends, on every rank, with the persistent trainer's m, q, prev_m and epochs bit for bit."""
+    import torch
+    ref, ref_st, parts = _lrts_setup(shards)
+    ep = ref.lrts_update(ref_st)
+    want = ref.lrts_state()
+    ref.close()
+    counts = np.zeros(6, np.int64)
+    for eng, st in parts:
+        key = st["key"][:int(st["count"][0])].cpu().numpy().view(np.uint32)
+        counts += np.bincount(key >> 16, minlength=6)[:6]
+    tots = [eng.lrts_rp_begin(st, samples_total=counts) for eng, st in parts]
+    while True:
+        for _ in range(64):
+            ks = [eng.lrts_rp_epoch(1) for eng, _ in parts]
+            if shards > 1:
+                s = sum(t[k & 1] for t, k in zip(tots, ks))
+                for t, k in zip(tots, ks):
+                    t[k & 1].copy_(s)
+        torch.cuda.synchronize()
+        left = [eng.lrts_rp_poll() for eng, _ in parts]
+        assert len(set(left)) == 1
+        if left[0] == 0:
+            break
+    for eng, _ in parts:
+        assert np.array_equal(eng.lrts_rp_end(), ep)
+        for x, y in zip(eng.lrts_state(), want):
+            assert np.array_equal(x, y)
+        eng.close()
