@@ -128,10 +128,6 @@ class Auction:
         self._learner = self._lrts | self._shading_rec
         self._stores = {}                       # device record stores, by learner family
         self._bounds = {"lrts": 0, "shading": 0}  # upper bounds of the records they hold
-        self._trained = False       # the stores' records were trained on
-        self._pending_state = {}    # trained state not yet applied to the host mirrors
-        self._claimed = set()       # learners whose update() consumed the training
-        self._cleared = set()       # ... and that cleared their logs since
 
     def _load_lrts(self):
         K, Do = self._engine.K, self.obs_embedding_size + 1
@@ -360,11 +356,13 @@ class Auction:
         self._logged_rounds += B
 
     # ------------------------------------------------------------------ Agent.update
-    # Learners (LR-TS allocators, EmpiricalShadedBidder) update from their logs of the
-    # iteration. Their records are collected on the device after every batch; the first
-    # learner's update() trains every learner at once (agents' updates are independent:
-    # same results as the reference's per-agent loop, src/main.py:127-152); the stores are
-    # emptied once every learner has called update() and clear_logs().
+    # Learners (LR-TS allocators, EmpiricalShadedBidder and the learning bidders) update from
+    # their current logs. Their records are collected on the device after every batch into
+    # append-only stores (one per learner family); an agent's clear_logs() removes its records
+    # (keeping the last M with memory = M), so the stores always hold every learner's current
+    # logs and each update() trains that agent alone on them, at its own call -- as the
+    # reference does (src/Agent.py:79-94, src/main.py:127-152): rounds may be simulated between
+    # updates, and an update may be repeated.
     _CAP_KEY = {"lrts": "key", "shading": "agent"}
 
     def _grow(self, name, need, make):
@@ -385,10 +383,6 @@ class Auction:
         return st
 
     def _collect(self, inp, out, B, first_auction):
-        if self._trained:
-            raise NotImplementedError(
-                "rounds were simulated after an update before every learning agent called "
-                "update() and clear_logs() (log memory across updates is not supported)")
         eng = self._engine
         if self._lrts.any():
             need = self._bounds["lrts"] + B
@@ -402,52 +396,32 @@ class Auction:
             eng.shading_collect(inp, out, st, first_auction=first_auction)
             self._bounds["shading"] = need
 
-    def _train_all(self):
-        """One launch per learner family; each agent's new host-side state is applied when
-        that agent's own update() runs (the device state is only read by the next batch,
-        which the reference also runs after every update)."""
-        eng = self._engine
-        self._pending_state = {}
-        if self._lrts.any() and "lrts" in self._stores:
-            ep = eng.lrts_update(self._stores["lrts"])
-            m, q, pm = eng.lrts_state()
-            for i in np.nonzero(self._lrts)[0]:
-                self._pending_state.setdefault(int(i), {})["lrts"] = (m[i].copy(), q[i].copy(),
-                                                                      pm[i].copy(), int(ep[i]))
-        if self._empirical.any():
-            st = self._stores.get("shading") or eng.new_shading_samples(1, learning=bool(self._learning.any()))
-            pg = eng.empirical_update(st)
-            for i in np.nonzero(self._empirical)[0]:
-                self._pending_state.setdefault(int(i), {})["prev_gamma"] = float(pg[i])
-
-    def _apply_state(self, index):
-        ag = self.agents[index]
-        state = self._pending_state.pop(index, {})
-        if "lrts" in state:
-            m, q, pm, ep = state["lrts"]
-            rm = ag.allocator.response_model
-            k = self._num_items[index]  # the agent's own rows
-            rm.m, rm.q, rm.prev_iter_m = (torch.from_numpy(np.ascontiguousarray(x[:k])) for x in (m, q, pm))
-            ag.allocator.epochs = ep
-        if "prev_gamma" in state:
-            ag.bidder.prev_gamma = state["prev_gamma"]
-
     def _update_agent(self, index, iteration):
-        """Agent.update (src/Agent.py:79-94) of agent `index` on the GPU: its allocator's update
-        (LR-TS: batched over all LR-TS agents at the first update, they draw nothing), then its
-        bidder's."""
+        """Agent.update (src/Agent.py:79-94) of agent `index` on the GPU, on its current logs: its
+        allocator's update (LR-TS: the resumable update of this agent alone, ag_lrts_rp_*), then
+        its bidder's (EmpiricalShadedBidder: ag_empirical_update_agents; the learning bidders:
+        learner_update)."""
         if not self._learner[index]:
             return
         self._flush()
-        if index in self._claimed:
-            raise NotImplementedError("a second update() of the same logs")
-        if not self._trained:
-            self._train_all()
-            self._trained = True
-        self._apply_state(index)
+        eng = self._engine
+        ag = self.agents[index]
+        mask = np.zeros(len(self.agents), np.int32)
+        mask[index] = 1
+        if self._lrts[index]:
+            st = self._stores.get("lrts") or eng.new_lrts_samples(1)
+            ep = _lrts_train(eng, st, mask)
+            m, q, pm = eng.lrts_state()
+            rm = ag.allocator.response_model
+            k = self._num_items[index]  # the agent's own rows
+            rm.m, rm.q, rm.prev_iter_m = (torch.from_numpy(np.ascontiguousarray(x[index, :k])) for x in (m, q, pm))
+            ag.allocator.epochs = int(ep[index])
+        if self._empirical[index]:
+            st = self._stores.get("shading") or eng.new_shading_samples(1, learning=bool(self._learning.any()))
+            pg = eng.empirical_update(st, agents=mask)
+            ag.bidder.prev_gamma = float(pg[index])
         if self._learning[index]:
             self._update_learner(index)
-        self._claimed.add(index)
 
     def _update_learner(self, index):
         """One learning bidder's update (ag_bidder_update with a one-agent mask)."""
@@ -456,60 +430,60 @@ class Auction:
         learner_update(eng, st, index, self.agents[index].bidder, self.agents[index].name)
 
     def _cleared_logs(self, index):
+        """Agent.clear_logs (src/Agent.py:124-129) of agent `index`: its records leave the device
+        stores; with memory = M the last M go back (the records its next update trains on and its
+        metrics read, src/Agent.py:81-94)."""
         if not self._learner[index]:
             return
-        if index in self._claimed:
-            self._cleared.add(index)
-        if self._trained and len(self._cleared) == int(self._learner.sum()):
-            for st in self._stores.values():
-                st["count"].zero_()
-            self._bounds = {"lrts": 0, "shading": 0}
-            self._restore_kept()
-            self._trained = False
-            self._claimed, self._cleared = set(), set()
+        self._flush()
+        for name, st in self._stores.items():
+            n = min(int(st["count"][0].item()), self._bounds[name])
+            agent = (((st["key"][:n].to(torch.int64) >> 16) & 0xFFFF) if name == "lrts"
+                     else st["agent"][:n].to(torch.int64))
+            keep = agent != index
+            m = int(keep.sum().item())
+            if m < n:
+                for k, v in st.items():
+                    if k != "count":
+                        v[..., :m] = v[..., :n][..., keep]
+            st["count"][0] = m
+            self._bounds[name] = m
+        cols = self.agents[index]._kept
+        if cols is not None:
+            self._append_kept(index, cols)
 
-    def _restore_kept(self):
-        """Agent(memory=M): the records the learners kept (src/Agent.py:128) go back into the
-        emptied device stores, so the next update trains on them and the new rounds' records
-        -- as the reference's update reads the kept logs (src/Agent.py:81-94). LR-TS won
-        samples as ag_lrts_collect writes them; shading records with their log order."""
+    def _append_kept(self, i, cols):
+        """Agent(memory=M): the M records agent i kept (src/Agent.py:128) back into the device
+        stores -- LR-TS won samples as ag_lrts_collect writes them, shading records with their
+        log order -- so its next update trains on them and the new rounds' records."""
         eng, d = self._engine, self._engine.device
-        lr, sh = [], []
-        for i, a in enumerate(self.agents):
-            cols = a._kept if self._learner[i] else None
-            if cols is None:
-                continue
-            if self._lrts[i]:
-                w = cols["won"].astype(bool)
-                if w.any():
-                    lr.append((i, {k: v[w] for k, v in cols.items()}))
-            if self._shading_rec[i]:
-                sh.append((i, cols))
-        if lr:
-            key = np.concatenate([(np.int64(i) << 16) | (c["item"] << 1) | c["outcome"].astype(np.int64)
-                                  for i, c in lr]).astype(np.uint32).view(np.int32)
-            x = np.concatenate([c["context"] for _, c in lr]).astype(np.float32).T
-            n = len(key)
-            st = self._grow("lrts", n, eng.new_lrts_samples)
-            st["key"][:n] = torch.from_numpy(key).to(d)
-            st["x"][:, :n] = torch.from_numpy(np.ascontiguousarray(x)).to(d)
-            st["count"][0] = n
-            self._bounds["lrts"] = n
-        if sh:
-            cols = {k: np.concatenate([c[k] for _, c in sh]) for k in sh[0][1]}
-            n = len(cols["item"])
+        if self._lrts[i]:
+            w = cols["won"].astype(bool)
+            if w.any():
+                key = ((np.int64(i) << 16) | (cols["item"][w] << 1) | cols["outcome"][w].astype(np.int64))
+                key = key.astype(np.uint32).view(np.int32)
+                x = np.ascontiguousarray(cols["context"][w].astype(np.float32).T)
+                n0, k = self._bounds["lrts"], len(key)
+                st = self._grow("lrts", n0 + k, eng.new_lrts_samples)
+                st["key"][n0:n0 + k] = torch.from_numpy(key).to(d)
+                st["x"][:, n0:n0 + k] = torch.from_numpy(x).to(d)
+                st["count"][0] = n0 + k
+                self._bounds["lrts"] = n0 + k
+        if self._shading_rec[i]:
+            k = len(cols["item"])
             won = cols["won"].astype(bool)
             util = np.where(won, cols["value"] * cols["outcome"].astype(np.float64) - cols["price"], 0.0)
             learning = bool(self._learning.any())
-            st = self._grow("shading", n, lambda cap: eng.new_shading_samples(cap, learning=learning))
-            fields = {"agent": np.concatenate([np.full(len(c["item"]), i, np.int32) for i, c in sh]),
-                      "gamma": cols["gamma"], "utility": util, "ctr": cols["est_ctr"], "value": cols["value"],
-                      "propensity": cols["propensity"], "won": won.astype(np.uint8), "order": cols["order"]}
-            for k, v in fields.items():
-                if k in st:
-                    st[k][:n] = torch.from_numpy(np.ascontiguousarray(v)).to(device=d, dtype=st[k].dtype)
-            st["count"][0] = n
-            self._bounds["shading"] = n
+            n0 = self._bounds["shading"]
+            st = self._grow("shading", n0 + k, lambda cap: eng.new_shading_samples(cap, learning=learning))
+            fields = {"agent": np.full(k, i, np.int32), "gamma": cols["gamma"], "utility": util,
+                      "ctr": cols["est_ctr"], "value": cols["value"], "propensity": cols["propensity"],
+                      "won": won.astype(np.uint8), "order": cols["order"]}
+            for f, v in fields.items():
+                if f in st:
+                    st[f][n0:n0 + k] = torch.from_numpy(np.ascontiguousarray(v)).to(device=d, dtype=st[f].dtype)
+            st["count"][0] = n0 + k
+            self._bounds["shading"] = n0 + k
 
     def _agent_columns(self, index, start_round):
         """Agent(memory=M): columns of agent `index`'s records since start_round (host)."""
@@ -545,6 +519,18 @@ class Auction:
     def clear_revenue(self):
         self._flush()
         self._revenue_fx = 0
+
+
+def _lrts_train(eng, store, mask, launches=256):
+    """PyTorchLogisticRegressionAllocator.update of the LR-TS agents of `mask` alone on the
+    store's samples (the resumable per-epoch update, ag_lrts_rp_*, one process): the other
+    agents' posteriors stay as they are. Returns epochs [N]."""
+    eng.lrts_rp_begin(store, agents=mask)
+    while True:
+        eng.lrts_rp_epoch(launches)
+        if eng.lrts_rp_poll() == 0:
+            break
+    return eng.lrts_rp_end()
 
 
 NOISE_WINDOW_FLOATS = 1 << 26  # host-drawn rsample noise per window (256 MB)

@@ -48,7 +48,7 @@ EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params
            "ag_last_error",
            "ag_abi_version", "ag_ts_noise_index", "ag_generate_ts_noise_compact", "ag_torch_normal_epochs",
            "ag_bidder_rp_begin", "ag_bidder_rp_epoch", "ag_bidder_rp_noise", "ag_bidder_rp_poll", "ag_bidder_rp_end",
-           "ag_lrts_rp_begin", "ag_lrts_rp_epoch", "ag_lrts_rp_poll", "ag_lrts_rp_end")
+           "ag_lrts_rp_begin", "ag_lrts_rp_epoch", "ag_lrts_rp_poll", "ag_lrts_rp_end", "ag_empirical_update_agents")
 ABI_VERSION = 16
 LEARNER_UNINITIALISED, LEARNER_POLICY, LEARNER_SEARCH = 0, 1, 2
 VL_SEARCH, VL_POLICY = 0, 1
@@ -142,6 +142,7 @@ def load(path=None):
         "ag_shading_collect": (ctypes.c_int, [vp, i64, i64, ctypes.POINTER(AgBatchIn),
                                               ctypes.POINTER(AgBatchOut), ctypes.POINTER(AgShadingSamples), vp]),
         "ag_empirical_update": (ctypes.c_int, [vp, ctypes.POINTER(AgShadingSamples), vp, vp]),
+        "ag_empirical_update_agents": (ctypes.c_int, [vp, ctypes.POINTER(AgShadingSamples), vp, vp, vp]),
         "ag_set_dr_state": (ctypes.c_int, [vp, vp, vp]),
         "ag_get_dr_state": (ctypes.c_int, [vp, vp, vp]),
         "ag_shading_counts": (ctypes.c_int, [vp, ctypes.POINTER(AgShadingSamples), vp, vp]),

@@ -580,13 +580,15 @@ class AuctionEngine:
         self._check(self.L.ag_shading_collect(self._h, int(first_auction), B, ctypes.byref(bi), ctypes.byref(bo),
                                               ctypes.byref(st), _stream()), "ag_shading_collect")
 
-    def empirical_update(self, store):
-        """EmpiricalShadedBidder.update of every such agent (ag_empirical_update); returns the
-        prev_gamma of all agents [N] after the update."""
+    def empirical_update(self, store, agents=None):
+        """EmpiricalShadedBidder.update of every such agent, or of the agents of the [N] mask
+        `agents` (ag_empirical_update_agents); returns the prev_gamma of all agents [N] after it."""
         pg = np.zeros(self.N, np.float64)
         st = self._shading(store)
-        self._check(self.L.ag_empirical_update(self._h, ctypes.byref(st), pg.ctypes.data, _stream()),
-                    "ag_empirical_update")
+        mask = None if agents is None else np.ascontiguousarray(agents, np.int32).reshape(self.N)
+        self._check(self.L.ag_empirical_update_agents(self._h, ctypes.byref(st),
+                                                      None if mask is None else mask.ctypes.data, pg.ctypes.data,
+                                                      _stream()), "ag_empirical_update")
         return pg
 
     # ---------------------------------------------------------------- counters

@@ -101,9 +101,9 @@ __device__ __forceinline__ int find_bucket(const double *edge, int M, double g) 
 __global__ __launch_bounds__(kShThreads) void k_empirical_update(
     int N, const int32_t *__restrict__ bkind, const int32_t *__restrict__ s_agent,
     const double *__restrict__ s_gamma, const double *__restrict__ s_util, int64_t n,
-    double *__restrict__ prev_gamma, int32_t *__restrict__ status) {
+    double *__restrict__ prev_gamma, int32_t *__restrict__ status, const int32_t *__restrict__ mask) {
   const int a = blockIdx.x, tid = threadIdx.x;
-  if (bkind[a] != AG_BIDDER_EMPIRICAL_SHADED) {
+  if (bkind[a] != AG_BIDDER_EMPIRICAL_SHADED || (mask && !mask[a])) {
     if (tid == 0) status[a] = 0;
     return;
   }
@@ -259,6 +259,11 @@ int ag_shading_collect(ag_ctx *c, int64_t first, int64_t B, const ag_batch_in *i
 }
 
 int ag_empirical_update(ag_ctx *c, const ag_shading_samples *s, double *prev_gamma, void *stream) {
+  return ag_empirical_update_agents(c, s, nullptr, prev_gamma, stream);
+}
+
+int ag_empirical_update_agents(ag_ctx *c, const ag_shading_samples *s, const int32_t *agents, double *prev_gamma,
+                               void *stream) {
   if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   if (int rc = check_store(c, s, "ag_empirical_update")) return rc;
   const int N = c->shape.num_agents;
@@ -270,9 +275,14 @@ int ag_empirical_update(ag_ctx *c, const ag_shading_samples *s, double *prev_gam
   if ((int64_t)n > s->capacity)
     return ag_set_error(AG_ERR_INVALID, "ag_empirical_update: %llu samples overflowed the store (capacity %lld)",
                         (unsigned long long)n, (long long)s->capacity);
-  if (!c->d_status) AG_HIP(hipMalloc(&c->d_status, sizeof(int32_t) * N));
+  if (!c->d_status) AG_HIP(hipMalloc(&c->d_status, sizeof(int32_t) * 2 * N));  // status [N], mask [N]
+  int32_t *d_mask = nullptr;
+  if (agents) {
+    d_mask = c->d_status + N;
+    AG_HIP(hipMemcpyAsync(d_mask, agents, sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
+  }
   hipLaunchKernelGGL(k_empirical_update, dim3(N), dim3(kShThreads), 0, st, N, c->d_bkind, s->agent, s->gamma,
-                     s->utility, (int64_t)n, c->d_pg, c->d_status);
+                     s->utility, (int64_t)n, c->d_pg, c->d_status, d_mask);
   AG_HIP(hipGetLastError());
   int32_t *status = new int32_t[N];
   hipError_t e = hipMemcpyAsync(status, c->d_status, sizeof(int32_t) * N, hipMemcpyDeviceToHost, st);

@@ -459,6 +459,11 @@ int ag_shading_collect(ag_ctx *ctx, int64_t first_auction, int64_t B, const ag_b
  * with two samples). Arithmetic: oracle/ag_oracle.c ora_empirical_update. */
 int ag_empirical_update(ag_ctx *ctx, const ag_shading_samples *samples, double *prev_gamma,
                         void *stream);
+/* The same for the agents of host int32 [N] mask `agents` only (NULL: every one): the
+ * reference's per-agent Agent.update (src/main.py:127-128) -- the other agents' prev_gamma and
+ * errors are untouched. */
+int ag_empirical_update_agents(ag_ctx *ctx, const ag_shading_samples *samples, const int32_t *agents,
+                               double *prev_gamma, void *stream);
 
 /* ---- Learning bidders: ValueLearningBidder, PolicyLearningBidder, DoublyRobustBidder ----
  * (src/Bidder.py:156-623). Per-agent model state, host float32 [N][16]:

@@ -965,6 +965,57 @@ def memory_driver_kat(out_name="memory_driver_kat"):
     np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
 
 
+INTERLEAVE_STEPS = (("sim", 600), ("upd", 0), ("sim", 300), ("upd", 0), ("upd", 1), ("clr", 1), ("clr", 0),
+                    ("sim", 200), ("upd", 0), ("upd", 1), ("upd", 2), ("upd", 3), ("upd", 4), ("upd", 5),
+                    ("sim", 150))
+
+
+def interleave_kat(out_name="interleave_kat"):
+    """Notebook-style use of the per-agent surface (src/Agent.py:79-94, :124-129): rounds
+    simulated between one agent's update() and the others', a second update() of an agent's
+    grown logs, clear_logs() of some agents only -- the sequence INTERLEAVE_STEPS on two
+    populations (EmpiricalShadedBidders, FirstPrice: exact; SP_Truthful_TS LR-TS allocators:
+    float32 torch fits). Recorded after every step: revenue, utilities, every agent's log count
+    and learner state (prev_gamma / LR-TS m, q)."""
+    import torch
+    import main as M
+    out = {"steps": np.array(json.dumps(INTERLEAVE_STEPS))}
+    for name in ("empirical", "lrts"):
+        if name == "empirical":
+            cfg = oracle_truthful_cfg(6, 12, 2, "FirstPrice", seed=5)
+            cfg["agents"][0]["bidder"] = {"type": "EmpiricalShadedBidder",
+                                          "kwargs": {"gamma_sigma": 0.05, "init_gamma": 0.9}}
+        else:
+            cfg = load_cfg("SP_Truthful_TS.json", random_seed=5)
+        cfg["num_runs"], cfg["num_iter"] = 1, 1
+        out[f"{name}_cfg"] = np.array(json.dumps(cfg))
+        path = write_cfg(cfg)
+        (rng, config, agent_configs, a2i, a2v, _, max_slots, E, var, OE) = M.parse_config(path)
+        os.unlink(path)
+        torch.manual_seed(0)
+        agents = M.instantiate_agents(rng, agent_configs, a2v, a2i)
+        auction, _, _, _ = M.instantiate_auction(rng, config, a2i, a2v, agents, max_slots, E, var, OE)
+        for j, (op, arg) in enumerate(INTERLEAVE_STEPS):
+            if op == "sim":
+                for _ in range(arg):
+                    auction.simulate_opportunity()
+            elif op == "upd":
+                agents[arg].update(iteration=j)
+            else:
+                agents[arg].clear_logs()
+            k = f"{name}_s{j}"
+            out[k + "_revenue"] = np.array(auction.revenue)
+            out[k + "_net"] = np.array([a.net_utility for a in agents])
+            out[k + "_nlogs"] = np.array([len(a.logs) for a in agents])
+            if name == "empirical":
+                out[k + "_pg"] = np.array([float(a.bidder.prev_gamma) for a in agents])
+            else:
+                out[k + "_m"] = np.stack([a.allocator.response_model.m.detach().numpy().copy() for a in agents])
+                out[k + "_q"] = np.stack([a.allocator.response_model.q.detach().numpy().copy() for a in agents])
+        print("interleave", name, float(out[k + "_revenue"]), flush=True)
+    np.savez_compressed(os.path.join(OUT, out_name + ".npz"), **out)
+
+
 CSV_CASES = {
     # name: config overrides on oracle_truthful_cfg(...) (both populations run end to end on
     # the GPU path, so main.py's CSV files can be compared cell by cell)
@@ -1049,10 +1100,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also run SP_Oracle as shipped (3x20x10k rounds, ~1 min)")
     ap.add_argument("--which", choices=["dm", "ips", "dr", "dmo", "search"], help="with --only learners/drivers: one config")
-    ap.add_argument("--only", choices=["empirical", "csv", "dr", "learners", "drivers", "memory", "later", "mixedts", "ragged"],
+    ap.add_argument("--only", choices=["empirical", "csv", "dr", "learners", "drivers", "memory", "later", "mixedts", "ragged",
+                                       "interleave"],
                     help="regenerate one fixture family only")
     args = ap.parse_args()
     install_shims()
+    if args.only == "interleave":
+        interleave_kat()
+        return
     if args.only == "mixedts":
         mixed_ts_flags_capture()
         return

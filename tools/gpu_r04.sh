@@ -10,7 +10,7 @@ for s in ${STEPS:-smoke configs suite bench}; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     configs) step pytest_configs 600 python -u -m pytest tests/test_00_configs_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
-    rp) step pytest_rp 900 python -u -m pytest tests/test_gpu_rp.py tests/test_gpu_parity.py tests/test_gpu_distributed.py -m gpu -v --timeout 300 --timeout-method thread -k "rp_ or driver_fp or dropin_batch_small or record_parallel" ;;
+    rp) step pytest_rp 900 python -u -m pytest tests/test_gpu_rp.py tests/test_gpu_parity.py tests/test_gpu_distributed.py -m gpu -v --timeout 300 --timeout-method thread -k "rp_ or driver_ or dropin_ or record_parallel or interleaved or memory or empirical or lrts" ;;
     dropin) step dropin_dr 600 python tools/dropin_update_time.py dr 2 && step dropin_dm 600 python tools/dropin_update_time.py dm 2 ;;
     suite) step pytest_gpu 1200 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
     bench) step bench_driver 400 python bench.py --steps 20 --warmup 5 ;;
