@@ -31,6 +31,10 @@
 #include "ag_sim_oracle.h"
 #include "ag_sim_pop.h"
 
+#ifndef AG_SIM_WIDE_AB
+#define AG_SIM_WIDE_AB 0  // AG_SIM_KERNEL_WIDE (the runtime-P kernel at any P): A/B variant builds only
+#endif
+
 // ------------------------------------------------------------------------------------
 // error plumbing (declared in ag_host.h)
 // ------------------------------------------------------------------------------------
@@ -915,6 +919,9 @@ int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
     case AG_OPT_SIMULATE_KERNEL:
       if (value < AG_SIM_KERNEL_AUTO || value > AG_SIM_KERNEL_WIDE)
         return ag_set_error(AG_ERR_INVALID, "ag_set_option: bad simulate kernel %lld", (long long)value);
+      if (value == AG_SIM_KERNEL_WIDE && !AG_SIM_WIDE_AB)  // the round-3 A/B (2.3x slower): variant builds only
+        return ag_set_error(AG_ERR_UNSUPPORTED, "ag_set_option: AG_SIM_KERNEL_WIDE is built only in the A/B "
+                                                "variant (make variant VFLAGS=-DAG_SIM_WIDE_AB=1)");
       c->sim_kernel = (int32_t)value;
       return AG_OK;
     default:
@@ -1038,7 +1045,7 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
     const int rc = simulate_pop(c, B, in, out, counters_fx, (hipStream_t)stream);
     if (rc != AG_ERR_UNSUPPORTED) return rc;  // launched (or failed); else k_simulate below
   }
-  const int W = (prune && (B % 2) == 0 && c->wide && !c->general && s.num_participants <= kMaxP) ? 2 : 1;
+  int W = (prune && (B % 2) == 0 && c->wide && !c->general && s.num_participants <= kMaxP) ? 2 : 1;
   size_t lds = (size_t)prm.lds.total;
   if (lds > 160 * 1024)
     return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
@@ -1055,14 +1062,20 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   // width compile-time (k_simulate's DOS); AG_OPT_SIM_SHIPPED_SHAPE 0 turns them off (A/B)
   const int ship = (c->general && c->ship_shape && D == 6 && prm.lds.ts_do == kShipDo) ? kGenShip : 0;
   SimKernel k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
+  if (!k && W == 2) {  // the two-auctions-per-lane build is an A/B variant only (AG_LANE_PAIRS)
+    W = 1;
+    k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
+  }
   if (!k && bt != kThreads) {
     bt = kThreads;
     k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
   }
+#if AG_SIM_WIDE_AB
   if (c->general && c->sim_kernel == AG_SIM_KERNEL_WIDE) {  // the runtime-P kernel at any P (A/B)
     bt = kThreads;
     k = pick_kernel_for<0>(D, prune, 1, kGenAll, kThreads);
   }
+#endif
   if (!k) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: no kernel for P=%d D=%d", s.num_participants, D);
   if (gmode == kGenAll && bt == kLargeThreads) {  // the compacted fitted-policy pass's per-wave task slots
     add_policy_tasks(prm.lds, bt);

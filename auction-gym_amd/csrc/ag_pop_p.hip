@@ -10,7 +10,13 @@
 
 namespace ag {
 
-#if AG_P >= 1
+// AUTO runs k_pop only for TruthfulBidder-only populations at P = 8 (k_simulate is faster at
+// P = 2 on every population line, profiles/r03_ab_pop_vs_generic.log): the other participant
+// counts are built only for A/B variants (make variant VFLAGS=-DAG_POP_ALL_P=1)
+#ifndef AG_POP_ALL_P
+#define AG_POP_ALL_P 0
+#endif
+#if AG_P >= 8 || (AG_P >= 1 && AG_POP_ALL_P)
 // k_pop: the shipped catalogue shape only (K = 12, E = 5, OE = 4); mode kGenTruthful or
 // kGenAll, 256- or 1024-lane workgroups
 template <>
@@ -35,6 +41,11 @@ TsChoiceKernel pick_ts_choice_for<AG_P>(int K, int DO) {
   return k_ts_choice<AG_P, 12, 5, kThreads>;
 }
 
+#else
+template <>
+PopKernel pick_pop_for<AG_P>(int, int, int, int, int, bool) { return nullptr; }
+template <>
+TsChoiceKernel pick_ts_choice_for<AG_P>(int, int) { return nullptr; }
 #endif
 
 }  // namespace ag

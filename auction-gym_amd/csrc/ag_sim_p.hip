@@ -6,6 +6,9 @@
 #ifndef AG_P
 #error "compile with -DAG_P=<participants>"
 #endif
+#ifndef AG_LANE_PAIRS
+#define AG_LANE_PAIRS 0
+#endif
 
 namespace ag {
 namespace {
@@ -64,7 +67,13 @@ SimKernel pick_kernel_for<AG_P>(int D, bool prune, int W, int general, int bt) {
     return prune ? pick_d<P, true, 1, kGenAll>(D) : pick_d<P, false, 1, kGenAll>(D);
   }
   if (bt != kThreads) return nullptr;
-  if (prune) return W == 2 ? pick_d<P, true, 2, kGenOracle>(D) : pick_d<P, true, 1, kGenOracle>(D);
+#if AG_LANE_PAIRS
+  // two auctions per lane (AG_OPT_LANE_AUCTIONS = 2): an A/B build only (a wash isolated, slower
+  // sustained; k_oracle is the Oracle populations' kernel)
+  if (prune && W == 2) return pick_d<P, true, 2, kGenOracle>(D);
+#endif
+  if (W != 1) return nullptr;
+  if (prune) return pick_d<P, true, 1, kGenOracle>(D);
   if (D <= 8) return pick_d<P, false, 1, kGenOracle>(D);
   switch (D) {
     case 9: return k_simulate<P, 9, false, 1, kGenOracle>;

@@ -1930,6 +1930,10 @@ POP_CASES = [  # (P, mech, ts_sample, compact, block, B, launch cap, counters, p
     (1, 0, True, False, 0, 20000, 0, True, "mix"),                  # P = 1: nobody charged
     (2, 0, True, False, 0, 30000, 0, False, "search"),              # 'search' bids, no counters
     (5, 1, True, True, 1024, 50000, 0, True, "all"),                # every bidder kind / state
+    # k_pop ships for P = 8 only (AUTO: TruthfulBidder populations at P = 8); the cases above
+    # at P < 8 compare k_simulate with itself unless the library is an AG_POP_ALL_P variant
+    (8, 1, True, False, 0, (1 << 17) + 5, 0, True, "ts"),           # configs_1 at P = 8
+    (8, 0, True, True, 1024, 33333, 11111, True, "all"),
 ]
 
 
