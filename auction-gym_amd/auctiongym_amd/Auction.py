@@ -540,8 +540,8 @@ def learner_update(eng, store, index, bidder, name):
     """Bidder.update of the learning bidder at engine slot `index` from the records of the
     device store, the bidder's host mirror refreshed afterwards. The DR and ValueLearning
     'policy' fits draw one rsample per record per epoch from torch's global generator
-    (src/Models.py:160, :87): they train as the resumable one-launch-per-epoch update
-    (ag_bidder_rp_*), fed the reference's draws window by window -- made in C from the
+    (src/Models.py:160, :87): they train as the resumable update (ag_bidder_rp_*, run in
+    persistent launches), fed the reference's draws window by window -- made in C from the
     generator's state (ag_torch_normal_epochs: torch's own normal kernels, the same numbers) --
     so the fit runs once, however long; the generator is then left exactly where the
     reference's is after the update (its fit's epochs drawn, plus the rsample of every record
@@ -568,9 +568,10 @@ def learner_update(eng, store, index, bidder, name):
     return ep[index].copy()
 
 
-def _fit_with_torch_noise(eng, store, mask, index, n, launches=256):
+def _fit_with_torch_noise(eng, store, mask, index, n):
     """One agent's update with the reference's torch rsample draws, single pass: windows of
-    W policy-fit epochs drawn from the generator state as the fit reaches them."""
+    W policy-fit epochs drawn from the generator state as the fit reaches them; the fits run
+    in persistent launches (ag_bidder_rp_run) that stop at a window's end."""
     from .engine import torch_normal_epochs
     W = int(min(4096, max(16, NOISE_WINDOW_FLOATS // n)))
     state = torch.get_rng_state().numpy().copy()  # advanced window by window
@@ -579,7 +580,7 @@ def _fit_with_torch_noise(eng, store, mask, index, n, launches=256):
     win = torch.from_numpy(torch_normal_epochs(state, n, W)).to(eng.device)
     eng.bidder_rp_noise(win, n, w0, W)
     while True:
-        eng.bidder_rp_epoch(launches)
+        eng.bidder_rp_run()
         fit, ep, need = eng.bidder_rp_poll()
         if fit[index] < 0:
             break

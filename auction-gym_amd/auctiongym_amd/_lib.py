@@ -47,7 +47,7 @@ EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params
            "ag_counters_to_double", "ag_sigmoid", "ag_exp", "ag_replay_draw", "ag_replay_draw_population",
            "ag_last_error",
            "ag_abi_version", "ag_ts_noise_index", "ag_generate_ts_noise_compact", "ag_torch_normal_epochs",
-           "ag_bidder_rp_begin", "ag_bidder_rp_epoch", "ag_bidder_rp_noise", "ag_bidder_rp_poll", "ag_bidder_rp_end",
+           "ag_bidder_rp_begin", "ag_bidder_rp_epoch", "ag_bidder_rp_run", "ag_bidder_rp_noise", "ag_bidder_rp_poll", "ag_bidder_rp_end",
            "ag_lrts_rp_begin", "ag_lrts_rp_epoch", "ag_lrts_rp_poll", "ag_lrts_rp_end", "ag_empirical_update_agents")
 ABI_VERSION = 16
 LEARNER_UNINITIALISED, LEARNER_POLICY, LEARNER_SEARCH = 0, 1, 2
@@ -172,6 +172,7 @@ def load(path=None):
         "ag_torch_normal_epochs": (ctypes.c_int, [vp, i64, i64, i32, vp]),
         "ag_bidder_rp_begin": (ctypes.c_int, [vp, ctypes.POINTER(AgShadingSamples), vp, vp, vp, vp, vp]),
         "ag_bidder_rp_epoch": (ctypes.c_int, [vp, i32, ctypes.POINTER(i64), vp, vp]),
+        "ag_bidder_rp_run": (ctypes.c_int, [vp, vp, vp]),
         "ag_bidder_rp_noise": (ctypes.c_int, [vp, vp, i64, i32, i32]),
         "ag_bidder_rp_poll": (ctypes.c_int, [vp, vp, vp, vp, vp]),
         "ag_bidder_rp_end": (ctypes.c_int, [vp, vp, vp, vp]),

@@ -546,6 +546,11 @@ class AuctionEngine:
                     "ag_bidder_rp_epoch")
         return k.value
 
+    def bidder_rp_run(self, traces=None):
+        """One process holding every record: run the learners in persistent launches until each
+        is done or waits for noise (ag_bidder_rp_run; the same state bidder_rp_epoch steps)."""
+        self._check(self.L.ag_bidder_rp_run(self._h, _ptr(traces), _stream()), "ag_bidder_rp_run")
+
     def bidder_rp_noise(self, noise, noise_n, first_epoch, epochs):
         """The host-drawn rsample window (device float32 [epochs][noise_n]) of the policy fits."""
         self._rp_noise = noise  # kept alive while the launches read it

@@ -146,6 +146,82 @@ __device__ __forceinline__ void agent_allreduce_i64(unsigned *bar, int64_t *acc,
   __syncthreads();
 }
 
+// agent_allreduce_i64 split in two so that a workgroup computes something else while the sum
+// climbs the tree (ag_dr.hip k_bidder_pipe: the next learner's epoch): _start adds the
+// workgroup's W words (LDS vals) up the tree -- the root's last arriver stores the totals to
+// row 0 and bumps the generation -- and returns whether this workgroup was that root (every
+// thread gets it); thread 0 keeps the generation it read before arriving in *s_gen.
+// _finish waits for the generation to move (the root does not wait) and reads row 0 into
+// tot. Between the two the workgroup may run other _start / _finish pairs on OTHER regions;
+// on one region the calls alternate (a region's next _start follows its _finish). Every
+// workgroup of the region must be resident (cooperative launch). nblk <= 1: vals is the total
+// (tot must then be vals).
+__device__ __forceinline__ bool agent_allreduce_start(unsigned *bar, int64_t *acc, int stride, int rank, int nblk,
+                                                      const int64_t *vals, int W, unsigned *s_gen, int *s_flag) {
+  const int t = threadIdx.x, nt = blockDim.x;
+  __syncthreads();
+  if (nblk <= 1) return true;
+  for (int j = t; j < W; j += nt)
+    __hip_atomic_fetch_add(acc + (size_t)(1 + rank / kBarFanIn) * stride + j, vals[j], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  unsigned *gen = bar;
+  if (t == 0) *s_gen = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int idx = rank, members_prev = nblk, base = 1;
+  bool root = false;
+  for (;;) {
+    const int nodes = (members_prev + kBarFanIn - 1) / kBarFanIn, q = idx / kBarFanIn;
+    const int members = members_prev - q * kBarFanIn < kBarFanIn ? members_prev - q * kBarFanIn : kBarFanIn;
+    __syncthreads();  // this workgroup's additions to the node are issued before it arrives
+    if (t == 0) {
+      unsigned *cnt = bar + (size_t)(base + q) * kBarLineWords;
+      const bool last =
+          __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)members - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      *s_flag = last;
+    }
+    __syncthreads();
+    if (!*s_flag) break;
+    int64_t *node = acc + (size_t)(base + q) * stride;
+    int64_t *dst = nodes == 1 ? acc : acc + (size_t)(base + nodes + q / kBarFanIn) * stride;
+    for (int j = t; j < W; j += nt) {
+      const int64_t v = __hip_atomic_load(node + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(node + j, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (nodes == 1)
+        __hip_atomic_store(dst + j, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        __hip_atomic_fetch_add(dst + j, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (nodes == 1) {
+      root = true;
+      break;
+    }
+    base += nodes;
+    idx = q;
+    members_prev = nodes;
+  }
+  __syncthreads();  // the root's totals are stored before the generation moves
+  if (t == 0 && root) __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  return root;
+}
+__device__ __forceinline__ void agent_allreduce_finish(unsigned *bar, const int64_t *acc, int nblk, bool root,
+                                                       const unsigned *s_gen, int W, int64_t *tot) {
+  if (nblk <= 1) return;
+  const int t = threadIdx.x, nt = blockDim.x;
+  if (t == 0 && !root) {
+    const unsigned g = *s_gen;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g)
+      __builtin_amdgcn_s_sleep(AG_BAR_SLEEP);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  for (int j = t; j < W; j += nt)
+    tot[j] = __hip_atomic_load(const_cast<int64_t *>(acc) + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+}
+
 // The same combining-tree sum without the wait (per-epoch launches, ag_dr.hip k_bidder_epoch):
 // each workgroup adds its W words (LDS vals) up the tree and the root's last arriver stores
 // the totals to `out` (a global row read by the NEXT launch: the kernel boundary orders it);

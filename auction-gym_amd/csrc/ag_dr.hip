@@ -15,6 +15,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <type_traits>
 #include <vector>
 
 #include <hipcub/hipcub.hpp>
@@ -57,6 +58,10 @@ __device__ __forceinline__ int64_t fxb(double v) {
   if (__builtin_expect(__builtin_fabs(x) < 0x1p51, 1)) return (int64_t)agexp::asu64(x + 0x1.8p52);
   return (int64_t)((uint64_t)(int64_t)__builtin_rint(x) + kFxMagic);
 }
+// fxb's fast path on x = v * 2^40 already formed, and its range test (callers test a
+// record's terms together and take fxb for all of them when one is out of range)
+__device__ __forceinline__ int64_t fxb_x(double x) { return (int64_t)agexp::asu64(x + 0x1.8p52); }
+__device__ __forceinline__ bool fx_in(double x) { return __builtin_fabs(x) < 0x1p51; }
 __device__ __forceinline__ void addw(int64_t &a, int64_t t) { a = (int64_t)((uint64_t)a + (uint64_t)t); }
 __device__ __forceinline__ void fx_unbias(int64_t &a, int64_t n) {
   a = (int64_t)((uint64_t)a - (uint64_t)n * kFxMagic);
@@ -177,6 +182,71 @@ __device__ __forceinline__ void policy_fwd(const float *p, double c, double v, P
   f.sp_sigma = softplus_fast(f.as, f.eas, tab);
   f.sigma = f.sp_sigma + 0.01;  // min_sigma (src/Models.py:104)
 }
+// softplus through the main paths alone (ok cleared when an input leaves them)
+__device__ __forceinline__ double softplus_main(double u, double &e, const uint64_t *tab, bool &ok) {
+  e = agexp::exp_main(u, tab);
+  bool lok;
+  const double l = aglog1p::log1p_main(e, lok);
+  ok = (int)ok & (int)agexp::exp_in_main(u) & ((int)lok | (int)(u > 20.0));
+  return u > 20.0 ? u : l;
+}
+// policy_fwd through the main paths alone: true when they gave policy_fwd's values (every
+// softplus input inside them), else the caller runs policy_fwd -- one rare branch per record
+// instead of one per softplus
+__device__ __forceinline__ bool policy_fwd_main(const float *p, double c, double v, PolF &f, const uint64_t *tab) {
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    f.h[j] = c * (double)p[2 * j] + v * (double)p[2 * j + 1] + (double)p[4 + j];
+    f.s[j] = softplus_main(f.h[j], f.eh[j], tab, ok);
+  }
+  f.am = f.s[0] * (double)p[6] + f.s[1] * (double)p[7] + (double)p[8];
+  f.as = f.s[0] * (double)p[9] + f.s[1] * (double)p[10] + (double)p[11];
+  f.mu = softplus_main(f.am, f.eam, tab, ok);
+  f.sp_sigma = softplus_main(f.as, f.eas, tab, ok);
+  f.sigma = f.sp_sigma + 0.01;
+  return ok;
+}
+__device__ __forceinline__ void policy_fwd_fast(const float *p, double c, double v, PolF &f, const uint64_t *tab) {
+  if (__builtin_expect(!policy_fwd_main(p, c, v, f, tab), 0)) policy_fwd(p, c, v, f, tab);
+}
+// policy_bwd's twelve gradient terms as doubles (d[j]: parameter j), the same expressions
+__device__ __forceinline__ void policy_terms(const float *p, double c, double v, const PolF &f, double dmu,
+                                             double dsigma, double *d) {
+  const double dam = dmu * dsoftplus_e(f.am, f.eam), das = dsigma * dsoftplus_e(f.as, f.eas);
+  double ds[2];
+  ds[0] = dam * (double)p[6] + das * (double)p[9];
+  ds[1] = dam * (double)p[7] + das * (double)p[10];
+  d[6] = dam * f.s[0];
+  d[7] = dam * f.s[1];
+  d[8] = dam;
+  d[9] = das * f.s[0];
+  d[10] = das * f.s[1];
+  d[11] = das;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const double dh = ds[j] * dsoftplus_e(f.h[j], f.eh[j]);
+    d[2 * j] = dh * c;
+    d[2 * j + 1] = dh * v;
+    d[4 + j] = dh;
+  }
+}
+// a record's N fixed-point terms through fxb's fast path when every one is in its range (ok
+// in: the record's main-path test), added to acc[0..N); false (nothing added) otherwise
+template <int N>
+__device__ __forceinline__ bool fx_add_fast(int64_t (&acc)[16], const double (&d)[N], bool ok) {
+  double x[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    x[k] = d[k] * kGrid;
+    ok = (int)ok & (int)fx_in(x[k]);
+  }
+  if (__builtin_expect(!ok, 0)) return false;
+#pragma unroll
+  for (int k = 0; k < N; ++k) addw(acc[k], fxb_x(x[k]));
+  return true;
+}
+
 __device__ __forceinline__ void policy_bwd(const float *p, double c, double v, const PolF &f, double dmu,
                                            double dsigma, int64_t (&G)[16], int off, const uint64_t *tab) {
   const double dam = dmu * dsoftplus_e(f.am, f.eam), das = dsigma * dsoftplus_e(f.as, f.eas);
@@ -379,7 +449,37 @@ struct RecView {
   __device__ __forceinline__ double util(int64_t j) const { return f(kFUtil, R.util, j); }
   __device__ __forceinline__ double eut(int64_t j) const { return f(kFEu, eu, j); }
   __device__ __forceinline__ double won(int64_t j) const { return (double)(j < cap ? lw[j] : R.won[c0 + j]); }
+  // the same fields with the LDS / global choice known at compile time (each_record's loops)
+  template <bool L>
+  __device__ __forceinline__ double fl(int fld, const double *g, int64_t j) const {
+    if constexpr (L) return (double)lf[(int64_t)fld * cap + j];
+    else return (double)(float)g[c0 + j];
+  }
+  template <bool L> __device__ __forceinline__ double ctr_(int64_t j) const { return fl<L>(kFCtr, R.ctr, j); }
+  template <bool L> __device__ __forceinline__ double val_(int64_t j) const { return fl<L>(kFVal, R.value, j); }
+  template <bool L> __device__ __forceinline__ double gam_(int64_t j) const { return fl<L>(kFGam, R.gamma, j); }
+  template <bool L> __device__ __forceinline__ double util_(int64_t j) const { return fl<L>(kFUtil, R.util, j); }
+  template <bool L> __device__ __forceinline__ double eut_(int64_t j) const { return fl<L>(kFEu, eu, j); }
+  template <bool L> __device__ __forceinline__ float prop_(int64_t j) const {
+    if constexpr (L) return lf[(int64_t)kFProp * cap + j];
+    else return (float)R.prop[c0 + j];
+  }
+  template <bool L> __device__ __forceinline__ double won_(int64_t j) const {
+    if constexpr (L) return (double)lw[j];
+    else return (double)R.won[c0 + j];
+  }
 };
+
+// f(j, std::true_type / std::false_type) for this thread's records j of [0, nb): the staged
+// ones (j < cap, read from LDS) then the rest (global) -- two loops with the source known at
+// compile time, instead of a per-field test (cap is a multiple of kDrThreads)
+template <class F>
+__device__ __forceinline__ void each_record(const RecView &V, int64_t nb, F &&f) {
+  const int64_t ns = nb < V.cap ? nb : V.cap;
+  int64_t j = threadIdx.x;
+  for (; j < ns; j += kDrThreads) f(j, std::true_type());
+  for (; j < nb; j += kDrThreads) f(j, std::false_type());
+}
 
 // One BCE row of the win-rate fit (its loss and gradient terms, biased: see fxb) at the model
 // (w0, w1, w2, w3). One exp per row (oracle/ag_oracle_dr.c fit_winrate): e = exp(-|z|), L =
@@ -394,19 +494,33 @@ __device__ __forceinline__ void wr_row(int64_t (&acc)[5], double c, double v, do
   double e = agexp::exp_main(-a, tab);
   bool lok;
   double Lz = aglog1p::log1p_main(e, lok);
-  if (__builtin_expect(!(agexp::exp_in_main(a) && lok), 0)) {
-    e = agexp::exp(-a, tab);
-    Lz = aglog1p::log1p(e);
-  }
-  const double pw = (z >= 0.0 ? 1.0 : e) / (1.0 + e);
   const double u = y > 0.0 ? -z : z;
-  const double t = fmin(u > 20.0 ? u : (u > 0.0 ? a + Lz : Lz), 100.0);
-  // |t| <= 100, |pw - y| <= 1, ctr in [0, 1]: these terms are far inside fxr's fast range
+  double pw = (z >= 0.0 ? 1.0 : e) / (1.0 + e);
+  double t = fmin(u > 20.0 ? u : (u > 0.0 ? a + Lz : Lz), 100.0);
+  double gz = pw - y;
+  // |t| <= 100, |pw - y| <= 1, ctr in [0, 1]: those terms are far inside fxb's fast range;
+  // gz * value and gz * gamma are checked. ONE rare branch per row (the exp / log1p patch and
+  // an out-of-range term together) instead of one per patch: the common path stays straight.
+  const double x2 = (gz * v) * kGrid, x3 = (gz * g) * kGrid;
+  int64_t t2, t3;
+  if (__builtin_expect((int)agexp::exp_in_main(a) & (int)lok & (int)fx_in(x2) & (int)fx_in(x3), 1)) {
+    t2 = fxb_x(x2);
+    t3 = fxb_x(x3);
+  } else {
+    if (!(agexp::exp_in_main(a) && lok)) {
+      e = agexp::exp(-a, tab);
+      Lz = aglog1p::log1p(e);
+      pw = (z >= 0.0 ? 1.0 : e) / (1.0 + e);
+      t = fmin(u > 20.0 ? u : (u > 0.0 ? a + Lz : Lz), 100.0);
+      gz = pw - y;
+    }
+    t2 = fxb(gz * v);
+    t3 = fxb(gz * g);
+  }
   addw(acc[0], fxb_fast(t));
-  const double gz = pw - y;
   addw(acc[1], fxb_fast(gz * c));
-  addw(acc[2], fxb(gz * v));
-  if (!aug) addw(acc[3], fxb(gz * g));  // the augmentation row's g = 0 term is +-0: rounds to 0
+  addw(acc[2], t2);
+  if (!aug) addw(acc[3], t3);  // the augmentation row's g = 0 term is +-0: rounds to 0
   addw(acc[4], fxb_fast(gz));
 }
 // a lane that ran wr_row for nrec records (both rows each): its accumulators unbiased
@@ -437,12 +551,13 @@ __device__ int fit_winrate(const RecView &V, const Chunk &K, TrainLds &S, Coop &
     // record j's logged row and its gamma = 0, y = 0 augmentation row together (two
     // independent chains for the scheduler; the sums are exact, so any order)
     int64_t nrec = 0;
-    for (int64_t j = tid; j < K.nb; j += kDrThreads) {
-      const double c = V.ctr(j), v = V.val(j);
-      wr_row(acc, c, v, V.gam(j), V.won(j), false, w0, w1, w2, w3, S.tab);
+    each_record(V, K.nb, [&](int64_t j, auto L) {
+      constexpr bool l = decltype(L)::value;
+      const double c = V.template ctr_<l>(j), v = V.template val_<l>(j);
+      wr_row(acc, c, v, V.template gam_<l>(j), V.template won_<l>(j), false, w0, w1, w2, w3, S.tab);
       wr_row(acc, c, v, 0.0, 0.0, true, w0, w1, w2, w3, S.tab);
       ++nrec;
-    }
+    });
     wr_unbias(acc, nrec);
     exact_totals<5>(acc, S, C);
     // every thread: the same loss; threads 0..3 step their parameter
@@ -460,14 +575,32 @@ __device__ int fit_winrate(const RecView &V, const Chunk &K, TrainLds &S, Coop &
 
 // one record of the imitation fit: MSE terms of mu to the logged gamma and of softplus(sigma)
 // to 0.05 (acc[12], acc[13]) and their gradient (acc[0..11]), biased
-__device__ __forceinline__ void imit_rec(int64_t (&acc)[16], const float *pol, double c, double v, double g,
-                                         const uint64_t *tab) {
+__device__ __noinline__ void imit_rec_exact(int64_t (&acc)[16], const float *pol, double c, double v, double g,
+                                            const uint64_t *tab) {
   PolF f;
   policy_fwd(pol, c, v, f, tab);
   const double dm = f.mu - g, dsg = f.sp_sigma - 0.05;
   addw(acc[12], fxb(dm * dm));
   addw(acc[13], fxb(dsg * dsg));
   policy_bwd(pol, c, v, f, 2.0 * dm, 2.0 * dsg, acc, 0, tab);
+}
+// the common path: main-path functions and fast fixed-point terms, imit_rec_exact (the same
+// terms) when a record leaves them
+__device__ __forceinline__ void imit_rec(int64_t (&acc)[16], const float *pol, double c, double v, double g,
+                                         const uint64_t *tab) {
+  PolF f;
+  const bool ok = policy_fwd_main(pol, c, v, f, tab);
+  const double dm = f.mu - g, dsg = f.sp_sigma - 0.05;
+  double d[14];
+  policy_terms(pol, c, v, f, 2.0 * dm, 2.0 * dsg, d);
+  d[12] = dm * dm;
+  d[13] = dsg * dsg;
+  if (__builtin_expect(!fx_add_fast<14>(acc, d, ok), 0)) {  // (a separate array: acc stays in registers)
+    int64_t t[16] = {};
+    imit_rec_exact(t, pol, c, v, g, tab);
+#pragma unroll
+    for (int k = 0; k < 14; ++k) addw(acc[k], t[k]);
+  }
 }
 
 // BidShadingContextualBandit.initialise_policy (src/Models.py:106-137): imitation of the
@@ -484,7 +617,10 @@ __device__ int fit_imitation(const RecView &V, const Chunk &K, TrainLds &S, Coop
     int64_t acc[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = 0;
-    for (int64_t j = tid; j < K.nb; j += kDrThreads) imit_rec(acc, S.pol, V.ctr(j), V.val(j), V.gam(j), S.tab);
+    each_record(V, K.nb, [&](int64_t j, auto L) {
+      constexpr bool l = decltype(L)::value;
+      imit_rec(acc, S.pol, V.template ctr_<l>(j), V.template val_<l>(j), V.template gam_<l>(j), S.tab);
+    });
     const int64_t nrec = K.nb > tid ? (K.nb - tid + kDrThreads - 1) / kDrThreads : 0;
 #pragma unroll
     for (int q = 0; q < 14; ++q) fx_unbias(acc[q], nrec);
@@ -502,8 +638,8 @@ __device__ int fit_imitation(const RecView &V, const Chunk &K, TrainLds &S, Coop
 
 // one record of the DR policy fit (fit_dr): its loss term (acc[12]) and gradient (acc[0..11]),
 // biased; du = utility - estimated utility, ep = the epoch's rsample draw
-__device__ __forceinline__ void dr_rec(int64_t (&acc)[16], const float *pol, const float *wr, double c, double v,
-                                       double g, float prop, double du, double ep, const uint64_t *tab) {
+__device__ __noinline__ void dr_rec_exact(int64_t (&acc)[16], const float *pol, const float *wr, double c,
+                                          double v, double g, float prop, double du, double ep, const uint64_t *tab) {
   const double inv_sqrt2pi = 1.0 / __builtin_sqrt(2.0 * 3.141592653589793);
   PolF f;
   policy_fwd(pol, c, v, f, tab);
@@ -530,6 +666,45 @@ __device__ __forceinline__ void dr_rec(int64_t (&acc)[16], const float *pol, con
   if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)wr[2];
   policy_bwd(pol, c, v, f, -(dpi_dmu + ddm), -(dpi_dsg + ddm * ep), acc, 0, tab);
 }
+// the common path of dr_rec_exact (main-path exp / softplus, fast fixed-point terms; the
+// same expressions), dr_rec_exact when a record leaves it
+__device__ __forceinline__ void dr_rec(int64_t (&acc)[16], const float *pol, const float *wr, double c, double v,
+                                       double g, float prop, double du, double ep, const uint64_t *tab) {
+  const double inv_sqrt2pi = 1.0 / __builtin_sqrt(2.0 * 3.141592653589793);
+  PolF f;
+  bool ok = policy_fwd_main(pol, c, v, f, tab);
+  const double mu = f.mu, sg = f.sigma;
+  const double zz = (mu - g) / sg;
+  const double xp = -(zz * zz) / 2.0;
+  const double pdf_raw = agexp::exp_main(xp, tab) / sg * inv_sqrt2pi;
+  const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
+  const double p0 = (double)fmaxf(prop, 1e-15f);
+  const double iw = pi / p0;
+  const double iwc = iw < 1.0 / 50.0 ? 1.0 / 50.0 : (iw > 50.0 ? 50.0 : iw);
+  const double raw = mu + sg * ep;
+  const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
+  const double zw = c * (double)wr[0] + v * (double)wr[1] + gs * (double)wr[2] + (double)wr[3];
+  const double Wv = 1.0 / (1.0 + agexp::exp_main(-zw, tab));
+  ok = (int)ok & (int)agexp::exp_in_main(xp) & (int)agexp::exp_in_main(-zw);
+  const double V = c * v;
+  double d[13];
+  d[12] = -(du * iwc + Wv * (V - V * gs));
+  double dpi_dmu = 0.0, dpi_dsg = 0.0;
+  if (pdf_raw >= 1e-30 && iw >= 1.0 / 50.0 && iw <= 50.0) {
+    const double k = du / p0;
+    dpi_dmu = k * pdf_raw * (g - mu) / (sg * sg);
+    dpi_dsg = k * pdf_raw * ((g - mu) * (g - mu) / (sg * sg * sg) - 1.0 / sg);
+  }
+  double ddm = 0.0;
+  if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)wr[2];
+  policy_terms(pol, c, v, f, -(dpi_dmu + ddm), -(dpi_dsg + ddm * ep), d);
+  if (__builtin_expect(!fx_add_fast<13>(acc, d, ok), 0)) {
+    int64_t t[16] = {};
+    dr_rec_exact(t, pol, wr, c, v, g, prop, du, ep, tab);
+#pragma unroll
+    for (int k = 0; k < 13; ++k) addw(acc[k], t[k]);
+  }
+}
 
 // DoublyRobustBidder's policy fit (src/Bidder.py:562-590, src/Models.py:201-218): loss
 // -mean((u - u^) clip(pi / pi0, 1/50, 50) + W(ctr, value, g~) (V - V g~)), g~ = clip(mu +
@@ -548,9 +723,11 @@ __device__ int fit_dr(const RecView &V, const Chunk &K, TrainLds &S, Coop &C,
     int64_t acc[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = 0;
-    for (int64_t j = tid; j < K.nb; j += kDrThreads)
-      dr_rec(acc, S.pol, S.wr, V.ctr(j), V.val(j), V.gam(j), V.prop(j), V.util(j) - V.eut(j),
-             fit_eps(F, e, K.c0 + j), S.tab);
+    each_record(V, K.nb, [&](int64_t j, auto L) {
+      constexpr bool l = decltype(L)::value;
+      dr_rec(acc, S.pol, S.wr, V.template ctr_<l>(j), V.template val_<l>(j), V.template gam_<l>(j),
+             V.template prop_<l>(j), V.template util_<l>(j) - V.template eut_<l>(j), fit_eps(F, e, K.c0 + j), S.tab);
+    });
     const int64_t nrec = K.nb > tid ? (K.nb - tid + kDrThreads - 1) / kDrThreads : 0;
 #pragma unroll
     for (int q = 0; q < 13; ++q) fx_unbias(acc[q], nrec);
@@ -570,8 +747,8 @@ __device__ int fit_dr(const RecView &V, const Chunk &K, TrainLds &S, Coop &C,
 }
 
 // one record of the ValueLearningBidder policy fit (fit_dm), biased
-__device__ __forceinline__ void dm_rec(int64_t (&acc)[16], const float *pol, const float *wr, double c, double v,
-                                       double ep, const uint64_t *tab) {
+__device__ __noinline__ void dm_rec_exact(int64_t (&acc)[16], const float *pol, const float *wr, double c,
+                                          double v, double ep, const uint64_t *tab) {
   PolF f;
   policy_fwd(pol, c, v, f, tab);
   const double raw = f.mu + f.sigma * ep;
@@ -583,6 +760,29 @@ __device__ __forceinline__ void dm_rec(int64_t (&acc)[16], const float *pol, con
   double ddm = 0.0;
   if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)wr[2];
   policy_bwd(pol, c, v, f, -ddm, -(ddm * ep), acc, 0, tab);
+}
+// the common path of dm_rec_exact, dm_rec_exact when a record leaves it
+__device__ __forceinline__ void dm_rec(int64_t (&acc)[16], const float *pol, const float *wr, double c, double v,
+                                       double ep, const uint64_t *tab) {
+  PolF f;
+  bool ok = policy_fwd_main(pol, c, v, f, tab);
+  const double raw = f.mu + f.sigma * ep;
+  const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
+  const double zw = c * (double)wr[0] + v * (double)wr[1] + gs * (double)wr[2] + (double)wr[3];
+  const double Wv = 1.0 / (1.0 + agexp::exp_main(-zw, tab));
+  ok = (int)ok & (int)agexp::exp_in_main(-zw);
+  const double V = c * v;
+  double d[13];
+  d[12] = -(Wv * (V - V * gs));
+  double ddm = 0.0;
+  if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)wr[2];
+  policy_terms(pol, c, v, f, -ddm, -(ddm * ep), d);
+  if (__builtin_expect(!fx_add_fast<13>(acc, d, ok), 0)) {
+    int64_t t[16] = {};
+    dm_rec_exact(t, pol, wr, c, v, ep, tab);
+#pragma unroll
+    for (int k = 0; k < 13; ++k) addw(acc[k], t[k]);
+  }
 }
 
 // ValueLearningBidder's policy fit (inference 'policy', src/Bidder.py:258-303): loss
@@ -602,8 +802,10 @@ __device__ int fit_dm(const RecView &V, const Chunk &K, TrainLds &S, Coop &C, co
     int64_t acc[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = 0;
-    for (int64_t j = tid; j < K.nb; j += kDrThreads)
-      dm_rec(acc, S.pol, S.wr, V.ctr(j), V.val(j), fit_eps(F, e, K.c0 + j), S.tab);
+    each_record(V, K.nb, [&](int64_t j, auto L) {
+      constexpr bool l = decltype(L)::value;
+      dm_rec(acc, S.pol, S.wr, V.template ctr_<l>(j), V.template val_<l>(j), fit_eps(F, e, K.c0 + j), S.tab);
+    });
     const int64_t nrec = K.nb > tid ? (K.nb - tid + kDrThreads - 1) / kDrThreads : 0;
 #pragma unroll
     for (int q = 0; q < 13; ++q) fx_unbias(acc[q], nrec);
@@ -664,7 +866,7 @@ __device__ int fit_pl(const RecView &V, const Chunk &K, TrainLds &S, Coop &C, in
     for (int64_t j = tid; j < K.nb; j += kDrThreads) {
       const double c = V.ctr(j), v = V.val(j), g = V.gam(j);
       PolF f;
-      policy_fwd(S.pol, c, v, f, S.tab);
+      policy_fwd_fast(S.pol, c, v, f, S.tab);
       const double mu = f.mu, sg = f.sigma;
       const double zz = (mu - g) / sg;
       const double pdf_raw = exp_fast(-(zz * zz) / 2.0, S.tab) / sg * inv_sqrt2pi;
@@ -799,7 +1001,7 @@ __global__ __launch_bounds__(kDrThreads, PH == 0 ? 4 : 1) void k_bidder_train(
       ep0 = fit_winrate(V, K, S, C, 256, 0.2, 1024, adam_tab, tr);
     } else {  // ValueLearningBidder
       int64_t acc[1] = {0};
-      for (int64_t j = tid; j < K.nb; j += kDrThreads) acc[0] += V.won(j) != 0.0 ? 1 : 0;
+      each_record(V, K.nb, [&](int64_t j, auto L) { acc[0] += V.template won_<decltype(L)::value>(j) != 0.0 ? 1 : 0; });
       exact_totals<1>(acc, S, C);
       if (S.tot[0] == 0 && S.tot[1] == 0)
         stat = 1;  // src/Bidder.py:206-211: revert to Gaussian shading, nothing trained
@@ -1110,6 +1312,247 @@ __global__ __launch_bounds__(kDrThreads) void k_bidder_epoch(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Pipelined persistent training (ag_bidder_rp_run; ag_bidder_update's exact-sum learners):
+// the FitSt state machine of k_bidder_epoch inside ONE cooperative launch per phase, every
+// workgroup holding a contiguous slice of EVERY learner's records (slot i: learner
+// agents[i]). A round visits the learners in turn: finish learner i's last epoch sum (its
+// combining tree, agent_allreduce_finish), step its state (fit_step: loss, Adam, scheduler,
+// early stop, next fit -- every workgroup the same integers, so the same step), add this
+// workgroup's exact terms of its next epoch and start that sum up the tree
+// (agent_allreduce_start) -- then the next learner. A learner's sum climbs the tree while the
+// workgroups compute the OTHER learners' epochs, so the cross-workgroup latency that one
+// learner per launch (k_bidder_train) or per epoch (k_bidder_epoch) waits out is hidden
+// behind useful work. Integer sums: the same models, epochs and status bit for bit as both.
+//   PH = 0: the win count and the win-rate fit (4 workgroups per CU, <= 128 VGPRs);
+//   PH = 1: estimated utilities, imitation, the policy fits (2 per CU).
+// A policy fit whose host-drawn noise window ends waits with its state kept (need_noise);
+// the launch ends when no learner has an epoch left in its phase.
+constexpr int kPipeMaxAgents = 16;
+struct PipeArgs {
+  int NA;                       // learners in the launch (<= kPipeMaxAgents)
+  const int32_t *agents;        // [NA] their agent indices
+  const int32_t *bkind, *bmode, *initialised;
+  const int64_t *offsets;       // [N + 1] sorted records
+  const int64_t *n_total;       // [N] the learners' record counts (fit_step's n)
+  DrRecords R0;
+  double *eu_ws;
+  FitSt *st;                    // [N] in / out
+  const int64_t *tot_in;        // [N][32] totals pending from ag_bidder_rp_epoch (have_tot)
+  int64_t *acc;                 // [NA][lines][32] combining-tree rows
+  unsigned *bars;               // [NA][lines][kBarLineWords]
+  int lines;
+  const int32_t *lds_off;       // [NA] record-cache byte offsets (dynamic LDS, after the FitSt copies)
+  const int32_t *lds_cap;       // [NA] records cached per workgroup
+  const float *noise;           // host-drawn draws or NULL (synthetic)
+  const int64_t *noise_off;     // [N] per-learner offsets (NULL: 0)
+  int64_t noise_stride;         // floats per epoch (0: the learner's record count)
+  int32_t noise_e0, noise_epochs;
+  uint64_t noise_seed;
+  const double *adam_tab;
+  float *traces;                // [N][3][kDrEpochs] or NULL
+};
+
+// this workgroup's slice [c0, c0 + nb) of n records over G workgroups
+__device__ __forceinline__ void pipe_chunk(int64_t n, int G, int rank, int64_t &c0, int64_t &nb) {
+  const int64_t per = (n + G - 1) / G;
+  c0 = (int64_t)rank * per < n ? (int64_t)rank * per : n;
+  nb = (c0 + per < n ? c0 + per : n) - c0;
+}
+
+template <int PH>
+__device__ __forceinline__ bool pipe_in_phase(int fit) {
+  return PH == 0 ? (fit == kFitWins || fit == kFitWr) : (fit == kFitEu || fit == kFitInit || fit == kFitPol);
+}
+
+// this workgroup's exact partial sums of the learner's current epoch -> S.tot; returns the
+// words to sum (k_bidder_epoch's step 2)
+template <int PH>
+__device__ __forceinline__ int pipe_partial(const FitSt &st, const RecView &V, int64_t nb, int bk, const FitNoise &F,
+                                            TrainLds &S) {
+  const int tid = threadIdx.x;
+  const int64_t nrec = nb > tid ? (nb - tid + kDrThreads - 1) / kDrThreads : 0;
+  if constexpr (PH == 0) {
+    if (st.fit == kFitWins) {
+      int64_t acc[1] = {0};
+      each_record(V, nb, [&](int64_t j, auto L) { acc[0] += V.template won_<decltype(L)::value>(j) != 0.0 ? 1 : 0; });
+      block_sums<1>(acc, S.w, S.tot);
+      return 2;
+    }
+    int64_t acc[5] = {0, 0, 0, 0, 0};
+    const double w0 = (double)st.wr[0], w1 = (double)st.wr[1], w2 = (double)st.wr[2], w3 = (double)st.wr[3];
+    each_record(V, nb, [&](int64_t j, auto L) {
+      constexpr bool l = decltype(L)::value;
+      const double c = V.template ctr_<l>(j), v = V.template val_<l>(j);
+      wr_row(acc, c, v, V.template gam_<l>(j), V.template won_<l>(j), false, w0, w1, w2, w3, S.tab);
+      wr_row(acc, c, v, 0.0, 0.0, true, w0, w1, w2, w3, S.tab);
+    });
+    wr_unbias(acc, nrec);
+    block_sums<5>(acc, S.w, S.tot);
+    return 10;
+  } else {
+    int64_t acc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0;
+    const int e = st.epoch;
+    if (st.fit == kFitInit) {
+      each_record(V, nb, [&](int64_t j, auto L) {
+        constexpr bool l = decltype(L)::value;
+        imit_rec(acc, st.pol, V.template ctr_<l>(j), V.template val_<l>(j), V.template gam_<l>(j), S.tab);
+      });
+#pragma unroll
+      for (int q = 0; q < 14; ++q) fx_unbias(acc[q], nrec);
+    } else if (bk == AG_BIDDER_DOUBLY_ROBUST) {
+      each_record(V, nb, [&](int64_t j, auto L) {
+        constexpr bool l = decltype(L)::value;
+        dr_rec(acc, st.pol, st.wr, V.template ctr_<l>(j), V.template val_<l>(j), V.template gam_<l>(j),
+               V.template prop_<l>(j), V.template util_<l>(j) - V.template eut_<l>(j), fit_eps(F, e, V.c0 + j), S.tab);
+      });
+#pragma unroll
+      for (int q = 0; q < 13; ++q) fx_unbias(acc[q], nrec);
+    } else {
+      each_record(V, nb, [&](int64_t j, auto L) {
+        constexpr bool l = decltype(L)::value;
+        dm_rec(acc, st.pol, st.wr, V.template ctr_<l>(j), V.template val_<l>(j), fit_eps(F, e, V.c0 + j), S.tab);
+      });
+#pragma unroll
+      for (int q = 0; q < 13; ++q) fx_unbias(acc[q], nrec);
+    }
+    block_sums<16>(acc, S.w, S.tot);
+    return 32;
+  }
+}
+
+template <int PH>
+__global__ __launch_bounds__(kDrThreads, PH == 0 ? 4 : 2) void k_bidder_pipe(PipeArgs A) {
+  __shared__ TrainLds S;
+  __shared__ float s_grad[16], s_loss;
+  __shared__ int s_np;
+  __shared__ unsigned s_gen[kPipeMaxAgents];
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+  FitSt *fst = reinterpret_cast<FitSt *>(s_dyn);
+  const int tid = threadIdx.x, G = gridDim.x, rank = blockIdx.x, NA = A.NA;
+  for (int i = tid; i < 256; i += kDrThreads) S.tab[i] = ag_exp_tab[i];
+  for (int i = tid; i < NA; i += kDrThreads) fst[i] = A.st[A.agents[i]];
+  __syncthreads();
+  // stage every slot's cached records (this phase's fields)
+  for (int i = 0; i < NA; ++i) {
+    const int a = A.agents[i], bk = A.bkind[a];
+    const int64_t s0 = A.offsets[a];
+    int64_t c0, nb;
+    pipe_chunk(A.offsets[a + 1] - s0, G, rank, c0, nb);
+    const int64_t cap = A.lds_cap[i], ns = nb < cap ? nb : cap;
+    float *lf = reinterpret_cast<float *>(s_dyn + A.lds_off[i]);
+    const bool dr = bk == AG_BIDDER_DOUBLY_ROBUST;
+    const int nf = PH == 0 ? 3 : (dr ? 6 : 2);
+    uint8_t *lw = reinterpret_cast<uint8_t *>(lf + (size_t)nf * cap);
+    const bool eu_ready = dr && fst[i].fit > kFitEu && fst[i].fit != kFitDone;
+    for (int64_t j = tid; j < ns; j += kDrThreads) {
+      const int64_t r = s0 + c0 + j;
+      lf[kFCtr * cap + j] = (float)A.R0.ctr[r];
+      lf[kFVal * cap + j] = (float)A.R0.value[r];
+      if (PH == 0 || dr) lf[kFGam * cap + j] = (float)A.R0.gamma[r];
+      if (PH == 0) lw[j] = A.R0.won[r];
+      if (PH == 1 && dr) {
+        lf[kFProp * cap + j] = (float)A.R0.prop[r];
+        lf[kFUtil * cap + j] = (float)A.R0.util[r];
+        if (eu_ready) lf[kFEu * cap + j] = (float)A.eu_ws[r];
+      }
+    }
+  }
+  __syncthreads();
+  auto view = [&](int i, int64_t &nb) -> RecView {
+    const int a = A.agents[i];
+    const int64_t s0 = A.offsets[a];
+    int64_t c0;
+    pipe_chunk(A.offsets[a + 1] - s0, G, rank, c0, nb);
+    const int64_t cap = A.lds_cap[i];
+    const float *lf = reinterpret_cast<const float *>(s_dyn + A.lds_off[i]);
+    const int nf = PH == 0 ? 3 : (A.bkind[a] == AG_BIDDER_DOUBLY_ROBUST ? 6 : 2);
+    const DrRecords R{A.R0.ctr + s0, A.R0.value + s0, A.R0.gamma + s0, A.R0.prop + s0, A.R0.util + s0, A.R0.won + s0};
+    return RecView{R, A.eu_ws + s0, c0, lf, reinterpret_cast<const uint8_t *>(lf + (size_t)nf * cap), cap};
+  };
+  auto tr_of = [&](int a, const FitSt &st) -> float * {
+    if (!A.traces || rank != 0 || st.fit < kFitWr) return nullptr;
+    return A.traces + ((size_t)a * 3 + (st.fit == kFitWr ? 0 : (st.fit == kFitInit ? 1 : 2))) * kDrEpochs;
+  };
+  auto step = [&](int i, const int64_t *tot) {
+    const int a = A.agents[i];
+    fit_step(fst[i], tot, (double)A.n_total[a], A.bkind[a], A.bmode[a], A.initialised[a], A.adam_tab, s_grad, &s_loss,
+             &s_np, tr_of(a, fst[i]));
+  };
+  // the next epoch of slot i: estimated utilities when its fit reaches them, then its partial
+  // sums started up its tree; false when it has no epoch left in this phase (or waits for noise)
+  auto begin = [&](int i, bool &root) -> bool {
+    FitSt &st = fst[i];
+    const int a = A.agents[i], bk = A.bkind[a];
+    int64_t nb;
+    const RecView V = view(i, nb);
+    if (PH == 1 && st.fit == kFitEu) {
+      // src/Bidder.py:541-546 with the fitted win-rate model (k_bidder_epoch's arithmetic);
+      // each_record's thread mapping, so a thread reads back what it wrote
+      double *eu = A.eu_ws + A.offsets[a];
+      float *lfe = const_cast<float *>(V.lf) + (size_t)kFEu * V.cap;
+      for (int64_t j = tid; j < nb; j += kDrThreads) {
+        const int64_t r = V.c0 + j;
+        const double c = (double)(float)V.R.ctr[r], v = (double)(float)V.R.value[r], g = (double)(float)V.R.gamma[r];
+        const double z = c * (double)st.wr[0] + v * (double)st.wr[1] + g * (double)st.wr[2] + (double)st.wr[3];
+        const float W = (float)(1.0 / (1.0 + agexp::exp(-z, S.tab)));
+        const double Vv = V.R.ctr[r] * V.R.value[r], P = V.R.ctr[r] * V.R.value[r] * V.R.gamma[r];
+        eu[r] = (double)W * (Vv - P);
+        if (j < V.cap) lfe[j] = (float)eu[r];
+      }
+      __syncthreads();
+      if (tid == 0) fit_after(st, bk, A.bmode[a], A.initialised[a]);
+      __syncthreads();
+    }
+    if (!pipe_in_phase<PH>(st.fit) || st.fit == kFitEu) return false;
+    const bool wait = PH == 1 && st.fit == kFitPol && A.noise &&
+                      (st.epoch < A.noise_e0 || st.epoch >= A.noise_e0 + A.noise_epochs);
+    __syncthreads();
+    if (tid == 0) st.need_noise = wait ? 1 : 0;
+    __syncthreads();
+    if (wait) return false;
+    const int64_t stride = A.noise_stride ? A.noise_stride : A.n_total[a];
+    const FitNoise F{A.noise ? A.noise + (A.noise_off ? A.noise_off[a] : 0) - (int64_t)A.noise_e0 * stride : nullptr,
+                     stride, A.noise_seed, (uint32_t)a, 1 << 30};
+    const int W = pipe_partial<PH>(st, V, nb, bk, F, S);
+    root = agcoop::agent_allreduce_start(A.bars + (size_t)i * A.lines * kBarLineWords, A.acc + (size_t)i * A.lines * 32,
+                                         32, rank, G, S.tot, W, &s_gen[i], &S.flag);
+    return true;
+  };
+  // totals left by ag_bidder_rp_epoch launches
+  for (int i = 0; i < NA; ++i)
+    if (fst[i].have_tot && fst[i].fit != kFitDone) step(i, A.tot_in + (size_t)A.agents[i] * 32);
+  uint32_t pend = 0, roots = 0;
+  for (int i = 0; i < NA; ++i) {
+    bool root = false;
+    if (begin(i, root)) pend |= 1u << i;
+    if (root) roots |= 1u << i;
+  }
+  while (pend) {
+    for (int i = 0; i < NA; ++i) {
+      if (!(pend >> i & 1)) continue;
+      const int W = fst[i].fit == kFitWins ? 2 : (fst[i].fit == kFitWr ? 10 : 32);
+      agcoop::agent_allreduce_finish(A.bars + (size_t)i * A.lines * kBarLineWords, A.acc + (size_t)i * A.lines * 32, G,
+                                     roots >> i & 1, &s_gen[i], W, S.tot);
+      step(i, S.tot);
+      bool root = false;
+      pend &= ~(1u << i);
+      roots &= ~(1u << i);
+      if (begin(i, root)) pend |= 1u << i;
+      if (root) roots |= 1u << i;
+    }
+  }
+  __syncthreads();
+  if (rank == 0)
+    for (int i = tid; i < NA; i += kDrThreads) {
+      FitSt f = fst[i];
+      f.have_tot = 0;
+      A.st[A.agents[i]] = f;
+    }
+}
+
 // the learners' FitSt at the start of a resumable update (state16: win-rate model, policy)
 __global__ void k_rp_init(int N, const int32_t *__restrict__ bkind, const int32_t *__restrict__ bmode,
                           const int32_t *__restrict__ mask, const float *__restrict__ state, FitSt *__restrict__ st) {
@@ -1185,7 +1628,142 @@ void ag_dr_release(ag_ctx *c) {
   (void)hipFree(w.rp.st);
   (void)hipFree(w.rp.acc);
   (void)hipFree(w.rp.tables);
+  (void)hipFree(w.rp.pipe);
+  (void)hipFree(w.rp.pipe_st);
   w = ag_dr_ws();
+}
+
+// The sorted record arrays of the workspace (sort_records' layout) for n records
+static DrRecords sorted_view(ag_dr_ws &w, int64_t n, double **eu) {
+  const int64_t cap = n > 0 ? n : 1;
+  double *b = (double *)w.buf;
+  *eu = b + 5 * cap;
+  return DrRecords{b, b + cap, b + 2 * cap, b + 3 * cap, b + 4 * cap,
+                   (const uint8_t *)((uint32_t *)((uint64_t *)(b + 6 * cap) + 2 * cap) + 2 * cap)};
+}
+
+// k_bidder_pipe's record-cache budgets (dynamic LDS per workgroup: 4 / 2 per CU) and the
+// records per workgroup it aims at (AG_PIPE_RECS overrides, for tuning): fewer workgroups for
+// small learners -- a shorter tree to climb each epoch -- and the whole resident grid for
+// large ones
+constexpr size_t kPipeLds[2] = {32 * 1024, 72 * 1024};
+constexpr int64_t kPipeRecs = 512;
+
+struct PipeNoise {
+  const float *noise = nullptr;
+  const int64_t *noise_off = nullptr;
+  int64_t stride = 0;
+  int32_t e0 = 0, epochs = 0;
+};
+
+// Runs the learners `slots` (agent indices; FitSt in d_st) through k_bidder_pipe's phases
+// `phases` (bit p: phase p), one cooperative launch each.
+static int pipe_run(ag_ctx *c, const std::vector<int32_t> &slots, const std::vector<int64_t> &cnt, const DrRecords &R,
+                    double *eu, const int64_t *d_off, const int64_t *d_ntot, FitSt *d_st, const int64_t *tot_in,
+                    const PipeNoise &nz, float *traces, int phases, hipStream_t st) {
+  ag_dr_ws &w = c->dr;
+  ag_dr_rp &rp = w.rp;
+  const int NA = (int)slots.size();
+  if (NA == 0) return AG_OK;
+  if (NA > kPipeMaxAgents) return ag_set_error(AG_ERR_UNSUPPORTED, "k_bidder_pipe: > %d learners", kPipeMaxAgents);
+  int64_t recs = 0;
+  for (int a : slots) recs += cnt[a];
+  int64_t want_recs = kPipeRecs;
+  if (const char *e = getenv("AG_PIPE_RECS")) want_recs = std::max<int64_t>(1, atoll(e));
+  for (int ph = 0; ph < 2; ++ph)
+    if (!rp.pipe_blocks[ph]) {
+      const void *fn = ph == 0 ? (const void *)k_bidder_pipe<0> : (const void *)k_bidder_pipe<1>;
+      int per_cu = 0, cus = 0;
+      AG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPipeLds[ph]));
+      AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kDrThreads, kPipeLds[ph]));
+      AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+      rp.pipe_blocks[ph] = std::max(1, per_cu * cus);
+    }
+  // device tables, sized once for the largest grid: [3][kPipeMaxAgents] i32 per phase, then
+  // per phase the acc rows [kPipeMaxAgents][lines][32] i64 and barrier lines (the two
+  // launches of a run never share a word)
+  const size_t lines_max = (size_t)std::max(1, bar_lines(std::max(rp.pipe_blocks[0], rp.pipe_blocks[1])));
+  const size_t rows_max = (size_t)kPipeMaxAgents * lines_max * 32;
+  const size_t per_ph = 3 * kPipeMaxAgents * sizeof(int32_t) + rows_max * (sizeof(int64_t) + sizeof(unsigned)) + 64;
+  if (2 * per_ph > rp.pipe_bytes) {
+    (void)hipFree(rp.pipe);  // (synchronises: no launch of an earlier run uses it any more)
+    rp.pipe = nullptr;
+    rp.pipe_bytes = 0;
+    AG_HIP(hipMalloc(&rp.pipe, 2 * per_ph));
+    rp.pipe_bytes = 2 * per_ph;
+  }
+  for (int ph = 0; ph < 2; ++ph) {
+    if (!(phases >> ph & 1)) continue;
+    const void *fn = ph == 0 ? (const void *)k_bidder_pipe<0> : (const void *)k_bidder_pipe<1>;
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(rp.pipe_blocks[ph], (recs + want_recs - 1) / want_recs));
+    const int lines = std::max(1, bar_lines(G));
+    // record caches after the FitSt copies: slot i caches min(chunk, share) records
+    const size_t fst_bytes = ((size_t)NA * sizeof(FitSt) + 15) / 16 * 16;
+    const size_t budget = kPipeLds[ph] - fst_bytes;
+    std::vector<int64_t> chunk(NA), bytes(NA);
+    double total = 0.0;
+    for (int i = 0; i < NA; ++i) {
+      const int bk = c->h_bkind[slots[i]];
+      chunk[i] = (cnt[slots[i]] + G - 1) / G;
+      bytes[i] = ph == 0 ? 13 : (bk == AG_BIDDER_DOUBLY_ROBUST ? 24 : 8);
+      total += (double)(chunk[i] * bytes[i] + 16);
+    }
+    const double f = total > (double)budget ? (double)budget / total : 1.0;
+    std::vector<int32_t> tab(3 * kPipeMaxAgents, 0);
+    size_t off = fst_bytes;
+    for (int i = 0; i < NA; ++i) {
+      const int64_t cap = std::min<int64_t>(chunk[i], (int64_t)((double)chunk[i] * f));
+      tab[i] = slots[i];
+      tab[kPipeMaxAgents + i] = (int32_t)off;
+      tab[2 * kPipeMaxAgents + i] = (int32_t)cap;
+      off += ((size_t)cap * bytes[i] + 15) / 16 * 16;
+    }
+    if (off > kPipeLds[ph])
+      return ag_set_error(AG_ERR_UNSUPPORTED, "k_bidder_pipe: record cache plan %zu > %zu", off, kPipeLds[ph]);
+    int32_t *d_tab = (int32_t *)((char *)rp.pipe + ph * per_ph);
+    int64_t *d_acc = (int64_t *)(((uintptr_t)(d_tab + 3 * kPipeMaxAgents) + 15) & ~(uintptr_t)15);
+    const size_t rows = (size_t)NA * lines * 32;
+    unsigned *d_bar = (unsigned *)(d_acc + rows);
+    AG_HIP(hipMemcpyAsync(d_tab, tab.data(), sizeof(int32_t) * tab.size(), hipMemcpyHostToDevice, st));
+    AG_HIP(hipMemsetAsync(d_acc, 0, rows * (sizeof(int64_t) + sizeof(unsigned)), st));
+    PipeArgs A;
+    A.NA = NA;
+    A.agents = d_tab;
+    A.bkind = c->d_bkind;
+    A.bmode = w.mode;
+    A.initialised = w.init;
+    A.offsets = d_off;
+    A.n_total = d_ntot;
+    A.R0 = R;
+    A.eu_ws = eu;
+    A.st = d_st;
+    A.tot_in = tot_in;
+    A.acc = d_acc;
+    A.bars = d_bar;
+    A.lines = lines;
+    A.lds_off = d_tab + kPipeMaxAgents;
+    A.lds_cap = d_tab + 2 * kPipeMaxAgents;
+    A.noise = nz.noise;
+    A.noise_off = nz.noise_off;
+    A.noise_stride = nz.stride;
+    A.noise_e0 = nz.e0;
+    A.noise_epochs = nz.epochs;
+    A.noise_seed = c->fit_noise_seed;
+    A.adam_tab = w.adam_tab;
+    A.traces = traces;
+    void *args[] = {&A};
+    AG_HIP(hipLaunchCooperativeKernel(fn, dim3(G), dim3(kDrThreads), args, kPipeLds[ph], st));
+  }
+  return AG_OK;
+}
+
+// FitSt [N] then a mask [N] for ag_bidder_update's pipe run (its own buffer: pipe_run may
+// reallocate the tables)
+static FitSt *pipe_fitst(ag_ctx *c) {
+  ag_dr_rp &rp = c->dr.rp;
+  const size_t N = (size_t)c->shape.num_agents;
+  if (!rp.pipe_st && hipMalloc(&rp.pipe_st, (sizeof(FitSt) + sizeof(int32_t)) * N) != hipSuccess) return nullptr;
+  return (FitSt *)rp.pipe_st;
 }
 
 // which agents bid from a fitted policy / a win-rate search (ag_simulate checks its inputs)
@@ -1373,10 +1951,28 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agen
   // workgroup; a PolicyLearningBidder (fixed-order float sums: its result follows the split)
   // keeps one workgroup per kBidderChunk records. Both phases use the same rule with their
   // own grid.
+  // The exact-sum learners (ValueLearning, DoublyRobust) train in k_bidder_pipe (all of them
+  // in the same persistent launches, their epochs' cross-workgroup sums overlapped with each
+  // other's work) unless there are more than kPipeMaxAgents of them, a fixed block split is
+  // asked for (AG_OPT_BIDDER_BLOCK_SAMPLES) or AG_BIDDER_PIPE=0 (A/B); the rest in
+  // k_bidder_train
+  std::vector<int32_t> pipe_slots, pipe_mask(N, 0);
+  {
+    const char *e = getenv("AG_BIDDER_PIPE");
+    const bool off = (e && e[0] == '0') || c->bidder_chunk > 0;
+    for (int a = 0; a < N && !off; ++a) {
+      const int bk = c->h_bkind[a];
+      // (a learner without logs takes k_bidder_train's no-logs path: fallback or error)
+      if ((bk == AG_BIDDER_VALUE_LEARNING || bk == AG_BIDDER_DOUBLY_ROBUST) && !(agents && !agents[a]) && cnt[a] > 0)
+        pipe_slots.push_back(a);
+    }
+    if ((int)pipe_slots.size() > kPipeMaxAgents) pipe_slots.clear();
+    for (int a : pipe_slots) pipe_mask[a] = 1;
+  }
   auto is_learner = [&](int a) {
     const int bk = c->h_bkind[a];
     return (bk == AG_BIDDER_VALUE_LEARNING || bk == AG_BIDDER_POLICY_LEARNING || bk == AG_BIDDER_DOUBLY_ROBUST) &&
-           !(agents && !agents[a]);
+           !(agents && !agents[a]) && !pipe_mask[a];
   };
   struct Plan {
     const void *fn = nullptr;
@@ -1500,11 +2096,50 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agen
       AG_HIP(hipLaunchKernel(P.fn, dim3(P.G), dim3(kDrThreads), args, P.dyn, st));
     return AG_OK;
   };
+  FitSt *pst = nullptr;
+  if (!pipe_slots.empty()) {
+    pst = pipe_fitst(c);
+    if (!pst) return ag_set_error(AG_ERR_HIP, "ag_bidder_update: FitSt allocation failed");
+    int32_t *d_pmask = (int32_t *)(pst + N);
+    AG_HIP(hipMemcpyAsync(d_pmask, pipe_mask.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_rp_init, dim3((N + 255) / 256), dim3(256), 0, st, N, c->d_bkind, w.mode, d_pmask, w.state,
+                       pst);
+    AG_HIP(hipGetLastError());
+    // n_total = the counts (w.counts [N]); noise: agent a's draws of epoch e at noise_offsets[a] + e n_a
+    PipeNoise nz;
+    nz.noise = noise;
+    nz.noise_off = d_noff;
+    nz.stride = 0;
+    nz.e0 = 0;
+    nz.epochs = noise_epochs;
+    const DrRecords R{b_ctr, b_val, b_gam, b_prop, b_util, b_won};
+    if (int rc = pipe_run(c, pipe_slots, cnt, R, b_eu, d_off, w.counts, pst, nullptr, nz, traces, 3, st)) return rc;
+  }
   if (int rc = launch(P0)) return rc;
   if (int rc = launch(P1)) return rc;
   std::vector<int32_t> h(4 * (size_t)N);
   AG_HIP(hipMemcpyAsync(h.data(), d_epochs, sizeof(int32_t) * 4 * N, hipMemcpyDeviceToHost, st));
   AG_HIP(hipStreamSynchronize(st));
+  if (pst) {  // the pipe's learners: epochs, status and (unless out of noise) their models
+    std::vector<FitSt> fs(N);
+    std::vector<float> state(16 * (size_t)N);
+    AG_HIP(hipMemcpy(fs.data(), pst, sizeof(FitSt) * N, hipMemcpyDeviceToHost));
+    AG_HIP(hipMemcpy(state.data(), w.state, sizeof(float) * 16 * N, hipMemcpyDeviceToHost));
+    for (int a : pipe_slots) {
+      const FitSt &f = fs[a];
+      for (int j = 0; j < 3; ++j) h[3 * a + j] = f.ep[j];
+      int stt = f.status;
+      if (f.fit != kFitDone) {  // waits for noise epochs past noise_epochs: not applied
+        stt = -3;
+        h[3 * a + 2] = f.epoch;
+      } else if (stt != 1) {
+        for (int j = 0; j < 4; ++j) state[16 * (size_t)a + j] = f.wr[j];
+        for (int j = 0; j < 12; ++j) state[16 * (size_t)a + 4 + j] = f.pol[j];
+      }
+      h[3 * (size_t)N + a] = stt;
+    }
+    AG_HIP(hipMemcpy(w.state, state.data(), sizeof(float) * 16 * N, hipMemcpyHostToDevice));
+  }
   if (epochs) memcpy(epochs, h.data(), sizeof(int32_t) * 3 * N);
   if (status) memcpy(status, h.data() + 3 * (size_t)N, sizeof(int32_t) * N);
   static const char *names[] = {"", "", "ValueLearningBidder", "PolicyLearningBidder", "DoublyRobustBidder"};
@@ -1641,9 +2276,67 @@ int ag_bidder_rp_begin(ag_ctx *c, const ag_shading_samples *s, const int32_t *ag
   rp.noise_n = 0;
   rp.noise_e0 = rp.noise_epochs = 0;
   rp.n_local = SR.n;
+  rp.single = true;
+  for (int a = 0; a < N; ++a)
+    if (mask[a] && (nt[a] != cnt[a] || nt[N + a] != 0)) rp.single = false;
   rp.active = true;
   (void)mode;
   return AG_OK;
+}
+
+// The rest of a one-rank resumable update in persistent launches (k_bidder_pipe): every
+// learner under training runs until it is done or waits for the next noise window
+// (ag_bidder_rp_noise) -- ag_bidder_rp_poll tells which; ag_bidder_rp_end applies the result.
+// The launches read and write the same FitSt as ag_bidder_rp_epoch (which it may follow or
+// precede), so the two mix freely.
+int ag_bidder_rp_run(ag_ctx *c, float *traces, void *stream) {
+  if (!c || !c->dr.rp.active) return ag_set_error(AG_ERR_STATE, "ag_bidder_rp_run: no ag_bidder_rp_begin");
+  ag_dr_ws &w = c->dr;
+  ag_dr_rp &rp = w.rp;
+  if (!rp.single)
+    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_bidder_rp_run: this rank holds part of the learners' records "
+                        "(records_total / records_base): the ranks' sums meet per epoch, ag_bidder_rp_epoch");
+  AgDeviceGuard g(c->device);
+  const int N = c->shape.num_agents;
+  hipStream_t st = (hipStream_t)stream;
+  std::vector<int32_t> mask(N);
+  std::vector<int64_t> cnt(N + 1);
+  std::vector<FitSt> h(N);
+  FitSt *S = (FitSt *)rp.st + (size_t)(rp.k & 1) * N;
+  AG_HIP(hipMemcpyAsync(mask.data(), rp.mask, sizeof(int32_t) * N, hipMemcpyDeviceToHost, st));
+  AG_HIP(hipMemcpyAsync(cnt.data(), w.counts + N, sizeof(int64_t) * (N + 1), hipMemcpyDeviceToHost, st));
+  AG_HIP(hipMemcpyAsync(h.data(), S, sizeof(FitSt) * N, hipMemcpyDeviceToHost, st));
+  AG_HIP(hipStreamSynchronize(st));
+  std::vector<int32_t> slots;
+  std::vector<int64_t> n(N, 0);
+  bool ph0 = false;
+  for (int a = 0; a < N; ++a) {
+    n[a] = cnt[a + 1] - cnt[a];
+    if (mask[a] && h[a].fit != kFitDone) {
+      slots.push_back(a);
+      ph0 |= h[a].fit == kFitWins || h[a].fit == kFitWr;
+    }
+  }
+  if (slots.empty()) return AG_OK;
+  if ((int)slots.size() > kPipeMaxAgents) {  // per-epoch launches, polled, until done or waiting
+    std::vector<int32_t> fit(N), ep(N), need(N);
+    for (;;) {
+      if (int rc = ag_bidder_rp_epoch(c, 64, nullptr, traces, stream)) return rc;
+      if (int rc = ag_bidder_rp_poll(c, fit.data(), ep.data(), need.data(), stream)) return rc;
+      bool busy = false;
+      for (int a = 0; a < N; ++a) busy |= mask[a] && fit[a] >= 0 && need[a] < 0;
+      if (!busy) return AG_OK;
+    }
+  }
+  double *eu = nullptr;
+  const DrRecords R = sorted_view(w, rp.n_local, &eu);
+  PipeNoise nz;
+  nz.noise = rp.noise;
+  nz.stride = rp.noise_n;
+  nz.e0 = rp.noise_e0;
+  nz.epochs = rp.noise_epochs;
+  return pipe_run(c, slots, n, R, eu, w.counts + N, rp.ntot, S, rp.totals + (size_t)((rp.k + 1) & 1) * 32 * N, nz,
+                  traces, ph0 ? 3 : 2, st);
 }
 
 int ag_bidder_rp_noise(ag_ctx *c, const float *noise, int64_t noise_n, int32_t first_epoch, int32_t epochs) {

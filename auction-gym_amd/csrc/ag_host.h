@@ -78,6 +78,13 @@ struct ag_dr_rp {
   int32_t noise_e0 = 0, noise_epochs = 0;
   int32_t *mask = nullptr;      // [N] the agents under training (host copy in `agents`)
   int64_t n_local = 0;
+  bool single = false;          // this rank holds every record (ag_bidder_rp_run allowed)
+  // k_bidder_pipe (ag_bidder_rp_run, ag_bidder_update): slot tables, tree rows / barrier
+  // lines, its own FitSt [N] for ag_bidder_update
+  void *pipe = nullptr;
+  size_t pipe_bytes = 0;
+  void *pipe_st = nullptr;      // FitSt [N] of ag_bidder_update's pipe run
+  int pipe_blocks[2] = {0, 0};  // co-resident workgroups per phase
 };
 
 // DoublyRobustBidder workspace (ag_dr.hip)

@@ -561,6 +561,12 @@ int ag_bidder_rp_begin(ag_ctx *ctx, const ag_shading_samples *samples, const int
  * NULL) = the last launch's index: its rank totals are at totals + 32 N (launch_index & 1).
  * traces: dev float32 [N][3][32768] per-epoch losses (the rank holding global record 0), or NULL. */
 int ag_bidder_rp_epoch(ag_ctx *ctx, int32_t launches, int64_t *launch_index, float *traces, void *stream);
+/* One process holding every record (records_total / records_base NULL): the rest of the update
+ * in persistent launches (every learner under training together, each one's per-epoch sum
+ * overlapped with the others' epochs) until every learner is done or waits for noise
+ * (ag_bidder_rp_poll tells which); the same state ag_bidder_rp_epoch steps, bit for bit, so the
+ * two mix. Stream-ordered; AG_ERR_UNSUPPORTED on a rank holding part of the records. */
+int ag_bidder_rp_run(ag_ctx *ctx, float *traces, void *stream);
 /* The host-drawn rsample window of the noisy policy fits: noise dev float32, policy-fit epoch e
  * of record i (global index) at noise[(e - first_epoch) * noise_n + i], first_epoch <= e <
  * first_epoch + epochs; NULL: synthetic draws (AG_OPT_FIT_NOISE_SEED). */

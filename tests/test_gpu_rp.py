@@ -235,3 +235,112 @@ def test_lrts_rp_equals_persistent_trainer(gpu, shards):
         for x, y in zip(eng.lrts_state(), want):
             assert np.array_equal(x, y)
         eng.close()
+
+
+# ---- the pipelined persistent launches (k_bidder_pipe: ag_bidder_update's exact-sum
+# learners, ag_bidder_rp_run) ----
+def _trained(eng):
+    state, init = eng.dr_state()
+    return state, init
+
+
+@pytest.mark.parametrize("host_noise", [False, True], ids=["synthetic", "host_noise"])
+def test_pipe_equals_persistent_trainer(gpu, monkeypatch, host_noise):
+    """ag_bidder_update's pipelined launches (every ValueLearning / DoublyRobust learner in the
+    same persistent launches, each one's per-epoch sum overlapped with the others' epochs)
+    against k_bidder_train (AG_BIDDER_PIPE=0): epochs, status and models bit for bit -- DM and
+    DR learners (DR imitating on its first update) trained together, a PPO PolicyLearningBidder
+    beside them (k_bidder_train either way). host_noise: the caller's draws with 600 policy
+    epochs, too few for some fits (status -3, model not applied, in both)."""
+    import torch
+    specs = SPECS + [("ips", "ips_update_kat.npz", 0)]
+    bk, modes, state0, recs, _ = _kat_learners(specs)
+    N = len(specs)
+    E = 600 if host_noise else 0
+    ns = [len(r) for r in recs["agent"]]
+    noff = np.concatenate([[0], np.cumsum([n * E for n in ns])[:-1]]).astype(np.int64)
+    z = np.random.default_rng(3).standard_normal(sum(ns) * E).astype(np.float32) if host_noise else None
+    runs = []
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("AG_BIDDER_PIPE", pipe)
+        eng = _engine(bk, modes, state0)
+        st = _learner_store(eng, recs)
+        noise = torch.from_numpy(z).to(eng.device) if host_noise else None
+        ep, stat = eng.bidder_update(st, noise, noff, E)
+        runs.append((ep, stat) + _trained(eng))
+        eng.close()
+    ep, stat = runs[0][:2]
+    assert (ep[:4, 0] > 0).all()
+    assert np.isin(stat, [0, -3] if host_noise else [0]).all()
+    for x, y in zip(*runs):
+        assert np.array_equal(x, y)
+
+
+def test_rp_run_windows_equal_one_shot(gpu, oracle):
+    """ag_bidder_rp_run fed the rsample noise window by window (it stops at a window's end, the
+    state kept) equals the persistent trainer given every epoch's draws at once, and the
+    oracle: the drop-in update's path (Auction._fit_with_torch_noise)."""
+    import torch
+    specs = [("dr", "dr_update_kat.npz", 0)]
+    bk, modes, state0, recs, data = _kat_learners(specs)
+    k = data[0]
+    n = len(k("est_ctr"))
+    E = 6000
+    z = _dr_noise(k("dr_rng_state"), n, E)
+    r = oracle.dr_update(k("est_ctr"), k("value"), k("gamma"), k("propensity"), k("won"), k("util"),
+                         state0[0, :4], state0[0, 4:], False, z)
+    eng = _engine(bk, modes, state0)
+    st = _learner_store(eng, recs)
+    eng.bidder_rp_begin(st, agents=np.ones(1, np.int32))
+    W, w0, waits = 333, 0, 0
+    eng.bidder_rp_noise(torch.from_numpy(z[:W].ravel()).to(eng.device), n, 0, W)
+    while True:
+        eng.bidder_rp_run()
+        fit, epoch, need = eng.bidder_rp_poll()
+        if fit[0] < 0:
+            break
+        assert need[0] == w0 + W and fit[0] == 4
+        w0 = int(need[0])
+        waits += 1
+        eng.bidder_rp_noise(torch.from_numpy(z[w0:w0 + W].ravel()).to(eng.device), n, w0, W)
+    ep, stat = eng.bidder_rp_end()
+    state, _ = eng.dr_state()
+    assert stat[0] == 0 and waits >= ep[0, 2] // W - 1
+    assert list(ep[0]) == list(r["epochs"]) and np.array_equal(state[0, 4:], r["pol"])
+    eng.close()
+
+
+def test_rp_run_after_epoch_launches(gpu, monkeypatch):
+    """Per-epoch launches (ag_bidder_rp_epoch, their last totals pending) then ag_bidder_rp_run
+    to the end: the persistent trainer's epochs, status and models bit for bit."""
+    bk, modes, state0, recs, _ = _kat_learners(SPECS)
+    N = len(SPECS)
+    monkeypatch.setenv("AG_BIDDER_PIPE", "0")
+    ref = _engine(bk, modes, state0)
+    ep, stat = ref.bidder_update(_learner_store(ref, recs), None, np.zeros(N, np.int64), 0)
+    want = (ep, stat) + _trained(ref)
+    ref.close()
+    eng = _engine(bk, modes, state0)
+    st = _learner_store(eng, recs)
+    eng.bidder_rp_begin(st, agents=np.ones(N, np.int32))
+    eng.bidder_rp_epoch(37)
+    eng.bidder_rp_run()
+    fit, _, _ = eng.bidder_rp_poll()
+    assert (fit < 0).all()
+    got = eng.bidder_rp_end() + _trained(eng)
+    for x, y in zip(got, want):
+        assert np.array_equal(x, y)
+    eng.close()
+
+
+def test_rp_run_refuses_a_shard(gpu):
+    """A rank holding part of the records steps per epoch with the other ranks: rp_run refuses."""
+    bk, modes, state0, recs, _ = _kat_learners(SPECS[:1])
+    eng = _engine(bk, modes, state0)
+    st = _learner_store(eng, recs)
+    n = len(recs["agent"][0])
+    eng.bidder_rp_begin(st, agents=np.ones(1, np.int32), records_total=np.array([2 * n]),
+                        records_base=np.array([0]))
+    with pytest.raises(NotImplementedError, match="ag_bidder_rp_epoch"):
+        eng.bidder_rp_run()
+    eng.close()

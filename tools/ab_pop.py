@@ -6,7 +6,8 @@ interleaved in ONE process; outputs and counters checked equal across builds.
     python tools/ab_pop.py configs_4 early [more variants...]
     AG_AB_DENSE=1: the dense Thompson-noise layout instead of the compact one.
     A variant named "generic" is the base library with AG_SIM_KERNEL_GENERIC (k_simulate
-    instead of the dedicated kernels); "bt256" / "bt1024" force the workgroup size.
+    instead of the dedicated kernels), "<variant>+generic" that variant with it; "bt256" /
+    "bt1024" force the workgroup size.
 """
 import os
 import sys
@@ -31,8 +32,9 @@ def main():
     vdir = os.path.join(ROOT, "auction-gym_amd", "build", "variants")
     paths = {"base": _lib.LIB_PATH}
     special = {"generic", "fused", "split", "wide", "bt256", "bt1024", "nocnt", "noship"}
-    for n in sys.argv[2:]:
-        paths[n] = _lib.LIB_PATH if n in special else os.path.join(vdir, f"libauctiongym_hip_{n}.so")
+    for n in sys.argv[2:]:  # "<variant>+generic": that build with k_simulate forced
+        v = n[:-len("+generic")] if n.endswith("+generic") else n
+        paths[n] = _lib.LIB_PATH if v in special else os.path.join(vdir, f"libauctiongym_hip_{v}.so")
     base_path = _lib.LIB_PATH
     runs = {}
     for n, p in paths.items():
@@ -56,6 +58,8 @@ def main():
             eng.set_dr_state(st16, np.where(bk >= 2, 1, 0).astype(np.int32))
         if n in ("generic", "fused", "split", "wide"):
             eng.set_simulate_kernel(True if n == "generic" else n)
+        elif n.endswith("+generic"):
+            eng.set_simulate_kernel(True)
         if n == "noship":  # k_simulate's runtime-shape build
             eng._check(eng.L.ag_set_option(eng._h, _lib.OPT_SIM_SHIPPED_SHAPE, 0), "ag_set_option")
         if n in ("bt256", "bt1024"):

@@ -10,7 +10,13 @@ for s in ${STEPS:-smoke configs suite bench}; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     configs) step pytest_configs 600 python -u -m pytest tests/test_00_configs_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
-    rp) step pytest_rp 900 python -u -m pytest tests/test_gpu_rp.py tests/test_gpu_parity.py tests/test_gpu_distributed.py -m gpu -v --timeout 300 --timeout-method thread -k "rp_ or driver_ or dropin_ or record_parallel or interleaved or memory or empirical or lrts" ;;
+    rp) step pytest_rp 900 python -u -m pytest tests/test_gpu_rp.py tests/test_gpu_parity.py tests/test_gpu_distributed.py -m gpu -v --timeout 300 --timeout-method thread -k "rp_ or pipe or driver_ or dropin_ or record_parallel or interleaved or memory or empirical or lrts" ;;
+    upd)
+      U="python bench.py --steps 5 --warmup 2 --no-ts --no-p8 --no-generate --no-cpu-baseline --populations configs_2,configs_3,configs_4"
+      step upd_train 600 env AG_BIDDER_PIPE=0 $U &&
+      step upd_pipe 600 $U &&
+      step upd_pipe128 600 env AG_PIPE_RECS=128 $U &&
+      step upd_pipe2048 600 env AG_PIPE_RECS=2048 $U ;;
     dropin) step dropin_dr 600 python tools/dropin_update_time.py dr 2 && step dropin_dm 600 python tools/dropin_update_time.py dm 2 ;;
     suite) step pytest_gpu 1200 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
     bench) step bench_driver 400 python bench.py --steps 20 --warmup 5 ;;
