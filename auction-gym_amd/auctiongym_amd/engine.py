@@ -202,11 +202,8 @@ class AuctionEngine:
     def set_simulate_kernel(self, generic):
         """generic=True: always the general simulate kernel (k_simulate); False (default):
         k_oracle for OracleAllocator + TruthfulBidder populations, k_simulate for the others;
-        "fused": k_pop (general populations of the shipped shape) making its Thompson choices
-        itself; "split": k_ts_choice then k_pop; "wide": the runtime-P kernel at any P.
-        Identical results."""
-        mode = {"fused": _lib.SIM_KERNEL_FUSED, "split": _lib.SIM_KERNEL_SPLIT,
-                "wide": _lib.SIM_KERNEL_WIDE}.get(generic) or (
+        "wide": the runtime-P kernel at any P (A/B variant builds only). Identical results."""
+        mode = {"wide": _lib.SIM_KERNEL_WIDE}.get(generic) or (
             _lib.SIM_KERNEL_GENERIC if generic else _lib.SIM_KERNEL_AUTO)
         self._check(self.L.ag_set_option(self._h, _lib.OPT_SIMULATE_KERNEL, mode), "ag_set_option")
 

@@ -21,10 +21,10 @@ namespace agcoop {
 // stay off the counters' lines). Lines: [0] generation, then level 0's ceil(nblk / F)
 // nodes, level 1's, ...
 constexpr int kBarFanIn = AG_BAR_FANIN, kBarLineWords = 32;
-__host__ __device__ inline int bar_lines(int nblk) {
+__host__ __device__ inline int bar_lines(int nblk, int F = kBarFanIn) {
   if (nblk <= 1) return 0;
   int lines = 1;
-  for (int m = nblk; m > 1; m = (m + kBarFanIn - 1) / kBarFanIn) lines += (m + kBarFanIn - 1) / kBarFanIn;
+  for (int m = nblk; m > 1; m = (m + F - 1) / F) lines += (m + F - 1) / F;
   return lines;
 }
 
@@ -69,83 +69,6 @@ __device__ __forceinline__ void agent_barrier(unsigned *bar, int rank, int nblk)
   __syncthreads();
 }
 
-// Exact int64 all-reduce of W words over the workgroups of one agent, summed up the same
-// combining tree with integer atomics (exact in any order), every workgroup taking part:
-//  - each workgroup adds its words (LDS vals [W]) to its level-0 node's accumulator row;
-//  - the last arriver at a node (decided by thread 0, broadcast through LDS) moves the node's
-//    row into its parent's with all its threads, zeroing the node row, and arrives one level
-//    up; the root's last arriver writes the totals to row 0 and bumps the generation;
-//  - everyone then reads row 0 into LDS tot [W].
-// acc: the agent's rows [bar_lines(nblk)][stride] int64 (stride >= W), zero on entry and --
-// row 0 aside -- zero again on return, so the next call needs no clearing. Instead of every
-// workgroup reading every other workgroup's partials (nblk lines from other XCDs each), a
-// workgroup reads one row. Call with every thread; nblk <= 1 copies vals to tot.
-__device__ __forceinline__ void agent_allreduce_i64(unsigned *bar, int64_t *acc, int stride, int rank, int nblk,
-                                                    const int64_t *vals, int W, int64_t *tot, int *s_flag) {
-  const int t = threadIdx.x, nt = blockDim.x;
-  __syncthreads();
-  if (nblk <= 1) {
-    for (int j = t; j < W; j += nt) tot[j] = vals[j];
-    __syncthreads();
-    return;
-  }
-  for (int j = t; j < W; j += nt)
-    __hip_atomic_fetch_add(acc + (size_t)(1 + rank / kBarFanIn) * stride + j, vals[j], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-  unsigned *gen = bar;
-  unsigned g = 0;
-  if (t == 0) g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  int idx = rank, members_prev = nblk, base = 1;
-  bool root = false;
-  for (;;) {
-    const int nodes = (members_prev + kBarFanIn - 1) / kBarFanIn, q = idx / kBarFanIn;
-    const int members = members_prev - q * kBarFanIn < kBarFanIn ? members_prev - q * kBarFanIn : kBarFanIn;
-    __syncthreads();  // this workgroup's additions to the node are issued before it arrives
-    if (t == 0) {
-      unsigned *cnt = bar + (size_t)(base + q) * kBarLineWords;
-      const bool last =
-          __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)members - 1;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      *s_flag = last;
-    }
-    __syncthreads();
-    if (!*s_flag) break;
-    int64_t *node = acc + (size_t)(base + q) * stride;
-    int64_t *dst = nodes == 1 ? acc : acc + (size_t)(base + nodes + q / kBarFanIn) * stride;
-    for (int j = t; j < W; j += nt) {
-      const int64_t v = __hip_atomic_load(node + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(node + j, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (nodes == 1)
-        __hip_atomic_store(dst + j, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        __hip_atomic_fetch_add(dst + j, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (nodes == 1) {
-      root = true;
-      break;
-    }
-    base += nodes;
-    idx = q;
-    members_prev = nodes;
-  }
-  __syncthreads();  // the root's totals are stored before the generation moves
-  if (t == 0) {
-    if (root) {
-      __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g)
-        __builtin_amdgcn_s_sleep(AG_BAR_SLEEP);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-  }
-  __syncthreads();
-  for (int j = t; j < W; j += nt) tot[j] = __hip_atomic_load(acc + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-}
-
 // agent_allreduce_i64 split in two so that a workgroup computes something else while the sum
 // climbs the tree (ag_dr.hip k_bidder_pipe: the next learner's epoch): _start adds the
 // workgroup's W words (LDS vals) up the tree -- the root's last arriver stores the totals to
@@ -156,37 +79,46 @@ __device__ __forceinline__ void agent_allreduce_i64(unsigned *bar, int64_t *acc,
 // on one region the calls alternate (a region's next _start follows its _finish). Every
 // workgroup of the region must be resident (cooperative launch). nblk <= 1: vals is the total
 // (tot must then be vals).
+// Fence-free: every word that moves between workgroups is an 8-B agent-scope atomic (add,
+// store, load: sc1, served by L2, never by a stale L1) on both sides, every wave's atomics are
+// complete (s_waitcnt vmcnt(0), then a workgroup barrier) before its workgroup signals, and
+// the wave that polled or arrived last is the one that reads (MI355X_MICROARCH.md, the
+// fence-free hand-off forms): no agent release (an L2 write-back, ~1.7 us) per arrival and no
+// agent acquire (an L1 invalidate, ~6.5 us at 4 workgroups per CU) per read. Nothing else may
+// be handed over through these calls: a caller reading other workgroups' PLAIN stores needs
+// agent_allreduce_i64's fences.
+// F: the tree's fan-in (bar_lines(nblk, F) lines / rows per region).
+#define AG_VMCNT0() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+template <int F = kBarFanIn>
 __device__ __forceinline__ bool agent_allreduce_start(unsigned *bar, int64_t *acc, int stride, int rank, int nblk,
                                                       const int64_t *vals, int W, unsigned *s_gen, int *s_flag) {
   const int t = threadIdx.x, nt = blockDim.x;
   __syncthreads();
   if (nblk <= 1) return true;
   for (int j = t; j < W; j += nt)
-    __hip_atomic_fetch_add(acc + (size_t)(1 + rank / kBarFanIn) * stride + j, vals[j], __ATOMIC_RELAXED,
+    __hip_atomic_fetch_add(acc + (size_t)(1 + rank / F) * stride + j, vals[j], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
   unsigned *gen = bar;
   if (t == 0) *s_gen = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   int idx = rank, members_prev = nblk, base = 1;
   bool root = false;
   for (;;) {
-    const int nodes = (members_prev + kBarFanIn - 1) / kBarFanIn, q = idx / kBarFanIn;
-    const int members = members_prev - q * kBarFanIn < kBarFanIn ? members_prev - q * kBarFanIn : kBarFanIn;
-    __syncthreads();  // this workgroup's additions to the node are issued before it arrives
+    const int nodes = (members_prev + F - 1) / F, q = idx / F;
+    const int members = members_prev - q * F < F ? members_prev - q * F : F;
+    AG_VMCNT0();
+    __syncthreads();  // this workgroup's additions to the node are performed before it arrives
     if (t == 0) {
       unsigned *cnt = bar + (size_t)(base + q) * kBarLineWords;
       const bool last =
-          __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)members - 1;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+          __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)members - 1;
+      if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *s_flag = last;
     }
     __syncthreads();
     if (!*s_flag) break;
     int64_t *node = acc + (size_t)(base + q) * stride;
-    int64_t *dst = nodes == 1 ? acc : acc + (size_t)(base + nodes + q / kBarFanIn) * stride;
-    for (int j = t; j < W; j += nt) {
+    int64_t *dst = nodes == 1 ? acc : acc + (size_t)(base + nodes + q / F) * stride;
+    for (int j = t; j < W; j += nt) {  // (the arriving wave; the others after the barrier above)
       const int64_t v = __hip_atomic_load(node + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(node + j, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (nodes == 1)
@@ -202,8 +134,9 @@ __device__ __forceinline__ bool agent_allreduce_start(unsigned *bar, int64_t *ac
     idx = q;
     members_prev = nodes;
   }
-  __syncthreads();  // the root's totals are stored before the generation moves
-  if (t == 0 && root) __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  AG_VMCNT0();
+  __syncthreads();  // the root's totals (and every zeroed node) are stored before the generation moves
+  if (t == 0 && root) __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return root;
 }
 __device__ __forceinline__ void agent_allreduce_finish(unsigned *bar, const int64_t *acc, int nblk, bool root,
@@ -214,19 +147,44 @@ __device__ __forceinline__ void agent_allreduce_finish(unsigned *bar, const int6
     const unsigned g = *s_gen;
     while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g)
       __builtin_amdgcn_s_sleep(AG_BAR_SLEEP);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
-  for (int j = t; j < W; j += nt)
+  for (int j = t; j < W; j += nt)  // (the polling wave; the others after the barrier above)
     tot[j] = __hip_atomic_load(const_cast<int64_t *>(acc) + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
+}
+
+// Exact int64 all-reduce of W words over the workgroups of one agent, summed up the same
+// combining tree with integer atomics (exact in any order), every workgroup taking part:
+//  - each workgroup adds its words (LDS vals [W]) to its level-0 node's accumulator row;
+//  - the last arriver at a node (decided by thread 0, broadcast through LDS) moves the node's
+//    row into its parent's with all its threads, zeroing the node row, and arrives one level
+//    up; the root's last arriver writes the totals to row 0 and bumps the generation;
+//  - everyone then reads row 0 into LDS tot [W].
+// acc: the agent's rows [bar_lines(nblk)][stride] int64 (stride >= W), zero on entry and --
+// row 0 aside -- zero again on return, so the next call needs no clearing. Instead of every
+// workgroup reading every other workgroup's partials (nblk lines from other XCDs each), a
+// workgroup reads one row. Call with every thread; nblk <= 1 copies vals to tot. Fence-free
+// (agent_allreduce_start / _finish below: 8-B agent atomics both sides), so the caller may
+// hand nothing else over through it.
+__device__ __forceinline__ void agent_allreduce_i64(unsigned *bar, int64_t *acc, int stride, int rank, int nblk,
+                                                    const int64_t *vals, int W, int64_t *tot, int *s_flag) {
+  __shared__ unsigned s_gen;
+  if (nblk <= 1) {
+    __syncthreads();
+    for (int j = threadIdx.x; j < W; j += blockDim.x) tot[j] = vals[j];
+    __syncthreads();
+    return;
+  }
+  const bool root = agent_allreduce_start(bar, acc, stride, rank, nblk, vals, W, &s_gen, s_flag);
+  agent_allreduce_finish(bar, acc, nblk, root, &s_gen, W, tot);
 }
 
 // The same combining-tree sum without the wait (per-epoch launches, ag_dr.hip k_bidder_epoch):
 // each workgroup adds its W words (LDS vals) up the tree and the root's last arriver stores
 // the totals to `out` (a global row read by the NEXT launch: the kernel boundary orders it);
 // nobody spins, so the workgroups need not be co-resident. acc / bar: as agent_allreduce_i64
-// (zero on entry, zero again on return). nblk <= 1 stores vals to out.
+// (zero on entry, zero again on return; fence-free the same way). nblk <= 1 stores vals to out.
 __device__ __forceinline__ void agent_reduce_nowait(unsigned *bar, int64_t *acc, int stride, int rank, int nblk,
                                                     const int64_t *vals, int W, int64_t *out, int *s_flag) {
   const int t = threadIdx.x, nt = blockDim.x;
@@ -242,15 +200,13 @@ __device__ __forceinline__ void agent_reduce_nowait(unsigned *bar, int64_t *acc,
   for (;;) {
     const int nodes = (members_prev + kBarFanIn - 1) / kBarFanIn, q = idx / kBarFanIn;
     const int members = members_prev - q * kBarFanIn < kBarFanIn ? members_prev - q * kBarFanIn : kBarFanIn;
-    __syncthreads();  // this workgroup's additions to the node are issued before it arrives
+    AG_VMCNT0();
+    __syncthreads();  // this workgroup's additions to the node are performed before it arrives
     if (t == 0) {
       unsigned *cnt = bar + (size_t)(base + q) * kBarLineWords;
       const bool last =
-          __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)members - 1;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+          __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)members - 1;
+      if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *s_flag = last;
     }
     __syncthreads();

@@ -13,6 +13,7 @@
 
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <type_traits>
@@ -1136,8 +1137,8 @@ __device__ __forceinline__ int fit_max_epochs(int fit, int bk) {
 
 // step 1 (thread 0 with threads 0..15 for Adam): the learner's state after the epoch whose
 // summed partials are tot (hi, lo pairs); n: the learner's records over all ranks
-__device__ void fit_step(FitSt &st, const int64_t *tot, double n, int bk, int mode, int init, const double *adam_tab,
-                         float *s_grad, float *s_loss, int *s_np, float *tr) {
+__device__ __forceinline__ void fit_step(FitSt &st, const int64_t *tot, double n, int bk, int mode, int init, const double *adam_tab,
+                         float *s_grad, float *s_loss, int *s_np, float *tr, const double *bcp = nullptr) {
   const int tid = threadIdx.x;
   if (tid == 0) {
     *s_np = 0;
@@ -1169,7 +1170,12 @@ __device__ void fit_step(FitSt &st, const int64_t *tot, double n, int bk, int mo
                                                                                                          : (float)1e-6);
   double bc1;
   float bc2f;
-  bias_corrections(e, adam_tab, bc2f, bc1);
+  if (bcp) {  // adam_tab[e], adam_tab[kDrEpochs + e] fetched by the caller
+    bc1 = bcp[0];
+    bc2f = (float)bcp[1];
+  } else {
+    bias_corrections(e, adam_tab, bc2f, bc1);
+  }
   const float neg_step = (float)(-(st.lr / bc1));
   float *par = st.fit == kFitWr ? st.wr : st.pol;
   __syncthreads();
@@ -1329,6 +1335,7 @@ __global__ __launch_bounds__(kDrThreads) void k_bidder_epoch(
 // A policy fit whose host-drawn noise window ends waits with its state kept (need_noise);
 // the launch ends when no learner has an epoch left in its phase.
 constexpr int kPipeMaxAgents = 16;
+constexpr int kPipeFanIn = 32;  // the trees' fan-in: 2 levels up to 1024 workgroups
 struct PipeArgs {
   int NA;                       // learners in the launch (<= kPipeMaxAgents)
   const int32_t *agents;        // [NA] their agent indices
@@ -1351,6 +1358,7 @@ struct PipeArgs {
   uint64_t noise_seed;
   const double *adam_tab;
   float *traces;                // [N][3][kDrEpochs] or NULL
+  long long *prof;              // diagnostics (AG_PIPE_PROF): [G][8] wall-clock ticks per part, or NULL
 };
 
 // this workgroup's slice [c0, c0 + nb) of n records over G workgroups
@@ -1423,32 +1431,54 @@ __device__ __forceinline__ int pipe_partial(const FitSt &st, const RecView &V, i
   }
 }
 
+// a slot's constants, read once into LDS (the rounds read nothing from global memory but the
+// records beyond the cache and the Adam table)
+struct PipeSlot {
+  int64_t s0, c0, nb, cap;  // the learner's first sorted record; this workgroup's slice; cached records
+  double n;                 // records (fit_step's n)
+  uint32_t off;             // record cache: byte offset in the dynamic LDS (not a pointer: kept
+                            // an LDS address, ds_read, not a flat load through a generic pointer)
+  int a, bk, mode, init, nf;
+};
+
 template <int PH>
 __global__ __launch_bounds__(kDrThreads, PH == 0 ? 4 : 2) void k_bidder_pipe(PipeArgs A) {
   __shared__ TrainLds S;
   __shared__ float s_grad[16], s_loss;
   __shared__ int s_np;
   __shared__ unsigned s_gen[kPipeMaxAgents];
+  __shared__ PipeSlot s_slot[kPipeMaxAgents];
+  __shared__ double s_bc[kPipeMaxAgents][2];  // the Adam bias corrections of each slot's epoch in flight
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   FitSt *fst = reinterpret_cast<FitSt *>(s_dyn);
   const int tid = threadIdx.x, G = gridDim.x, rank = blockIdx.x, NA = A.NA;
   for (int i = tid; i < 256; i += kDrThreads) S.tab[i] = ag_exp_tab[i];
-  for (int i = tid; i < NA; i += kDrThreads) fst[i] = A.st[A.agents[i]];
+  for (int i = tid; i < NA; i += kDrThreads) {
+    const int a = A.agents[i], bk = A.bkind[a];
+    fst[i] = A.st[a];
+    PipeSlot &P = s_slot[i];
+    P.a = a;
+    P.bk = bk;
+    P.mode = A.bmode[a];
+    P.init = A.initialised[a];
+    P.n = (double)A.n_total[a];
+    P.s0 = A.offsets[a];
+    pipe_chunk(A.offsets[a + 1] - P.s0, G, rank, P.c0, P.nb);
+    P.cap = A.lds_cap[i];
+    P.off = (uint32_t)A.lds_off[i];
+    P.nf = PH == 0 ? 3 : (bk == AG_BIDDER_DOUBLY_ROBUST ? 6 : 2);
+  }
   __syncthreads();
   // stage every slot's cached records (this phase's fields)
   for (int i = 0; i < NA; ++i) {
-    const int a = A.agents[i], bk = A.bkind[a];
-    const int64_t s0 = A.offsets[a];
-    int64_t c0, nb;
-    pipe_chunk(A.offsets[a + 1] - s0, G, rank, c0, nb);
-    const int64_t cap = A.lds_cap[i], ns = nb < cap ? nb : cap;
-    float *lf = reinterpret_cast<float *>(s_dyn + A.lds_off[i]);
-    const bool dr = bk == AG_BIDDER_DOUBLY_ROBUST;
-    const int nf = PH == 0 ? 3 : (dr ? 6 : 2);
-    uint8_t *lw = reinterpret_cast<uint8_t *>(lf + (size_t)nf * cap);
+    const PipeSlot &P = s_slot[i];
+    const int64_t cap = P.cap, ns = P.nb < cap ? P.nb : cap;
+    float *lf = reinterpret_cast<float *>(s_dyn + P.off);
+    const bool dr = P.bk == AG_BIDDER_DOUBLY_ROBUST;
+    uint8_t *lw = reinterpret_cast<uint8_t *>(lf + (size_t)P.nf * cap);
     const bool eu_ready = dr && fst[i].fit > kFitEu && fst[i].fit != kFitDone;
     for (int64_t j = tid; j < ns; j += kDrThreads) {
-      const int64_t r = s0 + c0 + j;
+      const int64_t r = P.s0 + P.c0 + j;
       lf[kFCtr * cap + j] = (float)A.R0.ctr[r];
       lf[kFVal * cap + j] = (float)A.R0.value[r];
       if (PH == 0 || dr) lf[kFGam * cap + j] = (float)A.R0.gamma[r];
@@ -1461,49 +1491,48 @@ __global__ __launch_bounds__(kDrThreads, PH == 0 ? 4 : 2) void k_bidder_pipe(Pip
     }
   }
   __syncthreads();
-  auto view = [&](int i, int64_t &nb) -> RecView {
-    const int a = A.agents[i];
-    const int64_t s0 = A.offsets[a];
-    int64_t c0;
-    pipe_chunk(A.offsets[a + 1] - s0, G, rank, c0, nb);
-    const int64_t cap = A.lds_cap[i];
-    const float *lf = reinterpret_cast<const float *>(s_dyn + A.lds_off[i]);
-    const int nf = PH == 0 ? 3 : (A.bkind[a] == AG_BIDDER_DOUBLY_ROBUST ? 6 : 2);
+  // AG_PIPE_PROF: finish, step, partial, start, total, finishes (thread 0's; LDS, not registers)
+  __shared__ long long pr[8];
+  if (tid < 8) pr[tid] = 0;
+  auto view = [&](const PipeSlot &P) -> RecView {
+    const int64_t s0 = P.s0;
     const DrRecords R{A.R0.ctr + s0, A.R0.value + s0, A.R0.gamma + s0, A.R0.prop + s0, A.R0.util + s0, A.R0.won + s0};
-    return RecView{R, A.eu_ws + s0, c0, lf, reinterpret_cast<const uint8_t *>(lf + (size_t)nf * cap), cap};
+    const float *lf = reinterpret_cast<const float *>(s_dyn + P.off);
+    return RecView{R, A.eu_ws + s0, P.c0, lf, reinterpret_cast<const uint8_t *>(lf + (size_t)P.nf * P.cap), P.cap};
   };
   auto tr_of = [&](int a, const FitSt &st) -> float * {
     if (!A.traces || rank != 0 || st.fit < kFitWr) return nullptr;
     return A.traces + ((size_t)a * 3 + (st.fit == kFitWr ? 0 : (st.fit == kFitInit ? 1 : 2))) * kDrEpochs;
   };
-  auto step = [&](int i, const int64_t *tot) {
-    const int a = A.agents[i];
-    fit_step(fst[i], tot, (double)A.n_total[a], A.bkind[a], A.bmode[a], A.initialised[a], A.adam_tab, s_grad, &s_loss,
-             &s_np, tr_of(a, fst[i]));
+  auto step = [&](int i, const int64_t *tot, bool prefetched) {
+    const PipeSlot &P = s_slot[i];
+    fit_step(fst[i], tot, P.n, P.bk, P.mode, P.init, A.adam_tab, s_grad, &s_loss, &s_np, tr_of(P.a, fst[i]),
+             prefetched ? s_bc[i] : nullptr);
   };
   // the next epoch of slot i: estimated utilities when its fit reaches them, then its partial
   // sums started up its tree; false when it has no epoch left in this phase (or waits for noise)
   auto begin = [&](int i, bool &root) -> bool {
     FitSt &st = fst[i];
-    const int a = A.agents[i], bk = A.bkind[a];
-    int64_t nb;
-    const RecView V = view(i, nb);
+    const PipeSlot &P = s_slot[i];
+    const int a = P.a, bk = P.bk;
+    const int64_t nb = P.nb;
+    const RecView V = view(P);
     if (PH == 1 && st.fit == kFitEu) {
       // src/Bidder.py:541-546 with the fitted win-rate model (k_bidder_epoch's arithmetic);
       // each_record's thread mapping, so a thread reads back what it wrote
-      double *eu = A.eu_ws + A.offsets[a];
-      float *lfe = const_cast<float *>(V.lf) + (size_t)kFEu * V.cap;
+      double *eu = A.eu_ws + P.s0;
+      float *lfe = reinterpret_cast<float *>(s_dyn + P.off) + (size_t)kFEu * V.cap;
       for (int64_t j = tid; j < nb; j += kDrThreads) {
         const int64_t r = V.c0 + j;
         const double c = (double)(float)V.R.ctr[r], v = (double)(float)V.R.value[r], g = (double)(float)V.R.gamma[r];
         const double z = c * (double)st.wr[0] + v * (double)st.wr[1] + g * (double)st.wr[2] + (double)st.wr[3];
         const float W = (float)(1.0 / (1.0 + agexp::exp(-z, S.tab)));
-        const double Vv = V.R.ctr[r] * V.R.value[r], P = V.R.ctr[r] * V.R.value[r] * V.R.gamma[r];
-        eu[r] = (double)W * (Vv - P);
+        const double Vv = V.R.ctr[r] * V.R.value[r], Pp = V.R.ctr[r] * V.R.value[r] * V.R.gamma[r];
+        eu[r] = (double)W * (Vv - Pp);
         if (j < V.cap) lfe[j] = (float)eu[r];
       }
       __syncthreads();
-      if (tid == 0) fit_after(st, bk, A.bmode[a], A.initialised[a]);
+      if (tid == 0) fit_after(st, bk, P.mode, P.init);
       __syncthreads();
     }
     if (!pipe_in_phase<PH>(st.fit) || st.fit == kFitEu) return false;
@@ -1513,18 +1542,41 @@ __global__ __launch_bounds__(kDrThreads, PH == 0 ? 4 : 2) void k_bidder_pipe(Pip
     if (tid == 0) st.need_noise = wait ? 1 : 0;
     __syncthreads();
     if (wait) return false;
-    const int64_t stride = A.noise_stride ? A.noise_stride : A.n_total[a];
+    // this epoch's Adam bias corrections, loaded now and stored after the partial sums (the
+    // load's latency hidden behind them); fit_step reads them from LDS
+    const int e = st.epoch;
+    double b1 = 0.0, b2 = 0.0;
+    if (tid == 0 && st.fit != kFitWins) {
+      b1 = A.adam_tab[e];
+      b2 = A.adam_tab[kDrEpochs + e];
+    }
+    const int64_t stride = A.noise_stride ? A.noise_stride : (int64_t)P.n;
     const FitNoise F{A.noise ? A.noise + (A.noise_off ? A.noise_off[a] : 0) - (int64_t)A.noise_e0 * stride : nullptr,
                      stride, A.noise_seed, (uint32_t)a, 1 << 30};
+    long long tp = A.prof && tid == 0 ? wall_clock64() : 0;
     const int W = pipe_partial<PH>(st, V, nb, bk, F, S);
-    root = agcoop::agent_allreduce_start(A.bars + (size_t)i * A.lines * kBarLineWords, A.acc + (size_t)i * A.lines * 32,
+    if (tid == 0) {
+      s_bc[i][0] = b1;
+      s_bc[i][1] = b2;
+    }
+    if (A.prof) {
+      __syncthreads();
+      if (tid == 0) {
+        const long long tq = wall_clock64();
+        pr[2] += tq - tp;
+        tp = tq;
+      }
+    }
+    root = agcoop::agent_allreduce_start<kPipeFanIn>(A.bars + (size_t)i * A.lines * kBarLineWords, A.acc + (size_t)i * A.lines * 32,
                                          32, rank, G, S.tot, W, &s_gen[i], &S.flag);
+    if (A.prof && tid == 0) pr[3] += wall_clock64() - tp;
     return true;
   };
   // totals left by ag_bidder_rp_epoch launches
   for (int i = 0; i < NA; ++i)
-    if (fst[i].have_tot && fst[i].fit != kFitDone) step(i, A.tot_in + (size_t)A.agents[i] * 32);
+    if (fst[i].have_tot && fst[i].fit != kFitDone) step(i, A.tot_in + (size_t)s_slot[i].a * 32, false);
   uint32_t pend = 0, roots = 0;
+  const long long t_start = A.prof ? wall_clock64() : 0;
   for (int i = 0; i < NA; ++i) {
     bool root = false;
     if (begin(i, root)) pend |= 1u << i;
@@ -1534,9 +1586,20 @@ __global__ __launch_bounds__(kDrThreads, PH == 0 ? 4 : 2) void k_bidder_pipe(Pip
     for (int i = 0; i < NA; ++i) {
       if (!(pend >> i & 1)) continue;
       const int W = fst[i].fit == kFitWins ? 2 : (fst[i].fit == kFitWr ? 10 : 32);
+      long long tf = A.prof && tid == 0 ? wall_clock64() : 0;
       agcoop::agent_allreduce_finish(A.bars + (size_t)i * A.lines * kBarLineWords, A.acc + (size_t)i * A.lines * 32, G,
                                      roots >> i & 1, &s_gen[i], W, S.tot);
-      step(i, S.tot);
+      if (A.prof && tid == 0) {
+        const long long tg = wall_clock64();
+        pr[0] += tg - tf;
+        tf = tg;
+        pr[5] += 1;
+      }
+      step(i, S.tot, true);
+      if (A.prof) {
+        __syncthreads();
+        if (tid == 0) pr[1] += wall_clock64() - tf;
+      }
       bool root = false;
       pend &= ~(1u << i);
       roots &= ~(1u << i);
@@ -1545,11 +1608,15 @@ __global__ __launch_bounds__(kDrThreads, PH == 0 ? 4 : 2) void k_bidder_pipe(Pip
     }
   }
   __syncthreads();
+  if (A.prof && tid == 0) {
+    pr[4] = wall_clock64() - t_start;
+    for (int k = 0; k < 8; ++k) A.prof[(size_t)rank * 8 + k] = pr[k];
+  }
   if (rank == 0)
     for (int i = tid; i < NA; i += kDrThreads) {
       FitSt f = fst[i];
       f.have_tot = 0;
-      A.st[A.agents[i]] = f;
+      A.st[s_slot[i].a] = f;
     }
 }
 
@@ -1682,7 +1749,7 @@ static int pipe_run(ag_ctx *c, const std::vector<int32_t> &slots, const std::vec
   // device tables, sized once for the largest grid: [3][kPipeMaxAgents] i32 per phase, then
   // per phase the acc rows [kPipeMaxAgents][lines][32] i64 and barrier lines (the two
   // launches of a run never share a word)
-  const size_t lines_max = (size_t)std::max(1, bar_lines(std::max(rp.pipe_blocks[0], rp.pipe_blocks[1])));
+  const size_t lines_max = (size_t)std::max(1, bar_lines(std::max(rp.pipe_blocks[0], rp.pipe_blocks[1]), kPipeFanIn));
   const size_t rows_max = (size_t)kPipeMaxAgents * lines_max * 32;
   const size_t per_ph = 3 * kPipeMaxAgents * sizeof(int32_t) + rows_max * (sizeof(int64_t) + sizeof(unsigned)) + 64;
   if (2 * per_ph > rp.pipe_bytes) {
@@ -1696,7 +1763,7 @@ static int pipe_run(ag_ctx *c, const std::vector<int32_t> &slots, const std::vec
     if (!(phases >> ph & 1)) continue;
     const void *fn = ph == 0 ? (const void *)k_bidder_pipe<0> : (const void *)k_bidder_pipe<1>;
     const int G = (int)std::max<int64_t>(1, std::min<int64_t>(rp.pipe_blocks[ph], (recs + want_recs - 1) / want_recs));
-    const int lines = std::max(1, bar_lines(G));
+    const int lines = std::max(1, bar_lines(G, kPipeFanIn));
     // record caches after the FitSt copies: slot i caches min(chunk, share) records
     const size_t fst_bytes = ((size_t)NA * sizeof(FitSt) + 15) / 16 * 16;
     const size_t budget = kPipeLds[ph] - fst_bytes;
@@ -1751,8 +1818,22 @@ static int pipe_run(ag_ctx *c, const std::vector<int32_t> &slots, const std::vec
     A.noise_seed = c->fit_noise_seed;
     A.adam_tab = w.adam_tab;
     A.traces = traces;
+    A.prof = nullptr;
+    const bool prof = getenv("AG_PIPE_PROF") != nullptr;
+    if (prof) AG_HIP(hipMalloc(&A.prof, sizeof(long long) * 8 * G));
     void *args[] = {&A};
     AG_HIP(hipLaunchCooperativeKernel(fn, dim3(G), dim3(kDrThreads), args, kPipeLds[ph], st));
+    if (prof) {  // diagnostics: mean over workgroups of each part, microseconds (100 MHz clock)
+      std::vector<long long> h(8 * (size_t)G);
+      AG_HIP(hipMemcpy(h.data(), A.prof, sizeof(long long) * 8 * G, hipMemcpyDeviceToHost));
+      (void)hipFree(A.prof);
+      double m[8] = {0};
+      for (int b = 0; b < G; ++b)
+        for (int k = 0; k < 8; ++k) m[k] += (double)h[8 * (size_t)b + k] / G;
+      fprintf(stderr, "k_bidder_pipe<%d> G=%d NA=%d: finish-wait %.0f us, step %.0f us, partial %.0f us, start %.0f "
+              "us, total %.0f us, finishes %.0f\n", ph, G, NA, m[0] / 100, m[1] / 100, m[2] / 100, m[3] / 100,
+              m[4] / 100, m[5]);
+    }
   }
   return AG_OK;
 }
@@ -1870,7 +1951,6 @@ static int sort_records(ag_ctx *c, const ag_shading_samples *s, std::vector<int6
 extern "C" {
 
 int ag_set_dr_state(ag_ctx *c, const float *state, const int32_t *initialised) {
-  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   if (!c || !state || !initialised) return ag_set_error(AG_ERR_INVALID, "ag_set_dr_state: null argument");
   AgDeviceGuard g(c->device);
   if (int rc = dr_ws_ready(c)) return rc;
@@ -1922,7 +2002,6 @@ int ag_shading_counts(ag_ctx *c, const ag_shading_samples *s, int64_t *counts, v
 int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agents, const float *noise,
                      const int64_t *noise_offsets, int32_t noise_epochs, int32_t *epochs, int32_t *status,
                      float *traces, void *stream) {
-  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   if (!c || !s || !noise_offsets) return ag_set_error(AG_ERR_INVALID, "ag_bidder_update: null argument");
   AG_CHECK_STRUCT(s, "ag_bidder_update", "ag_shading_samples");
   if (!s->ctr || !s->value || !s->propensity || !s->won || !s->order)
@@ -1951,15 +2030,16 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agen
   // workgroup; a PolicyLearningBidder (fixed-order float sums: its result follows the split)
   // keeps one workgroup per kBidderChunk records. Both phases use the same rule with their
   // own grid.
-  // The exact-sum learners (ValueLearning, DoublyRobust) train in k_bidder_pipe (all of them
-  // in the same persistent launches, their epochs' cross-workgroup sums overlapped with each
-  // other's work) unless there are more than kPipeMaxAgents of them, a fixed block split is
-  // asked for (AG_OPT_BIDDER_BLOCK_SAMPLES) or AG_BIDDER_PIPE=0 (A/B); the rest in
-  // k_bidder_train
+  // k_bidder_train, one group of workgroups per learner, by default: measured on the bench's
+  // populations (profiles/r04j_*), the pipelined launches (k_bidder_pipe, every learner in
+  // every workgroup) lose -- each round pays one epoch's serial step and tree climb per
+  // learner on 1/A of the work, 1.4-3.4x the time. AG_BIDDER_PIPE=1 takes the pipe for the
+  // exact-sum learners (A/B); ag_bidder_rp_run (one learner of the drop-in update at a time,
+  // where the alternative is a launch per epoch) always does.
   std::vector<int32_t> pipe_slots, pipe_mask(N, 0);
   {
     const char *e = getenv("AG_BIDDER_PIPE");
-    const bool off = (e && e[0] == '0') || c->bidder_chunk > 0;
+    const bool off = !(e && e[0] == '1') || c->bidder_chunk > 0;
     for (int a = 0; a < N && !off; ++a) {
       const int bk = c->h_bkind[a];
       // (a learner without logs takes k_bidder_train's no-logs path: fallback or error)
@@ -2173,7 +2253,6 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agen
 
 int ag_dr_update(ag_ctx *c, const ag_shading_samples *s, const float *noise, const int64_t *noise_offsets,
                  int32_t noise_epochs, int32_t *epochs, float *traces, void *stream) {
-  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   std::vector<int32_t> stat(c->shape.num_agents);
   if (int rc = ag_bidder_update(c, s, nullptr, noise, noise_offsets, noise_epochs, epochs, stat.data(), traces, stream))
     return rc;
@@ -2186,7 +2265,6 @@ int ag_dr_update(ag_ctx *c, const ag_shading_samples *s, const float *noise, con
 // ---- resumable / record-parallel training (k_bidder_epoch) ----
 int ag_bidder_rp_begin(ag_ctx *c, const ag_shading_samples *s, const int32_t *agents, const int64_t *records_total,
                        const int64_t *records_base, int64_t *totals, void *stream) {
-  if (c) c->image_dirty = true;
   if (!c || !s || !totals) return ag_set_error(AG_ERR_INVALID, "ag_bidder_rp_begin: null argument");
   AG_CHECK_STRUCT(s, "ag_bidder_rp_begin", "ag_shading_samples");
   if (!s->ctr || !s->value || !s->propensity || !s->won || !s->order)
@@ -2401,7 +2479,6 @@ int ag_bidder_rp_poll(ag_ctx *c, int32_t *fit, int32_t *epoch, int32_t *need_noi
 
 int ag_bidder_rp_end(ag_ctx *c, int32_t *epochs, int32_t *status, void *stream) {
   if (!c || !c->dr.rp.active) return ag_set_error(AG_ERR_STATE, "ag_bidder_rp_end: no ag_bidder_rp_begin");
-  c->image_dirty = true;
   AgDeviceGuard g(c->device);
   const int N = c->shape.num_agents;
   ag_dr_ws &w = c->dr;
@@ -2453,7 +2530,6 @@ int ag_bidder_rp_end(ag_ctx *c, int32_t *epochs, int32_t *status, void *stream) 
 }
 
 int ag_set_bidder_modes(ag_ctx *c, const int32_t *modes) {
-  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   if (!c || !modes) return ag_set_error(AG_ERR_INVALID, "ag_set_bidder_modes: null argument");
   AgDeviceGuard g(c->device);
   if (int rc = dr_ws_ready(c)) return rc;

@@ -128,14 +128,6 @@ struct ag_ctx {
   int32_t grid_per_cu = 0;                  // AG_OPT_SIM_BLOCKS_PER_CU (0: as many as fit)
   int32_t block_threads = 0;                // AG_OPT_SIM_BLOCK_THREADS (0: auto)
   int32_t resident_ora[4] = {};             // resident blocks of k_oracle [generate][counters]
-  int32_t resident_pop[8] = {};             // resident blocks of k_pop [all modes][1024 lanes][counters]
-  float *d_nz_zero = nullptr;               // k_pop: [K * (OE + 1)][64] zero Thompson noise
-  uint8_t *d_ts_item = nullptr;             // k_ts_choice -> k_pop: [P][B] LR-TS item choices
-  unsigned char *d_pop_image = nullptr;     // k_pop_image -> k_pop / k_ts_choice LDS images
-  bool image_dirty = true;                  // set by every entry point that changes agent state
-  unsigned *d_ticket = nullptr;             // k_pop's last-workgroup ticket (zero between launches)
-  int64_t ts_item_cap = 0;
-  int32_t resident_tsc = 0;                 // resident blocks of k_ts_choice
   // general populations (anything beyond OracleAllocator + TruthfulBidder)
   bool general = false, has_lrts = false, has_shading = false, lrts_loaded = false;
   int32_t ts_sample = 1;

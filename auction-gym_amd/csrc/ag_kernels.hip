@@ -29,7 +29,6 @@
 #include "ag_philox.h"
 #include "ag_sim.h"
 #include "ag_sim_oracle.h"
-#include "ag_sim_pop.h"
 
 #ifndef AG_SIM_WIDE_AB
 #define AG_SIM_WIDE_AB 0  // AG_SIM_KERNEL_WIDE (the runtime-P kernel at any P): A/B variant builds only
@@ -492,178 +491,6 @@ int simulate_oracle(ag_ctx *c, OraKernel k, int64_t B, const ag_batch_in *in, co
   return AG_OK;
 }
 
-PopKernel pick_pop(int P, int D, int K, int DO, int mode, int bt, bool tsx) {
-  switch (P) {
-    case 1: return pick_pop_for<1>(D, K, DO, mode, bt, tsx);
-    case 2: return pick_pop_for<2>(D, K, DO, mode, bt, tsx);
-    case 3: return pick_pop_for<3>(D, K, DO, mode, bt, tsx);
-    case 4: return pick_pop_for<4>(D, K, DO, mode, bt, tsx);
-    case 5: return pick_pop_for<5>(D, K, DO, mode, bt, tsx);
-    case 6: return pick_pop_for<6>(D, K, DO, mode, bt, tsx);
-    case 7: return pick_pop_for<7>(D, K, DO, mode, bt, tsx);
-    case 8: return pick_pop_for<8>(D, K, DO, mode, bt, tsx);
-    default: return nullptr;
-  }
-}
-
-TsChoiceKernel pick_ts_choice(int P, int K, int DO) {
-  switch (P) {
-    case 1: return pick_ts_choice_for<1>(K, DO);
-    case 2: return pick_ts_choice_for<2>(K, DO);
-    case 3: return pick_ts_choice_for<3>(K, DO);
-    case 4: return pick_ts_choice_for<4>(K, DO);
-    case 5: return pick_ts_choice_for<5>(K, DO);
-    case 6: return pick_ts_choice_for<6>(K, DO);
-    case 7: return pick_ts_choice_for<7>(K, DO);
-    case 8: return pick_ts_choice_for<8>(K, DO);
-    default: return nullptr;
-  }
-}
-
-// ag_simulate for general populations of the shipped catalogue shape: k_pop (ag_sim_pop.h).
-// Returns AG_ERR_UNSUPPORTED without launching anything when k_pop has no instantiation for
-// the shape (the caller then runs k_simulate).
-int simulate_pop(ag_ctx *c, int64_t B, const ag_batch_in *in, const ag_batch_out *out, int64_t *counters_fx,
-                 hipStream_t st) {
-  const ag_shape &s = c->shape;
-  constexpr int K = 12, D = 6, DO = 5;  // the instantiated shape (ag_sim_p.hip pick_pop_for)
-  if (c->D != D || s.num_items != K || s.obs_embedding_size + 1 != DO || s.num_participants > kMaxP || c->ragged)
-    return AG_ERR_UNSUPPORTED;  // (per-agent item counts: k_simulate)
-  const int mode = (c->has_shading || c->gen_mode_all) ? kGenAll : kGenTruthful;
-  const bool counters = counters_fx != nullptr;
-  // workgroup size: 256 lanes while the LDS image (agent records + >= 16 counter replicas)
-  // leaves 4 workgroups per CU, else 1024 lanes (one image shared by 16 waves)
-  // workgroups of 1024 lanes (one per CU: the prologue's image copy and the epilogue's replica
-  // sums amortised over 16 waves; configs_3 0.124 -> 0.115 ms, profiles/r03j_ab.log) unless
-  // AG_OPT_SIM_BLOCK_THREADS asks for 256
-  int bt = c->block_threads ? c->block_threads : kLargeThreads;
-  PopLayout L = make_pop_layout<K, D, DO>(s.num_agents, counters,
-                                          bt == kLargeThreads ? 150 * 1024 : AG_POP_LDS_BUDGET);
-  if (L.total > 160 * 1024) return AG_ERR_UNSUPPORTED;
-  // the split pass: k_ts_choice makes every LR-TS participant's Thompson choice into
-  // c->d_ts_item, k_pop reads it. AUTO takes it for TruthfulBidder-only populations (k_pop is
-  // light there, and k_ts_choice streams the noise at high occupancy: configs_1 0.183 ->
-  // 0.180 ms vs k_pop fused 0.201 ms) and k_pop fused otherwise (the policy / shading FP64
-  // work overlaps the noise loads: configs_2 0.226 -> 0.198 ms, profiles/r03c_ab_pop.log)
-  const bool tsx = c->has_lrts && (c->sim_kernel == AG_SIM_KERNEL_SPLIT ||
-                                   (c->sim_kernel == AG_SIM_KERNEL_AUTO && mode == kGenTruthful));
-  PopKernel k = pick_pop(s.num_participants, D, K, DO, mode, bt, tsx);
-  TsChoiceKernel kt = tsx ? pick_ts_choice(s.num_participants, K, DO) : nullptr;
-  if (!k || (tsx && !kt)) return AG_ERR_UNSUPPORTED;
-  if (!c->d_nz_zero) {
-    AG_HIP(hipMalloc(&c->d_nz_zero, (size_t)K * DO * 64 * sizeof(float)));
-    AG_HIP(hipMemset(c->d_nz_zero, 0, (size_t)K * DO * 64 * sizeof(float)));
-  }
-  // the LDS images (the agents' state as it is at this point of the stream), rebuilt after
-  // any entry point that changes that state (catalogue, kinds, shading parameters, LR-TS
-  // posteriors, learner models -- set by the caller or by an update); stream-ordered
-  using Img = PopImage<K, D, DO>;
-  if (!c->d_pop_image) AG_HIP(hipMalloc(&c->d_pop_image, (size_t)Img::total(s.num_agents)));
-  if (c->image_dirty) {
-    c->image_dirty = false;
-    PopImageParams ip;
-    ip.N = s.num_agents;
-    ip.items = c->d_items;
-    ip.values = c->d_values;
-    ip.akind = c->d_akind;
-    ip.bkind = c->d_bkind;
-    ip.pg = c->d_pg;
-    ip.gs = c->d_gs;
-    ip.tsm = c->lrts_loaded ? c->d_tsm : nullptr;
-    ip.drs = c->dr_loaded ? c->dr.state : nullptr;
-    ip.dri = c->dr_loaded ? c->dr.init : nullptr;
-    ip.image = c->d_pop_image;
-    PopImageKernel ik = k_pop_image<K, D, DO>;
-    hipLaunchKernelGGL(ik, dim3(s.num_agents + 1), dim3(256), 0, st, ip);
-    AG_HIP(hipGetLastError());
-  }
-  if (tsx) {
-    const int64_t need = (int64_t)s.num_participants * B;
-    if (need > c->ts_item_cap) {
-      if (c->d_ts_item) AG_HIP(hipFree(c->d_ts_item));
-      c->d_ts_item = nullptr;
-      c->ts_item_cap = 0;
-      AG_HIP(hipMalloc(&c->d_ts_item, (size_t)need));
-      c->ts_item_cap = need;
-    }
-    TsChoiceParams tp;
-    tp.B = (int32_t)B;
-    tp.lo = 0;
-    tp.hi = (int32_t)B;
-    tp.N = s.num_agents;
-    tp.image = c->d_pop_image + Img::pop_bytes(s.num_agents);
-    tp.ctx = in->ctx;
-    tp.part = in->part;
-    tp.ts_noise = c->ts_sample ? in->ts_noise : nullptr;
-    tp.ts_noise_index = in->ts_noise_index;
-    tp.nz_zero = c->d_nz_zero;
-    tp.ts_item = c->d_ts_item;
-    const size_t tlds = (size_t)kPopTabBytes + (size_t)s.num_agents * TsChoiceRec<K, DO>::stride;
-    if (tlds > 160 * 1024) return AG_ERR_UNSUPPORTED;
-    if (tlds > 64 * 1024)
-      AG_HIP(hipFuncSetAttribute((const void *)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tlds));
-    if (c->resident_tsc == 0) {
-      int per_cu = 0, cus = 0;
-      AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)kt, kThreads, tlds));
-      AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-      c->resident_tsc = per_cu * cus > 0 ? per_cu * cus : 1;
-    }
-    const int64_t tiles = (B + kThreads - 1) / kThreads;
-    const int tgrid = (int)(tiles < c->resident_tsc ? tiles : c->resident_tsc);
-    hipLaunchKernelGGL(kt, dim3(tgrid), dim3(kThreads), tlds, st, tp);
-    AG_HIP(hipGetLastError());
-  }
-  PopParams prm;
-  prm.B = (int32_t)B;
-  prm.N = s.num_agents;
-  prm.mech = s.mechanism;
-  prm.want_counters = counters;
-  prm.ts_sample = c->ts_sample;
-  prm.L = L;
-  prm.image = c->d_pop_image;
-  prm.nz_zero = c->d_nz_zero;
-  prm.ts_item = tsx ? c->d_ts_item : nullptr;
-  prm.in = *in;
-  prm.out = *out;
-  prm.partials = c->d_partials;
-  // the counters are summed by the launch's last workgroup (no k_reduce_counters launch)
-  if (!c->d_ticket) {
-    AG_HIP(hipMalloc(&c->d_ticket, sizeof(unsigned)));
-    AG_HIP(hipMemset(c->d_ticket, 0, sizeof(unsigned)));
-  }
-  prm.limbs = counters_fx;
-  prm.ticket = c->d_ticket;
-  const size_t lds = (size_t)L.total;
-  if (lds > 64 * 1024)
-    AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  int &res = c->resident_pop[(mode == kGenAll ? 4 : 0) + (bt == kLargeThreads ? 2 : 0) + (counters ? 1 : 0)];
-  if (res == 0) {
-    int per_cu = 0, cus = 0;
-    AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k, bt, lds));
-    AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-    res = per_cu * cus;
-    if (res < 1) res = 1;
-    if (res > c->partial_blocks) res = c->partial_blocks;
-  }
-  // a workgroup resolves at most kAuctionsPerReplica x replicas auctions per launch (every
-  // replica's int64 sum exact); larger batches run as consecutive launches
-  int64_t chunk_max = (int64_t)res * kAuctionsPerReplica * L.replicas;
-  if (c->launch_cap > 0 && c->launch_cap < chunk_max) chunk_max = c->launch_cap;
-  if (chunk_max < 1) chunk_max = 1;
-  const int nc = s.num_agents * kC;
-  for (int64_t lo = 0; lo < B; lo += chunk_max) {
-    const int64_t hi = lo + chunk_max < B ? lo + chunk_max : B;
-    const int64_t tiles = (hi - lo + bt - 1) / bt;
-    const int grid = (int)(tiles < res ? tiles : res);
-    prm.lo = (int32_t)lo;
-    prm.hi = (int32_t)hi;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(bt), lds, st, prm);
-    AG_HIP(hipGetLastError());
-  }
-  (void)nc;
-  return AG_OK;
-}
-
 int grid_for(int64_t B, int64_t per_block_cap) {
   int64_t tiles = (B + kThreads - 1) / kThreads;
   int64_t need = (B + per_block_cap - 1) / per_block_cap;
@@ -747,10 +574,6 @@ int ag_create(int32_t device, const ag_shape *s, ag_ctx **out) {
 int ag_destroy(ag_ctx *c) {
   if (!c) return AG_OK;
   AgDeviceGuard g(c->device);
-  (void)hipFree(c->d_nz_zero);
-  (void)hipFree(c->d_ts_item);
-  (void)hipFree(c->d_pop_image);
-  (void)hipFree(c->d_ticket);
   (void)hipFree(c->d_items);
   (void)hipFree(c->d_values);
   (void)hipFree(c->d_partials);
@@ -787,13 +610,11 @@ int ag_set_agent_items(ag_ctx *c, const int32_t *num_items) {
     AG_HIP(hipMemcpy(c->d_kag, num_items, sizeof(int32_t) * N, hipMemcpyHostToDevice));
   }
   c->ragged = ragged;
-  c->image_dirty = true;
   return AG_OK;
 }
 
 int ag_set_agent_params(ag_ctx *c, const int32_t *alloc_kind, const int32_t *bid_kind,
                         const double *prev_gamma, const double *gamma_sigma) {
-  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   if (!c) return ag_set_error(AG_ERR_INVALID, "ag_set_agent_params: null ctx");
   const int N = c->shape.num_agents;
   bool general = false, lrts = false, shading = false;
@@ -845,7 +666,6 @@ int ag_set_agent_params(ag_ctx *c, const int32_t *alloc_kind, const int32_t *bid
 }
 
 int ag_set_agent_kinds(ag_ctx *c, const int32_t *alloc_kind, const int32_t *bid_kind) {
-  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   if (!c) return ag_set_error(AG_ERR_INVALID, "ag_set_agent_kinds: null ctx");
   for (int a = 0; a < c->shape.num_agents; ++a)
     if (bid_kind && bid_kind[a] != AG_BIDDER_TRUTHFUL)
@@ -855,7 +675,6 @@ int ag_set_agent_kinds(ag_ctx *c, const int32_t *alloc_kind, const int32_t *bid_
 
 int ag_load_lrts(ag_ctx *c, const float *m, const float *q, const float *prev_m,
                  int32_t thompson_sampling) {
-  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   if (!c || !m || !q) return ag_set_error(AG_ERR_INVALID, "ag_load_lrts: null argument");
   AgDeviceGuard g(c->device);
   const size_t n = (size_t)c->shape.num_agents * c->shape.num_items * (c->shape.obs_embedding_size + 1);
@@ -919,6 +738,9 @@ int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
     case AG_OPT_SIMULATE_KERNEL:
       if (value < AG_SIM_KERNEL_AUTO || value > AG_SIM_KERNEL_WIDE)
         return ag_set_error(AG_ERR_INVALID, "ag_set_option: bad simulate kernel %lld", (long long)value);
+      if (value == AG_SIM_KERNEL_FUSED || value == AG_SIM_KERNEL_SPLIT)
+        return ag_set_error(AG_ERR_UNSUPPORTED, "ag_set_option: k_pop (AG_SIM_KERNEL_FUSED / SPLIT) was retired in "
+                                                "round 4: k_simulate is as fast on every population line");
       if (value == AG_SIM_KERNEL_WIDE && !AG_SIM_WIDE_AB)  // the round-3 A/B (2.3x slower): variant builds only
         return ag_set_error(AG_ERR_UNSUPPORTED, "ag_set_option: AG_SIM_KERNEL_WIDE is built only in the A/B "
                                                 "variant (make variant VFLAGS=-DAG_SIM_WIDE_AB=1)");
@@ -930,7 +752,6 @@ int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
 }
 
 int ag_load_catalog(ag_ctx *c, const double *item_emb, const double *item_val) {
-  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   if (!c || !item_emb || !item_val) return ag_set_error(AG_ERR_INVALID, "ag_load_catalog: null argument");
   AgDeviceGuard g(c->device);
   const size_t n = (size_t)c->shape.num_agents * c->shape.num_items;
@@ -1033,18 +854,10 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   if (prune && !c->general && c->ora_catalog && c->sim_kernel != AG_SIM_KERNEL_GENERIC && !c->wide)
     if (OraKernel ok = pick_oracle(s.num_participants, D, false))
       return simulate_oracle(c, ok, B, in, out, counters_fx, (hipStream_t)stream);
-  // k_pop when asked for, and by AUTO only for TruthfulBidder-only populations at P >= 8 (the
-  // split pass: configs_1 at P = 8 0.632 ms against k_simulate's 0.777). At P = 2 it is slower
-  // than k_simulate on every population line (one-process A/B, configs_1..4: 0.234 / 0.248 /
-  // 0.172 / 0.465 ms against 0.178 / 0.234 / 0.141 / 0.398, 256- and 1024-lane builds alike;
+  // (round 4 retired k_pop, the dedicated shipped-shape population kernel: k_simulate was as
+  // fast or faster on every line, P = 8 included once its slots stream -- configs_1 at P = 8
+  // 0.665 against 0.680 ms, profiles/r04k_ab_c1p8.log; at P = 2 on every line,
   // profiles/r03_ab_pop_vs_generic.log)
-  const bool truthful_only = !(c->has_shading || c->gen_mode_all);
-  const bool want_pop = c->sim_kernel == AG_SIM_KERNEL_FUSED || c->sim_kernel == AG_SIM_KERNEL_SPLIT ||
-                        (c->sim_kernel == AG_SIM_KERNEL_AUTO && truthful_only && s.num_participants >= 8);
-  if (prune && c->general && want_pop && (c->ts_sample == 0 || !c->has_lrts || in->ts_noise)) {
-    const int rc = simulate_pop(c, B, in, out, counters_fx, (hipStream_t)stream);
-    if (rc != AG_ERR_UNSUPPORTED) return rc;  // launched (or failed); else k_simulate below
-  }
   int W = (prune && (B % 2) == 0 && c->wide && !c->general && s.num_participants <= kMaxP) ? 2 : 1;
   size_t lds = (size_t)prm.lds.total;
   if (lds > 160 * 1024)

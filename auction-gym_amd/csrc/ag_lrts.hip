@@ -714,7 +714,6 @@ static int bucket_samples(ag_ctx *c, const ag_lrts_samples *s, hipStream_t st, c
 }
 
 int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *loss_trace, void *stream) {
-  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   if (int rc = check_store(c, s, "ag_lrts_update")) return rc;
   if (!c->has_lrts) return AG_OK;
   if (!c->lrts_loaded) return ag_set_error(AG_ERR_STATE, "ag_lrts_update: ag_load_lrts not called");
@@ -848,7 +847,6 @@ int ag_lrts_update(ag_ctx *c, const ag_lrts_samples *s, int32_t *epochs, float *
 // ---- resumable / record-parallel LR-TS training (k_lrts_epoch) ----
 int ag_lrts_rp_begin(ag_ctx *c, const ag_lrts_samples *s, const int32_t *agents, const int64_t *samples_total,
                      int64_t *totals, void *stream) {
-  if (c) c->image_dirty = true;
   if (int rc = check_store(c, s, "ag_lrts_rp_begin")) return rc;
   if (!totals) return ag_set_error(AG_ERR_INVALID, "ag_lrts_rp_begin: null totals");
   if (!c->lrts_loaded) return ag_set_error(AG_ERR_STATE, "ag_lrts_rp_begin: ag_load_lrts not called");
@@ -966,7 +964,6 @@ int ag_lrts_rp_poll(ag_ctx *c, int32_t *training, void *stream) {
 
 int ag_lrts_rp_end(ag_ctx *c, int32_t *epochs, void *stream) {
   if (!c || !c->lrts.rp.active) return ag_set_error(AG_ERR_STATE, "ag_lrts_rp_end: no ag_lrts_rp_begin");
-  c->image_dirty = true;
   int32_t training = 0;
   if (int rc = ag_lrts_rp_poll(c, &training, stream)) return rc;
   c->lrts.rp.active = false;

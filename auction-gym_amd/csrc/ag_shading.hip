@@ -264,7 +264,6 @@ int ag_empirical_update(ag_ctx *c, const ag_shading_samples *s, double *prev_gam
 
 int ag_empirical_update_agents(ag_ctx *c, const ag_shading_samples *s, const int32_t *agents, double *prev_gamma,
                                void *stream) {
-  if (c) c->image_dirty = true;  // the agents' state changes: k_pop_image rebuilds the LDS images
   if (int rc = check_store(c, s, "ag_empirical_update")) return rc;
   const int N = c->shape.num_agents;
   AgDeviceGuard g(c->device);

@@ -904,7 +904,10 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
   int jv[PA][W];  // compact ts_noise_index entries (GENERAL with ts_noise_index; else kTsjLoad)
   const bool pre_tsj = GENERAL && !AG_PREFETCH && in.ts_noise_index && in.ts_noise && prm.ts_sample;
   // streamed slots (below): each slot's participant / noise index loaded with the slot
-  constexpr bool kStream = GENERAL != kGenOracle && W == 1 && P >= AG_STREAM_MIN_P;
+  // streamed slots for TruthfulBidder-only populations (configs_1 at P = 8: 0.665 vs 0.730 ms
+  // kept per-slot arrays) but not for the full mix (configs_4 at P = 8: 1.687 vs 1.632 ms;
+  // profiles/r04k_ab_*.log)
+  constexpr bool kStream = GENERAL == kGenTruthful && W == 1 && P >= AG_STREAM_MIN_P;
   auto load_tile = [&](uint32_t i) {
 #pragma unroll
     for (int e = 0; e < D - 1; ++e) ld_f64<W>(in.ctx + e * B + i, xv[e]);

@@ -697,6 +697,8 @@ def main():
     ap.add_argument("--no-ts", action="store_true", help="skip the SP_Truthful_TS (configs[1]) line")
     ap.add_argument("--no-update", action="store_true", help="skip timing the Agent.update of learners")
     ap.add_argument("--no-p8", action="store_true", help="skip the P = 8 variants of configs_1 and configs_4")
+    ap.add_argument("--p8-only", action="store_true",
+                    help="of configs_1 / the populations, only the P = 8 lines (profiling passes)")
     ap.add_argument("--no-populations", action="store_true",
                     help="skip the configs[2..4] lines (FP_DM_TS, FP_DR_TS, mixed population)")
     ap.add_argument("--populations", default=",".join(POPULATIONS),
@@ -877,11 +879,11 @@ def main():
     usable = min(n_threads, int(np.ceil(quota))) if quota else n_threads
     threads = args.cpu_threads or usable
     cpu_lines = threads if (rank == 0 and world == 1 and not args.no_cpu_baseline) else 0
-    if not args.no_ts:
+    if not args.no_ts and not args.p8_only:
         result["configs_1"] = run_sp_ts(args.ts_batch, args.steps, args.warmup, world, rank, local,
                                         with_update=not args.no_update, cpu_threads=cpu_lines)
 
-    if not args.no_populations:
+    if not args.no_populations and not args.p8_only:
         for key in [k for k in args.populations.split(",") if k]:
             result[key] = run_population(key, max(5, args.steps // 5), max(5, args.warmup // 5), world, rank, local,
                                          with_update=not args.no_update, cpu_threads=cpu_lines)

@@ -246,12 +246,10 @@ typedef enum ag_sim_kernel {
                                values lie in (0, 1024): the dedicated Oracle kernel; else the
                                general one */
   AG_SIM_KERNEL_GENERIC = 1, /* always the general simulate kernel (A/B and parity tests) */
-  AG_SIM_KERNEL_FUSED = 2,   /* general populations of the shipped shape (K = 12, E = 5, OE = 4):
-                                the dedicated kernel k_pop making its Thompson choices itself */
-  AG_SIM_KERNEL_SPLIT = 3,   /* ... the split pass, k_ts_choice then k_pop. FUSED / SPLIT are
-                                A/B and parity variants (identical results); AUTO runs the
-                                general kernel (faster at P = 2 on every population line),
-                                the split pass for TruthfulBidder-only populations at P >= 8 */
+  AG_SIM_KERNEL_FUSED = 2,   /* retired (round 4): the dedicated shipped-shape population
+                                kernel k_pop no longer ships -- the general kernel was as fast
+                                on every line; ag_set_option refuses these two values */
+  AG_SIM_KERNEL_SPLIT = 3,
   AG_SIM_KERNEL_WIDE = 4     /* general populations: the runtime-P kernel (slot results not
                                 kept in registers, resolved again for the counters) at any P;
                                 A/B of wide auctions, identical results */

@@ -46,8 +46,8 @@ def _oracle_on(eng, dims, inp, st16, init, B):
 @pytest.mark.parametrize("P", [2, 8])
 def test_configs_1_sp_truthful_ts_full_size(gpu, oracle, P):
     """configs[1] (SP_Truthful_TS: 8 LR-TS Thompson-sampling truthful bidders, SecondPrice) at
-    the bench's 2^20 auctions, P = 2 (k_simulate's TruthfulBidder build) and P = 8 (AUTO's split
-    k_pop / k_ts_choice pass), inputs and Thompson noise as the bench generates them."""
+    the bench's 2^20 auctions, P = 2 and P = 8 (k_simulate's TruthfulBidder build; streamed
+    slots at P = 8), inputs and Thompson noise as the bench generates them."""
     import torch
     import bench
     B = 1 << 20

@@ -246,9 +246,9 @@ def _trained(eng):
 
 @pytest.mark.parametrize("host_noise", [False, True], ids=["synthetic", "host_noise"])
 def test_pipe_equals_persistent_trainer(gpu, monkeypatch, host_noise):
-    """ag_bidder_update's pipelined launches (every ValueLearning / DoublyRobust learner in the
-    same persistent launches, each one's per-epoch sum overlapped with the others' epochs)
-    against k_bidder_train (AG_BIDDER_PIPE=0): epochs, status and models bit for bit -- DM and
+    """ag_bidder_update's pipelined launches (AG_BIDDER_PIPE=1: every ValueLearning /
+    DoublyRobust learner in the same persistent launches, each one's per-epoch sum overlapped
+    with the others' epochs) against k_bidder_train (the default): epochs, status and models bit for bit -- DM and
     DR learners (DR imitating on its first update) trained together, a PPO PolicyLearningBidder
     beside them (k_bidder_train either way). host_noise: the caller's draws with 600 policy
     epochs, too few for some fits (status -3, model not applied, in both)."""

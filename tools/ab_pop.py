@@ -31,7 +31,7 @@ def main():
         key, P = key.split(":")[0], int(key.split(":")[1])
     vdir = os.path.join(ROOT, "auction-gym_amd", "build", "variants")
     paths = {"base": _lib.LIB_PATH}
-    special = {"generic", "fused", "split", "wide", "bt256", "bt1024", "nocnt", "noship"}
+    special = {"generic", "wide", "bt256", "bt1024", "nocnt", "noship"}
     for n in sys.argv[2:]:  # "<variant>+generic": that build with k_simulate forced
         v = n[:-len("+generic")] if n.endswith("+generic") else n
         paths[n] = _lib.LIB_PATH if v in special else os.path.join(vdir, f"libauctiongym_hip_{v}.so")
@@ -56,7 +56,7 @@ def main():
         else:
             eng, what, B, ak, bk, st16, dims = bench.build_population(key, 0, P=P)
             eng.set_dr_state(st16, np.where(bk >= 2, 1, 0).astype(np.int32))
-        if n in ("generic", "fused", "split", "wide"):
+        if n in ("generic", "wide"):
             eng.set_simulate_kernel(True if n == "generic" else n)
         elif n.endswith("+generic"):
             eng.set_simulate_kernel(True)
