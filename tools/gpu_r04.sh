@@ -27,6 +27,9 @@ for s in ${STEPS:-smoke configs suite bench}; do
       step ab_c3 300 python tools/ab_pop.py configs_3 stream1 &&
       step ab_c2 300 python tools/ab_pop.py configs_2 stream1 &&
       step ab_c1 300 python tools/ab_pop.py configs_1 stream1 ;;
+    ab_p8)
+      step ab_c4p8 300 python tools/ab_pop.py configs_4:8 bt768 bt768s streamall &&
+      step ab_c4 300 python tools/ab_pop.py configs_4 bt768 streamall ;;
     stats) step kernel_stats 500 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
   esac
 done
