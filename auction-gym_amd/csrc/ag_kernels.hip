@@ -874,7 +874,15 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   // the shipped shape (E = 5, LR-TS width OE + 1 = 5 in the layout) has builds with the LR-TS
   // width compile-time (k_simulate's DOS); AG_OPT_SIM_SHIPPED_SHAPE 0 turns them off (A/B)
   const int ship = (c->general && c->ship_shape && D == 6 && prm.lds.ts_do == kShipDo) ? kGenShip : 0;
+  // the full mix at P >= 3 in the large-image case: the streamed 768-lane build (shipped shape)
+  if (bt == kLargeThreads && c->block_threads == 0 && gmode == kGenAll && ship && s.num_participants >= AG_STREAM_MIN_P &&
+      s.num_participants <= kMaxP)
+    bt = kMidThreads;
   SimKernel k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
+  if (!k && bt == kMidThreads) {
+    bt = kLargeThreads;
+    k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
+  }
   if (!k && W == 2) {  // the two-auctions-per-lane build is an A/B variant only (AG_LANE_PAIRS)
     W = 1;
     k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
@@ -883,10 +891,12 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
     bt = kThreads;
     k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
   }
+  bool wide_ab = false;
 #if AG_SIM_WIDE_AB
   if (c->general && c->sim_kernel == AG_SIM_KERNEL_WIDE) {  // the runtime-P kernel at any P (A/B)
     bt = kThreads;
     k = pick_kernel_for<0>(D, prune, 1, kGenAll, kThreads);
+    wide_ab = true;
   }
 #endif
   if (!k) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: no kernel for P=%d D=%d", s.num_participants, D);
@@ -901,8 +911,11 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
     AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   // Persistent grid: exactly the blocks the device keeps resident (no partial last round),
   // each striding over bt-auction tiles.
-  int &res = c->resident[(ship ? 64 : 0) + (gmode == kGenTruthful ? 32 : 0) + (bt == kThreads ? 0 : 16) + (c->general ? 8 : 0) +
-                         (W == 2 ? 4 : 0) + (prune ? 2 : 0) + (prm.want_counters ? 1 : 0)];
+  // (the WIDE A/B kernel has slots of its own: its occupancy is not the AUTO kernel's)
+  int &res = wide_ab ? c->resident_wide[prm.want_counters ? 1 : 0]
+                     : c->resident[(bt == kMidThreads ? 128 : 0) + (ship ? 64 : 0) + (gmode == kGenTruthful ? 32 : 0) +
+                                   (bt == kThreads ? 0 : 16) + (c->general ? 8 : 0) + (W == 2 ? 4 : 0) +
+                                   (prune ? 2 : 0) + (prm.want_counters ? 1 : 0)];
   if (res == 0) {
     int per_cu = 0, cus = 0;
     AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k, bt, lds));

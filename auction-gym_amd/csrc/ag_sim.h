@@ -43,6 +43,9 @@ namespace ag {
 #ifndef AG_MIN_WAVES
 #define AG_MIN_WAVES 1
 #endif
+#ifndef AG_STREAM_GENALL
+#define AG_STREAM_GENALL 0  // A/B: streamed slots for the full mix too (make variant)
+#endif
 #ifndef AG_STREAM_MIN_P
 #define AG_STREAM_MIN_P 3  // general kernel: streamed slots (no per-slot result arrays) from this P on
 #endif
@@ -55,6 +58,11 @@ constexpr int kThreads = 256;              // 4 waves of 64 lanes
 #define AG_LARGE_BT 1024
 #endif
 constexpr int kLargeThreads = AG_LARGE_BT;  // the general kernel's workgroups for large LDS images
+// ... and for the full mix at P >= 3 (streamed slots): 12 waves, <= 168 VGPRs, one workgroup
+// per CU. The streamed full build at 1024 lanes (128 VGPRs) spilled; kept per-slot arrays
+// spill more: configs_4 at P = 8 1.507 ms (1024, kept) / 1.624 (1024, streamed) / 1.592 (768,
+// kept) / 1.387 (768, streamed), profiles/r04l_ab_c4p8.log
+constexpr int kMidThreads = 768;
 // k_simulate's GENERAL modes: Oracle + Truthful only; any population; allocators of any
 // kind with TruthfulBidders only (no bid-shading code: fewer VGPRs, 4 waves per SIMD)
 constexpr int kGenOracle = 0, kGenAll = 1, kGenTruthful = 2;
@@ -905,9 +913,11 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
   const bool pre_tsj = GENERAL && !AG_PREFETCH && in.ts_noise_index && in.ts_noise && prm.ts_sample;
   // streamed slots (below): each slot's participant / noise index loaded with the slot
   // streamed slots for TruthfulBidder-only populations (configs_1 at P = 8: 0.665 vs 0.730 ms
-  // kept per-slot arrays) but not for the full mix (configs_4 at P = 8: 1.687 vs 1.632 ms;
-  // profiles/r04k_ab_*.log)
-  constexpr bool kStream = GENERAL == kGenTruthful && W == 1 && P >= AG_STREAM_MIN_P;
+  // kept per-slot arrays, profiles/r04k_ab_c1p8.log) and for the full mix in its 768-lane build
+  // (kMidThreads)
+  constexpr bool kStream =
+      (GENERAL == kGenTruthful || (GENERAL == kGenAll && (BT == kMidThreads || AG_STREAM_GENALL))) && W == 1 &&
+      P >= AG_STREAM_MIN_P;
   auto load_tile = [&](uint32_t i) {
 #pragma unroll
     for (int e = 0; e < D - 1; ++e) ld_f64<W>(in.ctx + e * B + i, xv[e]);

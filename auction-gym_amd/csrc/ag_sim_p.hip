@@ -54,6 +54,8 @@ SimKernel pick_kernel_for<AG_P>(int D, bool prune, int W, int general, int bt) {
   general &= ~kGenShip;
   if (general && ship && prune && D == 6) {  // the shipped shape: LR-TS width 5 compile-time
     if (bt == kLargeThreads) return k_simulate<P, 6, true, 1, kGenAll, kLargeThreads, kShipDo>;
+    if constexpr (P >= AG_STREAM_MIN_P)  // the full mix at P >= 3: streamed, 768 lanes
+      if (bt == kMidThreads && general == kGenAll) return k_simulate<P, 6, true, 1, kGenAll, kMidThreads, kShipDo>;
     if (bt != kThreads) return nullptr;
     if (general == kGenTruthful) return k_simulate<P, 6, true, 1, kGenTruthful, kThreads, kShipDo>;
     return k_simulate<P, 6, true, 1, kGenAll, kThreads, kShipDo>;

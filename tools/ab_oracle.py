@@ -27,8 +27,10 @@ def main():
     inp = eng.alloc_inputs(B)
     eng.generate(0, 0, inp)
     fields = ("winner", "price", "outcome", "item", "bid", "est_ctr", "true_ctr", "best_ev")
-    # variants: (generic kernel?, blocks per CU)
-    variants = [(False, 0), (True, 0), (False, 1), (False, 2), (False, 3), (False, 4)]
+    # variants: (generic kernel?, blocks per CU); AG_AB_BPC="4,5,6": only k_oracle at those
+    bpc = os.environ.get("AG_AB_BPC")
+    variants = ([(False, int(x)) for x in bpc.split(",")] if bpc else
+                [(False, 0), (True, 0), (False, 1), (False, 2), (False, 3), (False, 4)])
     out = {v: eng.alloc_outputs(B, fields) for v in variants}
     cnt = {v: eng.new_counters() for v in variants}
     st = torch.cuda.current_stream()
