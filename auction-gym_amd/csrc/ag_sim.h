@@ -34,6 +34,10 @@ namespace ag {
                                 // configs_2 0.212 -> 0.203 ms, configs_3 0.129 -> 0.121 ms in one
                                 // process (profiles/r03s11_ab_w4.log)
 #endif
+#ifndef AG_TB_WIDE_MIN_WAVES
+#define AG_TB_WIDE_MIN_WAVES 3  // ... at P >= 3 (streamed slots): 168 VGPRs, 2 spilled instead of 81;
+                                // configs_1 at P = 8 0.658 -> 0.558 ms (profiles/r04o_ab_c1p8_tb3.log)
+#endif
 #ifndef AG_TB_MIN_WAVES
 #define AG_TB_MIN_WAVES 4  // the general kernel for truthful bidders only: <= 128 VGPRs
 #endif
@@ -815,7 +819,7 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
 // scratch per lane). K stays a runtime value: with it compile-time the item loops unroll
 // fully and spill (200 VGPRs at P = 2), measured.
 template <int P, int D, bool PRUNE, int W, int GENERAL, int BT = kThreads, int DOS = 0>
-__global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? AG_TB_MIN_WAVES
+__global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_MIN_WAVES : AG_TB_MIN_WAVES)
                                  : (GENERAL ? ((DOS && P > 0 && P <= 2) ? AG_GEN_DOS_MIN_WAVES : AG_GEN_MIN_WAVES)
                                             : AG_MIN_WAVES)) void k_simulate(SimParams prm) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

@@ -9,6 +9,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -32,14 +33,15 @@ def main():
             return None, 0
         return f["FETCH_SIZE"] * 2 * 1024 + w["WRITE_SIZE"] * 1024, min(nf, nw)
 
-    def step_counter(path, name):
-        """(mean per step of the counter summed over the step's kernels, steps, kernel names)"""
+    def step_counter(path, name, P):
+        """(mean per step of the counter summed over the step's kernels -- those of P
+        participants: a pass's command may run other lines too --, steps, kernel names)"""
         fs = glob.glob(os.path.join(d, path, "**", "*counter_collection.csv"), recursive=True)
         if not fs:
             return None, 0, []
         per, kern = collections.OrderedDict(), {}
         for r in csv.DictReader(open(fs[0])):
-            if r["Counter_Name"] == name:
+            if r["Counter_Name"] == name and re.search(rf"<{P}, ", r["Kernel_Name"]):
                 i = int(r["Dispatch_Id"])
                 per[i] = per.get(i, 0.0) + float(r["Counter_Value"])
                 kern[i] = r["Kernel_Name"]
@@ -48,14 +50,19 @@ def main():
         steps = len(ids) / len(names)
         return sum(per[i] for i in ids) / steps, int(steps), names
 
-    def step_traffic(fetch, write):
-        f, nf, names = step_counter(fetch, "FETCH_SIZE")
-        w, nw, _ = step_counter(write, "WRITE_SIZE")
+    def step_traffic(fetch, write, P):
+        f, nf, names = step_counter(fetch, "FETCH_SIZE", P)
+        w, nw, _ = step_counter(write, "WRITE_SIZE", P)
         if f is None or w is None:
             return None, 0, []
         return f * 2 * 1024 + w * 1024, min(nf, nw), [n.split("(")[0] for n in names]
 
+    head_dir = os.environ.get("HEAD_DIR")  # the headline passes of another run (same build)
+    if head_dir:
+        d_pop, d = d, head_dir
     t, n = traffic("fetch", "write")
+    if head_dir:
+        d = d_pop
     B = bench["config"]["auctions_per_gpu_per_step"]
     if t is None:  # no headline pass in this run (k_oracle unchanged): keep the committed one
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
@@ -68,7 +75,7 @@ def main():
                     "over_algorithmic": t / (bench["roofline"]["algorithmic_bytes_per_auction"] * B)})
     for c in ("1", "2", "3", "4", "1p8", "4p8"):
         key = f"configs_{c[0]}" + ("_p8" if c.endswith("p8") else "")
-        t, n, names = step_traffic(f"c{c}_fetch", f"c{c}_write")
+        t, n, names = step_traffic(f"c{c}_fetch", f"c{c}_write", 8 if c.endswith("p8") else 2)
         if t is None or key not in bench:
             continue
         b = bench[key]["auctions_per_gpu_per_step"]

@@ -12,8 +12,8 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 HEAD="python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-ts --no-populations --no-generate"
-ts() { echo "python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-update --no-populations --no-generate --batch 1048576 ${1:-}"; }
-pop() { echo "python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-ts --no-update --no-generate --batch 1048576 --populations $1 ${2:-}"; }
+ts() { echo "python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-update --no-populations --no-generate --batch 1048576 ${1:---no-p8}"; }
+pop() { echo "python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-ts --no-update --no-generate --batch 1048576 --populations $1 ${2:---no-p8}"; }
 HK='k_oracle<2, 6, false>'
 GK='k_simulate'
 SQA="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM"
