@@ -493,8 +493,8 @@ def build_population(key, local, P=2):
 def _record_parallel(bk, world):
     from auctiongym_amd.sharding import record_parallel_pays
     learners = [a for a in range(len(bk)) if bk[a] >= 2]
-    if LEARNER_PARALLEL != "auto":
-        return LEARNER_PARALLEL == "record" and world > 1
+    if LEARNER_PARALLEL != "auto":  # (forced "record" at N = 1: the per-epoch launches, no exchange)
+        return LEARNER_PARALLEL == "record"
     return all(bk[a] in (2, 4) for a in learners) and record_parallel_pays(len(learners), world)
 
 
