@@ -38,7 +38,13 @@ constexpr int kWrEpochs = 32768, kInitEpochs = 16384, kDrEpochs = 32768;
 constexpr int64_t kBidderChunk = 8192;  // records per workgroup of a PolicyLearningBidder (default)
 constexpr int64_t kMinChunk = 1024;     // fewest records per workgroup of an exact-sum learner's split
 constexpr size_t kRecLdsBytes0 = 32 * 1024;  // record cache per workgroup, win-rate phase (4 per CU)
-constexpr size_t kRecLdsBytes = 72 * 1024;   // record cache per workgroup, later fits (2 per CU)
+#ifndef AG_DR_REC_LDS
+#define AG_DR_REC_LDS (48 * 1024)  // (3 workgroups per CU: profiles/r04r_ab_trainer_*.log)
+#endif
+#ifndef AG_DR_PH1_MIN_WAVES
+#define AG_DR_PH1_MIN_WAVES 3  // the later fits: <= 168 VGPRs, 3 waves per SIMD (FP_DR_TS update 1.96 -> 1.69 s)
+#endif
+constexpr size_t kRecLdsBytes = AG_DR_REC_LDS;  // record cache per workgroup, later fits
 constexpr double kGrid = 0x1p40, kInv = 0x1p-40;
 constexpr int64_t kLo24 = (int64_t(1) << 24) - 1;
 
@@ -933,7 +939,7 @@ __device__ int fit_pl(const RecView &V, const Chunk &K, TrainLds &S, Coop &C, in
 // -2 NaN loss, -3 out of noise epochs (state not written); epochs [3] = (win-rate,
 // imitation, policy fit); traces [3][32768] (workgroup 0).
 template <int PH>
-__global__ __launch_bounds__(kDrThreads, PH == 0 ? 4 : 1) void k_bidder_train(
+__global__ __launch_bounds__(kDrThreads, PH == 0 ? 4 : AG_DR_PH1_MIN_WAVES) void k_bidder_train(
     const int32_t *__restrict__ bkind, const int32_t *__restrict__ bmode, const int32_t *__restrict__ blk_agent,
     const int32_t *__restrict__ blk_rank, const int32_t *__restrict__ agent_nblk,
     const int64_t *__restrict__ offsets, DrRecords R0, double *__restrict__ eu_ws, float *__restrict__ state,
@@ -1331,7 +1337,7 @@ __global__ __launch_bounds__(kDrThreads) void k_bidder_epoch(
 // learner per launch (k_bidder_train) or per epoch (k_bidder_epoch) waits out is hidden
 // behind useful work. Integer sums: the same models, epochs and status bit for bit as both.
 //   PH = 0: the win count and the win-rate fit (4 workgroups per CU, <= 128 VGPRs);
-//   PH = 1: estimated utilities, imitation, the policy fits (2 per CU).
+//   PH = 1: estimated utilities, imitation, the policy fits (3 per CU).
 // A policy fit whose host-drawn noise window ends waits with its state kept (need_noise);
 // the launch ends when no learner has an epoch left in its phase.
 constexpr int kPipeMaxAgents = 16;
@@ -1442,7 +1448,7 @@ struct PipeSlot {
 };
 
 template <int PH>
-__global__ __launch_bounds__(kDrThreads, PH == 0 ? 4 : 2) void k_bidder_pipe(PipeArgs A) {
+__global__ __launch_bounds__(kDrThreads, PH == 0 ? 4 : AG_DR_PH1_MIN_WAVES) void k_bidder_pipe(PipeArgs A) {
   __shared__ TrainLds S;
   __shared__ float s_grad[16], s_loss;
   __shared__ int s_np;
@@ -1709,11 +1715,11 @@ static DrRecords sorted_view(ag_dr_ws &w, int64_t n, double **eu) {
                    (const uint8_t *)((uint32_t *)((uint64_t *)(b + 6 * cap) + 2 * cap) + 2 * cap)};
 }
 
-// k_bidder_pipe's record-cache budgets (dynamic LDS per workgroup: 4 / 2 per CU) and the
+// k_bidder_pipe's record-cache budgets (dynamic LDS per workgroup: 4 / 3 per CU) and the
 // records per workgroup it aims at (AG_PIPE_RECS overrides, for tuning): fewer workgroups for
 // small learners -- a shorter tree to climb each epoch -- and the whole resident grid for
 // large ones
-constexpr size_t kPipeLds[2] = {32 * 1024, 72 * 1024};
+constexpr size_t kPipeLds[2] = {32 * 1024, 44 * 1024};
 constexpr int64_t kPipeRecs = 512;
 
 struct PipeNoise {

@@ -730,6 +730,8 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
       for (int d = 0; d < D; ++d) xo[d] = d < Do - 1 ? (float)x[d] : (d == Do - 1 ? 1.0f : 0.0f);
       // the agent's own Ka items: its torch model's rows (the sgemv block / remainder rows and
       // the sigmoid's chunks follow Ka); the catalogue rows beyond are padding (value 0)
+      // (per-agent Ka even when every agent has K: the uniform-K form, scalar item loops, ran
+      // 2-4 % slower on every population line, profiles/r04s_ab_c*_kag.log)
       const int Ka = T.kag[a];
       best = ts_select<D>(m, xo, nz, Ka, Do, T.vals + a * T.values_stride, T.tab);
       est = (double)ts_ctr_k<D>(m + best * Do, xo, xo, false, Do, best, Ka, T.tab);
