@@ -37,9 +37,15 @@ constexpr int kDrThreads = 256;
 constexpr int kWrEpochs = 32768, kInitEpochs = 16384, kDrEpochs = 32768;
 constexpr int64_t kBidderChunk = 8192;  // records per workgroup of a PolicyLearningBidder (default)
 constexpr int64_t kMinChunk = 1024;     // fewest records per workgroup of an exact-sum learner's split
-constexpr size_t kRecLdsBytes0 = 32 * 1024;  // record cache per workgroup, win-rate phase (4 per CU)
+#ifndef AG_DR_REC_LDS0
+#define AG_DR_REC_LDS0 (32 * 1024)
+#endif
+constexpr size_t kRecLdsBytes0 = AG_DR_REC_LDS0;  // record cache per workgroup, win-rate phase (4 per CU)
 #ifndef AG_DR_REC_LDS
 #define AG_DR_REC_LDS (48 * 1024)  // (3 workgroups per CU: profiles/r04r_ab_trainer_*.log)
+#endif
+#ifndef AG_DR_PH0_MIN_WAVES
+#define AG_DR_PH0_MIN_WAVES 4  // the win-rate fits: <= 128 VGPRs
 #endif
 #ifndef AG_DR_PH1_MIN_WAVES
 #define AG_DR_PH1_MIN_WAVES 3  // the later fits: <= 168 VGPRs, 3 waves per SIMD (FP_DR_TS update 1.96 -> 1.69 s)
@@ -939,7 +945,7 @@ __device__ int fit_pl(const RecView &V, const Chunk &K, TrainLds &S, Coop &C, in
 // -2 NaN loss, -3 out of noise epochs (state not written); epochs [3] = (win-rate,
 // imitation, policy fit); traces [3][32768] (workgroup 0).
 template <int PH>
-__global__ __launch_bounds__(kDrThreads, PH == 0 ? 4 : AG_DR_PH1_MIN_WAVES) void k_bidder_train(
+__global__ __launch_bounds__(kDrThreads, PH == 0 ? AG_DR_PH0_MIN_WAVES : AG_DR_PH1_MIN_WAVES) void k_bidder_train(
     const int32_t *__restrict__ bkind, const int32_t *__restrict__ bmode, const int32_t *__restrict__ blk_agent,
     const int32_t *__restrict__ blk_rank, const int32_t *__restrict__ agent_nblk,
     const int64_t *__restrict__ offsets, DrRecords R0, double *__restrict__ eu_ws, float *__restrict__ state,
