@@ -33,6 +33,10 @@ for s in ${STEPS:-bench head pops sq stats}; do
         pmc c${c}_fetch "$GK" FETCH_SIZE $(pop configs_$c) && pmc c${c}_write "$GK" WRITE_SIZE $(pop configs_$c) || exit 1
       done &&
       pmc c4p8_fetch "$GK" FETCH_SIZE $(pop configs_4 --p8-only) && pmc c4p8_write "$GK" WRITE_SIZE $(pop configs_4 --p8-only) ;;
+    p8)
+      pmc c1p8_fetch "$GK" FETCH_SIZE $(ts "--p8-only") && pmc c1p8_write "$GK" WRITE_SIZE $(ts "--p8-only") &&
+      pmc c4p8_fetch "$GK" FETCH_SIZE $(pop configs_4 --p8-only) && pmc c4p8_write "$GK" WRITE_SIZE $(pop configs_4 --p8-only) &&
+      pmc c4p8_sqA "$GK" "$SQA" $(pop configs_4 --p8-only) && pmc c4p8_sqB "$GK" "$SQB" $(pop configs_4 --p8-only) ;;
     sq)
       pmc c1_sqA "$GK" "$SQA" $(ts) && pmc c1_sqB "$GK" "$SQB" $(ts) &&
       for c in 2 4; do
