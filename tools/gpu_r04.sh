@@ -20,6 +20,7 @@ for s in ${STEPS:-smoke configs suite bench}; do
     dropin) step dropin_dr 600 python tools/dropin_update_time.py dr 2 && step dropin_dm 600 python tools/dropin_update_time.py dm 2 ;;
     suite) step pytest_gpu 1200 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
     bench) step bench_driver 400 python bench.py --steps 20 --warmup 5 ;;
+    bench_default) step bench_default 600 python bench.py ;;
     ab_stream)
       step ab_c4p8 300 python tools/ab_pop.py configs_4:8 nostream stream1 &&
       step ab_c1p8 300 python tools/ab_pop.py configs_1:8 generic &&
