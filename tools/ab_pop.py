@@ -7,7 +7,9 @@ interleaved in ONE process; outputs and counters checked equal across builds.
     AG_AB_DENSE=1: the dense Thompson-noise layout instead of the compact one.
     A variant named "generic" is the base library with AG_SIM_KERNEL_GENERIC (k_simulate
     instead of the dedicated kernels), "<variant>+generic" that variant with it; "bt256" /
-    "bt1024" force the workgroup size.
+    "bt1024" force the workgroup size; "grouporder" is the base library reading the compact
+    Thompson noise with its pairs ranked in (64-auction group, slot, auction) order instead of
+    ag_ts_noise_index's (slot, auction) order (one contiguous run per wave over all its slots).
 """
 import os
 import sys
@@ -31,7 +33,7 @@ def main():
         key, P = key.split(":")[0], int(key.split(":")[1])
     vdir = os.path.join(ROOT, "auction-gym_amd", "build", "variants")
     paths = {"base": _lib.LIB_PATH}
-    special = {"generic", "wide", "bt256", "bt1024", "nocnt", "noship"}
+    special = {"generic", "wide", "bt256", "bt1024", "nocnt", "noship", "grouporder"}
     for n in sys.argv[2:]:  # "<variant>+generic": that build with k_simulate forced
         v = n[:-len("+generic")] if n.endswith("+generic") else n
         paths[n] = _lib.LIB_PATH if v in special else os.path.join(vdir, f"libauctiongym_hip_{v}.so")
@@ -68,6 +70,19 @@ def main():
         eng.generate(1, 0, inp)
         compact = not os.environ.get("AG_AB_DENSE") and bool((ak == 1).any() and (ak != 1).any())
         eng.generate_noise(1, 0, inp, compact=compact)
+        if n == "grouporder" and compact:  # the same draws, pairs ranked in (i / 64, slot, i) order
+            from auctiongym_amd.engine import _ptr, _stream
+            fl = torch.from_numpy(ak).to(inp["part"].device)[inp["part"].long()] == 1
+            Pn, Bn = fl.shape
+            T = (Bn + 63) // 64
+            fp = torch.zeros((Pn, T * 64), dtype=torch.int64, device=fl.device)
+            fp[:, :Bn] = fl
+            r = torch.cumsum(fp.view(Pn, T, 64).transpose(0, 1).flatten(), 0) - 1
+            r = r.view(T, Pn, 64).transpose(0, 1).reshape(Pn, T * 64)[:, :Bn]
+            inp["ts_noise_index"] = torch.where(fl, r, -1).to(torch.int32).contiguous()
+            eng._check(eng.L.ag_generate_ts_noise_compact(eng._h, 1, 0, B, _ptr(inp["part"]),
+                                                          _ptr(inp["ts_noise_index"]), _ptr(inp["ts_noise"]),
+                                                          _stream()), "ag_generate_ts_noise_compact")
         out = eng.alloc_outputs(B)
         cnt = None if n == "nocnt" else eng.new_counters()
         runs[n] = (eng, inp, out, cnt)

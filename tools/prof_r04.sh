@@ -37,6 +37,7 @@ for s in ${STEPS:-bench head pops sq stats}; do
       pmc c1p8_fetch "$GK" FETCH_SIZE $(ts "--p8-only") && pmc c1p8_write "$GK" WRITE_SIZE $(ts "--p8-only") &&
       pmc c4p8_fetch "$GK" FETCH_SIZE $(pop configs_4 --p8-only) && pmc c4p8_write "$GK" WRITE_SIZE $(pop configs_4 --p8-only) &&
       pmc c4p8_sqA "$GK" "$SQA" $(pop configs_4 --p8-only) && pmc c4p8_sqB "$GK" "$SQB" $(pop configs_4 --p8-only) ;;
+    c4) pmc c4_fetch "$GK" FETCH_SIZE $(pop configs_4) && pmc c4_write "$GK" WRITE_SIZE $(pop configs_4) ;;
     sq)
       pmc c1_sqA "$GK" "$SQA" $(ts) && pmc c1_sqB "$GK" "$SQB" $(ts) &&
       for c in 2 4; do
@@ -52,6 +53,15 @@ for s in ${STEPS:-bench head pops sq stats}; do
       timeout -k 10 300 rocprofv3 --pmc $CTR --kernel-include-regex "k_bidder_train|k_lrts_train" --output-format csv -d "$OUT/$s" -o run -- $UPD > "$OUT/$s.log" 2>&1
       echo "rc=$?"
       break ;;
+    sizes)  # the L2's memory-side read / write requests by size: calibrates FETCH_SIZE x 2 on the
+      # headline (16 B per lane, known bytes) against the general kernel's 4-B-per-lane noise reads
+      rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1 || true
+      CS=$(grep -o 'TCC_EA0_\(RD\|WR\)REQ[A-Z0-9_]*' "$OUT/avail.txt" | sed 's/_*$//' | sort -u | tr '\n' ' ')
+      echo "tcc request counters: $CS"
+      for c in $CS; do
+        pmc "hd_$c" "$HK" "${c}_sum" $HEAD && pmc "c4p8_$c" "$GK" "${c}_sum" $(pop configs_4 --p8-only) &&
+        pmc "c1_$c" "$GK" "${c}_sum" $(ts) || exit 1
+      done ;;
     stats) step kernel_stats 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
   esac
 done
