@@ -39,7 +39,9 @@ namespace ag {
                                 // configs_1 at P = 8 0.658 -> 0.558 ms (profiles/r04o_ab_c1p8_tb3.log)
 #endif
 #ifndef AG_TB_MIN_WAVES
-#define AG_TB_MIN_WAVES 4  // the general kernel for truthful bidders only: <= 128 VGPRs
+#define AG_TB_MIN_WAVES 4  // the general kernel for truthful bidders only: <= 128 VGPRs (115, none
+                           // spilled; 5 waves: 96 VGPRs, 22 spilled, configs_1 0.160 -> 0.174 ms in
+                           // one process, profiles/r04_ab_tb5.log)
 #endif
 #ifndef AG_TS_SCREEN
 #define AG_TS_SCREEN 1  // screened Thompson item choice (ts_select)
