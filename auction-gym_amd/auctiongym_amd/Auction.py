@@ -25,7 +25,7 @@ import torch
 
 from . import Agent as _agent_mod
 from . import _lib
-from .engine import AuctionEngine
+from .engine import TORCH_NORMAL_AVX2, AuctionEngine
 from .replay import draw_round, draw_round_population, draw_rounds_native, draw_rounds_native_population
 
 C = _agent_mod.C
@@ -192,10 +192,10 @@ class Auction:
             search = [x == _lib.LEARNER_SEARCH for x in ls]
         return shading, models, policy, search
 
-    # torch CPU builds whose float normal_ of >= 16 elements runs normal_fill_16_AVX2 (the
-    # kernel ag_replay.cpp restates: compiled under __AVX2__, which the AVX512 build defines
-    # too); the DEFAULT build takes the scalar normal_fill with libm logf / cosf
-    _TORCH_NORMAL_AVX2 = ("AVX2", "AVX512")
+    # torch CPU builds whose float normal_ of >= 16 elements runs the kernel ag_replay.cpp
+    # restates (engine.TORCH_NORMAL_AVX2; the learner fits' draws are gated the same way in
+    # engine.torch_normal_epochs)
+    _TORCH_NORMAL_AVX2 = TORCH_NORMAL_AVX2
 
     def _native_draws(self):
         """True when the draws can be made in C for a whole batch: numpy's Generator on PCG64

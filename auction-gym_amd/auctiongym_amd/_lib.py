@@ -49,7 +49,7 @@ EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params
            "ag_abi_version", "ag_ts_noise_index", "ag_generate_ts_noise_compact", "ag_torch_normal_epochs",
            "ag_bidder_rp_begin", "ag_bidder_rp_epoch", "ag_bidder_rp_run", "ag_bidder_rp_noise", "ag_bidder_rp_poll", "ag_bidder_rp_end",
            "ag_lrts_rp_begin", "ag_lrts_rp_epoch", "ag_lrts_rp_poll", "ag_lrts_rp_end", "ag_empirical_update_agents")
-ABI_VERSION = 16
+ABI_VERSION = 17
 LEARNER_UNINITIALISED, LEARNER_POLICY, LEARNER_SEARCH = 0, 1, 2
 VL_SEARCH, VL_POLICY = 0, 1
 PL_LOSSES = {"REINFORCE": 0, "REINFORCE_offpolicy": 1, "TRPO": 2, "PPO": 3}
@@ -85,7 +85,8 @@ class AgBatchOut(_Sized):
                 ("second_price", ctypes.c_void_p), ("outcome", ctypes.c_void_p),
                 ("item", ctypes.c_void_p), ("bid", ctypes.c_void_p), ("est_ctr", ctypes.c_void_p),
                 ("true_ctr", ctypes.c_void_p), ("best_ev", ctypes.c_void_p),
-                ("gamma", ctypes.c_void_p), ("propensity", ctypes.c_void_p)]
+                ("gamma", ctypes.c_void_p), ("propensity", ctypes.c_void_p),
+                ("winner_outcome", ctypes.c_void_p), ("record", ctypes.c_void_p)]  # ABI 17
 
 
 class AgLrtsSamples(_Sized):

@@ -18,8 +18,51 @@ NUM_COUNTERS = _lib.NUM_COUNTERS
 FX_LIMBS = _lib.FX_LIMBS
 
 _OUT_FIELDS = ("winner", "price", "second_price", "outcome", "item", "bid", "est_ctr",
-               "true_ctr", "best_ev", "gamma", "propensity")
+               "true_ctr", "best_ev", "gamma", "propensity", "winner_outcome", "record")
 _CORE_FIELDS = _OUT_FIELDS[:9]
+# ABI 17 packed record layout (include/auctiongym.h): winner | outcome << 31, the per-slot
+# {bid, est_ctr, true_ctr, best_ev} record, and the item and price arrays of the per-field form
+PACKED_FIELDS = ("winner_outcome", "price", "item", "record")
+# the headline's output set: every per-field array, winner and outcome as the packed word (the
+# 1-B outcome stream alone cost 6 % of k_oracle's time, profiles/r05c_ab_packed.log; the
+# record form of the other four was no faster than their arrays)
+HEADLINE_FIELDS = ("winner_outcome", "price", "item", "bid", "est_ctr", "true_ctr", "best_ev")
+REC_LAYOUT = 2  # csrc/ag_record.h kRecLayout: 64-auction tiles of (bid, est) / (true, best_ev) pairs
+_REC_FIELDS = ("bid", "est_ctr", "true_ctr", "best_ev")
+
+
+def record_doubles(P, B):
+    """Doubles of a packed record array (every layout fits P * ceil(B / 64) * 256)."""
+    return P * ((B + 63) // 64) * 256
+
+
+def record_field(record, P, B, f, layout=REC_LAYOUT):
+    """Field f (0 bid, 1 est_ctr, 2 true_ctr, 3 best_ev) of a packed record as a [P][B] view."""
+    T = (B + 63) // 64
+    r = record.reshape(P, -1)
+    if layout == 0:
+        return r[:, :B * 4].reshape(P, B, 4)[:, :, f]
+    if layout == 1:
+        return r[:, :T * 256].reshape(P, T, 4, 64)[:, :, f, :].reshape(P, T * 64)[:, :B]
+    return r[:, :T * 256].reshape(P, T, 2, 64, 2)[:, :, f // 2, :, f % 2].reshape(P, T * 64)[:, :B]
+
+
+def unpack_outputs(outputs, P=None, B=None, layout=REC_LAYOUT):
+    """Per-field views of a packed output dict (winner, outcome, bid, est_ctr, true_ctr,
+    best_ev from winner_outcome / record), for comparing the two layouts."""
+    o = dict(outputs)
+    if "winner_outcome" in o:
+        wo = o["winner_outcome"].to(torch.int64) & 0xffffffff
+        o["winner"] = (wo & 0x7fffffff).to(torch.int32)
+        o["outcome"] = (wo >> 31).to(torch.uint8)
+    if "record" in o:
+        if B is None:
+            B = o["winner_outcome"].shape[0] if "winner_outcome" in o else o["price"].shape[0]
+        if P is None:
+            P = o["record"].shape[0]
+        for j, f in enumerate(_REC_FIELDS):
+            o[f] = record_field(o["record"], P, B, j, layout)
+    return o
 
 
 def _ptr(t):
@@ -286,14 +329,16 @@ class AuctionEngine:
 
     def alloc_outputs(self, B, fields=None):
         if fields is None:
-            fields = _OUT_FIELDS if getattr(self, "shading", False) else _CORE_FIELDS
+            fields = _OUT_FIELDS[:11] if getattr(self, "shading", False) else _CORE_FIELDS
         d, P = self.device, self.P
         spec = {"winner": ((B,), torch.int32), "price": ((B,), torch.float64),
                 "second_price": ((B,), torch.float64), "outcome": ((B,), torch.uint8),
                 "item": ((P, B), torch.int32), "bid": ((P, B), torch.float64),
                 "est_ctr": ((P, B), torch.float64), "true_ctr": ((P, B), torch.float64),
                 "best_ev": ((P, B), torch.float64), "gamma": ((P, B), torch.float64),
-                "propensity": ((P, B), torch.float64)}
+                "propensity": ((P, B), torch.float64),
+                "winner_outcome": ((B,), torch.int32),
+                "record": ((P, record_doubles(1, B)), torch.float64)}
         return {k: torch.empty(spec[k][0], dtype=spec[k][1], device=d) for k in fields}
 
     def new_counters(self):
@@ -316,7 +361,7 @@ class AuctionEngine:
         """Generate mode (ag_simulate_generated): B = outputs["winner"].shape[0] rounds whose
         inputs are drawn inside the kernel -- the same bits generate(seed, first_auction)
         writes -- so only the outputs touch HBM."""
-        B = outputs["winner"].shape[0]
+        B = (outputs["winner"] if "winner" in outputs else outputs["winner_outcome"]).shape[0]
         bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
         self._check(self.L.ag_simulate_generated(self._h, int(seed), int(first_auction), B, ctypes.byref(bo),
                                                  _ptr(counters), _stream()), "ag_simulate_generated")
@@ -606,11 +651,30 @@ class AuctionEngine:
         return out.reshape(fx.shape[:-1])
 
 
+# torch CPU builds whose float normal_ of >= 16 elements runs normal_fill_16_AVX2 (the kernel
+# ag_replay.cpp restates: compiled under __AVX2__, which the AVX512 build defines too); the
+# DEFAULT build takes the scalar normal_fill with libm logf / cosf over the whole tensor
+TORCH_NORMAL_AVX2 = ("AVX2", "AVX512")
+
+
 def torch_normal_epochs(state, n, epochs):
     """`epochs` x torch.empty(n).normal_() from the torch CPU generator state blob `state`
     (numpy uint8 [5056], advanced in place): float32 [epochs][n] (ag_torch_normal_epochs, the C
-    restatement of torch's normal kernels; the same numbers as the calls themselves)."""
+    restatement of torch's normal kernels; the same numbers as the calls themselves). On a torch
+    build without the vectorised kernel the C restatement does not apply to n >= 16: the draws
+    are then torch's own calls from `state` (the caller's generator state is left as it was)."""
     from . import _lib
+    if n >= 16 and torch.backends.cpu.get_cpu_capability() not in TORCH_NORMAL_AVX2:
+        saved = torch.get_rng_state()
+        try:
+            torch.set_rng_state(torch.from_numpy(state.copy()))
+            out = np.empty((int(epochs), int(n)), np.float32)
+            for e in range(int(epochs)):
+                out[e] = torch.empty(int(n)).normal_().numpy()
+            state[:] = torch.get_rng_state().numpy()
+        finally:
+            torch.set_rng_state(saved)
+        return out
     L = _lib.load()
     out = np.empty((int(epochs), int(n)), np.float32)
     rc = L.ag_torch_normal_epochs(state.ctypes.data, state.nbytes, int(n), int(epochs), out.ctypes.data)

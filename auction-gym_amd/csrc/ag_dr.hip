@@ -1634,7 +1634,8 @@ __global__ __launch_bounds__(kDrThreads, PH == 0 ? 4 : AG_DR_PH1_MIN_WAVES) void
 
 // the learners' FitSt at the start of a resumable update (state16: win-rate model, policy)
 __global__ void k_rp_init(int N, const int32_t *__restrict__ bkind, const int32_t *__restrict__ bmode,
-                          const int32_t *__restrict__ mask, const float *__restrict__ state, FitSt *__restrict__ st) {
+                          const int32_t *__restrict__ mask, const float *__restrict__ state, FitSt *__restrict__ st,
+                          int parities) {
   const int a = blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= N) return;
   FitSt f;
@@ -1647,6 +1648,8 @@ __global__ void k_rp_init(int N, const int32_t *__restrict__ bkind, const int32_
   else
     fit_enter(f, kFitDone, bk, bmode[a]);
   st[a] = f;
+  if (parities == 2) st[N + a] = f;  // [2][N] states: parity 1 too -- the epoch launches never
+                                     // write unmasked agents' rows
 }
 
 __global__ __launch_bounds__(kDrThreads) void k_sh_hist(const int32_t *__restrict__ agent, int64_t n, int N,
@@ -2195,7 +2198,7 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agen
     int32_t *d_pmask = (int32_t *)(pst + N);
     AG_HIP(hipMemcpyAsync(d_pmask, pipe_mask.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_rp_init, dim3((N + 255) / 256), dim3(256), 0, st, N, c->d_bkind, w.mode, d_pmask, w.state,
-                       pst);
+                       pst, 1);
     AG_HIP(hipGetLastError());
     // n_total = the counts (w.counts [N]); noise: agent a's draws of epoch e at noise_offsets[a] + e n_a
     PipeNoise nz;
@@ -2316,19 +2319,24 @@ int ag_bidder_rp_begin(ag_ctx *c, const ag_shading_samples *s, const int32_t *ag
     }
   }
   const int G = (int)blk_agent.size();
-  if ((size_t)G > rp.cap_g || (size_t)lines > rp.cap_lines || !rp.st) {
+  if ((size_t)G > rp.cap_g || (size_t)lines > rp.cap_lines || !rp.st || !rp.acc || !rp.tables) {
     (void)hipFree(rp.st);
     (void)hipFree(rp.acc);
     (void)hipFree(rp.tables);
     rp.st = nullptr;
     rp.acc = nullptr;
     rp.tables = nullptr;
-    rp.cap_g = (size_t)G + 64;
-    rp.cap_lines = (size_t)lines + 16;
+    // capacities zero until every buffer is allocated: a failed allocation leaves the
+    // workspace empty, and the next call allocates it again
+    rp.cap_g = 0;
+    rp.cap_lines = 0;
+    const size_t cap_g = (size_t)G + 64, cap_lines = (size_t)lines + 16;
     AG_HIP(hipMalloc(&rp.st, sizeof(FitSt) * 2 * (size_t)N));
     // accumulator rows and barrier lines: [cap_lines][32] each
-    AG_HIP(hipMalloc(&rp.acc, (sizeof(int64_t) + sizeof(unsigned)) * 32 * rp.cap_lines));
-    AG_HIP(hipMalloc(&rp.tables, sizeof(int32_t) * (2 * rp.cap_g + 3 * (size_t)N) + sizeof(int64_t) * 2 * N + 16));
+    AG_HIP(hipMalloc(&rp.acc, (sizeof(int64_t) + sizeof(unsigned)) * 32 * cap_lines));
+    AG_HIP(hipMalloc(&rp.tables, sizeof(int32_t) * (2 * cap_g + 3 * (size_t)N) + sizeof(int64_t) * 2 * N + 16));
+    rp.cap_g = cap_g;
+    rp.cap_lines = cap_lines;
   }
   rp.bar = (unsigned *)(rp.acc + 32 * rp.cap_lines);
   int32_t *d_bagent = rp.tables, *d_brank = d_bagent + rp.cap_g, *d_nblk = d_brank + rp.cap_g,
@@ -2355,7 +2363,7 @@ int ag_bidder_rp_begin(ag_ctx *c, const ag_shading_samples *s, const int32_t *ag
   if (lines) AG_HIP(hipMemsetAsync(rp.acc, 0, (sizeof(int64_t) + sizeof(unsigned)) * 32 * rp.cap_lines, st));
   AG_HIP(hipMemsetAsync(totals, 0, sizeof(int64_t) * 2 * 32 * (size_t)N, st));
   hipLaunchKernelGGL(k_rp_init, dim3((N + 255) / 256), dim3(256), 0, st, N, c->d_bkind, w.mode, d_mask, w.state,
-                     (FitSt *)rp.st);
+                     (FitSt *)rp.st, 2);
   AG_HIP(hipGetLastError());
   if (int rc = dr_ws_ready(c)) return rc;  // the Adam table
   rp.G = G;

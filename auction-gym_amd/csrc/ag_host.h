@@ -33,6 +33,33 @@ inline int ag_check_struct(const T *p, const char *who, const char *type) {
     if (int rc_ = ag_check_struct(p, who, type)) return rc_; \
   } while (0)
 
+// ag_batch_out of ABI 17 or of ABI 15/16 (AG_BATCH_OUT_V16_SIZE: no packed fields), read into
+// a full ABI-17 struct `v` (the packed fields NULL for the older layout); the packed record
+// must be 16-B aligned (it is written with 16-B stores).
+inline int ag_read_out(const ag_batch_out *p, ag_batch_out *v, const char *who) {
+  if (!p) return ag_set_error(AG_ERR_INVALID, "%s: null ag_batch_out", who);
+  if (p->struct_size == (uint64_t)sizeof(ag_batch_out)) {
+    *v = *p;
+  } else if (p->struct_size == AG_BATCH_OUT_V16_SIZE) {
+    *v = ag_batch_out{};
+    __builtin_memcpy(v, p, AG_BATCH_OUT_V16_SIZE);
+    v->struct_size = sizeof(ag_batch_out);
+  } else {
+    return ag_set_error(AG_ERR_INVALID,
+                        "%s: ag_batch_out.struct_size is %llu, this library (ABI %d) expects %llu (or %llu, "
+                        "the ABI 16 layout) -- the caller's binding declares another layout of include/auctiongym.h",
+                        who, (unsigned long long)p->struct_size, AG_ABI_VERSION,
+                        (unsigned long long)sizeof(ag_batch_out), (unsigned long long)AG_BATCH_OUT_V16_SIZE);
+  }
+  if (((uintptr_t)v->record & 15u) != 0)
+    return ag_set_error(AG_ERR_INVALID, "%s: ag_batch_out.record must be 16-B aligned", who);
+  return AG_OK;
+}
+#define AG_READ_OUT(p, v, who) \
+  do {                         \
+    if (int rc_ = ag_read_out(p, &(v), who)) return rc_; \
+  } while (0)
+
 // LR-TS training workspace (ag_lrts.hip), grown on demand by ag_lrts_update.
 struct ag_lrts_ws {
   int64_t cap = 0;            // samples the bucket arrays hold

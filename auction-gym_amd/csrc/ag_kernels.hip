@@ -448,6 +448,8 @@ int simulate_oracle(ag_ctx *c, OraKernel k, int64_t B, const ag_batch_in *in, co
   prm.est_ctr = out->est_ctr;
   prm.true_ctr = out->true_ctr;
   prm.best_ev = out->best_ev;
+  prm.winner_outcome = out->winner_outcome;
+  prm.record = out->record;
   prm.partials = c->d_partials;
   const size_t lds = (size_t)prm.L.total;
   if (lds > 160 * 1024)
@@ -795,11 +797,13 @@ int ag_allocate(ag_ctx *c, const double *bids, int64_t B, int32_t *winner, doubl
   return AG_OK;
 }
 
-int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, int64_t *counters_fx,
+int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out_arg, int64_t *counters_fx,
                 void *stream) {
-  if (!c || !in || !out) return ag_set_error(AG_ERR_INVALID, "ag_simulate: null argument");
+  if (!c || !in || !out_arg) return ag_set_error(AG_ERR_INVALID, "ag_simulate: null argument");
   AG_CHECK_STRUCT(in, "ag_simulate", "ag_batch_in");
-  AG_CHECK_STRUCT(out, "ag_simulate", "ag_batch_out");
+  ag_batch_out outv;
+  AG_READ_OUT(out_arg, outv, "ag_simulate");
+  const ag_batch_out *out = &outv;
   if (!c->can_simulate)
     return ag_set_error(AG_ERR_UNSUPPORTED,
                      "ag_simulate: supports E+1 in {2..9,11,13,16} (E+1 <= 8 when P > %d) and a catalogue "
@@ -948,10 +952,12 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out, 
   return AG_OK;
 }
 
-int ag_simulate_generated(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, ag_batch_out *out,
+int ag_simulate_generated(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, ag_batch_out *out_arg,
                           int64_t *counters_fx, void *stream) {
-  if (!c || !out) return ag_set_error(AG_ERR_INVALID, "ag_simulate_generated: null argument");
-  AG_CHECK_STRUCT(out, "ag_simulate_generated", "ag_batch_out");
+  if (!c || !out_arg) return ag_set_error(AG_ERR_INVALID, "ag_simulate_generated: null argument");
+  ag_batch_out outv;
+  AG_READ_OUT(out_arg, outv, "ag_simulate_generated");
+  const ag_batch_out *out = &outv;
   if (!c->catalog) return ag_set_error(AG_ERR_STATE, "ag_simulate_generated: ag_load_catalog not called");
   if (B < 0) return ag_set_error(AG_ERR_INVALID, "ag_simulate_generated: B < 0");
   if (B == 0) return AG_OK;

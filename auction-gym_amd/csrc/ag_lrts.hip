@@ -63,19 +63,22 @@ __device__ __forceinline__ int64_t wave_sum(int64_t v) {
 __global__ __launch_bounds__(kLrThreads) void k_lrts_collect(
     int64_t B, int P, int OE, const double *__restrict__ ctx, const int32_t *__restrict__ part,
     const int32_t *__restrict__ winner, const int32_t *__restrict__ item, const uint8_t *__restrict__ outcome,
-    const int32_t *__restrict__ akind, uint32_t *__restrict__ key, float *__restrict__ x, int64_t cap,
-    unsigned long long *__restrict__ count) {
+    const uint32_t *__restrict__ winner_outcome, const int32_t *__restrict__ akind, uint32_t *__restrict__ key,
+    float *__restrict__ x, int64_t cap, unsigned long long *__restrict__ count) {
   const int lane = threadIdx.x & 63;
   for (int64_t base = (int64_t)blockIdx.x * kLrThreads; base < B; base += (int64_t)gridDim.x * kLrThreads) {
     const int64_t i = base + threadIdx.x;
     bool take = false;
     uint32_t k = 0;
     if (i < B && P >= 2) {  // P == 1: nobody is charged, no record is won (src/Auction.py:68)
-      const int w = winner[i];
+      // winner and outcome from their arrays, or from the ABI 17 packed word
+      const uint32_t wo = winner ? 0u : winner_outcome[i];
+      const int w = winner ? winner[i] : (int)(wo & 0x7fffffffu);
       const int a = part[(size_t)w * B + i];
       if (akind[a] == AG_ALLOCATOR_LRTS) {
         take = true;
-        k = ((uint32_t)a << 16) | ((uint32_t)item[(size_t)w * B + i] << 1) | (outcome[i] ? 1u : 0u);
+        const bool oc = outcome ? outcome[i] != 0 : (wo >> 31) != 0;
+        k = ((uint32_t)a << 16) | ((uint32_t)item[(size_t)w * B + i] << 1) | (oc ? 1u : 0u);
       }
     }
     const uint64_t ballot = __ballot(take);
@@ -418,21 +421,26 @@ struct LrSt {
   float hist[kHistory];
 };
 
+// Both parities of the state ([2][N]) are initialised: k_lrts_epoch writes st_out only for
+// the masked agents, so an unmasked agent's parity-1 row must already read Done when
+// ag_lrts_rp_poll looks at it after an odd number of launches.
 __global__ void k_lrts_rp_init(int N, int KD, const int32_t *__restrict__ mask, const float *__restrict__ gm,
                                LrSt *__restrict__ st) {
   const int a = blockIdx.x;
   if (a >= N) return;
-  LrSt &f = st[a];
-  for (int c = threadIdx.x; c < kLrMaxKD; c += blockDim.x) {
-    f.m[c] = c < KD ? gm[(size_t)a * KD + c] : 0.0f;
-    f.ea[c] = f.es[c] = 0.0f;
-  }
-  for (int c = threadIdx.x; c < kHistory; c += blockDim.x) f.hist[c] = 0.0f;
-  if (threadIdx.x == 0) {
-    f.phase = mask[a] ? kLrTrain : kLrDone;
-    f.epoch = f.have_tot = f.bad = 0;
-    f.lr = 2e-3;
-    f.best = INFINITY;
+  for (int par = 0; par < 2; ++par) {
+    LrSt &f = st[(size_t)par * N + a];
+    for (int c = threadIdx.x; c < kLrMaxKD; c += blockDim.x) {
+      f.m[c] = c < KD ? gm[(size_t)a * KD + c] : 0.0f;
+      f.ea[c] = f.es[c] = 0.0f;
+    }
+    for (int c = threadIdx.x; c < kHistory; c += blockDim.x) f.hist[c] = 0.0f;
+    if (threadIdx.x == 0) {
+      f.phase = mask[a] ? kLrTrain : kLrDone;
+      f.epoch = f.have_tot = f.bad = 0;
+      f.lr = 2e-3;
+      f.best = INFINITY;
+    }
   }
 }
 
@@ -630,23 +638,26 @@ void ag_lrts_release(ag_ctx *c) {
 
 extern "C" {
 
-int ag_lrts_collect(ag_ctx *c, int64_t B, const ag_batch_in *in, const ag_batch_out *out,
+int ag_lrts_collect(ag_ctx *c, int64_t B, const ag_batch_in *in, const ag_batch_out *out_arg,
                     const ag_lrts_samples *s, void *stream) {
   if (int rc = check_store(c, s, "ag_lrts_collect")) return rc;
-  if (!in || !out) return ag_set_error(AG_ERR_INVALID, "ag_lrts_collect: null argument");
+  if (!in || !out_arg) return ag_set_error(AG_ERR_INVALID, "ag_lrts_collect: null argument");
   AG_CHECK_STRUCT(in, "ag_lrts_collect", "ag_batch_in");
-  AG_CHECK_STRUCT(out, "ag_lrts_collect", "ag_batch_out");
+  ag_batch_out outv;
+  AG_READ_OUT(out_arg, outv, "ag_lrts_collect");
+  const ag_batch_out *out = &outv;
   if (B < 0) return ag_set_error(AG_ERR_INVALID, "ag_lrts_collect: B < 0");
   if (B == 0 || !c->has_lrts) return AG_OK;
   if (c->shape.num_agents > 65536 || c->shape.num_items > 32768)
     return ag_set_error(AG_ERR_UNSUPPORTED, "ag_lrts_collect: sample keys hold N <= 65536, K <= 32768");
-  if (!in->ctx || !in->part || !out->winner || !out->item || !out->outcome)
-    return ag_set_error(AG_ERR_INVALID, "ag_lrts_collect: needs in.ctx, in.part, out.winner, out.item, "
-                                        "out.outcome");
+  if (!in->ctx || !in->part || !out->item || !((out->winner && out->outcome) || out->winner_outcome))
+    return ag_set_error(AG_ERR_INVALID, "ag_lrts_collect: needs in.ctx, in.part, out.item and out.winner + "
+                                        "out.outcome (or out.winner_outcome)");
   AgDeviceGuard g(c->device);
   hipLaunchKernelGGL(k_lrts_collect, dim3(grid_over(B)), dim3(kLrThreads), 0, (hipStream_t)stream, B,
-                     c->shape.num_participants, c->shape.obs_embedding_size, in->ctx, in->part, out->winner,
-                     out->item, out->outcome, c->d_akind, s->key, s->x, s->capacity,
+                     c->shape.num_participants, c->shape.obs_embedding_size, in->ctx, in->part,
+                     out->winner && out->outcome ? out->winner : nullptr, out->item,
+                     out->winner && out->outcome ? out->outcome : nullptr, out->winner_outcome, c->d_akind, s->key, s->x, s->capacity,
                      (unsigned long long *)s->count);
   AG_HIP(hipGetLastError());
   return AG_OK;
@@ -881,18 +892,23 @@ int ag_lrts_rp_begin(ag_ctx *c, const ag_lrts_samples *s, const int32_t *agents,
     }
   }
   const int G = (int)blk_agent.size();
-  if ((size_t)G > rp.cap_g || (size_t)lines > rp.cap_lines || !rp.st) {
+  if ((size_t)G > rp.cap_g || (size_t)lines > rp.cap_lines || !rp.st || !rp.acc || !rp.tables) {
     (void)hipFree(rp.st);
     (void)hipFree(rp.acc);
     (void)hipFree(rp.tables);
     rp.st = nullptr;
     rp.acc = nullptr;
     rp.tables = nullptr;
-    rp.cap_g = (size_t)G + 64;
-    rp.cap_lines = (size_t)lines + 16;
+    // capacities zero until every buffer is allocated: a failed allocation leaves the
+    // workspace empty, and the next call allocates it again
+    rp.cap_g = 0;
+    rp.cap_lines = 0;
+    const size_t cap_g = (size_t)G + 64, cap_lines = (size_t)lines + 16;
     AG_HIP(hipMalloc(&rp.st, sizeof(LrSt) * 2 * (size_t)N));
-    AG_HIP(hipMalloc(&rp.acc, sizeof(int64_t) * kLrAccStride * rp.cap_lines + sizeof(unsigned) * 32 * rp.cap_lines));
-    AG_HIP(hipMalloc(&rp.tables, sizeof(int32_t) * (2 * rp.cap_g + 3 * (size_t)N)));
+    AG_HIP(hipMalloc(&rp.acc, sizeof(int64_t) * kLrAccStride * cap_lines + sizeof(unsigned) * 32 * cap_lines));
+    AG_HIP(hipMalloc(&rp.tables, sizeof(int32_t) * (2 * cap_g + 3 * (size_t)N)));
+    rp.cap_g = cap_g;
+    rp.cap_lines = cap_lines;
   }
   rp.bar = (unsigned *)(rp.acc + kLrAccStride * rp.cap_lines);
   int32_t *d_bagent = rp.tables, *d_brank = d_bagent + rp.cap_g, *d_nblk = d_brank + rp.cap_g,

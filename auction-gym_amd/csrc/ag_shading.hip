@@ -17,6 +17,7 @@
 #include <stdint.h>
 
 #include "ag_host.h"
+#include "ag_record.h"
 
 namespace {
 
@@ -34,7 +35,9 @@ __global__ __launch_bounds__(kShThreads) void k_shading_collect(
   for (int64_t base = (int64_t)blockIdx.x * kShThreads; base < B; base += (int64_t)gridDim.x * kShThreads) {
     const int64_t i = base + threadIdx.x;
     const bool live = i < B;
-    const int w = live ? out.winner[i] : -1;
+    // winner and outcome from their arrays, or from the ABI 17 packed word
+    const uint32_t wo = (live && !out.winner) ? out.winner_outcome[i] : 0u;
+    const int w = live ? (out.winner ? out.winner[i] : (int)(wo & 0x7fffffffu)) : -1;
     for (int s = 0; s < P; ++s) {
       int a = -1;
       bool take = false;
@@ -56,8 +59,9 @@ __global__ __launch_bounds__(kShThreads) void k_shading_collect(
       const double v = values[(size_t)a * K + out.item[o]];
       st.agent[slot] = a;
       st.gamma[slot] = out.gamma[o];
-      st.utility[slot] = won ? v * (out.outcome[i] ? 1.0 : 0.0) - out.price[i] : 0.0;  // src/Bidder.py:62-63
-      if (st.ctr) st.ctr[slot] = out.est_ctr[o];
+      const bool oc = out.winner ? out.outcome[i] != 0 : (wo >> 31) != 0;
+      st.utility[slot] = won ? v * (oc ? 1.0 : 0.0) - out.price[i] : 0.0;  // src/Bidder.py:62-63
+      if (st.ctr) st.ctr[slot] = out.est_ctr ? out.est_ctr[o] : out.record[ag::rec_field(ag::kRecLayout, (uint32_t)s, (uint32_t)i, (uint32_t)B, 1)];
       if (st.value) st.value[slot] = v;
       if (st.propensity) st.propensity[slot] = out.propensity[o];
       if (st.won) st.won[slot] = won ? 1 : 0;
@@ -236,20 +240,23 @@ int check_store(const ag_ctx *c, const ag_shading_samples *s, const char *who) {
 
 extern "C" {
 
-int ag_shading_collect(ag_ctx *c, int64_t first, int64_t B, const ag_batch_in *in, const ag_batch_out *out,
+int ag_shading_collect(ag_ctx *c, int64_t first, int64_t B, const ag_batch_in *in, const ag_batch_out *out_arg,
                        const ag_shading_samples *s, void *stream) {
   if (int rc = check_store(c, s, "ag_shading_collect")) return rc;
-  if (!in || !out) return ag_set_error(AG_ERR_INVALID, "ag_shading_collect: null argument");
+  if (!in || !out_arg) return ag_set_error(AG_ERR_INVALID, "ag_shading_collect: null argument");
   AG_CHECK_STRUCT(in, "ag_shading_collect", "ag_batch_in");
-  AG_CHECK_STRUCT(out, "ag_shading_collect", "ag_batch_out");
+  ag_batch_out outv;
+  AG_READ_OUT(out_arg, outv, "ag_shading_collect");
+  if (!(outv.winner && outv.outcome)) outv.winner = nullptr;  // then the packed word is read
+  const ag_batch_out *out = &outv;
   if (B < 0) return ag_set_error(AG_ERR_INVALID, "ag_shading_collect: B < 0");
   if (B == 0 || !c->has_shading) return AG_OK;
-  if (!in->part || !out->winner || !out->item || !out->outcome || !out->price || !out->gamma)
-    return ag_set_error(AG_ERR_INVALID, "ag_shading_collect: needs in.part, out.winner, out.item, "
-                                        "out.outcome, out.price, out.gamma");
-  if ((s->ctr && !out->est_ctr) || (s->propensity && !out->propensity))
+  if (!in->part || !(out->winner || out->winner_outcome) || !out->item || !out->price || !out->gamma)
+    return ag_set_error(AG_ERR_INVALID, "ag_shading_collect: needs in.part, out.winner + out.outcome (or "
+                                        "out.winner_outcome), out.item, out.price, out.gamma");
+  if ((s->ctr && !out->est_ctr && !out->record) || (s->propensity && !out->propensity))
     return ag_set_error(AG_ERR_INVALID, "ag_shading_collect: the store's ctr / propensity need "
-                                        "out.est_ctr / out.propensity");
+                                        "out.est_ctr (or out.record) / out.propensity");
   AgDeviceGuard g(c->device);
   hipLaunchKernelGGL(k_shading_collect, dim3(grid_over(B)), dim3(kShThreads), 0, (hipStream_t)stream, first, B,
                      c->shape.num_participants, c->shape.num_items, in->part, *out, c->d_bkind, c->d_values, *s,

@@ -96,6 +96,8 @@ struct OraParams {
   uint8_t *outcome;
   int32_t *item;
   double *bid, *est_ctr, *true_ctr, *best_ev;
+  uint32_t *winner_outcome;  // ABI 17 packed layout: [B] winner | outcome << 31
+  double *record;            // ... {bid, est_ctr, true_ctr, best_ev} per (slot, auction)
   int64_t *partials;  // [grid][N][AG_NUM_COUNTERS][2]
   // generate mode (GEN): inputs drawn on the chip as ag_generate draws them
   uint64_t seed, first;  // Philox key; global index of auction 0 of the batch
@@ -316,6 +318,10 @@ __global__ __launch_bounds__(kThreads) void k_oracle(OraParams prm) {
       if (prm.est_ctr) stg(prm.est_ctr + o, c);
       if (prm.true_ctr) stg(prm.true_ctr + o, c);
       if (prm.best_ev) stg(prm.best_ev + o, sc);
+      if (prm.record) {  // ABI 17 packed record: the same four values
+        st_record_lo(prm.record, s, i, B, b, c);
+        st_record_hi(prm.record, s, i, B, c, sc);
+      }
       // streaming top-2, ties -> lowest slot (src/AuctionAllocation.py:19-34)
       if (s == 0) {
         m1 = b;
@@ -337,6 +343,7 @@ __global__ __launch_bounds__(kThreads) void k_oracle(OraParams prm) {
     if (prm.price) stg(prm.price + i, charged ? price : (double)NAN);
     if (prm.second_price) stg(prm.second_price + i, charged ? m2 : (double)NAN);
     if (prm.outcome) stg(prm.outcome + i, (uint8_t)oc);
+    if (prm.winner_outcome) stg(prm.winner_outcome + i, pack_wo(w, oc));
 
     if (prm.want_counters) {
 #pragma unroll

@@ -15,7 +15,7 @@ per-auction / per-participant output in SoA form; with N > 1 the per-agent count
 then summed across GPUs (int64 all-reduce over RCCL: the only collective of the path).
 
 Printed: one JSON line (rank 0). `roofline.achieved` = algorithmic bytes per launch
-(141 B per auction) / average ag_simulate duration from HIP events on the
+(140 B per auction: SURVEY §8d's 141 with winner and outcome as one 4-B word) / average ag_simulate duration from HIP events on the
 launch stream. `cpu_baseline` = the oracle (the C restatement of the reference path,
 kind "port") timed on host cores on a bounded sample of the same inputs.
 """
@@ -59,9 +59,11 @@ def all_reduce_max(t):
     return t
 
 
-def algorithmic_bytes_per_auction(E, P, first_price):
+def algorithmic_bytes_per_auction(E, P, first_price, packed_winner=False):
+    """packed_winner: winner and outcome as the one ABI 17 word winner | outcome << 31 (4 B)
+    instead of the int32 winner and the byte outcome (5 B)."""
     reads = 8 * E + 4 * P + 8                       # ctx, part, u
-    writes = 4 + 8 + 1 + P * (4 + 8 + 8 + 8 + 8)    # winner, price, outcome; per slot
+    writes = (4 if packed_winner else 4 + 1) + 8 + P * (4 + 8 + 8 + 8 + 8)  # winner(+outcome), price; per slot
     if first_price:
         writes += 8                                 # second price (== price under SP)
     return reads + writes
@@ -743,8 +745,10 @@ def main():
     inp = eng.alloc_inputs(B)
     lo, hi = shard_range(B * world, rank, world)  # global auction indices of this rank
     eng.generate(0, lo, inp)
-    fields = ("winner", "price", "outcome", "item", "bid", "est_ctr", "true_ctr", "best_ev")
-    out = eng.alloc_outputs(B, fields)
+    # every output of the round: winner and outcome as the ABI 17 packed word (the byte-wide
+    # outcome stream cost 6 % of the kernel's time, profiles/r05c_ab_packed.log), the rest per field
+    from auctiongym_amd.engine import HEADLINE_FIELDS, unpack_outputs
+    out = eng.alloc_outputs(B, HEADLINE_FIELDS)
     cnt = eng.new_counters()
     torch.cuda.synchronize()
 
@@ -785,7 +789,7 @@ def main():
 
     total_auctions = B * world * args.steps
     value = total_auctions / elapsed
-    bpa = algorithmic_bytes_per_auction(E, P, first_price=False)
+    bpa = algorithmic_bytes_per_auction(E, P, first_price=False, packed_winner=True)
     achieved = bpa * B / (kern_ms * 1e-3) / 1e9
 
     gen = None
@@ -866,7 +870,9 @@ def main():
                      "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
                      "traffic_source": traffic_src,
                      "kernel": "ag_simulate (k_oracle + k_reduce_counters)",
-                     "kernel_ms": kern_ms, "algorithmic_bytes_per_auction": bpa},
+                     "kernel_ms": kern_ms, "algorithmic_bytes_per_auction": bpa,
+                     "bytes_what": "56 read (ctx 40, part 8, u 8) + 84 written (winner | outcome << 31 4, "
+                                   "price 8, per slot item 4 + bid, est_ctr, true_ctr, best_ev 8 each)"},
     }
 
     if gen is not None:
@@ -903,7 +909,7 @@ def main():
         cps, dt, passes, o = cpu_baseline(items, values, inp, sample, threads)
         gpu_bid = out["bid"][:, :sample].cpu().numpy().T
         same = bool(np.array_equal(gpu_bid, o["bid"]) and
-                    np.array_equal(out["winner"][:sample].cpu().numpy(), o["winner"]))
+                    np.array_equal(unpack_outputs(out)["winner"][:sample].cpu().numpy(), o["winner"]))
         s1 = min(1 << 22, sample)
         cps1, dt1, passes1, _ = cpu_baseline(items, values, inp, s1, 1, min_seconds=5.0)
         result["cpu_baseline"] = {

@@ -1,0 +1,180 @@
+"""ABI 17 packed output layout (include/auctiongym.h ag_batch_out.winner_outcome / .record):
+the same values as the per-field arrays, bit for bit, on every simulate kernel -- k_oracle
+(replay and generate mode), the general kernel's kept-slot, early-count and streamed-slot
+paths -- and the learner stores collected from packed-only outputs equal those collected
+from the per-field arrays. The reference logs one ImpressionOpportunity record per
+participation (src/Impression.py:4-31, appended at src/Agent.py:55-66); the packed record is
+that record's {bid, estimated_CTR, true_CTR, best_expected_value} in one 32-B row.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+PER_FIELD = ("winner", "price", "second_price", "outcome", "item", "bid", "est_ctr", "true_ctr", "best_ev")
+
+
+def _same(a, b):
+    import torch
+    a, b = a.contiguous(), b.contiguous()
+    if a.dtype == torch.float64:
+        return torch.equal(a.view(torch.int64), b.view(torch.int64))
+    return torch.equal(a, b)
+
+
+def _check_packed(per_field, packed):
+    from auctiongym_amd.engine import unpack_outputs
+    up = unpack_outputs(packed)
+    for f in ("winner", "outcome", "bid", "est_ctr", "true_ctr", "best_ev"):
+        assert _same(per_field[f], up[f]), f
+    for f in ("price", "item"):
+        assert _same(per_field[f], packed[f]), f
+
+
+def _oracle_engine(N, P, mech, seed=0):
+    from auctiongym_amd.engine import AuctionEngine
+    g = np.random.default_rng(seed)
+    eng = AuctionEngine(N, P, 12, 5, 4, mech, 1.0)
+    eng.load_catalog(np.concatenate([g.normal(0, 1, (N, 12, 5)), -3.0 - g.random((N, 12, 1))], axis=2),
+                     g.lognormal(0.1, 0.2, (N, 12)))
+    return eng
+
+
+@pytest.mark.parametrize("N,P,mech,B", [(6, 2, 1, (1 << 20) + 37), (8, 3, 0, 5000), (4, 1, 1, 999),
+                                        (32, 8, 1, 1 << 16)])
+def test_oracle_kernel_packed_equals_per_field(gpu, N, P, mech, B):
+    """k_oracle (the headline kernel): packed outputs == per-field outputs, replay and
+    generate mode, counters unchanged by the layout."""
+    import torch
+    from auctiongym_amd.engine import PACKED_FIELDS
+    eng = _oracle_engine(N, P, mech)
+    inp = eng.alloc_inputs(B)
+    eng.generate(3, 11, inp)
+    a = eng.alloc_outputs(B, PER_FIELD)
+    b = eng.alloc_outputs(B, PACKED_FIELDS)
+    ca, cb = eng.new_counters(), eng.new_counters()
+    eng.simulate(inp, a, ca)
+    eng.simulate(inp, b, cb)
+    torch.cuda.synchronize()
+    _check_packed(a, b)
+    assert torch.equal(ca, cb)
+    # generate mode (inputs drawn on the chip): the same again
+    g = eng.alloc_outputs(B, PACKED_FIELDS)
+    cg = eng.new_counters()
+    eng.simulate_generated(3, 11, g, cg)
+    torch.cuda.synchronize()
+    _check_packed(a, g)
+    assert torch.equal(ca, cg)
+    eng.close()
+
+
+def test_abi16_batch_out_is_still_accepted(gpu):
+    """A binding compiled against the ABI 16 ag_batch_out (11 pointers, no packed fields)
+    keeps working: struct_size == AG_BATCH_OUT_V16_SIZE is read as the older layout."""
+    import torch
+    from auctiongym_amd import _lib
+
+    class OutV16(ctypes.Structure):
+        _fields_ = [("struct_size", ctypes.c_uint64)] + [(n, ctypes.c_void_p) for n in (
+            "winner", "price", "second_price", "outcome", "item", "bid", "est_ctr", "true_ctr", "best_ev",
+            "gamma", "propensity")]
+    assert ctypes.sizeof(OutV16) == 8 + 11 * 8
+    eng = _oracle_engine(6, 2, 1)
+    B = 4096
+    inp = eng.alloc_inputs(B)
+    eng.generate(0, 0, inp)
+    ref = eng.alloc_outputs(B, PER_FIELD)
+    eng.simulate(inp, ref)
+    out = eng.alloc_outputs(B, PER_FIELD)
+    bo = OutV16(ctypes.sizeof(OutV16), *[out[k].data_ptr() if k in out else None for k in (
+        "winner", "price", "second_price", "outcome", "item", "bid", "est_ctr", "true_ctr", "best_ev", "gamma",
+        "propensity")])
+    bi = _lib.AgBatchIn(inp["ctx"].data_ptr(), inp["part"].data_ptr(), inp["u"].data_ptr())
+    rc = eng.L.ag_simulate(eng._h, B, ctypes.byref(bi), ctypes.cast(ctypes.pointer(bo), ctypes.POINTER(_lib.AgBatchOut)),
+                           None, None)
+    assert rc == 0, eng.L.ag_last_error()
+    torch.cuda.synchronize()
+    for k in PER_FIELD:
+        assert _same(ref[k], out[k]), k
+    # a misaligned record is refused
+    rec = torch.empty(2 * B * 4 + 1, dtype=torch.float64, device="cuda")
+    bo2 = _lib.AgBatchOut(*[None] * 12, rec.data_ptr() + 8)
+    rc = eng.L.ag_simulate(eng._h, B, ctypes.byref(bi), ctypes.byref(bo2), None, None)
+    assert rc == _lib.AG_ERR_INVALID and b"16-B aligned" in eng.L.ag_last_error()
+    eng.close()
+
+
+def _mixed_engine(P, block):
+    from auctiongym_amd import _lib
+    from auctiongym_amd.engine import AuctionEngine
+    N, K, E, OE = 20, 12, 5, 4
+    g = np.random.default_rng(5)
+    items = np.concatenate([g.normal(0, 1, (N, K, E)), -3.0 - g.random((N, K, 1))], axis=2)
+    values = g.lognormal(0.1, 0.2, (N, K))
+    ak = np.array([i % 2 for i in range(N)], np.int32)
+    bk = np.array([4 if i % 3 else (i // 3) % 4 for i in range(N)], np.int32)
+    pg = 0.5 + 0.5 * g.random(N)
+    gs = 0.01 + 0.05 * g.random(N)
+    m = g.normal(0, 1, (N, K, OE + 1)).astype(np.float32)
+    q = (1.0 + 3.0 * g.random((N, K, OE + 1))).astype(np.float32)
+    state = g.normal(0, 0.7, (N, 16)).astype(np.float32)
+    init = np.array([1 if (bk[a] >= 2 and a % 2 == 0) else 0 for a in range(N)], np.int32)
+    eng = AuctionEngine(N, P, K, E, OE, 0, 1.0)
+    eng.set_agent_params(ak, bk, pg, gs)
+    eng.load_catalog(items, values)
+    eng.load_lrts(m, q, thompson_sampling=True)
+    eng.set_dr_state(state, init)
+    if block:
+        eng._check(eng.L.ag_set_option(eng._h, _lib.OPT_SIM_BLOCK_THREADS, block), "ag_set_option")
+    return eng
+
+
+@pytest.mark.parametrize("P,B,block", [(2, (1 << 17) + 45, 0), (2, 3001, 1024), (8, 1 << 15, 0), (12, 4000, 0)])
+def test_general_kernel_packed_equals_per_field_and_collects(gpu, P, B, block):
+    """The general kernel (LR-TS / shading / fitted-policy mix; P = 2 kept slots, the
+    1024-lane early-count path, P = 8 streamed slots, P = 12 the runtime-P kernel): packed ==
+    per-field, and the LR-TS and learning-bidder stores collected from packed-only outputs
+    (winner_outcome + record) hold the same records."""
+    import torch
+    eng = _mixed_engine(P, block)
+    inp = eng.alloc_inputs(B)
+    eng.generate(9, 0, inp)
+    eng.generate_noise(9, 0, inp)
+    full = PER_FIELD + ("gamma", "propensity")
+    a = eng.alloc_outputs(B, full)
+    b = eng.alloc_outputs(B, ("winner_outcome", "price", "second_price", "item", "record", "gamma", "propensity"))
+    ca, cb = eng.new_counters(), eng.new_counters()
+    eng.simulate(inp, a, ca)
+    eng.simulate(inp, b, cb)
+    torch.cuda.synchronize()
+    _check_packed(a, b)
+    for f in ("second_price", "gamma", "propensity"):
+        assert _same(a[f], b[f]), f
+    assert torch.equal(ca, cb)
+    # stores from both layouts: the same multisets of records
+    la, lb = eng.new_lrts_samples(2 * B), eng.new_lrts_samples(2 * B)
+    eng.lrts_collect(inp, a, la)
+    eng.lrts_collect(inp, b, lb)
+    sa, sb = eng.new_shading_samples(2 * P * B, learning=True), eng.new_shading_samples(2 * P * B, learning=True)
+    eng.shading_collect(inp, a, sa)
+    eng.shading_collect(inp, b, sb)
+    torch.cuda.synchronize()
+    n = int(la["count"].item())
+    assert n == int(lb["count"].item()) and n > 0
+    ka = la["key"][:n].cpu().numpy().astype(np.int64)
+    kb = lb["key"][:n].cpu().numpy().astype(np.int64)
+    assert np.array_equal(np.sort(ka), np.sort(kb))
+    n = int(sa["count"].item())
+    assert n == int(sb["count"].item()) and n > 0
+
+    def rows(st):
+        order = st["order"][:n].cpu().numpy()
+        idx = np.argsort(order)
+        return {k: st[k][:n].cpu().numpy()[idx] for k in ("agent", "gamma", "utility", "ctr", "value",
+                                                          "propensity", "won")}
+    ra, rb = rows(sa), rows(sb)
+    for k in ra:
+        assert np.array_equal(ra[k].view(np.uint8), rb[k].view(np.uint8)), k
+    eng.close()

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 def test_library_loads_without_gpu_and_reports_abi():
     from auctiongym_amd import _lib
     L = _lib.load()
-    assert L.ag_abi_version() == _lib.ABI_VERSION == 16
+    assert L.ag_abi_version() == _lib.ABI_VERSION == 17
 
 
 def test_ctypes_structs_match_the_c_header(tmp_path):
@@ -505,3 +505,35 @@ def test_native_draws_gate():
     with mock.patch("torch.backends.cpu.get_cpu_capability", return_value="DEFAULT"):
         assert not Auction._native_draws(ns(12, 4))
         assert Auction._native_draws(ns(12, 4, ts=False))
+
+
+def test_fit_noise_draws_gate_on_torch_build():
+    """The learner fits' rsample windows (engine.torch_normal_epochs): with torch's vectorised
+    normal kernel the C restatement equals torch's own calls number for number and state for
+    state; on a torch build without it (mocked DEFAULT capability) the windows are torch's own
+    calls from the given state, the caller's generator untouched (the restatement
+    must not be used where it does not hold)."""
+    from unittest import mock
+
+    import torch
+    from auctiongym_amd.engine import TORCH_NORMAL_AVX2, torch_normal_epochs
+    torch.manual_seed(123)
+    start = torch.get_rng_state().numpy().copy()
+    n, epochs = 37, 5
+
+    def via_torch():
+        torch.set_rng_state(torch.from_numpy(start.copy()))
+        out = np.stack([torch.empty(n).normal_().numpy() for _ in range(epochs)])
+        return out, torch.get_rng_state().numpy().copy()
+    want, want_state = via_torch()
+    if torch.backends.cpu.get_cpu_capability() in TORCH_NORMAL_AVX2:
+        st = start.copy()
+        got = torch_normal_epochs(st, n, epochs)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)) and np.array_equal(st, want_state)
+    torch.manual_seed(7)
+    caller = torch.get_rng_state().clone()
+    with mock.patch("torch.backends.cpu.get_cpu_capability", return_value="DEFAULT"):
+        st = start.copy()
+        got = torch_normal_epochs(st, n, epochs)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32)) and np.array_equal(st, want_state)
+    assert torch.equal(torch.get_rng_state(), caller)

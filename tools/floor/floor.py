@@ -24,7 +24,7 @@ class Ptrs(ctypes.Structure):
 def main():
     L = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libfloor.so"))
     L.floor_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(Ptrs), ctypes.c_int64, ctypes.c_void_p]
-    B = 1 << 24
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 27
     items, values = bench.catalogue()
     eng = AuctionEngine(6, 2, 12, 5, 4, _lib.SECOND_PRICE, 1.0, device=0)
     eng.load_catalog(items, values)
@@ -33,9 +33,15 @@ def main():
     full = ("winner", "price", "outcome", "item", "bid", "est_ctr", "true_ctr", "best_ev")
     out = eng.alloc_outputs(B, full)
     cnt = eng.new_counters()
+    from auctiongym_amd.engine import HEADLINE_FIELDS
+    outw = eng.alloc_outputs(B, HEADLINE_FIELDS)
     P = lambda t: t.data_ptr()  # noqa: E731
     p = Ptrs(P(inp["ctx"]), P(inp["part"]), P(inp["u"]), P(out["winner"]), P(out["item"]), P(out["price"]),
              P(out["bid"]), P(out["est_ctr"]), P(out["true_ctr"]), P(out["best_ev"]), P(out["outcome"]))
+    tin = torch.zeros(7 * B, dtype=torch.float64, device="cuda")      # 56 B per auction, tiled
+    tout = torch.empty(84 * B // 8, dtype=torch.float64, device="cuda")  # 84 B per auction, tiled
+    p2 = Ptrs(P(tin), P(inp["part"]), P(inp["u"]), P(out["winner"]), P(out["item"]), P(tout),
+              P(out["bid"]), P(out["est_ctr"]), P(out["true_ctr"]), P(out["best_ev"]), P(out["outcome"]))
     st = torch.cuda.current_stream()
     sp = ctypes.c_void_p(st.cuda_stream)
     cus = torch.cuda.get_device_properties(0).multi_processor_count
@@ -46,7 +52,14 @@ def main():
         "floor w2 nt 8 blocks/CU": lambda: L.floor_run(3, cus * 8, ctypes.byref(p), B, sp),
         "floor w2 nt 4 blocks/CU": lambda: L.floor_run(3, cus * 4, ctypes.byref(p), B, sp),
         "floor one tile per block": lambda: L.floor_run(0, 0, ctypes.byref(p), B, sp),
-        "ag_simulate (bench)": lambda: eng.simulate(inp, out, cnt),
+        "floor nt 4/CU, winner|outcome word": lambda: L.floor_run(4, cus * 4, ctypes.byref(p), B, sp),
+        "floor nt 8/CU, winner|outcome word": lambda: L.floor_run(4, cus * 8, ctypes.byref(p), B, sp),
+        "floor nt 4/CU, tiled inputs": lambda: L.floor_run(5, cus * 4, ctypes.byref(p2), B, sp),
+        "floor nt 4/CU, tiled outputs": lambda: L.floor_run(6, cus * 4, ctypes.byref(p2), B, sp),
+        "floor nt 4/CU, tiled in + out": lambda: L.floor_run(7, cus * 4, ctypes.byref(p2), B, sp),
+        "floor nt 8/CU, tiled in + out": lambda: L.floor_run(7, cus * 8, ctypes.byref(p2), B, sp),
+        "ag_simulate (r04 fields)": lambda: eng.simulate(inp, out, cnt),
+        "ag_simulate (bench: winner|outcome)": lambda: eng.simulate(inp, outw, cnt),
         "ag_simulate, no counters": lambda: eng.simulate(inp, out, None),
         "torch copy+fill of the same bytes": None,
     }
@@ -58,13 +71,13 @@ def main():
     big = torch.empty(141 * B // 16, dtype=torch.float64, device="cuda")  # 141 B per auction moved
     big2 = torch.empty_like(big)
     runs["ag_stream_copy of 141 B/auction (read+write)"] = lambda: stream_copy(big, big2)
-    for _ in range(200):
+    for _ in range(max(5, (200 << 24) // B)):
         for f in runs.values():
             f()
     torch.cuda.synchronize()
     iso = {k: [] for k in runs}
     sus = {k: [] for k in runs}
-    for r in range(12):
+    for r in range(12 if B <= 1 << 24 else 4):
         for k, f in runs.items():
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(st)
@@ -73,11 +86,11 @@ def main():
             torch.cuda.synchronize()
             iso[k].append(a.elapsed_time(b))
             a.record(st)
-            for _ in range(20):
+            for _ in range(10):
                 f()
             b.record(st)
             torch.cuda.synchronize()
-            sus[k].append(a.elapsed_time(b) / 20)
+            sus[k].append(a.elapsed_time(b) / 10)
     for k in runs:
         mi, ms = float(np.median(iso[k])), float(np.median(sus[k]))
         print(f"{k:36s} isolated {mi:7.4f} ms ({141 * B / mi / 1e9:7.1f} GB/s)   back-to-back {ms:7.4f} ms "

@@ -21,16 +21,21 @@ template <bool NT, typename T> __device__ __forceinline__ T L(const T *q) {
 template <bool NT, typename T> __device__ __forceinline__ void S(T *q, T v) {
   if constexpr (NT) __builtin_nontemporal_store(v, q); else *q = v;
 }
-template <bool NT = false>
+// WO: winner and outcome as one word (ABI 17 winner_outcome), no byte stream
+template <bool NT = false, bool WO = false>
 __device__ __forceinline__ void one(const Ptrs &p, int64_t B, int64_t i) {
   double x0 = L<NT>(p.ctx + i), x1 = L<NT>(p.ctx + B + i), x2 = L<NT>(p.ctx + 2 * B + i),
          x3 = L<NT>(p.ctx + 3 * B + i), x4 = L<NT>(p.ctx + 4 * B + i);
   int a0 = L<NT>(p.part + i), a1 = L<NT>(p.part + B + i);
   double u = L<NT>(p.u + i);
   double s = x0 + x1 + x2 + x3 + x4;
-  S<NT>(p.winner + i, (int32_t)(a0 > a1));
+  if constexpr (WO) {
+    S<NT>(p.winner + i, (int32_t)((uint32_t)(a0 > a1) | ((uint32_t)(u > 0.5) << 31)));
+  } else {
+    S<NT>(p.winner + i, (int32_t)(a0 > a1));
+    S<NT>(p.outcome + i, (uint8_t)(u > 0.5));
+  }
   S<NT>(p.price + i, s * u);
-  S<NT>(p.outcome + i, (uint8_t)(u > 0.5));
   S<NT>(p.item + i, (int32_t)a0);
   S<NT>(p.item + B + i, (int32_t)a1);
   S<NT>(p.bid + i, s);
@@ -79,13 +84,87 @@ __global__ __launch_bounds__(256) void k_floor_persistent(Ptrs p, int64_t B) {
 __global__ __launch_bounds__(256) void k_floor_persistent_nt(Ptrs p, int64_t B) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < B; i += (int64_t)gridDim.x * 256) one<true>(p, B, i);
 }
+__global__ __launch_bounds__(256) void k_floor_persistent_nt_wo(Ptrs p, int64_t B) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < B; i += (int64_t)gridDim.x * 256)
+    one<true, true>(p, B, i);
+}
 __global__ __launch_bounds__(256) void k_floor_tiles(Ptrs p, int64_t B) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < B) one(p, B, i);
 }
 
+
+// Tiled ("AoSoA") batch layouts, 64 auctions per tile, every field of a tile contiguous:
+// inputs [T][ctx0..4, u, part0|part1][64] (7 x 512 B = 3.5 KB per tile), outputs
+// [T][winner|outcome (256 B), price, item0|item1, bid0, bid1, est0, est1, tru0, tru1, bev0, bev1][64]
+// (84 B x 64 = 5376 B per tile): one read stream and one write stream.
+template <bool TIN, bool TOUT>
+__device__ __forceinline__ void one_tiled(const Ptrs &p, int64_t B, int64_t i) {
+  const int64_t t = i >> 6, l = i & 63;
+  double x0, x1, x2, x3, x4, u;
+  int a0, a1;
+  if constexpr (TIN) {
+    const double *tin = p.ctx + t * 7 * 64 + l;
+    x0 = __builtin_nontemporal_load(tin);
+    x1 = __builtin_nontemporal_load(tin + 64);
+    x2 = __builtin_nontemporal_load(tin + 128);
+    x3 = __builtin_nontemporal_load(tin + 192);
+    x4 = __builtin_nontemporal_load(tin + 256);
+    u = __builtin_nontemporal_load(tin + 320);
+    const i32x2 a = __builtin_nontemporal_load(reinterpret_cast<const i32x2 *>(tin + 384));
+    a0 = a.x;
+    a1 = a.y;
+  } else {
+    x0 = L<true>(p.ctx + i); x1 = L<true>(p.ctx + B + i); x2 = L<true>(p.ctx + 2 * B + i);
+    x3 = L<true>(p.ctx + 3 * B + i); x4 = L<true>(p.ctx + 4 * B + i);
+    a0 = L<true>(p.part + i); a1 = L<true>(p.part + B + i);
+    u = L<true>(p.u + i);
+  }
+  const double s = x0 + x1 + x2 + x3 + x4;
+  const int32_t wo = (int32_t)((uint32_t)(a0 > a1) | ((uint32_t)(u > 0.5) << 31));
+  if constexpr (TOUT) {
+    unsigned char *to = reinterpret_cast<unsigned char *>(p.price) + t * 84 * 64;
+    __builtin_nontemporal_store(wo, reinterpret_cast<int32_t *>(to) + l);
+    double *d = reinterpret_cast<double *>(to + 256);
+    __builtin_nontemporal_store(s * u, d + l);
+    __builtin_nontemporal_store(i32x2{a0, a1}, reinterpret_cast<i32x2 *>(d + 64) + l);
+    __builtin_nontemporal_store(s, d + 128 + l);
+    __builtin_nontemporal_store(s + u, d + 192 + l);
+    __builtin_nontemporal_store(x0, d + 256 + l);
+    __builtin_nontemporal_store(x1, d + 320 + l);
+    __builtin_nontemporal_store(x2, d + 384 + l);
+    __builtin_nontemporal_store(x3, d + 448 + l);
+    __builtin_nontemporal_store(x4, d + 512 + l);
+    __builtin_nontemporal_store(u, d + 576 + l);
+  } else {
+    S<true>(p.winner + i, wo);
+    S<true>(p.price + i, s * u);
+    S<true>(p.item + i, (int32_t)a0);
+    S<true>(p.item + B + i, (int32_t)a1);
+    S<true>(p.bid + i, s);
+    S<true>(p.bid + B + i, s + u);
+    S<true>(p.est + i, x0);
+    S<true>(p.est + B + i, x1);
+    S<true>(p.tru + i, x2);
+    S<true>(p.tru + B + i, x3);
+    S<true>(p.bev + i, x4);
+    S<true>(p.bev + B + i, u);
+  }
+}
+template <bool TIN, bool TOUT>
+__global__ __launch_bounds__(256) void k_floor_tiled(Ptrs p, int64_t B) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < B; i += (int64_t)gridDim.x * 256)
+    one_tiled<TIN, TOUT>(p, B, i);
+}
+
 extern "C" int floor_run(int persistent, int grid, const Ptrs *p, int64_t B, void *stream) {
-  if (persistent == 3)
+  if (persistent >= 5 && persistent <= 7) {
+    auto k = persistent == 5 ? k_floor_tiled<true, false> : persistent == 6 ? k_floor_tiled<false, true>
+                                                                            : k_floor_tiled<true, true>;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, (hipStream_t)stream, *p, B);
+  } else if (persistent == 4)
+    hipLaunchKernelGGL(k_floor_persistent_nt_wo, dim3(grid), dim3(256), 0, (hipStream_t)stream, *p, B);
+  else if (persistent == 3)
     hipLaunchKernelGGL(k_floor_w2, dim3(grid), dim3(256), 0, (hipStream_t)stream, *p, B);
   else if (persistent == 2)
     hipLaunchKernelGGL(k_floor_persistent_nt, dim3(grid), dim3(256), 0, (hipStream_t)stream, *p, B);
