@@ -86,7 +86,7 @@ class AgBatchOut(_Sized):
                 ("item", ctypes.c_void_p), ("bid", ctypes.c_void_p), ("est_ctr", ctypes.c_void_p),
                 ("true_ctr", ctypes.c_void_p), ("best_ev", ctypes.c_void_p),
                 ("gamma", ctypes.c_void_p), ("propensity", ctypes.c_void_p),
-                ("winner_outcome", ctypes.c_void_p), ("record", ctypes.c_void_p)]  # ABI 17
+                ("winner_outcome", ctypes.c_void_p)]  # ABI 17
 
 
 class AgLrtsSamples(_Sized):

@@ -18,51 +18,26 @@ NUM_COUNTERS = _lib.NUM_COUNTERS
 FX_LIMBS = _lib.FX_LIMBS
 
 _OUT_FIELDS = ("winner", "price", "second_price", "outcome", "item", "bid", "est_ctr",
-               "true_ctr", "best_ev", "gamma", "propensity", "winner_outcome", "record")
+               "true_ctr", "best_ev", "gamma", "propensity", "winner_outcome")
 _CORE_FIELDS = _OUT_FIELDS[:9]
-# ABI 17 packed record layout (include/auctiongym.h): winner | outcome << 31, the per-slot
-# {bid, est_ctr, true_ctr, best_ev} record, and the item and price arrays of the per-field form
-PACKED_FIELDS = ("winner_outcome", "price", "item", "record")
-# the headline's output set: every per-field array, winner and outcome as the packed word (the
-# 1-B outcome stream alone cost 6 % of k_oracle's time, profiles/r05c_ab_packed.log; the
-# record form of the other four was no faster than their arrays)
+# ABI 17 (include/auctiongym.h): winner and outcome as one word. The headline's output set:
+# every per-field array, winner and outcome as that word (the 1-B outcome stream alone cost
+# 6 % of k_oracle's time, profiles/r05i_ab_packed.log)
 HEADLINE_FIELDS = ("winner_outcome", "price", "item", "bid", "est_ctr", "true_ctr", "best_ev")
-REC_LAYOUT = 2  # csrc/ag_record.h kRecLayout: 64-auction tiles of (bid, est) / (true, best_ev) pairs
-_REC_FIELDS = ("bid", "est_ctr", "true_ctr", "best_ev")
 
 
-def record_doubles(P, B):
-    """Doubles of a packed record array (every layout fits P * ceil(B / 64) * 256)."""
-    return P * ((B + 63) // 64) * 256
-
-
-def record_field(record, P, B, f, layout=REC_LAYOUT):
-    """Field f (0 bid, 1 est_ctr, 2 true_ctr, 3 best_ev) of a packed record as a [P][B] view."""
-    T = (B + 63) // 64
-    r = record.reshape(P, -1)
-    if layout == 0:
-        return r[:, :B * 4].reshape(P, B, 4)[:, :, f]
-    if layout == 1:
-        return r[:, :T * 256].reshape(P, T, 4, 64)[:, :, f, :].reshape(P, T * 64)[:, :B]
-    return r[:, :T * 256].reshape(P, T, 2, 64, 2)[:, :, f // 2, :, f % 2].reshape(P, T * 64)[:, :B]
-
-
-def unpack_outputs(outputs, P=None, B=None, layout=REC_LAYOUT):
-    """Per-field views of a packed output dict (winner, outcome, bid, est_ctr, true_ctr,
-    best_ev from winner_outcome / record), for comparing the two layouts."""
+def unpack_outputs(outputs):
+    """Per-field views of an output dict: winner and outcome from a winner_outcome word."""
     o = dict(outputs)
     if "winner_outcome" in o:
         wo = o["winner_outcome"].to(torch.int64) & 0xffffffff
         o["winner"] = (wo & 0x7fffffff).to(torch.int32)
         o["outcome"] = (wo >> 31).to(torch.uint8)
-    if "record" in o:
-        if B is None:
-            B = o["winner_outcome"].shape[0] if "winner_outcome" in o else o["price"].shape[0]
-        if P is None:
-            P = o["record"].shape[0]
-        for j, f in enumerate(_REC_FIELDS):
-            o[f] = record_field(o["record"], P, B, j, layout)
     return o
+
+
+def _batch_out(outputs):
+    return AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
 
 
 def _ptr(t):
@@ -186,7 +161,7 @@ class AuctionEngine:
         """Append the won LR-TS samples of a simulated batch (ag_lrts_collect)."""
         B = inputs["u"].shape[0]
         bi = _batch_in(inputs)
-        bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
+        bo = _batch_out(outputs)
         st = self._samples(store)
         self._check(self.L.ag_lrts_collect(self._h, B, ctypes.byref(bi), ctypes.byref(bo),
                                            ctypes.byref(st), _stream()), "ag_lrts_collect")
@@ -337,8 +312,7 @@ class AuctionEngine:
                 "est_ctr": ((P, B), torch.float64), "true_ctr": ((P, B), torch.float64),
                 "best_ev": ((P, B), torch.float64), "gamma": ((P, B), torch.float64),
                 "propensity": ((P, B), torch.float64),
-                "winner_outcome": ((B,), torch.int32),
-                "record": ((P, record_doubles(1, B)), torch.float64)}
+                "winner_outcome": ((B,), torch.int32)}
         return {k: torch.empty(spec[k][0], dtype=spec[k][1], device=d) for k in fields}
 
     def new_counters(self):
@@ -353,7 +327,7 @@ class AuctionEngine:
         if inputs["ctx"].shape != (self.E, B) or inputs["part"].shape != (self.P, B):
             raise ValueError("inputs must be SoA: ctx [E][B], part [P][B], u [B]")
         bi = _batch_in(inputs)
-        bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
+        bo = _batch_out(outputs)
         self._check(self.L.ag_simulate(self._h, B, ctypes.byref(bi), ctypes.byref(bo),
                                  _ptr(counters), _stream()), "ag_simulate")
 
@@ -362,7 +336,7 @@ class AuctionEngine:
         inputs are drawn inside the kernel -- the same bits generate(seed, first_auction)
         writes -- so only the outputs touch HBM."""
         B = (outputs["winner"] if "winner" in outputs else outputs["winner_outcome"]).shape[0]
-        bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
+        bo = _batch_out(outputs)
         self._check(self.L.ag_simulate_generated(self._h, int(seed), int(first_auction), B, ctypes.byref(bo),
                                                  _ptr(counters), _stream()), "ag_simulate_generated")
 
@@ -622,7 +596,7 @@ class AuctionEngine:
         [first_auction, first_auction + B) (ag_shading_collect)."""
         B = inputs["u"].shape[0]
         bi = _batch_in(inputs)
-        bo = AgBatchOut(*[_ptr(outputs.get(f)).value for f in _OUT_FIELDS])
+        bo = _batch_out(outputs)
         st = self._shading(store)
         self._check(self.L.ag_shading_collect(self._h, int(first_auction), B, ctypes.byref(bi), ctypes.byref(bo),
                                               ctypes.byref(st), _stream()), "ag_shading_collect")

@@ -33,9 +33,8 @@ inline int ag_check_struct(const T *p, const char *who, const char *type) {
     if (int rc_ = ag_check_struct(p, who, type)) return rc_; \
   } while (0)
 
-// ag_batch_out of ABI 17 or of ABI 15/16 (AG_BATCH_OUT_V16_SIZE: no packed fields), read into
-// a full ABI-17 struct `v` (the packed fields NULL for the older layout); the packed record
-// must be 16-B aligned (it is written with 16-B stores).
+// ag_batch_out of ABI 17 or of ABI 15/16 (AG_BATCH_OUT_V16_SIZE: no ABI 17 fields), read into
+// a full ABI-17 struct `v` (winner_outcome NULL for the older layout).
 inline int ag_read_out(const ag_batch_out *p, ag_batch_out *v, const char *who) {
   if (!p) return ag_set_error(AG_ERR_INVALID, "%s: null ag_batch_out", who);
   if (p->struct_size == (uint64_t)sizeof(ag_batch_out)) {
@@ -51,8 +50,6 @@ inline int ag_read_out(const ag_batch_out *p, ag_batch_out *v, const char *who) 
                         who, (unsigned long long)p->struct_size, AG_ABI_VERSION,
                         (unsigned long long)sizeof(ag_batch_out), (unsigned long long)AG_BATCH_OUT_V16_SIZE);
   }
-  if (((uintptr_t)v->record & 15u) != 0)
-    return ag_set_error(AG_ERR_INVALID, "%s: ag_batch_out.record must be 16-B aligned", who);
   return AG_OK;
 }
 #define AG_READ_OUT(p, v, who) \

@@ -449,7 +449,6 @@ int simulate_oracle(ag_ctx *c, OraKernel k, int64_t B, const ag_batch_in *in, co
   prm.true_ctr = out->true_ctr;
   prm.best_ev = out->best_ev;
   prm.winner_outcome = out->winner_outcome;
-  prm.record = out->record;
   prm.partials = c->d_partials;
   const size_t lds = (size_t)prm.L.total;
   if (lds > 160 * 1024)

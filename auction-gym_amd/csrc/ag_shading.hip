@@ -17,7 +17,6 @@
 #include <stdint.h>
 
 #include "ag_host.h"
-#include "ag_record.h"
 
 namespace {
 
@@ -61,7 +60,7 @@ __global__ __launch_bounds__(kShThreads) void k_shading_collect(
       st.gamma[slot] = out.gamma[o];
       const bool oc = out.winner ? out.outcome[i] != 0 : (wo >> 31) != 0;
       st.utility[slot] = won ? v * (oc ? 1.0 : 0.0) - out.price[i] : 0.0;  // src/Bidder.py:62-63
-      if (st.ctr) st.ctr[slot] = out.est_ctr ? out.est_ctr[o] : out.record[ag::rec_field(ag::kRecLayout, (uint32_t)s, (uint32_t)i, (uint32_t)B, 1)];
+      if (st.ctr) st.ctr[slot] = out.est_ctr[o];
       if (st.value) st.value[slot] = v;
       if (st.propensity) st.propensity[slot] = out.propensity[o];
       if (st.won) st.won[slot] = won ? 1 : 0;
@@ -254,9 +253,9 @@ int ag_shading_collect(ag_ctx *c, int64_t first, int64_t B, const ag_batch_in *i
   if (!in->part || !(out->winner || out->winner_outcome) || !out->item || !out->price || !out->gamma)
     return ag_set_error(AG_ERR_INVALID, "ag_shading_collect: needs in.part, out.winner + out.outcome (or "
                                         "out.winner_outcome), out.item, out.price, out.gamma");
-  if ((s->ctr && !out->est_ctr && !out->record) || (s->propensity && !out->propensity))
+  if ((s->ctr && !out->est_ctr) || (s->propensity && !out->propensity))
     return ag_set_error(AG_ERR_INVALID, "ag_shading_collect: the store's ctr / propensity need "
-                                        "out.est_ctr (or out.record) / out.propensity");
+                                        "out.est_ctr / out.propensity");
   AgDeviceGuard g(c->device);
   hipLaunchKernelGGL(k_shading_collect, dim3(grid_over(B)), dim3(kShThreads), 0, (hipStream_t)stream, first, B,
                      c->shape.num_participants, c->shape.num_items, in->part, *out, c->d_bkind, c->d_values, *s,

@@ -10,7 +10,6 @@
 #include "ag_exp.h"
 #include "ag_exp_table.h"
 #include "ag_log1p.h"
-#include "ag_record.h"
 
 namespace ag {
 
@@ -367,28 +366,7 @@ __device__ __forceinline__ void stg(T *p, T v) {
   if constexpr (AG_NT_STORES) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
-// ABI 17 packed layout: record indexing in ag_record.h; the stores
-template <int LAYOUT = kRecLayout>
-__device__ __forceinline__ void st_record_half(double *rec, uint32_t s, uint32_t i, uint32_t B, int h, double a,
-                                               double b) {
-  if constexpr (LAYOUT == 2) {  // one 16-B store; the wave's 64 lanes cover 1 KB contiguously
-    const uint32_t T = (B + 63) >> 6;
-    const size_t j = ((((size_t)s * T + (i >> 6)) * 2 + h) * 64 + (i & 63)) * 2;
-    stg(reinterpret_cast<f64x2 *>(rec + j), f64x2{a, b});
-  } else if constexpr (LAYOUT == 1) {
-    const size_t j = rec_index(1, s, i, B, h);
-    stg(rec + j, a);
-    stg(rec + j + 64, b);
-  } else {
-    stg(reinterpret_cast<f64x2 *>(rec + rec_index(0, s, i, B, h)), f64x2{a, b});
-  }
-}
-__device__ __forceinline__ void st_record_lo(double *rec, uint32_t s, uint32_t i, uint32_t B, double bid, double est) {
-  st_record_half(rec, s, i, B, 0, bid, est);
-}
-__device__ __forceinline__ void st_record_hi(double *rec, uint32_t s, uint32_t i, uint32_t B, double tru, double bev) {
-  st_record_half(rec, s, i, B, 1, tru, bev);
-}
+// ABI 17: winner and outcome as one word (ag_batch_out.winner_outcome)
 __device__ __forceinline__ uint32_t pack_wo(int w, int oc) { return (uint32_t)w | ((uint32_t)(oc & 1) << 31); }
 
 template <int W>
@@ -1108,10 +1086,6 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
         if (out.best_ev) stg(out.best_ev + o, q.bev);
         if (out.gamma) stg(out.gamma + o, q.gamma);
         if (out.propensity) stg(out.propensity + o, q.prop);
-        if (out.record) {
-          st_record_lo(out.record, s, i, B, q.bid, q.est);
-          st_record_hi(out.record, s, i, B, q.ctr, q.bev);
-        }
         top2_step(s, q.bid, m1, m2, w);
         if (w == s) ctr_w = q.ctr;  // the current leader's true CTR
       }
@@ -1174,10 +1148,6 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
         if (out.best_ev) stg(out.best_ev + o, q.bev);
         if (out.gamma) stg(out.gamma + o, q.gamma);
         if (out.propensity) stg(out.propensity + o, q.prop);
-        if (out.record) {
-          st_record_lo(out.record, s, i, B, q.bid, q.est);
-          st_record_hi(out.record, s, i, B, q.ctr, q.bev);
-        }
         if (prm.want_counters) count_pre(a, q.ctr, q.val, q.est, q.bev);
         bidv[s] = q.bid;
         tvv[s] = q.ctr * q.val;
@@ -1244,7 +1214,6 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
         if (out.est_ctr) stg(out.est_ctr + o, q.est);
         if (out.true_ctr) stg(out.true_ctr + o, q.ctr);
         if (out.best_ev) stg(out.best_ev + o, q.bev);
-        if (out.record) st_record_hi(out.record, s, i, B, q.ctr, q.bev);
         if (prm.want_counters) count_pre(a, q.ctr, q.val, q.est, q.bev);
         bidv[s] = q.bid;
         valv[s] = q.val;
@@ -1332,7 +1301,6 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
       for (int s = 0; s < P; ++s) {
         const uint32_t o = s * B + i;
         if (out.bid) stg(out.bid + o, bidv[s]);
-        if (out.record) st_record_lo(out.record, s, i, B, bidv[s], estv[s]);
         if (out.gamma) stg(out.gamma + o, gmv[s]);
         if (out.propensity) stg(out.propensity + o, prv[s]);
         top2_step(s, bidv[s], m1, m2, w);
@@ -1402,13 +1370,6 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
       if (out.best_ev) st_f64<W>(out.best_ev + o, ev);
       if (out.gamma) st_f64<W>(out.gamma + o, gv);
       if (out.propensity) st_f64<W>(out.propensity + o, pv2);
-      if (out.record) {
-#pragma unroll
-        for (int q = 0; q < W; ++q) {
-          st_record_lo(out.record, s, i + q, B, bv[q], sv[q]);
-          st_record_hi(out.record, s, i + q, B, cv[q], ev[q]);
-        }
-      }
     }
     {
       int wv[W], ov[W];

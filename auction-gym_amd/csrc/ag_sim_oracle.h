@@ -45,6 +45,9 @@ constexpr double kOraMaxValue = 1024.0;
 #ifndef AG_ORA_PREFETCH
 #define AG_ORA_PREFETCH 0  // software-pipelined input loads (A/B: make variant VFLAGS=-DAG_ORA_PREFETCH=1)
 #endif
+#ifndef AG_ORA_STORE_LATE
+#define AG_ORA_STORE_LATE 1  // every per-slot output stored after the slots, field by field (A/B: 0 stores each slot's as it resolves; 3.73 -> 3.59 ms per 2^27, profiles/r05h_ab_packed.log)
+#endif
 constexpr int kOraFlush = 255;
 constexpr int kOraBlocksPerCu = 4;  // default persistent grid (ag_kernels.hip simulate_oracle)
 __host__ inline int64_t ora_lane_cap(int R) { return 512 * (int64_t)R; }
@@ -96,8 +99,7 @@ struct OraParams {
   uint8_t *outcome;
   int32_t *item;
   double *bid, *est_ctr, *true_ctr, *best_ev;
-  uint32_t *winner_outcome;  // ABI 17 packed layout: [B] winner | outcome << 31
-  double *record;            // ... {bid, est_ctr, true_ctr, best_ev} per (slot, auction)
+  uint32_t *winner_outcome;  // ABI 17: [B] winner | outcome << 31
   int64_t *partials;  // [grid][N][AG_NUM_COUNTERS][2]
   // generate mode (GEN): inputs drawn on the chip as ag_generate draws them
   uint64_t seed, first;  // Philox key; global index of auction 0 of the batch
@@ -277,6 +279,10 @@ __global__ __launch_bounds__(kThreads) void k_oracle(OraParams prm) {
     int w = 0;
     double m1 = 0.0, m2 = -INFINITY, ctr_w = 0.0, val_w = 0.0;
     double bevs[P];
+#if AG_ORA_STORE_LATE
+    int itv[P];
+    double bdv[P], ctv[P];
+#endif
 #pragma unroll
     for (int s = 0; s < P; ++s) {
       const int a = ag[s];
@@ -312,16 +318,18 @@ __global__ __launch_bounds__(kThreads) void k_oracle(OraParams prm) {
       const double v = vv[best];
       const double b = v * c;  // TruthfulBidder.bid: value * estimated CTR (src/Bidder.py:35)
       bevs[s] = sc;  // max_k CTR_k * value_k (src/Auction.py:53); == b for an Oracle agent
+#if AG_ORA_STORE_LATE
+      itv[s] = best;
+      bdv[s] = b;
+      ctv[s] = c;
+#else
       const uint32_t o = s * B + i;
       if (prm.item) stg(prm.item + o, (int32_t)best);
       if (prm.bid) stg(prm.bid + o, b);
       if (prm.est_ctr) stg(prm.est_ctr + o, c);
       if (prm.true_ctr) stg(prm.true_ctr + o, c);
       if (prm.best_ev) stg(prm.best_ev + o, sc);
-      if (prm.record) {  // ABI 17 packed record: the same four values
-        st_record_lo(prm.record, s, i, B, b, c);
-        st_record_hi(prm.record, s, i, B, c, sc);
-      }
+#endif
       // streaming top-2, ties -> lowest slot (src/AuctionAllocation.py:19-34)
       if (s == 0) {
         m1 = b;
@@ -339,6 +347,24 @@ __global__ __launch_bounds__(kThreads) void k_oracle(OraParams prm) {
     }
     const double price = fp ? m1 : m2;
     const int oc = bernoulli(ctr_w, u);  // src/Auction.py:65 (true CTR of the winner's item)
+#if AG_ORA_STORE_LATE
+    // every per-slot output after the slots, field by field
+#pragma unroll
+    for (int s = 0; s < P; ++s)
+      if (prm.item) stg(prm.item + s * B + i, (int32_t)itv[s]);
+#pragma unroll
+    for (int s = 0; s < P; ++s)
+      if (prm.bid) stg(prm.bid + s * B + i, bdv[s]);
+#pragma unroll
+    for (int s = 0; s < P; ++s)
+      if (prm.est_ctr) stg(prm.est_ctr + s * B + i, ctv[s]);
+#pragma unroll
+    for (int s = 0; s < P; ++s)
+      if (prm.true_ctr) stg(prm.true_ctr + s * B + i, ctv[s]);
+#pragma unroll
+    for (int s = 0; s < P; ++s)
+      if (prm.best_ev) stg(prm.best_ev + s * B + i, bevs[s]);
+#endif
     if (prm.winner) stg(prm.winner + i, (int32_t)w);
     if (prm.price) stg(prm.price + i, charged ? price : (double)NAN);
     if (prm.second_price) stg(prm.second_price + i, charged ? m2 : (double)NAN);

@@ -173,18 +173,15 @@ typedef struct ag_batch_out {
   double *propensity;    /* [P][B] density of gamma under the bidder's logging policy:
                             the Gaussian around prev_gamma (uninitialised learning
                             bidders) or the fitted policy's (DR); NaN otherwise          */
-  /* ABI 17, the packed record layout (opt-in; NULL = not written; may be combined with the
-   * per-field arrays above, which then are written too). The reference logs each
-   * participation as ONE record (ImpressionOpportunity, src/Impression.py:4-31, appended
-   * at src/Agent.py:55-66): these hold the same values as the per-field arrays, bit for bit,
-   * in fewer, wider store streams (ag_simulate writes each as 16-B accesses). */
-  uint32_t *winner_outcome; /* [B] winner | outcome << 31 (winner: the slot, as `winner`)   */
-  double *record;        /* [P][B][4] per (slot, auction): {bid, est_ctr, true_ctr, best_ev}
-                            (32 B, 16-B aligned), the values of those four arrays          */
+  /* ABI 17 (opt-in; NULL = not written): winner and outcome as one word. A byte-wide
+   * outcome stream is the costliest of the per-field arrays: with this word instead of
+   * `winner` + `outcome` the headline kernel runs 5-7 % faster (profiles/r05i_ab_packed.log). */
+  uint32_t *winner_outcome; /* [B] winner | outcome << 31 (winner: the slot, as `winner`)    */
 } ag_batch_out;
-/* Size of the ABI 15/16 ag_batch_out (without the packed fields): still accepted as
- * struct_size, the packed fields then read as NULL. */
+/* Size of the ABI 15/16 ag_batch_out (without winner_outcome): still accepted as struct_size,
+ * winner_outcome then reads as NULL. */
 #define AG_BATCH_OUT_V16_SIZE ((uint64_t)(8 + 11 * sizeof(void *)))
+
 
 /* Create a context on `device` for one auction population (src/main.py:98-109
  * instantiate_auction). Validates the shape; allocates device workspace once. */

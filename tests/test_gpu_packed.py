@@ -1,10 +1,8 @@
-"""ABI 17 packed output layout (include/auctiongym.h ag_batch_out.winner_outcome / .record):
-the same values as the per-field arrays, bit for bit, on every simulate kernel -- k_oracle
-(replay and generate mode), the general kernel's kept-slot, early-count and streamed-slot
-paths -- and the learner stores collected from packed-only outputs equal those collected
-from the per-field arrays. The reference logs one ImpressionOpportunity record per
-participation (src/Impression.py:4-31, appended at src/Agent.py:55-66); the packed record is
-that record's {bid, estimated_CTR, true_CTR, best_expected_value} in one 32-B row.
+"""ABI 17 winner | outcome word (include/auctiongym.h ag_batch_out.winner_outcome): the same
+values as the per-field winner and outcome arrays, bit for bit, on every simulate kernel --
+k_oracle in replay and generate mode; the general kernel's kept-slot, early-count,
+streamed-slot and runtime-P paths -- and the learner stores collected with it equal those
+collected from the per-field arrays (src/Auction.py:60-65: the winner and its click).
 """
 import ctypes
 
@@ -27,10 +25,9 @@ def _same(a, b):
 def _check_packed(per_field, packed):
     from auctiongym_amd.engine import unpack_outputs
     up = unpack_outputs(packed)
-    for f in ("winner", "outcome", "bid", "est_ctr", "true_ctr", "best_ev"):
-        assert _same(per_field[f], up[f]), f
-    for f in ("price", "item"):
-        assert _same(per_field[f], packed[f]), f
+    for f in per_field:
+        if f in up:
+            assert _same(per_field[f], up[f]), f
 
 
 def _oracle_engine(N, P, mech, seed=0):
@@ -44,29 +41,28 @@ def _oracle_engine(N, P, mech, seed=0):
 
 @pytest.mark.parametrize("N,P,mech,B", [(6, 2, 1, (1 << 20) + 37), (8, 3, 0, 5000), (4, 1, 1, 999),
                                         (32, 8, 1, 1 << 16)])
-def test_oracle_kernel_packed_equals_per_field(gpu, N, P, mech, B):
-    """k_oracle (the headline kernel): packed outputs == per-field outputs, replay and
-    generate mode, counters unchanged by the layout."""
+def test_oracle_kernel_winner_word_equals_per_field(gpu, N, P, mech, B):
+    """k_oracle (the headline kernel): the headline's output set (winner | outcome word, the
+    other arrays per field) == the per-field outputs, replay and generate mode, the counters
+    unchanged by the layout."""
     import torch
-    from auctiongym_amd.engine import PACKED_FIELDS
+    from auctiongym_amd.engine import HEADLINE_FIELDS
     eng = _oracle_engine(N, P, mech)
     inp = eng.alloc_inputs(B)
     eng.generate(3, 11, inp)
     a = eng.alloc_outputs(B, PER_FIELD)
-    b = eng.alloc_outputs(B, PACKED_FIELDS)
-    ca, cb = eng.new_counters(), eng.new_counters()
+    ca = eng.new_counters()
     eng.simulate(inp, a, ca)
-    eng.simulate(inp, b, cb)
-    torch.cuda.synchronize()
-    _check_packed(a, b)
-    assert torch.equal(ca, cb)
-    # generate mode (inputs drawn on the chip): the same again
-    g = eng.alloc_outputs(B, PACKED_FIELDS)
-    cg = eng.new_counters()
-    eng.simulate_generated(3, 11, g, cg)
-    torch.cuda.synchronize()
-    _check_packed(a, g)
-    assert torch.equal(ca, cg)
+    b = eng.alloc_outputs(B, HEADLINE_FIELDS + ("second_price",))
+    for gen in (False, True):
+        cb = eng.new_counters()
+        if gen:
+            eng.simulate_generated(3, 11, b, cb)
+        else:
+            eng.simulate(inp, b, cb)
+        torch.cuda.synchronize()
+        _check_packed(a, b)
+        assert torch.equal(ca, cb), gen
     eng.close()
 
 
@@ -98,11 +94,11 @@ def test_abi16_batch_out_is_still_accepted(gpu):
     torch.cuda.synchronize()
     for k in PER_FIELD:
         assert _same(ref[k], out[k]), k
-    # a misaligned record is refused
-    rec = torch.empty(2 * B * 4 + 1, dtype=torch.float64, device="cuda")
-    bo2 = _lib.AgBatchOut(*[None] * 12, rec.data_ptr() + 8)
-    rc = eng.L.ag_simulate(eng._h, B, ctypes.byref(bi), ctypes.byref(bo2), None, None)
-    assert rc == _lib.AG_ERR_INVALID and b"16-B aligned" in eng.L.ag_last_error()
+    # any other struct size is refused
+    bo.struct_size = ctypes.sizeof(OutV16) + 4
+    rc = eng.L.ag_simulate(eng._h, B, ctypes.byref(bi), ctypes.cast(ctypes.pointer(bo), ctypes.POINTER(_lib.AgBatchOut)),
+                           None, None)
+    assert rc == _lib.AG_ERR_INVALID and b"struct_size" in eng.L.ag_last_error()
     eng.close()
 
 
@@ -132,11 +128,11 @@ def _mixed_engine(P, block):
 
 
 @pytest.mark.parametrize("P,B,block", [(2, (1 << 17) + 45, 0), (2, 3001, 1024), (8, 1 << 15, 0), (12, 4000, 0)])
-def test_general_kernel_packed_equals_per_field_and_collects(gpu, P, B, block):
+def test_general_kernel_winner_word_and_collects(gpu, P, B, block):
     """The general kernel (LR-TS / shading / fitted-policy mix; P = 2 kept slots, the
-    1024-lane early-count path, P = 8 streamed slots, P = 12 the runtime-P kernel): packed ==
-    per-field, and the LR-TS and learning-bidder stores collected from packed-only outputs
-    (winner_outcome + record) hold the same records."""
+    1024-lane early-count path, P = 8 streamed slots, P = 12 the runtime-P kernel): the
+    winner | outcome word == the per-field winner and outcome, and the LR-TS and
+    learning-bidder stores collected with it (no winner / outcome arrays) hold the same records."""
     import torch
     eng = _mixed_engine(P, block)
     inp = eng.alloc_inputs(B)
@@ -144,14 +140,13 @@ def test_general_kernel_packed_equals_per_field_and_collects(gpu, P, B, block):
     eng.generate_noise(9, 0, inp)
     full = PER_FIELD + ("gamma", "propensity")
     a = eng.alloc_outputs(B, full)
-    b = eng.alloc_outputs(B, ("winner_outcome", "price", "second_price", "item", "record", "gamma", "propensity"))
+    b = eng.alloc_outputs(B, ("winner_outcome", "price", "second_price", "item", "bid", "est_ctr", "true_ctr",
+                              "best_ev", "gamma", "propensity"))  # no winner / outcome arrays
     ca, cb = eng.new_counters(), eng.new_counters()
     eng.simulate(inp, a, ca)
     eng.simulate(inp, b, cb)
     torch.cuda.synchronize()
     _check_packed(a, b)
-    for f in ("second_price", "gamma", "propensity"):
-        assert _same(a[f], b[f]), f
     assert torch.equal(ca, cb)
     # stores from both layouts: the same multisets of records
     la, lb = eng.new_lrts_samples(2 * B), eng.new_lrts_samples(2 * B)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""ABI 17 packed output layout vs the per-field layout on the headline kernel (k_oracle,
+"""The ABI 17 winner | outcome word vs the per-field winner and outcome arrays on the headline kernel (k_oracle,
 SP_Oracle shape, 2^27 auctions unless given): the same launch back to back in ONE process,
 alternating, with the outputs checked equal bit for bit. Also the general kernel on
 SP_Truthful_TS (configs_1) when --pop is given. Diagnostic only.
@@ -17,7 +17,7 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 from auctiongym_amd import _lib  # noqa: E402
-from auctiongym_amd.engine import AuctionEngine, PACKED_FIELDS, unpack_outputs  # noqa: E402
+from auctiongym_amd.engine import AuctionEngine, HEADLINE_FIELDS, unpack_outputs  # noqa: E402
 
 
 P, E = 2, 5
@@ -47,14 +47,14 @@ def main():
     inp = eng.alloc_inputs(B)
     eng.generate(0, 0, inp)
     per_field = eng.alloc_outputs(B, FIELDS)
-    packed = eng.alloc_outputs(B, PACKED_FIELDS)
+    packed = eng.alloc_outputs(B, HEADLINE_FIELDS)
     cnt = eng.new_counters()
     cnt2 = eng.new_counters()
     eng.simulate(inp, per_field, cnt)
     torch.cuda.synchronize()
     eng.simulate(inp, packed, cnt2)
     torch.cuda.synchronize()
-    up = unpack_outputs(packed, P, B)
+    up = unpack_outputs(packed)
     for f in FIELDS:
         a, b = per_field[f], up[f].contiguous()
         if a.dtype == torch.float64:
@@ -65,11 +65,19 @@ def main():
     reads = 8 * E + 4 * P + 8
     writes = {"per-field (13 streams)": 4 + 8 + 1 + 36 * P}
     outs = {"per-field (13 streams)": (per_field, None)}
-    wo_fields = ("winner_outcome", "price", "item", "bid", "est_ctr", "true_ctr", "best_ev")
     writes["per-field, winner_outcome (12)"] = 4 + 8 + 36 * P
-    outs["per-field, winner_outcome (12)"] = (eng.alloc_outputs(B, wo_fields), None)
-    writes["packed (6 streams)"] = 4 + 8 + 36 * P
-    outs["packed (6 streams)"] = (packed, None)
+    outs["per-field, winner_outcome (12)"] = (eng.alloc_outputs(B, HEADLINE_FIELDS), None)
+    writes["per-field, winner_outcome, 5/CU"] = 4 + 8 + 36 * P
+    outs["per-field, winner_outcome, 5/CU"] = (packed, 5)
+    engs = {n: eng for n in outs}
+    for v in [a[len("--lib="):] for a in sys.argv[1:] if a.startswith("--lib=")]:  # make variant builds
+        ev = AuctionEngine(6, P, 12, E, 4, _lib.SECOND_PRICE, 1.0, device=0,
+                           lib_path=os.path.join(ROOT, "auction-gym_amd", "build", "variants", f"libauctiongym_hip_{v}.so"))
+        ev.load_catalog(items, values)
+        for n in ("per-field (13 streams)", "per-field, winner_outcome (12)"):
+            writes[f"{v}: {n}"] = writes[n]
+            outs[f"{v}: {n}"] = outs[n]
+            engs[f"{v}: {n}"] = ev
     for _ in range(30):
         cnt.zero_()
         eng.simulate(inp, per_field, cnt)
@@ -77,10 +85,12 @@ def main():
     t = {n: [] for n in outs}
     for r in range(6):
         for n, (o, lay) in outs.items():
+            e = engs[n]
+            e.set_blocks_per_cu(lay or 0)
 
-            def step(o=o):
+            def step(o=o, e=e):
                 cnt.zero_()
-                eng.simulate(inp, o, cnt)
+                e.simulate(inp, o, cnt)
             t[n] += timeit(step, reps=2, inner=5)
     for n in outs:
         ms = float(np.median(t[n]))

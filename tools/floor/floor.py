@@ -58,6 +58,8 @@ def main():
         "floor nt 4/CU, tiled outputs": lambda: L.floor_run(6, cus * 4, ctypes.byref(p2), B, sp),
         "floor nt 4/CU, tiled in + out": lambda: L.floor_run(7, cus * 4, ctypes.byref(p2), B, sp),
         "floor nt 8/CU, tiled in + out": lambda: L.floor_run(7, cus * 8, ctypes.byref(p2), B, sp),
+        "floor nt 4/CU, 16-B tiles in + out": lambda: L.floor_run(8, cus * 4, ctypes.byref(p2), B, sp),
+        "floor nt 8/CU, 16-B tiles in + out": lambda: L.floor_run(8, cus * 8, ctypes.byref(p2), B, sp),
         "ag_simulate (r04 fields)": lambda: eng.simulate(inp, out, cnt),
         "ag_simulate (bench: winner|outcome)": lambda: eng.simulate(inp, outw, cnt),
         "ag_simulate, no counters": lambda: eng.simulate(inp, out, None),

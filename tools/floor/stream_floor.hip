@@ -157,8 +157,34 @@ __global__ __launch_bounds__(256) void k_floor_tiled(Ptrs p, int64_t B) {
     one_tiled<TIN, TOUT>(p, B, i);
 }
 
+// 16-B tiles: inputs [T][{x0,x1},{x2,x3},{x4,u}][64] (3 KB) + [T][part0|part1][64] (512 B);
+// outputs [T][{price,bid0},{bid1,est0},{est1,tru0},{tru1,bev0},{bev1,item0|item1}][64] (5 KB)
+// + [T][winner|outcome][64] (256 B): every lane access 16 B except the part pair and the word.
+__global__ __launch_bounds__(256) void k_floor_tiled16(Ptrs p, int64_t B) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < B; i += (int64_t)gridDim.x * 256) {
+    const int64_t t = i >> 6, l = i & 63;
+    const f64x2 *tin = reinterpret_cast<const f64x2 *>(p.ctx + t * 7 * 64) + l;
+    const f64x2 c0 = __builtin_nontemporal_load(tin), c1 = __builtin_nontemporal_load(tin + 64),
+                c2 = __builtin_nontemporal_load(tin + 128);
+    const i32x2 a = __builtin_nontemporal_load(reinterpret_cast<const i32x2 *>(p.ctx + t * 7 * 64 + 384) + l);
+    const double u = c2.y;
+    const double s = c0.x + c0.y + c1.x + c1.y + c2.x;
+    const int32_t wo = (int32_t)((uint32_t)(a.x > a.y) | ((uint32_t)(u > 0.5) << 31));
+    unsigned char *to = reinterpret_cast<unsigned char *>(p.price) + t * 84 * 64;
+    f64x2 *d = reinterpret_cast<f64x2 *>(to) + l;
+    __builtin_nontemporal_store(f64x2{s * u, s}, d);
+    __builtin_nontemporal_store(f64x2{s + u, c0.x}, d + 64);
+    __builtin_nontemporal_store(f64x2{c0.y, c1.x}, d + 128);
+    __builtin_nontemporal_store(f64x2{c1.y, c2.x}, d + 192);
+    __builtin_nontemporal_store(f64x2{u, __builtin_bit_cast(double, a)}, d + 256);
+    __builtin_nontemporal_store(wo, reinterpret_cast<int32_t *>(to + 80 * 64) + l);
+  }
+}
+
 extern "C" int floor_run(int persistent, int grid, const Ptrs *p, int64_t B, void *stream) {
-  if (persistent >= 5 && persistent <= 7) {
+  if (persistent == 8) {
+    hipLaunchKernelGGL(k_floor_tiled16, dim3(grid), dim3(256), 0, (hipStream_t)stream, *p, B);
+  } else if (persistent >= 5 && persistent <= 7) {
     auto k = persistent == 5 ? k_floor_tiled<true, false> : persistent == 6 ? k_floor_tiled<false, true>
                                                                             : k_floor_tiled<true, true>;
     hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, (hipStream_t)stream, *p, B);
