@@ -532,6 +532,17 @@ constexpr int kTsGroup = AG_TS_GROUP;
 constexpr int kTsScreenK = 12;
 constexpr int kShipDo = 5;   // the shipped configs' LR-TS model width (OE = 4)
 constexpr int kGenShip = 8;  // pick_kernel_for: OR-ed into `general` for that width (D = 6)
+// the noise of items k0 .. k0 + kTsGroup - 1 (coefficient stride 64: the tile layout). (Tried:
+// non-temporal loads of the dense layout, and loading the first group before the true-CTR
+// search: no gain / scratch spills, profiles/r05m_ab_pre.log, r05n_ab_nt.log.)
+template <int DW>
+__device__ __forceinline__ void ts_load_group(const float *nz, int k0, int K, int Do, float (&nzv)[kTsGroup][DW]) {
+#pragma unroll
+  for (int g = 0; g < kTsGroup; ++g)
+#pragma unroll
+    for (int d = 0; d < DW; ++d)
+      nzv[g][d] = (nz && k0 + g < K && d < Do) ? nz[(size_t)((k0 + g) * Do + d) * 64] : 0.0f;
+}
 template <int DW>
 __device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], const float *nz, int K, int Do,
                                          const double *vals, const uint64_t *tab) {
@@ -542,11 +553,7 @@ __device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], 
     for (int k0 = 0; k0 < kTsScreenK; k0 += kTsGroup) {
       if (k0 < K) {
         float nzv[kTsGroup][DW];
-#pragma unroll
-        for (int g = 0; g < kTsGroup; ++g)
-#pragma unroll
-          for (int d = 0; d < DW; ++d)
-            nzv[g][d] = (nz && k0 + g < K && d < Do) ? nz[(size_t)((k0 + g) * Do + d) * 64] : 0.0f;
+        ts_load_group<DW>(nz, k0, K, Do, nzv);
 #pragma unroll
         for (int g = 0; g < kTsGroup; ++g) {
           const int k = k0 + g;
@@ -598,11 +605,7 @@ __device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], 
   int best = 0;
   for (int k0 = 0; k0 < K; k0 += kTsGroup) {
     float nzv[kTsGroup][DW];
-#pragma unroll
-    for (int g = 0; g < kTsGroup; ++g)
-#pragma unroll
-      for (int d = 0; d < DW; ++d)
-        nzv[g][d] = (nz && k0 + g < K && d < Do) ? nz[(size_t)((k0 + g) * Do + d) * 64] : 0.0f;
+    ts_load_group<DW>(nz, k0, K, Do, nzv);
 #pragma unroll
     for (int g = 0; g < kTsGroup; ++g) {
       const int k = k0 + g;
@@ -693,6 +696,15 @@ struct SlotResult {
   bool pol;  // DEFER: a fitted-policy bid left to the caller (bid = value * est, gamma / prop NaN)
 };
 
+// Diagnostic ablations of the general kernel (WRONG results; make variant-p VFLAGS=-DAG_ABLATE=..):
+// 1 no fitted-policy forward (gamma 1), 2 no Thompson item choice (the true-CTR leader),
+// 4 no exact true-CTR item search (item 0, CTR 0.5), 16 no MAP estimate (0.5), 32 no re-scored
+// true CTR of the Thompson choice (the leader's)
+#ifndef AG_ABLATE
+#define AG_ABLATE 0
+#endif
+constexpr int kAblate = AG_ABLATE;
+
 template <int D, bool PRUNE, int GENERAL, bool DEFER = false>
 __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const double (&x)[kMaxD],
                                                    const float (&xf)[kMaxD], float xabs, int a, int s,
@@ -700,16 +712,19 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
                                                    int tsj = kTsjLoad) {
   // true CTRs (src/Auction.py:52-53): exact search on the true context; for an Oracle
   // agent this IS Agent.select_item (src/BidderAllocation.py:81-82)
-  double c, bs;
+  double c = 0.5, bs = 0.5;
   const double *itm = T.items + a * T.items_stride;
-  const int best_t = select_item<D, PRUNE>(itm, T.vals + a * T.values_stride,
-                                           T.scr + a * T.scr_stride, T.scr_val + a * T.scr_val_stride,
-                                           PRUNE ? T.amax[a] : 0.0f, K, T.kpairs, x, xf, xabs, T.tab, c, bs);
+  const bool lrts = GENERAL && T.akind[a] == AG_ALLOCATOR_LRTS;
+  const int best_t = (kAblate & 4) ? 0
+                                   : select_item<D, PRUNE>(itm, T.vals + a * T.values_stride,
+                                                           T.scr + a * T.scr_stride, T.scr_val + a * T.scr_val_stride,
+                                                           PRUNE ? T.amax[a] : 0.0f, K, T.kpairs, x, xf, xabs, T.tab,
+                                                           c, bs);
   int best = best_t;
   double est = c, tru = c;
   double g = NAN, prop = NAN;
   if constexpr (GENERAL) {
-    if (T.akind[a] == AG_ALLOCATOR_LRTS) {
+    if (lrts) {
       // LR-TS (src/Agent.py:29-42): the sampled CTRs on the observed context pick the
       // item by first argmax of CTR * value (float32 CTR widened to double), the MAP CTR
       // of that item is the estimate
@@ -738,9 +753,10 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
       // (per-agent Ka even when every agent has K: the uniform-K form, scalar item loops, ran
       // 2-4 % slower on every population line, profiles/r04s_ab_c*_kag.log)
       const int Ka = T.kag[a];
-      best = ts_select<D>(m, xo, nz, Ka, Do, T.vals + a * T.values_stride, T.tab);
-      est = (double)ts_ctr_k<D>(m + best * Do, xo, xo, false, Do, best, Ka, T.tab);
-      tru = best == best_t ? c : agexp::sigmoid_fast(dot_ref<D>(itm + best * D, x), T.tab);
+      best = (kAblate & 2) ? best_t
+                           : ts_select<D>(m, xo, nz, Ka, Do, T.vals + a * T.values_stride, T.tab);
+      est = (kAblate & 16) ? 0.5 : (double)ts_ctr_k<D>(m + best * Do, xo, xo, false, Do, best, Ka, T.tab);
+      tru = (best == best_t || (kAblate & 32)) ? c : agexp::sigmoid_fast(dot_ref<D>(itm + best * D, x), T.tab);
     }
   }
   const double v = T.vals[a * T.values_stride + best];
@@ -751,6 +767,9 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
     if (bk >= AG_BIDDER_VALUE_LEARNING && T.drs && T.dri[a] == AG_LEARNER_POLICY) {  // the fitted policy
       if constexpr (DEFER) {
         pol = true;
+      } else if constexpr (kAblate & 1) {
+        g = 1.0;
+        prop = 1.0;
       } else {
         policy_bid(T.drs + a * T.drs_stride + 4, est, v, in.policy_eps[(size_t)s * B + i], T.tab, g, prop);
         b = b * g;
