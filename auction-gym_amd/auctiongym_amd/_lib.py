@@ -27,7 +27,6 @@ OPT_SIM_BLOCKS_PER_CU = 8
 OPT_SIM_BLOCK_THREADS = 9
 OPT_SIM_GENERAL_MODE = 10
 OPT_SIM_SHIPPED_SHAPE = 11
-OPT_SIM_PRODUCER_WAVES = 12
 SIM_KERNEL_AUTO, SIM_KERNEL_GENERIC, SIM_KERNEL_FUSED, SIM_KERNEL_SPLIT, SIM_KERNEL_WIDE = 0, 1, 2, 3, 4
 ITEM_SEARCH_AUTO, ITEM_SEARCH_EXACT = 0, 1
 

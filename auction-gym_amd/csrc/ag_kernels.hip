@@ -732,11 +732,6 @@ int ag_set_option(ag_ctx *c, int32_t option, int64_t value) {
       if (value != 0 && value != 1) return ag_set_error(AG_ERR_INVALID, "ag_set_option: general mode must be 0 or 1");
       c->gen_mode_all = value == 1;
       return AG_OK;
-    case AG_OPT_SIM_PRODUCER_WAVES:
-      if (value < -1 || value > 15)
-        return ag_set_error(AG_ERR_INVALID, "ag_set_option: producer waves must be -1 (off), 0 (auto) or 1..15");
-      c->pc_producers = (int32_t)value;
-      return AG_OK;
     case AG_OPT_SIM_SHIPPED_SHAPE:
       if (value != 0 && value != 1) return ag_set_error(AG_ERR_INVALID, "ag_set_option: shipped shape must be 0 or 1");
       c->ship_shape = value == 1;
@@ -886,22 +881,7 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out_a
   if (bt == kLargeThreads && c->block_threads == 0 && gmode == kGenAll && ship && s.num_participants >= AG_STREAM_MIN_P &&
       s.num_participants <= kMaxP)
     bt = kMidThreads;
-  // the producer / consumer build (k_simulate PC): Thompson-sampling populations of the shipped
-  // shape at P <= 2, 1024-lane workgroups; auto: 6 producer waves for TruthfulBidder-only
-  // populations, 4 with the bid-shading work (the consumers' share grows with the FP64 work)
-  int npw = 0;
-  SimKernel k = nullptr;
-  if (c->general && ship && prune && W == 1 && c->has_lrts && c->ts_sample && in->ts_noise &&
-      s.num_participants <= 2 && c->pc_producers >= 0 && c->sim_kernel != AG_SIM_KERNEL_WIDE &&
-      (c->block_threads == 0 || c->block_threads == kLargeThreads)) {
-    npw = c->pc_producers > 0 ? c->pc_producers : (gmode == kGenTruthful ? 6 : 4);
-    k = pick_kernel(s.num_participants, D, prune, W, gmode | ship | kGenPC, kLargeThreads);
-    if (k)
-      bt = kLargeThreads;
-    else
-      npw = 0;
-  }
-  if (!k) k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
+  SimKernel k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
   if (!k && bt == kMidThreads) {
     bt = kLargeThreads;
     k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
@@ -926,14 +906,9 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out_a
   if (gmode == kGenAll && bt == kLargeThreads) {  // the compacted fitted-policy pass's per-wave task slots
     add_policy_tasks(prm.lds, bt);
     lds = (size_t)prm.lds.total;
+    if (lds > 160 * 1024)
+      return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
   }
-  prm.pc_producers = npw;
-  if (npw) {
-    add_pc_ring(prm.lds, s.num_participants, kLargeThreads / 64 - npw);
-    lds = (size_t)prm.lds.total;
-  }
-  if (lds > 160 * 1024)
-    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
   hipStream_t st = (hipStream_t)stream;
   if (lds > 64 * 1024)
     AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -941,7 +916,7 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out_a
   // each striding over bt-auction tiles.
   // (the WIDE A/B kernel has slots of its own: its occupancy is not the AUTO kernel's)
   int &res = wide_ab ? c->resident_wide[prm.want_counters ? 1 : 0]
-                     : c->resident[(npw ? 256 : 0) + (bt == kMidThreads ? 128 : 0) + (ship ? 64 : 0) + (gmode == kGenTruthful ? 32 : 0) +
+                     : c->resident[(bt == kMidThreads ? 128 : 0) + (ship ? 64 : 0) + (gmode == kGenTruthful ? 32 : 0) +
                                    (bt == kThreads ? 0 : 16) + (c->general ? 8 : 0) + (W == 2 ? 4 : 0) +
                                    (prune ? 2 : 0) + (prm.want_counters ? 1 : 0)];
   if (res == 0) {

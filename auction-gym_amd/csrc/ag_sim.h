@@ -147,7 +147,6 @@ struct LdsLayout {
   int32_t tsm_stride;      // floats between agents' LR-TS means (K * ts_do, made odd)
   int32_t drs_stride;      // floats between agents' learner models (17: odd)
   int32_t pol;             // per-wave fitted-policy task slots [BT/64][64][32 B] (0: none)
-  int32_t pc;              // producer / consumer build: the (item, est) ring [2][P][set] x 2 (0: none)
 };
 
 __host__ inline int32_t align16(int64_t b) { return (int32_t)((b + 15) & ~(int64_t)15); }
@@ -222,16 +221,7 @@ __host__ inline LdsLayout make_layout(int N, int K, int D, bool counters, bool g
   b = L.cnt + (counters ? (int64_t)R * N * L.ncnt * 8 : 0);
   L.total = align16(b);
   L.pol = 0;
-  L.pc = 0;
   return L;
-}
-
-// The producer / consumer build (k_simulate PC): `consumers` consumer waves resolve sets of
-// consumers * 64 auctions while the producer waves make the next set's LR-TS picks; the picks
-// pass through a double-buffered ring [2][P][set] of int32 items and float32 estimates.
-__host__ inline void add_pc_ring(LdsLayout &L, int P, int consumers) {
-  L.pc = L.total;
-  L.total = align16((int64_t)L.total + (int64_t)2 * P * consumers * 64 * 8);
 }
 
 // the per-wave task slots of the compacted fitted-policy pass (full general build, bt lanes)
@@ -261,7 +251,6 @@ struct SimParams {
   ag_batch_out out;
   int64_t *partials;      // [grid][N][AG_NUM_COUNTERS][2]
   int32_t P;              // participants per round (read by the runtime-P kernel, P = 0)
-  int32_t pc_producers;   // producer waves of the producer / consumer build (k_simulate PC)
 };
 
 // Screening margin. The screen ranks items by t_k = (1 + 2^(z'_k)) / v_k = 1 / (exact
@@ -543,46 +532,30 @@ constexpr int kTsGroup = AG_TS_GROUP;
 constexpr int kTsScreenK = 12;
 constexpr int kShipDo = 5;   // the shipped configs' LR-TS model width (OE = 4)
 constexpr int kGenShip = 8;  // pick_kernel_for: OR-ed into `general` for that width (D = 6)
-#ifndef AG_PC_GROUP
-#define AG_PC_GROUP 12  // producer waves: items whose Thompson noise is loaded together
-#endif
-constexpr int kGenPC = 16;   // pick_kernel_for: the producer / consumer build (P <= 2, shipped shape, 1024 lanes)
 // the noise of items k0 .. k0 + kTsGroup - 1 (coefficient stride 64: the tile layout). (Tried:
 // non-temporal loads of the dense layout, and loading the first group before the true-CTR
 // search: no gain / scratch spills, profiles/r05m_ab_pre.log, r05n_ab_nt.log.)
-template <int DW, int G = kTsGroup>
-__device__ __forceinline__ void ts_load_group(const float *nz, int k0, int K, int Do, float (&nzv)[G][DW]) {
+template <int DW>
+__device__ __forceinline__ void ts_load_group(const float *nz, int k0, int K, int Do, float (&nzv)[kTsGroup][DW]) {
 #pragma unroll
-  for (int g = 0; g < G; ++g)
+  for (int g = 0; g < kTsGroup; ++g)
 #pragma unroll
     for (int d = 0; d < DW; ++d)
       nzv[g][d] = (nz && k0 + g < K && d < Do) ? nz[(size_t)((k0 + g) * Do + d) * 64] : 0.0f;
 }
-// G: items whose noise is loaded together (kTsGroup; the producer waves of the producer /
-// consumer build load all 12 at once: no FP64 state competes for their registers)
-// pre: every item's noise already loaded by the caller ([kTsScreenK][DW], K <= kTsScreenK), or nullptr
-template <int DW, int G = kTsGroup>
+template <int DW>
 __device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], const float *nz, int K, int Do,
-                                         const double *vals, const uint64_t *tab,
-                                         const float (*pre)[DW] = nullptr) {
-  static_assert(kTsScreenK % G == 0, "G divides kTsScreenK");
+                                         const double *vals, const uint64_t *tab) {
   if (AG_TS_SCREEN && K <= kTsScreenK) {
     float zk[kTsScreenK], ek[kTsScreenK];  // logits; score estimates (-1: score exactly)
     float best_est = 0.0f;
 #pragma unroll
-    for (int k0 = 0; k0 < kTsScreenK; k0 += G) {
+    for (int k0 = 0; k0 < kTsScreenK; k0 += kTsGroup) {
       if (k0 < K) {
-        float nzv[G][DW];
-        if (pre) {
+        float nzv[kTsGroup][DW];
+        ts_load_group<DW>(nz, k0, K, Do, nzv);
 #pragma unroll
-          for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int d = 0; d < DW; ++d) nzv[g][d] = pre[k0 + g][d];
-        } else {
-          ts_load_group<DW, G>(nz, k0, K, Do, nzv);
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
+        for (int g = 0; g < kTsGroup; ++g) {
           const int k = k0 + g;
           zk[k] = 0.0f;
           ek[k] = -1.0f;
@@ -599,7 +572,7 @@ __device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], 
         }
       } else {
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
+        for (int g = 0; g < kTsGroup; ++g) {
           zk[k0 + g] = 0.0f;
           ek[k0 + g] = -1.0f;
         }
@@ -732,50 +705,11 @@ struct SlotResult {
 #endif
 constexpr int kAblate = AG_ABLATE;
 
-// An LR-TS agent's item choice (src/Agent.py:29-42): the sampled CTRs on the observed
-// context pick the item by first argmax of CTR * value (float32 CTR widened to double); the
-// MAP CTR of that item is the estimate (est, float32). x: the true context, its first Do - 1
-// dims observed (src/Auction.py:36). Called by resolve_slot, and by the producer waves of the
-// producer / consumer build (k_simulate PC), which hand (item, est) to the consumers in LDS.
-template <int D, int G = kTsGroup>
-__device__ __forceinline__ int ts_pick(const Lds &T, int K, const double *x, int a, int s, const ag_batch_in &in,
-                                       uint32_t B, uint32_t i, bool ts_sample, int tsj, float &est) {
-  const int Do = T.ts_do;
-  const float *m = T.tsm + (size_t)a * T.tsm_stride;
-  // tiled noise: coefficient c of auction i at ((s*T + i/64)*K*Do + c)*64 + i%64; the
-  // compact layout tiles the batch's LR-TS pairs only, pair j = ts_noise_index[s*B + i]
-  // in place of s*T*64 + i (mixed populations: no noise stored or fetched for the
-  // slots of other agents)
-  const float *nz = nullptr;
-  if (ts_sample && in.ts_noise) {
-    if (in.ts_noise_index) {
-      // prefetched with the tile's inputs (tsj), or loaded here
-      const uint32_t j = (uint32_t)(tsj != kTsjLoad ? tsj : ldg(in.ts_noise_index + (size_t)s * B + i));
-      nz = in.ts_noise + ((size_t)(j >> 6) * K * Do) * 64 + (j & 63);
-    } else {
-      nz = in.ts_noise + ((size_t)(s * ((B + 63) >> 6) + (i >> 6)) * K * Do) * 64 + (i & 63);
-    }
-  }
-  // observed context (src/Auction.py:36) in a register row of width D >= Do
-  float xo[D];
-#pragma unroll
-  for (int d = 0; d < D; ++d) xo[d] = d < Do - 1 ? (float)x[d] : (d == Do - 1 ? 1.0f : 0.0f);
-  // the agent's own Ka items: its torch model's rows (the sgemv block / remainder rows and
-  // the sigmoid's chunks follow Ka); the catalogue rows beyond are padding (value 0)
-  // (per-agent Ka even when every agent has K: the uniform-K form, scalar item loops, ran
-  // 2-4 % slower on every population line, profiles/r04s_ab_c*_kag.log)
-  const int Ka = T.kag[a];
-  const int best = ts_select<D, G>(m, xo, nz, Ka, Do, T.vals + a * T.values_stride, T.tab);
-  est = (kAblate & 16) ? 0.5f : ts_ctr_k<D>(m + best * Do, xo, xo, false, Do, best, Ka, T.tab);
-  return best;
-}
-
-// pk / pk_est: an LR-TS slot's (item, estimate) made by a producer wave (ts_pick), or pk < 0
 template <int D, bool PRUNE, int GENERAL, bool DEFER = false>
 __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const double (&x)[kMaxD],
                                                    const float (&xf)[kMaxD], float xabs, int a, int s,
                                                    const ag_batch_in &in, uint32_t B, uint32_t i, bool ts_sample,
-                                                   int tsj = kTsjLoad, int pk = -1, float pk_est = 0.0f) {
+                                                   int tsj = kTsjLoad) {
   // true CTRs (src/Auction.py:52-53): exact search on the true context; for an Oracle
   // agent this IS Agent.select_item (src/BidderAllocation.py:81-82)
   double c = 0.5, bs = 0.5;
@@ -791,13 +725,37 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
   double g = NAN, prop = NAN;
   if constexpr (GENERAL) {
     if (lrts) {
-      // LR-TS (src/Agent.py:29-42): the Thompson choice and its MAP estimate, here or by a producer
-      float e = pk_est;
-      if (pk >= 0)
-        best = pk;
-      else
-        best = (kAblate & 2) ? best_t : ts_pick<D>(T, K, x, a, s, in, B, i, ts_sample, tsj, e);
-      est = (double)e;
+      // LR-TS (src/Agent.py:29-42): the sampled CTRs on the observed context pick the
+      // item by first argmax of CTR * value (float32 CTR widened to double), the MAP CTR
+      // of that item is the estimate
+      const int Do = T.ts_do;
+      const float *m = T.tsm + (size_t)a * T.tsm_stride;
+      // tiled noise: coefficient c of auction i at ((s*T + i/64)*K*Do + c)*64 + i%64; the
+      // compact layout tiles the batch's LR-TS pairs only, pair j = ts_noise_index[s*B + i]
+      // in place of s*T*64 + i (mixed populations: no noise stored or fetched for the
+      // slots of other agents)
+      const float *nz = nullptr;
+      if (ts_sample && in.ts_noise) {
+        if (in.ts_noise_index) {
+          // prefetched with the tile's inputs (tsj), or loaded here
+          const uint32_t j = (uint32_t)(tsj != kTsjLoad ? tsj : ldg(in.ts_noise_index + (size_t)s * B + i));
+          nz = in.ts_noise + ((size_t)(j >> 6) * K * Do) * 64 + (j & 63);
+        } else {
+          nz = in.ts_noise + ((size_t)(s * ((B + 63) >> 6) + (i >> 6)) * K * Do) * 64 + (i & 63);
+        }
+      }
+      // observed context (src/Auction.py:36) in a register row of width D >= Do
+      float xo[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) xo[d] = d < Do - 1 ? (float)x[d] : (d == Do - 1 ? 1.0f : 0.0f);
+      // the agent's own Ka items: its torch model's rows (the sgemv block / remainder rows and
+      // the sigmoid's chunks follow Ka); the catalogue rows beyond are padding (value 0)
+      // (per-agent Ka even when every agent has K: the uniform-K form, scalar item loops, ran
+      // 2-4 % slower on every population line, profiles/r04s_ab_c*_kag.log)
+      const int Ka = T.kag[a];
+      best = (kAblate & 2) ? best_t
+                           : ts_select<D>(m, xo, nz, Ka, Do, T.vals + a * T.values_stride, T.tab);
+      est = (kAblate & 16) ? 0.5 : (double)ts_ctr_k<D>(m + best * Do, xo, xo, false, Do, best, Ka, T.tab);
       tru = (best == best_t || (kAblate & 32)) ? c : agexp::sigmoid_fast(dot_ref<D>(itm + best * D, x), T.tab);
     }
   }
@@ -851,16 +809,14 @@ template <int P, int D, bool PRUNE, int GENERAL>
 __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const double (&x)[kMaxD],
                                         const float (&xf)[kMaxD], float xabs, const int (&ag)[P], double u,
                                         const ag_batch_in &in, uint32_t B, uint32_t i, bool ts_sample,
-                                        const int (&tsj)[P], Resolved<P> &r, const int (&pk)[P],
-                                        const float (&pke)[P]) {
+                                        const int (&tsj)[P], Resolved<P> &r) {
   double m1 = 0.0, m2 = -INFINITY;
   int w = 0;
 #pragma unroll
   for (int s = 0; s < P; ++s) {
     const int a = ag[s];
     r.ag[s] = a;
-    const SlotResult q =
-        resolve_slot<D, PRUNE, GENERAL>(T, K, x, xf, xabs, a, s, in, B, i, ts_sample, tsj[s], pk[s], pke[s]);
+    const SlotResult q = resolve_slot<D, PRUNE, GENERAL>(T, K, x, xf, xabs, a, s, in, B, i, ts_sample, tsj[s]);
     r.item[s] = q.item;
     r.val[s] = q.val;
     r.bid[s] = q.bid;
@@ -888,7 +844,7 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
 // 441 -> 155 SGPRs spilled to VGPR lanes; the full build at 1024 lanes: 112 -> 52 B of
 // scratch per lane). K stays a runtime value: with it compile-time the item loops unroll
 // fully and spill (200 VGPRs at P = 2), measured.
-template <int P, int D, bool PRUNE, int W, int GENERAL, int BT = kThreads, int DOS = 0, bool PC = false>
+template <int P, int D, bool PRUNE, int W, int GENERAL, int BT = kThreads, int DOS = 0>
 __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_MIN_WAVES : AG_TB_MIN_WAVES)
                                  : (GENERAL ? ((DOS && P > 0 && P <= 2) ? AG_GEN_DOS_MIN_WAVES : AG_GEN_MIN_WAVES)
                                             : AG_MIN_WAVES)) void k_simulate(SimParams prm) {
@@ -973,14 +929,6 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
   const int rep = tid & (R - 1);
   const ag_batch_in in = prm.in;
   const ag_batch_out out = prm.out;
-  // Producer / consumer build (PC): waves [0, npw) are producers, the rest consumers; a phase's
-  // set holds cset = consumers * 64 auctions, one per consumer lane (see the phase loop below)
-  static_assert(!PC || (P > 0 && P <= 2 && W == 1 && !AG_PREFETCH), "PC: P <= 2, one auction per lane");
-  const int npw = PC ? prm.pc_producers : 0;
-  const bool producer = PC && (tid >> 6) < npw;
-  const uint32_t cset = PC ? (uint32_t)(BT / 64 - npw) * 64u : 0u;
-  int32_t *ring_item = reinterpret_cast<int32_t *>(smem + L.pc);                       // [2][P][cset]
-  float *ring_est = reinterpret_cast<float *>(smem + L.pc + (size_t)2 * P * cset * 4);  // [2][P][cset]
   // P == 0: the runtime-P kernel (more than kMaxP participants; slot results are not kept
   // in registers -- see the wide path in the loop)
   constexpr int PA = P > 0 ? P : 1;  // register array extent
@@ -992,7 +940,7 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
   int pv[PA][W];
   double uv[W];
   int jv[PA][W];  // compact ts_noise_index entries (GENERAL with ts_noise_index; else kTsjLoad)
-  const bool pre_tsj = GENERAL && !AG_PREFETCH && !PC && in.ts_noise_index && in.ts_noise && prm.ts_sample;
+  const bool pre_tsj = GENERAL && !AG_PREFETCH && in.ts_noise_index && in.ts_noise && prm.ts_sample;
   // streamed slots (below): each slot's participant / noise index loaded with the slot
   // streamed slots for TruthfulBidder-only populations (configs_1 at P = 8: 0.665 vs 0.730 ms
   // kept per-slot arrays, profiles/r04k_ab_c1p8.log) and for the full mix in its 768-lane build
@@ -1024,7 +972,7 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
   // Participation / win counts: a lane resolves at most kAuctionsPerReplica * R / BT
   // (<= 255) auctions per launch, so for N <= 8 agents its counts fit 8-bit fields of one
   // register each; flushed to the LDS counters once, after the loop.
-  const bool packed = P > 0 && N <= 8 && kAuctionsPerReplica * R / (PC ? (int)cset : BT) <= 255;
+  const bool packed = P > 0 && N <= 8 && kAuctionsPerReplica * R / BT <= 255;
   uint64_t n_logs_packed = 0, n_won_packed = 0;
   // the counter terms of one participant (src/Agent.py:96-118, via the exact LDS replicas)
   auto count_slot = [&](int a, bool won, double lp, double price, double second, double bid, double ctr,
@@ -1106,10 +1054,8 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
   double un[W];
   if (lo + blockIdx.x * (BT * W) + tid * W < hi) load_tile(lo + blockIdx.x * (BT * W) + tid * W);
 #endif
-  // One tile: auctions i .. i + W - 1 of this lane (W consecutive auctions: even chunk bounds
-  // when W = 2); PC: its LR-TS picks at ring [pkb][s][pkj]. (A do-while body: `continue` ends it.)
-  auto auction = [&](const uint32_t i, const int pkb, const uint32_t pkj) {
-   do {
+  for (uint32_t base = lo + blockIdx.x * (BT * W); base < hi; base += stride) {
+    const uint32_t i = base + tid * W;  // W consecutive auctions (even chunk bounds when W = 2)
 #if AG_PREFETCH
     if (i >= hi) continue;
 #pragma unroll
@@ -1128,8 +1074,6 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
 #define UV un
 #else
     if (i >= hi) continue;
-    (void)pkb;
-    (void)pkj;
     if constexpr (P == 0) {
       // more than kMaxP participants (runtime P): the slots are resolved in a loop, their
       // outputs written as they come; the counter terms need the winner and price, so the
@@ -1284,8 +1228,7 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
         const uint32_t o = s * B + i;
         const int a = PV[s][0];
         const SlotResult q = resolve_slot<D, PRUNE, GENERAL, kCompactPolicy>(
-            T, K, x, xf, xabs, a, s, in, B, i, prm.ts_sample != 0, AG_PREFETCH ? kTsjLoad : jv[s][0],
-            PC ? ring_item[((size_t)pkb * P + s) * cset + pkj] : -1, PC ? ring_est[((size_t)pkb * P + s) * cset + pkj] : 0.0f);
+            T, K, x, xf, xabs, a, s, in, B, i, prm.ts_sample != 0, AG_PREFETCH ? kTsjLoad : jv[s][0]);
         if (out.item) stg(out.item + o, (int32_t)q.item);
         if (out.est_ctr) stg(out.est_ctr + o, q.est);
         if (out.true_ctr) stg(out.true_ctr + o, q.ctr);
@@ -1413,17 +1356,14 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
       x[D - 1] = 1.0;  // intercept (src/Auction.py:33)
       xf[D - 1] = 1.0f;
       xabs *= 1.001f;
-      int ag[PA], tj[PA], pk[PA];
-      float pke[PA];
+      int ag[PA], tj[PA];
 #pragma unroll
       for (int s = 0; s < P; ++s) {
         ag[s] = PV[s][q];
         tj[s] = AG_PREFETCH ? kTsjLoad : jv[s][q];
-        pk[s] = PC ? ring_item[((size_t)pkb * P + s) * cset + pkj] : -1;
-        pke[s] = PC ? ring_est[((size_t)pkb * P + s) * cset + pkj] : 0.0f;
       }
       resolve<PA, D, PRUNE, GENERAL>(T, K, prm.mech, x, xf, xabs, ag, UV[q], in, B, i + q,
-                                    prm.ts_sample != 0, tj, r[q], pk, pke);
+                                    prm.ts_sample != 0, tj, r[q]);
     }
 
     // SoA stores, W auctions per access
@@ -1479,68 +1419,6 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
           count_slot(rr.ag[s], charged && s == rr.w, charged ? rr.price : 0.0, rr.price, rr.second, rr.bid[s],
                      rr.ctr[s], rr.val[s], rr.est[s], rr.bev[s], rr.oc);
       }
-    }
-   } while (0);
-  };
-
-  if constexpr (!PC) {
-    for (uint32_t base = lo + blockIdx.x * (BT * W); base < hi; base += stride) auction(base + tid * W, 0, 0);
-  } else {
-    // Producer / consumer phases. The workgroup's sets are blockIdx.x, + gridDim.x, ... In phase
-    // ph the producer waves make set ph's LR-TS picks (ts_pick: the Thompson noise stream and the
-    // float32 choice) into ring[ph & 1] while the consumer waves resolve set ph - 1 with the picks
-    // of ring[(ph - 1) & 1] (the FP64 work); one workgroup barrier per phase. The two roles keep
-    // their own registers: the noise in flight does not compete with the FP64 state. Every wave
-    // of the workgroup runs the same my_sets + 1 phases (no early exit before a barrier).
-    const uint32_t nsets = (hi - lo + cset - 1) / cset;
-    const uint32_t my_sets = nsets > blockIdx.x ? (nsets - 1 - blockIdx.x) / gridDim.x + 1 : 0;
-    for (uint32_t ph = 0; ph <= my_sets; ++ph) {
-      if (producer) {
-        if (ph < my_sets) {
-          const uint32_t base = lo + (blockIdx.x + ph * gridDim.x) * cset;
-          const int buf = (int)(ph & 1);
-          const uint32_t L_ = (uint32_t)npw * 64u, npairs = (uint32_t)P * cset;
-          const int Do = L.ts_do;
-          for (uint32_t q = (uint32_t)tid; q < npairs; q += L_) {
-            const uint32_t s = q / cset, j = q - s * cset, i = base + j;
-            if (i < hi) {
-              // the pair's participant, observed context and Thompson noise (every item's: one
-              // memory round trip per pair) loaded together, before the agent's kind is known
-              // (dense layout: the noise of a non-LR-TS pair is zeros, read and unused)
-              const int a = ldg(in.part + (size_t)s * B + i);
-              double x[kMaxD];
-#pragma unroll
-              for (int e = 0; e < D - 1; ++e) x[e] = e < Do - 1 ? ldg(in.ctx + (size_t)e * B + i) : 0.0;
-              const float *nz = nullptr;
-              if (prm.ts_sample && in.ts_noise) {
-                if (in.ts_noise_index) {
-                  const int32_t jn = ldg(in.ts_noise_index + (size_t)s * B + i);
-                  if (jn >= 0) nz = in.ts_noise + ((size_t)((uint32_t)jn >> 6) * K * Do) * 64 + (jn & 63);
-                } else {
-                  nz = in.ts_noise + ((size_t)(s * ((B + 63) >> 6) + (i >> 6)) * K * Do) * 64 + (i & 63);
-                }
-              }
-              const int Ka = T.kag[a];
-              float nzv[kTsScreenK][D];
-              ts_load_group<D, kTsScreenK>(nz, 0, Ka, Do, nzv);
-              if (T.akind[a] == AG_ALLOCATOR_LRTS) {
-                float xo[D];
-#pragma unroll
-                for (int d = 0; d < D; ++d) xo[d] = d < Do - 1 ? (float)x[d] : (d == Do - 1 ? 1.0f : 0.0f);
-                const float *m = T.tsm + (size_t)a * T.tsm_stride;
-                const int best = ts_select<D, kTsScreenK>(m, xo, nz, Ka, Do, T.vals + a * T.values_stride, T.tab,
-                                                           nz ? nzv : nullptr);
-                ring_item[((size_t)buf * P + s) * cset + j] = best;
-                ring_est[((size_t)buf * P + s) * cset + j] = ts_ctr_k<D>(m + best * Do, xo, xo, false, Do, best, Ka, T.tab);
-              }
-            }
-          }
-        }
-      } else if (ph >= 1) {
-        const uint32_t j = (uint32_t)(tid - npw * 64);
-        auction(lo + (blockIdx.x + (ph - 1) * gridDim.x) * cset + j, (int)((ph - 1) & 1), j);
-      }
-      __syncthreads();
     }
   }
 

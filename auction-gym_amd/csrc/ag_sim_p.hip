@@ -38,7 +38,6 @@ SimKernel pick_d(int D) {
 // P = 0: the runtime-P kernel (more than kMaxP participants), one auction per lane.
 template <>
 SimKernel pick_kernel_for<0>(int D, bool prune, int W, int general, int bt) {
-  if (general & kGenPC) return nullptr;
   general &= ~kGenShip;  // no shipped-shape build of the runtime-P kernel
   if (W != 1 || bt != kThreads || D > 8) return nullptr;
   if (general) return prune ? pick_d<0, true, 1, kGenAll>(D) : pick_d<0, false, 1, kGenAll>(D);
@@ -51,16 +50,8 @@ OraKernel pick_oracle_for<0>(int, bool) { return nullptr; }
 template <>
 SimKernel pick_kernel_for<AG_P>(int D, bool prune, int W, int general, int bt) {
   constexpr int P = AG_P;
-  const bool ship = (general & kGenShip) != 0, pc = (general & kGenPC) != 0;
-  general &= ~(kGenShip | kGenPC);
-  if (pc) {  // the producer / consumer build: shipped shape, P <= 2, 1024 lanes
-    if constexpr (P == 2) {
-      if (!(general && ship && prune && D == 6 && W == 1 && bt == kLargeThreads)) return nullptr;
-      if (general == kGenTruthful) return k_simulate<P, 6, true, 1, kGenTruthful, kLargeThreads, kShipDo, true>;
-      return k_simulate<P, 6, true, 1, kGenAll, kLargeThreads, kShipDo, true>;
-    }
-    return nullptr;
-  }
+  const bool ship = (general & kGenShip) != 0;
+  general &= ~kGenShip;
   if (general && ship && prune && D == 6) {  // the shipped shape: LR-TS width 5 compile-time
     if (bt == kLargeThreads) return k_simulate<P, 6, true, 1, kGenAll, kLargeThreads, kShipDo>;
     if constexpr (P >= AG_STREAM_MIN_P)  // the full mix at P >= 3: streamed, 768 lanes

@@ -243,16 +243,10 @@ typedef enum ag_option {
   AG_OPT_SIM_GENERAL_MODE = 10,   /* value: 0 = auto (TruthfulBidder-only populations run the
                                      general kernel built without the bid-shading code: fewer
                                      VGPRs), 1 = always the full general build; identical results */
-  AG_OPT_SIM_SHIPPED_SHAPE = 11,  /* value: 1 (default) = general populations of the shipped
+  AG_OPT_SIM_SHIPPED_SHAPE = 11   /* value: 1 (default) = general populations of the shipped
                                      shape (E = 5, OE = 4) run a build of the general kernel
                                      with the LR-TS model width compile-time; 0 = the
                                      runtime-width build; identical results */
-  AG_OPT_SIM_PRODUCER_WAVES = 12  /* ABI 17. value: producer waves (1..15) of the general kernel's
-                                     producer / consumer build -- shipped shape, P <= 2, Thompson
-                                     sampling: 1024-lane workgroups whose producer waves stream the
-                                     Thompson noise and make the LR-TS item choices of the next set
-                                     of auctions while the consumer waves resolve the current one;
-                                     0 = auto, -1 = the single-role build; identical results */
 } ag_option;
 
 typedef enum ag_sim_kernel {

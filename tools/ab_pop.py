@@ -11,8 +11,6 @@ interleaved in ONE process; outputs and counters checked equal across builds.
     "bt1024" force the workgroup size; "grouporder" is the base library reading the compact
     Thompson noise with its pairs ranked in (64-auction group, slot, auction) order instead of
     ag_ts_noise_index's (slot, auction) order (one contiguous run per wave over all its slots).
-    "pcoff" / "pc<N>": the base library without / with N producer waves in the general kernel's
-    producer / consumer build (AG_OPT_SIM_PRODUCER_WAVES).
 """
 import os
 import sys
@@ -36,8 +34,7 @@ def main():
         key, P = key.split(":")[0], int(key.split(":")[1])
     vdir = os.path.join(ROOT, "auction-gym_amd", "build", "variants")
     paths = {"base": _lib.LIB_PATH}
-    special = {"generic", "wide", "bt256", "bt1024", "nocnt", "noship", "grouporder", "pcoff"} | {
-        f"pc{n}" for n in range(1, 16)}
+    special = {"generic", "wide", "bt256", "bt1024", "nocnt", "noship", "grouporder"}
     for n in sys.argv[2:]:  # "<variant>+generic": that build with k_simulate forced
         v = n[:-len("+generic")] if n.endswith("+generic") else n
         paths[n] = _lib.LIB_PATH if v in special else os.path.join(vdir, f"libauctiongym_hip_{v}.so")
@@ -68,9 +65,6 @@ def main():
             eng.set_simulate_kernel(True)
         if n == "noship":  # k_simulate's runtime-shape build
             eng._check(eng.L.ag_set_option(eng._h, _lib.OPT_SIM_SHIPPED_SHAPE, 0), "ag_set_option")
-        if n == "pcoff" or (n.startswith("pc") and n[2:].isdigit()):  # the producer / consumer build
-            eng._check(eng.L.ag_set_option(eng._h, _lib.OPT_SIM_PRODUCER_WAVES, -1 if n == "pcoff" else int(n[2:])),
-                       "ag_set_option")
         if n in ("bt256", "bt1024"):
             eng._check(eng.L.ag_set_option(eng._h, _lib.OPT_SIM_BLOCK_THREADS, int(n[2:])), "ag_set_option")
         inp = eng.alloc_inputs(B)
