@@ -311,10 +311,64 @@ def record_counts_over_ranks(eng, store, group=None):
     return allc.sum(0), allc[:rank].sum(0)
 
 
-RP_POLL_LAUNCHES = 64  # epoch launches between two polls of the learners' progress
+RP_POLL_LAUNCHES = 64  # epoch launches between two polls of the learners' progress (even)
+# record-parallel epochs: each block of launches + exchanges captured in a hipGraph. Off by
+# default: measured in one process (tools/rp_issue.py, profiles/r05s_rp_issue.log) the eager
+# per-epoch loop costs 2-3 us per epoch over the launches issued back to back from C, against
+# 33-38 us of kernel per epoch -- the host already runs ahead -- and the graph saved nothing
+# there; an untested RCCL-in-graph capture is not worth the 8-GPU run's risk
+RP_GRAPH = False
 
 
-def bidder_update_record_parallel(eng, store, learners, group=None, poll=RP_POLL_LAUNCHES):
+def _capturable(group, exchange):
+    """The block can be captured: the exchange runs on the device stream (RCCL, or a
+    stand-in device copy); gloo goes through host memory and is issued eagerly."""
+    if exchange is not None:
+        return True
+    return dist.is_initialized() and dist.get_backend(group) == "nccl"
+
+
+def rp_epoch_blocks(epoch, tot, done, poll=RP_POLL_LAUNCHES, exchange=None, group=None, graph=None):
+    """Run the record-parallel epochs until done(): blocks of `poll` (even) iterations of
+    [one epoch launch -> exchange of its int64 totals tot[k & 1]], done() polled between blocks.
+    The exchange is the SUM over the ranks (_allreduce_sum; `exchange` replaces it, e.g. a
+    same-size device copy standing in for it in one process). With graph (default RP_GRAPH)
+    and a device-side exchange the first block is captured into a hipGraph (torch.cuda.CUDAGraph)
+    and replayed: one host call per block instead of two per epoch. The launches' arguments
+    depend only on the launch parity (ag_*_rp_epoch), so an even-length block replays exactly:
+    the same launches, in the same order, as the eager loop. Returns the blocks run."""
+    if poll % 2:
+        raise ValueError("poll must be even (a block must end on the parity it starts with)")
+    ex = exchange or (lambda t: _allreduce_sum(t, group))
+    graph = RP_GRAPH if graph is None else graph
+
+    def block():
+        for _ in range(poll):
+            k = epoch()
+            ex(tot[k & 1])
+
+    if graph and _capturable(group, exchange):
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g):  # recorded, not run: no launch happens here
+            block()
+        # (rp.k advanced by the even block on the host, no launch ran: the parity is unchanged)
+        n = 0
+        while True:
+            g.replay()
+            n += 1
+            if done():
+                return n
+    n = 0
+    while True:
+        block()
+        n += 1
+        if done():
+            return n
+
+
+def bidder_update_record_parallel(eng, store, learners, group=None, poll=RP_POLL_LAUNCHES, exchange=None,
+                                  graph=None):
     """Agent.update of the exact-sum learning bidders (ValueLearningBidder, DoublyRobustBidder;
     src/Bidder.py:204-325, :473-615) record-parallel: every rank trains every learner on its own
     records, one launch per epoch (ag_bidder_rp_epoch), each epoch's exact int64 partial sums
@@ -328,23 +382,26 @@ def bidder_update_record_parallel(eng, store, learners, group=None, poll=RP_POLL
     total, base = record_counts_over_ranks(eng, store, group)
     tot = eng.bidder_rp_begin(store, agents=mask, records_total=total, records_base=base)
     sel = mask.astype(bool)
-    while True:
-        if world > 1:
-            for _ in range(poll):
-                k = eng.bidder_rp_epoch(1)
-                _allreduce_sum(tot[k & 1], group)
-        else:
-            eng.bidder_rp_epoch(4 * poll)
+
+    def done():
         fit, ep, _ = eng.bidder_rp_poll()
-        if (fit[sel] < 0).all():
-            break
+        return bool((fit[sel] < 0).all())
+    if world > 1 or exchange is not None:
+        rp_epoch_blocks(lambda: eng.bidder_rp_epoch(1), tot, done, poll, exchange, group, graph)
+    else:  # one process, nothing to exchange: the launches back to back from C
+        while True:
+            eng.bidder_rp_epoch(4 * poll)
+            if done():
+                break
     return eng.bidder_rp_end()
 
 
 def record_parallel_pays(num_learners, world):
     """DESIGN.md section 7's cost model: agent-parallel gives each owner ceil(A / G) agents of
     G times one GPU's records, i.e. ceil(A / G) * G / A of one GPU's update work; record-parallel
-    keeps one GPU's work plus one small all-reduce per epoch (measured ~0.6 of it at G = 8)."""
+    keeps one GPU's work plus one small all-reduce per epoch. The threshold is a cost model, not
+    a measurement: no 8-GPU run of the update exists here (the per-epoch issue cost at world 1
+    is measured, tools/rp_issue.py)."""
     A = int(num_learners)
     if world <= 1 or A == 0:
         return False
@@ -361,7 +418,8 @@ def bidder_update(eng, store, learners, group=None):
     return bidder_update_agent_parallel(eng, store, learners, group)
 
 
-def lrts_update_record_parallel(eng, store, lrts_agents, group=None, poll=RP_POLL_LAUNCHES):
+def lrts_update_record_parallel(eng, store, lrts_agents, group=None, poll=RP_POLL_LAUNCHES, exchange=None,
+                                graph=None):
     """Agent.update of the LR-TS allocators (src/BidderAllocation.py:29-65) record-parallel:
     every rank keeps its own won samples, the fit runs one launch per epoch (ag_lrts_rp_epoch)
     with each epoch's exact partials (and the Laplace terms) all-reduced -- every rank ends
@@ -379,15 +437,14 @@ def lrts_update_record_parallel(eng, store, lrts_agents, group=None, poll=RP_POL
         _allreduce_sum(t, group)
         cnt = t
     tot = eng.lrts_rp_begin(store, agents=mask, samples_total=cnt.cpu().numpy())
-    while True:
-        if world > 1:
-            for _ in range(poll):
-                k = eng.lrts_rp_epoch(1)
-                _allreduce_sum(tot[k & 1], group)
-        else:
+    if world > 1 or exchange is not None:
+        rp_epoch_blocks(lambda: eng.lrts_rp_epoch(1), tot, lambda: eng.lrts_rp_poll() == 0, poll, exchange, group,
+                        graph)
+    else:
+        while True:
             eng.lrts_rp_epoch(4 * poll)
-        if eng.lrts_rp_poll() == 0:
-            break
+            if eng.lrts_rp_poll() == 0:
+                break
     return eng.lrts_rp_end()
 
 

@@ -348,20 +348,21 @@ def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True, cpu_thread
 
     elapsed, kern_ms = timed_steps(step, steps, warmup, world, stream)
     bpa = algorithmic_bytes_ts(E, P, K, Do)
-    traffic = None
+    traffic = traffic_src = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tfile):
         with open(tfile) as f:
             tj = json.load(f).get("configs_1" if P == 2 else f"configs_1_p{P}", {})
         if tj.get("batch") == B:
             traffic = tj.get("hbm_bytes_per_launch")
+            traffic_src = tj.get("source")
     res = {"workload": "SP_Truthful_TS (configs[1]): 8 LR-TS Thompson-sampling truthful bidders, "
                        f"K=12, E=5, OE=4, P={P}, SecondPrice",
            "value": B * world * steps / elapsed, "unit": "auctions/s", "ms_per_step": elapsed / steps * 1e3,
            "auctions_per_gpu_per_step": B, "kernel_ms": kern_ms, "algorithmic_bytes_per_auction": bpa,
            "roofline": {"bound": "hbm", "achieved": bpa * B / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": bpa * B / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                        "traffic": traffic}}
+                        "traffic": traffic, "traffic_source": traffic_src}}
     if cpu_threads:
         rate, dt, passes, same = cpu_baseline_population(eng, items, values, inp, out, np.ones(N, np.int32),
                                                          np.zeros(N, np.int32), None, None, 1 << 15, cpu_threads)
@@ -656,13 +657,14 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
 
     elapsed, kern_ms = timed_steps(step, steps, warmup, world, stream)
     bpa = algorithmic_bytes_population(E, P, K, Do, ak, bk, init, compact)
-    traffic = None
+    traffic = traffic_src = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tfile):
         with open(tfile) as f:
             tj = json.load(f).get(key if P == 2 else f"{key}_p{P}", {})
         if tj.get("batch") == B:
             traffic = tj.get("hbm_bytes_per_launch")
+            traffic_src = tj.get("source")
     if cpu_threads:
         rate, dt, passes, same = cpu_baseline_population(eng, dims["items"], dims["values"], inp, out, ak, bk, st_fit,
                                                          init, 1 << 14, cpu_threads)
@@ -675,7 +677,7 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
                 "kernel_ms": kern_ms, "algorithmic_bytes_per_auction": bpa,
                 "roofline": {"bound": "hbm", "achieved": bpa * B / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": bpa * B / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                             "traffic": traffic}})
+                             "traffic": traffic, "traffic_source": traffic_src}})
     eng.close()
     return res
 
