@@ -29,21 +29,36 @@ __device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, ui
 }
 
 // One synthetic auction (ag_generate; fused into k_oracle's generate mode): Philox4x32-10
-// keyed by seed, counter = (global auction index, sub-stream). u ~ U[0,1) with 53 bits
-// (stream 0); the participants by Floyd's algorithm, slot order = insertion order (stream
-// 1); the context as Box-Muller pairs (stream 2), ctx = 0 + scale * z (numpy normal(0,
-// scale)). oracle/ag_oracle.c ora_gen_* restate it. part holds P <= MAXP entries, x E.
+// keyed by seed, counter = (global auction index, block, stream). Stream 0, block 0: u ~ U[0,1)
+// with 53 bits from words 0-1, the first two participants (Floyd's algorithm, slot order =
+// insertion order) from words 2-3; later picks from stream 1, four per call. The context
+// (stream 2, two Box-Muller pairs per call): normals z ~ N(0, 1) from 32-bit uniforms in
+// float32 -- the hardware log2 / sqrt / sin / cos (v_sin_f32(t) = sin(2 pi t)), |z| <= 6.7 --,
+// ctx = scale * z (numpy normal(0, scale) in distribution; tests check it). Round 5: 3
+// Philox calls per SP_Oracle auction instead of 5 and no FP64 log / sincos (the generate mode
+// was VALU-bound on them). oracle/ag_oracle.c ora_gen_* restate u and the participants bit
+// for bit. part holds P <= MAXP entries, x E.
+__device__ __forceinline__ float gen_normal_r(uint32_t a) {  // sqrt(-2 ln u1), u1 = (a + 1) / 2^32 in (0, 1]
+  const float u1 = (float)(((double)a + 1.0) * 0x1p-32);
+  return __builtin_sqrtf(-2.0f * 0.693147180559945309f * __builtin_amdgcn_logf(u1));
+}
 template <int MAXP, int MAXE>
 __device__ __forceinline__ void gen_auction(uint32_t k0, uint32_t k1, uint64_t idx, int N, int P, int E,
                                             double scale, double (&x)[MAXE], int (&part)[MAXP], double &u) {
   const uint32_t c0 = (uint32_t)idx, c1 = (uint32_t)(idx >> 32);
-  uint32_t w[4];
+  uint32_t w[4], v[4];
   philox(c0, c1, 0, 0, k0, k1, w);
   u = (double)((((uint64_t)w[0] << 32) | w[1]) >> 11) * 0x1p-53;
   for (int j = N - P; j < N; ++j) {
     const int step = j - (N - P);
-    if ((step & 3) == 0) philox(c0, c1, (uint32_t)(step >> 2), 1, k0, k1, w);
-    int pick = (int)(((uint64_t)w[step & 3] * (uint64_t)(j + 1)) >> 32);
+    uint32_t word;
+    if (step < 2) {
+      word = w[2 + step];
+    } else {
+      if (((step - 2) & 3) == 0) philox(c0, c1, (uint32_t)((step - 2) >> 2), 1, k0, k1, v);
+      word = v[(step - 2) & 3];
+    }
+    int pick = (int)(((uint64_t)word * (uint64_t)(j + 1)) >> 32);
     for (int q = 0; q < step; ++q)
       if (part[q] == pick) {
         pick = j;
@@ -52,13 +67,10 @@ __device__ __forceinline__ void gen_auction(uint32_t k0, uint32_t k1, uint64_t i
     part[step] = pick;
   }
   for (int m = 0; 2 * m < E; ++m) {
-    philox(c0, c1, (uint32_t)m, 2, k0, k1, w);
-    const double u1 = (double)(((((uint64_t)w[0] << 32) | w[1]) >> 11) + 1) * 0x1p-53;
-    const double u2 = (double)((((uint64_t)w[2] << 32) | w[3]) >> 11) * 0x1p-53;
-    const double r = sqrt(-2.0 * log(u1));
-    double sn, cs;
-    sincospi(2.0 * u2, &sn, &cs);
-    x[2 * m] = 0.0 + scale * (r * cs);
-    if (2 * m + 1 < E) x[2 * m + 1] = 0.0 + scale * (r * sn);
+    if ((m & 1) == 0) philox(c0, c1, (uint32_t)(m >> 1), 2, k0, k1, v);
+    const float r = gen_normal_r(v[2 * (m & 1)]);
+    const float t = (float)v[2 * (m & 1) + 1] * 0x1p-32f;  // [0, 1]
+    x[2 * m] = 0.0 + scale * (double)(r * __builtin_amdgcn_cosf(t));
+    if (2 * m + 1 < E) x[2 * m + 1] = 0.0 + scale * (double)(r * __builtin_amdgcn_sinf(t));
   }
 }

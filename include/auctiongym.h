@@ -299,8 +299,8 @@ int ag_simulate_generated(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, in
 
 /* Synthetic replay inputs for auctions [first_auction, first_auction + B) (dev, SoA):
  * Philox4x32-10 keyed by seed and the GLOBAL auction index, so a sharded batch is
- * bit-identical to the unsharded one. ctx ~ N(0, embedding_var) (Box-Muller), part =
- * P distinct of N (Floyd), u ~ U[0,1) with 53 bits. */
+ * bit-identical to the unsharded one. ctx ~ N(0, embedding_var) (Box-Muller in float32 from
+ * 32-bit uniforms, ABI 17), part = P distinct of N (Floyd), u ~ U[0,1) with 53 bits. */
 int ag_generate(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B, double *ctx_out,
                 int32_t *part_out, double *u_out, void *stream);
 

@@ -409,14 +409,23 @@ double ora_gen_uniform(uint64_t seed, uint64_t idx) {
 }
 
 /* Floyd's sampling of P distinct agents out of N; slot order = insertion order.
- * Step j (j = N-P .. N-1) draws t = floor(word * (j+1) / 2^32) from stream 1. */
+ * Step j (j = N-P .. N-1) draws t = floor(word * (j+1) / 2^32): steps 0 and 1 from words 2-3 of
+ * stream 0's block 0 (the call whose words 0-1 make u), later steps from stream 1, four per
+ * call (csrc/ag_philox.h gen_auction, round 5). */
 void ora_gen_participants(uint64_t seed, uint64_t idx, int32_t N, int32_t P, int32_t *part_out) {
-  uint32_t w[4];
+  uint32_t w0[4], w[4];
   int32_t n = 0;
+  block(seed, idx, 0, 0, w0);
   for (int32_t j = N - P; j < N; ++j) {
     int32_t step = j - (N - P);
-    if ((step & 3) == 0) block(seed, idx, (uint32_t)(step >> 2), 1, w);
-    uint32_t t = (uint32_t)(((uint64_t)w[step & 3] * (uint64_t)(j + 1)) >> 32);
+    uint32_t word;
+    if (step < 2) {
+      word = w0[2 + step];
+    } else {
+      if (((step - 2) & 3) == 0) block(seed, idx, (uint32_t)((step - 2) >> 2), 1, w);
+      word = w[(step - 2) & 3];
+    }
+    uint32_t t = (uint32_t)(((uint64_t)word * (uint64_t)(j + 1)) >> 32);
     int32_t pick = (int32_t)t;
     for (int32_t q = 0; q < n; ++q)
       if (part_out[q] == pick) {

@@ -120,6 +120,14 @@ def test_generator_matches_oracle(gpu, oracle):
         assert np.array_equal(part[:, i], oracle.gen_participants(1234, idx, 32, 8))
     assert abs(ctx.mean()) < 0.01 and abs(ctx.std() - 1.0) < 0.01
     assert (np.sort(part, axis=0)[1:] != np.sort(part, axis=0)[:-1]).all()
+    # the contexts' distribution (float32 Box-Muller from 32-bit uniforms, round 5): N(0, 1) by a
+    # Kolmogorov-Smirnov test over 500k draws, and the tails' frequencies
+    from scipy import stats
+    z = ctx.ravel()
+    assert stats.kstest(z, "norm").pvalue > 1e-4
+    for t, p in ((2.0, 0.0455), (3.0, 0.0027), (4.0, 6.33e-5)):
+        f = float(np.mean(np.abs(z) > t))
+        assert abs(f - p) < 5 * np.sqrt(p / z.size) + 1e-6, (t, f, p)
     eng.close()
 
 
