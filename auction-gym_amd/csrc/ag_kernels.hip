@@ -464,7 +464,9 @@ int simulate_oracle(ag_ctx *c, OraKernel k, int64_t B, const ag_batch_in *in, co
   // 4 persistent workgroups per CU than on 8 or 16, tools/floor/copy_peak.py)
   int res = res_max;
   {
-    const int per_cu = c->grid_per_cu > 0 ? c->grid_per_cu : kOraBlocksPerCu;
+    // generate mode (no input stream, VALU-heavier): as many as fit (5 at 87 VGPRs) --
+    // 4.02 -> 3.87 ms per 2^27 auctions (profiles/r05w_ab_gen.log)
+    const int per_cu = c->grid_per_cu > 0 ? c->grid_per_cu : (in ? kOraBlocksPerCu : 8);
     int cus = 0;
     AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
     if ((int64_t)per_cu * cus < res) res = per_cu * cus;
