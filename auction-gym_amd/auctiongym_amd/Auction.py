@@ -128,6 +128,10 @@ class Auction:
         self._learner = self._lrts | self._shading_rec
         self._stores = {}                       # device record stores, by learner family
         self._bounds = {"lrts": 0, "shading": 0}  # upper bounds of the records they hold
+        # LR-TS updates deferred until something needs their result (_settle_lrts), so that
+        # the agents updated one after the other train in one launch
+        self._lrts_pending = np.zeros(N, bool)
+        self._lrts_drop = np.zeros(N, bool)  # cleared agents whose won samples go at the settle
 
     def _load_lrts(self):
         K, Do = self._engine.K, self.obs_embedding_size + 1
@@ -174,6 +178,7 @@ class Auction:
 
     def simulate_opportunity(self):
         """One round (src/Auction.py:28-74), queued into the next batched launch."""
+        self._settle_lrts()
         self._draw_round()
         if len(self._pending) >= self._flush_limit():
             self._flush()
@@ -222,6 +227,7 @@ class Auction:
         draw_rounds_native_population: the same numbers and the same numpy and torch generator
         states afterwards as the per-round loop); otherwise the per-round Python loop."""
         B = int(B)
+        self._settle_lrts()
         if not self._native_draws():
             for _ in range(B):
                 self._draw_round()
@@ -265,6 +271,7 @@ class Auction:
 
     def simulate_synthetic(self, B, seed, first_auction=0):
         """B rounds with on-device Philox inputs (throughput mode; parity via the oracle)."""
+        self._settle_lrts()
         self._flush()
         eng = self._engine
         inp = eng.alloc_inputs(int(B))
@@ -409,13 +416,13 @@ class Auction:
         mask = np.zeros(len(self.agents), np.int32)
         mask[index] = 1
         if self._lrts[index]:
-            st = self._stores.get("lrts") or eng.new_lrts_samples(1)
-            ep = _lrts_train(eng, st, mask)
-            m, q, pm = eng.lrts_state()
-            rm = ag.allocator.response_model
-            k = self._num_items[index]  # the agent's own rows
-            rm.m, rm.q, rm.prev_iter_m = (torch.from_numpy(np.ascontiguousarray(x[index, :k])) for x in (m, q, pm))
-            ag.allocator.epochs = int(ep[index])
+            # deferred: trained with the other LR-TS agents' updates at the next round, posterior
+            # read or repeated update (_settle_lrts); on the samples it holds now (rounds cannot
+            # be added before the settle), so the result is this call's
+            if self._lrts_pending[index]:
+                self._settle_lrts()
+            self._lrts_pending[index] = True
+            ag.allocator._settle = self._settle_lrts
         if self._empirical[index]:
             st = self._stores.get("shading") or eng.new_shading_samples(1, learning=bool(self._learning.any()))
             pg = eng.empirical_update(st, agents=mask)
@@ -429,26 +436,75 @@ class Auction:
         st = self._stores.get("shading") or eng.new_shading_samples(1, learning=True)
         learner_update(eng, st, index, self.agents[index].bidder, self.agents[index].name)
 
+    def _settle_lrts(self):
+        """The deferred LR-TS updates (_update_agent), trained together: every LR-TS agent's in
+        one persistent launch (ag_lrts_update) when all of them are pending -- the reference's
+        main loop updates every agent each iteration --, otherwise the pending ones alone
+        (_lrts_train, the resumable update with their mask). Each agent trains on its own won
+        samples, exact sums: the same posteriors and epochs as one update per call
+        (tools/dropin_update_cost.py checks it; 747 -> 79 ms for configs[1]'s 8 agents,
+        profiles/r05z_dropin_update.log). Then the won samples of the agents cleared meanwhile
+        leave the store."""
+        if not self._lrts_pending.any():
+            return
+        idx = np.flatnonzero(self._lrts_pending)
+        mask = self._lrts_pending.astype(np.int32)
+        self._lrts_pending[:] = False
+        for i in idx:
+            self.agents[i].allocator._settle = None
+        eng = self._engine
+        st = self._stores.get("lrts") or eng.new_lrts_samples(1)
+        if np.array_equal(mask.astype(bool), self._lrts):
+            ep = eng.lrts_update(st)
+        else:
+            ep = _lrts_train(eng, st, mask)
+        m, q, pm = eng.lrts_state()
+        for i in idx:
+            al = self.agents[i].allocator
+            rm = al.response_model
+            k = self._num_items[i]  # the agent's own rows
+            rm.m, rm.q, rm.prev_iter_m = (torch.from_numpy(np.ascontiguousarray(x[i, :k])) for x in (m, q, pm))
+            al.epochs = int(ep[i])
+        if self._lrts_drop.any():
+            drop = self._lrts_drop.copy()
+            self._lrts_drop[:] = False
+            self._drop_records("lrts", drop)
+
+    def _drop_records(self, name, drop):
+        """Remove the records of the agents `drop` (bool [N]) from the device store `name`."""
+        st = self._stores.get(name)
+        if st is None:
+            return
+        n = min(int(st["count"][0].item()), self._bounds[name])
+        agent = (((st["key"][:n].to(torch.int64) >> 16) & 0xFFFF) if name == "lrts"
+                 else st["agent"][:n].to(torch.int64))
+        keep = ~torch.from_numpy(drop).to(agent.device)[agent]
+        m = int(keep.sum().item())
+        if m < n:
+            for k, v in st.items():
+                if k != "count":
+                    v[..., :m] = v[..., :n][..., keep]
+        st["count"][0] = m
+        self._bounds[name] = m
+
     def _cleared_logs(self, index):
         """Agent.clear_logs (src/Agent.py:124-129) of agent `index`: its records leave the device
         stores; with memory = M the last M go back (the records its next update trains on and its
-        metrics read, src/Agent.py:81-94)."""
+        metrics read, src/Agent.py:81-94). The won samples of an agent whose LR-TS update is
+        still deferred leave at the settle (it trains on them)."""
         if not self._learner[index]:
             return
         self._flush()
-        for name, st in self._stores.items():
-            n = min(int(st["count"][0].item()), self._bounds[name])
-            agent = (((st["key"][:n].to(torch.int64) >> 16) & 0xFFFF) if name == "lrts"
-                     else st["agent"][:n].to(torch.int64))
-            keep = agent != index
-            m = int(keep.sum().item())
-            if m < n:
-                for k, v in st.items():
-                    if k != "count":
-                        v[..., :m] = v[..., :n][..., keep]
-            st["count"][0] = m
-            self._bounds[name] = m
         cols = self.agents[index]._kept
+        if cols is not None:  # memory: the kept samples go back now, so the update runs first
+            self._settle_lrts()
+        drop = np.zeros(len(self.agents), bool)
+        drop[index] = True
+        for name in list(self._stores):
+            if name == "lrts" and self._lrts_pending[index]:
+                self._lrts_drop[index] = True
+                continue
+            self._drop_records(name, drop)
         if cols is not None:
             self._append_kept(index, cols)
 

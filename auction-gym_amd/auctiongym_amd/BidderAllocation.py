@@ -67,12 +67,35 @@ class PyTorchLogisticRegressionAllocator(Allocator):
     kind = _lib.ALLOCATOR_LRTS
 
     def __init__(self, rng, embedding_size, num_items, thompson_sampling=True):
+        # an Auction defers this allocator's update to train it together with the other LR-TS
+        # agents' (Auction._settle_lrts); reading the posterior or the epochs runs it first
+        self._settle = None
         self.response_model = PyTorchLogisticRegression(n_dim=embedding_size, n_items=num_items)
         self.thompson_sampling = thompson_sampling
         self.embedding_size = embedding_size
         self.num_items = num_items
         self.epochs = None  # epochs run by the last update (None: not updated yet)
         super().__init__(rng)
+
+    @property
+    def response_model(self):
+        if self._settle is not None:
+            self._settle()
+        return self._response_model
+
+    @response_model.setter
+    def response_model(self, model):
+        self._response_model = model
+
+    @property
+    def epochs(self):
+        if self._settle is not None:
+            self._settle()
+        return self._epochs
+
+    @epochs.setter
+    def epochs(self, n):
+        self._epochs = n
 
     def estimate_CTR(self, context, sample=True):
         """src/BidderAllocation.py:67-68 on the GPU (ag_estimate_ctr): float32 CTRs [K] of the

@@ -12,6 +12,16 @@
 #ifndef AG_BAR_FANIN
 #define AG_BAR_FANIN 16
 #endif
+// AG_COOP_FENCED=1: the combining-tree sums below with the C++-model hand-off as well -- every
+// thread an agent-scope fence (__threadfence: release + acquire) after its atomics and before
+// the workgroup barrier that precedes an arrival, and again after the barrier that follows an
+// observed arrival / generation move. The default (0) relies on gfx950's ordering of
+// sc1 atomics after s_waitcnt vmcnt(0) + the workgroup barrier (see agent_allreduce_start);
+// the fenced build is the A/B and the fallback if that ever proves wrong
+// (tests/test_gpu_coop.py stresses both forms through ag_coop_selftest).
+#ifndef AG_COOP_FENCED
+#define AG_COOP_FENCED 0
+#endif
 
 namespace agcoop {
 
@@ -89,6 +99,13 @@ __device__ __forceinline__ void agent_barrier(unsigned *bar, int rank, int nblk)
 // agent_allreduce_i64's fences.
 // F: the tree's fan-in (bar_lines(nblk, F) lines / rows per region).
 #define AG_VMCNT0() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#if AG_COOP_FENCED
+#define AG_COOP_REL() __threadfence()
+#define AG_COOP_ACQ() __threadfence()
+#else
+#define AG_COOP_REL() ((void)0)
+#define AG_COOP_ACQ() ((void)0)
+#endif
 template <int F = kBarFanIn>
 __device__ __forceinline__ bool agent_allreduce_start(unsigned *bar, int64_t *acc, int stride, int rank, int nblk,
                                                       const int64_t *vals, int W, unsigned *s_gen, int *s_flag) {
@@ -106,6 +123,7 @@ __device__ __forceinline__ bool agent_allreduce_start(unsigned *bar, int64_t *ac
     const int nodes = (members_prev + F - 1) / F, q = idx / F;
     const int members = members_prev - q * F < F ? members_prev - q * F : F;
     AG_VMCNT0();
+    AG_COOP_REL();
     __syncthreads();  // this workgroup's additions to the node are performed before it arrives
     if (t == 0) {
       unsigned *cnt = bar + (size_t)(base + q) * kBarLineWords;
@@ -116,6 +134,7 @@ __device__ __forceinline__ bool agent_allreduce_start(unsigned *bar, int64_t *ac
     }
     __syncthreads();
     if (!*s_flag) break;
+    AG_COOP_ACQ();
     int64_t *node = acc + (size_t)(base + q) * stride;
     int64_t *dst = nodes == 1 ? acc : acc + (size_t)(base + nodes + q / F) * stride;
     for (int j = t; j < W; j += nt) {  // (the arriving wave; the others after the barrier above)
@@ -135,6 +154,7 @@ __device__ __forceinline__ bool agent_allreduce_start(unsigned *bar, int64_t *ac
     members_prev = nodes;
   }
   AG_VMCNT0();
+  AG_COOP_REL();
   __syncthreads();  // the root's totals (and every zeroed node) are stored before the generation moves
   if (t == 0 && root) __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return root;
@@ -149,6 +169,7 @@ __device__ __forceinline__ void agent_allreduce_finish(unsigned *bar, const int6
       __builtin_amdgcn_s_sleep(AG_BAR_SLEEP);
   }
   __syncthreads();
+  AG_COOP_ACQ();
   for (int j = t; j < W; j += nt)  // (the polling wave; the others after the barrier above)
     tot[j] = __hip_atomic_load(const_cast<int64_t *>(acc) + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
@@ -201,6 +222,7 @@ __device__ __forceinline__ void agent_reduce_nowait(unsigned *bar, int64_t *acc,
     const int nodes = (members_prev + kBarFanIn - 1) / kBarFanIn, q = idx / kBarFanIn;
     const int members = members_prev - q * kBarFanIn < kBarFanIn ? members_prev - q * kBarFanIn : kBarFanIn;
     AG_VMCNT0();
+    AG_COOP_REL();
     __syncthreads();  // this workgroup's additions to the node are performed before it arrives
     if (t == 0) {
       unsigned *cnt = bar + (size_t)(base + q) * kBarLineWords;
@@ -211,6 +233,7 @@ __device__ __forceinline__ void agent_reduce_nowait(unsigned *bar, int64_t *acc,
     }
     __syncthreads();
     if (!*s_flag) return;
+    AG_COOP_ACQ();
     int64_t *node = acc + (size_t)(base + q) * stride;
     int64_t *dst = nodes == 1 ? out : acc + (size_t)(base + nodes + q / kBarFanIn) * stride;
     for (int j = t; j < W; j += nt) {

@@ -1,0 +1,119 @@
+// ag_selftest.hip -- stress test of the learners' cross-workgroup exact sums (ag_coop.h), the
+// hand-off every trainer relies on (k_lrts_train, k_bidder_train, the pipe, the per-epoch
+// kernels): many cooperative workgroups -- spread over every XCD -- run generation after
+// generation of interleaved combining-tree all-reduces of int64 words whose totals each
+// workgroup also knows in closed form, and count every total that differs. A stale read (a
+// node row or total seen before another XCD's addition, or a counter / generation observed
+// out of order) shows up as a wrong total or a hang, so tests/test_gpu_coop.py runs it under a
+// time limit on the built form (AG_COOP_FENCED 0 by default; the fenced form is the A/B build
+// `make variant NAME=fenced VFLAGS=-DAG_COOP_FENCED=1`).
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "ag_coop.h"
+#include "ag_host.h"
+
+namespace {
+
+constexpr int kStThreads = 256;
+constexpr int kStWords = 32;     // words per all-reduce (the pipe's row width)
+constexpr int kStMaxRegions = 4;
+
+// the word a workgroup contributes: any function of (generation, region, rank, word) that
+// changes every generation
+__device__ __forceinline__ int64_t st_val(uint32_t gen, int region, int rank, int j) {
+  uint64_t x = ((uint64_t)gen << 40) ^ ((uint64_t)region << 32) ^ ((uint64_t)rank << 8) ^ (uint64_t)j;
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (int64_t)x;
+}
+
+// Every workgroup is a member of every region (as in k_bidder_pipe, where each workgroup takes
+// part in every learner's sum): generation g starts the regions' sums one after the other and
+// then finishes them in the same order, so up to `regions` sums climb the trees at once.
+__global__ __launch_bounds__(kStThreads) void k_coop_stress(unsigned *bars, int64_t *acc, int lines, int regions,
+                                                            int gens, unsigned long long *bad) {
+  __shared__ int64_t s_vals[kStMaxRegions][kStWords], s_tot[kStMaxRegions][kStWords], s_want[kStWords];
+  __shared__ unsigned s_gen[kStMaxRegions];
+  __shared__ int s_flag;
+  __shared__ bool s_root[kStMaxRegions];
+  const int t = threadIdx.x, rank = blockIdx.x, nblk = gridDim.x;
+  unsigned long long nbad = 0;
+  for (int g = 0; g < gens; ++g) {
+    for (int r = 0; r < regions; ++r) {
+      if (t < kStWords) s_vals[r][t] = st_val((uint32_t)g, r, rank, t);
+      // (agent_allreduce_start's leading workgroup barrier publishes s_vals)
+      const bool root = agcoop::agent_allreduce_start(bars + (size_t)r * lines * agcoop::kBarLineWords,
+                                                      acc + (size_t)r * lines * kStWords, kStWords, rank, nblk,
+                                                      s_vals[r], kStWords, &s_gen[r], &s_flag);
+      if (t == 0) s_root[r] = root;
+    }
+    for (int r = 0; r < regions; ++r) {
+      __syncthreads();
+      agcoop::agent_allreduce_finish(bars + (size_t)r * lines * agcoop::kBarLineWords,
+                                     acc + (size_t)r * lines * kStWords, nblk, s_root[r], &s_gen[r], kStWords,
+                                     s_tot[r]);
+      // the closed form: every rank's word summed mod 2^64 (the threads split the ranks)
+      if (t < kStWords) s_want[t] = 0;
+      __syncthreads();
+      for (int j = 0; j < kStWords; ++j) {
+        uint64_t part = 0;
+        for (int q = t; q < nblk; q += kStThreads) part += (uint64_t)st_val((uint32_t)g, r, q, j);
+        for (int o = 32; o > 0; o >>= 1) part += (uint64_t)__shfl_xor((long long)part, o, 64);
+        if ((t & 63) == 0) atomicAdd((unsigned long long *)&s_want[j], (unsigned long long)part);
+      }
+      __syncthreads();
+      if (t < kStWords && s_tot[r][t] != s_want[t]) ++nbad;
+    }
+  }
+  if (nbad) atomicAdd(bad, nbad);
+}
+
+}  // namespace
+
+extern "C" int ag_coop_selftest(int32_t device, int32_t workgroups, int32_t generations, int32_t regions,
+                                int64_t *mismatches) {
+  if (!mismatches) return ag_set_error(AG_ERR_INVALID, "ag_coop_selftest: null mismatches");
+  if (generations < 0 || regions < 1 || regions > kStMaxRegions)
+    return ag_set_error(AG_ERR_INVALID, "ag_coop_selftest: generations >= 0, regions in [1, %d]", kStMaxRegions);
+  AgDeviceGuard dg(device);
+  int cus = 0, per_cu = 0;
+  AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+  AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_coop_stress, kStThreads, 0));
+  const int cap = per_cu * cus;
+  int G = workgroups > 0 ? workgroups : 4 * cus;
+  if (G > cap)
+    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_coop_selftest: %d workgroups > %d co-resident", G, cap);
+  int lines = agcoop::bar_lines(G);
+  if (lines < 1) lines = 1;
+  // bars: [regions][lines][32] u32; acc: [regions][lines][32] int64 (zero on entry, zero again
+  // after every sum but row 0); bad: one u64
+  unsigned *bars = nullptr;
+  int64_t *acc = nullptr;
+  unsigned long long *bad = nullptr;
+  const size_t nb = (size_t)regions * lines * agcoop::kBarLineWords * sizeof(unsigned);
+  const size_t na = (size_t)regions * lines * kStWords * sizeof(int64_t);
+  hipError_t e = hipMalloc(&bars, nb);
+  if (e == hipSuccess) e = hipMalloc(&acc, na);
+  if (e == hipSuccess) e = hipMalloc(&bad, sizeof(*bad));
+  if (e == hipSuccess) e = hipMemset(bars, 0, nb);
+  if (e == hipSuccess) e = hipMemset(acc, 0, na);
+  if (e == hipSuccess) e = hipMemset(bad, 0, sizeof(*bad));
+  int rg = regions;
+  void *args[] = {&bars, &acc, &lines, &rg, &generations, &bad};
+  if (e == hipSuccess)
+    e = hipLaunchCooperativeKernel((const void *)k_coop_stress, dim3(G), dim3(kStThreads), args, 0, nullptr);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  unsigned long long h = 0;
+  if (e == hipSuccess) e = hipMemcpy(&h, bad, sizeof(h), hipMemcpyDeviceToHost);
+  (void)hipFree(bars);
+  (void)hipFree(acc);
+  (void)hipFree(bad);
+  if (e != hipSuccess) return ag_set_error(AG_ERR_HIP, "ag_coop_selftest: %s", hipGetErrorString(e));
+  *mismatches = (int64_t)h;
+  return AG_OK;
+}

@@ -22,6 +22,12 @@ namespace ag {
 #ifndef AG_EARLY_COUNT
 #define AG_EARLY_COUNT 1  // general kernel: per-slot stores and counter terms as slots resolve
 #endif
+#ifndef AG_STREAM_SYNC
+#define AG_STREAM_SYNC 0  // streamed slots (P >= 3): workgroup barrier per tile (1) or per slot (2), A/B
+#endif
+#ifndef AG_STREAM_PACK_AGENTS
+#define AG_STREAM_PACK_AGENTS 0  // streamed slots (P >= 3): the counter pass's agents kept packed in registers
+#endif
 #ifndef AG_PREFETCH
 #define AG_PREFETCH 0
 #endif
@@ -1056,6 +1062,8 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
 #endif
   for (uint32_t base = lo + blockIdx.x * (BT * W); base < hi; base += stride) {
     const uint32_t i = base + tid * W;  // W consecutive auctions (even chunk bounds when W = 2)
+    if constexpr (kStream && AG_STREAM_SYNC == 1) __syncthreads();
+    [[maybe_unused]] const bool wg_full = base + BT * W <= hi;  // uniform over the workgroup
 #if AG_PREFETCH
     if (i >= hi) continue;
 #pragma unroll
@@ -1154,10 +1162,22 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
       double m1 = 0.0, m2 = -INFINITY, ctr_w = 0.0, val_w = 0.0, rat_w = 0.0;
       int w = 0;
       double bidv[PA], tvv[PA];
+#if AG_STREAM_PACK_AGENTS
+      uint32_t apk[(PA + 1) / 2];  // the slots' agents, 16 bits each (N <= 65536), for the counter pass
+#endif
 #pragma unroll
       for (int s = 0; s < P; ++s) {
+        if constexpr (AG_STREAM_SYNC == 2) {
+          if (wg_full) __syncthreads();
+        }
         const uint32_t o = s * B + i;
         const int a = ldg(in.part + o);
+#if AG_STREAM_PACK_AGENTS
+        if (s & 1)
+          apk[s >> 1] |= (uint32_t)a << 16;
+        else
+          apk[s >> 1] = (uint32_t)a;
+#endif
         const SlotResult q = resolve_slot<D, PRUNE, GENERAL, false>(T, K, x, xf, xabs, a, s, in, B, i,
                                                                     prm.ts_sample != 0);
         if (out.item) stg(out.item + o, (int32_t)q.item);
@@ -1191,9 +1211,14 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
       if (out.winner_outcome) stg(out.winner_outcome + i, pack_wo(w, oc));
       if (prm.want_counters) {
 #pragma unroll
-        for (int s = 0; s < P; ++s)
-          count_post(ldg(in.part + s * B + i), charged && s == w, charged ? price : 0.0, price, m2, bidv[s], tvv[s],
-                     val_w, rat_w, oc);
+        for (int s = 0; s < P; ++s) {
+#if AG_STREAM_PACK_AGENTS
+          const int a = (int)((apk[s >> 1] >> (16 * (s & 1))) & 0xffffu);
+#else
+          const int a = ldg(in.part + s * B + i);
+#endif
+          count_post(a, charged && s == w, charged ? price : 0.0, price, m2, bidv[s], tvv[s], val_w, rat_w, oc);
+        }
       }
       continue;
     }

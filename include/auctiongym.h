@@ -624,6 +624,14 @@ int ag_exp(const double *x, double *out, int64_t n, void *stream);
  * lane, one 256-lane tile per workgroup, on the current device, stream-ordered. */
 int ag_stream_copy(const void *src, void *dst, int64_t nbytes, void *stream);
 
+/* Self-test of the learners' cross-workgroup exact sums (the combining-tree all-reduce every
+ * trainer runs per epoch): `workgroups` cooperative workgroups on `device` (0: 4 per CU, every
+ * XCD) run `generations` rounds of `regions` (1..4) interleaved 32-word int64 all-reduces and
+ * compare every total with its closed form; *mismatches = the wrong totals seen (0 expected).
+ * Synchronous. Test hook, no reference counterpart. */
+int ag_coop_selftest(int32_t device, int32_t workgroups, int32_t generations, int32_t regions,
+                     int64_t *mismatches);
+
 /* Thread-local description of the last error. */
 const char *ag_last_error(void);
 int32_t ag_abi_version(void);

@@ -3,9 +3,9 @@
 # passes) of the headline kernel and of the general kernel on every population line incl.
 # the P = 8 lines, the SQ passes (instruction mix, LDS bank conflicts, SALU) of the headline
 # and of configs_2 / configs_4, the driver-shaped bench line and the kernel-trace stats.
-# Usage: TAG=r04x bash tools/prof_r05.sh; then (here)
-#   python tools/make_pmc_traffic.py gpurun_out/prof_<tag> <tag> > profiles/pmc_traffic.json
+# Usage: TAG=r05x bash tools/prof_r05.sh; then (here)
 #   python tools/summarize_pmc.py gpurun_out/prof_<tag> > profiles/<tag>_pmc_summary.json
+#   python tools/make_pmc_traffic.py profiles/<tag>_pmc_summary.json > profiles/pmc_traffic.json
 set -u
 TAG=${TAG:-r05x}
 OUT=gpurun_out/prof_$TAG
