@@ -25,6 +25,9 @@ namespace ag {
 #ifndef AG_STREAM_SYNC
 #define AG_STREAM_SYNC 0  // streamed slots (P >= 3): workgroup barrier per tile (1) or per slot (2), A/B
 #endif
+#ifndef AG_XCD_MAP
+#define AG_XCD_MAP 0  // general kernel: consecutive auction tiles to the workgroups of one XCD (A/B)
+#endif
 #ifndef AG_STREAM_PACK_AGENTS
 #define AG_STREAM_PACK_AGENTS 0  // streamed slots (P >= 3): the counter pass's agents kept packed in registers
 #endif
@@ -975,6 +978,11 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
     }
   };
   const uint32_t stride = gridDim.x * (BT * W);
+  // the workgroup's tile in each grid stride: blockIdx, or with AG_XCD_MAP the workgroups of one
+  // XCD (dispatched round-robin over the 8) on consecutive tiles, so the lines two neighbouring
+  // tiles share (the compact Thompson noise's runs) meet in one L2
+  const uint32_t wg_tile = (AG_XCD_MAP && gridDim.x % 8 == 0) ? (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8
+                                                               : blockIdx.x;
   // Participation / win counts: a lane resolves at most kAuctionsPerReplica * R / BT
   // (<= 255) auctions per launch, so for N <= 8 agents its counts fit 8-bit fields of one
   // register each; flushed to the LDS counters once, after the loop.
@@ -1058,9 +1066,9 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
   double xn[kMaxD][W];
   int pn[PA][W];
   double un[W];
-  if (lo + blockIdx.x * (BT * W) + tid * W < hi) load_tile(lo + blockIdx.x * (BT * W) + tid * W);
+  if (lo + wg_tile * (BT * W) + tid * W < hi) load_tile(lo + wg_tile * (BT * W) + tid * W);
 #endif
-  for (uint32_t base = lo + blockIdx.x * (BT * W); base < hi; base += stride) {
+  for (uint32_t base = lo + wg_tile * (BT * W); base < hi; base += stride) {
     const uint32_t i = base + tid * W;  // W consecutive auctions (even chunk bounds when W = 2)
     if constexpr (kStream && AG_STREAM_SYNC == 1) __syncthreads();
     [[maybe_unused]] const bool wg_full = base + BT * W <= hi;  // uniform over the workgroup
