@@ -302,9 +302,13 @@ class AuctionEngine:
         P, T, KDo, _ = t.shape
         return np.ascontiguousarray(t.transpose(1, 3, 0, 2).reshape(T * 64, P, KDo)[:B])
 
-    def alloc_outputs(self, B, fields=None):
+    def alloc_outputs(self, B, fields=None, packed=False):
+        """Device output arrays (ag_batch_out) of B auctions; packed: the ABI 17 word
+        winner_outcome (winner | outcome << 31) instead of the winner and outcome arrays."""
         if fields is None:
             fields = _OUT_FIELDS[:11] if getattr(self, "shading", False) else _CORE_FIELDS
+        if packed:
+            fields = [f for f in fields if f not in ("winner", "outcome")] + ["winner_outcome"]
         d, P = self.device, self.P
         spec = {"winner": ((B,), torch.int32), "price": ((B,), torch.float64),
                 "second_price": ((B,), torch.float64), "outcome": ((B,), torch.uint8),

@@ -159,6 +159,8 @@ def cpu_baseline_population(eng, items, values, inp, out, ak, bk, st16, init, sa
     fn = lambda: O.simulate_pop(*args, **kw)  # noqa: E731
     fn()  # warm
     passes, dt, o = timed(fn, min_seconds)
+    from auctiongym_amd.engine import unpack_outputs
+    out = unpack_outputs(out)
     same = all(np.array_equal(out[k][..., :sample].cpu().numpy().T if out[k].dim() == 2 else
                               out[k][:sample].cpu().numpy(), o[k], equal_nan=True)
                for k in ("item", "bid", "winner", "price"))
@@ -255,8 +257,9 @@ SP_TS = dict(SP_ORACLE, agents=[{"name": "Truthful TS", "num_copies": 8, "num_it
 
 
 def algorithmic_bytes_ts(E, P, K, Do):
-    """SP_Truthful_TS replay: the Thompson noise of both participants is read from HBM."""
-    return algorithmic_bytes_per_auction(E, P, first_price=False) + P * K * Do * 4
+    """SP_Truthful_TS replay: the Thompson noise of both participants is read from HBM; winner
+    and outcome written as the one ABI 17 word."""
+    return algorithmic_bytes_per_auction(E, P, first_price=False, packed_winner=True) + P * K * Do * 4
 
 
 def timed_steps(step, steps, warmup, world, stream):
@@ -315,7 +318,7 @@ def build_sp_ts(B, local, P=None, world=1, rank=0):
     lo, hi = shard_range(B * world, rank, world)
     eng.generate(0, lo, inp)
     eng.generate_noise(0, lo, inp)
-    out = eng.alloc_outputs(B)
+    out = eng.alloc_outputs(B, packed=True)  # winner | outcome << 31 (ABI 17), as the headline
     cnt = eng.new_counters()
     torch.cuda.synchronize()
     dims = dict(N=N, K=K, E=E, P=P, OE=OE, Do=Do, items=items, values=values, lo=lo,
@@ -442,8 +445,8 @@ def algorithmic_bytes_population(E, P, K, Do, ak, bk, init, compact=False):
     reads ctx, part, u and, per participant (uniform over agents), its Thompson noise (LR-TS),
     its rsample draw (fitted policy) or shading draw (uninitialised shading); writes winner,
     price, second price, outcome and per participant item, bid, est / true CTR, best EV,
-    gamma, propensity. compact: the Thompson noise in the compact layout, located through
-    ts_noise_index (4 B per LR-TS slot)."""
+    gamma, propensity (winner and outcome as the one ABI 17 word). compact: the Thompson noise
+    in the compact layout, located through ts_noise_index (4 B per LR-TS slot)."""
     per_slot = []
     for a in range(len(ak)):
         b = K * Do * 4 + (4 if compact else 0) if ak[a] == 1 else 0  # + its ts_noise_index entry
@@ -451,7 +454,7 @@ def algorithmic_bytes_population(E, P, K, Do, ak, bk, init, compact=False):
             b += 4 if init[a] == 1 else 8
         per_slot.append(b)
     reads = 8 * E + 4 * P + 8 + P * float(np.mean(per_slot))
-    writes = 4 + 8 + 8 + 1 + P * (4 + 8 * 6)
+    writes = 4 + 8 + 8 + P * (4 + 8 * 6)  # winner_outcome, price, second price; per slot
     return reads + writes
 
 
@@ -513,7 +516,7 @@ def population_first_iteration(key, local, P=2, batch=None, world=1, rank=0):
     inp = eng.alloc_inputs(B)
     eng.generate(0, lo, inp)
     eng.generate_noise(0, lo, inp)
-    out = eng.alloc_outputs(B)
+    out = eng.alloc_outputs(B, packed=True)  # winner | outcome << 31 (ABI 17), as the headline
     cnt = eng.new_counters()
     eng.simulate(inp, out, cnt)
     torch.cuda.synchronize()

@@ -22,7 +22,10 @@ _ROUND = ("winner", "price", "second_price", "outcome")
 
 
 def _compare(out, cnt, orc, what):
-    """Device outputs ([P][B] / [B]) and counters against the oracle's ([B][P] / [B])."""
+    """Device outputs ([P][B] / [B]) and counters against the oracle's ([B][P] / [B]); a
+    winner_outcome word (the bench lines' ABI 17 output) is checked as its winner and outcome."""
+    from auctiongym_amd.engine import unpack_outputs
+    out = unpack_outputs(out)
     for k in _FIELDS:
         if k in out:
             got = np.ascontiguousarray(out[k].cpu().numpy().T)
@@ -57,7 +60,7 @@ def test_configs_1_sp_truthful_ts_full_size(gpu, oracle, P):
     orc = _oracle_on(eng, dims, inp, None, None, B)
     _compare(out, cnt, orc, f"configs_1 P={P}")
     # the bench's timed loop re-runs the same step: same bits every launch
-    out2, cnt2 = eng.alloc_outputs(B), eng.new_counters()
+    out2, cnt2 = eng.alloc_outputs(B, packed=True), eng.new_counters()
     eng.simulate(inp, out2, cnt2)
     for k in out:
         assert torch.equal(out[k], out2[k]), k

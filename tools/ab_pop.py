@@ -10,7 +10,9 @@ interleaved in ONE process; outputs and counters checked equal across builds.
     instead of the dedicated kernels), "<variant>+generic" that variant with it; "bt256" /
     "bt1024" force the workgroup size; "grouporder" is the base library reading the compact
     Thompson noise with its pairs ranked in (64-auction group, slot, auction) order instead of
-    ag_ts_noise_index's (slot, auction) order (one contiguous run per wave over all its slots).
+    ag_ts_noise_index's (slot, auction) order (one contiguous run per wave over all its slots);
+    "packed" is the base library writing the ABI 17 word winner | outcome << 31 instead of the
+    winner and outcome arrays.
 """
 import os
 import sys
@@ -34,7 +36,7 @@ def main():
         key, P = key.split(":")[0], int(key.split(":")[1])
     vdir = os.path.join(ROOT, "auction-gym_amd", "build", "variants")
     paths = {"base": _lib.LIB_PATH}
-    special = {"generic", "wide", "bt256", "bt1024", "nocnt", "noship", "grouporder"}
+    special = {"generic", "wide", "bt256", "bt1024", "nocnt", "noship", "grouporder", "packed"}
     for n in sys.argv[2:]:  # "<variant>+generic": that build with k_simulate forced
         v = n[:-len("+generic")] if n.endswith("+generic") else n
         paths[n] = _lib.LIB_PATH if v in special else os.path.join(vdir, f"libauctiongym_hip_{v}.so")
@@ -84,7 +86,13 @@ def main():
             eng._check(eng.L.ag_generate_ts_noise_compact(eng._h, 1, 0, B, _ptr(inp["part"]),
                                                           _ptr(inp["ts_noise_index"]), _ptr(inp["ts_noise"]),
                                                           _stream()), "ag_generate_ts_noise_compact")
-        out = eng.alloc_outputs(B)
+        if n == "packed":  # the ABI 17 word winner | outcome << 31 instead of the two arrays
+            from auctiongym_amd.engine import _CORE_FIELDS, _OUT_FIELDS
+            fields = [f for f in (_OUT_FIELDS[:11] if getattr(eng, "shading", False) else _CORE_FIELDS)
+                      if f not in ("winner", "outcome")] + ["winner_outcome"]
+            out = eng.alloc_outputs(B, fields)
+        else:
+            out = eng.alloc_outputs(B)
         cnt = None if n == "nocnt" else eng.new_counters()
         runs[n] = (eng, inp, out, cnt)
     _lib.LIB_PATH = base_path
@@ -97,6 +105,11 @@ def main():
     ref = runs["base"]
     for n, (eng, inp, out, cnt) in ([] if os.environ.get("AG_AB_NOCHECK") else runs.items()):  # ablations differ
         for k in out:
+            if k == "winner_outcome":
+                wo = out[k].cpu().numpy().view(np.uint32)
+                assert np.array_equal((wo & 0x7FFFFFFF).astype(np.int32), ref[2]["winner"].cpu().numpy()), n
+                assert np.array_equal((wo >> 31).astype(np.uint8), ref[2]["outcome"].cpu().numpy()), n
+                continue
             a, b = out[k].cpu().numpy(), ref[2][k].cpu().numpy()
             assert np.array_equal(a, b, equal_nan=True), (n, k)
         assert cnt is None or torch.equal(cnt, ref[3]), n
