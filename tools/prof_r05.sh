@@ -42,7 +42,8 @@ for s in ${STEPS:-bench head pops sq stats}; do
       pmc c1_sqA "$GK" "$SQA" $(ts) && pmc c1_sqB "$GK" "$SQB" $(ts) &&
       for c in 2 4; do
         pmc c${c}_sqA "$GK" "$SQA" $(pop configs_$c) && pmc c${c}_sqB "$GK" "$SQB" $(pop configs_$c) || exit 1
-      done ;;
+      done &&
+      pmc c4p8_sqA "$GK" "$SQA" $(pop configs_4 --p8-only) && pmc c4p8_sqB "$GK" "$SQB" $(pop configs_4 --p8-only) ;;
     trainer*)  # the learners' update kernels (configs_2); LAST in a call: rocprofv3 has faulted at
       # exit after cooperative kernels (r03s7), so its rc is reported, not acted on, and nothing follows
       T1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64"
