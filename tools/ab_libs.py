@@ -3,6 +3,7 @@
 bench workload, interleaved in ONE process (cdna_hip_programming.md rule 24).
 
     python tools/ab_libs.py [variant names...]      (default: every build/variants/*.so)
+    AB_LOG2B=27 AB_HEAD=1: 2^27 auctions with the bench headline's fields (the winner word)
 """
 import glob
 import os
@@ -31,7 +32,7 @@ def main():
     else:
         for p in sorted(glob.glob(os.path.join(vdir, "*.so"))):
             paths[os.path.basename(p)[len("libauctiongym_hip_"):-3]] = p
-    B = 1 << 24
+    B = 1 << int(os.environ.get("AB_LOG2B", "24"))
     items, values = bench.catalogue()
     engs = {}
     for n, p in paths.items():
@@ -43,6 +44,9 @@ def main():
     inp = base.alloc_inputs(B)
     base.generate(0, 0, inp)
     full = ("winner", "price", "outcome", "item", "bid", "est_ctr", "true_ctr", "best_ev")
+    if os.environ.get("AB_HEAD"):
+        from auctiongym_amd.engine import HEADLINE_FIELDS
+        full = HEADLINE_FIELDS
     ref = base.alloc_outputs(B, full)
     cref = base.new_counters()
     base.simulate(inp, ref, cref)
@@ -50,7 +54,7 @@ def main():
     cnt = base.new_counters()
     st = torch.cuda.current_stream()
     times = {n: [] for n in engs}
-    for _ in range(150):  # past the clock ramp of a fresh process (tools/warm_probe.py)
+    for _ in range(max(10, (150 << 24) // B)):  # past the clock ramp of a fresh process (tools/warm_probe.py)
         cnt.zero_()
         base.simulate(inp, out, cnt)
     for r in range(25):
@@ -79,7 +83,7 @@ def main():
             torch.cuda.synchronize()
             if r >= 1:
                 sus[n].append(a.elapsed_time(b) / 20)
-    bpa = bench.algorithmic_bytes_per_auction(5, 2, False)
+    bpa = bench.algorithmic_bytes_per_auction(5, 2, False, packed_winner="winner_outcome" in full)
     for n, t in times.items():
         ms, lo = float(np.median(t)), float(np.min(t))
         ss = float(np.median(sus[n]))

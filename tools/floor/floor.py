@@ -38,6 +38,11 @@ def main():
     P = lambda t: t.data_ptr()  # noqa: E731
     p = Ptrs(P(inp["ctx"]), P(inp["part"]), P(inp["u"]), P(out["winner"]), P(out["item"]), P(out["price"]),
              P(out["bid"]), P(out["est_ctr"]), P(out["true_ctr"]), P(out["best_ev"]), P(out["outcome"]))
+    pw = Ptrs(P(inp["ctx"]), P(inp["part"]), P(inp["u"]), P(outw["winner_outcome"]), P(outw["item"]),
+              P(outw["price"]), P(outw["bid"]), P(outw["est_ctr"]), P(outw["true_ctr"]), P(outw["best_ev"]), None)
+    L.floor_queue.argtypes = [ctypes.c_int, ctypes.POINTER(Ptrs), ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
+    qbuf = torch.zeros(8 * 32, dtype=torch.int32, device="cuda")
+    qc = ctypes.c_void_p(qbuf.data_ptr())
     tin = torch.zeros(7 * B, dtype=torch.float64, device="cuda")      # 56 B per auction, tiled
     tout = torch.empty(84 * B // 8, dtype=torch.float64, device="cuda")  # 84 B per auction, tiled
     p2 = Ptrs(P(tin), P(inp["part"]), P(inp["u"]), P(out["winner"]), P(out["item"]), P(tout),
@@ -60,6 +65,9 @@ def main():
         "floor nt 8/CU, tiled in + out": lambda: L.floor_run(7, cus * 8, ctypes.byref(p2), B, sp),
         "floor nt 4/CU, 16-B tiles in + out": lambda: L.floor_run(8, cus * 4, ctypes.byref(p2), B, sp),
         "floor nt 8/CU, 16-B tiles in + out": lambda: L.floor_run(8, cus * 8, ctypes.byref(p2), B, sp),
+        "floor nt one tile per block, word": lambda: L.floor_run(9, 0, ctypes.byref(pw), B, sp),
+        "floor nt 4/CU work queue, word": lambda: L.floor_queue(cus * 4, ctypes.byref(pw), B, qc, sp),
+        "floor nt 8/CU work queue, word": lambda: L.floor_queue(cus * 8, ctypes.byref(pw), B, qc, sp),
         "ag_simulate (r04 fields)": lambda: eng.simulate(inp, out, cnt),
         "ag_simulate (bench: winner|outcome)": lambda: eng.simulate(inp, outw, cnt),
         "ag_simulate, no counters": lambda: eng.simulate(inp, out, None),

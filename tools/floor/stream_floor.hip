@@ -181,8 +181,41 @@ __global__ __launch_bounds__(256) void k_floor_tiled16(Ptrs p, int64_t B) {
   }
 }
 
+// one tile per block, NT, the winner|outcome word: the headline's pattern in dispatch order
+__global__ __launch_bounds__(256) void k_floor_tiles_nt_wo(Ptrs p, int64_t B) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < B) one<true, true>(p, B, i);
+}
+// persistent blocks taking 256-auction tiles from per-XCD work counters (block b counts as XCD
+// b % 8, the dispatcher's round-robin): XCD x's k-th claim is tile 8 k + x, so the tiles in
+// flight stay a narrow window in address order however the blocks drift. The claim for the
+// next tile is made while the current one is processed.
+__global__ __launch_bounds__(256) void k_floor_queue(Ptrs p, int64_t B, unsigned *ctr) {
+  __shared__ unsigned s_next[2];
+  const unsigned x = blockIdx.x & 7;
+  const int64_t tiles = (B + 255) / 256;
+  if (threadIdx.x == 0) s_next[0] = atomicAdd(ctr + 32 * x, 1u);
+  __syncthreads();
+  for (int k = 0;; k ^= 1) {
+    const int64_t t = (int64_t)s_next[k] * 8 + x;
+    if (t >= tiles) break;
+    if (threadIdx.x == 0) s_next[k ^ 1] = atomicAdd(ctr + 32 * x, 1u);
+    const int64_t i = t * 256 + threadIdx.x;
+    if (i < B) one<true, true>(p, B, i);
+    __syncthreads();
+  }
+}
+
+extern "C" int floor_queue(int grid, const Ptrs *p, int64_t B, unsigned *ctr, void *stream) {
+  hipMemsetAsync(ctr, 0, 8 * 32 * sizeof(unsigned), (hipStream_t)stream);
+  hipLaunchKernelGGL(k_floor_queue, dim3(grid), dim3(256), 0, (hipStream_t)stream, *p, B, ctr);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int floor_run(int persistent, int grid, const Ptrs *p, int64_t B, void *stream) {
-  if (persistent == 8) {
+  if (persistent == 9) {
+    hipLaunchKernelGGL(k_floor_tiles_nt_wo, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, *p, B);
+  } else if (persistent == 8) {
     hipLaunchKernelGGL(k_floor_tiled16, dim3(grid), dim3(256), 0, (hipStream_t)stream, *p, B);
   } else if (persistent >= 5 && persistent <= 7) {
     auto k = persistent == 5 ? k_floor_tiled<true, false> : persistent == 6 ? k_floor_tiled<false, true>
