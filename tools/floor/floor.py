@@ -41,6 +41,7 @@ def main():
     pw = Ptrs(P(inp["ctx"]), P(inp["part"]), P(inp["u"]), P(outw["winner_outcome"]), P(outw["item"]),
               P(outw["price"]), P(outw["bid"]), P(outw["est_ctr"]), P(outw["true_ctr"]), P(outw["best_ev"]), None)
     L.floor_queue.argtypes = [ctypes.c_int, ctypes.POINTER(Ptrs), ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
+    L.floor_chunk.argtypes = [ctypes.c_int, ctypes.POINTER(Ptrs), ctypes.c_int64, ctypes.c_void_p]
     qbuf = torch.zeros(8 * 32, dtype=torch.int32, device="cuda")
     qc = ctypes.c_void_p(qbuf.data_ptr())
     tin = torch.zeros(7 * B, dtype=torch.float64, device="cuda")      # 56 B per auction, tiled
@@ -67,6 +68,11 @@ def main():
         "floor nt 8/CU, 16-B tiles in + out": lambda: L.floor_run(8, cus * 8, ctypes.byref(p2), B, sp),
         "floor nt one tile per block, word": lambda: L.floor_run(9, 0, ctypes.byref(pw), B, sp),
         "floor nt 4/CU work queue, word": lambda: L.floor_queue(cus * 4, ctypes.byref(pw), B, qc, sp),
+        "floor nt 2 tiles per block, word": lambda: L.floor_chunk(2, ctypes.byref(pw), B, sp),
+        "floor nt 4 tiles per block, word": lambda: L.floor_chunk(4, ctypes.byref(pw), B, sp),
+        "floor nt 8 tiles per block, word": lambda: L.floor_chunk(8, ctypes.byref(pw), B, sp),
+        "floor nt 16 tiles per block, word": lambda: L.floor_chunk(16, ctypes.byref(pw), B, sp),
+        "floor nt 64 tiles per block, word": lambda: L.floor_chunk(64, ctypes.byref(pw), B, sp),
         "floor nt 8/CU work queue, word": lambda: L.floor_queue(cus * 8, ctypes.byref(pw), B, qc, sp),
         "ag_simulate (r04 fields)": lambda: eng.simulate(inp, out, cnt),
         "ag_simulate (bench: winner|outcome)": lambda: eng.simulate(inp, outw, cnt),

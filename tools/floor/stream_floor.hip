@@ -206,6 +206,20 @@ __global__ __launch_bounds__(256) void k_floor_queue(Ptrs p, int64_t B, unsigned
   }
 }
 
+// T consecutive tiles per block (dispatch order still follows addresses; the per-block setup
+// of a real kernel is paid once per T tiles)
+__global__ __launch_bounds__(256) void k_floor_chunk(Ptrs p, int64_t B, int T) {
+  for (int k = 0; k < T; ++k) {
+    const int64_t i = ((int64_t)blockIdx.x * T + k) * 256 + threadIdx.x;
+    if (i < B) one<true, true>(p, B, i);
+  }
+}
+extern "C" int floor_chunk(int T, const Ptrs *p, int64_t B, void *stream) {
+  const int64_t tiles = (B + 255) / 256;
+  hipLaunchKernelGGL(k_floor_chunk, dim3((unsigned)((tiles + T - 1) / T)), dim3(256), 0, (hipStream_t)stream, *p, B, T);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int floor_queue(int grid, const Ptrs *p, int64_t B, unsigned *ctr, void *stream) {
   hipMemsetAsync(ctr, 0, 8 * 32 * sizeof(unsigned), (hipStream_t)stream);
   hipLaunchKernelGGL(k_floor_queue, dim3(grid), dim3(256), 0, (hipStream_t)stream, *p, B, ctr);
