@@ -138,6 +138,7 @@ struct ag_ctx {
   double *d_items = nullptr;
   double *d_values = nullptr;
   int64_t *d_partials = nullptr;
+  uint32_t *d_queue = nullptr;  // k_oracle's chunk counters (AG_ORA_QUEUE): 64 x 32 words
   int32_t partial_blocks = 0;
   int32_t resident_wide[2] = {};  // the AG_SIM_KERNEL_WIDE A/B kernel's [counters]
   int32_t resident[256] = {};  // resident blocks [768 lanes][shipped shape][truthful-only][768 / 1024 lanes][general][W][screened][counters]

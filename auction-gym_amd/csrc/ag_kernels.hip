@@ -450,6 +450,7 @@ int simulate_oracle(ag_ctx *c, OraKernel k, int64_t B, const ag_batch_in *in, co
   prm.best_ev = out->best_ev;
   prm.winner_outcome = out->winner_outcome;
   prm.partials = c->d_partials;
+  prm.queue = c->d_queue;
   const size_t lds = (size_t)prm.L.total;
   if (lds > 160 * 1024)
     return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
@@ -474,6 +475,13 @@ int simulate_oracle(ag_ctx *c, OraKernel k, int64_t B, const ag_batch_in *in, co
   // a lane resolves at most ora_lane_cap(R) auctions per launch (replica sums in range):
   // larger batches run as consecutive launches
   int64_t chunk_max = (int64_t)res * kThreads * ora_lane_cap(prm.L.replicas);
+#if AG_ORA_QUEUE
+  // a wave may take up to ora_lane_cap(R) auctions per lane; a launch holds half of what the
+  // grid could take (every counter has as many waves), so the rest always finds a wave
+  if (res >= 16) res &= ~15;
+  chunk_max = (int64_t)res * kThreads * (ora_lane_cap(prm.L.replicas) / 2);
+  prm.lane_tiles = (uint32_t)ora_lane_cap(prm.L.replicas);
+#endif
   if (chunk_max > INT32_MAX) chunk_max = INT32_MAX;
   if (c->launch_cap > 0 && c->launch_cap < chunk_max) chunk_max = c->launch_cap;
   if (chunk_max < 1) chunk_max = 1;
@@ -484,6 +492,9 @@ int simulate_oracle(ag_ctx *c, OraKernel k, int64_t B, const ag_batch_in *in, co
     const int grid = (int)(tiles < res ? tiles : res);
     prm.lo = (int32_t)lo;
     prm.hi = (int32_t)hi;
+#if AG_ORA_QUEUE
+    AG_HIP(hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t) * 64 * 32, st));
+#endif
     hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), lds, st, prm);  // generate mode: same lo/hi
     AG_HIP(hipGetLastError());
     if (counters_fx) {
@@ -556,7 +567,9 @@ int ag_create(int32_t device, const ag_shape *s, ag_ctx **out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_tsm, sizeof(float) * nkd);
   if (e == hipSuccess) e = hipMalloc(&c->d_tsq, sizeof(float) * nkd);
   if (e == hipSuccess) e = hipMalloc(&c->d_tsprev, sizeof(float) * nkd);
+  if (e == hipSuccess) e = hipMalloc(&c->d_queue, sizeof(uint32_t) * 64 * 32);
   if (e != hipSuccess) {
+    (void)hipFree(c->d_queue);
     (void)hipFree(c->d_items);
     (void)hipFree(c->d_values);
     (void)hipFree(c->d_partials);
@@ -580,6 +593,7 @@ int ag_destroy(ag_ctx *c) {
   (void)hipFree(c->d_items);
   (void)hipFree(c->d_values);
   (void)hipFree(c->d_partials);
+  (void)hipFree(c->d_queue);
   (void)hipFree(c->d_akind);
   (void)hipFree(c->d_bkind);
   (void)hipFree(c->d_kag);

@@ -45,6 +45,18 @@ constexpr double kOraMaxValue = 1024.0;
 #ifndef AG_ORA_PREFETCH
 #define AG_ORA_PREFETCH 0  // software-pipelined input loads (A/B: make variant VFLAGS=-DAG_ORA_PREFETCH=1)
 #endif
+#ifndef AG_ORA_QUEUE
+// Waves take 256-auction chunks from 64 work counters (1) instead of the static grid stride
+// (0): the chunks in flight stay a narrow address window however the persistent blocks drift,
+// which is what the byte pattern's floor rewards (tools/floor: 3.64 ms persistent, 3.50 with
+// work counters). 3.87 -> 3.73 ms per 2^27 auctions, outputs identical
+// (profiles/r05zk_ab_wq.log); block-level claims with a barrier (4.20 ms) and per-wave
+// 64-auction claims (5.24 ms: same-address atomics serialise) lost (r05zg_ab_queue.log)
+#define AG_ORA_QUEUE 1
+#endif
+#if AG_ORA_QUEUE && AG_ORA_PREFETCH
+#error "AG_ORA_QUEUE and AG_ORA_PREFETCH are exclusive"
+#endif
 #ifndef AG_ORA_STORE_LATE
 #define AG_ORA_STORE_LATE 1  // every per-slot output stored after the slots, field by field (A/B: 0 stores each slot's as it resolves; 3.73 -> 3.59 ms per 2^27, profiles/r05h_ab_packed.log)
 #endif
@@ -101,6 +113,8 @@ struct OraParams {
   double *bid, *est_ctr, *true_ctr, *best_ev;
   uint32_t *winner_outcome;  // ABI 17: [B] winner | outcome << 31
   int64_t *partials;  // [grid][N][AG_NUM_COUNTERS][2]
+  uint32_t *queue;      // AG_ORA_QUEUE: 64 chunk counters, 32 words apart, zero at launch
+  uint32_t lane_tiles;  // AG_ORA_QUEUE: auctions one lane may take per launch
   // generate mode (GEN): inputs drawn on the chip as ag_generate draws them
   uint64_t seed, first;  // Philox key; global index of auction 0 of the batch
   double scale;          // embedding_var
@@ -236,7 +250,41 @@ __global__ __launch_bounds__(kThreads) void k_oracle(OraParams prm) {
     un = ldg(prm.u + i0);
   }
 #endif
+#if AG_ORA_QUEUE
+  // wave w of block b claims from counter q = (4 b + w) mod 64; the k-th claim of counter q is
+  // the 256-auction chunk 64 k + q, resolved as 4 tiles of 64. Lane 0 claims the chunk after
+  // next while the current one resolves; the ticket is read only once that chunk is done.
+  // At most lane_tiles / 4 claims per wave; tickets only grow, so a claim left in flight at
+  // the exit is past the end too.
+  (void)stride;
+  const uint32_t q_lane = tid & 63;
+  const uint32_t q_idx = ((uint32_t)blockIdx.x * (kThreads / 64) + (uint32_t)(tid >> 6)) & 63u;
+  uint32_t *const q_ctr = prm.queue + q_idx * 32;
+  const uint32_t q_chunks = (hi - lo + 255) / 256;
+  uint32_t q_claims = 0;
+  auto q_claim = [&]() -> uint32_t {
+    uint32_t r = 0xffffffffu;
+    if (q_claims < prm.lane_tiles / 4) {
+      if (q_lane == 0) r = atomicAdd(q_ctr, 1u);
+      ++q_claims;
+    }
+    return r;
+  };
+  auto q_chunk_of = [&](uint32_t raw) -> uint32_t {
+    const uint32_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int)raw);
+    return t == 0xffffffffu ? 0xffffffffu : t * 64u + q_idx;
+  };
+  uint32_t q_cur = q_chunk_of(q_claim());
+  uint32_t q_raw = q_claim();
+  for (;;) {
+    if (q_cur >= q_chunks) break;
+#pragma nounroll
+    for (int q_s = 0; q_s < 4; ++q_s) {
+    const uint32_t i = lo + q_cur * 256 + (uint32_t)q_s * 64 + q_lane;
+    if (i >= hi) break;
+#else
   for (uint32_t i = lo + blockIdx.x * kThreads + tid; i < hi; i += stride) {
+#endif
     double x[kMaxD];
     float xf[kMaxD];
     float xabs = 1.0f;
@@ -398,6 +446,11 @@ __global__ __launch_bounds__(kThreads) void k_oracle(OraParams prm) {
       }
       if (packed && ++since_flush == kOraFlush) flush_counts();
     }
+#if AG_ORA_QUEUE
+    }
+    q_cur = q_chunk_of(q_raw);
+    q_raw = q_claim();
+#endif
   }
 
   if (!prm.want_counters) return;
