@@ -459,10 +459,10 @@ int simulate_oracle(ag_ctx *c, OraKernel k, int64_t B, const ag_batch_in *in, co
   int &res_max = c->resident_ora[(prm.want_counters ? 1 : 0) + (in ? 0 : 2)];
   if (res_max == 0)
     if (int rc = resident_blocks(c, (const void *)k, lds, &res_max)) return rc;
-  // Persistent grid of kOraBlocksPerCu workgroups per CU (AG_OPT_SIM_BLOCKS_PER_CU overrides):
-  // fewer than the 5 the registers allow streams better (tools/ab_oracle.py: 4 per CU 0.473 ms
-  // vs 5 per CU 0.503 ms on one box, equal on another; a 16-B copy likewise runs faster on
-  // 4 persistent workgroups per CU than on 8 or 16, tools/floor/copy_peak.py)
+  // Persistent grid of kOraBlocksPerCu workgroups per CU, capped by residency
+  // (AG_OPT_SIM_BLOCKS_PER_CU overrides). With the static stride fewer than the 5 the
+  // registers allow streamed better (round 4: 4 per CU 0.473 ms vs 5 per CU 0.503 ms); with
+  // the work counters (AG_ORA_QUEUE) all 5 do (3.57 -> 3.41 ms per 2^27, r05zm_ab_sub_bpc.log)
   int res = res_max;
   {
     // generate mode (no input stream, VALU-heavier): as many as fit (5 at 87 VGPRs) --

@@ -46,13 +46,16 @@ constexpr double kOraMaxValue = 1024.0;
 #define AG_ORA_PREFETCH 0  // software-pipelined input loads (A/B: make variant VFLAGS=-DAG_ORA_PREFETCH=1)
 #endif
 #ifndef AG_ORA_QUEUE
-// Waves take 256-auction chunks from 64 work counters (1) instead of the static grid stride
+// Waves take 512-auction chunks from 64 work counters (1) instead of the static grid stride
 // (0): the chunks in flight stay a narrow address window however the persistent blocks drift,
 // which is what the byte pattern's floor rewards (tools/floor: 3.64 ms persistent, 3.50 with
 // work counters). 3.87 -> 3.73 ms per 2^27 auctions, outputs identical
 // (profiles/r05zk_ab_wq.log); block-level claims with a barrier (4.20 ms) and per-wave
 // 64-auction claims (5.24 ms: same-address atomics serialise) lost (r05zg_ab_queue.log)
 #define AG_ORA_QUEUE 1
+#endif
+#ifndef AG_ORA_QUEUE_SUB
+#define AG_ORA_QUEUE_SUB 8  // 64-auction tiles per claimed chunk (2 / 4 / 8: 3.46 / 3.41 / 3.38 ms at 5 per CU, r05zm_ab_sub_bpc.log)
 #endif
 #if AG_ORA_QUEUE && AG_ORA_PREFETCH
 #error "AG_ORA_QUEUE and AG_ORA_PREFETCH are exclusive"
@@ -61,7 +64,10 @@ constexpr double kOraMaxValue = 1024.0;
 #define AG_ORA_STORE_LATE 1  // every per-slot output stored after the slots, field by field (A/B: 0 stores each slot's as it resolves; 3.73 -> 3.59 ms per 2^27, profiles/r05h_ab_packed.log)
 #endif
 constexpr int kOraFlush = 255;
-constexpr int kOraBlocksPerCu = 4;  // default persistent grid (ag_kernels.hip simulate_oracle)
+// default persistent grid (ag_kernels.hip simulate_oracle): as many workgroups as fit (5 per CU
+// at 85 VGPRs). With the static stride 4 streamed better than 5 (the blocks drift apart); with
+// the work counters 5 per CU is 4.7 % faster than 4 (profiles/r05zm_ab_sub_bpc.log)
+constexpr int kOraBlocksPerCu = 8;
 __host__ inline int64_t ora_lane_cap(int R) { return 512 * (int64_t)R; }
 
 struct OraLayout {
@@ -260,11 +266,12 @@ __global__ __launch_bounds__(kThreads) void k_oracle(OraParams prm) {
   const uint32_t q_lane = tid & 63;
   const uint32_t q_idx = ((uint32_t)blockIdx.x * (kThreads / 64) + (uint32_t)(tid >> 6)) & 63u;
   uint32_t *const q_ctr = prm.queue + q_idx * 32;
-  const uint32_t q_chunks = (hi - lo + 255) / 256;
+  constexpr uint32_t q_len = 64 * AG_ORA_QUEUE_SUB;
+  const uint32_t q_chunks = (hi - lo + q_len - 1) / q_len;
   uint32_t q_claims = 0;
   auto q_claim = [&]() -> uint32_t {
     uint32_t r = 0xffffffffu;
-    if (q_claims < prm.lane_tiles / 4) {
+    if (q_claims < prm.lane_tiles / AG_ORA_QUEUE_SUB) {
       if (q_lane == 0) r = atomicAdd(q_ctr, 1u);
       ++q_claims;
     }
@@ -279,8 +286,8 @@ __global__ __launch_bounds__(kThreads) void k_oracle(OraParams prm) {
   for (;;) {
     if (q_cur >= q_chunks) break;
 #pragma nounroll
-    for (int q_s = 0; q_s < 4; ++q_s) {
-    const uint32_t i = lo + q_cur * 256 + (uint32_t)q_s * 64 + q_lane;
+    for (int q_s = 0; q_s < AG_ORA_QUEUE_SUB; ++q_s) {
+    const uint32_t i = lo + q_cur * q_len + (uint32_t)q_s * 64 + q_lane;
     if (i >= hi) break;
 #else
   for (uint32_t i = lo + blockIdx.x * kThreads + tid; i < hi; i += stride) {
