@@ -55,7 +55,7 @@ constexpr double kOraMaxValue = 1024.0;
 #define AG_ORA_QUEUE 1
 #endif
 #ifndef AG_ORA_QUEUE_SUB
-#define AG_ORA_QUEUE_SUB 8  // 64-auction tiles per claimed chunk (2 / 4 / 8: 3.46 / 3.41 / 3.38 ms at 5 per CU, r05zm_ab_sub_bpc.log)
+#define AG_ORA_QUEUE_SUB 8  // 64-auction tiles per claimed chunk (2 / 4 / 8: 3.46 / 3.41 / 3.38 ms at 5 per CU, r05zm_ab_sub_bpc.log; 8 / 16 / 32: 3.33 / 3.36 / 3.43 ms on another box, r05zn_ab_sub16.log)
 #endif
 #if AG_ORA_QUEUE && AG_ORA_PREFETCH
 #error "AG_ORA_QUEUE and AG_ORA_PREFETCH are exclusive"
