@@ -943,17 +943,24 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out_a
     if (res < 1) res = 1;
     if (res > c->partial_blocks) res = c->partial_blocks;
   }
+  // AG_OPT_SIM_BLOCKS_PER_CU caps the grid below residency (A/B; 0 = every resident block)
+  int grid_max = res;
+  if (c->grid_per_cu > 0) {
+    int cus = 0;
+    AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    if ((int64_t)c->grid_per_cu * cus < grid_max) grid_max = c->grid_per_cu * cus;
+  }
   // Batches larger than one launch's exact-counter capacity (resident blocks x
   // kAuctionsPerReplica x replicas) run as consecutive launches over auction ranges.
   const int64_t per_block = (int64_t)kAuctionsPerReplica * prm.lds.replicas;
-  int64_t chunk_max = (int64_t)res * per_block;
+  int64_t chunk_max = (int64_t)grid_max * per_block;
   if (c->launch_cap > 0 && c->launch_cap < chunk_max) chunk_max = c->launch_cap;
   chunk_max &= ~(int64_t)1;
   if (chunk_max < 2) chunk_max = 2;
   for (int64_t lo = 0; lo < B; lo += chunk_max) {
     const int64_t hi = lo + chunk_max < B ? lo + chunk_max : B;
     const int64_t tiles = (hi - lo + bt * W - 1) / (bt * W);
-    const int grid = (int)(tiles < res ? tiles : res);
+    const int grid = (int)(tiles < grid_max ? tiles : grid_max);
     prm.lo = (int32_t)lo;
     prm.hi = (int32_t)hi;
     hipLaunchKernelGGL(k, dim3(grid), dim3(bt), lds, st, prm);  // generate mode: same lo/hi

@@ -234,8 +234,9 @@ typedef enum ag_option {
                                    trainer stages in LDS (-1 = default: as many as fit; 0 = none,
                                    every epoch reads the store); identical results */
   AG_OPT_SIMULATE_KERNEL = 7,     /* value: ag_sim_kernel; identical results */
-  AG_OPT_SIM_BLOCKS_PER_CU = 8,   /* value: workgroups per CU of the Oracle kernel's persistent
-                                     grid (0 = default 4, capped by what fits); identical results */
+  AG_OPT_SIM_BLOCKS_PER_CU = 8,   /* value: workgroups per CU of the simulate kernels' persistent
+                                     grids (0 = default: every workgroup that fits); a cap, never
+                                     above what fits; identical results */
   AG_OPT_SIM_BLOCK_THREADS = 9,   /* value: lanes per workgroup of the general simulate kernel:
                                      0 = auto (1024 when the population's LDS would keep fewer than
                                      16 waves resident per CU with 256-lane workgroups), 256 or

@@ -36,7 +36,8 @@ def main():
         key, P = key.split(":")[0], int(key.split(":")[1])
     vdir = os.path.join(ROOT, "auction-gym_amd", "build", "variants")
     paths = {"base": _lib.LIB_PATH}
-    special = {"generic", "wide", "bt256", "bt1024", "nocnt", "noship", "grouporder", "packed"}
+    special = {"generic", "wide", "bt256", "bt1024", "nocnt", "noship", "grouporder", "packed",
+               "bpc1", "bpc2", "bpc3"}
     for n in sys.argv[2:]:  # "<variant>+generic": that build with k_simulate forced
         v = n[:-len("+generic")] if n.endswith("+generic") else n
         paths[n] = _lib.LIB_PATH if v in special else os.path.join(vdir, f"libauctiongym_hip_{v}.so")
@@ -67,6 +68,8 @@ def main():
             eng.set_simulate_kernel(True)
         if n == "noship":  # k_simulate's runtime-shape build
             eng._check(eng.L.ag_set_option(eng._h, _lib.OPT_SIM_SHIPPED_SHAPE, 0), "ag_set_option")
+        if n in ("bpc1", "bpc2", "bpc3"):  # the grid capped at that many workgroups per CU
+            eng.set_blocks_per_cu(int(n[3:]))
         if n in ("bt256", "bt1024"):
             eng._check(eng.L.ag_set_option(eng._h, _lib.OPT_SIM_BLOCK_THREADS, int(n[2:])), "ag_set_option")
         inp = eng.alloc_inputs(B)
