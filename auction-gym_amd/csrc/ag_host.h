@@ -141,7 +141,7 @@ struct ag_ctx {
   uint32_t *d_queue = nullptr;  // k_oracle's chunk counters (AG_ORA_QUEUE): 64 x 32 words
   int32_t partial_blocks = 0;
   int32_t resident_wide[2] = {};  // the AG_SIM_KERNEL_WIDE A/B kernel's [counters]
-  int32_t resident[256] = {};  // resident blocks [768 lanes][shipped shape][truthful-only][768 / 1024 lanes][general][W][screened][counters]
+  int32_t resident[512] = {};  // resident blocks [generate mode][768 lanes][shipped shape][truthful-only][768 / 1024 lanes][general][W][screened][counters]
   bool ship_shape = true;      // AG_OPT_SIM_SHIPPED_SHAPE: the compile-time shipped-shape general build
   bool gen_mode_all = false;   // AG_OPT_SIM_GENERAL_MODE = 1: the full general build for every population
   int64_t launch_cap = 0;  // AG_OPT_LAUNCH_AUCTIONS

@@ -23,6 +23,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 
 #include "ag_host.h"
@@ -189,19 +190,10 @@ __global__ __launch_bounds__(kThreads) void k_generate(uint64_t seed, uint64_t f
   }
 }
 
-// Synthetic per-participant noise (streams 3 and 4 + slot of the same Philox key/counter
-// scheme): shading bidders' gamma_raw = prev_gamma + sigma * z (numpy normal(loc, scale)),
-// LR-TS agents' ts_noise = z * (1 / sqrt(q)) (torch.normal(0, 1 / sqrt(q)), src/Models.py:31).
-__device__ __forceinline__ void box_muller(const uint32_t (&w)[4], double &z0, double &z1) {
-  const double u1 = (double)(((((uint64_t)w[0] << 32) | w[1]) >> 11) + 1) * 0x1p-53;
-  const double u2 = (double)((((uint64_t)w[2] << 32) | w[3]) >> 11) * 0x1p-53;
-  const double r = sqrt(-2.0 * log(u1));
-  double sn, cs;
-  sincospi(2.0 * u2, &sn, &cs);
-  z0 = r * cs;
-  z1 = r * sn;
-}
-
+// Synthetic per-participant noise (ag_philox.h gen_normals4 / gen_normal1 / gen_shading_raw,
+// which the general kernel's generate mode draws in place): shading bidders' gamma_raw =
+// prev_gamma + sigma * z (numpy normal(loc, scale)), LR-TS agents' ts_noise = z * (1 / sqrt(q))
+// (torch.normal(0, 1 / sqrt(q)), src/Models.py:31), fitted policies' rsample draws.
 __global__ __launch_bounds__(kThreads) void k_generate_noise(uint64_t seed, uint64_t first, int64_t B, int P,
                                                             int KDo, const int32_t *part,
                                                             const int32_t *akind, const int32_t *bkind,
@@ -217,37 +209,21 @@ __global__ __launch_bounds__(kThreads) void k_generate_noise(uint64_t seed, uint
     const uint32_t c0 = (uint32_t)idx, c1 = (uint32_t)(idx >> 32);
     for (int s = 0; s < P; ++s) {
       const int a = part[(int64_t)s * B + i];
-      uint32_t w[4];
-      double z0, z1;
-      if (gamma_raw) {
-        if (bkind[a] != AG_BIDDER_TRUTHFUL) {
-          philox(c0, c1, (uint32_t)s, 3, k0, k1, w);
-          box_muller(w, z0, z1);
-          gamma_raw[(int64_t)s * B + i] = pg[a] + gs[a] * z0;
-        } else {
-          gamma_raw[(int64_t)s * B + i] = NAN;
-        }
-      }
-      if (policy_eps) {  // the rsample draw of a fitted DR policy
-        philox(c0, c1, 0, 16 + (uint32_t)s, k0, k1, w);
-        box_muller(w, z0, z1);
-        policy_eps[(int64_t)s * B + i] = (float)z0;
-      }
+      if (gamma_raw)
+        gamma_raw[(int64_t)s * B + i] =
+            bkind[a] != AG_BIDDER_TRUTHFUL ? gen_shading_raw(c0, c1, s, k0, k1, pg[a], gs[a]) : NAN;
+      if (policy_eps)  // the rsample draw of a fitted policy
+        policy_eps[(int64_t)s * B + i] = gen_normal1(c0, c1, 0, 16 + (uint32_t)s, k0, k1);
       if (ts_noise && (!ts_index || akind[a] == AG_ALLOCATOR_LRTS)) {
         const bool lr = akind[a] == AG_ALLOCATOR_LRTS;
         // dense tiles: pair (s, i) at s*T*64 + i; compact: the LR-TS pair's rank j
         const int64_t pj = ts_index ? (int64_t)(uint32_t)ts_index[(int64_t)s * B + i] : s * T * 64 + i;
-        for (int j = 0; j < KDo; j += 2) {
-          if (lr) {
-            philox(c0, c1, (uint32_t)(j >> 1), 4 + (uint32_t)s, k0, k1, w);
-            box_muller(w, z0, z1);
-          } else {
-            z0 = z1 = 0.0;
-          }
-          const float *qa = q + (size_t)a * KDo;
+        const float *qa = q + (size_t)a * KDo;
+        for (int j = 0; j < KDo; j += 4) {
+          float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+          if (lr) gen_normals4(c0, c1, (uint32_t)(j >> 2), 4 + (uint32_t)s, k0, k1, z);
           float *row = ts_noise + ((pj >> 6) * KDo + j) * 64 + (pj & 63);
-          row[0] = lr ? (float)z0 * (1.0f / sqrtf(qa[j])) : 0.0f;
-          if (j + 1 < KDo) row[64] = lr ? (float)z1 * (1.0f / sqrtf(qa[j + 1])) : 0.0f;
+          for (int t = 0; t < 4 && j + t < KDo; ++t) row[64 * t] = lr ? z[t] * (1.0f / sqrtf(qa[j + t])) : 0.0f;
         }
       }
     }
@@ -489,7 +465,15 @@ int simulate_oracle(ag_ctx *c, OraKernel k, int64_t B, const ag_batch_in *in, co
   for (int64_t lo = 0; lo < B; lo += chunk_max) {
     const int64_t hi = lo + chunk_max < B ? lo + chunk_max : B;
     const int64_t tiles = (hi - lo + kThreads - 1) / kThreads;
-    const int grid = (int)(tiles < res ? tiles : res);
+    int grid = (int)(tiles < res ? tiles : res);
+#if AG_ORA_QUEUE
+    // wave w of block b serves work counter (4 b + w) mod 64, and chunk c belongs to counter
+    // c mod 64: every counter the launch's chunks reach needs a wave. A grid below 16 blocks
+    // (a small device or partition: res < 16) covers only 4 * grid counters -- raise it (the
+    // extra blocks wait for a CU; nothing in k_oracle waits on another block)
+    const int64_t chunks = (hi - lo + 64 * AG_ORA_QUEUE_SUB - 1) / (64 * AG_ORA_QUEUE_SUB);
+    if (grid < 16 && chunks > 4 * (int64_t)grid) grid = (int)std::min<int64_t>(16, (chunks + 3) / 4);
+#endif
     prm.lo = (int32_t)lo;
     prm.hi = (int32_t)hi;
 #if AG_ORA_QUEUE
@@ -499,6 +483,149 @@ int simulate_oracle(ag_ctx *c, OraKernel k, int64_t B, const ag_batch_in *in, co
     AG_HIP(hipGetLastError());
     if (counters_fx) {
       hipLaunchKernelGGL(k_reduce_counters, dim3(nc), dim3(kThreads), 0, st, c->d_partials, grid, nc, counters_fx);
+      AG_HIP(hipGetLastError());
+    }
+  }
+  return AG_OK;
+}
+
+// k_simulate over a batch (replay / HBM-resident inputs, or generate mode: gen, every input drawn
+// in the kernel from (seed, first + auction index) as ag_generate + ag_generate_noise draw them)
+int simulate_general(ag_ctx *c, int64_t B, const ag_batch_in *in, const ag_batch_out *out, int64_t *counters_fx,
+                     hipStream_t st, bool gen, uint64_t seed, uint64_t first) {
+  const ag_shape &s = c->shape;
+  const int nc = s.num_agents * kC;
+  const int D = c->D;
+  const bool prune = c->item_search == AG_ITEM_SEARCH_AUTO && D <= 8 && s.num_items <= 2 * kMaxKPairs &&
+                     c->values_positive;
+  SimParams prm;
+  prm.B = B;
+  prm.N = s.num_agents;
+  prm.K = s.num_items;
+  prm.mech = s.mechanism;
+  prm.want_counters = counters_fx != nullptr;
+  prm.lds = make_layout(s.num_agents, s.num_items, D, prm.want_counters, c->general,
+                        s.obs_embedding_size + 1, gen);
+  prm.ts_sample = c->ts_sample;
+  prm.akind = c->d_akind;
+  prm.bkind = c->d_bkind;
+  prm.pg = c->d_pg;
+  prm.gs = c->d_gs;
+  prm.tsm = c->d_tsm;
+  prm.drs = c->dr_loaded ? c->dr.state : nullptr;
+  prm.dri = c->dr_loaded ? c->dr.init : nullptr;
+  prm.kag = c->ragged ? c->d_kag : nullptr;
+  prm.items = c->d_items;
+  prm.values = c->d_values;
+  prm.in = in ? *in : ag_batch_in{};
+  prm.out = *out;
+  prm.partials = c->d_partials;
+  prm.P = s.num_participants;
+  prm.tsq = c->d_tsq;
+  prm.seed = seed;
+  prm.first = first;
+  prm.scale = s.embedding_var;
+  // (round 4 retired k_pop, the dedicated shipped-shape population kernel: k_simulate was as
+  // fast or faster on every line, P = 8 included once its slots stream -- configs_1 at P = 8
+  // 0.665 against 0.680 ms, profiles/r04k_ab_c1p8.log; at P = 2 on every line,
+  // profiles/r03_ab_pop_vs_generic.log)
+  int W = (prune && (B % 2) == 0 && c->wide && !c->general && s.num_participants <= kMaxP) ? 2 : 1;
+  size_t lds = (size_t)prm.lds.total;
+  if (lds > 160 * 1024)
+    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
+  // Lanes per workgroup: the LDS image (catalogue, screen, LR-TS means, counter replicas) is
+  // per workgroup, so a large population with 256-lane workgroups keeps few waves resident
+  // (N = 32: ~75 KB -> 2 workgroups = 2 waves per SIMD); 1024-lane workgroups share one
+  // image among 16 waves. Same results (the counters are exact sums).
+  int bt = c->block_threads;
+  if (bt == 0) bt = (c->general && prune && lds > 40 * 1024) ? kLargeThreads : kThreads;
+  // AG_OPT_SIM_GENERAL_MODE 0 (auto): TruthfulBidder-only populations take the build
+  // without the bid-shading code (kGenTruthful); 1: always the full general build
+  const int gmode = !c->general ? kGenOracle : (c->has_shading || c->gen_mode_all) ? kGenAll : kGenTruthful;
+  // the shipped shape (E = 5, LR-TS width OE + 1 = 5 in the layout) has builds with the LR-TS
+  // width compile-time (k_simulate's DOS); AG_OPT_SIM_SHIPPED_SHAPE 0 turns them off (A/B)
+  const int ship = (c->general && c->ship_shape && D == 6 && prm.lds.ts_do == kShipDo) ? kGenShip : 0;
+  // the full mix at P >= 3 in the large-image case: the streamed 768-lane build (shipped shape)
+  if (bt == kLargeThreads && c->block_threads == 0 && gmode == kGenAll && ship && s.num_participants >= AG_STREAM_MIN_P &&
+      s.num_participants <= kMaxP)
+    bt = kMidThreads;
+  const int genb = gen ? kGenGen : 0;  // generate mode: the shipped shape's GEN builds
+  SimKernel k = pick_kernel(s.num_participants, D, prune, W, gmode | ship | genb, bt);
+  if (!k && bt == kMidThreads) {
+    bt = kLargeThreads;
+    k = pick_kernel(s.num_participants, D, prune, W, gmode | ship | genb, bt);
+  }
+  if (!k && W == 2) {  // the two-auctions-per-lane build is an A/B variant only (AG_LANE_PAIRS)
+    W = 1;
+    k = pick_kernel(s.num_participants, D, prune, W, gmode | ship | genb, bt);
+  }
+  if (!k && bt != kThreads) {
+    bt = kThreads;
+    k = pick_kernel(s.num_participants, D, prune, W, gmode | ship | genb, bt);
+  }
+  bool wide_ab = false;
+#if AG_SIM_WIDE_AB
+  if (c->general && c->sim_kernel == AG_SIM_KERNEL_WIDE) {  // the runtime-P kernel at any P (A/B)
+    bt = kThreads;
+    k = pick_kernel_for<0>(D, prune, 1, kGenAll, kThreads);
+    wide_ab = true;
+  }
+#endif
+  if (!k && gen)
+    return ag_set_error(AG_ERR_UNSUPPORTED,
+                        "ag_simulate_generated: general populations in the shipped shape only (E = 5, OE = 4, "
+                        "K <= %d, positive catalogue values, P <= %d; P=%d D=%d)",
+                        2 * kMaxKPairs, kMaxP, s.num_participants, D);
+  if (!k) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: no kernel for P=%d D=%d", s.num_participants, D);
+  if (gmode == kGenAll && bt == kLargeThreads) {  // the compacted fitted-policy pass's per-wave task slots
+    add_policy_tasks(prm.lds, bt);
+    lds = (size_t)prm.lds.total;
+    if (lds > 160 * 1024)
+      return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
+  }
+  if (lds > 64 * 1024)
+    AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  // Persistent grid: exactly the blocks the device keeps resident (no partial last round),
+  // each striding over bt-auction tiles.
+  // (the WIDE A/B kernel has slots of its own: its occupancy is not the AUTO kernel's)
+  int &res = wide_ab ? c->resident_wide[prm.want_counters ? 1 : 0]
+                     : c->resident[(gen ? 256 : 0) + (bt == kMidThreads ? 128 : 0) + (ship ? 64 : 0) +
+                                   (gmode == kGenTruthful ? 32 : 0) +
+                                   (bt == kThreads ? 0 : 16) + (c->general ? 8 : 0) + (W == 2 ? 4 : 0) +
+                                   (prune ? 2 : 0) + (prm.want_counters ? 1 : 0)];
+  if (res == 0) {
+    int per_cu = 0, cus = 0;
+    AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k, bt, lds));
+    AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    res = per_cu * cus;
+    if (res < 1) res = 1;
+    if (res > c->partial_blocks) res = c->partial_blocks;
+  }
+  // AG_OPT_SIM_BLOCKS_PER_CU caps the grid below residency (A/B; 0 = every resident block)
+  int grid_max = res;
+  if (c->grid_per_cu > 0) {
+    int cus = 0;
+    AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    if ((int64_t)c->grid_per_cu * cus < grid_max) grid_max = c->grid_per_cu * cus;
+  }
+  // Batches larger than one launch's exact-counter capacity (resident blocks x
+  // kAuctionsPerReplica x replicas) run as consecutive launches over auction ranges.
+  const int64_t per_block = (int64_t)kAuctionsPerReplica * prm.lds.replicas;
+  int64_t chunk_max = (int64_t)grid_max * per_block;
+  if (c->launch_cap > 0 && c->launch_cap < chunk_max) chunk_max = c->launch_cap;
+  chunk_max &= ~(int64_t)1;
+  if (chunk_max < 2) chunk_max = 2;
+  for (int64_t lo = 0; lo < B; lo += chunk_max) {
+    const int64_t hi = lo + chunk_max < B ? lo + chunk_max : B;
+    const int64_t tiles = (hi - lo + bt * W - 1) / (bt * W);
+    const int grid = (int)(tiles < grid_max ? tiles : grid_max);
+    prm.lo = (int32_t)lo;
+    prm.hi = (int32_t)hi;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(bt), lds, st, prm);  // generate mode: same lo/hi
+    AG_HIP(hipGetLastError());
+    if (counters_fx) {
+      hipLaunchKernelGGL(k_reduce_counters, dim3(nc), dim3(kThreads), 0, st, c->d_partials, grid, nc,
+                         counters_fx);
       AG_HIP(hipGetLastError());
     }
   }
@@ -833,7 +960,6 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out_a
                      "split the batch");
   AgDeviceGuard g(c->device);
   const ag_shape &s = c->shape;
-  const int nc = s.num_agents * kC;
   const int D = c->D;
   const bool prune = c->item_search == AG_ITEM_SEARCH_AUTO && D <= 8 && s.num_items <= 2 * kMaxKPairs &&
                      c->values_positive;
@@ -847,132 +973,12 @@ int ag_simulate(ag_ctx *c, int64_t B, const ag_batch_in *in, ag_batch_out *out_a
     return ag_set_error(AG_ERR_INVALID, "ag_simulate: learning bidders with a fitted policy need policy_eps");
   if (c->vl_any_search && !in->gamma_grid)
     return ag_set_error(AG_ERR_INVALID, "ag_simulate: ValueLearningBidders bidding by search need gamma_grid");
-  SimParams prm;
-  prm.B = B;
-  prm.N = s.num_agents;
-  prm.K = s.num_items;
-  prm.mech = s.mechanism;
-  prm.want_counters = counters_fx != nullptr;
-  prm.lds = make_layout(s.num_agents, s.num_items, D, prm.want_counters, c->general,
-                        s.obs_embedding_size + 1);
-  prm.ts_sample = c->ts_sample;
-  prm.akind = c->d_akind;
-  prm.bkind = c->d_bkind;
-  prm.pg = c->d_pg;
-  prm.gs = c->d_gs;
-  prm.tsm = c->d_tsm;
-  prm.drs = c->dr_loaded ? c->dr.state : nullptr;
-  prm.dri = c->dr_loaded ? c->dr.init : nullptr;
-  prm.kag = c->ragged ? c->d_kag : nullptr;
-  prm.items = c->d_items;
-  prm.values = c->d_values;
-  prm.in = *in;
-  prm.out = *out;
-  prm.partials = c->d_partials;
-  prm.P = s.num_participants;
   if (prune && !c->general && c->ora_catalog && c->sim_kernel != AG_SIM_KERNEL_GENERIC && !c->wide)
     if (OraKernel ok = pick_oracle(s.num_participants, D, false))
       return simulate_oracle(c, ok, B, in, out, counters_fx, (hipStream_t)stream);
-  // (round 4 retired k_pop, the dedicated shipped-shape population kernel: k_simulate was as
-  // fast or faster on every line, P = 8 included once its slots stream -- configs_1 at P = 8
-  // 0.665 against 0.680 ms, profiles/r04k_ab_c1p8.log; at P = 2 on every line,
-  // profiles/r03_ab_pop_vs_generic.log)
-  int W = (prune && (B % 2) == 0 && c->wide && !c->general && s.num_participants <= kMaxP) ? 2 : 1;
-  size_t lds = (size_t)prm.lds.total;
-  if (lds > 160 * 1024)
-    return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
-  // Lanes per workgroup: the LDS image (catalogue, screen, LR-TS means, counter replicas) is
-  // per workgroup, so a large population with 256-lane workgroups keeps few waves resident
-  // (N = 32: ~75 KB -> 2 workgroups = 2 waves per SIMD); 1024-lane workgroups share one
-  // image among 16 waves. Same results (the counters are exact sums).
-  int bt = c->block_threads;
-  if (bt == 0) bt = (c->general && prune && lds > 40 * 1024) ? kLargeThreads : kThreads;
-  // AG_OPT_SIM_GENERAL_MODE 0 (auto): TruthfulBidder-only populations take the build
-  // without the bid-shading code (kGenTruthful); 1: always the full general build
-  const int gmode = !c->general ? kGenOracle : (c->has_shading || c->gen_mode_all) ? kGenAll : kGenTruthful;
-  // the shipped shape (E = 5, LR-TS width OE + 1 = 5 in the layout) has builds with the LR-TS
-  // width compile-time (k_simulate's DOS); AG_OPT_SIM_SHIPPED_SHAPE 0 turns them off (A/B)
-  const int ship = (c->general && c->ship_shape && D == 6 && prm.lds.ts_do == kShipDo) ? kGenShip : 0;
-  // the full mix at P >= 3 in the large-image case: the streamed 768-lane build (shipped shape)
-  if (bt == kLargeThreads && c->block_threads == 0 && gmode == kGenAll && ship && s.num_participants >= AG_STREAM_MIN_P &&
-      s.num_participants <= kMaxP)
-    bt = kMidThreads;
-  SimKernel k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
-  if (!k && bt == kMidThreads) {
-    bt = kLargeThreads;
-    k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
-  }
-  if (!k && W == 2) {  // the two-auctions-per-lane build is an A/B variant only (AG_LANE_PAIRS)
-    W = 1;
-    k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
-  }
-  if (!k && bt != kThreads) {
-    bt = kThreads;
-    k = pick_kernel(s.num_participants, D, prune, W, gmode | ship, bt);
-  }
-  bool wide_ab = false;
-#if AG_SIM_WIDE_AB
-  if (c->general && c->sim_kernel == AG_SIM_KERNEL_WIDE) {  // the runtime-P kernel at any P (A/B)
-    bt = kThreads;
-    k = pick_kernel_for<0>(D, prune, 1, kGenAll, kThreads);
-    wide_ab = true;
-  }
-#endif
-  if (!k) return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: no kernel for P=%d D=%d", s.num_participants, D);
-  if (gmode == kGenAll && bt == kLargeThreads) {  // the compacted fitted-policy pass's per-wave task slots
-    add_policy_tasks(prm.lds, bt);
-    lds = (size_t)prm.lds.total;
-    if (lds > 160 * 1024)
-      return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
-  }
-  hipStream_t st = (hipStream_t)stream;
-  if (lds > 64 * 1024)
-    AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  // Persistent grid: exactly the blocks the device keeps resident (no partial last round),
-  // each striding over bt-auction tiles.
-  // (the WIDE A/B kernel has slots of its own: its occupancy is not the AUTO kernel's)
-  int &res = wide_ab ? c->resident_wide[prm.want_counters ? 1 : 0]
-                     : c->resident[(bt == kMidThreads ? 128 : 0) + (ship ? 64 : 0) + (gmode == kGenTruthful ? 32 : 0) +
-                                   (bt == kThreads ? 0 : 16) + (c->general ? 8 : 0) + (W == 2 ? 4 : 0) +
-                                   (prune ? 2 : 0) + (prm.want_counters ? 1 : 0)];
-  if (res == 0) {
-    int per_cu = 0, cus = 0;
-    AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k, bt, lds));
-    AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-    res = per_cu * cus;
-    if (res < 1) res = 1;
-    if (res > c->partial_blocks) res = c->partial_blocks;
-  }
-  // AG_OPT_SIM_BLOCKS_PER_CU caps the grid below residency (A/B; 0 = every resident block)
-  int grid_max = res;
-  if (c->grid_per_cu > 0) {
-    int cus = 0;
-    AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-    if ((int64_t)c->grid_per_cu * cus < grid_max) grid_max = c->grid_per_cu * cus;
-  }
-  // Batches larger than one launch's exact-counter capacity (resident blocks x
-  // kAuctionsPerReplica x replicas) run as consecutive launches over auction ranges.
-  const int64_t per_block = (int64_t)kAuctionsPerReplica * prm.lds.replicas;
-  int64_t chunk_max = (int64_t)grid_max * per_block;
-  if (c->launch_cap > 0 && c->launch_cap < chunk_max) chunk_max = c->launch_cap;
-  chunk_max &= ~(int64_t)1;
-  if (chunk_max < 2) chunk_max = 2;
-  for (int64_t lo = 0; lo < B; lo += chunk_max) {
-    const int64_t hi = lo + chunk_max < B ? lo + chunk_max : B;
-    const int64_t tiles = (hi - lo + bt * W - 1) / (bt * W);
-    const int grid = (int)(tiles < grid_max ? tiles : grid_max);
-    prm.lo = (int32_t)lo;
-    prm.hi = (int32_t)hi;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(bt), lds, st, prm);  // generate mode: same lo/hi
-    AG_HIP(hipGetLastError());
-    if (counters_fx) {
-      hipLaunchKernelGGL(k_reduce_counters, dim3(nc), dim3(kThreads), 0, st, c->d_partials, grid, nc,
-                         counters_fx);
-      AG_HIP(hipGetLastError());
-    }
-  }
-  return AG_OK;
+  return simulate_general(c, B, in, out, counters_fx, (hipStream_t)stream, false, 0, 0);
 }
+
 
 int ag_simulate_generated(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, ag_batch_out *out_arg,
                           int64_t *counters_fx, void *stream) {
@@ -986,12 +992,26 @@ int ag_simulate_generated(ag_ctx *c, uint64_t seed, uint64_t first, int64_t B, a
   const ag_shape &s = c->shape;
   if (B * s.num_participants > INT32_MAX)
     return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate_generated: B * P must be < 2^31; split the batch");
+  if (c->general) {
+    // every draw in the kernel (k_simulate<..., GEN>): contexts, participants, uniforms, the
+    // LR-TS agents' Thompson noise, the fitted policies' rsample draws, the shading draws
+    if (c->has_lrts && !c->lrts_loaded)
+      return ag_set_error(AG_ERR_STATE, "ag_simulate_generated: LR-TS agents need ag_load_lrts");
+    if (c->vl_any_search)
+      return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate_generated: ValueLearningBidders bidding by search "
+                                              "(their 128-point grids are not drawn in the kernel)");
+    if (c->shape.num_participants > 64)
+      return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate_generated: P > 64");
+    AgDeviceGuard g(c->device);
+    return simulate_general(c, B, nullptr, out, counters_fx, (hipStream_t)stream, true, seed, first);
+  }
   OraKernel k = (!c->general && c->ora_catalog && s.num_items <= 2 * kMaxKPairs)
                     ? pick_oracle(s.num_participants, c->D, true) : nullptr;
   if (!k)
     return ag_set_error(AG_ERR_UNSUPPORTED,
                         "ag_simulate_generated: OracleAllocator + TruthfulBidder populations with P <= %d, "
-                        "E + 1 <= 8, K <= %d and catalogue values in (0, %g) only",
+                        "E + 1 <= 8, K <= %d and catalogue values in (0, %g) only (general populations: the "
+                        "shipped shape)",
                         kMaxP, 2 * kMaxKPairs, kOraMaxValue);
   AgDeviceGuard g(c->device);
   // a launch covers auctions [lo, hi) of the batch: their global indices are first + lo ...

@@ -74,3 +74,37 @@ __device__ __forceinline__ void gen_auction(uint32_t k0, uint32_t k1, uint64_t i
     if (2 * m + 1 < E) x[2 * m + 1] = 0.0 + scale * (double)(r * __builtin_amdgcn_sinf(t));
   }
 }
+
+// Synthetic per-participant draws (ag_generate_noise writes them; the general kernel's generate
+// mode draws the same bits in place). Same key and counter scheme, stream by kind and slot s:
+//  - LR-TS Thompson noise (torch.normal(0, 1/sqrt(q)), src/Models.py:31): coefficient c of slot
+//    s from block c / 4 of stream 4 + s, four float32 normals per Philox call (two Box-Muller
+//    pairs from 32-bit uniforms, the hardware transcendentals, as the contexts above; round 6:
+//    before, one FP64 pair per call -- 30 calls and 30 FP64 log / sincos per slot), times
+//    1 / sqrtf(q) of the coefficient;
+//  - a fitted policy's rsample draw: the first normal of block 0 of stream 16 + s;
+//  - shading draws N(prev_gamma, sigma) (numpy normal(loc, scale), src/Bidder.py:51, :177):
+//    prev_gamma + sigma * the first normal of block s of stream 3 (round 6: float32 Box-Muller;
+//    before, an FP64 pair -- its log / sincospi held ~100 VGPRs in the generate-mode kernel).
+__device__ __forceinline__ void gen_normals4(uint32_t c0, uint32_t c1, uint32_t blk, uint32_t stream, uint32_t k0,
+                                             uint32_t k1, float (&z)[4]) {
+  uint32_t w[4];
+  philox(c0, c1, blk, stream, k0, k1, w);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float r = gen_normal_r(w[2 * h]);
+    const float t = (float)w[2 * h + 1] * 0x1p-32f;
+    z[2 * h] = r * __builtin_amdgcn_cosf(t);
+    z[2 * h + 1] = r * __builtin_amdgcn_sinf(t);
+  }
+}
+__device__ __forceinline__ float gen_normal1(uint32_t c0, uint32_t c1, uint32_t blk, uint32_t stream, uint32_t k0,
+                                             uint32_t k1) {
+  uint32_t w[4];
+  philox(c0, c1, blk, stream, k0, k1, w);
+  return gen_normal_r(w[0]) * __builtin_amdgcn_cosf((float)w[1] * 0x1p-32f);
+}
+__device__ __forceinline__ double gen_shading_raw(uint32_t c0, uint32_t c1, int s, uint32_t k0, uint32_t k1,
+                                                  double prev_gamma, double sigma) {
+  return prev_gamma + sigma * (double)gen_normal1(c0, c1, (uint32_t)s, 3, k0, k1);
+}

@@ -10,6 +10,7 @@
 #include "ag_exp.h"
 #include "ag_exp_table.h"
 #include "ag_log1p.h"
+#include "ag_philox.h"
 
 namespace ag {
 
@@ -66,6 +67,12 @@ namespace ag {
 #endif
 #ifndef AG_MAX_REPLICAS
 #define AG_MAX_REPLICAS 16
+#endif
+#ifndef AG_TS_DMA
+#define AG_TS_DMA 0  // replayed Thompson noise streamed into a per-wave LDS ring by LDS-DMA (A/B)
+#endif
+#ifndef AG_TS_DMA_AHEAD
+#define AG_TS_DMA_AHEAD 2  // ... items in flight ahead of the one being scored
 #endif
 
 constexpr int kThreads = 256;              // 4 waves of 64 lanes
@@ -145,6 +152,7 @@ __device__ __forceinline__ unsigned long long to_fx(double x) {
 // LDS carve of k_simulate (all pieces 16-B aligned; offsets in bytes).
 struct LdsLayout {
   int32_t tab, items, values, scr, scr_val, amax, akind, bkind, pg, gs, tsm, drs, dri, kag, cnt, total;
+  int32_t tsr;             // generate mode: the LR-TS agents' 1 / sqrtf(q), laid out as tsm (0: none)
   int32_t items_stride;    // doubles between agents (odd: spreads agents over banks)
   int32_t values_stride;   // doubles
   int32_t scr_stride;      // floats between agents in the screening catalogue
@@ -173,7 +181,7 @@ enum { kSlotGross = 0, kSlotPaid, kSlotOverbid, kSlotUnderbid, kSlotBestEv, kSlo
        kSlotAlloc, kSlotEst, kSlotSqerr, kSlotBias };
 
 __host__ inline LdsLayout make_layout(int N, int K, int D, bool counters, bool general = false,
-                                      int ts_do = 0) {
+                                      int ts_do = 0, bool gen = false) {
   LdsLayout L;
   L.items_stride = (K * D) | 1;
   L.values_stride = K | 1;
@@ -228,6 +236,11 @@ __host__ inline LdsLayout make_layout(int N, int K, int D, bool counters, bool g
   b = L.kag + (general ? (int64_t)N * 4 : 0);
   L.cnt = align16(b);
   b = L.cnt + (counters ? (int64_t)R * N * L.ncnt * 8 : 0);
+  L.tsr = 0;
+  if (general && gen) {  // after the counters: the other offsets are those of the replay layout
+    L.tsr = align16(b);
+    b = L.tsr + (int64_t)N * L.tsm_stride * 4;
+  }
   L.total = align16(b);
   L.pol = 0;
   return L;
@@ -260,6 +273,10 @@ struct SimParams {
   ag_batch_out out;
   int64_t *partials;      // [grid][N][AG_NUM_COUNTERS][2]
   int32_t P;              // participants per round (read by the runtime-P kernel, P = 0)
+  // generate mode (k_simulate<..., GEN = true>): every input drawn in the kernel
+  const float *tsq;       // [N][K][OE+1] LR-TS q (the Thompson noise's scale 1 / sqrtf(q))
+  uint64_t seed, first;   // Philox key; global index of the batch's auction 0
+  double scale;           // embedding_var (the contexts' scale)
 };
 
 // Screening margin. The screen ranks items by t_k = (1 + 2^(z'_k)) / v_k = 1 / (exact
@@ -428,7 +445,62 @@ struct Lds {
   const float *drs;
   const int32_t *dri;
   const int32_t *kag;  // general: each agent's own item count (src/main.py:61,66)
+  const float *tsr;    // generate mode: the LR-TS agents' 1 / sqrtf(q) (stride tsm_stride)
+  const float *ring;   // AG_TS_DMA: this wave's Thompson-noise ring (NULL: none)
+  uint32_t ring_lds;   // ... its LDS byte address
 };
+
+// generate mode: one auction's Philox counter (its global index) and key
+struct GenKey {
+  uint32_t c0, c1, k0, k1;
+};
+
+// Where a slot's Thompson noise comes from: the HBM tiles (replay and HBM-resident synthetic
+// batches) or, in generate mode, the draws ag_generate_noise would have stored there.
+struct TsSrc {
+  const float *nz;   // HBM: coefficient c at nz[c * 64] (NULL: no noise)
+  const float *rsq;  // generate mode: the agent's 1 / sqrtf(q) [K][Do] (NULL: no noise)
+  GenKey key;
+  uint32_t stream;   // generate mode: 4 + slot
+  // AG_TS_DMA: the wave's LDS ring of kTsDmaBufs item buffers (DOS rows of 64 floats each),
+  // its LDS byte address, and the batch's item count K (wave-uniform: the DMA schedule)
+  const float *ring;
+  uint32_t ring_lds;
+  int kg;
+};
+
+// ---- AG_TS_DMA: the replayed Thompson noise of a slot streamed into the wave's LDS ring by
+// LDS-DMA (global_load_lds_dword: no VGPR held while in flight), kTsDmaAhead items ahead of
+// the one being scored; the first items issued before the slot's exact true-CTR search. The
+// loads are inline asm, outside the compiler's s_waitcnt bookkeeping: every wait is our own
+// vmcnt(N), N = the DMA instructions issued after the item's (the compiler's own vector memory
+// operations are made to complete before the first issue, so none sits between).
+constexpr int kTsDmaAhead = AG_TS_DMA_AHEAD;
+constexpr int kTsDmaBufs = kTsDmaAhead + 1;
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// the 5 noise rows of one item (the lane's element of row c at src + 64 c floats) into the LDS
+// rows at lds + 256 c bytes (lds wave-uniform); the ring buffer it overwrites was read by the
+// item before (lgkmcnt(0): those reads done)
+__device__ __forceinline__ void ts_dma_item5(const float *src, uint32_t lds_any) {
+  const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_any);
+  uint32_t keep;
+  asm volatile(
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
+      "s_mov_b32 m0, %7\n\ts_nop 0\n\tglobal_load_lds_dword %2, off\n\t"
+      "s_mov_b32 m0, %8\n\ts_nop 0\n\tglobal_load_lds_dword %3, off\n\t"
+      "s_mov_b32 m0, %9\n\ts_nop 0\n\tglobal_load_lds_dword %4, off\n\t"
+      "s_mov_b32 m0, %10\n\ts_nop 0\n\tglobal_load_lds_dword %5, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "v"(src + 64), "v"(src + 128), "v"(src + 192), "v"(src + 256), "s"(lds), "s"(lds + 256u),
+        "s"(lds + 512u), "s"(lds + 768u), "s"(lds + 1024u)
+      : "memory");
+}
 
 // One auction resolved (src/Auction.py:28-74 minus the draws).
 template <int P>
@@ -541,35 +613,99 @@ constexpr int kTsGroup = AG_TS_GROUP;
 constexpr int kTsScreenK = 12;
 constexpr int kShipDo = 5;   // the shipped configs' LR-TS model width (OE = 4)
 constexpr int kGenShip = 8;  // pick_kernel_for: OR-ed into `general` for that width (D = 6)
+constexpr int kGenGen = 16;  // pick_kernel_for: OR-ed into `general` for the generate-mode build
 // the noise of items k0 .. k0 + kTsGroup - 1 (coefficient stride 64: the tile layout). (Tried:
 // non-temporal loads of the dense layout, and loading the first group before the true-CTR
 // search: no gain / scratch spills, profiles/r05m_ab_pre.log, r05n_ab_nt.log.)
 template <int DW>
-__device__ __forceinline__ void ts_load_group(const float *nz, int k0, int K, int Do, float (&nzv)[kTsGroup][DW]) {
+__device__ __forceinline__ void ts_load_group(const TsSrc &src, int k0, int K, int Do, float (&nzv)[kTsGroup][DW]) {
+  const float *nz = src.nz;
 #pragma unroll
   for (int g = 0; g < kTsGroup; ++g)
 #pragma unroll
     for (int d = 0; d < DW; ++d)
       nzv[g][d] = (nz && k0 + g < K && d < Do) ? nz[(size_t)((k0 + g) * Do + d) * 64] : 0.0f;
 }
-template <int DW>
-__device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], const float *nz, int K, int Do,
+// Generate mode (compile-time model width DOS): the noise of item k0 + g, drawn as
+// ag_generate_noise draws it -- coefficient c = k Do + d is normal c % 4 of Philox block c / 4
+// (ag_philox.h gen_normals4) times the coefficient's 1 / sqrtf(q). A group's kTsGroup items are
+// kTsGroup DOS / 4 whole blocks (k0 % 4 == 0); the items are drawn in order (g compile-time
+// after unrolling), each block when its first coefficient comes, the block's normals carried
+// in z4 -- at most 4 + DOS noise values live instead of a group's kTsGroup DOS.
+template <int DW, int DOS>
+__device__ __forceinline__ void ts_gen_item(const TsSrc &src, int k0, int g, float (&z4)[4], float (&nzg)[DW]) {
+  static_assert(DOS > 0 && DOS <= DW && kTsGroup % 4 == 0, "generate mode: compile-time width, whole blocks");
+#pragma unroll
+  for (int d = 0; d < DW; ++d) nzg[d] = 0.0f;
+  if (!src.rsq) return;
+  const uint32_t b0 = (uint32_t)(k0 * DOS) >> 2;
+#pragma unroll
+  for (int d = 0; d < DOS; ++d) {
+    const int c = g * DOS + d;
+    if ((c & 3) == 0)
+      gen_normals4(src.key.c0, src.key.c1, b0 + (uint32_t)(c >> 2), src.stream, src.key.k0, src.key.k1, z4);
+    nzg[d] = z4[c & 3] * src.rsq[(k0 + g) * DOS + d];
+  }
+}
+template <int DW, bool GEN = false, int DOS = 0>
+__device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], const TsSrc &src, int K, int Do,
                                          const double *vals, const uint64_t *tab) {
+  const bool noisy = GEN ? src.rsq != nullptr : src.nz != nullptr;
   if (AG_TS_SCREEN && K <= kTsScreenK) {
     float zk[kTsScreenK], ek[kTsScreenK];  // logits; score estimates (-1: score exactly)
     float best_est = 0.0f;
+    if (AG_TS_DMA && !GEN && DOS == 5 && src.ring) {
+      // the noise from the wave's LDS ring: items 0 .. kTsDmaAhead - 1 were issued before the
+      // slot's true-CTR search; item k issues item k + kTsDmaAhead, then waits for its own.
+      // The batch's K is kTsScreenK (resolve_slot's condition), whatever the lane's own count:
+      // the schedule and every vmcnt are compile-time constants
+      constexpr int KG = kTsScreenK;
+      const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+      for (int k = 0; k < KG; ++k) {
+        zk[k] = 0.0f;
+        ek[k] = -1.0f;
+        {
+          if (k + kTsDmaAhead < KG)
+            ts_dma_item5(src.nz + (size_t)(k + kTsDmaAhead) * 5 * 64,
+                         src.ring_lds + (uint32_t)(((k + kTsDmaAhead) % kTsDmaBufs) * 5 * 256));
+          constexpr int kLast = KG - 1;
+          const int later = (k + kTsDmaAhead < kLast ? k + kTsDmaAhead : kLast) - k;  // items issued after k
+          if (later == 2) wait_vm<10>();
+          else if (later == 1) wait_vm<5>();
+          else if (later == 0) wait_vm<0>();
+          else if (later == 3) wait_vm<15>();
+          else wait_vm<0>();
+          const float *row = src.ring + (k % kTsDmaBufs) * 5 * 64 + lane;
+          float nzg[DW];
+#pragma unroll
+          for (int d = 0; d < DW; ++d) nzg[d] = d < 5 ? row[d * 64] : 0.0f;
+          if (k < K) {
+            const float z = ts_logit<DW>(m + k * Do, xo, nzg, noisy, Do, k, K);
+            const float v = (float)vals[k];
+            const bool ok = __builtin_fabsf(z) < 64.0f && v > 0.0f;
+            const float e = __builtin_amdgcn_exp2f(-z * 1.44269504f);
+            const float est = ok ? __builtin_amdgcn_rcpf(1.0f + e) * v : -1.0f;
+            zk[k] = z;
+            ek[k] = est;
+            best_est = est > best_est ? est : best_est;
+          }
+        }
+      }
+    } else
 #pragma unroll
     for (int k0 = 0; k0 < kTsScreenK; k0 += kTsGroup) {
       if (k0 < K) {
-        float nzv[kTsGroup][DW];
-        ts_load_group<DW>(nz, k0, K, Do, nzv);
+        float nzv[GEN ? 1 : kTsGroup][DW], z4[4];
+        if constexpr (!GEN) ts_load_group<DW>(src, k0, K, Do, nzv);
 #pragma unroll
         for (int g = 0; g < kTsGroup; ++g) {
           const int k = k0 + g;
           zk[k] = 0.0f;
           ek[k] = -1.0f;
           if (k < K) {
-            const float z = ts_logit<DW>(m + k * Do, xo, nzv[g], nz != nullptr, Do, k, K);
+            if constexpr (GEN) ts_gen_item<DW, DOS>(src, k0, g, z4, nzv[0]);
+            const float z = ts_logit<DW>(m + k * Do, xo, nzv[GEN ? 0 : g], noisy, Do, k, K);
             const float v = (float)vals[k];
             const bool ok = __builtin_fabsf(z) < 64.0f && v > 0.0f;
             const float e = __builtin_amdgcn_exp2f(-z * 1.44269504f);
@@ -613,13 +749,14 @@ __device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], 
   double best_sc = 0.0;
   int best = 0;
   for (int k0 = 0; k0 < K; k0 += kTsGroup) {
-    float nzv[kTsGroup][DW];
-    ts_load_group<DW>(nz, k0, K, Do, nzv);
+    float nzv[GEN ? 1 : kTsGroup][DW], z4[4];
+    if constexpr (!GEN) ts_load_group<DW>(src, k0, K, Do, nzv);
 #pragma unroll
     for (int g = 0; g < kTsGroup; ++g) {
       const int k = k0 + g;
       if (k < K) {
-        const float ck = ts_ctr_k<DW>(m + k * Do, xo, nzv[g], nz != nullptr, Do, k, K, tab);
+        if constexpr (GEN) ts_gen_item<DW, DOS>(src, k0, g, z4, nzv[0]);
+        const float ck = ts_ctr_k<DW>(m + k * Do, xo, nzv[GEN ? 0 : g], noisy, Do, k, K, tab);
         const double sc = (double)ck * vals[k];
         if (k == 0 || sc > best_sc) {
           best_sc = sc;
@@ -714,16 +851,47 @@ struct SlotResult {
 #endif
 constexpr int kAblate = AG_ABLATE;
 
-template <int D, bool PRUNE, int GENERAL, bool DEFER = false>
+// GEN: generate mode -- the slot's draws (Thompson noise, rsample, shading) made here from the
+// auction's Philox counter `gk`, the bits ag_generate_noise stores (ag_philox.h); `in` unread.
+template <int D, bool PRUNE, int GENERAL, bool DEFER = false, bool GEN = false, int DOS = 0>
 __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const double (&x)[kMaxD],
                                                    const float (&xf)[kMaxD], float xabs, int a, int s,
                                                    const ag_batch_in &in, uint32_t B, uint32_t i, bool ts_sample,
-                                                   int tsj = kTsjLoad) {
+                                                   int tsj = kTsjLoad, GenKey gk = GenKey{0, 0, 0, 0}) {
   // true CTRs (src/Auction.py:52-53): exact search on the true context; for an Oracle
   // agent this IS Agent.select_item (src/BidderAllocation.py:81-82)
   double c = 0.5, bs = 0.5;
   const double *itm = T.items + a * T.items_stride;
   const bool lrts = GENERAL && T.akind[a] == AG_ALLOCATOR_LRTS;
+  // LR-TS: where the slot's Thompson noise comes from (tiled noise: coefficient c of auction i
+  // at ((s*T + i/64)*K*Do + c)*64 + i%64; the compact layout tiles the batch's LR-TS pairs
+  // only, pair j = ts_noise_index[s*B + i] in place of s*T*64 + i -- mixed populations: no
+  // noise stored or fetched for the slots of other agents)
+  TsSrc nz{nullptr, nullptr, gk, 4u + (uint32_t)s};
+  if constexpr (GENERAL) {
+    const int Do = DOS > 0 ? DOS : T.ts_do;
+    if constexpr (GEN) {
+      if (lrts && ts_sample) nz.rsq = T.tsr + (size_t)a * T.tsm_stride;
+    } else if (lrts && ts_sample && in.ts_noise) {
+      if (in.ts_noise_index) {
+        // prefetched with the tile's inputs (tsj), or loaded here
+        const uint32_t j = (uint32_t)(tsj != kTsjLoad ? tsj : ldg(in.ts_noise_index + (size_t)s * B + i));
+        nz.nz = in.ts_noise + ((size_t)(j >> 6) * K * Do) * 64 + (j & 63);
+      } else {
+        nz.nz = in.ts_noise + ((size_t)(s * ((B + 63) >> 6) + (i >> 6)) * K * Do) * 64 + (i & 63);
+      }
+      if (AG_TS_DMA && DOS == 5 && T.ring && K == kTsScreenK) {
+        // the first kTsDmaAhead items' rows into the wave's ring now: they land while the exact
+        // true-CTR search below runs (k_simulate has made the compiler wait for all of the
+        // tile's own loads already, so no compiler-counted load sits behind these DMAs)
+        nz.ring = T.ring;
+        nz.ring_lds = T.ring_lds;
+        nz.kg = kTsScreenK;
+#pragma unroll
+        for (int k = 0; k < kTsDmaAhead; ++k) ts_dma_item5(nz.nz + (size_t)k * 5 * 64, T.ring_lds + (uint32_t)(k * 5 * 256));
+      }
+    }
+  }
   const int best_t = (kAblate & 4) ? 0
                                    : select_item<D, PRUNE>(itm, T.vals + a * T.values_stride,
                                                            T.scr + a * T.scr_stride, T.scr_val + a * T.scr_val_stride,
@@ -737,22 +905,8 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
       // LR-TS (src/Agent.py:29-42): the sampled CTRs on the observed context pick the
       // item by first argmax of CTR * value (float32 CTR widened to double), the MAP CTR
       // of that item is the estimate
-      const int Do = T.ts_do;
+      const int Do = DOS > 0 ? DOS : T.ts_do;
       const float *m = T.tsm + (size_t)a * T.tsm_stride;
-      // tiled noise: coefficient c of auction i at ((s*T + i/64)*K*Do + c)*64 + i%64; the
-      // compact layout tiles the batch's LR-TS pairs only, pair j = ts_noise_index[s*B + i]
-      // in place of s*T*64 + i (mixed populations: no noise stored or fetched for the
-      // slots of other agents)
-      const float *nz = nullptr;
-      if (ts_sample && in.ts_noise) {
-        if (in.ts_noise_index) {
-          // prefetched with the tile's inputs (tsj), or loaded here
-          const uint32_t j = (uint32_t)(tsj != kTsjLoad ? tsj : ldg(in.ts_noise_index + (size_t)s * B + i));
-          nz = in.ts_noise + ((size_t)(j >> 6) * K * Do) * 64 + (j & 63);
-        } else {
-          nz = in.ts_noise + ((size_t)(s * ((B + 63) >> 6) + (i >> 6)) * K * Do) * 64 + (i & 63);
-        }
-      }
       // observed context (src/Auction.py:36) in a register row of width D >= Do
       float xo[D];
 #pragma unroll
@@ -763,7 +917,7 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
       // 2-4 % slower on every population line, profiles/r04s_ab_c*_kag.log)
       const int Ka = T.kag[a];
       best = (kAblate & 2) ? best_t
-                           : ts_select<D>(m, xo, nz, Ka, Do, T.vals + a * T.values_stride, T.tab);
+                           : ts_select<D, GEN, DOS>(m, xo, nz, Ka, Do, T.vals + a * T.values_stride, T.tab);
       est = (kAblate & 16) ? 0.5 : (double)ts_ctr_k<D>(m + best * Do, xo, xo, false, Do, best, Ka, T.tab);
       tru = (best == best_t || (kAblate & 32)) ? c : agexp::sigmoid_fast(dot_ref<D>(itm + best * D, x), T.tab);
     }
@@ -780,15 +934,18 @@ __device__ __forceinline__ SlotResult resolve_slot(const Lds &T, int K, const do
         g = 1.0;
         prop = 1.0;
       } else {
-        policy_bid(T.drs + a * T.drs_stride + 4, est, v, in.policy_eps[(size_t)s * B + i], T.tab, g, prop);
+        const float eps = GEN ? gen_normal1(gk.c0, gk.c1, 0, 16u + (uint32_t)s, gk.k0, gk.k1)
+                              : in.policy_eps[(size_t)s * B + i];
+        policy_bid(T.drs + a * T.drs_stride + 4, est, v, eps, T.tab, g, prop);
         b = b * g;
       }
-    } else if (bk == AG_BIDDER_VALUE_LEARNING && T.drs && T.dri[a] == AG_LEARNER_SEARCH) {
+    } else if (!GEN && bk == AG_BIDDER_VALUE_LEARNING && T.drs && T.dri[a] == AG_LEARNER_SEARCH) {
+      // (generate mode has no search grids: the host refuses such populations)
       g = search_gamma(T.drs + a * T.drs_stride, est, v, in.gamma_grid + (size_t)s * 128 * B + i, B, T.tab);
       prop = 1.0;  // src/Bidder.py:196
       b = b * g;
     } else if (bk != AG_BIDDER_TRUTHFUL) {
-      g = in.gamma_raw[(size_t)s * B + i];
+      g = GEN ? gen_shading_raw(gk.c0, gk.c1, s, gk.k0, gk.k1, T.pg[a], T.gs[a]) : in.gamma_raw[(size_t)s * B + i];
       if (bk == AG_BIDDER_EMPIRICAL_SHADED) {  // clipped to [0, 1] (src/Bidder.py:52-55)
         if (g < 0.0) g = 0.0;
         if (g > 1.0) g = 1.0;
@@ -814,18 +971,19 @@ __device__ __forceinline__ void top2_step(int s, double b, double &m1, double &m
   }
 }
 
-template <int P, int D, bool PRUNE, int GENERAL>
+template <int P, int D, bool PRUNE, int GENERAL, bool GEN = false, int DOS = 0>
 __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const double (&x)[kMaxD],
                                         const float (&xf)[kMaxD], float xabs, const int (&ag)[P], double u,
                                         const ag_batch_in &in, uint32_t B, uint32_t i, bool ts_sample,
-                                        const int (&tsj)[P], Resolved<P> &r) {
+                                        const int (&tsj)[P], Resolved<P> &r, GenKey gk) {
   double m1 = 0.0, m2 = -INFINITY;
   int w = 0;
 #pragma unroll
   for (int s = 0; s < P; ++s) {
     const int a = ag[s];
     r.ag[s] = a;
-    const SlotResult q = resolve_slot<D, PRUNE, GENERAL>(T, K, x, xf, xabs, a, s, in, B, i, ts_sample, tsj[s]);
+    const SlotResult q =
+        resolve_slot<D, PRUNE, GENERAL, false, GEN, DOS>(T, K, x, xf, xabs, a, s, in, B, i, ts_sample, tsj[s], gk);
     r.item[s] = q.item;
     r.val[s] = q.val;
     r.bid[s] = q.bid;
@@ -853,7 +1011,11 @@ __device__ __forceinline__ void resolve(const Lds &T, int K, int mech, const dou
 // 441 -> 155 SGPRs spilled to VGPR lanes; the full build at 1024 lanes: 112 -> 52 B of
 // scratch per lane). K stays a runtime value: with it compile-time the item loops unroll
 // fully and spill (200 VGPRs at P = 2), measured.
-template <int P, int D, bool PRUNE, int W, int GENERAL, int BT = kThreads, int DOS = 0>
+// GEN: generate mode (ag_simulate_generated) -- every input drawn in the kernel from the
+// auction's global index, the bits ag_generate + ag_generate_noise store (contexts,
+// participants, uniform: gen_auction; Thompson noise, rsample and shading draws: resolve_slot);
+// only the outputs touch HBM. Shipped-shape builds (DOS > 0) only.
+template <int P, int D, bool PRUNE, int W, int GENERAL, int BT = kThreads, int DOS = 0, bool GEN = false>
 __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_MIN_WAVES : AG_TB_MIN_WAVES)
                                  : (GENERAL ? ((DOS && P > 0 && P <= 2) ? AG_GEN_DOS_MIN_WAVES : AG_GEN_MIN_WAVES)
                                             : AG_MIN_WAVES)) void k_simulate(SimParams prm) {
@@ -877,6 +1039,11 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
   float *s_drs = reinterpret_cast<float *>(smem + L.drs);
   int32_t *s_dri = reinterpret_cast<int32_t *>(smem + L.dri);
   int32_t *s_kag = reinterpret_cast<int32_t *>(smem + L.kag);
+  float *s_tsr = reinterpret_cast<float *>(smem + L.tsr);
+  // AG_TS_DMA: every wave's Thompson-noise ring (kTsDmaBufs items of 5 rows x 64 floats)
+  constexpr bool kDma = AG_TS_DMA && GENERAL && DOS == 5 && !GEN;
+  __shared__ __attribute__((aligned(16))) float s_ring[kDma ? (BT / 64) * kTsDmaBufs * 5 * 64 : 1];
+  static_assert(!GEN || (DOS > 0 && P > 0 && W == 1 && GENERAL), "generate mode: shipped-shape general builds");
   unsigned long long *s_cnt = reinterpret_cast<unsigned long long *>(smem + L.cnt);
 
   const int tid = threadIdx.x;
@@ -891,6 +1058,8 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
     for (int j = tid; j < N * K * L.ts_do; j += BT) {
       const int a = j / (K * L.ts_do);
       s_tsm[a * L.tsm_stride + (j - a * K * L.ts_do)] = prm.tsm[j];
+      // generate mode: the noise scale as k_generate_noise computes it
+      if constexpr (GEN) s_tsr[a * L.tsm_stride + (j - a * K * L.ts_do)] = 1.0f / sqrtf(prm.tsq[j]);
     }
     if (prm.drs) {
       for (int j = tid; j < N * 16; j += BT) s_drs[(j >> 4) * L.drs_stride + (j & 15)] = prm.drs[j];
@@ -931,10 +1100,17 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
     for (int i = tid; i < R * N * L.ncnt; i += BT) s_cnt[i] = 0ull;
   __syncthreads();
 
-  const Lds T{s_tab, s_items, s_vals, s_scr, s_scr_val, s_amax, L.items_stride, L.values_stride,
+  Lds T{s_tab, s_items, s_vals, s_scr, s_scr_val, s_amax, L.items_stride, L.values_stride,
               L.scr_stride, L.scr_val_stride, L.kpairs, s_akind, s_bkind, s_pg, s_gs, s_tsm, L.ts_do,
               L.tsm_stride, L.drs_stride, (GENERAL && prm.drs) ? s_drs : nullptr, s_dri,
-              GENERAL ? s_kag : nullptr};
+              GENERAL ? s_kag : nullptr, GEN ? s_tsr : nullptr, nullptr, 0u};
+  if constexpr (kDma) {
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    T.ring = s_ring + wv * kTsDmaBufs * 5 * 64;
+    T.ring_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float *)s_ring +
+                 (uint32_t)(wv * kTsDmaBufs * 5 * 256);
+    T.ring_lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)T.ring_lds);
+  }
   const int rep = tid & (R - 1);
   const ag_batch_in in = prm.in;
   const ag_batch_out out = prm.out;
@@ -949,7 +1125,23 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
   int pv[PA][W];
   double uv[W];
   int jv[PA][W];  // compact ts_noise_index entries (GENERAL with ts_noise_index; else kTsjLoad)
-  const bool pre_tsj = GENERAL && !AG_PREFETCH && in.ts_noise_index && in.ts_noise && prm.ts_sample;
+  const bool pre_tsj = !GEN && GENERAL && !AG_PREFETCH && in.ts_noise_index && in.ts_noise && prm.ts_sample;
+  static_assert(!GEN || !AG_PREFETCH, "generate mode has no input loads to pipeline");
+  const uint32_t gk0 = (uint32_t)prm.seed, gk1 = (uint32_t)(prm.seed >> 32);
+  // generate mode: the tile's inputs drawn (ag_generate's bits) instead of loaded
+  auto gen_tile = [&](uint32_t i) {
+    double x[kMaxD], u;
+    int pk[PA];
+    gen_auction<PA, kMaxD>(gk0, gk1, prm.first + i, N, PA, D - 1, prm.scale, x, pk, u);
+#pragma unroll
+    for (int e = 0; e < D - 1; ++e) xv[e][0] = x[e];
+#pragma unroll
+    for (int s = 0; s < PA; ++s) {
+      pv[s][0] = pk[s];
+      jv[s][0] = kTsjLoad;
+    }
+    uv[0] = u;
+  };
   // streamed slots (below): each slot's participant / noise index loaded with the slot
   // streamed slots for TruthfulBidder-only populations (configs_1 at P = 8: 0.665 vs 0.730 ms
   // kept per-slot arrays, profiles/r04k_ab_c1p8.log) and for the full mix in its 768-lane build
@@ -1070,6 +1262,8 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
 #endif
   for (uint32_t base = lo + wg_tile * (BT * W); base < hi; base += stride) {
     const uint32_t i = base + tid * W;  // W consecutive auctions (even chunk bounds when W = 2)
+    // generate mode: the auction's Philox counter (its global index) for the slots' draws
+    const GenKey gk{(uint32_t)(prm.first + i), (uint32_t)((prm.first + i) >> 32), gk0, gk1};
     if constexpr (kStream && AG_STREAM_SYNC == 1) __syncthreads();
     [[maybe_unused]] const bool wg_full = base + BT * W <= hi;  // uniform over the workgroup
 #if AG_PREFETCH
@@ -1141,7 +1335,22 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
       }
       continue;
     }
-    load_tile(i);
+    if constexpr (GEN)
+      gen_tile(i);
+    else
+      load_tile(i);
+    if constexpr (kDma) {
+      // AG_TS_DMA: every input of the tile used here, so the compiler waits for all of its own
+      // loads now -- none is left for it to wait for (with a count that cannot see the noise
+      // DMAs) once the slots' DMAs are in flight
+#pragma unroll
+      for (int e = 0; e < D - 1; ++e) asm volatile("" ::"v"(xv[e][0]));
+      asm volatile("" ::"v"(uv[0]));
+      if constexpr (!kStream) {
+#pragma unroll
+        for (int s = 0; s < PA; ++s) asm volatile("" ::"v"(pv[s][0]), "v"(jv[s][0]));
+      }
+    }
 #define XV xv
 #define PV pv
 #define UV uv
@@ -1179,15 +1388,15 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
           if (wg_full) __syncthreads();
         }
         const uint32_t o = s * B + i;
-        const int a = ldg(in.part + o);
+        const int a = GEN ? PV[s][0] : ldg(in.part + o);
 #if AG_STREAM_PACK_AGENTS
         if (s & 1)
           apk[s >> 1] |= (uint32_t)a << 16;
         else
           apk[s >> 1] = (uint32_t)a;
 #endif
-        const SlotResult q = resolve_slot<D, PRUNE, GENERAL, false>(T, K, x, xf, xabs, a, s, in, B, i,
-                                                                    prm.ts_sample != 0);
+        const SlotResult q = resolve_slot<D, PRUNE, GENERAL, false, GEN, DOS>(T, K, x, xf, xabs, a, s, in, B, i,
+                                                                              prm.ts_sample != 0, kTsjLoad, gk);
         if (out.item) stg(out.item + o, (int32_t)q.item);
         if (out.bid) stg(out.bid + o, q.bid);
         if (out.est_ctr) stg(out.est_ctr + o, q.est);
@@ -1223,7 +1432,7 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
 #if AG_STREAM_PACK_AGENTS
           const int a = (int)((apk[s >> 1] >> (16 * (s & 1))) & 0xffffu);
 #else
-          const int a = ldg(in.part + s * B + i);
+          const int a = GEN ? PV[s][0] : ldg(in.part + s * B + i);
 #endif
           count_post(a, charged && s == w, charged ? price : 0.0, price, m2, bidv[s], tvv[s], val_w, rat_w, oc);
         }
@@ -1260,8 +1469,8 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
       for (int s = 0; s < P; ++s) {
         const uint32_t o = s * B + i;
         const int a = PV[s][0];
-        const SlotResult q = resolve_slot<D, PRUNE, GENERAL, kCompactPolicy>(
-            T, K, x, xf, xabs, a, s, in, B, i, prm.ts_sample != 0, AG_PREFETCH ? kTsjLoad : jv[s][0]);
+        const SlotResult q = resolve_slot<D, PRUNE, GENERAL, kCompactPolicy, GEN, DOS>(
+            T, K, x, xf, xabs, a, s, in, B, i, prm.ts_sample != 0, AG_PREFETCH ? kTsjLoad : jv[s][0], gk);
         if (out.item) stg(out.item + o, (int32_t)q.item);
         if (out.est_ctr) stg(out.est_ctr + o, q.est);
         if (out.true_ctr) stg(out.true_ctr + o, q.ctr);
@@ -1297,8 +1506,9 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
         for (int s = 0; s < P; ++s) {
           if (polx[s] >= 0) {
             double g, pr;
-            policy_bid(T.drs + PV[s][0] * T.drs_stride + 4, estv[s], valv[s], ldg(in.policy_eps + (size_t)s * B + i), T.tab,
-                       g, pr);
+            const float eps = GEN ? gen_normal1(gk.c0, gk.c1, 0, 16u + (uint32_t)s, gk.k0, gk.k1)
+                                  : ldg(in.policy_eps + (size_t)s * B + i);
+            policy_bid(T.drs + PV[s][0] * T.drs_stride + 4, estv[s], valv[s], eps, T.tab, g, pr);
             gmv[s] = g;
             prv[s] = pr;
             bidv[s] = bidv[s] * g;
@@ -1316,7 +1526,9 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
               reinterpret_cast<double *>(slots)[t] = estv[s];
               reinterpret_cast<double *>(slots)[64 + t] = valv[s];
               reinterpret_cast<int32_t *>(slots + 1024)[t] = PV[s][0];
-              reinterpret_cast<float *>(slots + 1280)[t] = ldg(in.policy_eps + (size_t)s * B + i);
+              reinterpret_cast<float *>(slots + 1280)[t] =
+                  GEN ? gen_normal1(gk.c0, gk.c1, 0, 16u + (uint32_t)s, gk.k0, gk.k1)
+                      : ldg(in.policy_eps + (size_t)s * B + i);
             }
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1395,8 +1607,8 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
         ag[s] = PV[s][q];
         tj[s] = AG_PREFETCH ? kTsjLoad : jv[s][q];
       }
-      resolve<PA, D, PRUNE, GENERAL>(T, K, prm.mech, x, xf, xabs, ag, UV[q], in, B, i + q,
-                                    prm.ts_sample != 0, tj, r[q]);
+      resolve<PA, D, PRUNE, GENERAL, GEN, DOS>(T, K, prm.mech, x, xf, xabs, ag, UV[q], in, B, i + q,
+                                              prm.ts_sample != 0, tj, r[q], gk);
     }
 
     // SoA stores, W auctions per access

@@ -258,10 +258,14 @@ __global__ __launch_bounds__(kThreads) void k_oracle(OraParams prm) {
 #endif
 #if AG_ORA_QUEUE
   // wave w of block b claims from counter q = (4 b + w) mod 64; the k-th claim of counter q is
-  // the 256-auction chunk 64 k + q, resolved as 4 tiles of 64. Lane 0 claims the chunk after
-  // next while the current one resolves; the ticket is read only once that chunk is done.
-  // At most lane_tiles / 4 claims per wave; tickets only grow, so a claim left in flight at
-  // the exit is past the end too.
+  // the chunk 64 k + q of q_len = 64 * AG_ORA_QUEUE_SUB auctions, resolved as AG_ORA_QUEUE_SUB
+  // tiles of 64 (one auction per lane per tile). Lane 0 claims the chunk after next while the
+  // current one resolves; the ticket is read only once that chunk is done. A wave makes at most
+  // lane_tiles / AG_ORA_QUEUE_SUB claims, so each lane resolves at most claims * SUB <= lane_tiles
+  // = ora_lane_cap(R) auctions: the range that keeps its exact 8-bit count fields and replica sums
+  // in range. The host sizes a launch to half of what the grid's waves may take and launches at
+  // least one wave per counter the chunks reach (simulate_oracle), so every chunk finds a wave
+  // below its cap. Tickets only grow, so a claim left in flight at the exit is past the end too.
   (void)stride;
   const uint32_t q_lane = tid & 63;
   const uint32_t q_idx = ((uint32_t)blockIdx.x * (kThreads / 64) + (uint32_t)(tid >> 6)) & 63u;

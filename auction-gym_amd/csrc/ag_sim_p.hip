@@ -38,6 +38,7 @@ SimKernel pick_d(int D) {
 // P = 0: the runtime-P kernel (more than kMaxP participants), one auction per lane.
 template <>
 SimKernel pick_kernel_for<0>(int D, bool prune, int W, int general, int bt) {
+  if (general & kGenGen) return nullptr;  // no generate-mode build of the runtime-P kernel
   general &= ~kGenShip;  // no shipped-shape build of the runtime-P kernel
   if (W != 1 || bt != kThreads || D > 8) return nullptr;
   if (general) return prune ? pick_d<0, true, 1, kGenAll>(D) : pick_d<0, false, 1, kGenAll>(D);
@@ -51,7 +52,17 @@ template <>
 SimKernel pick_kernel_for<AG_P>(int D, bool prune, int W, int general, int bt) {
   constexpr int P = AG_P;
   const bool ship = (general & kGenShip) != 0;
-  general &= ~kGenShip;
+  const bool genm = (general & kGenGen) != 0;
+  general &= ~(kGenShip | kGenGen);
+  if (genm) {  // generate mode (k_simulate<..., GEN>): the shipped shape's builds only
+    if (!general || !ship || !prune || D != 6 || W != 1) return nullptr;
+    if (bt == kLargeThreads) return k_simulate<P, 6, true, 1, kGenAll, kLargeThreads, kShipDo, true>;
+    if constexpr (P >= AG_STREAM_MIN_P)
+      if (bt == kMidThreads && general == kGenAll) return k_simulate<P, 6, true, 1, kGenAll, kMidThreads, kShipDo, true>;
+    if (bt != kThreads) return nullptr;
+    if (general == kGenTruthful) return k_simulate<P, 6, true, 1, kGenTruthful, kThreads, kShipDo, true>;
+    return k_simulate<P, 6, true, 1, kGenAll, kThreads, kShipDo, true>;
+  }
   if (general && ship && prune && D == 6) {  // the shipped shape: LR-TS width 5 compile-time
     if (bt == kLargeThreads) return k_simulate<P, 6, true, 1, kGenAll, kLargeThreads, kShipDo>;
     if constexpr (P >= AG_STREAM_MIN_P)  // the full mix at P >= 3: streamed, 768 lanes

@@ -286,6 +286,35 @@ def timed_steps(step, steps, warmup, world, stream):
     return elapsed, kern_ms
 
 
+def generate_mode_line(eng, seed, lo, out, cnt, B, steps, warmup, world, stream, write_bytes, what):
+    """SURVEY 8d's generate mode for a population line: the same step with every input drawn
+    inside the kernel (ag_simulate_generated -> k_simulate<..., GEN>: contexts, participants,
+    uniforms, the LR-TS agents' Thompson noise, the fitted policies' rsample draws -- the bits
+    ag_generate + ag_generate_noise store for the HBM-resident line, so the outputs are
+    identical); only the outputs touch HBM. Roofline: the writes against the HBM peak."""
+    from auctiongym_amd.sharding import allreduce_counters
+
+    def gstep(ev):
+        cnt.zero_()
+        if ev is not None:
+            ev[0].record(stream)
+        eng.simulate_generated(seed, lo, out, cnt)
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:
+            allreduce_counters(cnt)
+
+    elapsed, kern_ms = timed_steps(gstep, steps, warmup, world, stream)
+    ach = write_bytes * B / (kern_ms * 1e-3) / 1e9
+    return {"workload": what + " in generate mode: every input drawn on the chip (Philox4x32-10; the bits the "
+                               "HBM-resident line reads, outputs identical)",
+            "value": B * world * steps / elapsed, "unit": "auctions/s", "ms_per_step": elapsed / steps * 1e3,
+            "kernel_ms": kern_ms, "algorithmic_bytes_per_auction": write_bytes,
+            "roofline": {"bound": "VALU (Philox4x32-10: 15 calls per LR-TS participant for its 60 Thompson "
+                                  "normals) -- the writes' HBM roofline below",
+                         "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS}}
+
+
 def gpu_record_epochs(counts, epochs, ms):
     """Records x epochs (every fit's epochs summed) per second of a GPU update."""
     work = sum(int(n) * int(np.sum(e)) for n, e in zip(counts, epochs))
@@ -351,6 +380,11 @@ def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True, cpu_thread
 
     elapsed, kern_ms = timed_steps(step, steps, warmup, world, stream)
     bpa = algorithmic_bytes_ts(E, P, K, Do)
+    gen = None
+    if GENERATE_LINES:
+        wb = bpa - (8 * E + 4 * P + 8) - P * K * Do * 4  # the writes alone
+        gen = generate_mode_line(eng, 0, dims["lo"], out, cnt, B, steps, warmup, world, stream, wb,
+                                 f"SP_Truthful_TS (configs[1]), P={P}")
     traffic = traffic_src = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tfile):
@@ -366,6 +400,8 @@ def run_sp_ts(B, steps, warmup, world, rank, local, with_update=True, cpu_thread
            "roofline": {"bound": "hbm", "achieved": bpa * B / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": bpa * B / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                         "traffic": traffic, "traffic_source": traffic_src}}
+    if gen is not None:
+        res["generate_mode"] = gen
     if cpu_threads:
         rate, dt, passes, same = cpu_baseline_population(eng, items, values, inp, out, np.ones(N, np.int32),
                                                          np.zeros(N, np.int32), None, None, 1 << 15, cpu_threads)
@@ -525,6 +561,7 @@ def population_first_iteration(key, local, P=2, batch=None, world=1, rank=0):
 
 
 LEARNER_PARALLEL = "auto"  # --learner-parallel: multi-GPU learning-bidder updates
+GENERATE_LINES = True  # --no-generate: no generate-mode lines
 
 
 def population_update(eng, inp, out, B, lo, ak, bk, world):
@@ -660,6 +697,10 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
 
     elapsed, kern_ms = timed_steps(step, steps, warmup, world, stream)
     bpa = algorithmic_bytes_population(E, P, K, Do, ak, bk, init, compact)
+    if GENERATE_LINES:
+        wb = 4 + 8 + 8 + P * (4 + 8 * 6)  # the writes alone (algorithmic_bytes_population's)
+        res["generate_mode"] = generate_mode_line(eng, 1, lo, out, cnt, B, steps, warmup, world, stream, wb,
+                                                  what.split(":")[0])
     traffic = traffic_src = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tfile):
@@ -695,7 +736,7 @@ def main():
                     help="auctions per GPU per step (2^27: 19 GB of inputs + outputs resident in HBM; a "
                          "step of ~3.5 ms keeps the driver's few warm-up steps past the clock ramp of a "
                          "fresh process, DESIGN.md section 6)")
-    ap.add_argument("--no-generate", action="store_true", help="skip the generate-mode line")
+    ap.add_argument("--no-generate", action="store_true", help="skip the generate-mode lines")
     ap.add_argument("--peak-last", action="store_true",
                     help="measure the copy peak after the timed steps (A/B of the clock warm-up; default: before)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 24)
@@ -720,8 +761,9 @@ def main():
                          "(shards, counter all-reduce, agent-parallel updates) where only one GPU is at hand; "
                          "its timings mean nothing")
     args = ap.parse_args()
-    global LEARNER_PARALLEL
+    global LEARNER_PARALLEL, GENERATE_LINES
     LEARNER_PARALLEL = args.learner_parallel
+    GENERATE_LINES = not args.no_generate
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

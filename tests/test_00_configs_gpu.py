@@ -65,7 +65,23 @@ def test_configs_1_sp_truthful_ts_full_size(gpu, oracle, P):
     for k in out:
         assert torch.equal(out[k], out2[k]), k
     assert torch.equal(cnt, cnt2)
+    # the bench's generate-mode line: every draw inside the kernel, the same bits
+    _same_generated(eng, 0, dims["lo"], out, cnt, B)
     eng.close()
+
+
+def _same_generated(eng, seed, first, out, cnt, B):
+    """ag_simulate_generated(seed, first) == the HBM-resident batch's outputs and counters."""
+    import torch
+    out_g, cnt_g = eng.alloc_outputs(B, packed=True), eng.new_counters()
+    eng.simulate_generated(seed, first, out_g, cnt_g)
+    torch.cuda.synchronize()
+    from auctiongym_amd.engine import unpack_outputs
+    a, b = unpack_outputs(out), unpack_outputs(out_g)
+    for k in b:
+        if k in a:
+            assert np.array_equal(a[k].cpu().numpy(), b[k].cpu().numpy(), equal_nan=True), ("generated", k)
+    assert torch.equal(cnt, cnt_g), ("generated", "counters")
 
 
 @pytest.mark.parametrize("key,P,update", [("configs_2", 2, True), ("configs_3", 2, True),
@@ -102,6 +118,8 @@ def test_population_configs_full_size(gpu, oracle, key, P, update):
     torch.cuda.synchronize()
     orc = _oracle_on(eng, dims, inp, st_fit, init, B)
     _compare(out, cnt, orc, f"{key} P={P} fitted")
+    # the bench's generate-mode line (population_fitted_inputs draws with seed 1)
+    _same_generated(eng, 1, lo, out, cnt, B)
     eng.close()
 
 

@@ -321,6 +321,88 @@ def test_generate_mode_equals_hbm_inputs(gpu):
     eng.close()
 
 
+_GEN_POPS = {
+    # name: (N, mechanism, allocator kinds, bidder kinds, fitted policies)
+    "sp_truthful_ts": (8, 1, [1] * 8, [0] * 8, [0] * 8),                      # configs[1]
+    "fp_dr_ts": (3, 0, [1] * 3, [4] * 3, [1] * 3),                            # configs[3], fitted
+    "fp_dm_ts": (3, 0, [1] * 3, [2] * 3, [1] * 3),                            # configs[2], fitted
+    # 32 agents: Oracle / LR-TS allocators x Truthful, EmpiricalShaded, uninitialised and fitted
+    # learners (Gaussian shading draws, rsample draws)
+    "mix": (32, 0, [i % 2 for i in range(32)], [(0, 1, 2, 4, 4, 3, 0, 2)[i % 8] for i in range(32)],
+            [1 if i % 8 in (3, 5) else 0 for i in range(32)]),
+}
+
+
+@pytest.mark.parametrize("pop,P,B,cap", [("sp_truthful_ts", 2, (1 << 18) + 37, 0), ("sp_truthful_ts", 8, 70001, 0),
+                                         ("fp_dr_ts", 2, (1 << 18) + 3, 65536), ("fp_dm_ts", 2, 50000, 0),
+                                         ("mix", 2, (1 << 17) + 11, 0), ("mix", 8, 40000, 9000)])
+def test_generate_mode_general_equals_hbm_inputs(gpu, pop, P, B, cap):
+    """Generate mode for general populations (ag_simulate_generated ->
+    k_simulate<..., GEN>): contexts, participants, uniforms, the LR-TS agents' Thompson noise
+    (torch.normal(0, 1/sqrt(q)), src/Models.py:31), the fitted policies' rsample draws and the
+    shading draws made inside the kernel equal ag_generate + ag_generate_noise + ag_simulate bit
+    for bit -- every output and the exact counters -- for the TruthfulBidder build (P = 2 and the
+    streamed P = 8), the full build in 256-, 1024- and (P = 8) 768-lane workgroups, ragged
+    batches, several launches per batch, a nonzero first auction index."""
+    import torch
+    from auctiongym_amd.engine import AuctionEngine
+    N, mech, ak, bk, init = _GEN_POPS[pop]
+    K, E, OE = 12, 5, 4
+    ak, bk, init = (np.asarray(v, np.int32) for v in (ak, bk, init))
+    g = np.random.default_rng(71 + P)
+    items = np.concatenate([g.normal(0, 1, (N, K, E)), -3.0 - g.random((N, K, 1))], axis=2)
+    values = g.lognormal(0.1, 0.2, (N, K))
+    eng = AuctionEngine(N, P, K, E, OE, mech, 1.0)
+    eng.set_agent_params(ak, bk, 0.5 + 0.5 * g.random(N), 0.01 + 0.05 * g.random(N))
+    eng.load_catalog(items, values)
+    eng.load_lrts(g.normal(0, 1, (N, K, OE + 1)).astype(np.float32),
+                  (0.5 + 3.0 * g.random((N, K, OE + 1))).astype(np.float32), thompson_sampling=True)
+    if (bk >= 2).any():
+        eng.set_dr_state(g.normal(0, 0.7, (N, 16)).astype(np.float32), init)
+    eng.set_launch_auctions(cap)
+    first = 98765432109
+    inp = eng.alloc_inputs(B)
+    eng.generate(11, first, inp)
+    eng.generate_noise(11, first, inp)
+    out, cnt = eng.alloc_outputs(B), eng.new_counters()
+    eng.simulate(inp, out, cnt)
+    out_g, cnt_g = eng.alloc_outputs(B), eng.new_counters()
+    eng.simulate_generated(11, first, out_g, cnt_g)
+    torch.cuda.synchronize()
+    for k in out:
+        assert np.array_equal(out[k].cpu().numpy(), out_g[k].cpu().numpy(), equal_nan=True), k
+    assert torch.equal(cnt, cnt_g)
+    if pop == "mix":  # the generated draws are the stored ones: N(0, 1/q) noise, N(pg, sigma) shading
+        assert np.isfinite(out_g["gamma"].cpu().numpy()[:, :1000][bk[inp["part"][:, :1000].cpu().numpy()] != 0]).all()
+    eng.close()
+
+
+def test_generate_mode_general_refusals(gpu):
+    """Generate mode refuses, loudly, what it does not draw: ValueLearningBidder 'search' grids,
+    and general populations outside the shipped shape (E = 5, OE = 4)."""
+    from auctiongym_amd import _lib
+    from auctiongym_amd.engine import AuctionEngine
+    g = np.random.default_rng(3)
+    eng = AuctionEngine(3, 2, 12, 5, 4, 0, 1.0)
+    eng.set_agent_params(np.ones(3, np.int32), np.full(3, 2, np.int32), np.ones(3), np.full(3, 0.02))
+    eng.load_catalog(np.concatenate([g.normal(0, 1, (3, 12, 5)), -3.0 - g.random((3, 12, 1))], axis=2),
+                     g.lognormal(0.1, 0.2, (3, 12)))
+    eng.load_lrts(g.normal(0, 1, (3, 12, 5)).astype(np.float32), np.ones((3, 12, 5), np.float32))
+    eng.set_dr_state(g.normal(0, 0.7, (3, 16)).astype(np.float32), np.full(3, _lib.LEARNER_SEARCH, np.int32))
+    eng.set_bidder_modes(np.full(3, _lib.VL_SEARCH, np.int32))
+    with pytest.raises(NotImplementedError, match="search"):
+        eng.simulate_generated(0, 0, eng.alloc_outputs(64))
+    eng.close()
+    eng = AuctionEngine(4, 2, 12, 3, 2, 0, 1.0)  # E = 3: no shipped-shape build
+    eng.set_agent_params(np.ones(4, np.int32), np.zeros(4, np.int32))
+    eng.load_catalog(np.concatenate([g.normal(0, 1, (4, 12, 3)), -3.0 - g.random((4, 12, 1))], axis=2),
+                     g.lognormal(0.1, 0.2, (4, 12)))
+    eng.load_lrts(g.normal(0, 1, (4, 12, 3)).astype(np.float32), np.ones((4, 12, 3), np.float32))
+    with pytest.raises(NotImplementedError, match="shipped shape"):
+        eng.simulate_generated(0, 0, eng.alloc_outputs(64))
+    eng.close()
+
+
 def test_stale_binding_is_refused(gpu):
     """A caller compiled against another layout of the ABI structs (here the 3-field
     ag_batch_in of ABI 14) is refused with AG_ERR_INVALID before any field is used."""

@@ -237,6 +237,81 @@ def test_lrts_rp_equals_persistent_trainer(gpu, shards):
         eng.close()
 
 
+@pytest.mark.parametrize("agent,first", [(2, 3), (4, 37)])
+def test_lrts_rp_odd_polls_one_agent_mask(gpu, agent, first):
+    """One agent in the mask, polled after an odd number of launches (`first`, then 37 at a
+    time): ag_lrts_rp_poll reads the state of the launch parity it is at (k_lrts_rp_init writes
+    both parities, so a poll before the first even launch sees a started fit), the update
+    terminates, and the agent ends with the persistent trainer's m, q, prev_m and epochs bit for
+    bit; the agents outside the mask are left as they were."""
+    ref, ref_st, parts = _lrts_setup(1)
+    ep = ref.lrts_update(ref_st)
+    want = ref.lrts_state()
+    ref.close()
+    (eng, st), = parts
+    before = eng.lrts_state()
+    mask = np.zeros(6, np.int32)
+    mask[agent] = 1
+    eng.lrts_rp_begin(st, agents=mask)
+    launches, polls = 0, 0
+    n = first
+    while True:
+        eng.lrts_rp_epoch(n)
+        launches += n
+        polls += 1
+        left = eng.lrts_rp_poll()
+        assert left in (0, 1)
+        if left == 0:
+            break
+        assert launches < 20000, "the masked fit never finished"
+        n = 37
+    assert polls >= 2  # polled at odd launch counts (first, first + 74, ...) while the fit ran
+    ep2 = eng.lrts_rp_end()
+    assert ep2[agent] == ep[agent]
+    got = eng.lrts_state()
+    for x, y, b in zip(got, want, before):
+        assert np.array_equal(x[agent], y[agent])
+        others = np.arange(6) != agent
+        assert np.array_equal(x[others], b[others])
+    eng.close()
+
+
+def test_rp_graph_block_equals_eager(gpu):
+    """sharding.rp_epoch_blocks with graph=True (each block of launches + exchanges captured once
+    in a hipGraph and replayed) against the eager loop and the launches issued from C, with a
+    same-size device copy standing in for the all-reduce (one process): the same epochs and
+    the same posteriors, bit for bit (LR-TS), and the same models (learning bidders)."""
+    import torch
+    from auctiongym_amd.sharding import bidder_update_record_parallel, lrts_update_record_parallel
+    runs = []
+    for mode in ("c", "eager", "graph"):
+        ref, ref_st, parts = _lrts_setup(1)
+        ref.close()
+        (eng, st), = parts
+        if mode == "c":
+            ep = lrts_update_record_parallel(eng, st, range(6))
+        else:
+            ep = lrts_update_record_parallel(eng, st, range(6), poll=16, exchange=lambda t: t.copy_(t.clone()),
+                                             graph=(mode == "graph"))
+        torch.cuda.synchronize()
+        runs.append((ep,) + tuple(eng.lrts_state()))
+        eng.close()
+    for r in runs[1:]:
+        for x, y in zip(r, runs[0]):
+            assert np.array_equal(x, y)
+    bk, modes, state0, recs, _ = _kat_learners(SPECS)
+    res = []
+    for mode in ("eager", "graph"):
+        eng = _engine(bk, modes, state0)
+        st = _learner_store(eng, recs)
+        ep, stat = bidder_update_record_parallel(eng, st, range(len(SPECS)), poll=16,
+                                                 exchange=lambda t: t.copy_(t.clone()), graph=(mode == "graph"))
+        res.append((ep, stat) + tuple(eng.dr_state()))
+        eng.close()
+    for x, y in zip(*res):
+        assert np.array_equal(x, y)
+
+
 # ---- the pipelined persistent launches (k_bidder_pipe: ag_bidder_update's exact-sum
 # learners, ag_bidder_rp_run) ----
 def _trained(eng):

@@ -51,6 +51,15 @@ def main():
         calls["n"] += launches
         return orig_l(launches)
     eng.bidder_rp_epoch, eng.lrts_rp_epoch = count_b, count_l
+    # graph mode: the wrapped calls run once, at capture (no launch); each replay of a block runs
+    # `poll` launches -- so launches = blocks replayed x poll (rp_epoch_blocks returns the blocks)
+    blocks = {"n": 0}
+    orig_blocks = sharding.rp_epoch_blocks
+
+    def count_blocks(*a, **k):
+        blocks["n"] = orig_blocks(*a, **k)
+        return blocks["n"]
+    sharding.rp_epoch_blocks = count_blocks
 
     res = {}
     for what_ in ("bidders", "lrts"):
@@ -65,7 +74,7 @@ def main():
                     scratch = torch.empty_like(t)
                 scratch.copy_(t)
             kw = {} if mode == "from C" else {"exchange": copy, "graph": mode == "graph"}
-            calls["n"] = 0
+            calls["n"] = blocks["n"] = 0
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             if what_ == "bidders":
@@ -76,6 +85,8 @@ def main():
                 result = (np.asarray(ep).copy(), eng.lrts_state()[0].copy())
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
+            if mode == "graph":
+                calls["n"] = blocks["n"] * sharding.RP_POLL_LAUNCHES
             key = (what_, mode)
             if key in res:
                 assert all(np.array_equal(a, b) for a, b in zip(res[key][2], result)), key
