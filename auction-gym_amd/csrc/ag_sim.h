@@ -68,6 +68,9 @@ namespace ag {
 #ifndef AG_MAX_REPLICAS
 #define AG_MAX_REPLICAS 16
 #endif
+#ifndef AG_ABLATE
+#define AG_ABLATE 0  // diagnostic ablations of the general kernel (see kAblate below)
+#endif
 #ifndef AG_TS_DMA
 #define AG_TS_DMA 0  // replayed Thompson noise streamed into a per-wave LDS ring by LDS-DMA (A/B)
 #endif
@@ -619,6 +622,13 @@ constexpr int kGenGen = 16;  // pick_kernel_for: OR-ed into `general` for the ge
 // search: no gain / scratch spills, profiles/r05m_ab_pre.log, r05n_ab_nt.log.)
 template <int DW>
 __device__ __forceinline__ void ts_load_group(const TsSrc &src, int k0, int K, int Do, float (&nzv)[kTsGroup][DW]) {
+  if constexpr ((AG_ABLATE & 64) != 0) {  // ablation: the noise not read (a lane-dependent constant)
+#pragma unroll
+    for (int g = 0; g < kTsGroup; ++g)
+#pragma unroll
+      for (int d = 0; d < DW; ++d) nzv[g][d] = src.nz ? 1e-3f * (float)((threadIdx.x + g * 7 + d) & 15) : 0.0f;
+    return;
+  }
   const float *nz = src.nz;
 #pragma unroll
   for (int g = 0; g < kTsGroup; ++g)
@@ -845,7 +855,7 @@ struct SlotResult {
 // Diagnostic ablations of the general kernel (WRONG results; make variant-p VFLAGS=-DAG_ABLATE=..):
 // 1 no fitted-policy forward (gamma 1), 2 no Thompson item choice (the true-CTR leader),
 // 4 no exact true-CTR item search (item 0, CTR 0.5), 16 no MAP estimate (0.5), 32 no re-scored
-// true CTR of the Thompson choice (the leader's)
+// true CTR of the Thompson choice (the leader's), 64 the Thompson choice computed but its noise not read
 #ifndef AG_ABLATE
 #define AG_ABLATE 0
 #endif

@@ -473,7 +473,14 @@ POPULATIONS = {
                   [("Oracle", 11, ORACLE_A, "TruthfulBidder", {}), ("TS", 11, LRTS, "TruthfulBidder", {}),
                    ("DR", 10, LRTS, "DoublyRobustBidder", {"gamma_sigma": 0.02, "init_gamma": 1.0})],
                   1 << 21, "mixed"),
+    # not a BASELINE config (run with --populations fp_ips_ts): FP_IPS_TS.json's population, whose
+    # PolicyLearningBidder (PPO) fits stay agent-parallel over ranks
+    "fp_ips_ts": ("FP_IPS_TS (config/FP_IPS_TS.json): 3 LR-TS allocators + PolicyLearningBidder(PPO), FirstPrice; "
+                  "512k auctions per GPU",
+                  [("IPS", 3, LRTS, "PolicyLearningBidder", {"gamma_sigma": 0.02, "init_gamma": 1.0, "loss": "PPO"})],
+                  1 << 19, "ips"),
 }
+DEFAULT_POPULATIONS = "configs_2,configs_3,configs_4"
 
 
 def algorithmic_bytes_population(E, P, K, Do, ak, bk, init, compact=False):
@@ -506,12 +513,12 @@ def build_population(key, local, P=2):
     E, OE = D - 1, 4
     Do = OE + 1
     ak, bk, modes = [], [], []
-    kinds = {"TruthfulBidder": 0, "ValueLearningBidder": 2, "DoublyRobustBidder": 4}
+    kinds = {"TruthfulBidder": 0, "ValueLearningBidder": 2, "PolicyLearningBidder": 3, "DoublyRobustBidder": 4}
     for _, copies, alloc, bidder, kw in groups:
         for _ in range(copies):
             ak.append(1 if alloc == LRTS else 0)
             bk.append(kinds[bidder])
-            modes.append(_lib.VL_POLICY if kw.get("inference") == "policy" else 0)
+            modes.append(_lib.VL_POLICY if kw.get("inference") == "policy" else _lib.PL_LOSSES.get(kw.get("loss"), 0))
     ak, bk, modes = np.array(ak, np.int32), np.array(bk, np.int32), np.array(modes, np.int32)
     eng = AuctionEngine(N, P, K, E, OE, _lib.FIRST_PRICE, 1.0, device=local)
     eng.set_agent_params(ak, bk, np.ones(N), np.full(N, 0.02))
@@ -657,8 +664,8 @@ def run_population(key, steps, warmup, world, rank, local, batch=None, with_upda
         n_sh = int(sst["count"][0])
         rec_counts = np.bincount(sst["agent"][:n_sh].cpu().numpy(), minlength=N)
         res["agent_update"]["bidder_record_epochs_per_s"] = gpu_record_epochs(rec_counts[learners], ep[learners], ms[1])
-        if cpu_threads and len(learners):
-            kind = "dr" if bk[learners[0]] == 4 else "vl"
+        kind = {4: "dr", 2: "vl"}.get(int(bk[learners[0]])) if len(learners) else None
+        if cpu_threads and kind:
             rate, dt, n_s, ep_s = cpu_baseline_bidder(sst, int(learners[0]), st16, kind)
             res["agent_update"]["cpu_baseline"] = {
                 "value": rate, "unit": "record-epochs/s", "cores": 1, "kind": "port",
@@ -751,7 +758,7 @@ def main():
                     help="of configs_1 / the populations, only the P = 8 lines (profiling passes)")
     ap.add_argument("--no-populations", action="store_true",
                     help="skip the configs[2..4] lines (FP_DM_TS, FP_DR_TS, mixed population)")
-    ap.add_argument("--populations", default=",".join(POPULATIONS),
+    ap.add_argument("--populations", default=DEFAULT_POPULATIONS,
                     help="comma-separated subset of the configs[2..4] lines to run")
     ap.add_argument("--learner-parallel", choices=("auto", "agent", "record"), default="auto",
                     help="N > 1: learning-bidder updates agent-parallel, record-parallel, or by the cost model "
@@ -803,7 +810,7 @@ def main():
 
     # the measured HBM peak (ag_stream_copy, ~40 ms of streaming) before the timed steps: it is
     # part of the line, and it brings a fresh process's clocks up before the W warm-up steps
-    # (a cold process ran the first 2^27-auction steps up to 10 % slower, tools/warm_probe.py)
+    # (a cold process ran the first 2^27-auction steps up to 10 % slower, tools/archive/warm_probe.py)
     peak_meas = None if args.peak_last else measured_copy_peak()
     stream = torch.cuda.current_stream()
     nev = args.steps

@@ -54,7 +54,7 @@ def main():
     cnt = base.new_counters()
     st = torch.cuda.current_stream()
     times = {n: [] for n in engs}
-    for _ in range(max(10, (150 << 24) // B)):  # past the clock ramp of a fresh process (tools/warm_probe.py)
+    for _ in range(max(10, (150 << 24) // B)):  # past the clock ramp of a fresh process (tools/archive/warm_probe.py)
         cnt.zero_()
         base.simulate(inp, out, cnt)
     for r in range(25):

@@ -38,7 +38,7 @@ def main():
     }
     times = {k: [] for k in variants}
     st = torch.cuda.current_stream()
-    for _ in range(150):  # past the clock ramp of a fresh process (tools/warm_probe.py)
+    for _ in range(150):  # past the clock ramp of a fresh process (tools/archive/warm_probe.py)
         eng.simulate(inp, out, cnt)
     for r in range(rounds):
         for name, (exact, fields, want_cnt, lanes) in variants.items():

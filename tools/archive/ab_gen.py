@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
 """Generate mode (ag_simulate_generated, the headline workload with its inputs drawn on the chip)
 at 4 / 5 / 6 workgroups per CU of the Oracle kernel's persistent grid, in one process; outputs
-checked equal. Diagnostic only.   python tools/ab_gen.py [B]"""
+checked equal. Diagnostic only.   python tools/archive/ab_gen.py [B]"""
 import os
 import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "auction-gym_amd"), ROOT]
 import torch  # noqa: E402
 

@@ -3,7 +3,7 @@
 workgroup) on configs[1]'s won samples (bench.build_sp_ts, one simulate step), in ONE process,
 interleaved; the posteriors must be bit-identical across splits. Diagnostic.
 
-    python tools/ab_lrts.py [chunk ...]     (0 = the default split)
+    python tools/archive/ab_lrts.py [chunk ...]     (0 = the default split)
 """
 import os
 import sys
@@ -11,7 +11,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "auction-gym_amd")]
 import torch  # noqa: E402
 

@@ -1,16 +1,16 @@
 #!/usr/bin/env python3
 """A/B of the two simulate kernels on the bench workload (SP_Oracle shape, 2^24 auctions):
 the dedicated k_oracle (default) vs the general k_simulate, interleaved in ONE process after
-the clock ramp (tools/warm_probe.py); HIP events on the launch stream. Diagnostic only.
+the clock ramp (tools/archive/warm_probe.py); HIP events on the launch stream. Diagnostic only.
 
-    python tools/ab_oracle.py [B]
+    python tools/archive/ab_oracle.py [B]
 """
 import os
 import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "auction-gym_amd"), ROOT]
 import torch  # noqa: E402
 

@@ -3,7 +3,7 @@
 # process (tools/ab_pop.py, outputs checked equal), then FETCH_SIZE / WRITE_SIZE of each build's
 # simulate kernel (each copied over the library in the GPU box's scratch tree, one rocprofv3
 # pass per counter). Variants: make variant-p VP=8 NAME=<v> VFLAGS=...
-#   TAG=r05z VARIANTS="base8 pk8" PMC="base8 pk8 abl2" bash tools/ab_p8.sh
+#   TAG=r05z VARIANTS="base8 pk8" PMC="base8 pk8 abl2" bash tools/archive/ab_p8.sh
 # KEY / POPARGS select another line, e.g. KEY=configs_4 POPARGS="--populations configs_4 --no-p8" (P = 2)
 set -u
 TAG=${TAG:-r05z}

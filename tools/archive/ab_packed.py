@@ -4,14 +4,14 @@ SP_Oracle shape, 2^27 auctions unless given): the same launch back to back in ON
 alternating, with the outputs checked equal bit for bit. Also the general kernel on
 SP_Truthful_TS (configs_1) when --pop is given. Diagnostic only.
 
-    python tools/ab_packed.py [B] [--pop]
+    python tools/archive/ab_packed.py [B] [--pop]
 """
 import os
 import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "auction-gym_amd"), ROOT]
 import torch  # noqa: E402
 

@@ -6,14 +6,14 @@ dropping the small streams (winner 4 B, outcome 1 B) raises GB/s, packing them p
 GB/s stays flat, the stream count is not what holds the kernel below the copy peak.
 Diagnostic only.
 
-    python tools/ab_streams.py [B]
+    python tools/archive/ab_streams.py [B]
 """
 import os
 import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "auction-gym_amd"), ROOT]
 import torch  # noqa: E402
 

@@ -1,7 +1,7 @@
 // coop_exit.hip -- the exit-time crash probe without torch: one hipLaunchCooperativeKernel
 // with /opt/rocm's HIP runtime, then exit. Under rocprofv3 --kernel-trace this exits
-// cleanly or not; tools/exit_probe.sh compares it with the torch-hosted probe.
-//   hipcc --offload-arch=gfx950 -O2 -o build/coop_exit tools/coop_exit.hip
+// cleanly or not; tools/archive/exit_probe.sh compares it with the torch-hosted probe.
+//   hipcc --offload-arch=gfx950 -O2 -o build/coop_exit tools/archive/coop_exit.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
 

@@ -1,6 +1,6 @@
 """Diagnostics: the drop-in driver vs a reference driver capture (tests/golden/<tag>_driver_kat.npz).
 Prints per iteration / agent how the revenue, utilities, fit epochs, parameters and the
-torch / numpy generator states compare. Usage: python tools/driver_compare.py dr|dm|ips"""
+torch / numpy generator states compare. Usage: python tools/archive/driver_compare.py dr|dm|ips"""
 import json
 import os
 import sys
@@ -9,7 +9,7 @@ import tempfile
 import numpy as np
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "auction-gym_amd"))
 import auctiongym_amd.main as M  # noqa: E402
 

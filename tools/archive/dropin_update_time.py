@@ -7,7 +7,7 @@ fed the reference's torch rsample draws window by window) -- timed per agent and
 The config is the reference's FP_DR_TS.json / FP_DM_TS.json as captured in tests/golden
 (*_driver_kat.npz "cfg"), rounds_per_iter set to 10000. One JSON line per iteration.
 
-    python tools/dropin_update_time.py [dr|dm] [iterations]
+    python tools/archive/dropin_update_time.py [dr|dm] [iterations]
 """
 import json
 import os
@@ -17,7 +17,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "auction-gym_amd"))
 
 import torch  # noqa: E402

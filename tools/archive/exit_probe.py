@@ -3,14 +3,14 @@
 several workgroups per agent, hipLaunchCooperativeKernel) or as a plain launch (chunk 0: one
 workgroup per agent), then a normal interpreter exit. /proc/self/maps is written at exit so
 the PCs of a crash trace (rocprofv3's signal handler prints them unsymbolised) can be mapped
-to their libraries.     python tools/exit_probe.py coop|plain OUTDIR
+to their libraries.     python tools/archive/exit_probe.py coop|plain OUTDIR
 """
 import atexit
 import os
 import shutil
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "auction-gym_amd"), os.path.join(ROOT, "tests")]
 mode, outdir = sys.argv[1], sys.argv[2]
 os.makedirs(outdir, exist_ok=True)

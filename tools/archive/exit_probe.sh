@@ -1,11 +1,11 @@
 #!/bin/bash
-# rocprofv3 kernel trace of tools/exit_probe.py, plain launch first, cooperative second.
+# rocprofv3 kernel trace of tools/archive/exit_probe.py, plain launch first, cooperative second.
 set -u
 OUT=gpurun_out/exit_probe
 mkdir -p $OUT
 export TMPDIR=/tmp
 for m in plain coop; do
-  timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$m -o run -- python tools/exit_probe.py $m $OUT > $OUT/$m.log 2>&1
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$m -o run -- python tools/archive/exit_probe.py $m $OUT > $OUT/$m.log 2>&1
   echo "$m rc=$?"
 done
 grep -h "^    @\|SIGSEGV\|PC:" $OUT/*.log | head -40

@@ -17,7 +17,7 @@ for s in ${STEPS:-smoke configs suite bench}; do
       step upd_pipe 600 $U &&
       step upd_pipe128 600 env AG_PIPE_RECS=128 $U &&
       step upd_pipe2048 600 env AG_PIPE_RECS=2048 $U ;;
-    dropin) step dropin_dr 600 python tools/dropin_update_time.py dr 2 && step dropin_dm 600 python tools/dropin_update_time.py dm 2 ;;
+    dropin) step dropin_dr 600 python tools/archive/dropin_update_time.py dr 2 && step dropin_dm 600 python tools/archive/dropin_update_time.py dm 2 ;;
     suite) step pytest_gpu 1200 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
     bench) step bench_driver 400 python bench.py --steps 20 --warmup 5 ;;
     bench_default) step bench_default 600 python bench.py ;;

@@ -3,7 +3,7 @@ workgroups) -- a small command for profiler checks."""
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "auction-gym_amd"), os.path.join(ROOT, "tests")]
 import test_gpu_parity as T  # noqa: E402
 

@@ -7,7 +7,7 @@ coefficient c at ((j/64)*60 + c)*64 + j%64 floats: a 32-pair chunk of a row is o
 their union per XCD (workgroups dispatched round-robin over 8 XCDs; or mapped XCD-aware). Prints
 line bytes over algorithmic bytes (240 B per pair).
 
-    python tools/noise_model.py
+    python tools/archive/noise_model.py
 """
 import numpy as np
 rng=np.random.default_rng(0)

@@ -1,13 +1,13 @@
 #!/bin/bash
-# Round-5 evidence passes (on the GPU box): HBM traffic (FETCH_SIZE / WRITE_SIZE, separate
+# Round-4 evidence passes (on the GPU box): HBM traffic (FETCH_SIZE / WRITE_SIZE, separate
 # passes) of the headline kernel and of the general kernel on every population line incl.
 # the P = 8 lines, the SQ passes (instruction mix, LDS bank conflicts, SALU) of the headline
 # and of configs_2 / configs_4, the driver-shaped bench line and the kernel-trace stats.
-# Usage: TAG=r05x bash tools/prof_r05.sh; then (here)
+# Usage: TAG=r04x bash tools/archive/prof_r04.sh; then (here)
+#   python tools/make_pmc_traffic.py gpurun_out/prof_<tag> <tag> > profiles/pmc_traffic.json
 #   python tools/summarize_pmc.py gpurun_out/prof_<tag> > profiles/<tag>_pmc_summary.json
-#   python tools/make_pmc_traffic.py profiles/<tag>_pmc_summary.json > profiles/pmc_traffic.json
 set -u
-TAG=${TAG:-r05x}
+TAG=${TAG:-r04p}
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -24,8 +24,8 @@ for s in ${STEPS:-bench head pops sq stats}; do
   case $s in
     bench) step bench_driver 400 python bench.py --steps 20 --warmup 5 ;;
     head)
-      pmc hd_fetch "$HK" FETCH_SIZE $HEAD && pmc hd_write "$HK" WRITE_SIZE $HEAD &&
-      pmc hd_sqA "$HK" "$SQA" $HEAD && pmc hd_sqB "$HK" "$SQB" $HEAD ;;
+      pmc fetch "$HK" FETCH_SIZE $HEAD && pmc write "$HK" WRITE_SIZE $HEAD &&
+      pmc sqA "$HK" "$SQA" $HEAD && pmc sqB "$HK" "$SQB" $HEAD ;;
     pops)
       pmc c1_fetch "$GK" FETCH_SIZE $(ts) && pmc c1_write "$GK" WRITE_SIZE $(ts) &&
       pmc c1p8_fetch "$GK" FETCH_SIZE $(ts "--p8-only") && pmc c1p8_write "$GK" WRITE_SIZE $(ts "--p8-only") &&
@@ -42,8 +42,7 @@ for s in ${STEPS:-bench head pops sq stats}; do
       pmc c1_sqA "$GK" "$SQA" $(ts) && pmc c1_sqB "$GK" "$SQB" $(ts) &&
       for c in 2 4; do
         pmc c${c}_sqA "$GK" "$SQA" $(pop configs_$c) && pmc c${c}_sqB "$GK" "$SQB" $(pop configs_$c) || exit 1
-      done &&
-      pmc c4p8_sqA "$GK" "$SQA" $(pop configs_4 --p8-only) && pmc c4p8_sqB "$GK" "$SQB" $(pop configs_4 --p8-only) ;;
+      done ;;
     trainer*)  # the learners' update kernels (configs_2); LAST in a call: rocprofv3 has faulted at
       # exit after cooperative kernels (r03s7), so its rc is reported, not acted on, and nothing follows
       T1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64"

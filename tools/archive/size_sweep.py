@@ -2,13 +2,13 @@
 """Fixed vs per-auction cost of the simulate path: ag_simulate of one population line
 (configs_1..4, as tools/ab_pop.py builds them) at several batch sizes, HIP-event medians;
 run under rocprofv3 --kernel-trace for the per-kernel split.
-    python tools/size_sweep.py configs_1 [fused|generic]"""
+    python tools/archive/size_sweep.py configs_1 [fused|generic]"""
 import os
 import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "auction-gym_amd"))
 sys.path.insert(0, ROOT)
 
