@@ -9,7 +9,7 @@ tools/make_pmc_traffic.py derives profiles/pmc_traffic.json.
     python tools/summarize_pmc.py gpurun_out/prof_<tag> [bench_driver.log]
 
 Pass directories are named <workload>_<pass>: workloads `hd` (the headline), c1, c2, c3, c4,
-c1p8, c4p8 (bench.py's configs_1 ... configs_4_p8 lines); passes fetch, write (FETCH_SIZE /
+c1p8, c4p8 (bench.py's configs_1 ... configs_4_p8 lines), c1g (configs_1's generate mode); passes fetch, write (FETCH_SIZE /
 WRITE_SIZE: separate runs), sqA, sqB. Batch and algorithmic bytes per auction come from the
 bench JSON line (given, or <dir>/bench_driver.log). The first dispatch of every kernel in a
 pass is dropped (the populations' iteration-0 launch runs uninitialised learners; the first
@@ -23,7 +23,7 @@ import re
 import sys
 
 WORKLOADS = {"hd": "headline", "c1": "configs_1", "c2": "configs_2", "c3": "configs_3", "c4": "configs_4",
-             "c1p8": "configs_1_p8", "c4p8": "configs_4_p8"}
+             "c1p8": "configs_1_p8", "c4p8": "configs_4_p8", "c1g": "configs_1.generate_mode"}
 
 
 def pmc_by_kernel(path, skip_first=True):
@@ -69,9 +69,12 @@ def workload_shape(bench, key):
         return None, None
     if key == "headline":
         return bench["config"]["auctions_per_gpu_per_step"], bench["roofline"]["algorithmic_bytes_per_auction"]
-    b = bench.get(key)
+    parent, _, sub = key.partition(".")
+    b = bench.get(parent)
     if b is None:
         return None, None
+    if sub:  # a generate-mode line: the parent line's batch, its own (write) bytes
+        return b["auctions_per_gpu_per_step"], b.get(sub, {}).get("algorithmic_bytes_per_auction")
     return b["auctions_per_gpu_per_step"], b["algorithmic_bytes_per_auction"]
 
 
@@ -104,7 +107,7 @@ def summarize(root, bench):
     groups = collections.defaultdict(lambda: collections.defaultdict(dict))  # wl -> kernel -> pass
     for d in sorted(os.listdir(root)):
         p = os.path.join(root, d)
-        m = re.match(r"(hd|c\dp8|c\d)_(.+)$", d)
+        m = re.match(r"(hd|c\dp8|c\dg|c\d)_(.+)$", d)
         if not os.path.isdir(p) or not m:
             continue
         for k, (v, n) in pmc_by_kernel(p).items():
