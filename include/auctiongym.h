@@ -291,10 +291,15 @@ int ag_simulate(ag_ctx *ctx, int64_t B, const ag_batch_in *in, ag_batch_out *out
                 int64_t *counters_fx, void *stream);
 
 /* Generate mode: B rounds of Auction.simulate_opportunity whose inputs are drawn on the chip
- * inside the simulate kernel, the same bits ag_generate(seed, first_auction, B) writes (so
- * the outputs equal ag_generate followed by ag_simulate); nothing but the catalogue is read
- * from HBM. OracleAllocator + TruthfulBidder populations whose catalogue values lie in
- * (0, 1024), P <= 8, E + 1 <= 8, K <= 16; otherwise AG_ERR_UNSUPPORTED. */
+ * inside the simulate kernel, the same bits ag_generate(seed, first_auction, B) -- and, for
+ * general populations, ag_generate_noise(seed, first_auction, B) -- write (so the outputs and
+ * counters equal ag_generate (+ ag_generate_noise) followed by ag_simulate); nothing but the
+ * catalogue and the agents' parameters is read from HBM. OracleAllocator + TruthfulBidder
+ * populations whose catalogue values lie in (0, 1024), P <= 8, E + 1 <= 8, K <= 16; general
+ * populations (LR-TS allocators: their Thompson noise; shading and learning bidders: their
+ * Gaussian or rsample draws) in the shipped shape -- E = 5, OE = 4, K <= 16, positive values,
+ * P <= 8 -- except ValueLearningBidders bidding by search (their grids are not drawn);
+ * otherwise AG_ERR_UNSUPPORTED. (Round 6: the general populations; ABI unchanged.) */
 int ag_simulate_generated(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B, ag_batch_out *out,
                           int64_t *counters_fx, void *stream);
 
@@ -307,9 +312,10 @@ int ag_generate(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B, d
 
 /* Synthetic per-participant noise for the participants `part` (dev [P][B]) of auctions
  * [first_auction, first_auction + B): gamma_raw [P][B] = prev_gamma + gamma_sigma * z for
- * shading bidders (NaN otherwise), ts_noise (tiled as in ag_batch_in) = z / sqrt(q) for
+ * shading bidders (NaN otherwise), ts_noise (tiled as in ag_batch_in) = z * (1 / sqrtf(q)) for
  * LR-TS agents (0 otherwise), policy_eps [P][B] = z for every slot; any output may be NULL.
- * Same Philox key / counter scheme. */
+ * Same Philox key / counter scheme; z are float32 Box-Muller normals from 32-bit uniforms, four
+ * per Philox call (round 6; before, one FP64 pair per call). */
 /* Synthetic search grids gamma_grid [P][128][B] (U(0.1, 1), Philox as ag_generate_noise,
  * unsorted: the search takes the smallest gamma among tied maxima) for every slot. */
 int ag_generate_search_grid(ag_ctx *ctx, uint64_t seed, uint64_t first_auction, int64_t B, double *gamma_grid,

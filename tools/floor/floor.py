@@ -109,8 +109,8 @@ def main():
             sus[k].append(a.elapsed_time(b) / 10)
     for k in runs:
         mi, ms = float(np.median(iso[k])), float(np.median(sus[k]))
-        print(f"{k:36s} isolated {mi:7.4f} ms ({141 * B / mi / 1e9:7.1f} GB/s)   back-to-back {ms:7.4f} ms "
-              f"({141 * B / ms / 1e9:7.1f} GB/s)")
+        print(f"{k:36s} isolated {mi:7.4f} ms ({141 * B / (mi * 1e-3) / 1e12:7.2f} TB/s)   back-to-back {ms:7.4f} ms "
+              f"({141 * B / (ms * 1e-3) / 1e12:7.2f} TB/s)")
 
 
 if __name__ == "__main__":
