@@ -583,8 +583,6 @@ int simulate_general(ag_ctx *c, int64_t B, const ag_batch_in *in, const ag_batch
     if (lds > 160 * 1024)
       return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu B of LDS (> 160 KiB)", lds);
   }
-  if (lds > 64 * 1024)
-    AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   // Persistent grid: exactly the blocks the device keeps resident (no partial last round),
   // each striding over bt-auction tiles.
   // (the WIDE A/B kernel has slots of its own: its occupancy is not the AUTO kernel's)
@@ -593,6 +591,15 @@ int simulate_general(ag_ctx *c, int64_t B, const ag_batch_in *in, const ag_batch
                                    (gmode == kGenTruthful ? 32 : 0) +
                                    (bt == kThreads ? 0 : 16) + (c->general ? 8 : 0) + (W == 2 ? 4 : 0) +
                                    (prune ? 2 : 0) + (prm.want_counters ? 1 : 0)];
+  if (res == 0) {  // first launch of this build: the kernel's static LDS (AG_TS_DMA's noise rings) on top
+    hipFuncAttributes fa;
+    AG_HIP(hipFuncGetAttributes(&fa, (const void *)k));
+    if (lds + fa.sharedSizeBytes > 160 * 1024)
+      return ag_set_error(AG_ERR_UNSUPPORTED, "ag_simulate: population needs %zu + %zu B of LDS (> 160 KiB)", lds,
+                          (size_t)fa.sharedSizeBytes);
+  }
+  if (lds > 64 * 1024)
+    AG_HIP(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   if (res == 0) {
     int per_cu = 0, cus = 0;
     AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k, bt, lds));

@@ -72,7 +72,9 @@ namespace ag {
 #define AG_ABLATE 0  // diagnostic ablations of the general kernel (see kAblate below)
 #endif
 #ifndef AG_TS_DMA
-#define AG_TS_DMA 0  // replayed Thompson noise streamed into a per-wave LDS ring by LDS-DMA (A/B)
+#define AG_TS_DMA 1  // replayed Thompson noise streamed into a per-wave LDS ring by LDS-DMA: the
+                     // 256-lane P <= 2 shipped-shape builds (configs_1/2/3: 2-5 % in one process,
+                     // profiles/r06i_ab_*.log); 0: the VGPR loads (A/B)
 #endif
 #ifndef AG_TS_DMA_AHEAD
 #define AG_TS_DMA_AHEAD 2  // ... items in flight ahead of the one being scored
@@ -681,11 +683,18 @@ __device__ __forceinline__ int ts_select(const float *m, const float (&xo)[DW], 
                          src.ring_lds + (uint32_t)(((k + kTsDmaAhead) % kTsDmaBufs) * 5 * 256));
           constexpr int kLast = KG - 1;
           const int later = (k + kTsDmaAhead < kLast ? k + kTsDmaAhead : kLast) - k;  // items issued after k
-          if (later == 2) wait_vm<10>();
-          else if (later == 1) wait_vm<5>();
-          else if (later == 0) wait_vm<0>();
-          else if (later == 3) wait_vm<15>();
-          else wait_vm<0>();
+          static_assert(kTsDmaAhead <= 8, "vmcnt counts up to 63: at most 8 items of 5 DMAs ahead");
+          switch (later) {  // a constant after unrolling
+            case 1: wait_vm<5>(); break;
+            case 2: wait_vm<10>(); break;
+            case 3: wait_vm<15>(); break;
+            case 4: wait_vm<20>(); break;
+            case 5: wait_vm<25>(); break;
+            case 6: wait_vm<30>(); break;
+            case 7: wait_vm<35>(); break;
+            case 8: wait_vm<40>(); break;
+            default: wait_vm<0>(); break;
+          }
           const float *row = src.ring + (k % kTsDmaBufs) * 5 * 64 + lane;
           float nzg[DW];
 #pragma unroll
@@ -1051,7 +1060,7 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
   int32_t *s_kag = reinterpret_cast<int32_t *>(smem + L.kag);
   float *s_tsr = reinterpret_cast<float *>(smem + L.tsr);
   // AG_TS_DMA: every wave's Thompson-noise ring (kTsDmaBufs items of 5 rows x 64 floats)
-  constexpr bool kDma = AG_TS_DMA && GENERAL && DOS == 5 && !GEN;
+  constexpr bool kDma = AG_TS_DMA && GENERAL && DOS == 5 && !GEN && BT == kThreads && P >= 1 && P <= 2;
   __shared__ __attribute__((aligned(16))) float s_ring[kDma ? (BT / 64) * kTsDmaBufs * 5 * 64 : 1];
   static_assert(!GEN || (DOS > 0 && P > 0 && W == 1 && GENERAL), "generate mode: shipped-shape general builds");
   unsigned long long *s_cnt = reinterpret_cast<unsigned long long *>(smem + L.cnt);
