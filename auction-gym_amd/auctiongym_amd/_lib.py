@@ -49,7 +49,7 @@ EXPORTS = ("ag_create", "ag_destroy", "ag_set_agent_kinds", "ag_set_agent_params
            "ag_abi_version", "ag_ts_noise_index", "ag_generate_ts_noise_compact", "ag_torch_normal_epochs",
            "ag_bidder_rp_begin", "ag_bidder_rp_epoch", "ag_bidder_rp_run", "ag_bidder_rp_noise", "ag_bidder_rp_poll", "ag_bidder_rp_end",
            "ag_lrts_rp_begin", "ag_lrts_rp_epoch", "ag_lrts_rp_poll", "ag_lrts_rp_end", "ag_empirical_update_agents",
-           "ag_coop_selftest")
+           "ag_coop_selftest", "ag_div_selftest")
 ABI_VERSION = 17
 LEARNER_UNINITIALISED, LEARNER_POLICY, LEARNER_SEARCH = 0, 1, 2
 VL_SEARCH, VL_POLICY = 0, 1
@@ -165,6 +165,7 @@ def load(path=None):
         "ag_exp": (ctypes.c_int, [vp, vp, i64, vp]),
         "ag_stream_copy": (ctypes.c_int, [vp, vp, i64, vp]),
         "ag_coop_selftest": (ctypes.c_int, [i32, i32, i32, i32, ctypes.POINTER(i64)]),
+        "ag_div_selftest": (ctypes.c_int, [i32, i64, u64, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
         "ag_estimate_ctr": (ctypes.c_int, [vp, i32, i64, vp, vp, vp, vp]),
         "ag_bid": (ctypes.c_int, [vp, i32, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "ag_replay_draw": (ctypes.c_int, [ctypes.POINTER(AgPcg64State), i64, i32, i32, i32, ctypes.c_double, i32,

@@ -27,6 +27,7 @@
 #include "ag_log1p.h"
 #include "ag_philox.h"
 #include "ag_coop.h"
+#include "ag_div.h"
 
 namespace {
 
@@ -37,6 +38,9 @@ constexpr int kDrThreads = 256;
 constexpr int kWrEpochs = 32768, kInitEpochs = 16384, kDrEpochs = 32768;
 constexpr int64_t kBidderChunk = 8192;  // records per workgroup of a PolicyLearningBidder (default)
 constexpr int64_t kMinChunk = 1024;     // fewest records per workgroup of an exact-sum learner's split
+#ifndef AG_DR_SHARED_DIV
+#define AG_DR_SHARED_DIV 1  // the win-rate row's two divisions by 1 + e share one reciprocal (ag_div.h)
+#endif
 #ifndef AG_DR_REC_LDS0
 #define AG_DR_REC_LDS0 (32 * 1024)
 #endif
@@ -89,6 +93,13 @@ __device__ __forceinline__ double fxv(int64_t hi, int64_t lo) {
 // softplus(u) = u > 20 ? u : log1p(exp(u)) and its derivative exp(u) / (exp(u) + 1), from
 // e = exp(u) (the forward pass keeps it for the backward pass)
 __device__ __forceinline__ double dsoftplus_e(double u, double e) { return u > 20.0 ? 1.0 : e / (e + 1.0); }
+// log1p_main's divisions for a caller that holds r = the reciprocal of its 1 + x (ag_div.h)
+struct SharedDiv {
+  double r;
+  __device__ double cu(double c, double u) const { return agdiv::div_core(c, u, r); }
+  __device__ double fs(double f, double d) const { return agdiv::div_core(f, d, agdiv::recip(d)); }
+};
+
 // exp(x) and softplus from the branch-free main paths (the same bits), the rare inputs
 // outside them patched with the full functions
 using agexp::exp_fast;
@@ -182,6 +193,7 @@ __device__ __forceinline__ bool stop_step(Stopper &s, int epoch, float loss) {
 // pass's softplus derivatives
 struct PolF {
   double h[2], s[2], am, as, mu, sp_sigma, sigma, eh[2], eam, eas;
+  double rh[2], ram, ras;  // policy_fwd_main only: the reciprocals of 1 + eh / eam / eas (ag_div.h)
 };
 __device__ __forceinline__ void policy_fwd(const float *p, double c, double v, PolF &f, const uint64_t *tab) {
 #pragma unroll
@@ -195,13 +207,30 @@ __device__ __forceinline__ void policy_fwd(const float *p, double c, double v, P
   f.sp_sigma = softplus_fast(f.as, f.eas, tab);
   f.sigma = f.sp_sigma + 0.01;  // min_sigma (src/Models.py:104)
 }
-// softplus through the main paths alone (ok cleared when an input leaves them)
-__device__ __forceinline__ double softplus_main(double u, double &e, const uint64_t *tab, bool &ok) {
+// softplus through the main paths alone (ok cleared when an input leaves them); r = the
+// reciprocal of 1 + e, shared by log1p's c / (1 + e) and the backward pass's e / (e + 1)
+// (AG_DR_SHARED_DIV; where ok holds and u <= 20, e is in [2^-29, 2^29]: div_safe's range)
+__device__ __forceinline__ double softplus_main(double u, double &e, double &r, const uint64_t *tab, bool &ok) {
   e = agexp::exp_main(u, tab);
   bool lok;
+#if AG_DR_SHARED_DIV
+  r = agdiv::recip(1.0 + e);
+  const double l = aglog1p::log1p_main_t(e, lok, SharedDiv{r});
+#else
+  r = 0.0;
   const double l = aglog1p::log1p_main(e, lok);
+#endif
   ok = (int)ok & (int)agexp::exp_in_main(u) & ((int)lok | (int)(u > 20.0));
   return u > 20.0 ? u : l;
+}
+// dsoftplus_e from softplus_main's reciprocal (the same bits where its ok holds)
+__device__ __forceinline__ double dsoftplus_r(double u, double e, double r) {
+#if AG_DR_SHARED_DIV
+  return u > 20.0 ? 1.0 : agdiv::div_core(e, e + 1.0, r);
+#else
+  (void)r;
+  return dsoftplus_e(u, e);
+#endif
 }
 // policy_fwd through the main paths alone: true when they gave policy_fwd's values (every
 // softplus input inside them), else the caller runs policy_fwd -- one rare branch per record
@@ -211,22 +240,23 @@ __device__ __forceinline__ bool policy_fwd_main(const float *p, double c, double
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     f.h[j] = c * (double)p[2 * j] + v * (double)p[2 * j + 1] + (double)p[4 + j];
-    f.s[j] = softplus_main(f.h[j], f.eh[j], tab, ok);
+    f.s[j] = softplus_main(f.h[j], f.eh[j], f.rh[j], tab, ok);
   }
   f.am = f.s[0] * (double)p[6] + f.s[1] * (double)p[7] + (double)p[8];
   f.as = f.s[0] * (double)p[9] + f.s[1] * (double)p[10] + (double)p[11];
-  f.mu = softplus_main(f.am, f.eam, tab, ok);
-  f.sp_sigma = softplus_main(f.as, f.eas, tab, ok);
+  f.mu = softplus_main(f.am, f.eam, f.ram, tab, ok);
+  f.sp_sigma = softplus_main(f.as, f.eas, f.ras, tab, ok);
   f.sigma = f.sp_sigma + 0.01;
   return ok;
 }
 __device__ __forceinline__ void policy_fwd_fast(const float *p, double c, double v, PolF &f, const uint64_t *tab) {
   if (__builtin_expect(!policy_fwd_main(p, c, v, f, tab), 0)) policy_fwd(p, c, v, f, tab);
 }
-// policy_bwd's twelve gradient terms as doubles (d[j]: parameter j), the same expressions
+// policy_bwd's twelve gradient terms as doubles (d[j]: parameter j), the same expressions,
+// from policy_fwd_main's values (used only where its ok holds)
 __device__ __forceinline__ void policy_terms(const float *p, double c, double v, const PolF &f, double dmu,
                                              double dsigma, double *d) {
-  const double dam = dmu * dsoftplus_e(f.am, f.eam), das = dsigma * dsoftplus_e(f.as, f.eas);
+  const double dam = dmu * dsoftplus_r(f.am, f.eam, f.ram), das = dsigma * dsoftplus_r(f.as, f.eas, f.ras);
   double ds[2];
   ds[0] = dam * (double)p[6] + das * (double)p[9];
   ds[1] = dam * (double)p[7] + das * (double)p[10];
@@ -238,7 +268,7 @@ __device__ __forceinline__ void policy_terms(const float *p, double c, double v,
   d[11] = das;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const double dh = ds[j] * dsoftplus_e(f.h[j], f.eh[j]);
+    const double dh = ds[j] * dsoftplus_r(f.h[j], f.eh[j], f.rh[j]);
     d[2 * j] = dh * c;
     d[2 * j + 1] = dh * v;
     d[4 + j] = dh;
@@ -506,9 +536,17 @@ __device__ __forceinline__ void wr_row(int64_t (&acc)[5], double c, double v, do
   const double a = __builtin_fabs(z);
   double e = agexp::exp_main(-a, tab);
   bool lok;
+  // p's division and log1p's c / u both divide by 1 + e: one reciprocal (ag_div.h; on the main
+  // paths e >= exp(-512), c is 0 or >= 2^-81 in magnitude, |f| >= 2^-53: div_safe's range)
+#if AG_DR_SHARED_DIV
+  const double d1 = 1.0 + e, r1 = agdiv::recip(d1);
+  double Lz = aglog1p::log1p_main_t(e, lok, SharedDiv{r1});
+  double pw = agdiv::div_core(z >= 0.0 ? 1.0 : e, d1, r1);
+#else
   double Lz = aglog1p::log1p_main(e, lok);
-  const double u = y > 0.0 ? -z : z;
   double pw = (z >= 0.0 ? 1.0 : e) / (1.0 + e);
+#endif
+  const double u = y > 0.0 ? -z : z;
   double t = fmin(u > 20.0 ? u : (u > 0.0 ? a + Lz : Lz), 100.0);
   double gz = pw - y;
   // |t| <= 100, |pw - y| <= 1, ctr in [0, 1]: those terms are far inside fxb's fast range;
@@ -687,12 +725,26 @@ __device__ __forceinline__ void dr_rec(int64_t (&acc)[16], const float *pol, con
   PolF f;
   bool ok = policy_fwd_main(pol, c, v, f, tab);
   const double mu = f.mu, sg = f.sigma;
+  const double p0 = (double)fmaxf(prop, 1e-15f);
+#if AG_DR_SHARED_DIV
+  // three divisions by sg, two by p0: one reciprocal each (ag_div.h; a record whose operands
+  // leave div_safe's range takes dr_rec_exact)
+  const double rsg = agdiv::recip(sg), rp0 = agdiv::recip(p0);
+  const double zz = agdiv::div_core(mu - g, sg, rsg);
+  const double xp = -(zz * zz) / 2.0;
+  const double ex = agexp::exp_main(xp, tab);
+  const double pdf_raw = agdiv::div_core(ex, sg, rsg) * inv_sqrt2pi;
+  const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
+  const double iw = agdiv::div_core(pi, p0, rp0);
+  ok = (int)ok & (int)agdiv::div_safe(mu - g, sg) & (int)agdiv::div_safe(ex, sg) & (int)agdiv::div_safe(pi, p0) &
+       (int)agdiv::div_safe(du, p0);
+#else
   const double zz = (mu - g) / sg;
   const double xp = -(zz * zz) / 2.0;
   const double pdf_raw = agexp::exp_main(xp, tab) / sg * inv_sqrt2pi;
   const double pi = pdf_raw < 1e-30 ? 1e-30 : pdf_raw;
-  const double p0 = (double)fmaxf(prop, 1e-15f);
   const double iw = pi / p0;
+#endif
   const double iwc = iw < 1.0 / 50.0 ? 1.0 / 50.0 : (iw > 50.0 ? 50.0 : iw);
   const double raw = mu + sg * ep;
   const double gs = raw < 0.0 ? 0.0 : (raw > 1.0 ? 1.0 : raw);
@@ -704,9 +756,15 @@ __device__ __forceinline__ void dr_rec(int64_t (&acc)[16], const float *pol, con
   d[12] = -(du * iwc + Wv * (V - V * gs));
   double dpi_dmu = 0.0, dpi_dsg = 0.0;
   if (pdf_raw >= 1e-30 && iw >= 1.0 / 50.0 && iw <= 50.0) {
+#if AG_DR_SHARED_DIV
+    const double k = agdiv::div_core(du, p0, rp0);
+    dpi_dmu = k * pdf_raw * (g - mu) / (sg * sg);
+    dpi_dsg = k * pdf_raw * ((g - mu) * (g - mu) / (sg * sg * sg) - agdiv::div_core(1.0, sg, rsg));
+#else
     const double k = du / p0;
     dpi_dmu = k * pdf_raw * (g - mu) / (sg * sg);
     dpi_dsg = k * pdf_raw * ((g - mu) * (g - mu) / (sg * sg * sg) - 1.0 / sg);
+#endif
   }
   double ddm = 0.0;
   if (raw >= 0.0 && raw <= 1.0) ddm = -Wv * V + (V - V * gs) * Wv * (1.0 - Wv) * (double)wr[2];

@@ -13,8 +13,10 @@
 
 #if defined(__HIPCC__)
 #define AG_L1P_HD __host__ __device__ __forceinline__
+#define AG_L1P_MEMBER __host__ __device__ __forceinline__
 #else
 #define AG_L1P_HD static inline
+#define AG_L1P_MEMBER inline
 #endif
 
 namespace aglog1p {
@@ -101,7 +103,15 @@ AG_L1P_HD double log1p(double x) {
 // bit for bit (IEEE subtraction is antisymmetric, adding +0 is exact). ok = false outside
 // that range and on log1p's hu == 0 special case (f on a power-of-two boundary): the caller
 // then takes log1p(x).
-AG_L1P_HD double log1p_main(double x, bool &ok) {
+// D: the two divisions, c / u (u = 1 + x) and f / (2 + f), as D::cu(c, u) and D::fs(f, d) --
+// IeeeDiv the plain operator; a device caller may pass its own (ag_dr.hip: a reciprocal of
+// 1 + x shared with its own division by 1 + x), which must give the same bits
+struct IeeeDiv {
+  AG_L1P_MEMBER double cu(double c, double u) const { return c / u; }
+  AG_L1P_MEMBER double fs(double f, double d) const { return f / d; }
+};
+template <class D>
+AG_L1P_HD double log1p_main_t(double x, bool &ok, const D &div) {
   const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
   const double Lp1 = 6.666666666666735130e-01, Lp2 = 3.999999999940941908e-01,
                Lp3 = 2.857142874366239149e-01, Lp4 = 2.222219843214978396e-01,
@@ -113,7 +123,7 @@ AG_L1P_HD double log1p_main(double x, bool &ok) {
   int32_t hu = (int32_t)(bits(u) >> 32);
   int32_t k = (hu >> 20) - 1023;
   double c = (k > 0) ? 1.0 - (u - x) : x - (u - 1.0);
-  c /= u;
+  c = div.cu(c, u);
   hu &= 0x000fffff;
   const uint64_t lo = bits(u) & 0xffffffffull;
   const bool low = hu < 0x6a09e;
@@ -127,9 +137,10 @@ AG_L1P_HD double log1p_main(double x, bool &ok) {
   hu = small ? 1 : hu;
   ok = hx >= 0x3e200000 && hx < 0x43400000 && hu != 0;
   const double hfsq = 0.5 * f * f;
-  const double s = f / (2.0 + f), z = s * s;
+  const double s = div.fs(f, 2.0 + f), z = s * s;
   const double R = z * (Lp1 + z * (Lp2 + z * (Lp3 + z * (Lp4 + z * (Lp5 + z * (Lp6 + z * Lp7))))));
   return k * ln2_hi - ((hfsq - (s * (hfsq + R) + (k * ln2_lo + c))) - f);
 }
+AG_L1P_HD double log1p_main(double x, bool &ok) { return log1p_main_t(x, ok, IeeeDiv()); }
 
 }  // namespace aglog1p

@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include "ag_coop.h"
+#include "ag_div.h"
 #include "ag_host.h"
 
 namespace {
@@ -73,7 +74,83 @@ __global__ __launch_bounds__(kStThreads) void k_coop_stress(unsigned *bars, int6
   if (nbad) atomicAdd(bad, nbad);
 }
 
+// ag_div.h's split division against the compiler's `a / b`, bit for bit, over operands in
+// div_safe's range: per thread `iters` pairs of three kinds -- anywhere in the range; the BCE
+// row's (1 or e) / (1 + e) and log1p's c / (1 + e) with e down to 2^-740; log1p's f / (2 + f)
+__device__ __forceinline__ uint64_t st_mix(uint64_t x) {
+  x ^= x >> 31;
+  x *= 0x7fb5d329728ea185ull;
+  x ^= x >> 27;
+  x *= 0x81dadef4bc2dd44dull;
+  x ^= x >> 33;
+  return x;
+}
+__device__ __forceinline__ double st_num(uint64_t h, int lo, int hi) {  // +-(1 + m) 2^k, k in [lo, hi)
+  const int k = lo + (int)((h >> 52) % (uint64_t)(hi - lo));
+  const double m = __builtin_bit_cast(double, 0x3ff0000000000000ull | (h & 0x000fffffffffffffull));
+  return __builtin_ldexp((h >> 63) ? -m : m, k);
+}
+__global__ __launch_bounds__(256) void k_div_stress(uint64_t seed, int iters, unsigned long long *bad,
+                                                    unsigned long long *tested) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long nbad = 0, n = 0;
+  for (int i = 0; i < iters; ++i) {
+    const uint64_t h1 = st_mix(seed ^ (t * 0x9e3779b97f4a7c15ull) ^ ((uint64_t)i << 40) ^ 1),
+                   h2 = st_mix(h1 ^ 0x2545f4914f6cdd1dull), h3 = st_mix(h2 + 7);
+    double a, b;
+    switch (i % 3) {
+      case 0:
+        a = st_num(h1, -900, 600);
+        b = st_num(h2, -60, 60);
+        break;
+      case 1: {
+        const double e = __builtin_fabs(st_num(h1, -740, 0));
+        b = 1.0 + e;
+        const int w = (int)(h3 % 3);
+        a = w == 0 ? 1.0 : (w == 1 ? e : (e - (b - 1.0)));  // the last: log1p's c (may be +0)
+        break;
+      }
+      default: {
+        const double f = (double)(int64_t)(h1 >> 11) * 0x1p-53 * 0.71 - 0.29;  // [-0.29, 0.42)
+        a = f;
+        b = 2.0 + f;
+        break;
+      }
+    }
+    if (!agdiv::div_safe(a, b)) continue;
+    ++n;
+    const double want = a / b, got = agdiv::div_core(a, b, agdiv::recip(b));
+    if (__builtin_bit_cast(uint64_t, want) != __builtin_bit_cast(uint64_t, got)) ++nbad;
+  }
+  if (nbad) atomicAdd(bad, nbad);
+  atomicAdd(tested, n);
+}
+
 }  // namespace
+
+extern "C" int ag_div_selftest(int32_t device, int64_t pairs, uint64_t seed, int64_t *tested, int64_t *mismatches) {
+  if (!mismatches || !tested || pairs < 0)
+    return ag_set_error(AG_ERR_INVALID, "ag_div_selftest: pairs >= 0, non-null tested / mismatches");
+  AgDeviceGuard dg(device);
+  constexpr int kBlocks = 4096, kIters = 48;
+  const int64_t per_launch = (int64_t)kBlocks * 256 * kIters;
+  unsigned long long *cnt = nullptr;
+  hipError_t e = hipMalloc(&cnt, 2 * sizeof(*cnt));
+  if (e == hipSuccess) e = hipMemset(cnt, 0, 2 * sizeof(*cnt));
+  for (int64_t done = 0, l = 0; e == hipSuccess && done < pairs; done += per_launch, ++l) {
+    hipLaunchKernelGGL(k_div_stress, dim3(kBlocks), dim3(256), 0, nullptr, seed + (uint64_t)l * 0x100000001b3ull,
+                       kIters, cnt, cnt + 1);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  unsigned long long h[2] = {0, 0};
+  if (e == hipSuccess) e = hipMemcpy(h, cnt, sizeof(h), hipMemcpyDeviceToHost);
+  (void)hipFree(cnt);
+  if (e != hipSuccess) return ag_set_error(AG_ERR_HIP, "ag_div_selftest: %s", hipGetErrorString(e));
+  *mismatches = (int64_t)h[0];
+  *tested = (int64_t)h[1];
+  return AG_OK;
+}
 
 extern "C" int ag_coop_selftest(int32_t device, int32_t workgroups, int32_t generations, int32_t regions,
                                 int64_t *mismatches) {

@@ -639,6 +639,14 @@ int ag_stream_copy(const void *src, void *dst, int64_t nbytes, void *stream);
 int ag_coop_selftest(int32_t device, int32_t workgroups, int32_t generations, int32_t regions,
                      int64_t *mismatches);
 
+/* Self-test of the learners' split FP64 division (csrc/ag_div.h: the BCE rows share one
+ * reciprocal of 1 + e between two divisions): about `pairs` random operand pairs in the split
+ * form's range on `device` -- anywhere in it, and shaped as the win-rate row's and log1p's
+ * divisions -- each divided both ways; *tested = the pairs in range, *mismatches = those whose
+ * bits differ from the compiler's IEEE `a / b` (0 expected). Synchronous. Test hook, no
+ * reference counterpart. */
+int ag_div_selftest(int32_t device, int64_t pairs, uint64_t seed, int64_t *tested, int64_t *mismatches);
+
 /* Thread-local description of the last error. */
 const char *ag_last_error(void);
 int32_t ag_abi_version(void);

@@ -3,14 +3,14 @@
 process, interleaved: the same population line, the same records, the same synthetic noise;
 the fitted models must be bit-identical across builds.
 
-    python tools/archive/ab_trainer.py configs_2 r02 [more variants...]   (build/variants/*.so)
+    python tools/ab_trainer.py configs_2 r02 [more variants...]   (build/variants/*.so)
 """
 import os
 import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "auction-gym_amd"), os.path.join(ROOT, "tools")]
 from auctiongym_amd import _lib  # noqa: E402
 import trainer_sweep  # noqa: E402

@@ -3,8 +3,8 @@
 records-per-workgroup settings: time, epochs, and whether the fitted models are bit-identical
 to the first setting's (they must be: the win-rate / imitation / DR / DM fits use exact sums).
 
-    python tools/archive/trainer_sweep.py configs_2 8192 4096 2048
-    python tools/archive/trainer_sweep.py configs_2:65536 256 1073741824   (2^16 auctions per step)
+    python tools/trainer_sweep.py configs_2 8192 4096 2048
+    python tools/trainer_sweep.py configs_2:65536 256 1073741824   (2^16 auctions per step)
 """
 import os
 import sys
@@ -13,7 +13,7 @@ import time
 import numpy as np
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "auction-gym_amd")]
 import bench  # noqa: E402
 
