@@ -22,6 +22,10 @@
 #ifndef AG_COOP_FENCED
 #define AG_COOP_FENCED 0
 #endif
+#ifndef AG_COOP_GROUPED
+#define AG_COOP_GROUPED 0  // 1: the learning bidders' per-epoch sums by agent_allreduce_grouped (A/B:
+                           // within 1 % of the tree either way, profiles/r06k_ab_grouped_*.log)
+#endif
 
 namespace agcoop {
 
@@ -249,6 +253,72 @@ __device__ __forceinline__ void agent_reduce_nowait(unsigned *bar, int64_t *acc,
     idx = q;
     members_prev = nodes;
   }
+}
+
+// Grouped exact all-reduce (the trainers' per-epoch sums, AG_COOP_GROUPED): the data take one
+// level instead of climbing the tree. The workgroups form ceil(nblk / F) groups of F; each adds
+// its W words (LDS vals) to its group's accumulator row, waits for them to be performed, and
+// arrives at its group's counter; the group's last arriver arrives at the top counter, the
+// last group's bumps the generation word, and every workgroup, once the generation has moved,
+// reads the group rows and sums them. Nothing is ever reset: counters and generation count
+// monotonically (round r's arrivals at a counter of m members are its values m (r - 1) ..
+// m r - 1), and the rows accumulate -- per round parity, since a fast workgroup adds its round
+// r + 1 words while slower ones still read round r's -- so a workgroup's totals are the rows'
+// sum minus the same parity's sum it read two rounds earlier (prev, LDS [2][W], zero at the
+// start with the rows), exact in 2^64 arithmetic. After the last data add the critical path
+// is three arrivals, one poll and one read; the tree also moved every node's row up a level
+// (a load and an add per level). Fence-free as agent_allreduce_start: every word that moves is
+// an agent-scope atomic, each wave's atomics are complete (s_waitcnt vmcnt(0) and a barrier)
+// before its workgroup arrives, and the wave that polled reads (W <= 64).
+// lines: ceil(nblk / F) group counters, then the top counter, then the generation word (each
+// on its own kBarLineWords line); rows: [2][ceil(nblk / F)][stride] int64; all zero at the
+// first round; rnd: 1, 2, ... (the same in every workgroup).
+__host__ __device__ inline int group_lines(int nblk, int F = kBarFanIn) { return nblk > 1 ? (nblk + F - 1) / F + 2 : 0; }
+template <int F = kBarFanIn>
+__device__ __forceinline__ void agent_allreduce_grouped(unsigned *lines, int64_t *rows, int stride, int rank, int nblk,
+                                                        const int64_t *vals, int W, int64_t *tot, unsigned rnd,
+                                                        uint64_t (*prev)[32]) {
+  const int t = threadIdx.x;
+  const int G = (nblk + F - 1) / F, q = rank / F;
+  const unsigned members = (unsigned)(nblk - q * F < F ? nblk - q * F : F);
+  unsigned *top = lines + (size_t)G * kBarLineWords, *gen = top + kBarLineWords;
+  int64_t *par = rows + (size_t)(rnd & 1u) * G * stride;
+  __syncthreads();  // vals complete
+  if (t < W)
+    __hip_atomic_fetch_add(par + (size_t)q * stride + t, vals[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  AG_VMCNT0();
+  AG_COOP_REL();
+  __syncthreads();  // this workgroup's additions are performed before it arrives
+  if (t == 0) {
+    bool last = __hip_atomic_fetch_add(lines + (size_t)q * kBarLineWords, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT) == members * rnd - 1u;
+    if (last)
+      last = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)G * rnd - 1u;
+    if (last)
+      __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < rnd)
+        __builtin_amdgcn_s_sleep(AG_BAR_SLEEP);
+  }
+  if (t < 64) {  // (the polling wave)
+    AG_COOP_ACQ();
+    if (t < W) {
+      uint64_t sum = 0;
+      for (int g0 = 0; g0 < G; g0 += 8) {  // eight independent loads in flight (indices clamped)
+        uint64_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int g = g0 + k < G ? g0 + k : G - 1;
+          v[k] = (uint64_t)__hip_atomic_load(par + (size_t)g * stride + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sum += g0 + k < G ? v[k] : 0ull;
+      }
+      tot[t] = (int64_t)(sum - prev[rnd & 1u][t]);
+      prev[rnd & 1u][t] = sum;
+    }
+  }
+  __syncthreads();
 }
 
 }  // namespace agcoop

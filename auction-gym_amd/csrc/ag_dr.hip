@@ -336,6 +336,7 @@ struct TrainLds {
   int stop;       // a NaN loss
   int exhausted;  // a noise-driven fit ran out of noise epochs before it stopped
   int flag;       // agent_allreduce_i64's broadcast
+  uint64_t gprev[2][32];  // agent_allreduce_grouped's row sums of the last two rounds
 };
 
 __device__ __forceinline__ void adam_reset(TrainLds &S) {
@@ -355,7 +356,9 @@ struct Coop {
   unsigned *bar;  // the agent's barrier lines (bar_lines)
   int ph;         // exchanges so far (identical in every workgroup of the agent)
   int64_t *acc;   // exact_totals' accumulator rows [bar_lines][32] (row 0: the totals), zero
-                  // between exchanges
+                  // between exchanges; AG_COOP_GROUPED: agent_allreduce_grouped's [2][groups][32]
+  unsigned *gcnt; // AG_COOP_GROUPED: its group arrival counters (group_lines, after the barrier lines)
+  unsigned rnd;   // AG_COOP_GROUPED: exact_totals calls so far
 };
 
 // exact totals of NV fixed-point sums over the agent's records (S.tot: hi, lo pairs), summed
@@ -370,7 +373,11 @@ template <int NV>
 __device__ __forceinline__ void exact_totals(const int64_t (&acc)[NV], TrainLds &S, Coop &C) {
   block_sums<NV>(acc, S.w, S.tot);
   if (C.nblk > 1) {
+#if AG_COOP_GROUPED
+    agcoop::agent_allreduce_grouped(C.gcnt, C.acc, 32, C.rank, C.nblk, S.tot, 2 * NV, S.tot, ++C.rnd, S.gprev);
+#else
     agcoop::agent_allreduce_i64(C.bar, C.acc, 32, C.rank, C.nblk, S.tot, 2 * NV, S.tot, &S.flag);
+#endif
     ++C.ph;
   }
 }
@@ -1042,7 +1049,9 @@ __global__ __launch_bounds__(kDrThreads, PH == 0 ? AG_DR_PH0_MIN_WAVES : AG_DR_P
   // the agent's exchange region [2][nblk][32] (its workgroups have consecutive block indices)
   // the agent's exchange region: [2][nblk][32] parity buffers, then [nblk][32] accumulator rows
   int64_t *preg = partials + (size_t)(blockIdx.x - rank) * 3 * 32;
-  Coop C{rank, nblk, preg, barriers + (size_t)bar_off[a] * kBarLineWords, 0, preg + (size_t)2 * nblk * 32};
+  unsigned *abar = barriers + (size_t)bar_off[a] * kBarLineWords;
+  Coop C{rank, nblk, preg, abar, 0, preg + (size_t)2 * nblk * 32, abar + (size_t)bar_lines(nblk) * kBarLineWords, 0u};
+  if (tid < 64) S.gprev[tid >> 5][tid & 31] = 0;
   // stage the chunk's first `cap` records in LDS (the fields this phase's fits read)
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   float *lf = reinterpret_cast<float *>(s_dyn);
@@ -2181,7 +2190,7 @@ int ag_bidder_update(ag_ctx *c, const ag_shading_samples *s, const int32_t *agen
       P.multi |= nblk[a] > 1;
       if (nblk[a]) most = std::max<int64_t>(most, (cnt[a] + nblk[a] - 1) / nblk[a]);
       P.bar_off[a] = P.lines;
-      P.lines += bar_lines(nblk[a]);
+      P.lines += bar_lines(nblk[a]) + agcoop::group_lines(nblk[a]);  // (the tree's, then the grouped sums')
       for (int r = 0; r < nblk[a]; ++r) {
         P.blk_agent.push_back(a);
         P.blk_rank.push_back(r);

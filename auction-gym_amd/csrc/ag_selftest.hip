@@ -1,6 +1,6 @@
 // ag_selftest.hip -- stress test of the learners' cross-workgroup exact sums (ag_coop.h), the
 // hand-off every trainer relies on (k_lrts_train, k_bidder_train, the pipe, the per-epoch
-// kernels): many cooperative workgroups -- spread over every XCD -- run generation after
+// kernels; regions = 0: agent_allreduce_grouped, the learning bidders' per-epoch sums): many cooperative workgroups -- spread over every XCD -- run generation after
 // generation of interleaved combining-tree all-reduces of int64 words whose totals each
 // workgroup also knows in closed form, and count every total that differs. A stale read (a
 // node row or total seen before another XCD's addition, or a counter / generation observed
@@ -126,6 +126,34 @@ __global__ __launch_bounds__(256) void k_div_stress(uint64_t seed, int iters, un
   atomicAdd(tested, n);
 }
 
+// agent_allreduce_grouped (the trainers' per-epoch sums) under the same stress: every
+// workgroup one member, `gens` rounds of 32-word sums checked against the closed form
+__global__ __launch_bounds__(kStThreads) void k_group_stress(unsigned *cnt, int64_t *rows, int gens,
+                                                             unsigned long long *bad) {
+  __shared__ int64_t s_vals[kStWords], s_want[kStWords];
+  __shared__ uint64_t s_prev[2][32];
+  const int t = threadIdx.x, rank = blockIdx.x, nblk = gridDim.x;
+  if (t < 64) s_prev[t >> 5][t & 31] = 0;
+  unsigned long long nbad = 0;
+  for (int g = 0; g < gens; ++g) {
+    __syncthreads();
+    if (t < kStWords) s_vals[t] = st_val((uint32_t)g, 0, rank, t);
+    agcoop::agent_allreduce_grouped(cnt, rows, kStWords, rank, nblk, s_vals, kStWords, s_vals, (unsigned)g + 1u,
+                                    s_prev);
+    if (t < kStWords) s_want[t] = 0;
+    __syncthreads();
+    for (int j = 0; j < kStWords; ++j) {
+      uint64_t part = 0;
+      for (int q = t; q < nblk; q += kStThreads) part += (uint64_t)st_val((uint32_t)g, 0, q, j);
+      for (int o = 32; o > 0; o >>= 1) part += (uint64_t)__shfl_xor((long long)part, o, 64);
+      if ((t & 63) == 0) atomicAdd((unsigned long long *)&s_want[j], (unsigned long long)part);
+    }
+    __syncthreads();
+    if (t < kStWords && s_vals[t] != s_want[t]) ++nbad;
+  }
+  if (nbad) atomicAdd(bad, nbad);
+}
+
 }  // namespace
 
 extern "C" int ag_div_selftest(int32_t device, int64_t pairs, uint64_t seed, int64_t *tested, int64_t *mismatches) {
@@ -155,35 +183,38 @@ extern "C" int ag_div_selftest(int32_t device, int64_t pairs, uint64_t seed, int
 extern "C" int ag_coop_selftest(int32_t device, int32_t workgroups, int32_t generations, int32_t regions,
                                 int64_t *mismatches) {
   if (!mismatches) return ag_set_error(AG_ERR_INVALID, "ag_coop_selftest: null mismatches");
-  if (generations < 0 || regions < 1 || regions > kStMaxRegions)
-    return ag_set_error(AG_ERR_INVALID, "ag_coop_selftest: generations >= 0, regions in [1, %d]", kStMaxRegions);
+  if (generations < 0 || regions < 0 || regions > kStMaxRegions)
+    return ag_set_error(AG_ERR_INVALID, "ag_coop_selftest: generations >= 0, regions in [0, %d]", kStMaxRegions);
   AgDeviceGuard dg(device);
   int cus = 0, per_cu = 0;
   AG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-  AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_coop_stress, kStThreads, 0));
+  const void *kern = regions == 0 ? (const void *)k_group_stress : (const void *)k_coop_stress;
+  AG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kStThreads, 0));
   const int cap = per_cu * cus;
   int G = workgroups > 0 ? workgroups : 4 * cus;
   if (G > cap)
     return ag_set_error(AG_ERR_UNSUPPORTED, "ag_coop_selftest: %d workgroups > %d co-resident", G, cap);
-  int lines = agcoop::bar_lines(G);
+  int lines = regions == 0 ? agcoop::group_lines(G) : agcoop::bar_lines(G);
   if (lines < 1) lines = 1;
+  const int rg = regions == 0 ? 2 : regions;  // grouped: rows [2 parities][groups][32]
   // bars: [regions][lines][32] u32; acc: [regions][lines][32] int64 (zero on entry, zero again
   // after every sum but row 0); bad: one u64
   unsigned *bars = nullptr;
   int64_t *acc = nullptr;
   unsigned long long *bad = nullptr;
-  const size_t nb = (size_t)regions * lines * agcoop::kBarLineWords * sizeof(unsigned);
-  const size_t na = (size_t)regions * lines * kStWords * sizeof(int64_t);
+  const size_t nb = (size_t)rg * lines * agcoop::kBarLineWords * sizeof(unsigned);
+  const size_t na = (size_t)rg * lines * kStWords * sizeof(int64_t);
   hipError_t e = hipMalloc(&bars, nb);
   if (e == hipSuccess) e = hipMalloc(&acc, na);
   if (e == hipSuccess) e = hipMalloc(&bad, sizeof(*bad));
   if (e == hipSuccess) e = hipMemset(bars, 0, nb);
   if (e == hipSuccess) e = hipMemset(acc, 0, na);
   if (e == hipSuccess) e = hipMemset(bad, 0, sizeof(*bad));
-  int rg = regions;
-  void *args[] = {&bars, &acc, &lines, &rg, &generations, &bad};
+  int nreg = regions;
+  void *args[] = {&bars, &acc, &lines, &nreg, &generations, &bad};
+  void *gargs[] = {&bars, &acc, &generations, &bad};
   if (e == hipSuccess)
-    e = hipLaunchCooperativeKernel((const void *)k_coop_stress, dim3(G), dim3(kStThreads), args, 0, nullptr);
+    e = hipLaunchCooperativeKernel(kern, dim3(G), dim3(kStThreads), regions == 0 ? gargs : args, 0, nullptr);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   unsigned long long h = 0;
   if (e == hipSuccess) e = hipMemcpy(&h, bad, sizeof(h), hipMemcpyDeviceToHost);

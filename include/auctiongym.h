@@ -635,6 +635,7 @@ int ag_stream_copy(const void *src, void *dst, int64_t nbytes, void *stream);
  * trainer runs per epoch): `workgroups` cooperative workgroups on `device` (0: 4 per CU, every
  * XCD) run `generations` rounds of `regions` (1..4) interleaved 32-word int64 all-reduces and
  * compare every total with its closed form; *mismatches = the wrong totals seen (0 expected).
+ * regions = 0: the grouped one-level form (csrc/ag_coop.h agent_allreduce_grouped).
  * Synchronous. Test hook, no reference counterpart. */
 int ag_coop_selftest(int32_t device, int32_t workgroups, int32_t generations, int32_t regions,
                      int64_t *mismatches);

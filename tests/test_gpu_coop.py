@@ -30,7 +30,8 @@ print("WRONG_TOTALS", bad.value, flush=True)
 """
 
 
-@pytest.mark.parametrize("workgroups,generations,regions", [(0, 4000, 1), (0, 2000, 3), (1024, 1000, 4), (2, 5000, 2)])
+@pytest.mark.parametrize("workgroups,generations,regions", [(0, 4000, 1), (0, 2000, 3), (1024, 1000, 4), (2, 5000, 2),
+                                                            (0, 4000, 0), (1024, 2000, 0), (2, 5000, 0), (17, 5000, 0)])
 def test_combining_tree_sums_exact_under_stress(gpu, workgroups, generations, regions):
     try:
         r = subprocess.run([sys.executable, "-c", _CHILD, PKG, str(workgroups), str(generations), str(regions)],
@@ -46,5 +47,6 @@ def test_selftest_refuses_bad_arguments(gpu):
     L = _lib.load()
     bad = ctypes.c_int64(-1)
     assert L.ag_coop_selftest(0, 0, 10, 5, ctypes.byref(bad)) != 0  # regions > 4
+    assert L.ag_coop_selftest(0, 0, 10, -1, ctypes.byref(bad)) != 0
     assert L.ag_coop_selftest(0, 1 << 20, 10, 1, ctypes.byref(bad)) != 0  # not co-resident
     assert L.ag_coop_selftest(0, 0, 10, 1, None) != 0
