@@ -38,6 +38,9 @@ constexpr int kDrThreads = 256;
 constexpr int kWrEpochs = 32768, kInitEpochs = 16384, kDrEpochs = 32768;
 constexpr int64_t kBidderChunk = 8192;  // records per workgroup of a PolicyLearningBidder (default)
 constexpr int64_t kMinChunk = 1024;     // fewest records per workgroup of an exact-sum learner's split
+#ifndef AG_DR_ABLATE_XCHG
+#define AG_DR_ABLATE_XCHG 0  // diagnostic (wrong fits by design): each workgroup steps on its own partial sums
+#endif
 #ifndef AG_DR_SHARED_DIV
 #define AG_DR_SHARED_DIV 1  // the win-rate row's two divisions by 1 + e share one reciprocal (ag_div.h)
 #endif
@@ -372,7 +375,7 @@ struct Coop {
 template <int NV>
 __device__ __forceinline__ void exact_totals(const int64_t (&acc)[NV], TrainLds &S, Coop &C) {
   block_sums<NV>(acc, S.w, S.tot);
-  if (C.nblk > 1) {
+  if (C.nblk > 1 && !(AG_DR_ABLATE_XCHG & 1)) {
 #if AG_COOP_GROUPED
     agcoop::agent_allreduce_grouped(C.gcnt, C.acc, 32, C.rank, C.nblk, S.tot, 2 * NV, S.tot, ++C.rnd, S.gprev);
 #else
@@ -537,49 +540,90 @@ __device__ __forceinline__ void each_record(const RecView &V, int64_t nb, F &&f)
 // softplus(z) otherwise, softplus(u) = L for u <= 0, |z| + L for u > 0 (u past 20: u).
 // Branch-free main paths of exp and log1p (the same bits), the rare inputs outside them
 // patched with the full functions afterwards. aug: the gamma = 0, y = 0 augmentation row.
-__device__ __forceinline__ void wr_row(int64_t (&acc)[5], double c, double v, double g, double y, bool aug,
-                                       double w0, double w1, double w2, double w3, const uint64_t *tab) {
-  const double z = c * w0 + v * w1 + g * w2 + w3;
-  const double a = __builtin_fabs(z);
-  double e = agexp::exp_main(-a, tab);
+// The row in two parts so that a record's two rows (and a lane's records) can be computed
+// in one basic block before either takes its rare branch: wr_main is branch-free, wr_finish
+// patches (rarely) and adds the terms.
+struct WrMain {
+  double z, a, e, Lz, pw, u, t, gz, x2, x3;
+  bool main;  // exp and log1p on their main paths
+  bool ok;    // main, and the checked terms in fxb's fast range
+};
+__device__ __forceinline__ WrMain wr_main(double c, double v, double g, double y, bool aug, double w0, double w1,
+                                          double w2, double w3, const uint64_t *tab) {
+  WrMain m;
+  m.z = c * w0 + v * w1 + g * w2 + w3;
+  m.a = __builtin_fabs(m.z);
+  m.e = agexp::exp_main(-m.a, tab);
   bool lok;
   // p's division and log1p's c / u both divide by 1 + e: one reciprocal (ag_div.h; on the main
   // paths e >= exp(-512), c is 0 or >= 2^-81 in magnitude, |f| >= 2^-53: div_safe's range)
 #if AG_DR_SHARED_DIV
-  const double d1 = 1.0 + e, r1 = agdiv::recip(d1);
-  double Lz = aglog1p::log1p_main_t(e, lok, SharedDiv{r1});
-  double pw = agdiv::div_core(z >= 0.0 ? 1.0 : e, d1, r1);
+  const double d1 = 1.0 + m.e, r1 = agdiv::recip(d1);
+  m.Lz = aglog1p::log1p_main_t(m.e, lok, SharedDiv{r1});
+  m.pw = agdiv::div_core(m.z >= 0.0 ? 1.0 : m.e, d1, r1);
 #else
-  double Lz = aglog1p::log1p_main(e, lok);
-  double pw = (z >= 0.0 ? 1.0 : e) / (1.0 + e);
+  m.Lz = aglog1p::log1p_main(m.e, lok);
+  m.pw = (m.z >= 0.0 ? 1.0 : m.e) / (1.0 + m.e);
 #endif
-  const double u = y > 0.0 ? -z : z;
-  double t = fmin(u > 20.0 ? u : (u > 0.0 ? a + Lz : Lz), 100.0);
-  double gz = pw - y;
+  m.u = y > 0.0 ? -m.z : m.z;
+  m.t = fmin(m.u > 20.0 ? m.u : (m.u > 0.0 ? m.a + m.Lz : m.Lz), 100.0);
+  m.gz = m.pw - y;
   // |t| <= 100, |pw - y| <= 1, ctr in [0, 1]: those terms are far inside fxb's fast range;
   // gz * value and gz * gamma are checked. ONE rare branch per row (the exp / log1p patch and
   // an out-of-range term together) instead of one per patch: the common path stays straight.
-  const double x2 = (gz * v) * kGrid, x3 = (gz * g) * kGrid;
+  // (the augmentation row's x3 is gz * 0: always in range, and its term is never added)
+  m.x2 = (m.gz * v) * kGrid;
+  m.x3 = (m.gz * g) * kGrid;
+  m.main = (int)agexp::exp_in_main(m.a) & (int)lok;
+  m.ok = (int)m.main & (int)fx_in(m.x2) & ((int)aug | (int)fx_in(m.x3));
+  return m;
+}
+__device__ __forceinline__ void wr_finish(int64_t (&acc)[5], WrMain m, double c, double v, double g, double y,
+                                          bool aug, const uint64_t *tab) {
   int64_t t2, t3;
-  if (__builtin_expect((int)agexp::exp_in_main(a) & (int)lok & (int)fx_in(x2) & (int)fx_in(x3), 1)) {
-    t2 = fxb_x(x2);
-    t3 = fxb_x(x3);
+  if (__builtin_expect(m.ok, 1)) {
+    t2 = fxb_x(m.x2);
+    t3 = fxb_x(m.x3);
   } else {
-    if (!(agexp::exp_in_main(a) && lok)) {
-      e = agexp::exp(-a, tab);
-      Lz = aglog1p::log1p(e);
-      pw = (z >= 0.0 ? 1.0 : e) / (1.0 + e);
-      t = fmin(u > 20.0 ? u : (u > 0.0 ? a + Lz : Lz), 100.0);
-      gz = pw - y;
+    if (!m.main) {
+      m.e = agexp::exp(-m.a, tab);
+      m.Lz = aglog1p::log1p(m.e);
+      m.pw = (m.z >= 0.0 ? 1.0 : m.e) / (1.0 + m.e);
+      m.t = fmin(m.u > 20.0 ? m.u : (m.u > 0.0 ? m.a + m.Lz : m.Lz), 100.0);
+      m.gz = m.pw - y;
     }
-    t2 = fxb(gz * v);
-    t3 = fxb(gz * g);
+    t2 = fxb(m.gz * v);
+    t3 = fxb(m.gz * g);
   }
-  addw(acc[0], fxb_fast(t));
-  addw(acc[1], fxb_fast(gz * c));
+  addw(acc[0], fxb_fast(m.t));
+  addw(acc[1], fxb_fast(m.gz * c));
   addw(acc[2], t2);
   if (!aug) addw(acc[3], t3);  // the augmentation row's g = 0 term is +-0: rounds to 0
-  addw(acc[4], fxb_fast(gz));
+  addw(acc[4], fxb_fast(m.gz));
+}
+__device__ __forceinline__ void wr_row(int64_t (&acc)[5], double c, double v, double g, double y, bool aug,
+                                       double w0, double w1, double w2, double w3, const uint64_t *tab) {
+  wr_finish(acc, wr_main(c, v, g, y, aug, w0, w1, w2, w3, tab), c, v, g, y, aug, tab);
+}
+// a record's logged row and its gamma = 0, y = 0 augmentation row, both main paths first
+__device__ __forceinline__ void wr_pair(int64_t (&acc)[5], double c, double v, double g, double y, double w0,
+                                        double w1, double w2, double w3, const uint64_t *tab) {
+  const WrMain A = wr_main(c, v, g, y, false, w0, w1, w2, w3, tab);
+  const WrMain B = wr_main(c, v, 0.0, 0.0, true, w0, w1, w2, w3, tab);
+  if (__builtin_expect((int)A.ok & (int)B.ok, 1)) {  // one branch for both rows
+    addw(acc[0], fxb_fast(A.t));
+    addw(acc[1], fxb_fast(A.gz * c));
+    addw(acc[2], fxb_x(A.x2));
+    addw(acc[3], fxb_x(A.x3));
+    addw(acc[4], fxb_fast(A.gz));
+    addw(acc[0], fxb_fast(B.t));
+    addw(acc[1], fxb_fast(B.gz * c));
+    addw(acc[2], fxb_x(B.x2));
+    addw(acc[4], fxb_fast(B.gz));
+  } else {
+    wr_finish(acc, A, c, v, g, y, false, tab);
+    wr_finish(acc, B, c, v, 0.0, 0.0, true, tab);
+  }
 }
 // a lane that ran wr_row for nrec records (both rows each): its accumulators unbiased
 __device__ __forceinline__ void wr_unbias(int64_t (&acc)[5], int64_t nrec) {
@@ -609,11 +653,11 @@ __device__ int fit_winrate(const RecView &V, const Chunk &K, TrainLds &S, Coop &
     // record j's logged row and its gamma = 0, y = 0 augmentation row together (two
     // independent chains for the scheduler; the sums are exact, so any order)
     int64_t nrec = 0;
+    if (!(AG_DR_ABLATE_XCHG & 2))  // diagnostic: 2 = no records (the epoch's fixed cost alone)
     each_record(V, K.nb, [&](int64_t j, auto L) {
       constexpr bool l = decltype(L)::value;
       const double c = V.template ctr_<l>(j), v = V.template val_<l>(j);
-      wr_row(acc, c, v, V.template gam_<l>(j), V.template won_<l>(j), false, w0, w1, w2, w3, S.tab);
-      wr_row(acc, c, v, 0.0, 0.0, true, w0, w1, w2, w3, S.tab);
+      wr_pair(acc, c, v, V.template gam_<l>(j), V.template won_<l>(j), w0, w1, w2, w3, S.tab);
       ++nrec;
     });
     wr_unbias(acc, nrec);
@@ -880,6 +924,7 @@ __device__ int fit_dm(const RecView &V, const Chunk &K, TrainLds &S, Coop &C, co
     int64_t acc[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = 0;
+    if (!(AG_DR_ABLATE_XCHG & 2))
     each_record(V, K.nb, [&](int64_t j, auto L) {
       constexpr bool l = decltype(L)::value;
       dm_rec(acc, S.pol, S.wr, V.template ctr_<l>(j), V.template val_<l>(j), fit_eps(F, e, K.c0 + j), S.tab);
@@ -1471,8 +1516,7 @@ __device__ __forceinline__ int pipe_partial(const FitSt &st, const RecView &V, i
     each_record(V, nb, [&](int64_t j, auto L) {
       constexpr bool l = decltype(L)::value;
       const double c = V.template ctr_<l>(j), v = V.template val_<l>(j);
-      wr_row(acc, c, v, V.template gam_<l>(j), V.template won_<l>(j), false, w0, w1, w2, w3, S.tab);
-      wr_row(acc, c, v, 0.0, 0.0, true, w0, w1, w2, w3, S.tab);
+      wr_pair(acc, c, v, V.template gam_<l>(j), V.template won_<l>(j), w0, w1, w2, w3, S.tab);
     });
     wr_unbias(acc, nrec);
     block_sums<5>(acc, S.w, S.tot);
