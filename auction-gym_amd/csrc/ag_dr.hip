@@ -41,6 +41,12 @@ constexpr int64_t kMinChunk = 1024;     // fewest records per workgroup of an ex
 #ifndef AG_DR_ABLATE_XCHG
 #define AG_DR_ABLATE_XCHG 0  // diagnostic (wrong fits by design): each workgroup steps on its own partial sums
 #endif
+#ifndef AG_DR_WR_RECS
+#define AG_DR_WR_RECS 1  // records per iteration of the win-rate loop (2: wr_pair2; A/B)
+#endif
+#ifndef AG_DR_SLOW_OUTLINE
+#define AG_DR_SLOW_OUTLINE 0  // 1: the win-rate rows' rare path out of line (wr_slow; A/B)
+#endif
 #ifndef AG_DR_SHARED_DIV
 #define AG_DR_SHARED_DIV 1  // the win-rate row's two divisions by 1 + e share one reciprocal (ag_div.h)
 #endif
@@ -605,6 +611,30 @@ __device__ __forceinline__ void wr_row(int64_t (&acc)[5], double c, double v, do
                                        double w0, double w1, double w2, double w3, const uint64_t *tab) {
   wr_finish(acc, wr_main(c, v, g, y, aug, w0, w1, w2, w3, tab), c, v, g, y, aug, tab);
 }
+// the rare path of a row, out of line (the main path keeps its registers): the row from the
+// full exp / log1p and the general fixed-point conversion -- the same terms wr_finish adds
+struct WrTerms {
+  int64_t t[5];
+};
+__device__ __noinline__ WrTerms wr_slow(double c, double v, double g, double y, bool aug, double w0, double w1,
+                                        double w2, double w3, const uint64_t *tab) {
+  const double z = c * w0 + v * w1 + g * w2 + w3;
+  const double a = __builtin_fabs(z);
+  const double e = agexp::exp(-a, tab);
+  const double Lz = aglog1p::log1p(e);
+  const double pw = (z >= 0.0 ? 1.0 : e) / (1.0 + e);
+  const double u = y > 0.0 ? -z : z;
+  const double t = fmin(u > 20.0 ? u : (u > 0.0 ? a + Lz : Lz), 100.0);
+  const double gz = pw - y;
+  WrTerms r;
+  r.t[0] = fxb(t);
+  r.t[1] = fxb(gz * c);
+  r.t[2] = fxb(gz * v);
+  r.t[3] = aug ? 0 : fxb(gz * g);
+  r.t[4] = fxb(gz);
+  return r;
+}
+
 // a record's logged row and its gamma = 0, y = 0 augmentation row, both main paths first
 __device__ __forceinline__ void wr_pair(int64_t (&acc)[5], double c, double v, double g, double y, double w0,
                                         double w1, double w2, double w3, const uint64_t *tab) {
@@ -621,10 +651,60 @@ __device__ __forceinline__ void wr_pair(int64_t (&acc)[5], double c, double v, d
     addw(acc[2], fxb_x(B.x2));
     addw(acc[4], fxb_fast(B.gz));
   } else {
+#if AG_DR_SLOW_OUTLINE
+    const WrTerms ta = wr_slow(c, v, g, y, false, w0, w1, w2, w3, tab);
+    const WrTerms tb = wr_slow(c, v, 0.0, 0.0, true, w0, w1, w2, w3, tab);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      addw(acc[k], ta.t[k]);
+      if (k != 3) addw(acc[k], tb.t[k]);
+    }
+#else
     wr_finish(acc, A, c, v, g, y, false, tab);
     wr_finish(acc, B, c, v, 0.0, 0.0, true, tab);
+#endif
   }
 }
+// two records' four rows, main paths first, one rare branch (AG_DR_WR_RECS = 2)
+__device__ __forceinline__ void wr_pair2(int64_t (&acc)[5], double c0, double v0, double g0, double y0, double c1,
+                                         double v1, double g1, double y1, double w0, double w1, double w2, double w3,
+                                         const uint64_t *tab) {
+  const WrMain A0 = wr_main(c0, v0, g0, y0, false, w0, w1, w2, w3, tab);
+  const WrMain B0 = wr_main(c0, v0, 0.0, 0.0, true, w0, w1, w2, w3, tab);
+  const WrMain A1 = wr_main(c1, v1, g1, y1, false, w0, w1, w2, w3, tab);
+  const WrMain B1 = wr_main(c1, v1, 0.0, 0.0, true, w0, w1, w2, w3, tab);
+  if (__builtin_expect((int)A0.ok & (int)B0.ok & (int)A1.ok & (int)B1.ok, 1)) {
+    addw(acc[0], fxb_fast(A0.t));
+    addw(acc[1], fxb_fast(A0.gz * c0));
+    addw(acc[2], fxb_x(A0.x2));
+    addw(acc[3], fxb_x(A0.x3));
+    addw(acc[4], fxb_fast(A0.gz));
+    addw(acc[0], fxb_fast(B0.t));
+    addw(acc[1], fxb_fast(B0.gz * c0));
+    addw(acc[2], fxb_x(B0.x2));
+    addw(acc[4], fxb_fast(B0.gz));
+    addw(acc[0], fxb_fast(A1.t));
+    addw(acc[1], fxb_fast(A1.gz * c1));
+    addw(acc[2], fxb_x(A1.x2));
+    addw(acc[3], fxb_x(A1.x3));
+    addw(acc[4], fxb_fast(A1.gz));
+    addw(acc[0], fxb_fast(B1.t));
+    addw(acc[1], fxb_fast(B1.gz * c1));
+    addw(acc[2], fxb_x(B1.x2));
+    addw(acc[4], fxb_fast(B1.gz));
+  } else {
+    const WrTerms t[4] = {wr_slow(c0, v0, g0, y0, false, w0, w1, w2, w3, tab),
+                          wr_slow(c0, v0, 0.0, 0.0, true, w0, w1, w2, w3, tab),
+                          wr_slow(c1, v1, g1, y1, false, w0, w1, w2, w3, tab),
+                          wr_slow(c1, v1, 0.0, 0.0, true, w0, w1, w2, w3, tab)};
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        if (k != 3 || (r & 1) == 0) addw(acc[k], t[r].t[k]);
+  }
+}
+
 // a lane that ran wr_row for nrec records (both rows each): its accumulators unbiased
 __device__ __forceinline__ void wr_unbias(int64_t (&acc)[5], int64_t nrec) {
   fx_unbias(acc[0], 2 * nrec);
@@ -653,6 +733,25 @@ __device__ int fit_winrate(const RecView &V, const Chunk &K, TrainLds &S, Coop &
     // record j's logged row and its gamma = 0, y = 0 augmentation row together (two
     // independent chains for the scheduler; the sums are exact, so any order)
     int64_t nrec = 0;
+#if AG_DR_WR_RECS == 2
+    if (!(AG_DR_ABLATE_XCHG & 2)) {  // two staged records per iteration, then as each_record
+      const int64_t ns = K.nb < V.cap ? K.nb : V.cap;
+      int64_t j = tid;
+      for (; j + kDrThreads < ns; j += 2 * kDrThreads) {
+        const int64_t k = j + kDrThreads;
+        wr_pair2(acc, V.template ctr_<true>(j), V.template val_<true>(j), V.template gam_<true>(j),
+                 V.template won_<true>(j), V.template ctr_<true>(k), V.template val_<true>(k),
+                 V.template gam_<true>(k), V.template won_<true>(k), w0, w1, w2, w3, S.tab);
+        nrec += 2;
+      }
+      for (; j < ns; j += kDrThreads, ++nrec)
+        wr_pair(acc, V.template ctr_<true>(j), V.template val_<true>(j), V.template gam_<true>(j),
+                V.template won_<true>(j), w0, w1, w2, w3, S.tab);
+      for (; j < K.nb; j += kDrThreads, ++nrec)
+        wr_pair(acc, V.template ctr_<false>(j), V.template val_<false>(j), V.template gam_<false>(j),
+                V.template won_<false>(j), w0, w1, w2, w3, S.tab);
+    }
+#else
     if (!(AG_DR_ABLATE_XCHG & 2))  // diagnostic: 2 = no records (the epoch's fixed cost alone)
     each_record(V, K.nb, [&](int64_t j, auto L) {
       constexpr bool l = decltype(L)::value;
@@ -660,6 +759,7 @@ __device__ int fit_winrate(const RecView &V, const Chunk &K, TrainLds &S, Coop &
       wr_pair(acc, c, v, V.template gam_<l>(j), V.template won_<l>(j), w0, w1, w2, w3, S.tab);
       ++nrec;
     });
+#endif
     wr_unbias(acc, nrec);
     exact_totals<5>(acc, S, C);
     // every thread: the same loss; threads 0..3 step their parameter
