@@ -73,8 +73,12 @@ namespace ag {
 #endif
 #ifndef AG_TS_DMA
 #define AG_TS_DMA 1  // replayed Thompson noise streamed into a per-wave LDS ring by LDS-DMA: the
-                     // 256-lane P <= 2 shipped-shape builds (configs_1/2/3: 2-5 % in one process,
+                     // 256-lane shipped-shape builds (configs_1/2/3: 2-5 % in one process,
                      // profiles/r06i_ab_*.log); 0: the VGPR loads (A/B)
+#endif
+#ifndef AG_TS_DMA_MAXP
+#define AG_TS_DMA_MAXP 8  // ... in the 256-lane builds of up to this many participants (P = 8,
+                          // the streamed slots: configs_1_p8 -7 %, profiles/r06n_ab_dma8_c1p8.log)
 #endif
 #ifndef AG_TS_DMA_AHEAD
 #define AG_TS_DMA_AHEAD 2  // ... items in flight ahead of the one being scored
@@ -1060,7 +1064,7 @@ __global__ __launch_bounds__(BT, GENERAL == kGenTruthful ? (P >= 3 ? AG_TB_WIDE_
   int32_t *s_kag = reinterpret_cast<int32_t *>(smem + L.kag);
   float *s_tsr = reinterpret_cast<float *>(smem + L.tsr);
   // AG_TS_DMA: every wave's Thompson-noise ring (kTsDmaBufs items of 5 rows x 64 floats)
-  constexpr bool kDma = AG_TS_DMA && GENERAL && DOS == 5 && !GEN && BT == kThreads && P >= 1 && P <= 2;
+  constexpr bool kDma = AG_TS_DMA && GENERAL && DOS == 5 && !GEN && BT == kThreads && P >= 1 && P <= AG_TS_DMA_MAXP;
   __shared__ __attribute__((aligned(16))) float s_ring[kDma ? (BT / 64) * kTsDmaBufs * 5 * 64 : 1];
   static_assert(!GEN || (DOS > 0 && P > 0 && W == 1 && GENERAL), "generate mode: shipped-shape general builds");
   unsigned long long *s_cnt = reinterpret_cast<unsigned long long *>(smem + L.cnt);
